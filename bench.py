@@ -1,0 +1,216 @@
+"""Headline benchmark: agent-steps/sec, gym_flock_v2 (periodic) 256 agents x 4096 envs per MI355X (BASELINE config 3).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+One process per GPU. Envs are independent, so each rank steps its own 4096 envs with no data-path collective
+(weak scaling); the only collectives are the barrier around the timed region and the max-over-ranks of its time.
+A "step" = one vectorized env step of all the rank's envs (kinematics, boundary, all-pairs sensing, kNN obs,
+collision, reward, done: one HIP launch) plus, with --learner shared_critic, one shared-critic learn() (B=256).
+Inputs (state, a pool of synthetic actions) are resident in HBM before the timed region starts.
+
+Rank 0 prints ONE JSON line. Extra fields: roofline (dominant kernel, HIP events on the launch stream; algorithmic
+bytes 93 B/agent-step), valu (same kernel against the f32 VALU roof, which is what binds it), and
+cpu_baseline (the C oracle port, 1 thread, on a bounded sample of the same workload; N=1 only).
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_PEAK_TLANEOPS = 78.6        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (f32 non-packed lane-ops/s, /1e12)
+BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
+OPS_PER_PAIR = {True: 12, False: 7}  # algorithmic VALU ops per agent pair: periodic / Euclidean
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=256)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uw_discrete", "flock"])
+    ap.add_argument("--learner", default="none", choices=["none", "shared_critic"])
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    return world, rank, dev
+
+
+def barrier(world):
+    if world > 1:
+        torch.distributed.barrier()
+
+
+def cpu_baseline(args, box, seconds):
+    """The C oracle (oracle/flock_oracle.c, 1 thread) stepping a sample of the same workload sequentially."""
+    from oracle import oracle
+
+    E_s, N, k = 8, args.agents, args.k
+    rng = np.random.default_rng(0)
+    pos = rng.uniform(0, box, (E_s, N, 2)).astype(np.float32)
+    head = rng.uniform(0, 1.5 * np.pi, (E_s, N)).astype(np.float32)
+    prev = np.zeros((E_s, N), np.float32)
+    mem = np.zeros((E_s, N, 4, k), np.float32)
+    vel = np.zeros((E_s, N, 2), np.float32)
+    vel[..., 0] = 1.0
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        if args.variant == "uw_discrete":
+            act = rng.integers(0, 10, (E_s, N))
+            o = oracle.step_uwd(pos, head, prev, act, (0.1 * rng.standard_normal((E_s, N, 2))).astype(np.float32),
+                                k=k, box=box, cd=2.5)
+        else:
+            act = np.stack([rng.uniform(0, 1, (E_s, N)), rng.uniform(-1.5, 1.5, (E_s, N))], -1).astype(np.float32)
+            if args.variant == "v2":
+                o = oracle.step_v2(pos, head, act, k=k, box=box, cd=2.5)
+            elif args.variant == "uw":
+                o = oracle.step_uw(pos, head, prev, act, mem, k=k, box=box, cd=2.5)
+                mem = o["obs"]
+            else:
+                o = oracle.step_flock(pos, vel, act, mem, k=k, box=box, cd=2.5)
+                mem, vel = o["obs"], o["vel"]
+        pos = o["pos"]
+        head = o.get("heading", head)
+        prev = o.get("prev_heading", prev)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": E_s * N * n / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/flock_oracle.c {args.variant} step, {E_s} envs x {N} agents, {n} sequential "
+                      f"vectorized steps ({el:.1f} s), single thread, on this box's host"}
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+
+    E, N, k = args.envs, args.agents, args.k
+    box = float(round(np.sqrt(250.0 * N)))  # main.py density: 10 agents in 50x50
+    cfg = FlockConfig(variant=args.variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                      range_start=(0, box), sensor_range=14.0, seed=1234 + rank)
+    env = VecFlockEnv(cfg, device=dev)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    env.positions.copy_(torch.rand(E, N, 2, device=dev, generator=g) * box)
+    hmax = {"v2": 1.5 * np.pi, "uw": 2 * np.pi, "uw_discrete": np.pi / 1.2, "flock": 0.0}[args.variant]
+    env.headings.copy_((1.0 - torch.rand(E, N, device=dev, generator=g)) * hmax)
+    if args.variant == "flock":
+        env.velocities[..., 0] = 1.0
+    pool = []
+    for _ in range(8):
+        if args.variant == "uw_discrete":
+            pool.append(torch.randint(0, 10, (E, N), device=dev, generator=g))
+        elif args.variant == "v2":
+            pool.append(torch.stack([torch.rand(E, N, device=dev, generator=g),
+                                     torch.rand(E, N, device=dev, generator=g) * 3 - 1.5], -1).contiguous())
+        else:
+            pool.append((torch.rand(E, N, 2, device=dev, generator=g) * 2 - 1).contiguous())
+
+    learner = None
+    if args.learner == "shared_critic":
+        from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
+
+        learner = SharedCriticBench(env, device=dev, seed=1234 + rank)
+
+    def one_step(s):
+        env.step(pool[s % len(pool)])
+        if learner is not None:
+            learner.after_env_step(s)
+
+    for s in range(args.warmup):
+        one_step(s)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        env.step(pool[s % len(pool)])
+        ev[s][1].record(stream)
+        if learner is not None:
+            learner.after_env_step(s)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    total_agent_steps = world * E * N * args.steps
+    value = total_agent_steps / el
+    bytes_launch = BYTES_PER_AGENT_STEP[args.variant] * E * N
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    pmc_path = args.pmc or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                        f"pmc_{args.variant}_N{N}_E{E}.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    periodic = cfg.resolved().periodic
+    ops_launch = OPS_PER_PAIR[periodic] * (N - 1) * E * N
+    valu_t = ops_launch / (kern_ms * 1e-3) / 1e12
+    line = {
+        "metric": "agent-steps/sec at 256 agents x 4096 envs; 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "agent-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (uniform random positions/headings at main.py density, random actions; no checkpoints)",
+        "config": {
+            "workload": f"gym_flock_{args.variant} step, {N} agents x {E} envs per GPU"
+                        + (" (BASELINE config 3)" if (args.variant, N, E) == ("v2", 256, 4096) else ""),
+            "agents": N, "envs_per_gpu": E, "k": k, "box": box, "periodic": periodic,
+            "learner": ("none: env step only" if learner is None else learner.describe()),
+            "parallelism": f"env-shard x{world}",
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "step_kernel<6,periodic>", "kernel_ms": kern_ms,
+                     "bytes_per_agent_step": BYTES_PER_AGENT_STEP[args.variant]},
+        "valu": {"achieved": valu_t, "peak": VALU_PEAK_TLANEOPS, "unit": "Tlane-op/s",
+                 "frac": valu_t / VALU_PEAK_TLANEOPS, "ops_per_pair": OPS_PER_PAIR[periodic],
+                 "note": "the binding roofline of the O(N^2) sensing kernel"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args, box, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+/*
+ * flock_amd.h — C ABI of the MI355X (gfx950) flocking-environment stepper (libflock_amd.so).
+ *
+ * Plain C: pointers, sizes and scalars only; no torch or HIP types in any signature. Every pointer is a DEVICE
+ * pointer (HBM) unless stated otherwise; `stream` is a hipStream_t passed as an opaque pointer (NULL = default
+ * stream). Calls enqueue kernels on `stream` and never synchronise. Return 0 on success, a negative
+ * FLOCK_E* code otherwise; flock_last_error() then holds a message for the calling thread.
+ *
+ * Batched layout (E independent envs of N agents, k neighbours; row-major, contiguous):
+ *   pos [E][N][2] f32 · heading, prev_heading [E][N] f32 · vel [E][N][2] f32 · action [E][N][2] f32
+ *   action_id [E][N] i64 · noise [E][N][2] f32 · dnn [E][N][k] f32 · nn_idx [E][N][k] i64
+ *   reward [E][N] f32 · done [E][N] u8 · any_done [E] u8 · obs memory [E][N][4][k] f32
+ * State arrays marked (rw) are updated in place, as the reference mutates self.positions / self.headings.
+ *
+ * Each entry point replaces one reference step()/reset() (paths relative to RetamalVictor/marl-range-flocking):
+ *   flock_step_v2          environments/gym_flock_v2.py:71-83  (periodic=1; the RNN fork
+ *                          learners/maddpg_official_rnn/gym_flock_v2.py:71-82 is periodic=0, v_min=0.5)
+ *   flock_step_uw          environments/gym_flock_uw.py:69-81
+ *   flock_step_uw_discrete environments/gym_flock_uw_discrete.py:110-122
+ *   flock_step_flock       environments/gym_flock.py:48-60
+ *   flock_knn              _computePeriodicDistances gym_flock_v2.py:135-151 / _computeDistances :155-175
+ *   flock_reset            reset() gym_flock_v2.py:85-108, gym_flock_uw.py:83-111,
+ *                          gym_flock_uw_discrete.py:124-156, gym_flock.py:62-77 (bounded in-kernel rejection
+ *                          sampling instead of unbounded recursion)
+ * Limits of this build: 1 <= k <= 15, k + 1 <= N <= 1024.
+ */
+#ifndef FLOCK_AMD_H
+#define FLOCK_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLOCK_ABI_VERSION 1
+
+enum {
+    FLOCK_OK = 0,
+    FLOCK_E_K_RANGE = -1,   /* k + 1 > N ("selected index k out of range", as torch.topk raises) or k < 1 */
+    FLOCK_E_LIMIT = -2,     /* outside this build's limits (k > 15 or N > 1024) */
+    FLOCK_E_NULL = -3,      /* a required pointer is NULL */
+    FLOCK_E_LAUNCH = -4,    /* HIP launch error */
+    FLOCK_E_ARG = -5        /* other invalid argument */
+};
+
+/* variants for flock_reset */
+enum { FLOCK_VARIANT_V2 = 0, FLOCK_VARIANT_UW = 1, FLOCK_VARIANT_UW_DISCRETE = 2, FLOCK_VARIANT_FLOCK = 3 };
+
+int flock_abi_version(void);
+const char* flock_last_error(void);
+
+/* gym_flock_v2 step: pos (rw), heading (rw), action [lin, ang] → vel, dnn, nn_idx, reward, done, any_done. */
+int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                  float dt, float v_min, float v_max, int periodic, int rigid_boundary,
+                  float* pos, float* heading, const float* action,
+                  float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
+
+/* gym_flock_uw step: velocity actions; obs memory mem_in → mem_out (may alias); prev_heading (rw). nn_idx may be
+ * NULL (the reference does not keep it for this env). */
+int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                  float dt, int rigid_boundary,
+                  float* pos, const float* heading, float* prev_heading, const float* action,
+                  const float* mem_in, float* mem_out,
+                  float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
+
+/* gym_flock_uw_discrete step: action_id indexes table [n_actions][2] (action_dictionary means). noise [E][N][2]
+ * holds the N(0, noise_std) draws torch.normal adds to the means; if noise is NULL they are drawn in-kernel from
+ * Philox4x32-10(seed, counter = (agent, rng_offset)). status (may be NULL): device int, bit 0 set if any action id
+ * was outside [0, n_actions) (the reference raises KeyError); such agents get id 0. */
+int flock_step_uw_discrete(void* stream, int E, int N, int k, float box, float sensor_range,
+                           float collision_distance, float dt, float v_max, int rigid_boundary,
+                           float* pos, float* heading, float* prev_heading, const int64_t* action_id,
+                           const float* noise, float noise_std, uint64_t seed, uint64_t rng_offset,
+                           const float* table, int n_actions,
+                           float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                           int* status);
+
+/* gym_flock (original) step: vel (rw) holds the unit velocity state; obs memory mem_in → mem_out. */
+int flock_step_flock(void* stream, int E, int N, int k, float box, float collision_distance, float dt,
+                     int rigid_boundary, float* pos, float* vel, const float* action,
+                     const float* mem_in, float* mem_out,
+                     float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
+
+/* Sensing only: kNN of every agent from positions (no state change). clamp != 0 clamps to [0, sensor_range]. */
+int flock_knn(void* stream, int E, int N, int k, float box, float sensor_range, int periodic, int clamp,
+              const float* pos, float* dnn, int64_t* nn_idx);
+
+/*
+ * Device-side reset of the envs whose env_mask[e] != 0 (env_mask may be NULL = all). Draws positions and headings
+ * with the variant's distribution from Philox4x32-10(seed, counter = (agent, rng_offset + attempt)), applies
+ * check_boundary, and redraws the env while any Euclidean kNN distance is below check_distance, at most
+ * max_attempts times (the reference recurses without bound). Zeroes vel and prev_heading, and writes the reset
+ * observation: dnn (all variants) and, when mem is non-NULL, the 4-frame memory [dnn, 0, 0, 0].
+ * valid[e] (may be NULL) = 1 if the final draw is collision-free. range_lo/range_hi = range_start.
+ */
+int flock_reset(void* stream, int variant, int E, int N, int k, float range_lo, float range_hi, float box,
+                float sensor_range, float check_distance, int rigid_boundary, int max_attempts,
+                uint64_t seed, uint64_t rng_offset, const uint8_t* env_mask,
+                float* pos, float* heading, float* prev_heading, float* vel, float* dnn, int64_t* nn_idx,
+                float* mem, uint8_t* valid);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLOCK_AMD_H */

@@ -1,0 +1,816 @@
+// flock_env.hip — MI355X (gfx950) batched flocking-environment stepper. C ABI: include/flock_amd.h.
+//
+// One launch per vectorized step. A workgroup owns G whole envs (G = 256 / N for N <= 256, else 1; one agent per
+// lane), so every agent-agent pair of an env is visible in the workgroup's LDS and nothing crosses workgroups.
+//
+//   phase 1  kinematics + check_boundary for the lane's agent (reference _updateState / check_boundary), the new
+//            position is stored to HBM and to LDS [env][agent] (float2, env stride padded to even)
+//   phase 2  per-env float sums in a fixed power-of-two LDS tree (uw: centre of mass; uw_discrete: mean heading)
+//   phase 3  all-pairs scan: the lane streams its env's N positions from LDS (broadcast ds_read_b128, two
+//            candidates per read), computes d2 with the reference's op order, packs
+//            key = (bits(d2) with the low IB mantissa bits cleared) | j  (IB = ceil(log2 N)),
+//            and keeps the L = k+2 smallest keys in registers with a branch-free insertion network
+//            (1 v_min_u32 + (L-1) v_med3_u32 per candidate; no divergence, no sort)
+//   phase 4  exactness: the k+1 winners are re-sorted by their exact (d2, j); if the (k+2)-th key shares the
+//            truncated-d2 bucket of the (k+1)-th, the lane falls back to an exact (d2, j) rescan (rare). The
+//            result is the ascending (d2, j) order — a valid tie resolution of the reference's
+//            topk(-sqrt(d2), k+1) — identical to oracle/flock_oracle.c.
+//   phase 5  distances (correctly-rounded sqrt of the k winners only), clamp, collisions, done, per-env any_done
+//            (LDS atomic OR), reward, observation memory roll.
+//
+// Float arithmetic: every op is rounded separately (__fmul_rn / __fadd_rn / __fdiv_rn / __fsqrt_rn, and the file
+// is built with -ffp-contract=off), in the reference's op order; cosf/sinf are ocml's.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "flock_amd.h"
+
+namespace {
+
+constexpr int kMem = 4;  // observation memory depth (gym_flock_uw.py:59, gym_flock.py:42)
+constexpr int kSense = 4;  // internal variant: kNN only (flock_knn)
+constexpr float kHalfPi = 1.57079637f;  // float(pi/2): torch.clamp casts the bound to float (gym_flock_v2.py:327)
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+thread_local char g_err[256] = "";
+
+int fail(int code, const char* msg) {
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return code;
+}
+
+struct Params {
+    int E, N, k, G, S, P, ib;
+    int variant, periodic, rigid, clamp;
+    float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
+    uint64_t seed, rng_offset;
+    int n_actions;
+    float* pos;
+    float* heading;
+    float* prev_heading;
+    float* vel;
+    const float* action;
+    const int64_t* action_id;
+    const float* noise;
+    const float* table;
+    const float* mem_in;
+    float* mem_out;
+    float* dnn;
+    int64_t* idx;
+    float* reward;
+    uint8_t* done;
+    uint8_t* any_done;
+    int* status;
+    // reset
+    float range_lo, range_hi, head_hi, check_distance;
+    int max_attempts;
+    const uint8_t* env_mask;
+    uint8_t* valid;
+};
+
+// ---------------------------------------------------------------------------------------------------------------
+// small helpers
+
+__device__ __forceinline__ float clamp_t(float x, float lo, float hi) {  // torch.clamp: NaN propagates
+    x = (x < lo) ? lo : x;
+    return (x > hi) ? hi : x;
+}
+
+__device__ __forceinline__ float nan_to_num(float x) {  // torch.nan_to_num defaults
+    if (__builtin_isnan(x)) return 0.0f;
+    if (__builtin_isinf(x)) return x > 0.0f ? 3.402823466e+38f : -3.402823466e+38f;
+    return x;
+}
+
+// check_boundary, gym_flock_v2.py:271-304 (non-rigid: teleport to 0.001 / box, not a modulo)
+__device__ __forceinline__ float boundary(float v, float box, int rigid) {
+    if (rigid) {
+        v = (v < box) ? v : box;
+        return (v > 0.0f) ? v : 0.0f;
+    }
+    v = (v < box) ? v : 0.001f;
+    return (v > 0.0f) ? v : box;
+}
+
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// d2 with the reference op order: periodic gym_flock_v2.py:140-144 (|d|, B-|d| if |d| > B/2, mul, mul, add).
+// min(|d|, B-|d|) == where(|d| > B/2, B-|d|, |d|) bit for bit: B-|d| is exact for |d| >= B/2 (Sterbenz) and
+// rounds to >= B/2 otherwise.
+template <bool PERIODIC>
+__device__ __forceinline__ float pair_d2(float xi, float yi, float xj, float yj, float box) {
+    float dx = __fsub_rn(xi, xj);
+    float dy = __fsub_rn(yi, yj);
+    if (PERIODIC) {
+        const float ax = fabsf(dx), ay = fabsf(dy);
+        dx = fminf(ax, __fsub_rn(box, ax));
+        dy = fminf(ay, __fsub_rn(box, ay));
+    }
+    return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+}
+
+// Philox4x32-10 (Salmon et al. 2011), counter-based: (key = seed, counter = (c0, c1, c2, c3)).
+struct U4 {
+    uint32_t x, y, z, w;
+};
+__device__ __forceinline__ U4 philox(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return {c0, c1, c2, c3};
+}
+__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }  // [0,1)
+
+// ---------------------------------------------------------------------------------------------------------------
+// phase 3/4: kNN of one agent against its env's LDS-resident positions.
+// Output: bd[0..W) / bj[0..W) = the W = L-1 smallest (d2, j) in ascending order (slots beyond N: +inf / INT_MAX).
+
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N, int k, int ib, float xi, float yi,
+                                         float box, float (&bd)[L - 1], int (&bj)[L - 1]) {
+    constexpr int W = L - 1;
+    const uint32_t lo_mask = (1u << ib) - 1u, hi_mask = ~lo_mask;
+    uint32_t key[L];
+#pragma unroll
+    for (int s = 0; s < L; ++s) key[s] = kEmpty;
+
+    auto insert = [&](uint32_t kx) {
+        uint32_t nk[L];
+        nk[0] = min(key[0], kx);
+#pragma unroll
+        for (int s = 1; s < L; ++s) nk[s] = med3u(key[s - 1], kx, key[s]);
+#pragma unroll
+        for (int s = 0; s < L; ++s) key[s] = nk[s];
+    };
+
+    const float4* cand4 = reinterpret_cast<const float4*>(cand);
+    int j = 0;
+#pragma unroll 1
+    for (; j + 1 < N; j += 2) {
+        const float4 c = cand4[j >> 1];  // broadcast: every lane of the env reads the same 16 B
+        const float d0 = pair_d2<PERIODIC>(xi, yi, c.x, c.y, box);
+        const float d1 = pair_d2<PERIODIC>(xi, yi, c.z, c.w, box);
+        insert((__float_as_uint(d0) & hi_mask) | (uint32_t)j);
+        insert((__float_as_uint(d1) & hi_mask) | (uint32_t)(j + 1));
+    }
+    if (j < N) {
+        const float2 c = cand[j];
+        insert((__float_as_uint(pair_d2<PERIODIC>(xi, yi, c.x, c.y, box)) & hi_mask) | (uint32_t)j);
+    }
+
+    // (k+1)-th and (k+2)-th smallest keys (k is a runtime value <= L-2; static-index select, no scratch)
+    uint32_t kk = kEmpty, kr = kEmpty;
+#pragma unroll
+    for (int s = 0; s < L; ++s) {
+        if (s == k) kk = key[s];
+        if (s == k + 1) kr = key[s];
+    }
+    const bool ambiguous = (kr != kEmpty) && ((kr & hi_mask) == (kk & hi_mask));
+
+    if (!ambiguous) {
+        // exact (d2, j) for the W best keys, then an odd-even transposition sort (only same-bucket keys move)
+#pragma unroll
+        for (int s = 0; s < W; ++s) {
+            if (key[s] == kEmpty) {
+                bd[s] = __builtin_inff();
+                bj[s] = 0x7fffffff;
+            } else {
+                const int jj = (int)(key[s] & lo_mask);
+                const float2 c = cand[jj];
+                bd[s] = pair_d2<PERIODIC>(xi, yi, c.x, c.y, box);
+                bj[s] = jj;
+            }
+        }
+#pragma unroll
+        for (int pass = 0; pass < W; ++pass) {
+#pragma unroll
+            for (int s = (pass & 1); s + 1 < W; s += 2) {
+                const bool sw = (bd[s + 1] < bd[s]) || (bd[s + 1] == bd[s] && bj[s + 1] < bj[s]);
+                const float td = sw ? bd[s + 1] : bd[s];
+                const int tj = sw ? bj[s + 1] : bj[s];
+                bd[s + 1] = sw ? bd[s] : bd[s + 1];
+                bj[s + 1] = sw ? bj[s] : bj[s + 1];
+                bd[s] = td;
+                bj[s] = tj;
+            }
+        }
+    } else {
+        // exact rescan: branch-free ordered insertion of (d2, j); ascending j + strict '<' keeps lower j first
+#pragma unroll
+        for (int s = 0; s < W; ++s) {
+            bd[s] = __builtin_inff();
+            bj[s] = 0x7fffffff;
+        }
+        for (int jj = 0; jj < N; ++jj) {
+            const float2 c = cand[jj];
+            const float d = pair_d2<PERIODIC>(xi, yi, c.x, c.y, box);
+            if (d < bd[W - 1]) {
+                bool lt[W];
+#pragma unroll
+                for (int s = 0; s < W; ++s) lt[s] = d < bd[s];
+#pragma unroll
+                for (int s = W - 1; s >= 1; --s) {
+                    bd[s] = lt[s - 1] ? bd[s - 1] : (lt[s] ? d : bd[s]);
+                    bj[s] = lt[s - 1] ? bj[s - 1] : (lt[s] ? jj : bj[s]);
+                }
+                bd[0] = lt[0] ? d : bd[0];
+                bj[0] = lt[0] ? jj : bj[0];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// the fused step kernel
+
+template <int L, bool PERIODIC>
+__global__ __launch_bounds__(1024) void step_kernel(const Params p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float2* lpos = reinterpret_cast<float2*>(smem);               // [G][S]
+    float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
+    int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G]
+
+    const int t = threadIdx.x;
+    const int g = t / p.N;
+    const int i = t - g * p.N;
+    const int env = blockIdx.x * p.G + g;
+    const bool in_group = g < p.G;
+    const bool active = in_group && env < p.E;
+    const size_t a = (size_t)env * p.N + i;
+    const int variant = p.variant;
+    if (in_group && i == 0) flags[g] = 0;
+
+    // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
+    float x = 0.0f, y = 0.0f, h = 0.0f;
+    if (active) {
+        const float2 pp = reinterpret_cast<const float2*>(p.pos)[a];
+        x = pp.x;
+        y = pp.y;
+        if (variant == FLOCK_VARIANT_V2) {  // gym_flock_v2.py:317-350 (heading=True)
+            const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
+            const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
+            h = __fadd_rn(p.heading[a], __fmul_rn(ang, p.dt));               // :329
+            const float lin = clamp_t(ac.x, p.v_min, p.v_max);               // :331
+            float vx = __fmul_rn(lin, cosf(h));                              // :335
+            float vy = __fmul_rn(lin, sinf(h));                              // :336
+            vx = __fmul_rn(nan_to_num(vx), p.dt);                            // :346, :349
+            vy = __fmul_rn(nan_to_num(vy), p.dt);
+            x = __fadd_rn(x, vx);                                            // :350
+            y = __fadd_rn(y, vy);
+            p.heading[a] = h;
+            reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
+        } else if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:269-302 (heading=False)
+            const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
+            const float n = __fsqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
+            float vx = __fmul_rn(nan_to_num(__fdiv_rn(ac.x, n)), p.dt);     // :294-301
+            float vy = __fmul_rn(nan_to_num(__fdiv_rn(ac.y, n)), p.dt);
+            x = __fadd_rn(x, vx);                                            // :302
+            y = __fadd_rn(y, vy);
+            h = p.heading[a];
+            reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
+        } else if (variant == FLOCK_VARIANT_UW_DISCRETE) {  // gym_flock_uw_discrete.py:324-366
+            int64_t id = p.action_id[a];
+            if (id < 0 || id >= p.n_actions) {  // the reference raises KeyError (:329)
+                if (p.status) atomicOr(p.status, 1);
+                id = 0;
+            }
+            const float2 mean = reinterpret_cast<const float2*>(p.table)[id];
+            float nl, na;
+            if (p.noise) {
+                const float2 nz = reinterpret_cast<const float2*>(p.noise)[a];
+                nl = nz.x;
+                na = nz.y;
+            } else {  // torch.normal(mean, 0.1) (:333-334): Box-Muller on Philox uniforms
+                const U4 r = philox(p.seed, (uint32_t)a, (uint32_t)(a >> 32), (uint32_t)p.rng_offset,
+                                    (uint32_t)(p.rng_offset >> 32) ^ 0x5EEDu);
+                const float u1 = fmaxf(u01(r.x), 1.0f / 16777216.0f), u2 = u01(r.y);
+                const float rad = sqrtf(-2.0f * logf(u1));
+                nl = rad * cosf(6.28318530718f * u2) * p.noise_std;
+                na = rad * sinf(6.28318530718f * u2) * p.noise_std;
+            }
+            float lin = __fadd_rn(mean.x, nl);
+            const float ang = clamp_t(__fadd_rn(mean.y, na), -0.025f, 0.025f);  // :343
+            h = __fadd_rn(p.heading[a], __fmul_rn(ang, p.dt));                   // :345
+            lin = clamp_t(lin, 5e-6f, p.v_max);                                   // :347
+            float vx = __fmul_rn(lin, cosf(h));                                   // :351
+            float vy = __fmul_rn(lin, sinf(h));                                   // :352
+            const float n = __fsqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :358
+            vx = __fmul_rn(nan_to_num(__fdiv_rn(vx, n)), p.dt);                  // :358-365
+            vy = __fmul_rn(nan_to_num(__fdiv_rn(vy, n)), p.dt);
+            x = __fadd_rn(x, vx);                                                 // :366
+            y = __fadd_rn(y, vy);
+            p.heading[a] = h;
+            reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
+        } else if (variant == FLOCK_VARIANT_FLOCK) {  // gym_flock.py:194-200
+            const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
+            const float2 v0 = reinterpret_cast<const float2*>(p.vel)[a];
+            float vx = __fadd_rn(v0.x, __fmul_rn(ac.x, p.dt));                   // :196
+            float vy = __fadd_rn(v0.y, __fmul_rn(ac.y, p.dt));
+            const float n = __fsqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :198
+            vx = __fdiv_rn(vx, n);
+            vy = __fdiv_rn(vy, n);
+            x = __fadd_rn(x, __fmul_rn(vx, p.dt));                               // :200
+            y = __fadd_rn(y, __fmul_rn(vy, p.dt));
+            reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
+        }
+        if (variant != kSense) {
+            x = boundary(x, p.box, p.rigid);  // check_boundary :271-304
+            y = boundary(y, p.box, p.rigid);
+            reinterpret_cast<float2*>(p.pos)[a] = make_float2(x, y);
+        }
+        lpos[g * p.S + i] = make_float2(x, y);
+    }
+
+    // ---- phase 2: per-env sums in a fixed tree order (same order as oracle tree_sum) -------------------------
+    float s0 = 0.0f, s1 = 0.0f;
+    if (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_UW_DISCRETE) {
+        float* r0 = red + (size_t)g * 2 * p.P;
+        float* r1 = r0 + p.P;
+        if (in_group) {
+            r0[i] = active ? (variant == FLOCK_VARIANT_UW ? x : h) : 0.0f;
+            r1[i] = active ? y : 0.0f;
+            if (i < p.P - p.N) {
+                r0[p.N + i] = 0.0f;
+                r1[p.N + i] = 0.0f;
+            }
+        }
+        __syncthreads();
+        for (int s = p.P >> 1; s >= 1; s >>= 1) {
+            if (in_group && i < s) {
+                r0[i] = __fadd_rn(r0[i], r0[i + s]);
+                r1[i] = __fadd_rn(r1[i], r1[i + s]);
+            }
+            __syncthreads();
+        }
+        if (in_group) {
+            s0 = __fdiv_rn(r0[0], (float)p.N);
+            s1 = __fdiv_rn(r1[0], (float)p.N);
+        }
+    } else {
+        __syncthreads();
+    }
+
+    // ---- phase 3/4: kNN -------------------------------------------------------------------------------
+    float bd[L - 1];
+    int bj[L - 1];
+    if (active) knn_scan<L, PERIODIC>(lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);
+
+    // ---- phase 5: outputs -----------------------------------------------------------------------------
+    int coll = 0;
+    if (active) {
+        float dv[L - 1];
+#pragma unroll
+        for (int s = 1; s < L - 1; ++s) {
+            if (s <= p.k) {
+                float d = __fsqrt_rn(bd[s]);
+                if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);  // gym_flock_v2.py:151
+                dv[s - 1] = d;
+                coll |= (d < p.cd);                                   // :212-215
+                p.dnn[a * p.k + (s - 1)] = d;
+                if (p.idx) p.idx[a * p.k + (s - 1)] = (int64_t)bj[s];
+            }
+        }
+        if (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK) {  // torch.roll + insert (:120-123)
+            const float* mi = p.mem_in + a * kMem * p.k;
+            float* mo = p.mem_out + a * kMem * p.k;
+            for (int c = 0; c < p.k; ++c) {
+                for (int s = kMem - 1; s >= 1; --s) mo[s * p.k + c] = mi[(s - 1) * p.k + c];
+            }
+#pragma unroll
+            for (int s = 0; s < L - 2; ++s)
+                if (s < p.k) mo[s] = dv[s];
+        }
+        if (variant != kSense) {
+            p.done[a] = (uint8_t)coll;
+            float r;
+            if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:206-221
+                const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
+                const float dist = __fsqrt_rn(__fadd_rn(__fmul_rn(com_x, com_x), __fmul_rn(com_y, com_y)));
+                const float com = (dist < p.com_r) ? 0.01f : 0.0f;                  // :197
+                const float prev = p.prev_heading[a];
+                const float angp = (fabsf(__fsub_rn(prev, h)) > 0.27f) ? -0.01f : 0.001f;  // :202-204
+                p.prev_heading[a] = h;
+                r = __fadd_rn(__fadd_rn(coll ? -5.0f : 0.01f, com), angp);          // :220
+            } else if (variant == FLOCK_VARIANT_UW_DISCRETE) {  // gym_flock_uw_discrete.py:260-276
+                const float err = fabsf(__fsub_rn(s0, h));                            // :256-257
+                const float align = (err > 0.2f) ? 0.0f : 0.1f;                       // :258
+                p.prev_heading[a] = h;                                                // :270 side effect
+                r = __fadd_rn(coll ? -9.0f : 0.0f, align);                            // :237, :275
+            } else {
+                r = coll ? -5.0f : 0.01f;  // gym_flock_v2.py:217-220, gym_flock.py:142-145
+            }
+            p.reward[a] = r;
+        }
+    }
+    if (variant != kSense) {
+        if (active && coll) atomicOr(&flags[g], 1);
+        __syncthreads();
+        if (active && i == 0) p.any_done[env] = (uint8_t)flags[g];  // _computeDone :306-315
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// reset: bounded in-kernel rejection sampling (replaces the reference's unbounded recursion)
+
+template <int L>
+__global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float2* lpos = reinterpret_cast<float2*>(smem);
+    int* flags = reinterpret_cast<int*>(lpos + p.G * p.S);  // [G] collision flag of the current attempt
+    int* state = flags + p.G;                                // [G] 1 = still drawing
+
+    const int t = threadIdx.x;
+    const int g = t / p.N;
+    const int i = t - g * p.N;
+    const int env = blockIdx.x * p.G + g;
+    const bool in_group = g < p.G;
+    const bool active = in_group && env < p.E;
+    const size_t a = (size_t)env * p.N + i;
+    if (in_group && i == 0) state[g] = (env < p.E) && (p.env_mask == nullptr || p.env_mask[env] != 0);
+    __syncthreads();
+
+    float x = 0.0f, y = 0.0f, h = 0.0f;
+    float bd[L - 1];
+    int bj[L - 1];
+    for (int attempt = 0; attempt < p.max_attempts; ++attempt) {
+        const bool drawing = in_group && state[g];
+        if (in_group && i == 0) flags[g] = 0;
+        if (active && drawing) {
+            const uint64_t ctr = p.rng_offset + (uint64_t)attempt;
+            const U4 r = philox(p.seed, (uint32_t)a, (uint32_t)(a >> 32), (uint32_t)ctr, (uint32_t)(ctr >> 32));
+            // positions = (lo - hi) * U + hi  in (lo, hi]   (gym_flock_v2.py:87-89 and siblings)
+            const float span = p.range_lo - p.range_hi;
+            x = __fadd_rn(__fmul_rn(span, u01(r.x)), p.range_hi);
+            y = __fadd_rn(__fmul_rn(span, u01(r.y)), p.range_hi);
+            h = __fadd_rn(__fmul_rn(-p.head_hi, u01(r.z)), p.head_hi);  // headings (0 - c) * U + c  (:96)
+            x = boundary(x, p.box, p.rigid);                             // :99
+            y = boundary(y, p.box, p.rigid);
+            lpos[g * p.S + i] = make_float2(x, y);
+        }
+        __syncthreads();
+        if (active && drawing) {
+            knn_scan<L, false>(lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);  // Euclidean (:100)
+            int coll = 0;
+#pragma unroll
+            for (int s = 1; s < L - 1; ++s)
+                if (s <= p.k) {
+                    float d = __fsqrt_rn(bd[s]);
+                    if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);
+                    coll |= (d < p.check_distance);
+                }
+            if (coll) atomicOr(&flags[g], 1);
+        }
+        __syncthreads();
+        int more = 0;
+        if (in_group && i == 0 && state[g]) {
+            state[g] = flags[g];  // keep drawing while the draw has a collision (:105-108)
+        }
+        __syncthreads();
+        if (in_group) more = state[g];
+        if (!__syncthreads_or(more)) break;
+    }
+    const bool touched = active && (p.env_mask == nullptr || p.env_mask[env] != 0);
+    if (touched) {
+        reinterpret_cast<float2*>(p.pos)[a] = make_float2(x, y);
+        if (p.heading) p.heading[a] = h;
+        if (p.prev_heading) p.prev_heading[a] = 0.0f;
+        if (p.vel) reinterpret_cast<float2*>(p.vel)[a] = make_float2(0.0f, 0.0f);
+#pragma unroll
+        for (int s = 1; s < L - 1; ++s) {
+            if (s <= p.k) {
+                float d = __fsqrt_rn(bd[s]);
+                if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);
+                p.dnn[a * p.k + (s - 1)] = d;
+                if (p.idx) p.idx[a * p.k + (s - 1)] = (int64_t)bj[s];
+                if (p.mem_out) {
+                    float* mo = p.mem_out + a * kMem * p.k;
+                    mo[s - 1] = d;
+                    for (int f = 1; f < kMem; ++f) mo[f * p.k + (s - 1)] = 0.0f;
+                }
+            }
+        }
+        if (i == 0 && p.valid) p.valid[env] = (uint8_t)(state[g] == 0);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// host side
+
+int ceil_log2(int n) {
+    int b = 0;
+    while ((1 << b) < n) ++b;
+    return b;
+}
+
+struct Cfg {
+    int G, T, S, P, blocks;
+    size_t lds;
+};
+
+Cfg make_cfg(int E, int N, bool reset) {
+    Cfg c;
+    c.S = (N + 1) & ~1;
+    c.P = 1 << ceil_log2(N);
+    c.G = (N <= 256) ? (256 / N) : 1;
+    c.T = ((c.G * N + 63) / 64) * 64;
+    c.blocks = (E + c.G - 1) / c.G;
+    if (reset)
+        c.lds = (size_t)c.G * c.S * sizeof(float2) + 2 * c.G * sizeof(int);
+    else
+        c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + c.G * sizeof(int);
+    return c;
+}
+
+int check_common(int E, int N, int k) {
+    if (E < 0 || N < 1) return fail(FLOCK_E_ARG, "E must be >= 0 and N >= 1");
+    if (k < 1 || k + 1 > N) return fail(FLOCK_E_K_RANGE, "selected index k out of range");
+    if (k > 15) return fail(FLOCK_E_LIMIT, "this build supports k <= 15");
+    if (N > 1024) return fail(FLOCK_E_LIMIT, "this build supports N <= 1024 agents per env");
+    return FLOCK_OK;
+}
+
+template <int L>
+void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
+    if (p.periodic)
+        hipLaunchKernelGGL((step_kernel<L, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+    else
+        hipLaunchKernelGGL((step_kernel<L, false>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+}
+
+template <int L>
+void launch_reset_L(const Cfg& c, const Params& p, hipStream_t s) {
+    hipLaunchKernelGGL((reset_kernel<L>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+}
+
+int dispatch(Params& p, hipStream_t s, bool reset) {
+    if (p.E == 0) return FLOCK_OK;
+    const Cfg c = make_cfg(p.E, p.N, reset);
+    p.G = c.G;
+    p.S = c.S;
+    p.P = c.P;
+    p.ib = ceil_log2(p.N);
+    if (p.ib < 1) p.ib = 1;
+#define FLOCK_CASE(LL)                                   \
+    case LL:                                             \
+        if (reset)                                       \
+            launch_reset_L<LL>(c, p, s);                 \
+        else                                             \
+            launch_step_L<LL>(c, p, s);                  \
+        break;
+    const int L = (p.k + 2 <= 12) ? p.k + 2 : 17;
+    switch (L) {
+        FLOCK_CASE(3)
+        FLOCK_CASE(4)
+        FLOCK_CASE(5)
+        FLOCK_CASE(6)
+        FLOCK_CASE(7)
+        FLOCK_CASE(8)
+        FLOCK_CASE(9)
+        FLOCK_CASE(10)
+        FLOCK_CASE(11)
+        FLOCK_CASE(12)
+        FLOCK_CASE(17)
+        default:
+            return fail(FLOCK_E_LIMIT, "unsupported k");
+    }
+#undef FLOCK_CASE
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FLOCK_E_LAUNCH, hipGetErrorString(e));
+    return FLOCK_OK;
+}
+
+Params base(int E, int N, int k, float box) {
+    Params p;
+    memset(&p, 0, sizeof(p));
+    p.E = E;
+    p.N = N;
+    p.k = k;
+    p.box = box;
+    p.clamp = 1;
+    return p;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------------------
+// C ABI
+
+extern "C" {
+
+int flock_abi_version(void) { return FLOCK_ABI_VERSION; }
+
+const char* flock_last_error(void) { return g_err; }
+
+int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                  float dt, float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
+                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
+                  uint8_t* any_done) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done))
+        return fail(FLOCK_E_NULL, "flock_step_v2: NULL pointer");
+    Params p = base(E, N, k, box);
+    p.variant = FLOCK_VARIANT_V2;
+    p.periodic = periodic != 0;
+    p.rigid = rigid_boundary != 0;
+    p.sensor_range = sensor_range;
+    p.cd = collision_distance;
+    p.dt = dt;
+    p.v_min = v_min;
+    p.v_max = v_max;
+    p.pos = pos;
+    p.heading = heading;
+    p.action = action;
+    p.vel = vel;
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    p.reward = reward;
+    p.done = done;
+    p.any_done = any_done;
+    return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                  float dt, int rigid_boundary, float* pos, const float* heading, float* prev_heading,
+                  const float* action, const float* mem_in, float* mem_out, float* vel, float* dnn, int64_t* nn_idx,
+                  float* reward, uint8_t* done, uint8_t* any_done) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !heading || !prev_heading || !action || !mem_in || !mem_out || !vel || !dnn || !reward ||
+              !done || !any_done))
+        return fail(FLOCK_E_NULL, "flock_step_uw: NULL pointer");
+    Params p = base(E, N, k, box);
+    p.variant = FLOCK_VARIANT_UW;
+    p.rigid = rigid_boundary != 0;
+    p.sensor_range = sensor_range;
+    p.cd = collision_distance;
+    p.com_r = (float)((double)collision_distance * 4.0);  // collision_distance*4 (gym_flock_uw.py:197)
+    p.dt = dt;
+    p.pos = pos;
+    p.heading = const_cast<float*>(heading);
+    p.prev_heading = prev_heading;
+    p.action = action;
+    p.mem_in = mem_in;
+    p.mem_out = mem_out;
+    p.vel = vel;
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    p.reward = reward;
+    p.done = done;
+    p.any_done = any_done;
+    return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_step_uw_discrete(void* stream, int E, int N, int k, float box, float sensor_range,
+                           float collision_distance, float dt, float v_max, int rigid_boundary, float* pos,
+                           float* heading, float* prev_heading, const int64_t* action_id, const float* noise,
+                           float noise_std, uint64_t seed, uint64_t rng_offset, const float* table, int n_actions,
+                           float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                           int* status) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !heading || !prev_heading || !action_id || !table || !vel || !dnn || !reward || !done ||
+              !any_done))
+        return fail(FLOCK_E_NULL, "flock_step_uw_discrete: NULL pointer");
+    if (n_actions < 1) return fail(FLOCK_E_ARG, "n_actions must be >= 1");
+    Params p = base(E, N, k, box);
+    p.variant = FLOCK_VARIANT_UW_DISCRETE;
+    p.rigid = rigid_boundary != 0;
+    p.sensor_range = sensor_range;
+    p.cd = collision_distance;
+    p.dt = dt;
+    p.v_max = v_max;
+    p.noise_std = noise_std;
+    p.seed = seed;
+    p.rng_offset = rng_offset;
+    p.pos = pos;
+    p.heading = heading;
+    p.prev_heading = prev_heading;
+    p.action_id = action_id;
+    p.noise = noise;
+    p.table = table;
+    p.n_actions = n_actions;
+    p.vel = vel;
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    p.reward = reward;
+    p.done = done;
+    p.any_done = any_done;
+    p.status = status;
+    return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_step_flock(void* stream, int E, int N, int k, float box, float collision_distance, float dt,
+                     int rigid_boundary, float* pos, float* vel, const float* action, const float* mem_in,
+                     float* mem_out, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !vel || !action || !mem_in || !mem_out || !dnn || !reward || !done || !any_done))
+        return fail(FLOCK_E_NULL, "flock_step_flock: NULL pointer");
+    Params p = base(E, N, k, box);
+    p.variant = FLOCK_VARIANT_FLOCK;
+    p.rigid = rigid_boundary != 0;
+    p.clamp = 0;  // gym_flock.py:105: no clamp
+    p.cd = collision_distance;
+    p.dt = dt;
+    p.pos = pos;
+    p.vel = vel;
+    p.action = action;
+    p.mem_in = mem_in;
+    p.mem_out = mem_out;
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    p.reward = reward;
+    p.done = done;
+    p.any_done = any_done;
+    return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_knn(void* stream, int E, int N, int k, float box, float sensor_range, int periodic, int clamp,
+              const float* pos, float* dnn, int64_t* nn_idx) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !dnn)) return fail(FLOCK_E_NULL, "flock_knn: NULL pointer");
+    Params p = base(E, N, k, box);
+    p.variant = kSense;
+    p.periodic = periodic != 0;
+    p.clamp = clamp != 0;
+    p.sensor_range = sensor_range;
+    p.cd = 0.0f;
+    p.pos = const_cast<float*>(pos);
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_reset(void* stream, int variant, int E, int N, int k, float range_lo, float range_hi, float box,
+                float sensor_range, float check_distance, int rigid_boundary, int max_attempts, uint64_t seed,
+                uint64_t rng_offset, const uint8_t* env_mask, float* pos, float* heading, float* prev_heading,
+                float* vel, float* dnn, int64_t* nn_idx, float* mem, uint8_t* valid) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !dnn)) return fail(FLOCK_E_NULL, "flock_reset: NULL pointer");
+    if (max_attempts < 1) return fail(FLOCK_E_ARG, "max_attempts must be >= 1");
+    Params p = base(E, N, k, box);
+    p.variant = variant;
+    p.rigid = rigid_boundary != 0;
+    p.sensor_range = sensor_range;
+    p.check_distance = check_distance;
+    p.max_attempts = max_attempts;
+    p.seed = seed;
+    p.rng_offset = rng_offset;
+    p.env_mask = env_mask;
+    p.pos = pos;
+    p.heading = heading;
+    p.prev_heading = prev_heading;
+    p.vel = vel;
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    p.mem_out = mem;
+    p.valid = valid;
+    p.clamp = (variant == FLOCK_VARIANT_FLOCK) ? 0 : 1;
+    switch (variant) {  // position range and heading range per reference reset()
+        case FLOCK_VARIANT_V2:  // gym_flock_v2.py:87-96
+            p.range_lo = range_lo;
+            p.range_hi = range_hi;
+            p.head_hi = 4.71238898f;  // float(pi*1.5)
+            break;
+        case FLOCK_VARIANT_UW:  // gym_flock_uw.py:87-92: (r0 - r1//2) * U + r1//2, headings (0, 2pi]
+            p.range_lo = range_lo;
+            p.range_hi = (float)(long long)(range_hi / 2);
+            p.head_hi = 6.28318548f;
+            break;
+        case FLOCK_VARIANT_UW_DISCRETE:  // gym_flock_uw_discrete.py:125-133: headings (0, pi/1.2]
+            p.range_lo = range_lo;
+            p.range_hi = range_hi;
+            p.head_hi = 2.61799383f;
+            break;
+        case FLOCK_VARIANT_FLOCK:  // gym_flock.py:63
+            p.range_lo = range_lo;
+            p.range_hi = range_hi;
+            p.head_hi = 0.0f;
+            break;
+        default:
+            return fail(FLOCK_E_ARG, "unknown variant");
+    }
+    return dispatch(p, (hipStream_t)stream, true);
+}
+
+}  // extern "C"

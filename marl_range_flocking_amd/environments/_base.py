@@ -1,0 +1,141 @@
+"""Single-env ``gym.Env`` surface over VecFlockEnv(E=1): what the reference's callers touch, unchanged.
+
+Callers: main.py:15,26,34; learners/maddpg_official_rnn/train_flock.py; learners/vdn/
+train_flock.py:78-101; learners/maddpg_shared_critic/train_flock.py:36-117. They use ``reset()``, ``step(action)``
+returning ``(obs, reward (N,1), (dones (N,) bool, all_done: bool), {})``, ``num_particles``, ``k``, the spaces, and
+the state attributes ``positions / velocities / headings / nearest_neighbors`` (render, tests).
+
+State attributes are views of the device tensors; assigning to them (e.g. ``env.positions = t``) copies into the
+device state, which is how tests inject state into the reference envs too.
+"""
+import torch
+
+from ..vec_env import FlockConfig, VecFlockEnv
+
+try:
+    import gym  # type: ignore
+
+    _EnvBase = gym.Env
+except Exception:  # noqa: BLE001 - gym is not installed in this image
+    _EnvBase = object
+
+
+def _default_device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("marl_range_flocking_amd environments need a HIP device (MI355X); no CPU fallback")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class SingleFlockEnv(_EnvBase):
+    variant = "v2"
+    memory_size = 4
+
+    def __init__(self, agents, k, collision_distance, normalize_distance=False, rigid_boundary=False,
+                 range_start=(0, 100), sensor_range=7, max_linear_velocity=2.5, desired_distance=15, *,
+                 periodic=None, v_min=None, device=None, seed=0, max_reset_attempts=1024):
+        if normalize_distance:
+            # _computeDistances(normalize) (gym_flock_v2.py:157-163) is dead code in make_env (:424); not built.
+            raise NotImplementedError("normalize_distance=True is not supported by the HIP stepper")
+        self.num_particles = agents
+        self.k = k
+        self.rigid_boundary = rigid_boundary
+        self.boundary = range_start[1]
+        self.desired_distance = desired_distance
+        self.range_start = range_start
+        self.sensor_range = sensor_range
+        self.max_linear_velocity = max_linear_velocity
+        self.collision_distance = collision_distance
+        self.normalize_distances = normalize_distance
+        self._vec = VecFlockEnv(
+            FlockConfig(variant=self.variant, num_envs=1, num_agents=agents, k=k,
+                        collision_distance=collision_distance, range_start=tuple(range_start),
+                        sensor_range=sensor_range, max_linear_velocity=max_linear_velocity,
+                        rigid_boundary=rigid_boundary, periodic=periodic, v_min=v_min, seed=seed,
+                        max_reset_attempts=max_reset_attempts),
+            device=device or _default_device())
+        self.device = self._vec.device
+        # like the reference ctor (gym_flock_v2.py:54-57): random positions before the first reset
+        self._vec.positions.uniform_(0.0, 1.0).mul_(float(range_start[0] - range_start[1])).add_(range_start[1])
+
+    # ---- state views (shape as in the reference: (N, 2), (N,), (N, k)) --------------------------------------
+    def _view(name):  # noqa: N805
+        def get(self):
+            return getattr(self._vec, name)[0]
+
+        def set_(self, value):
+            getattr(self._vec, name)[0].copy_(torch.as_tensor(value).to(self.device).reshape(get(self).shape))
+
+        return property(get, set_)
+
+    positions = _view("positions")
+    velocities = _view("velocities")
+    headings = _view("headings")
+    prev_headings = _view("prev_headings")
+
+    @property
+    def distances_to_nearest_neighbors(self):
+        return self._vec.dnn[0]
+
+    @property
+    def nearest_neighbors(self):
+        return self._vec.nn_idx[0]
+
+    @property
+    def collisions(self):
+        return torch.where(self.distances_to_nearest_neighbors < self.collision_distance, 1, 0)
+
+    @property
+    def observation_memory(self):
+        m = self._vec.obs_memory
+        return None if m is None else m[0]
+
+    @observation_memory.setter
+    def observation_memory(self, value):
+        self._vec.obs_memory[0].copy_(torch.as_tensor(value).to(self.device))
+
+    # ---- gym surface ------------------------------------------------------------------------------------------
+    def _obs(self):
+        raise NotImplementedError
+
+    def _action(self, action):
+        a = torch.as_tensor(action)
+        return a.to(device=self.device)
+
+    def step(self, action, dt=0.1):
+        self._vec.step(self._action(action)[None], dt=dt)
+        dones = self._vec.done[0].clone()
+        all_done = bool(self._vec.any_done[0].item())  # the reference's host sync (gym_flock_v2.py:315)
+        return self._obs(), self._vec.reward[0].reshape(-1, 1).clone(), (dones, all_done), {}
+
+    def reset(self):
+        self._vec.reset()
+        return self._obs()
+
+    @property
+    def reset_valid(self):
+        """False if the bounded rejection sampling ran out of attempts (the reference would recurse on)."""
+        return bool(self._vec.valid[0].item())
+
+    def render(self):
+        import matplotlib.pyplot as plt
+
+        plt.ion()
+        pos = self.positions.detach().cpu()
+        vel = self.velocities.detach().cpu()
+        diff = pos - vel
+        plt.clf()
+        plt.gca().add_patch(plt.Rectangle((0, 0), self.boundary, self.boundary, fill=False))
+        plt.quiver(diff[:, 0], diff[:, 1], vel[:, 0], vel[:, 1], cmap="coolwarm")
+        plt.scatter(pos[:, 0], pos[:, 1], color="black", s=20)
+        plt.gca().add_patch(plt.Circle((float(pos[0, 0]), float(pos[0, 1])), self.sensor_range, fill=False))
+        plt.draw()
+        plt.axis([-10, self.boundary + 10, -10, self.boundary + 10])
+        plt.pause(0.001)
+
+    def close(self):
+        try:
+            import matplotlib.pyplot as plt
+
+            plt.close()
+        except Exception:  # noqa: BLE001
+            pass

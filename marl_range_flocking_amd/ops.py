@@ -1,0 +1,199 @@
+"""Torch-facing wrappers of the C ABI (include/flock_amd.h).
+
+Each function checks device / dtype / shape / contiguity, passes raw device pointers and the current HIP stream to
+libflock_amd.so and returns nothing (outputs are written into the tensors given). No host synchronisation happens
+here. Errors mirror the reference: ``k + 1 > N`` raises ``RuntimeError("selected index k out of range")`` as
+torch.topk does in gym_flock_v2.py:147.
+"""
+import ctypes
+
+import torch
+
+from . import _native
+
+UWD_TABLE = ((0.2, -1.2), (0.2, -0.5), (0.2, 0.0), (0.2, 0.5), (0.2, 1.2),
+             (0.6, -1.2), (0.6, -0.5), (0.6, 0.0), (0.6, 0.5), (0.6, 1.2))  # gym_flock_uw_discrete.py:59-75
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _need(t, name, dtype, shape, device):
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if t.device != device:
+        raise ValueError(f"{name} must be on {device}, got {t.device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _opt(t, name, dtype, shape, device):
+    if t is not None:
+        _need(t, name, dtype, shape, device)
+
+
+def _dims(pos):
+    if pos.dim() != 3 or pos.shape[-1] != 2:
+        raise ValueError(f"pos must be [E, N, 2], got {tuple(pos.shape)}")
+    if pos.device.type != "cuda":
+        raise RuntimeError("flock ops run on a HIP device only (no CPU fallback); got " + str(pos.device))
+    return pos.shape[0], pos.shape[1], pos.device
+
+
+def _check_k(N, k):
+    if k < 1 or k + 1 > N:
+        raise RuntimeError("selected index k out of range")
+
+
+def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k, box, sensor_range,
+            collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False):
+    """gym_flock_v2.MultiAgentEnv.step (gym_flock_v2.py:71-83) for E envs; pos/heading updated in place."""
+    E, N, dev = _dims(pos)
+    _check_k(N, k)
+    f32 = torch.float32
+    _need(pos, "pos", f32, (E, N, 2), dev)
+    _need(heading, "heading", f32, (E, N), dev)
+    _need(action, "action", f32, (E, N, 2), dev)
+    _need(vel, "vel", f32, (E, N, 2), dev)
+    _need(dnn, "dnn", f32, (E, N, k), dev)
+    _opt(nn_idx, "nn_idx", torch.int64, (E, N, k), dev)
+    _need(reward, "reward", f32, (E, N), dev)
+    _need(done, "done", torch.bool, (E, N), dev)
+    _need(any_done, "any_done", torch.bool, (E,), dev)
+    rc = _native.lib().flock_step_v2(
+        _stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt), float(v_min),
+        float(v_max), int(bool(periodic)), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(action),
+        _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
+    _native.check(rc, "flock_step_v2")
+
+
+def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done, *, k, box,
+            sensor_range, collision_distance, dt=0.1, rigid_boundary=False):
+    """gym_flock_uw.MultiAgentEnv.step (gym_flock_uw.py:69-81); mem_out = rolled 4-frame observation."""
+    E, N, dev = _dims(pos)
+    _check_k(N, k)
+    f32 = torch.float32
+    _need(pos, "pos", f32, (E, N, 2), dev)
+    _need(heading, "heading", f32, (E, N), dev)
+    _need(prev_heading, "prev_heading", f32, (E, N), dev)
+    _need(action, "action", f32, (E, N, 2), dev)
+    _need(mem_in, "mem_in", f32, (E, N, 4, k), dev)
+    _need(mem_out, "mem_out", f32, (E, N, 4, k), dev)
+    _need(vel, "vel", f32, (E, N, 2), dev)
+    _need(dnn, "dnn", f32, (E, N, k), dev)
+    _opt(nn_idx, "nn_idx", torch.int64, (E, N, k), dev)
+    _need(reward, "reward", f32, (E, N), dev)
+    _need(done, "done", torch.bool, (E, N), dev)
+    _need(any_done, "any_done", torch.bool, (E,), dev)
+    rc = _native.lib().flock_step_uw(
+        _stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
+        int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action), _ptr(mem_in),
+        _ptr(mem_out), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
+    _native.check(rc, "flock_step_uw")
+
+
+def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
+                     status=None, *, k, box, sensor_range, collision_distance, dt=0.1, v_max=2.5, rigid_boundary=False,
+                     noise_std=0.1, seed=0, rng_offset=0):
+    """gym_flock_uw_discrete.MultiAgentEnv.step (gym_flock_uw_discrete.py:110-122). noise=None → in-kernel
+    Philox N(0, noise_std) draws; otherwise noise [E,N,2] is added to the action-table means (parity mode)."""
+    E, N, dev = _dims(pos)
+    _check_k(N, k)
+    f32 = torch.float32
+    _need(pos, "pos", f32, (E, N, 2), dev)
+    _need(heading, "heading", f32, (E, N), dev)
+    _need(prev_heading, "prev_heading", f32, (E, N), dev)
+    _need(action_id, "action_id", torch.int64, (E, N), dev)
+    _opt(noise, "noise", f32, (E, N, 2), dev)
+    if table.dim() != 2 or table.shape[1] != 2:
+        raise ValueError("table must be [n_actions, 2]")
+    _need(table, "table", f32, tuple(table.shape), dev)
+    _need(vel, "vel", f32, (E, N, 2), dev)
+    _need(dnn, "dnn", f32, (E, N, k), dev)
+    _opt(nn_idx, "nn_idx", torch.int64, (E, N, k), dev)
+    _need(reward, "reward", f32, (E, N), dev)
+    _need(done, "done", torch.bool, (E, N), dev)
+    _need(any_done, "any_done", torch.bool, (E,), dev)
+    _opt(status, "status", torch.int32, (1,), dev)
+    rc = _native.lib().flock_step_uw_discrete(
+        _stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt), float(v_max),
+        int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action_id), _ptr(noise),
+        float(noise_std), int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(table), int(table.shape[0]),
+        _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done), _ptr(status))
+    _native.check(rc, "flock_step_uw_discrete")
+
+
+def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, *, k, box, collision_distance,
+               dt=0.1, rigid_boundary=False):
+    """gym_flock.MultiAgentEnv.step (gym_flock.py:48-60); vel is the unit-velocity state (rw)."""
+    E, N, dev = _dims(pos)
+    _check_k(N, k)
+    f32 = torch.float32
+    _need(pos, "pos", f32, (E, N, 2), dev)
+    _need(vel, "vel", f32, (E, N, 2), dev)
+    _need(action, "action", f32, (E, N, 2), dev)
+    _need(mem_in, "mem_in", f32, (E, N, 4, k), dev)
+    _need(mem_out, "mem_out", f32, (E, N, 4, k), dev)
+    _need(dnn, "dnn", f32, (E, N, k), dev)
+    _opt(nn_idx, "nn_idx", torch.int64, (E, N, k), dev)
+    _need(reward, "reward", f32, (E, N), dev)
+    _need(done, "done", torch.bool, (E, N), dev)
+    _need(any_done, "any_done", torch.bool, (E,), dev)
+    rc = _native.lib().flock_step_flock(
+        _stream(pos), E, N, k, float(box), float(collision_distance), float(dt), int(bool(rigid_boundary)), _ptr(pos),
+        _ptr(vel), _ptr(action), _ptr(mem_in), _ptr(mem_out), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done),
+        _ptr(any_done))
+    _native.check(rc, "flock_step_flock")
+
+
+def knn(pos, k, box, sensor_range=14.0, periodic=True, clamp=True, dnn=None, nn_idx=None):
+    """kNN sensing only (gym_flock_v2.py:135-151 periodic, :155-175 Euclidean). Returns (dnn, nn_idx)."""
+    E, N, dev = _dims(pos)
+    _check_k(N, k)
+    _need(pos, "pos", torch.float32, (E, N, 2), dev)
+    if dnn is None:
+        dnn = torch.empty((E, N, k), dtype=torch.float32, device=dev)
+    if nn_idx is None:
+        nn_idx = torch.empty((E, N, k), dtype=torch.int64, device=dev)
+    _need(dnn, "dnn", torch.float32, (E, N, k), dev)
+    _need(nn_idx, "nn_idx", torch.int64, (E, N, k), dev)
+    rc = _native.lib().flock_knn(_stream(pos), E, N, k, float(box), float(sensor_range), int(bool(periodic)),
+                                 int(bool(clamp)), _ptr(pos), _ptr(dnn), _ptr(nn_idx))
+    _native.check(rc, "flock_knn")
+    return dnn, nn_idx
+
+
+VARIANT_IDS = {"v2": 0, "uw": 1, "uw_discrete": 2, "flock": 3}
+
+
+def reset(variant, pos, dnn, *, k, range_start, box, sensor_range, check_distance, heading=None, prev_heading=None,
+          vel=None, nn_idx=None, mem=None, valid=None, env_mask=None, rigid_boundary=False, max_attempts=64, seed=0,
+          rng_offset=0):
+    """Device-side reset with bounded rejection sampling (reference reset() recursion, e.g. gym_flock_v2.py:85-108)."""
+    E, N, dev = _dims(pos)
+    _check_k(N, k)
+    f32 = torch.float32
+    _need(pos, "pos", f32, (E, N, 2), dev)
+    _need(dnn, "dnn", f32, (E, N, k), dev)
+    _opt(heading, "heading", f32, (E, N), dev)
+    _opt(prev_heading, "prev_heading", f32, (E, N), dev)
+    _opt(vel, "vel", f32, (E, N, 2), dev)
+    _opt(nn_idx, "nn_idx", torch.int64, (E, N, k), dev)
+    _opt(mem, "mem", f32, (E, N, 4, k), dev)
+    _opt(valid, "valid", torch.bool, (E,), dev)
+    _opt(env_mask, "env_mask", torch.bool, (E,), dev)
+    rc = _native.lib().flock_reset(
+        _stream(pos), VARIANT_IDS[variant], E, N, k, float(range_start[0]), float(range_start[1]), float(box),
+        float(sensor_range), float(check_distance), int(bool(rigid_boundary)), int(max_attempts),
+        int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(env_mask), _ptr(pos), _ptr(heading),
+        _ptr(prev_heading), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(mem), _ptr(valid))
+    _native.check(rc, "flock_reset")

@@ -1,0 +1,182 @@
+"""VecFlockEnv: E independent flocking envs of N agents, stepped by one HIP launch per vectorized step.
+
+This is the batched engine under the drop-in ``MultiAgentEnv`` classes (marl_range_flocking_amd/environments).
+All state lives in HBM as [E, N, ...] tensors. ``step()`` never synchronises with the host; the per-env
+``any_done`` flags stay on the device (the reference's ``.item()`` sync, gym_flock_v2.py:315, only happens in the
+single-env wrappers).
+
+Output buffers are double-buffered (ping-pong): the observation returned by step t stays valid through step t+1,
+so a caller can keep ``obs`` and ``next_obs`` side by side as main.py:32-41 does; pass ``copy=True`` to get fresh
+tensors instead.
+"""
+from dataclasses import dataclass, field
+
+import torch
+
+from . import ops
+
+VARIANTS = ("v2", "uw", "uw_discrete", "flock")
+
+
+@dataclass
+class FlockConfig:
+    """Every knob of the four reference envs (constructor args of gym_flock_v2.py:21-32 and siblings)."""
+
+    variant: str = "v2"
+    num_envs: int = 1
+    num_agents: int = 10
+    k: int = 4
+    collision_distance: float = 2.5
+    range_start: tuple = (0, 50)
+    sensor_range: float = 14.0
+    max_linear_velocity: float = 2.5
+    rigid_boundary: bool = False
+    periodic: bool = None          # default: True for v2 (step uses _computePeriodicDistances), else False
+    v_min: float = None            # v2 linear-speed floor: 0.005 (gym_flock_v2.py:331); RNN fork 0.5 (:310)
+    dt: float = 0.1
+    seed: int = 0
+    max_reset_attempts: int = 64
+    track_indices: bool = True     # keep nearest_neighbors (the reference keeps them for v2 only)
+    reset_check_distance: float = None  # uw_discrete resets with collision_distance = 4 (:145)
+    extra: dict = field(default_factory=dict)
+
+    def resolved(self):
+        c = FlockConfig(**{k: getattr(self, k) for k in self.__dataclass_fields__})
+        if c.variant not in VARIANTS:
+            raise ValueError(f"variant must be one of {VARIANTS}")
+        if c.periodic is None:
+            c.periodic = c.variant == "v2"
+        if c.v_min is None:
+            c.v_min = 0.005
+        if c.reset_check_distance is None:
+            c.reset_check_distance = 4.0 if c.variant == "uw_discrete" else c.collision_distance
+        return c
+
+
+class VecFlockEnv:
+    def __init__(self, config: FlockConfig = None, device="cuda", **kw):
+        cfg = (config or FlockConfig(**kw)).resolved()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("VecFlockEnv runs on a HIP device only (no CPU fallback)")
+        E, N, k = cfg.num_envs, cfg.num_agents, cfg.k
+        if k < 1 or k + 1 > N:
+            raise RuntimeError("selected index k out of range")
+        self.E, self.N, self.k = E, N, k
+        self.box = float(cfg.range_start[1])
+        dev, f32 = self.device, torch.float32
+        z = lambda *s, dtype=f32: torch.zeros(s, dtype=dtype, device=dev)  # noqa: E731
+        self.positions = z(E, N, 2)
+        self.velocities = z(E, N, 2)
+        self.headings = z(E, N)
+        self.prev_headings = z(E, N)
+        self.reward = z(E, N)
+        self.done = z(E, N, dtype=torch.bool)
+        self.any_done = z(E, dtype=torch.bool)
+        has_mem = cfg.variant in ("uw", "flock")
+        self._bufs = []
+        for _ in range(2):
+            self._bufs.append(dict(
+                dnn=z(E, N, k),
+                idx=z(E, N, k, dtype=torch.int64) if cfg.track_indices else None,
+                mem=z(E, N, 4, k) if has_mem else None,
+            ))
+        self._cur = 0
+        self.status = z(1, dtype=torch.int32)
+        self.valid = z(E, dtype=torch.bool)
+        self.table = torch.tensor(ops.UWD_TABLE, dtype=f32, device=dev)
+        self._rng_offset = 0
+        self.steps = 0
+
+    # ------------------------------------------------------------------ views
+    @property
+    def dnn(self):
+        return self._bufs[self._cur]["dnn"]
+
+    @property
+    def nn_idx(self):
+        return self._bufs[self._cur]["idx"]
+
+    @property
+    def obs_memory(self):
+        return self._bufs[self._cur]["mem"]
+
+    def observation(self, copy=False):
+        v = self.cfg.variant
+        o = self.obs_memory if v in ("uw", "flock") else self.dnn
+        if v == "v2":
+            return {"critic": o.clone(), "actors": o.clone()} if copy else {"critic": o, "actors": o}
+        return o.clone() if copy else o
+
+    # ------------------------------------------------------------------ reset
+    def reset(self, env_mask=None, copy=False):
+        """Device-side reset (bounded rejection sampling; gym_flock_v2.py:85-108 and siblings)."""
+        c = self.cfg
+        b = self._bufs[self._cur]
+        if env_mask is not None:
+            env_mask = env_mask.to(device=self.device, dtype=torch.bool).contiguous()
+        ops.reset(c.variant, self.positions, b["dnn"], k=self.k, range_start=c.range_start, box=self.box,
+                  sensor_range=c.sensor_range, check_distance=c.reset_check_distance,
+                  heading=self.headings if c.variant != "flock" else None, prev_heading=self.prev_headings,
+                  vel=self.velocities, nn_idx=b["idx"], mem=b["mem"], valid=self.valid, env_mask=env_mask,
+                  rigid_boundary=c.rigid_boundary, max_attempts=c.max_reset_attempts, seed=c.seed,
+                  rng_offset=self._rng_offset)
+        self._rng_offset += c.max_reset_attempts
+        if env_mask is None:
+            self.done.zero_()
+            self.any_done.zero_()
+        else:
+            self.done.masked_fill_(env_mask[:, None], False)
+            self.any_done.masked_fill_(env_mask, False)
+        return self.observation(copy)
+
+    def set_state(self, positions=None, headings=None, prev_headings=None, velocities=None, obs_memory=None):
+        """Inject state (tests, synthetic benchmarks, checkpoint restore)."""
+        for name, val in (("positions", positions), ("headings", headings), ("prev_headings", prev_headings),
+                          ("velocities", velocities)):
+            if val is not None:
+                getattr(self, name).copy_(torch.as_tensor(val).to(self.device).reshape(getattr(self, name).shape))
+        if obs_memory is not None:
+            self._bufs[self._cur]["mem"].copy_(torch.as_tensor(obs_memory).to(self.device))
+
+    # ------------------------------------------------------------------ step
+    def step(self, action, noise=None, dt=None, copy=False):
+        """One vectorized step. action: [E,N,2] f32 (v2: [lin, ang]; uw/flock: velocity/acceleration) or
+        [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info)."""
+        c = self.cfg
+        dt = c.dt if dt is None else float(dt)
+        E, N, k = self.E, self.N, self.k
+        nxt = self._cur ^ 1
+        src, dst = self._bufs[self._cur], self._bufs[nxt]
+        if c.variant == "uw_discrete":
+            a = torch.as_tensor(action, device=self.device)
+            if a.dtype != torch.int64:
+                a = a.to(torch.int64)  # VDN passes float ids (learners/vdn/train_flock.py:99)
+            a = a.reshape(E, N).contiguous()
+        else:
+            a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
+        common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
+                      rigid_boundary=c.rigid_boundary)
+        if c.variant == "v2":
+            ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
+                        self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
+                        v_max=c.max_linear_velocity, periodic=c.periodic, **common)
+        elif c.variant == "uw":
+            ops.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
+                        dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, sensor_range=c.sensor_range,
+                        **common)
+        elif c.variant == "uw_discrete":
+            if noise is not None:
+                noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
+            ops.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
+                                 self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
+                                 self.status, sensor_range=c.sensor_range, v_max=c.max_linear_velocity,
+                                 seed=c.seed, rng_offset=self._rng_offset, **common)
+            self._rng_offset += 1
+        else:
+            ops.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
+                           self.reward, self.done, self.any_done, **common)
+        self._cur = nxt
+        self.steps += 1
+        return self.observation(copy), self.reward, (self.done, self.any_done), {}

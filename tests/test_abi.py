@@ -1,0 +1,77 @@
+"""CPU tests of the C-ABI boundary: libflock_amd.so loads, exports every symbol include/flock_amd.h declares with the
+arity the Python binding uses, and rejects bad arguments before touching the GPU (no compute here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from marl_range_flocking_amd import _native, build
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "flock_amd.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:int|const char\*)\s+(flock_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.M | re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return _native.lib()
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ("flock_step_v2", "flock_step_uw", "flock_step_uw_discrete", "flock_step_flock", "flock_knn",
+                 "flock_reset", "flock_abi_version", "flock_last_error"):
+        assert name in fns, name
+
+
+def test_library_exports_every_declared_symbol_with_binding_arity(lib):
+    for name, nargs in header_functions().items():
+        assert hasattr(lib, name), f"{name} not exported"
+        assert name in _native.SIGNATURES, f"{name} has no Python binding"
+        assert len(_native.SIGNATURES[name]) == nargs, f"{name}: header has {nargs} args"
+
+
+def test_abi_version(lib):
+    assert lib.flock_abi_version() == 1
+
+
+def test_k_out_of_range_rejected_like_torch_topk(lib):
+    # N = 4, k = 4: the reference raises "selected index k out of range" (tests/golden/errors.json)
+    rc = lib.flock_knn(None, 1, 4, 4, 10.0, 7.0, 1, 1, None, None, None)
+    assert rc == -1
+    assert lib.flock_last_error().decode() == "selected index k out of range"
+
+
+def test_limits_and_null_pointers_rejected(lib):
+    assert lib.flock_knn(None, 1, 2048, 4, 10.0, 7.0, 1, 1, None, None, None) == -2
+    assert lib.flock_knn(None, 1, 64, 16, 10.0, 7.0, 1, 1, None, None, None) == -2
+    assert lib.flock_knn(None, 1, 64, 4, 10.0, 7.0, 1, 1, None, None, None) == -3
+    rc = lib.flock_reset(None, 0, 1, 64, 4, 0.0, 50.0, 50.0, 14.0, 2.5, 0, 0, 0, 0, *([None] * 9))
+    assert rc == -3
+    x = ctypes.c_float(0)
+    rc = lib.flock_reset(None, 9, 1, 64, 4, 0.0, 50.0, 50.0, 14.0, 2.5, 0, 4, 0, 0, None, ctypes.byref(x), None,
+                         None, None, ctypes.byref(x), None, None, None)
+    assert rc == -5
+
+
+def test_empty_batch_is_a_noop(lib):
+    assert lib.flock_knn(None, 0, 64, 4, 10.0, 7.0, 1, 1, None, None, None) == 0
+
+
+def test_ops_refuse_cpu_tensors():
+    import torch
+
+    from marl_range_flocking_amd import ops
+
+    with pytest.raises(RuntimeError, match="HIP device"):
+        ops.knn(torch.zeros(1, 8, 2), 4, 10.0)

@@ -1,0 +1,288 @@
+"""GPU parity of the HIP env stepper (libflock_amd.so) against the oracle and the reference's golden vectors.
+
+Bars (north_star): neighbour indices bit-exact; float32 state within rtol 1e-5.
+  * kNN stage: bit-exact against the oracle on the same positions (dnn and indices, every row), incl. ties,
+    duplicates, seams, k in 1..15 and N up to 1024;
+  * full steps: float state within rtol 1e-5 of the oracle and of the reference fixtures (teacher-forced),
+    indices bit-exact against the oracle run on the GPU's own post-step positions, tie-aware vs the reference;
+  * full-size (config 3: 4096 envs x 256 agents): size-independent properties + bit-exact kNN on sampled envs.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from marl_range_flocking_amd import FlockConfig, VecFlockEnv, ops
+from oracle import oracle as O
+from parity import allclose_rel, d2_rows, knn_mismatch, meta
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+VARIANT = {"v2": "v2", "v2fork": "v2", "uw": "uw", "uwd": "uw_discrete", "flock": "flock"}
+
+
+def _env(m, E, device):
+    v = m["variant"]
+    return VecFlockEnv(FlockConfig(variant=VARIANT[v], num_envs=E, num_agents=m["N"], k=m["k"],
+                                   collision_distance=m["collision_distance"], range_start=(0, m["box"]),
+                                   sensor_range=m.get("sensor_range", 14.0), periodic=(v == "v2"),
+                                   v_min=m.get("v_min", 0.005)), device=device)
+
+
+def _knn_exact(pos, k, box, sr, periodic, clamp, gdnn, gidx):
+    dnn, idx = O.knn(pos, k, box, sr, periodic=periodic, clamp=clamp)
+    np.testing.assert_array_equal(gidx, idx)
+    np.testing.assert_array_equal(gdnn, dnn)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "env_*.npz"))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_step_matches_reference_and_oracle(path, cuda):
+    z = np.load(path)
+    m = meta(z)
+    v, E, k = m["variant"], m["E"], m["k"]
+    env = _env(m, E, cuda)
+    periodic = v == "v2"
+    for t in range(m["T"]):
+        # teacher forcing from the reference's state at t-1
+        if t == 0:
+            st = dict(positions=z["pos0"], headings=z["head0"], prev_headings=z["prevh0"], velocities=z["vel0"])
+            mem = z["mem0"]
+        else:
+            st = dict(positions=z["pos"][t - 1], headings=z["head"][t - 1], prev_headings=z["prevh"][t - 1],
+                      velocities=z["vel"][t - 1])
+            mem = z["obs"][t - 1] if v in ("uw", "flock") else None
+        env.set_state(**st, obs_memory=mem if v in ("uw", "flock") else None)
+        act = torch.from_numpy(np.ascontiguousarray(z["actions"][t]))
+        noise = torch.from_numpy(np.ascontiguousarray(z["noise"][t])) if v == "uwd" else None
+        obs, rew, (done, any_done), _ = env.step(act, noise=noise)
+        torch.cuda.synchronize()
+        gpos = env.positions.cpu().numpy()
+        for name, got, want in (("pos", gpos, z["pos"][t]), ("vel", env.velocities.cpu().numpy(), z["vel"][t]),
+                                ("dnn", env.dnn.cpu().numpy(), z["dnn"][t])):
+            ok, err = allclose_rel(got, want, atol=1e-12)
+            assert ok, f"t={t} {name} vs reference: rel err {err}"
+        if v != "flock":
+            ok, err = allclose_rel(env.headings.cpu().numpy(), z["head"][t])
+            assert ok, f"t={t} heading rel err {err}"
+        np.testing.assert_array_equal(rew.cpu().numpy(), z["reward"][t])
+        np.testing.assert_array_equal(done.cpu().numpy(), z["done"][t])
+        np.testing.assert_array_equal(any_done.cpu().numpy(), z["any_done"][t])
+        if v in ("uw", "uwd"):
+            np.testing.assert_array_equal(env.prev_headings.cpu().numpy(), z["prevh"][t])
+        if v in ("uw", "flock"):
+            ok, err = allclose_rel(obs.cpu().numpy(), z["obs"][t], atol=1e-12)
+            assert ok, f"obs memory {err}"
+        gidx = env.nn_idx.cpu().numpy()
+        if v in ("v2", "v2fork"):
+            _, _, bad = knn_mismatch(z["nn_idx"][t], gidx, d2_rows(z["pos"][t], m["box"], periodic))
+            assert not bad, f"t={t} indices vs reference beyond ties: {bad[:4]}"
+        # bit-exact kNN against the oracle on the GPU's own positions
+        _knn_exact(gpos, k, m["box"], m.get("sensor_range", 14.0), periodic, v != "flock", env.dnn.cpu().numpy(),
+                   gidx)
+
+
+@pytest.mark.parametrize("N,k", [(2, 1), (5, 4), (8, 4), (64, 4), (100, 7), (256, 4), (257, 3), (512, 4),
+                                 (1000, 9), (1024, 4), (300, 15), (64, 11)])
+@pytest.mark.parametrize("periodic", [True, False], ids=["periodic", "euclid"])
+def test_knn_bit_exact_vs_oracle(N, k, periodic, cuda):
+    rng = np.random.default_rng(N * 31 + k)
+    E = max(2, 4096 // N)
+    box = float(round(np.sqrt(250 * N)))
+    pos = rng.uniform(0, box, (E, N, 2)).astype(np.float32)
+    pos[0, : N // 4] = pos[0, 0]  # exact duplicates (d2 = 0 ties, self among them)
+    if N >= 8:
+        pos[1, :3] = [[box - 1e-4, 1.0], [1e-4, 1.0], [box * 0.5, box - 1e-6]]  # seams
+    g = torch.from_numpy(pos).to(cuda)
+    dnn, idx = ops.knn(g, k, box, 14.0, periodic=periodic)
+    torch.cuda.synchronize()
+    _knn_exact(pos, k, box, 14.0, periodic, True, dnn.cpu().numpy(), idx.cpu().numpy())
+
+
+def test_knn_lattice_ties_bit_exact(cuda):
+    z = np.load(os.path.join(GOLD, "sense_N64_k4_lattice.npz"))
+    m = meta(z)
+    for periodic in (True, False):
+        dnn, idx = ops.knn(torch.from_numpy(z["pos"]).to(cuda), m["k"], m["box"], m["sensor_range"], periodic)
+        torch.cuda.synchronize()
+        _knn_exact(z["pos"], m["k"], m["box"], m["sensor_range"], periodic, True, dnn.cpu().numpy(),
+                   idx.cpu().numpy())
+        tag = "per" if periodic else "euc"
+        _, ties, bad = knn_mismatch(z[f"{tag}_idx"], idx.cpu().numpy(), z[f"{tag}_D"])
+        assert not bad
+
+
+def test_knn_bucket_collisions_take_exact_path(cuda):
+    """d2 values that share a truncated-key bucket force the exact rescan; results stay bit-exact."""
+    N, k, box = 256, 4, 253.0
+    rng = np.random.default_rng(7)
+    pos = rng.uniform(0, box, (64, N, 2)).astype(np.float32)
+    # neighbours at distances differing in the last mantissa bits
+    base = pos[:, :1, :].copy()
+    for s in range(1, 9):
+        off = np.float32(3.0) + np.float32(s) * np.float32(1e-6)
+        pos[:, s, 0] = base[:, 0, 0] + off
+        pos[:, s, 1] = base[:, 0, 1]
+    pos = np.clip(pos, 0.01, box - 0.01).astype(np.float32)
+    dnn, idx = ops.knn(torch.from_numpy(pos).to(cuda), k, box, 14.0, periodic=True)
+    torch.cuda.synchronize()
+    _knn_exact(pos, k, box, 14.0, True, True, dnn.cpu().numpy(), idx.cpu().numpy())
+
+
+@pytest.mark.parametrize("variant", ["v2", "uw", "uw_discrete", "flock"])
+def test_step_vs_oracle_mid_size(variant, cuda):
+    E, N, k = 128, 256, 4
+    box = 253.0
+    rng = np.random.default_rng(11)
+    pos = rng.uniform(0, box, (E, N, 2)).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    prev = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    vel = rng.standard_normal((E, N, 2)).astype(np.float32)
+    vel /= np.linalg.norm(vel, axis=-1, keepdims=True)
+    mem = rng.uniform(0, 14, (E, N, 4, k)).astype(np.float32)
+    env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                  range_start=(0, box), sensor_range=14.0), device=cuda)
+    env.set_state(positions=pos, headings=head, prev_headings=prev, velocities=vel,
+                  obs_memory=mem if variant in ("uw", "flock") else None)
+    if variant == "uw_discrete":
+        act = rng.integers(0, 10, (E, N)).astype(np.int64)
+        noise = (0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)
+        ref = O.step_uwd(pos, head, prev, act, noise, k=k, box=box, cd=2.5)
+        obs, rew, (done, anyd), _ = env.step(torch.from_numpy(act), noise=torch.from_numpy(noise))
+    else:
+        act = rng.uniform(-1.5, 2.5, (E, N, 2)).astype(np.float32)
+        if variant == "v2":
+            ref = O.step_v2(pos, head, act, k=k, box=box, cd=2.5)
+        elif variant == "uw":
+            ref = O.step_uw(pos, head, prev, act, mem, k=k, box=box, cd=2.5)
+        else:
+            ref = O.step_flock(pos, vel, act, mem, k=k, box=box, cd=2.5)
+        obs, rew, (done, anyd), _ = env.step(torch.from_numpy(act))
+    torch.cuda.synchronize()
+    gpos = env.positions.cpu().numpy()
+    ok, err = allclose_rel(gpos, ref["pos"])
+    assert ok, err
+    ok, err = allclose_rel(env.velocities.cpu().numpy(), ref["vel"], atol=1e-12)
+    assert ok, err
+    if variant in ("v2", "uw_discrete"):
+        ok, err = allclose_rel(env.headings.cpu().numpy(), ref["heading"])
+        assert ok, err
+    # kNN bit-exact on GPU positions
+    _knn_exact(gpos, k, box, 14.0, variant == "v2", variant != "flock", env.dnn.cpu().numpy(),
+               env.nn_idx.cpu().numpy())
+    # where positions are bitwise equal, everything downstream is bitwise equal
+    same = (gpos == ref["pos"]).all(axis=(1, 2))
+    if variant in ("uw", "flock"):  # no transcendentals on the path: bitwise-equal state everywhere
+        assert same.all()
+    for e in np.nonzero(same)[0][:16]:
+        np.testing.assert_array_equal(env.nn_idx.cpu().numpy()[e], ref["idx"][e])
+        np.testing.assert_array_equal(rew.cpu().numpy()[e], ref["reward"][e])
+        np.testing.assert_array_equal(done.cpu().numpy()[e], ref["done"][e].astype(bool))
+    # done/any_done consistent with the GPU's own distances
+    gd = env.dnn.cpu().numpy()
+    np.testing.assert_array_equal(done.cpu().numpy(), (gd < 2.5).any(-1))
+    np.testing.assert_array_equal(anyd.cpu().numpy(), done.cpu().numpy().any(-1))
+
+
+def test_config3_full_size_properties(cuda):
+    """BASELINE config 3 size (4096 envs x 256 agents, v2 periodic): properties over every row + bit-exact kNN on
+    a sample of envs, after 3 chained steps."""
+    E, N, k, box = 4096, 256, 4, 253.0
+    env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                  range_start=(0, box), sensor_range=14.0), device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(0)
+    env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
+    env.headings.copy_(torch.rand(E, N, device=cuda, generator=g) * 1.5 * np.pi)
+    for _ in range(3):
+        act = torch.stack([torch.rand(E, N, device=cuda, generator=g),
+                           torch.rand(E, N, device=cuda, generator=g) * 3 - 1.5], -1)
+        obs, rew, (done, anyd), _ = env.step(act)
+    torch.cuda.synchronize()
+    d = obs["actors"]
+    idx = env.nn_idx
+    assert bool((d[..., 1:] >= d[..., :-1]).all()), "distances sorted per row"
+    assert bool((d >= 0).all()) and bool((d <= 14.0).all())
+    assert bool((idx >= 0).all()) and bool((idx < N).all())
+    self_ids = torch.arange(N, device=cuda)[None, :, None]
+    assert int((idx == self_ids).sum()) == 0, "self never a neighbour without exact duplicates"
+    sidx, _ = idx.sort(-1)
+    assert bool((sidx[..., 1:] != sidx[..., :-1]).all()), "neighbours distinct"
+    assert torch.equal(done, (d < 2.5).any(-1))
+    assert torch.equal(anyd, done.any(-1))
+    assert torch.equal(rew, torch.where(done, torch.tensor(-5.0, device=cuda), torch.tensor(0.01, device=cuda)))
+    pos = env.positions
+    assert bool(((pos > 0) & (pos <= box)).all())
+    sample = torch.arange(0, E, 97, device=cuda)
+    _knn_exact(pos[sample].cpu().numpy(), k, box, 14.0, True, True, d[sample].cpu().numpy(),
+               idx[sample].cpu().numpy())
+
+
+@pytest.mark.parametrize("variant", ["v2", "uw", "uw_discrete", "flock"])
+def test_reset_properties(variant, cuda):
+    E, N, k = 64, 10, 4
+    cfg = FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5, range_start=(0, 50),
+                      sensor_range=14.0, seed=3)
+    env = VecFlockEnv(cfg, device=cuda)
+    obs = env.reset()
+    torch.cuda.synchronize()
+    pos = env.positions.cpu().numpy()
+    hi = 25.0 if variant == "uw" else 50.0
+    assert (pos > 0).all() and (pos <= hi).all()
+    assert env.valid.all(), "10 agents in 50x50 reset within the attempt budget"
+    chk = 4.0 if variant == "uw_discrete" else 2.5
+    dnn, _ = O.knn(pos, k, 50.0, 14.0, periodic=False, clamp=variant != "flock")
+    assert (dnn >= chk).all(), "no collision at reset (Euclidean, gym_flock_v2.py:100-108)"
+    np.testing.assert_array_equal(env.dnn.cpu().numpy(), dnn)
+    if variant in ("uw", "flock"):
+        mem = env.obs_memory.cpu().numpy()
+        np.testing.assert_array_equal(mem[:, :, 0], dnn)
+        assert (mem[:, :, 1:] == 0).all()
+    if variant != "flock":
+        h = env.headings.cpu().numpy()
+        top = {"v2": 1.5 * np.pi, "uw": 2 * np.pi, "uw_discrete": np.pi / 1.2}[variant]
+        assert (h > 0).all() and (h <= top + 1e-6).all()
+    # determinism: same seed → same reset
+    env2 = VecFlockEnv(cfg, device=cuda)
+    env2.reset()
+    assert torch.equal(env.positions, env2.positions)
+    # masked reset leaves other envs alone
+    before = env.positions.clone()
+    mask = torch.zeros(E, dtype=torch.bool, device=cuda)
+    mask[::2] = True
+    env.reset(env_mask=mask)
+    assert torch.equal(env.positions[1::2], before[1::2])
+    assert not torch.equal(env.positions[::2], before[::2])
+
+
+def test_uw_discrete_in_kernel_noise(cuda):
+    """noise=None draws N(0, 0.1) in-kernel: with mean angular 0 (action 2) the clamp to ±0.025 saturates with
+    probability P(|z| > 0.25) = 0.8026 (gym_flock_uw_discrete.py:333-345)."""
+    E, N = 512, 256
+    env = VecFlockEnv(FlockConfig(variant="uw_discrete", num_envs=E, num_agents=N, k=4, collision_distance=3.0,
+                                  range_start=(0, 358)), device=cuda)
+    env.positions.uniform_(1, 357)
+    h0 = env.headings.clone()
+    env.step(torch.full((E, N), 2, dtype=torch.int64, device=cuda))
+    dh = (env.headings - h0).cpu().numpy().ravel()
+    assert np.abs(dh).max() <= 0.0025 + 1e-6
+    sat = np.mean(np.abs(np.abs(dh) - 0.0025) < 1e-6)
+    assert abs(sat - 0.8026) < 0.01, sat
+    assert abs(np.mean(np.sign(dh))) < 0.01
+    h1 = env.headings.clone()
+    env.step(torch.full((E, N), 2, dtype=torch.int64, device=cuda))
+    assert not torch.equal(env.headings - h1, h1 - h0), "fresh draws every step"
+
+
+def test_uw_discrete_bad_action_flags_status(cuda):
+    env = VecFlockEnv(FlockConfig(variant="uw_discrete", num_envs=2, num_agents=8, k=4, range_start=(0, 50)),
+                      device=cuda)
+    env.positions.uniform_(1, 49)
+    env.step(torch.full((2, 8), 12, dtype=torch.int64))
+    assert env.status.item() & 1
+
+
+def test_k_out_of_range_raises(cuda):
+    with pytest.raises(RuntimeError, match="selected index k out of range"):
+        ops.knn(torch.zeros(1, 4, 2, device=cuda), 4, 10.0)
