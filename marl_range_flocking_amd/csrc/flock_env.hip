@@ -18,7 +18,7 @@
 //   phase 5  distances (correctly-rounded sqrt of the k winners only), clamp, collisions, done, per-env any_done
 //            (LDS atomic OR), reward, observation memory roll.
 //
-// Float arithmetic: every op is rounded separately (__fmul_rn / __fadd_rn / __fdiv_rn / __fsqrt_rn, and the file
+// Float arithmetic: every op is rounded separately (__fmul_rn / __fadd_rn / __fdiv_rn / sqrt_rn, and the file
 // is built with -ffp-contract=off), in the reference's op order; cosf/sinf are ocml's.
 #include <hip/hip_runtime.h>
 
@@ -27,6 +27,8 @@
 #include <string.h>
 
 #include "flock_amd.h"
+
+#pragma clang fp contract(off)
 
 namespace {
 
@@ -73,6 +75,10 @@ struct Params {
 
 // ---------------------------------------------------------------------------------------------------------------
 // small helpers
+
+// Correctly-rounded sqrt. NOTE: HIP's __fsqrt_rn is ocml's *native* (1-ulp) sqrt unless OCML_BASIC_ROUNDED_OPERATIONS
+// is defined; __builtin_sqrtf lowers to v_sqrt_f32 + the two-FMA correction (IEEE round-to-nearest), like torch.sqrt.
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 
 __device__ __forceinline__ float clamp_t(float x, float lo, float hi) {  // torch.clamp: NaN propagates
     x = (x < lo) ? lo : x;
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
         } else if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:269-302 (heading=False)
             const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
-            const float n = __fsqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
+            const float n = sqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
             float vx = __fmul_rn(nan_to_num(__fdiv_rn(ac.x, n)), p.dt);     // :294-301
             float vy = __fmul_rn(nan_to_num(__fdiv_rn(ac.y, n)), p.dt);
             x = __fadd_rn(x, vx);                                            // :302
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             lin = clamp_t(lin, 5e-6f, p.v_max);                                   // :347
             float vx = __fmul_rn(lin, cosf(h));                                   // :351
             float vy = __fmul_rn(lin, sinf(h));                                   // :352
-            const float n = __fsqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :358
+            const float n = sqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :358
             vx = __fmul_rn(nan_to_num(__fdiv_rn(vx, n)), p.dt);                  // :358-365
             vy = __fmul_rn(nan_to_num(__fdiv_rn(vy, n)), p.dt);
             x = __fadd_rn(x, vx);                                                 // :366
@@ -323,7 +329,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             const float2 v0 = reinterpret_cast<const float2*>(p.vel)[a];
             float vx = __fadd_rn(v0.x, __fmul_rn(ac.x, p.dt));                   // :196
             float vy = __fadd_rn(v0.y, __fmul_rn(ac.y, p.dt));
-            const float n = __fsqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :198
+            const float n = sqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :198
             vx = __fdiv_rn(vx, n);
             vy = __fdiv_rn(vy, n);
             x = __fadd_rn(x, __fmul_rn(vx, p.dt));                               // :200
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
 #pragma unroll
         for (int s = 1; s < L - 1; ++s) {
             if (s <= p.k) {
-                float d = __fsqrt_rn(bd[s]);
+                float d = sqrt_rn(bd[s]);
                 if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);  // gym_flock_v2.py:151
                 dv[s - 1] = d;
                 coll |= (d < p.cd);                                   // :212-215
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             float r;
             if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:206-221
                 const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
-                const float dist = __fsqrt_rn(__fadd_rn(__fmul_rn(com_x, com_x), __fmul_rn(com_y, com_y)));
+                const float dist = sqrt_rn(__fadd_rn(__fmul_rn(com_x, com_x), __fmul_rn(com_y, com_y)));
                 const float com = (dist < p.com_r) ? 0.01f : 0.0f;                  // :197
                 const float prev = p.prev_heading[a];
                 const float angp = (fabsf(__fsub_rn(prev, h)) > 0.27f) ? -0.01f : 0.001f;  // :202-204
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
 #pragma unroll
             for (int s = 1; s < L - 1; ++s)
                 if (s <= p.k) {
-                    float d = __fsqrt_rn(bd[s]);
+                    float d = sqrt_rn(bd[s]);
                     if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);
                     coll |= (d < p.check_distance);
                 }
@@ -495,7 +501,7 @@ __global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
 #pragma unroll
         for (int s = 1; s < L - 1; ++s) {
             if (s <= p.k) {
-                float d = __fsqrt_rn(bd[s]);
+                float d = sqrt_rn(bd[s]);
                 if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);
                 p.dnn[a * p.k + (s - 1)] = d;
                 if (p.idx) p.idx[a * p.k + (s - 1)] = (int64_t)bj[s];
