@@ -135,9 +135,10 @@ def main():
         learner = SharedCriticBench(env, device=dev, seed=1234 + rank)
 
     def one_step(s):
-        env.step(pool[s % len(pool)])
+        a = pool[s % len(pool)]
+        env.step(a)
         if learner is not None:
-            learner.after_env_step(s)
+            learner.after_env_step(s, a)
 
     for s in range(args.warmup):
         one_step(s)
@@ -149,11 +150,12 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
+        a = pool[s % len(pool)]
         ev[s][0].record(stream)
-        env.step(pool[s % len(pool)])
+        env.step(a)
         ev[s][1].record(stream)
         if learner is not None:
-            learner.after_env_step(s)
+            learner.after_env_step(s, a)
     torch.cuda.synchronize(dev)
     barrier(world)
     el = time.perf_counter() - t0

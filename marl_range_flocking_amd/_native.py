@@ -27,8 +27,18 @@ SIGNATURES = {
     "flock_knn": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int] + [_c_void_p] * 3,
     "flock_reset": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_float,
                     _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9,
+    # learner kernels (include/flock_learn.h)
+    "flock_learn_last_error": [],
+    "flock_adam_step": [_c_void_p, ctypes.c_int64] + [_c_void_p] * 5 + [_c_float] * 4 + [ctypes.c_int64, _c_void_p,
+                                                                                      _c_float, _c_int],
+    "flock_soft_update": [_c_void_p, ctypes.c_int64, _c_void_p, _c_void_p, _c_float, _c_int],
+    "flock_grad_norm": [_c_void_p, ctypes.c_int64, _c_void_p, _c_void_p, _c_int, _c_float, _c_void_p],
+    "flock_gru_fwd": [_c_void_p, ctypes.c_int64, _c_int] + [_c_void_p] * 5,
+    "flock_gru_bwd": [_c_void_p, ctypes.c_int64, _c_int] + [_c_void_p] * 6,
+    "flock_gather_rows": [_c_void_p, ctypes.c_int64, ctypes.c_int64, _c_void_p, _c_void_p, _c_void_p],
+    "flock_scatter_rows": [_c_void_p, ctypes.c_int64, ctypes.c_int64, _c_void_p, _c_void_p, _c_void_p],
 }
-RESTYPES = {"flock_last_error": ctypes.c_char_p}
+RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p}
 
 _lib = None
 
@@ -54,7 +64,7 @@ def lib():
     return _lib
 
 
-def check(rc: int, what: str):
+def check(rc: int, what: str, learn: bool = False):
     if rc != 0:
-        msg = lib().flock_last_error().decode()
+        msg = (lib().flock_learn_last_error() if learn else lib().flock_last_error()).decode()
         raise RuntimeError(f"{what}: {msg} (code {rc})")

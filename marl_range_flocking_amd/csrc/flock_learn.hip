@@ -1,0 +1,280 @@
+// flock_learn.hip — learner-side HIP kernels (gfx950): fused Adam + soft target update over flat parameter
+// buffers, global grad L2 norm (clip_grad_norm_ without a host sync), fused GRU-cell forward/backward (the
+// elementwise part of nn.GRUCell; the gate GEMMs run as batched rocBLAS/hipBLASLt GEMMs), and row gather/scatter
+// for the device-resident replay rings. C ABI: include/flock_learn.h.
+//
+// Every learner keeps its parameters, gradients and Adam moments of ALL agents in one flat f32 buffer each, so one
+// launch updates every parameter of every agent (the reference runs one torch.optim.Adam per agent network).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "flock_learn.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+thread_local char g_err[256] = "";
+int fail(int code, const char* msg) {
+    snprintf(g_err, sizeof(g_err), "%s", msg);
+    return code;
+}
+int launched() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : fail(-4, hipGetErrorString(e));
+}
+
+constexpr int kBlock = 256;
+
+int grid_for(int64_t n, int per_thread = 4) {
+    int64_t g = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;  // grid-stride beyond (memory-bound: 256 CUs x 8 blocks)
+    return (int)g;
+}
+
+__device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+
+// torch.optim.Adam, single-tensor path (torch/optim/adam.py _single_tensor_adam), per element:
+//   m = m.lerp(g, 1 - b1)                 lerp: w < 0.5 ? m + w * (g - m) : g - (g - m) * (1 - w)
+//   v = v * b2 + (1 - b2) * g * g         mul_(b2).addcmul_(g, g, value=1 - b2)
+//   p = p + (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)     addcdiv_
+// then optionally the target network soft update (mode 0: t*(1-tau) + p*tau, maddpg nets net.py:305-309;
+// mode 1: tau*p + (1-tau)*t, shared critic agent_simple_shared_critic.py:172-185).
+__global__ __launch_bounds__(kBlock) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ m, float* __restrict__ v,
+                                                      const float* __restrict__ grad_scale, float w1, float b2,
+                                                      float one_minus_b2, float neg_step_size, float bc2_sqrt,
+                                                      float eps, float* __restrict__ target, float tau,
+                                                      float one_minus_tau, int target_mode) {
+    const float gs = grad_scale ? *grad_scale : 1.0f;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        float gi = g[i];
+        if (grad_scale) gi = gi * gs;
+        float mi = m[i];
+        mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
+        float vi = v[i] * b2;
+        vi = vi + (one_minus_b2 * gi) * gi;
+        const float denom = sqrt_rn(vi) / bc2_sqrt + eps;
+        float pi = p[i] + (neg_step_size * mi) / denom;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi;
+        if (target) {
+            const float t = target[i];
+            target[i] = target_mode == 0 ? t * one_minus_tau + pi * tau : tau * pi + one_minus_tau * t;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void soft_update_kernel(int64_t n, float* __restrict__ target,
+                                                             const float* __restrict__ src, float tau,
+                                                             float one_minus_tau, int mode) {
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const float t = target[i], s = src[i];
+        target[i] = mode == 0 ? t * one_minus_tau + s * tau : tau * s + one_minus_tau * t;
+    }
+}
+
+// sum of squares: pass 1 per-block partials (f64 accumulation), pass 2 one block folds them and writes
+// out[0] = ||g||_2 and out[1] = min(max_norm / (||g|| + 1e-6), 1) (torch.nn.utils.clip_grad_norm_).
+__global__ __launch_bounds__(kBlock) void sq_partial_kernel(int64_t n, const float* __restrict__ g,
+                                                            double* __restrict__ partial) {
+    __shared__ double red[kBlock];
+    double acc = 0.0;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const double x = g[i];
+        acc += x * x;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(kBlock) void sq_final_kernel(int nparts, const double* __restrict__ partial,
+                                                          float max_norm, float* __restrict__ out) {
+    __shared__ double red[kBlock];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += kBlock) acc += partial[i];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float norm = (float)sqrt(red[0]);
+        out[0] = norm;
+        const float coef = max_norm / (norm + 1e-6f);
+        out[1] = coef < 1.0f ? coef : 1.0f;
+    }
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// nn.GRUCell elementwise part (ATen gru_cell, RNN.cpp): rows of gi = x W_ih^T + b_ih and gh = h W_hh^T + b_hh
+// (gate order r, z, n), h' = (h - n) * z + n. ws keeps (r, z, n, gh_n) for the backward.
+__global__ __launch_bounds__(kBlock) void gru_fwd_kernel(int64_t rows, int H, const float* __restrict__ gi,
+                                                         const float* __restrict__ gh, const float* __restrict__ h,
+                                                         float* __restrict__ hout, float* __restrict__ ws) {
+    const int64_t n = rows * H;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+        const int64_t row = e / H;
+        const int c = (int)(e - row * H);
+        const float* a = gi + row * 3 * H;
+        const float* b = gh + row * 3 * H;
+        const float r = sigmoidf_(b[c] + a[c]);
+        const float z = sigmoidf_(b[H + c] + a[H + c]);
+        const float ghn = b[2 * H + c];
+        const float nn = tanhf(a[2 * H + c] + ghn * r);
+        const float hv = h[e];
+        hout[e] = (hv - nn) * z + nn;
+        if (ws) {
+            float* w = ws + row * 4 * H;
+            w[c] = r;
+            w[H + c] = z;
+            w[2 * H + c] = nn;
+            w[3 * H + c] = ghn;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void gru_bwd_kernel(int64_t rows, int H, const float* __restrict__ dhout,
+                                                         const float* __restrict__ h, const float* __restrict__ ws,
+                                                         float* __restrict__ dgi, float* __restrict__ dgh,
+                                                         float* __restrict__ dh) {
+    const int64_t n = rows * H;
+    for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+        const int64_t row = e / H;
+        const int c = (int)(e - row * H);
+        const float* w = ws + row * 4 * H;
+        const float r = w[c], z = w[H + c], nn = w[2 * H + c], ghn = w[3 * H + c];
+        const float go = dhout[e];
+        const float hv = h[e];
+        const float dn = go * (1.0f - z);
+        const float dz = go * (hv - nn);
+        const float dan = dn * (1.0f - nn * nn);
+        const float dr = dan * ghn;
+        const float dar = dr * (r * (1.0f - r));
+        const float daz = dz * (z * (1.0f - z));
+        float* gi_ = dgi + row * 3 * H;
+        float* gh_ = dgh + row * 3 * H;
+        gi_[c] = dar;
+        gi_[H + c] = daz;
+        gi_[2 * H + c] = dan;
+        gh_[c] = dar;
+        gh_[H + c] = daz;
+        gh_[2 * H + c] = dan * r;
+        dh[e] = go * z;
+    }
+}
+
+// dst[r, :] = src[idx[r], :]  (replay minibatch / chunk gather); one wave per row, 16-B vectors when aligned
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(int64_t rows, int64_t width, const float* __restrict__ src,
+                                                             const int64_t* __restrict__ idx, float* __restrict__ dst,
+                                                             int scatter) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)kBlock + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+    const bool vec = (width & 3) == 0;
+    for (int64_t r = wave; r < rows; r += nwaves) {
+        const int64_t ir = idx[r];
+        const float* s = scatter ? src + r * width : src + ir * width;
+        float* d = scatter ? dst + ir * width : dst + r * width;
+        if (vec) {
+            const float4* s4 = reinterpret_cast<const float4*>(s);
+            float4* d4 = reinterpret_cast<float4*>(d);
+            for (int64_t c = lane; c < width / 4; c += 64) d4[c] = s4[c];
+        } else {
+            for (int64_t c = lane; c < width; c += 64) d[c] = s[c];
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* flock_learn_last_error(void) { return g_err; }
+
+int flock_adam_step(void* stream, int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                    const float* grad_scale, float lr, float beta1, float beta2, float eps, int64_t step,
+                    float* target, float tau, int target_mode) {
+    if (n <= 0) return 0;
+    if (!param || !grad || !exp_avg || !exp_avg_sq) return fail(-3, "flock_adam_step: NULL pointer");
+    if (step < 1) return fail(-5, "flock_adam_step: step must be >= 1");
+    // bias corrections in double then rounded, like the python-float math of _single_tensor_adam
+    const double bc1 = 1.0 - pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - pow((double)beta2, (double)step);
+    const float neg_step = (float)(-(double)lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, param, grad, exp_avg,
+                       exp_avg_sq, grad_scale, (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2),
+                       neg_step, bc2s, eps, target, tau, (float)(1.0 - (double)tau), target_mode);
+    return launched();
+}
+
+int flock_soft_update(void* stream, int64_t n, float* target, const float* src, float tau, int mode) {
+    if (n <= 0) return 0;
+    if (!target || !src) return fail(-3, "flock_soft_update: NULL pointer");
+    hipLaunchKernelGGL(soft_update_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, target, src,
+                       tau, (float)(1.0 - (double)tau), mode);
+    return launched();
+}
+
+int flock_grad_norm(void* stream, int64_t n, const float* grad, double* partial, int max_parts, float max_norm,
+                    float* out) {
+    if (!grad || !partial || !out) return fail(-3, "flock_grad_norm: NULL pointer");
+    int parts = grid_for(n);
+    if (parts > max_parts) parts = max_parts;
+    hipLaunchKernelGGL(sq_partial_kernel, dim3(parts), dim3(kBlock), 0, (hipStream_t)stream, n, grad, partial);
+    hipLaunchKernelGGL(sq_final_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, parts, partial, max_norm, out);
+    return launched();
+}
+
+int flock_gru_fwd(void* stream, int64_t rows, int H, const float* gi, const float* gh, const float* h, float* hout,
+                  float* ws) {
+    if (rows <= 0) return 0;
+    if (!gi || !gh || !h || !hout) return fail(-3, "flock_gru_fwd: NULL pointer");
+    hipLaunchKernelGGL(gru_fwd_kernel, dim3(grid_for(rows * H)), dim3(kBlock), 0, (hipStream_t)stream, rows, H, gi,
+                       gh, h, hout, ws);
+    return launched();
+}
+
+int flock_gru_bwd(void* stream, int64_t rows, int H, const float* dhout, const float* h, const float* ws, float* dgi,
+                  float* dgh, float* dh) {
+    if (rows <= 0) return 0;
+    if (!dhout || !h || !ws || !dgi || !dgh || !dh) return fail(-3, "flock_gru_bwd: NULL pointer");
+    hipLaunchKernelGGL(gru_bwd_kernel, dim3(grid_for(rows * H)), dim3(kBlock), 0, (hipStream_t)stream, rows, H, dhout,
+                       h, ws, dgi, dgh, dh);
+    return launched();
+}
+
+int flock_gather_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst) {
+    if (rows <= 0) return 0;
+    if (!src || !idx || !dst) return fail(-3, "flock_gather_rows: NULL pointer");
+    int blocks = (int)((rows * 64 + kBlock - 1) / kBlock);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, rows, width, src, idx,
+                       dst, 0);
+    return launched();
+}
+
+int flock_scatter_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst) {
+    if (rows <= 0) return 0;
+    if (!src || !idx || !dst) return fail(-3, "flock_scatter_rows: NULL pointer");
+    int blocks = (int)((rows * 64 + kBlock - 1) / kBlock);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(gather_rows_kernel, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, rows, width, src, idx,
+                       dst, 1);
+    return launched();
+}
+
+}  // extern "C"

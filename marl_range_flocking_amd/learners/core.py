@@ -1,0 +1,273 @@
+"""Batched-over-agents learner building blocks on MI355X.
+
+* ``FlatParams``: every parameter of every agent copy of one network lives in ONE flat f32 buffer (with flat grad,
+  Adam moment and optional target buffers), exposed as per-layer stacked leaf tensors [A, out, in] that alias it.
+  One ``flock_adam_step`` launch then updates all agents (the reference steps one torch.optim.Adam per agent).
+* ``blinear`` / ``blayer_norm``: per-agent Linear / LayerNorm over a leading agent axis; the GEMMs are batched
+  rocBLAS/hipBLASLt GEMMs (torch.bmm / baddbmm), f32 in and out (gfx950 has no xf32/TF32 path to fall into).
+* ``gru_cell``: nn.GRUCell with the gate GEMMs batched and the elementwise part in flock_gru_fwd/bwd.
+* ``ReplayRing``: device-resident ring of named row tensors with HIP row scatter (insert) / gather (sample).
+"""
+import ctypes
+import math
+from collections import OrderedDict
+
+import warnings
+
+import torch
+
+from .. import _native
+
+# agent-major stacked views are strided; their grads alias the same strides on purpose
+warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _require_cuda(t):
+    if t.device.type != "cuda":
+        raise RuntimeError("learner kernels run on a HIP device only (no CPU fallback)")
+
+
+class FlatParams:
+    """Stacked parameters of ``agents`` copies of one network, aliasing ONE flat f32 buffer.
+
+    shapes: name -> per-agent shape. Each name is exposed as a leaf Parameter [agents, *shape] whose grad aliases the
+    flat grad buffer. Layouts: layer-major (default; every stacked tensor contiguous — batched training of all
+    agents) or agent-major (each agent's parameters contiguous — per-agent Adam steps, as the shared-critic learner
+    updates one actor per learn() call; per-agent leaf views come from agent_params(i)).
+    """
+
+    def __init__(self, shapes, device, agents=1, agent_major=False, target=False, adam=True):
+        self.shapes = OrderedDict((k, tuple(v)) for k, v in shapes.items())
+        self.device = torch.device(device)
+        self.agents = int(agents)
+        self.agent_major = agent_major
+        self.per_agent = sum(math.prod(s) for s in self.shapes.values())
+        n = self.per_agent * self.agents
+        self.numel = n
+        z = lambda: torch.zeros(n, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.data, self.grad = z(), z()
+        self.exp_avg = z() if adam else None
+        self.exp_avg_sq = z() if adam else None
+        self.target = z() if target else None
+        self.step_count = 0
+        self.agent_steps = [0] * self.agents
+        self.offsets = OrderedDict()
+        off = 0
+        for name, shp in self.shapes.items():
+            m = math.prod(shp)
+            self.offsets[name] = (off, m)
+            off += m
+        self.params = OrderedDict()
+        for name in self.shapes:
+            p = torch.nn.Parameter(self.view(self.data, name))
+            p.grad = self.view(self.grad, name)
+            self.params[name] = p
+        self._agent_params = {}
+
+    def view(self, buf, name, agent=None):
+        """Stacked [agents, *shape] view of ``buf`` (data / grad / target / moments) for ``name``."""
+        off, m = self.offsets[name]
+        shp = self.shapes[name]
+        if self.agent_major:
+            v = buf.view(self.agents, self.per_agent)[:, off:off + m].view(self.agents, *shp)
+        else:
+            v = buf[self.agents * off:self.agents * (off + m)].view(self.agents, *shp)
+        return v if agent is None else v[agent:agent + 1]
+
+    def __getitem__(self, name):
+        return self.params[name]
+
+    def target_view(self, name, agent=None):
+        return self.view(self.target, name, agent)
+
+    def agent_params(self, i):
+        """Leaf Parameters [1, *shape] of agent i (agent-major layout), grads aliasing the flat grad buffer."""
+        assert self.agent_major
+        if i not in self._agent_params:
+            d = OrderedDict()
+            for name in self.shapes:
+                p = torch.nn.Parameter(self.view(self.data, name, i))
+                p.grad = self.view(self.grad, name, i)
+                d[name] = p
+            self._agent_params[i] = d
+        return self._agent_params[i]
+
+    def agent_range(self, i):
+        assert self.agent_major
+        return i * self.per_agent, (i + 1) * self.per_agent
+
+    def parameters(self):
+        return list(self.params.values())
+
+    def zero_grad(self, agent=None):
+        if agent is None:
+            self.grad.zero_()
+        else:
+            a, b = self.agent_range(agent)
+            self.grad[a:b].zero_()
+
+    def adam_step(self, lr, betas=(0.9, 0.999), eps=1e-8, grad_scale=None, tau=None, target_mode=0, agent=None):
+        """torch.optim.Adam.step() for every agent in one launch (or agent i's slice, agent-major), optionally
+        fused with the target soft update."""
+        _require_cuda(self.data)
+        if agent is None:
+            self.step_count += 1
+            lo, hi, step = 0, self.numel, self.step_count
+        else:
+            self.agent_steps[agent] += 1
+            (lo, hi), step = self.agent_range(agent), self.agent_steps[agent]
+        sl = lambda t: None if t is None else t[lo:hi]  # noqa: E731
+        rc = _native.lib().flock_adam_step(
+            _stream(self.device), hi - lo, _p(sl(self.data)), _p(sl(self.grad)), _p(sl(self.exp_avg)),
+            _p(sl(self.exp_avg_sq)), _p(grad_scale), float(lr), float(betas[0]), float(betas[1]), float(eps), step,
+            _p(sl(self.target)) if tau is not None else None, float(tau or 0.0), int(target_mode))
+        _native.check(rc, "flock_adam_step", learn=True)
+
+    def soft_update(self, tau, mode=0, agent=None, self_update=False):
+        """target <- mode 0: t*(1-tau)+p*tau, mode 1: tau*p+(1-tau)*t. self_update: params <- soft(params, params)
+        (the shared critic is its own target, agent_simple_shared_critic.py:63,76,172-178)."""
+        lo, hi = (0, self.numel) if agent is None else self.agent_range(agent)
+        dst = self.data if self_update else self.target
+        rc = _native.lib().flock_soft_update(_stream(self.device), hi - lo, _p(dst[lo:hi]), _p(self.data[lo:hi]),
+                                             float(tau), int(mode))
+        _native.check(rc, "flock_soft_update", learn=True)
+
+    def hard_update_target(self):
+        self.target.copy_(self.data)
+
+    def load(self, name, value, agent=None, target=False):
+        """Copy a per-agent (agent=i) or stacked value into params (or the target copy)."""
+        dst = self.view(self.target if target else self.data, name)
+        v = torch.as_tensor(value, dtype=torch.float32).to(self.device)
+        with torch.no_grad():
+            if agent is None:
+                dst.copy_(v.reshape(dst.shape))
+            else:
+                dst[agent].copy_(v.reshape(dst[agent].shape))
+
+    def export(self, name, agent=None, target=False):
+        v = self.view(self.target if target else self.data, name)
+        return v.detach().clone() if agent is None else v[agent].detach().clone()
+
+
+class GradNorm:
+    """clip_grad_norm_ without a host sync: out[0] = ||g||, out[1] = clip coefficient (feed to adam_step)."""
+
+    def __init__(self, device, max_parts=2048):
+        self.partial = torch.zeros(max_parts, dtype=torch.float64, device=device)
+        self.out = torch.zeros(2, dtype=torch.float32, device=device)
+        self.max_parts = max_parts
+
+    def __call__(self, grad, max_norm):
+        rc = _native.lib().flock_grad_norm(_stream(grad.device), grad.numel(), _p(grad), _p(self.partial),
+                                           self.max_parts, float(max_norm), _p(self.out))
+        _native.check(rc, "flock_grad_norm", learn=True)
+        return self.out
+
+
+def blinear(x, W, b=None):
+    """Per-agent Linear: x [A,B,in] (or [B,in] shared by all agents), W [A,out,in], b [A,out] -> [A,B,out]."""
+    if x.dim() == 2:
+        x = x.unsqueeze(0).expand(W.shape[0], *x.shape)
+    Wt = W.transpose(1, 2)
+    if b is None:
+        return torch.bmm(x, Wt)
+    return torch.baddbmm(b.unsqueeze(1), x, Wt)
+
+
+def blayer_norm(x, w, b, eps=1e-5):
+    """Per-agent LayerNorm over the last dim: normalise, then w[A,F], b[A,F] affine."""
+    y = torch.nn.functional.layer_norm(x, (x.shape[-1],), eps=eps)
+    return torch.addcmul(b.unsqueeze(1), y, w.unsqueeze(1))
+
+
+class _GRUCellFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gi, gh, h):
+        gi, gh, h = gi.contiguous(), gh.contiguous(), h.contiguous()
+        H = h.shape[-1]
+        rows = h.numel() // H
+        hout = torch.empty_like(h)
+        ws = torch.empty(rows * 4 * H, dtype=h.dtype, device=h.device)
+        rc = _native.lib().flock_gru_fwd(_stream(h.device), rows, H, _p(gi), _p(gh), _p(h), _p(hout), _p(ws))
+        _native.check(rc, "flock_gru_fwd", learn=True)
+        ctx.save_for_backward(h, ws)
+        ctx.H = H
+        return hout
+
+    @staticmethod
+    def backward(ctx, dhout):
+        h, ws = ctx.saved_tensors
+        H = ctx.H
+        rows = h.numel() // H
+        dhout = dhout.contiguous()
+        dgi = torch.empty(*h.shape[:-1], 3 * H, dtype=h.dtype, device=h.device)
+        dgh = torch.empty_like(dgi)
+        dh = torch.empty_like(h)
+        rc = _native.lib().flock_gru_bwd(_stream(h.device), rows, H, _p(dhout), _p(h), _p(ws), _p(dgi), _p(dgh),
+                                         _p(dh))
+        _native.check(rc, "flock_gru_bwd", learn=True)
+        return dgi, dgh, dh
+
+
+def gru_cell(x, h, W_ih, W_hh, b_ih, b_hh):
+    """nn.GRUCell for A agents at once: x [A,B,in] (or shared [B,in]), h [A,B,H] -> h' [A,B,H]."""
+    gi = blinear(x, W_ih, b_ih)
+    gh = blinear(h, W_hh, b_hh)
+    return _GRUCellFn.apply(gi, gh, h)
+
+
+class ReplayRing:
+    """Device-resident ring buffer of named row tensors (``fields``: name -> row shape)."""
+
+    def __init__(self, capacity, fields, device):
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        self.fields = OrderedDict((k, tuple(v)) for k, v in fields.items())
+        self.bufs = OrderedDict((k, torch.zeros((self.capacity, *v), dtype=torch.float32, device=self.device))
+                                for k, v in self.fields.items())
+        self.counter = 0
+
+    def __len__(self):
+        return min(self.counter, self.capacity)
+
+    def _width(self, name):
+        return math.prod(self.fields[name])
+
+    def store(self, rows: dict):
+        """Append n rows per field (all fields the same n) at positions counter..counter+n-1 (mod capacity)."""
+        n = next(iter(rows.values())).shape[0]
+        idx = (torch.arange(n, device=self.device, dtype=torch.int64) + self.counter) % self.capacity
+        for name, val in rows.items():
+            src = val.to(device=self.device, dtype=torch.float32).reshape(n, -1).contiguous()
+            w = self._width(name)
+            assert src.shape[1] == w, (name, src.shape, w)
+            rc = _native.lib().flock_scatter_rows(_stream(self.device), n, w, _p(src), _p(idx), _p(self.bufs[name]))
+            _native.check(rc, "flock_scatter_rows", learn=True)
+        self.counter += n
+        return idx
+
+    def gather(self, name, idx, out=None):
+        """rows idx (any shape of int64 indices) -> [*idx.shape, *row_shape]."""
+        idx = idx.to(device=self.device, dtype=torch.int64).contiguous()
+        w = self._width(name)
+        if out is None:
+            out = torch.empty((*idx.shape, *self.fields[name]), dtype=torch.float32, device=self.device)
+        rc = _native.lib().flock_gather_rows(_stream(self.device), idx.numel(), w, _p(self.bufs[name]), _p(idx),
+                                             _p(out))
+        _native.check(rc, "flock_gather_rows", learn=True)
+        return out
+
+
+def uniform_(t, bound, generator=None):
+    with torch.no_grad():
+        t.uniform_(-bound, bound, generator=generator)
+    return t

@@ -1,0 +1,212 @@
+"""Shared-critic DDPG learner (reference: learners/maddpg_shared_critic/), batched over agents on MI355X.
+
+Reference behaviour kept (agent_simple_shared_critic.py, ddpg_network.py, utils.py):
+  * one CriticNetwork shared by every agent and used as its own target (Q11, :63,76); per-agent actors with target
+    copies; LayerNorm MLPs fc1 -> LN -> ReLU -> fc2 -> LN (+ ReLU(action_value(a))) -> ReLU -> q (ddpg_network.py:278-290),
+    actor fc1 -> LN -> ReLU -> fc2 -> LN -> ReLU -> mu -> tanh (:352-361); reference initialisations (:255-271, :326-346);
+  * learn(i) == Agent.learn() of agent i (:115-155): sample B rows with replacement, y = r + gamma Q(s', mu'_i(s')) *
+    notdone, critic MSE + Adam(beta), actor loss -mean Q(s, mu_i(s)) + Adam(alpha), every update_rate-th call of that
+    agent the soft update (critic with itself tau*c + (1-tau)*c, target actor tau*a + (1-tau)*t, :158-185);
+  * ReplayBuffer (utils.py:28-76) semantics: rows in insertion order, terminal stored as 1 - done.
+What changes: all actors live in one agent-major flat buffer (per-agent Adam = one launch over the agent's slice),
+the replay ring is device-resident (HIP scatter/gather rows, no CPU round trip), choose_action runs every agent's
+actor in one batched GEMM chain, and the OU noise is a per-(env, agent) device process.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .core import FlatParams, ReplayRing, blayer_norm, blinear
+
+
+def critic_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
+    return {"fc1.weight": (fc1, input_dim), "fc1.bias": (fc1,), "bn1.weight": (fc1,), "bn1.bias": (fc1,),
+            "fc2.weight": (fc2, fc1), "fc2.bias": (fc2,), "bn2.weight": (fc2,), "bn2.bias": (fc2,),
+            "action_value.weight": (fc2, n_actions), "action_value.bias": (fc2,),
+            "q.weight": (1, fc2), "q.bias": (1,)}
+
+
+def actor_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
+    return {"fc1.weight": (fc1, input_dim), "fc1.bias": (fc1,), "bn1.weight": (fc1,), "bn1.bias": (fc1,),
+            "fc2.weight": (fc2, fc1), "fc2.bias": (fc2,), "bn2.weight": (fc2,), "bn2.bias": (fc2,),
+            "mu.weight": (n_actions, fc2), "mu.bias": (n_actions,)}
+
+
+def critic_forward(P, state, action):
+    """ddpg_network.py:278-290. P: name -> [A, ...]; state [A,B,in] or [B,in]; action [A,B,n] or [B,n]."""
+    sv = blinear(state, P["fc1.weight"], P["fc1.bias"])
+    sv = F.relu(blayer_norm(sv, P["bn1.weight"], P["bn1.bias"]))
+    sv = blinear(sv, P["fc2.weight"], P["fc2.bias"])
+    sv = blayer_norm(sv, P["bn2.weight"], P["bn2.bias"])
+    av = F.relu(blinear(action, P["action_value.weight"], P["action_value.bias"]))
+    return blinear(F.relu(sv + av), P["q.weight"], P["q.bias"])
+
+
+def actor_forward(P, state):
+    """ddpg_network.py:352-361."""
+    x = blinear(state, P["fc1.weight"], P["fc1.bias"])
+    x = F.relu(blayer_norm(x, P["bn1.weight"], P["bn1.bias"]))
+    x = blinear(x, P["fc2.weight"], P["fc2.bias"])
+    x = F.relu(blayer_norm(x, P["bn2.weight"], P["bn2.bias"]))
+    return torch.tanh(blinear(x, P["mu.weight"], P["mu.bias"]))
+
+
+def _init_mlp(fp, names_uniform, generator):
+    """Reference init: fc1/fc2 U(+-1/sqrt(out_features)) (note: size()[0]), heads U(+-0.003), LayerNorm (1, 0),
+    action_value nn.Linear default U(+-1/sqrt(in_features))."""
+    with torch.no_grad():
+        for name, shp in fp.shapes.items():
+            v = fp.view(fp.data, name)
+            if name.startswith("bn"):
+                v.fill_(1.0 if name.endswith("weight") else 0.0)
+                continue
+            layer = name.split(".")[0]
+            if layer in ("fc1", "fc2"):
+                bound = 1.0 / math.sqrt(fp.shapes[layer + ".weight"][0])
+            elif layer in ("q", "mu"):
+                bound = 0.003
+            else:
+                bound = 1.0 / math.sqrt(fp.shapes[layer + ".weight"][1])
+            v.uniform_(-bound, bound, generator=generator)
+
+
+class SharedCriticLearner:
+    def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
+                 tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
+                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2):
+        self.device = torch.device(device)
+        self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
+        self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
+        self.batch_size, self.update_rate = batch_size, update_rate
+        self.gen = torch.Generator(device=self.device).manual_seed(seed)
+        self.critic = FlatParams(critic_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=1)
+        self.actors = FlatParams(actor_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=n_agents,
+                                 agent_major=True, target=True)
+        _init_mlp(self.critic, None, self.gen)
+        _init_mlp(self.actors, None, self.gen)
+        self.actors.hard_update_target()  # update_network_parameters(tau=1) (:81)
+        self.count = [0] * n_agents
+        self.replay = ReplayRing(buffer_size, {"state": (input_dim,), "new_state": (input_dim,),
+                                               "action": (n_actions,), "reward": (1,), "terminal": ()}, self.device)
+        self.ou = dict(sigma=ou_sigma, theta=ou_theta, dt=ou_dt)
+        self.ou_state = None
+
+    # ------------------------------------------------------------------ acting
+    def _stacked(self, fp, target=False):
+        return {n: fp.view(fp.target if target else fp.data, n) for n in fp.shapes}
+
+    @torch.no_grad()
+    def choose_action(self, obs, noise=True):
+        """All agents at once: obs [..., n_agents, input_dim] -> actions [..., n_agents, n_actions] (mu + OU noise,
+        agent_simple_shared_critic.py:92-107; OUActionNoiseGPU utils.py:6-26 with one process per (env, agent))."""
+        lead = obs.shape[:-2]
+        x = obs.reshape(-1, self.n_agents, self.input_dim).transpose(0, 1)  # [A, rows, in]
+        mu = actor_forward(self._stacked(self.actors), x).transpose(0, 1).reshape(*lead, self.n_agents,
+                                                                                  self.n_actions)
+        if not noise:
+            return mu
+        if self.ou_state is None or self.ou_state.shape != mu.shape:
+            self.ou_state = torch.zeros_like(mu)
+        o = self.ou
+        z = torch.randn(mu.shape, device=self.device, generator=self.gen)
+        self.ou_state = self.ou_state + o["theta"] * (0.0 - self.ou_state) * o["dt"] + o["sigma"] * math.sqrt(
+            o["dt"]) * z
+        return mu + self.ou_state
+
+    def reset_noise(self):
+        self.ou_state = None
+
+    # ------------------------------------------------------------------ replay
+    def store_transitions(self, state, action, reward, new_state, done):
+        """ReplayBuffer.store_transitions (utils.py:47-54): rows [n, ...]; terminal stored as 1 - done."""
+        n = state.shape[0]
+        self.replay.store({"state": state.reshape(n, -1), "new_state": new_state.reshape(n, -1),
+                           "action": action.reshape(n, -1), "reward": reward.reshape(n, 1),
+                           "terminal": 1.0 - done.reshape(n).float()})
+
+    @property
+    def mem_cntr(self):
+        return self.replay.counter
+
+    def sample_indices(self):
+        return torch.randint(0, len(self.replay), (self.batch_size,), device=self.device, generator=self.gen)
+
+    # ------------------------------------------------------------------ learning
+    def learn(self, agent, idx=None):
+        """Agent.learn() of agent ``agent`` (agent_simple_shared_critic.py:115-155). Returns (actor_loss,
+        critic_loss, True) as device tensors (no host sync), or (0, 0, False) before the buffer holds a batch."""
+        B = self.batch_size
+        if self.replay.counter < B:
+            return 0, 0, False
+        idx = self.sample_indices() if idx is None else torch.as_tensor(idx, device=self.device)
+        state = self.replay.gather("state", idx)
+        action = self.replay.gather("action", idx)
+        reward = self.replay.gather("reward", idx)
+        new_state = self.replay.gather("new_state", idx)
+        terminal = self.replay.gather("terminal", idx)
+        C = self.critic.params
+        tgt = {n: self.actors.view(self.actors.target, n, agent) for n in self.actors.shapes}
+        with torch.no_grad():
+            target_actions = actor_forward(tgt, new_state)                    # :126
+            q_next = critic_forward(C, new_state, target_actions)[0]          # :127 (target critic == critic)
+            target = reward.view(B, 1) + self.gamma * q_next * terminal.reshape(-1, 1)  # :130
+        self.critic.zero_grad()                                               # :138
+        q = critic_forward(C, state, action)[0]                               # :128
+        critic_loss = F.mse_loss(target, q)                                   # :139
+        critic_loss.backward()
+        self.critic.adam_step(self.beta)                                      # :141
+        A = self.actors.agent_params(agent)
+        self.actors.zero_grad(agent)                                          # :144
+        mu = actor_forward(A, state)                                          # :145
+        actor_loss = torch.mean(-critic_forward(C, state, mu))                # :147-148
+        torch.autograd.backward(actor_loss, inputs=list(A.values()))
+        self.actors.adam_step(self.alpha, agent=agent)                        # :150
+        if self.count[agent] % self.update_rate == 0:                         # :152-154
+            self.critic.soft_update(self.tau, mode=1, self_update=True)       # :172-178 (critic is its own target)
+            self.actors.soft_update(self.tau, mode=1, agent=agent)            # :180-185
+        self.count[agent] += 1
+        return actor_loss.detach(), critic_loss.detach(), True
+
+    # ------------------------------------------------------------------ state dicts (reference key names)
+    def load_reference_state(self, critic_sd, actor_sds, target_actor_sds=None):
+        for n, v in critic_sd.items():
+            self.critic.load(n, v, agent=0)
+        for i, sd in enumerate(actor_sds):
+            for n, v in sd.items():
+                self.actors.load(n, v, agent=i)
+        if target_actor_sds is not None:
+            for i, sd in enumerate(target_actor_sds):
+                for n, v in sd.items():
+                    self.actors.load(n, v, agent=i, target=True)
+
+    def critic_state_dict(self):
+        return {n: self.critic.export(n, 0).cpu() for n in self.critic.shapes}
+
+    def actor_state_dict(self, i, target=False):
+        return {n: self.actors.export(n, i, target=target).cpu() for n in self.actors.shapes}
+
+
+class SharedCriticBench:
+    """bench.py hook for BASELINE config 3: after each vectorized env step, insert every agent's transition into the
+    replay ring and run ONE learn() (agent round-robin, B=256)."""
+
+    def __init__(self, env, device, seed=0):
+        self.env = env
+        self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
+                                           buffer_size=1_000_000)
+        self.prev_obs = env.dnn.clone()
+        self.prev_act = None
+
+    def describe(self):
+        return (f"maddpg_shared_critic learn() x1 per vectorized step (B={self.learner.batch_size}, agent = step mod "
+                f"{self.learner.n_agents}; all {self.env.E * self.env.N} transitions inserted into a 1e6-row "
+                f"device replay ring per step)")
+
+    def after_env_step(self, s, action):
+        env = self.env
+        n = env.E * env.N
+        self.learner.store_transitions(self.prev_obs.reshape(n, -1), action.reshape(n, -1), env.reward.reshape(n, 1),
+                                       env.dnn.reshape(n, -1), env.done.reshape(n))
+        self.prev_obs = env.dnn
+        self.learner.learn(s % self.learner.n_agents)

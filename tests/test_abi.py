@@ -8,11 +8,12 @@ import pytest
 
 from marl_range_flocking_amd import _native, build
 
-HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "flock_amd.h")
+INCLUDE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+HEADERS = [os.path.join(INCLUDE, h) for h in sorted(os.listdir(INCLUDE)) if h.endswith(".h")]
 
 
 def header_functions():
-    src = open(HEADER).read()
+    src = "\n".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
     for m in re.finditer(r"^\s*(?:int|const char\*)\s+(flock_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.M | re.S):
@@ -30,7 +31,8 @@ def lib():
 def test_header_declares_expected_entry_points():
     fns = header_functions()
     for name in ("flock_step_v2", "flock_step_uw", "flock_step_uw_discrete", "flock_step_flock", "flock_knn",
-                 "flock_reset", "flock_abi_version", "flock_last_error"):
+                 "flock_reset", "flock_abi_version", "flock_last_error", "flock_adam_step", "flock_soft_update",
+                 "flock_grad_norm", "flock_gru_fwd", "flock_gru_bwd", "flock_gather_rows", "flock_scatter_rows"):
         assert name in fns, name
 
 

@@ -1,0 +1,99 @@
+"""GPU numerics of the learner HIP kernels against plain PyTorch fp32 references of the same ops."""
+import numpy as np
+import pytest
+import torch
+
+from marl_range_flocking_amd.learners.core import FlatParams, GradNorm, ReplayRing, gru_cell
+
+pytestmark = pytest.mark.gpu
+
+
+def test_fused_adam_matches_torch_adam(cuda):
+    torch.manual_seed(0)
+    shapes = {"w": (37, 53), "b": (53,)}
+    fp = FlatParams(shapes, cuda, agents=5)
+    ref = [torch.nn.Parameter(torch.randn(5, *s, device=cuda)) for s in shapes.values()]
+    for (n, p), r in zip(fp.params.items(), ref):
+        with torch.no_grad():
+            p.copy_(r)
+    opt = torch.optim.Adam(ref, lr=3e-3, foreach=False)
+    for step in range(6):
+        grads = [torch.randn_like(r) * (10.0 ** (step - 3)) for r in ref]
+        for r, g in zip(ref, grads):
+            r.grad = g.clone()
+        opt.step()
+        fp.zero_grad()
+        for p, g in zip(fp.params.values(), grads):
+            p.grad.copy_(g)
+        fp.adam_step(3e-3)
+        for p, r in zip(fp.params.values(), ref):
+            torch.testing.assert_close(p.detach(), r.detach(), rtol=2e-6, atol=1e-7)
+
+
+def test_fused_adam_soft_update_and_per_agent(cuda):
+    shapes = {"w": (8, 4)}
+    fp = FlatParams(shapes, cuda, agents=3, agent_major=True, target=True)
+    with torch.no_grad():
+        fp.data.uniform_(-1, 1)
+        fp.target.uniform_(-1, 1)
+    p0, t0 = fp.data.clone(), fp.target.clone()
+    fp.grad.normal_()
+    fp.adam_step(1e-3, agent=1, tau=0.01, target_mode=0)
+    lo, hi = fp.agent_range(1)
+    assert torch.equal(fp.data[:lo], p0[:lo]) and torch.equal(fp.data[hi:], p0[hi:])
+    exp_t = t0[lo:hi] * (1 - 0.01) + fp.data[lo:hi] * 0.01
+    torch.testing.assert_close(fp.target[lo:hi], exp_t, rtol=1e-6, atol=1e-7)
+    assert fp.agent_steps == [0, 1, 0]
+    # mode 1 self update (shared critic is its own target)
+    c = fp.data.clone()
+    fp.soft_update(0.001, mode=1, self_update=True)
+    torch.testing.assert_close(fp.data, 0.001 * c + 0.999 * c, rtol=0, atol=0)
+
+
+def test_grad_norm_and_clip_scale(cuda):
+    g = torch.randn(1_000_003, device=cuda) * 0.01
+    out = GradNorm(cuda)(g, 5.0)
+    n = torch.linalg.vector_norm(g)
+    torch.testing.assert_close(out[0], n, rtol=1e-5, atol=0)
+    torch.testing.assert_close(out[1], torch.clamp(5.0 / (n + 1e-6), max=1.0), rtol=1e-5, atol=0)
+    out = GradNorm(cuda)(g * 1e4, 5.0)
+    torch.testing.assert_close(out[1], 5.0 / (torch.linalg.vector_norm(g * 1e4) + 1e-6), rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("A,B,IN,H", [(1, 5, 7, 32), (6, 128, 32, 32), (3, 64, 16, 20)])
+def test_gru_cell_matches_torch_grucell(A, B, IN, H, cuda):
+    torch.manual_seed(A * 100 + B)
+    cells = [torch.nn.GRUCell(IN, H).to(cuda) for _ in range(A)]
+    x = torch.randn(A, B, IN, device=cuda, requires_grad=True)
+    h = torch.randn(A, B, H, device=cuda, requires_grad=True)
+    Wih = torch.stack([c.weight_ih for c in cells]).detach().requires_grad_()
+    Whh = torch.stack([c.weight_hh for c in cells]).detach().requires_grad_()
+    bih = torch.stack([c.bias_ih for c in cells]).detach().requires_grad_()
+    bhh = torch.stack([c.bias_hh for c in cells]).detach().requires_grad_()
+    out = gru_cell(x, h, Wih, Whh, bih, bhh)
+    ref = torch.stack([cells[a](x[a], h[a]) for a in range(A)])
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-6)
+    go = torch.randn_like(out)
+    gx, gh, gw = torch.autograd.grad(out, (x, h, Wih), go)
+    rx, rh = torch.autograd.grad(ref, (x, h), go, retain_graph=True)
+    rw = torch.stack([torch.autograd.grad(ref, cells[a].weight_ih, go, retain_graph=True)[0] for a in range(A)])
+    torch.testing.assert_close(gx, rx, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(gh, rh, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(gw, rw, rtol=1e-4, atol=1e-5)
+
+
+def test_replay_ring_scatter_gather_wraps(cuda):
+    ring = ReplayRing(10, {"s": (3,), "d": ()}, cuda)
+    rows = [torch.arange(i * 3, i * 3 + 12, dtype=torch.float32, device=cuda).view(4, 3) for i in range(4)]
+    for r in rows:
+        ring.store({"s": r, "d": r[:, 0]})
+    allrows = torch.cat(rows)  # 16 rows into capacity 10: positions (i mod 10), last write wins
+    expect = torch.zeros(10, 3, device=cuda)
+    for i in range(16):
+        expect[i % 10] = allrows[i]
+    assert torch.equal(ring.bufs["s"], expect)
+    idx = torch.tensor([[0, 9], [3, 3]], device=cuda)
+    got = ring.gather("s", idx)
+    assert got.shape == (2, 2, 3) and torch.equal(got, expect[idx])
+    assert torch.equal(ring.gather("d", idx), expect[idx][..., 0])
+    assert len(ring) == 10 and ring.counter == 16

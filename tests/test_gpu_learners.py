@@ -1,0 +1,81 @@
+"""GPU learner updates against golden vectors produced by the REFERENCE learners (tests/golden/gen_golden_learn_*.py).
+
+Tolerance rules: losses rtol 1e-4; parameters after Adam compared only where every consumed
+gradient had |g| > 1e-6 (Adam's first steps are lr * g / (|g| + eps): sign-unstable for tiny g), rtol 1e-4 / atol 1e-6;
+frozen networks bitwise unchanged.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _sd(z, prefix):
+    out = {}
+    for k in z.files:
+        if k.startswith(prefix + "/"):
+            out[k[len(prefix) + 1:]] = z[k]
+    return out
+
+
+def _masked_close(got, want, grads, what, rtol=1e-4, atol=1e-6):
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    mask = np.ones(want.shape, bool)
+    for g in grads:
+        mask &= np.abs(g) > 1e-6
+    assert mask.mean() > 0.5, f"{what}: too few well-conditioned elements"
+    err = np.abs(got - want)
+    bad = mask & (err > atol + rtol * np.abs(want))
+    assert not bad.any(), f"{what}: {bad.sum()} / {mask.sum()} elements off, max err {err[mask].max()}"
+
+
+def test_shared_critic_learn_matches_reference(cuda):
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    z = np.load(os.path.join(GOLD, "learn_shared_critic.npz"))
+    m = json.loads(str(z["meta"]))
+    A, K = m["n_agents"], m["k"]
+    L = SharedCriticLearner(A, K, fc1=m["fc1"], fc2=m["fc2"], alpha=m["alpha"], beta=m["beta"], gamma=m["gamma"],
+                            tau=m["tau"], batch_size=m["batch"], update_rate=m["update_rate"],
+                            buffer_size=m["capacity"], device=cuda)
+    L.load_reference_state(_sd(z, "init/critic"), [_sd(z, f"init/actor{i}") for i in range(A)],
+                           [_sd(z, f"init/target_actor{i}") for i in range(A)])
+    for t in range(z["state"].shape[0]):
+        L.store_transitions(torch.tensor(z["state"][t]), torch.tensor(z["action"][t]), torch.tensor(z["reward"][t]),
+                            torch.tensor(z["next_state"][t]), torch.tensor(z["done"][t]))
+    for c, i in enumerate(m["calls"]):
+        al, cl, ok = L.learn(i, idx=torch.tensor(z["idx"][c]))
+        assert ok
+        np.testing.assert_allclose([al.item(), cl.item()], z["losses"][c], rtol=1e-4)
+    crit = L.critic_state_dict()
+    for n, v in crit.items():
+        grads = [z[f"grad/call{c}.critic.{n}"] for c in range(len(m["calls"]))]
+        _masked_close(v.numpy(), z[f"final/critic/{n}"], grads, f"critic {n}")
+    for i in range(A):
+        calls = [c for c, a in enumerate(m["calls"]) if a == i]
+        for target in (False, True):
+            sd = L.actor_state_dict(i, target=target)
+            tag = "target_actor" if target else "actor"
+            for n, v in sd.items():
+                grads = [z[f"grad/call{c}.actor.{n}"] for c in calls]
+                _masked_close(v.numpy(), z[f"final/{tag}{i}/{n}"], grads, f"{tag}{i} {n}")
+
+
+def test_shared_critic_choose_action_batched(cuda):
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner, actor_forward
+
+    L = SharedCriticLearner(5, 4, fc1=16, fc2=8, device=cuda)
+    obs = torch.rand(7, 5, 4, device=cuda) * 14
+    mu = L.choose_action(obs, noise=False)
+    for i in range(5):
+        P = {n: L.actors.view(L.actors.data, n, i) for n in L.actors.shapes}
+        ref = actor_forward(P, obs[:, i])[0]
+        torch.testing.assert_close(mu[:, i], ref, rtol=1e-5, atol=1e-6)
+    a = L.choose_action(obs)
+    assert a.shape == (7, 5, 2) and not torch.equal(a, mu)
