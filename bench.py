@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--agents", type=int, default=256)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uw_discrete", "flock"])
-    ap.add_argument("--learner", default="none", choices=["none", "shared_critic"])
+    ap.add_argument("--learner", default="shared_critic", choices=["none", "shared_critic"],
+                    help="config 3 pairs the env with the shared-critic update (default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")

@@ -33,6 +33,11 @@ int flock_adam_step(void* stream, int64_t n, float* param, const float* grad, fl
                     const float* grad_scale, float lr, float beta1, float beta2, float eps, int64_t step,
                     float* target, float tau, int target_mode);
 
+/* Same, with the step count read from device memory (*step, already incremented): HIP-graph capturable. */
+int flock_adam_step_dev(void* stream, int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        const float* grad_scale, float lr, float beta1, float beta2, float eps, const int64_t* step,
+                        float* target, float tau, int target_mode);
+
 int flock_soft_update(void* stream, int64_t n, float* target, const float* src, float tau, int mode);
 
 /* partial: device scratch of max_parts doubles; out: device float[2] */

@@ -31,6 +31,8 @@ SIGNATURES = {
     "flock_learn_last_error": [],
     "flock_adam_step": [_c_void_p, ctypes.c_int64] + [_c_void_p] * 5 + [_c_float] * 4 + [ctypes.c_int64, _c_void_p,
                                                                                       _c_float, _c_int],
+    "flock_adam_step_dev": [_c_void_p, ctypes.c_int64] + [_c_void_p] * 5 + [_c_float] * 4 + [_c_void_p, _c_void_p,
+                                                                                          _c_float, _c_int],
     "flock_soft_update": [_c_void_p, ctypes.c_int64, _c_void_p, _c_void_p, _c_float, _c_int],
     "flock_grad_norm": [_c_void_p, ctypes.c_int64, _c_void_p, _c_void_p, _c_int, _c_float, _c_void_p],
     "flock_gru_fwd": [_c_void_p, ctypes.c_int64, _c_int] + [_c_void_p] * 5,

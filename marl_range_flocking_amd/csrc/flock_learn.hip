@@ -70,6 +70,45 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(int64_t n, float* __restri
     }
 }
 
+// Same update with the step count read from device memory (graph-capturable: the bias corrections are computed
+// in-kernel, once per block, from *step).
+__global__ __launch_bounds__(kBlock) void adam_dev_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, float* __restrict__ v,
+                                                          const float* __restrict__ grad_scale,
+                                                          const int64_t* __restrict__ step, float lr, float beta1,
+                                                          float beta2, float eps, float* __restrict__ target,
+                                                          float tau, float one_minus_tau, int target_mode) {
+    __shared__ float sh[2];
+    if (threadIdx.x == 0) {
+        const double st = (double)*step;
+        const double bc1 = 1.0 - pow((double)beta1, st);
+        const double bc2 = 1.0 - pow((double)beta2, st);
+        sh[0] = (float)(-(double)lr / bc1);
+        sh[1] = (float)sqrt(bc2);
+    }
+    __syncthreads();
+    const float neg_step_size = sh[0], bc2_sqrt = sh[1];
+    const float w1 = (float)(1.0 - (double)beta1), one_minus_b2 = (float)(1.0 - (double)beta2);
+    const float gs = grad_scale ? *grad_scale : 1.0f;
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        float gi = g[i];
+        if (grad_scale) gi = gi * gs;
+        float mi = m[i];
+        mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
+        float vi = v[i] * beta2;
+        vi = vi + (one_minus_b2 * gi) * gi;
+        const float denom = sqrt_rn(vi) / bc2_sqrt + eps;
+        const float pi = p[i] + (neg_step_size * mi) / denom;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi;
+        if (target) {
+            const float t = target[i];
+            target[i] = target_mode == 0 ? t * one_minus_tau + pi * tau : tau * pi + one_minus_tau * t;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void soft_update_kernel(int64_t n, float* __restrict__ target,
                                                              const float* __restrict__ src, float tau,
                                                              float one_minus_tau, int mode) {
@@ -218,6 +257,17 @@ int flock_adam_step(void* stream, int64_t n, float* param, const float* grad, fl
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, param, grad, exp_avg,
                        exp_avg_sq, grad_scale, (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2),
                        neg_step, bc2s, eps, target, tau, (float)(1.0 - (double)tau), target_mode);
+    return launched();
+}
+
+int flock_adam_step_dev(void* stream, int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        const float* grad_scale, float lr, float beta1, float beta2, float eps, const int64_t* step,
+                        float* target, float tau, int target_mode) {
+    if (n <= 0) return 0;
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !step) return fail(-3, "flock_adam_step_dev: NULL pointer");
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, param, grad,
+                       exp_avg, exp_avg_sq, grad_scale, step, lr, beta1, beta2, eps, target, tau,
+                       (float)(1.0 - (double)tau), target_mode);
     return launched();
 }
 

@@ -59,6 +59,7 @@ class FlatParams:
         self.target = z() if target else None
         self.step_count = 0
         self.agent_steps = [0] * self.agents
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)  # for graph-captured steps
         self.offsets = OrderedDict()
         off = 0
         for name, shp in self.shapes.items():
@@ -131,6 +132,18 @@ class FlatParams:
             _p(sl(self.target)) if tau is not None else None, float(tau or 0.0), int(target_mode))
         _native.check(rc, "flock_adam_step", learn=True)
 
+    def adam_step_dev(self, lr, betas=(0.9, 0.999), eps=1e-8, grad_scale=None, tau=None, target_mode=0):
+        """Adam step with the step count kept on the device (step_dev += 1 then the update): HIP-graph capturable."""
+        self.step_dev.add_(1)
+        rc = _native.lib().flock_adam_step_dev(
+            _stream(self.device), self.numel, _p(self.data), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
+            _p(grad_scale), float(lr), float(betas[0]), float(betas[1]), float(eps), _p(self.step_dev),
+            _p(self.target) if tau is not None else None, float(tau or 0.0), int(target_mode))
+        _native.check(rc, "flock_adam_step_dev", learn=True)
+
+    def state_tensors(self):
+        return [t for t in (self.data, self.exp_avg, self.exp_avg_sq, self.target, self.step_dev) if t is not None]
+
     def soft_update(self, tau, mode=0, agent=None, self_update=False):
         """target <- mode 0: t*(1-tau)+p*tau, mode 1: tau*p+(1-tau)*t. self_update: params <- soft(params, params)
         (the shared critic is its own target, agent_simple_shared_critic.py:63,76,172-178)."""
@@ -174,7 +187,11 @@ class GradNorm:
 
 
 def blinear(x, W, b=None):
-    """Per-agent Linear: x [A,B,in] (or [B,in] shared by all agents), W [A,out,in], b [A,out] -> [A,B,out]."""
+    """Per-agent Linear: x [A,B,in] (or [B,in] shared by all agents), W [A,out,in], b [A,out] -> [A,B,out].
+    A == 1 goes through F.linear (one GEMM with the bias epilogue) instead of a batched GEMM."""
+    if W.shape[0] == 1:
+        x2 = x if x.dim() == 2 else x[0]
+        return torch.nn.functional.linear(x2, W[0], None if b is None else b[0]).unsqueeze(0)
     if x.dim() == 2:
         x = x.unsqueeze(0).expand(W.shape[0], *x.shape)
     Wt = W.transpose(1, 2)
@@ -185,6 +202,8 @@ def blinear(x, W, b=None):
 
 def blayer_norm(x, w, b, eps=1e-5):
     """Per-agent LayerNorm over the last dim: normalise, then w[A,F], b[A,F] affine."""
+    if w.shape[0] == 1:  # one network: the fused affine LayerNorm kernel (forward and backward)
+        return torch.nn.functional.layer_norm(x, (x.shape[-1],), w[0], b[0], eps=eps)
     y = torch.nn.functional.layer_norm(x, (x.shape[-1],), eps=eps)
     return torch.addcmul(b.unsqueeze(1), y, w.unsqueeze(1))
 
@@ -243,17 +262,31 @@ class ReplayRing:
         return math.prod(self.fields[name])
 
     def store(self, rows: dict):
-        """Append n rows per field (all fields the same n) at positions counter..counter+n-1 (mod capacity)."""
+        """Append n rows per field (all fields the same n) at positions counter..counter+n-1 (mod capacity): the
+        positions are consecutive, so each field is one or two contiguous streaming copies (split at the wrap)."""
         n = next(iter(rows.values())).shape[0]
-        idx = (torch.arange(n, device=self.device, dtype=torch.int64) + self.counter) % self.capacity
+        if n > self.capacity:  # only the last `capacity` rows survive
+            rows = {k: v[n - self.capacity:] for k, v in rows.items()}
+            self.counter += n - self.capacity
+            n = self.capacity
+        start = self.counter % self.capacity
+        first = min(n, self.capacity - start)
         for name, val in rows.items():
-            src = val.to(device=self.device, dtype=torch.float32).reshape(n, -1).contiguous()
-            w = self._width(name)
-            assert src.shape[1] == w, (name, src.shape, w)
-            rc = _native.lib().flock_scatter_rows(_stream(self.device), n, w, _p(src), _p(idx), _p(self.bufs[name]))
-            _native.check(rc, "flock_scatter_rows", learn=True)
+            dst = self.bufs[name].view(self.capacity, -1)
+            src = val.reshape(n, -1)
+            assert src.shape[1] == dst.shape[1], (name, src.shape, dst.shape)
+            dst[start:start + first].copy_(src[:first])
+            if first < n:
+                dst[:n - first].copy_(src[first:])
         self.counter += n
-        return idx
+
+    def scatter(self, name, idx, rows):
+        """Write rows at arbitrary positions idx (HIP row scatter)."""
+        idx = idx.to(device=self.device, dtype=torch.int64).contiguous()
+        src = rows.to(device=self.device, dtype=torch.float32).reshape(idx.numel(), -1).contiguous()
+        rc = _native.lib().flock_scatter_rows(_stream(self.device), idx.numel(), src.shape[1], _p(src), _p(idx),
+                                              _p(self.bufs[name]))
+        _native.check(rc, "flock_scatter_rows", learn=True)
 
     def gather(self, name, idx, out=None):
         """rows idx (any shape of int64 indices) -> [*idx.shape, *row_shape]."""
@@ -265,6 +298,25 @@ class ReplayRing:
                                              _p(out))
         _native.check(rc, "flock_gather_rows", learn=True)
         return out
+
+
+def capture_graph(fn, device, state, warmup=2):
+    """Capture ``fn`` (a learner update on static tensors) into a HIP graph. ``state``: tensors the warm-up runs
+    mutate (parameters, moments, step counters) — snapshotted and restored so capture has no side effect."""
+    snap = [t.clone() for t in state]
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        for _ in range(warmup):
+            fn()
+    torch.cuda.current_stream(device).wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fn()
+    with torch.no_grad():
+        for t, v in zip(state, snap):
+            t.copy_(v)
+    return g
 
 
 def uniform_(t, bound, generator=None):

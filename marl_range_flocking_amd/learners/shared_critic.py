@@ -17,7 +17,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-from .core import FlatParams, ReplayRing, blayer_norm, blinear
+from .core import FlatParams, ReplayRing, blayer_norm, blinear, capture_graph
 
 
 def critic_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
@@ -74,7 +74,7 @@ def _init_mlp(fp, names_uniform, generator):
 class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
-                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2):
+                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -91,6 +91,14 @@ class SharedCriticLearner:
                                                "action": (n_actions,), "reward": (1,), "terminal": ()}, self.device)
         self.ou = dict(sigma=ou_sigma, theta=ou_theta, dt=ou_dt)
         self.ou_state = None
+        # the update runs on static tensors so it can be replayed as one HIP graph: agent i's actor is copied into
+        # a scratch slot (params, target, Adam moments, step) and back around the replay
+        self.scratch = FlatParams(actor_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=1, target=True)
+        self.actor_steps = torch.zeros(n_agents, dtype=torch.int64, device=self.device)
+        self.static_idx = torch.zeros(batch_size, dtype=torch.int64, device=self.device)
+        self.losses = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.use_graph = use_graph
+        self.graph = None
 
     # ------------------------------------------------------------------ acting
     def _stacked(self, fp, target=False):
@@ -133,40 +141,70 @@ class SharedCriticLearner:
         return torch.randint(0, len(self.replay), (self.batch_size,), device=self.device, generator=self.gen)
 
     # ------------------------------------------------------------------ learning
-    def learn(self, agent, idx=None):
-        """Agent.learn() of agent ``agent`` (agent_simple_shared_critic.py:115-155). Returns (actor_loss,
-        critic_loss, True) as device tensors (no host sync), or (0, 0, False) before the buffer holds a batch."""
+    def _update(self):
+        """One Agent.learn() body on static tensors (agent_simple_shared_critic.py:118-150) for the actor in the
+        scratch slot; capturable."""
         B = self.batch_size
-        if self.replay.counter < B:
-            return 0, 0, False
-        idx = self.sample_indices() if idx is None else torch.as_tensor(idx, device=self.device)
+        idx = self.static_idx
         state = self.replay.gather("state", idx)
         action = self.replay.gather("action", idx)
         reward = self.replay.gather("reward", idx)
         new_state = self.replay.gather("new_state", idx)
         terminal = self.replay.gather("terminal", idx)
         C = self.critic.params
-        tgt = {n: self.actors.view(self.actors.target, n, agent) for n in self.actors.shapes}
+        S = self.scratch.params
+        tgt = {n: self.scratch.view(self.scratch.target, n) for n in self.scratch.shapes}
         with torch.no_grad():
             target_actions = actor_forward(tgt, new_state)                    # :126
             q_next = critic_forward(C, new_state, target_actions)[0]          # :127 (target critic == critic)
             target = reward.view(B, 1) + self.gamma * q_next * terminal.reshape(-1, 1)  # :130
-        self.critic.zero_grad()                                               # :138
+        self.critic.grad.zero_()                                              # :138
         q = critic_forward(C, state, action)[0]                               # :128
         critic_loss = F.mse_loss(target, q)                                   # :139
-        critic_loss.backward()
-        self.critic.adam_step(self.beta)                                      # :141
-        A = self.actors.agent_params(agent)
-        self.actors.zero_grad(agent)                                          # :144
-        mu = actor_forward(A, state)                                          # :145
+        torch.autograd.backward(critic_loss, inputs=list(C.values()))
+        self.critic.adam_step_dev(self.beta)                                  # :141
+        self.scratch.grad.zero_()                                             # :144
+        mu = actor_forward(S, state)                                          # :145
         actor_loss = torch.mean(-critic_forward(C, state, mu))                # :147-148
-        torch.autograd.backward(actor_loss, inputs=list(A.values()))
-        self.actors.adam_step(self.alpha, agent=agent)                        # :150
+        torch.autograd.backward(actor_loss, inputs=list(S.values()))
+        self.scratch.adam_step_dev(self.alpha)                                # :150
+        with torch.no_grad():
+            self.losses[0].copy_(actor_loss.detach())
+            self.losses[1].copy_(critic_loss.detach())
+
+    def learn(self, agent, idx=None):
+        """Agent.learn() of agent ``agent`` (agent_simple_shared_critic.py:115-155). Returns (actor_loss,
+        critic_loss, True) as device tensors (no host sync), or (0, 0, False) before the buffer holds a batch."""
+        B = self.batch_size
+        if self.replay.counter < B:
+            return 0, 0, False
+        if idx is None:                                                       # utils.py:65-76 (with replacement)
+            torch.randint(0, len(self.replay), (B,), device=self.device, generator=self.gen, out=self.static_idx)
+        else:
+            self.static_idx.copy_(torch.as_tensor(idx).to(self.device))
+        lo, hi = self.actors.agent_range(agent)
+        A, S = self.actors, self.scratch
+        with torch.no_grad():
+            for src, dst in ((A.data, S.data), (A.target, S.target), (A.exp_avg, S.exp_avg),
+                             (A.exp_avg_sq, S.exp_avg_sq)):
+                dst.copy_(src[lo:hi])
+            S.step_dev.copy_(self.actor_steps[agent:agent + 1])
+        if self.use_graph:
+            if self.graph is None:
+                self.graph = capture_graph(self._update, self.device,
+                                           self.critic.state_tensors() + S.state_tensors() + [self.losses])
+            self.graph.replay()
+        else:
+            self._update()
+        with torch.no_grad():
+            for src, dst in ((S.data, A.data), (S.exp_avg, A.exp_avg), (S.exp_avg_sq, A.exp_avg_sq)):
+                dst[lo:hi].copy_(src)
+            self.actor_steps[agent:agent + 1].copy_(S.step_dev)
         if self.count[agent] % self.update_rate == 0:                         # :152-154
             self.critic.soft_update(self.tau, mode=1, self_update=True)       # :172-178 (critic is its own target)
             self.actors.soft_update(self.tau, mode=1, agent=agent)            # :180-185
         self.count[agent] += 1
-        return actor_loss.detach(), critic_loss.detach(), True
+        return self.losses[0], self.losses[1], True
 
     # ------------------------------------------------------------------ state dicts (reference key names)
     def load_reference_state(self, critic_sd, actor_sds, target_actor_sds=None):

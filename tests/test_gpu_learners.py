@@ -23,19 +23,23 @@ def _sd(z, prefix):
     return out
 
 
-def _masked_close(got, want, grads, what, rtol=1e-4, atol=1e-6):
+def _masked_close(got, want, grads, what, lr, rtol=1e-4, atol=1e-6):
+    """Well-conditioned elements (every consumed |g| > 1e-6, or exactly 0 — dead ReLU units) within rtol/atol; the
+    rest may differ by at most the Adam step bound 2 * lr per step (sign-unstable lr * g / (|g| + eps))."""
     got = np.asarray(got, np.float64)
     want = np.asarray(want, np.float64)
     mask = np.ones(want.shape, bool)
     for g in grads:
-        mask &= np.abs(g) > 1e-6
-    assert mask.mean() > 0.5, f"{what}: too few well-conditioned elements"
+        mask &= (np.abs(g) > 1e-6) | (g == 0)
     err = np.abs(got - want)
     bad = mask & (err > atol + rtol * np.abs(want))
     assert not bad.any(), f"{what}: {bad.sum()} / {mask.sum()} elements off, max err {err[mask].max()}"
+    loose = ~mask & (err > 2.0 * lr * max(1, len(grads)) + atol)
+    assert not loose.any(), f"{what}: ill-conditioned elements beyond the Adam step bound: {err[~mask].max()}"
 
 
-def test_shared_critic_learn_matches_reference(cuda):
+@pytest.mark.parametrize("use_graph", [False, True], ids=["eager", "hipgraph"])
+def test_shared_critic_learn_matches_reference(use_graph, cuda):
     from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
 
     z = np.load(os.path.join(GOLD, "learn_shared_critic.npz"))
@@ -43,7 +47,7 @@ def test_shared_critic_learn_matches_reference(cuda):
     A, K = m["n_agents"], m["k"]
     L = SharedCriticLearner(A, K, fc1=m["fc1"], fc2=m["fc2"], alpha=m["alpha"], beta=m["beta"], gamma=m["gamma"],
                             tau=m["tau"], batch_size=m["batch"], update_rate=m["update_rate"],
-                            buffer_size=m["capacity"], device=cuda)
+                            buffer_size=m["capacity"], device=cuda, use_graph=use_graph)
     L.load_reference_state(_sd(z, "init/critic"), [_sd(z, f"init/actor{i}") for i in range(A)],
                            [_sd(z, f"init/target_actor{i}") for i in range(A)])
     for t in range(z["state"].shape[0]):
@@ -56,7 +60,7 @@ def test_shared_critic_learn_matches_reference(cuda):
     crit = L.critic_state_dict()
     for n, v in crit.items():
         grads = [z[f"grad/call{c}.critic.{n}"] for c in range(len(m["calls"]))]
-        _masked_close(v.numpy(), z[f"final/critic/{n}"], grads, f"critic {n}")
+        _masked_close(v.numpy(), z[f"final/critic/{n}"], grads, f"critic {n}", m["beta"])
     for i in range(A):
         calls = [c for c, a in enumerate(m["calls"]) if a == i]
         for target in (False, True):
@@ -64,7 +68,7 @@ def test_shared_critic_learn_matches_reference(cuda):
             tag = "target_actor" if target else "actor"
             for n, v in sd.items():
                 grads = [z[f"grad/call{c}.actor.{n}"] for c in calls]
-                _masked_close(v.numpy(), z[f"final/{tag}{i}/{n}"], grads, f"{tag}{i} {n}")
+                _masked_close(v.numpy(), z[f"final/{tag}{i}/{n}"], grads, f"{tag}{i} {n}", m["alpha"])
 
 
 def test_shared_critic_choose_action_batched(cuda):
