@@ -86,6 +86,18 @@ class FlatParams:
     def __getitem__(self, name):
         return self.params[name]
 
+    def new_leaves(self):
+        """A fresh set of leaf Parameters aliasing the same data/grad storage. Graph-captured updates use their own
+        set, so an autograd graph a caller keeps alive on ``params`` (e.g. a grad-enabled forward outside the
+        learner) never shares AccumulateGrad nodes with the captured backward (that combination crashed HIP graph
+        capture on ROCm 7.2)."""
+        d = OrderedDict()
+        for name in self.shapes:
+            p = torch.nn.Parameter(self.view(self.data, name))
+            p.grad = self.view(self.grad, name)
+            d[name] = p
+        return d
+
     def target_view(self, name, agent=None):
         return self.view(self.target, name, agent)
 

@@ -99,6 +99,8 @@ class SharedCriticLearner:
         self.losses = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.use_graph = use_graph
         self.graph = None
+        self.critic_leaves = self.critic.new_leaves()
+        self.scratch_leaves = self.scratch.new_leaves()
 
     # ------------------------------------------------------------------ acting
     def _stacked(self, fp, target=False):
@@ -151,8 +153,8 @@ class SharedCriticLearner:
         reward = self.replay.gather("reward", idx)
         new_state = self.replay.gather("new_state", idx)
         terminal = self.replay.gather("terminal", idx)
-        C = self.critic.params
-        S = self.scratch.params
+        C = self.critic_leaves
+        S = self.scratch_leaves
         tgt = {n: self.scratch.view(self.scratch.target, n) for n in self.scratch.shapes}
         with torch.no_grad():
             target_actions = actor_forward(tgt, new_state)                    # :126

@@ -1,0 +1,197 @@
+"""Recurrent VDN (reference: learners/vdn/), batched over agents on MI355X.
+
+Reference behaviour kept:
+  * QNet (learners/vdn/net.py:11-61): per agent Linear(n_obs,64)-ReLU-Linear(64,32)-ReLU-GRUCell(32,32)-Linear(32,|A|),
+    nn.Linear / nn.GRUCell default initialisation, ``sample_action`` epsilon-greedy with ONE coin per batch row (:52-58);
+  * train() (learners/vdn/train_flock.py:16-43): update_iter x [sample B chunk starts with replacement, run q and
+    q_target over the chunk, sum_q = sum_agents Q(s, a), target = sum r + gamma * sum_agents max Q'(s') * (1 - done),
+    loss = sum over steps of smooth_l1, reset hidden rows where done], then clip_grad_norm_(5) and Adam(lr);
+  * ReplayBufferVDN (utils.py:7-69): deque of whole-swarm transitions, oldest dropped at buffer_limit, chunk starts
+    uniform in [0, len - chunk).
+What changes: every agent's network is one slice of stacked [A, ...] tensors (batched GEMMs on hipBLASLt, GRU
+elementwise in flock_gru_fwd/bwd), one Adam launch for all agents with the clip coefficient read from device
+memory (flock_grad_norm: no host sync), the replay ring is device-resident, and one update iteration replays as a
+HIP graph.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell
+
+HX = 32
+
+
+def qnet_shapes(n_obs, n_actions, hx=HX, recurrent=True):
+    s = {"feat1.weight": (64, n_obs), "feat1.bias": (64,), "feat2.weight": (hx, 64), "feat2.bias": (hx,)}
+    if recurrent:
+        s.update({"gru.weight_ih": (3 * hx, hx), "gru.weight_hh": (3 * hx, hx), "gru.bias_ih": (3 * hx,),
+                  "gru.bias_hh": (3 * hx,)})
+    s.update({"q.weight": (n_actions, hx), "q.bias": (n_actions,)})
+    return s
+
+
+def reference_key(name, i):
+    """Our stacked name -> the reference QNet state_dict key of agent i (learners/vdn/net.py:19-25)."""
+    layer, kind = name.split(".")
+    return {"feat1": f"agent_feature_{i}.0.{kind}", "feat2": f"agent_feature_{i}.2.{kind}",
+            "gru": f"agent_gru_{i}.{kind}", "q": f"agent_q_{i}.{kind}"}[layer]
+
+
+class BatchedQNet:
+    def __init__(self, n_agents, n_obs, n_actions, recurrent=True, device="cuda", generator=None):
+        self.n_agents, self.n_obs, self.n_actions, self.recurrent = n_agents, n_obs, n_actions, recurrent
+        self.hx_size = HX
+        self.device = torch.device(device)
+        self.P = FlatParams(qnet_shapes(n_obs, n_actions, HX, recurrent), self.device, agents=n_agents)
+        with torch.no_grad():  # nn.Linear / nn.GRUCell defaults: U(+-1/sqrt(fan_in)), GRU U(+-1/sqrt(hidden))
+            for name, shp in self.P.shapes.items():
+                layer = name.split(".")[0]
+                fan = HX if layer == "gru" else self.P.shapes[layer + ".weight"][1]
+                b = 1.0 / math.sqrt(fan)
+                self.P.view(self.P.data, name).uniform_(-b, b, generator=generator)
+
+    def params(self, target=False):
+        buf = self.P.target if target else None
+        return self.P.params if buf is None else {n: self.P.view(buf, n) for n in self.P.shapes}
+
+    def forward_am(self, x, h, P=None):
+        """Agent-major forward: x [A,B,n_obs], h [A,B,H] -> q [A,B,n_actions], h' (QNet.forward net.py:27-37)."""
+        P = self.P.params if P is None else P
+        y = F.relu(blinear(x, P["feat1.weight"], P["feat1.bias"]))
+        y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
+        if self.recurrent:
+            y = gru_cell(y, h, P["gru.weight_ih"], P["gru.weight_hh"], P["gru.bias_ih"], P["gru.bias_hh"])
+            h = y
+        return blinear(y, P["q.weight"], P["q.bias"]), h
+
+    def __call__(self, obs, hidden):
+        """Reference layout: obs [B,A,n_obs], hidden [B,A,H] -> (q [B,A,n_actions], hidden [B,A,H])."""
+        q, h = self.forward_am(obs.transpose(0, 1), hidden.transpose(0, 1))
+        return q.transpose(0, 1), h.transpose(0, 1)
+
+    def init_hidden(self, batch_size=1):
+        return torch.zeros((batch_size, self.n_agents, HX), device=self.device)
+
+    @torch.no_grad()
+    def sample_action(self, obs, hidden, epsilon, generator=None):
+        """net.py:52-58: one exploration coin per batch row; returns float action ids [B, A]."""
+        out, hidden = self(obs, hidden)
+        B = out.shape[0]
+        mask = torch.rand((B,), device=self.device, generator=generator) <= epsilon
+        rnd = torch.randint(0, out.shape[2], (B, out.shape[1]), device=self.device, generator=generator)
+        action = torch.where(mask[:, None], rnd, out.argmax(dim=2)).float()
+        return action, hidden
+
+    def load_reference_state_dict(self, sd, target=False):
+        for name in self.P.shapes:
+            for i in range(self.n_agents):
+                self.P.load(name, sd[reference_key(name, i)], agent=i, target=target)
+
+    def state_dict(self):
+        """Reference key names (so learners/vdn/test_flock.py-style loaders can read it)."""
+        out = {}
+        for name in self.P.shapes:
+            v = self.P.view(self.P.data, name).detach().cpu()
+            for i in range(self.n_agents):
+                out[reference_key(name, i)] = v[i].clone()
+        return out
+
+
+class VDNLearner:
+    def __init__(self, n_agents, n_obs, n_actions, lr=1e-3, gamma=0.99, batch_size=32, chunk_size=10,
+                 update_iter=10, grad_clip_norm=5.0, buffer_limit=50_000, recurrent=True, device="cuda", seed=0,
+                 use_graph=True):
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device).manual_seed(seed)
+        self.q = BatchedQNet(n_agents, n_obs, n_actions, recurrent, self.device, self.gen)
+        self.q.P.target = torch.zeros_like(self.q.P.data)  # q_target lives in the target slot of the same buffer
+        self.sync_target()
+        self.A, self.n_obs, self.n_actions = n_agents, n_obs, n_actions
+        self.lr, self.gamma, self.B, self.grad_clip_norm = lr, gamma, batch_size, grad_clip_norm
+        self.chunk = chunk_size if recurrent else 1
+        self.update_iter = update_iter
+        self.replay = ReplayRing(buffer_limit, {"s": (n_agents, n_obs), "a": (n_agents,), "r": (n_agents,),
+                                                "s_prime": (n_agents, n_obs), "done": ()}, self.device)
+        self.norm = GradNorm(self.device)
+        self.static_idx = torch.zeros((batch_size, self.chunk), dtype=torch.int64, device=self.device)
+        self.loss = torch.zeros((), device=self.device)
+        self.use_graph = use_graph
+        self.graph = None
+        self.train_leaves = self.q.P.new_leaves()
+
+    def sync_target(self):
+        """q_target.load_state_dict(q.state_dict()) (train_flock.py:84, :114-115)."""
+        self.q.P.hard_update_target()
+
+    def put(self, s, a, r, s_prime, done):
+        """memory.put((s, a, r, s', [int(all_done)])) (train_flock.py:102); also accepts a batch of transitions
+        (one per env) with a leading dim."""
+        s = torch.as_tensor(s, device=self.device, dtype=torch.float32)
+        if s.dim() == 2:
+            s, a, r, s_prime = s[None], torch.as_tensor(a)[None], torch.as_tensor(r)[None], torch.as_tensor(s_prime)[None]
+            done = torch.as_tensor(done, dtype=torch.float32).reshape(1)
+        n = s.shape[0]
+        self.replay.store({"s": s, "a": torch.as_tensor(a, device=self.device).float().reshape(n, self.A),
+                           "r": torch.as_tensor(r, device=self.device).float().reshape(n, self.A),
+                           "s_prime": torch.as_tensor(s_prime, device=self.device).float(),
+                           "done": torch.as_tensor(done, device=self.device).float().reshape(n)})
+
+    def size(self):
+        return len(self.replay)
+
+    def _iteration(self):
+        """One update iteration on static tensors (train_flock.py:18-43); capturable."""
+        A, B, C = self.A, self.B, self.chunk
+        idx = self.static_idx
+        s = self.replay.gather("s", idx).permute(1, 2, 0, 3)          # [C, A, B, n_obs]
+        a = self.replay.gather("a", idx).permute(1, 2, 0).long()       # [C, A, B]
+        r = self.replay.gather("r", idx).permute(1, 0, 2)             # [C, B, A]
+        s2 = self.replay.gather("s_prime", idx).permute(1, 2, 0, 3)
+        done = self.replay.gather("done", idx).t()                      # [C, B]
+        Pq, Pt = self.train_leaves, self.q.params(target=True)
+        h = torch.zeros((A, B, HX), device=self.device)
+        ht = torch.zeros((A, B, HX), device=self.device)
+        loss = 0
+        for t in range(C):
+            q_out, h = self.q.forward_am(s[t], h, Pq)                    # [A, B, n_act]
+            q_a = q_out.gather(2, a[t].unsqueeze(-1)).squeeze(-1)        # [A, B]
+            sum_q = q_a.sum(dim=0).unsqueeze(1)                          # [B, 1]
+            with torch.no_grad():
+                qp, ht = self.q.forward_am(s2[t], ht, Pt)
+                max_q = qp.max(dim=2)[0]                                 # [A, B]
+                target_q = r[t].sum(dim=1, keepdim=True)
+                target_q = target_q + self.gamma * max_q.sum(dim=0).unsqueeze(1) * (1 - done[t]).unsqueeze(1)
+            loss = loss + F.smooth_l1_loss(sum_q, target_q)
+            keep = (done[t] == 0).view(1, B, 1)                          # hidden[done_mask] = 0 (:36-38)
+            h = torch.where(keep, h, torch.zeros((), device=self.device))
+            ht = torch.where(keep, ht, torch.zeros((), device=self.device))
+        self.q.P.grad.zero_()
+        torch.autograd.backward(loss, inputs=list(Pq.values()))
+        scale = self.norm(self.q.P.grad, self.grad_clip_norm)           # clip_grad_norm_(5) (:42)
+        self.q.P.adam_step_dev(self.lr, grad_scale=scale[1:])          # Adam (:43)
+        with torch.no_grad():
+            self.loss.copy_(loss.detach())
+
+    def sample_starts(self):
+        n = len(self.replay)
+        return torch.randint(0, n - self.chunk, (self.B,), device=self.device, generator=self.gen)
+
+    def train(self, starts=None):
+        """train(q, q_target, memory, optimizer, gamma, batch_size, update_iter, chunk_size) for every agent at
+        once. starts: optional [update_iter, B] logical chunk starts (parity tests); returns the last loss."""
+        n = len(self.replay)
+        base = self.replay.counter - n  # logical index 0 = oldest row still in the ring
+        ar = torch.arange(self.chunk, device=self.device)
+        for it in range(self.update_iter):
+            st = self.sample_starts() if starts is None else torch.as_tensor(starts[it], device=self.device)
+            self.static_idx.copy_((base + st[:, None] + ar[None, :]) % self.replay.capacity)
+            if self.use_graph:
+                if self.graph is None:
+                    self.graph = capture_graph(self._iteration, self.device,
+                                               self.q.P.state_tensors() + [self.loss, self.norm.out])
+                self.graph.replay()
+            else:
+                self._iteration()
+        return self.loss

@@ -83,3 +83,45 @@ def test_shared_critic_choose_action_batched(cuda):
         torch.testing.assert_close(mu[:, i], ref, rtol=1e-5, atol=1e-6)
     a = L.choose_action(obs)
     assert a.shape == (7, 5, 2) and not torch.equal(a, mu)
+
+
+@pytest.mark.parametrize("use_graph", [False, True], ids=["eager", "hipgraph"])
+def test_vdn_train_matches_reference(use_graph, cuda):
+    from marl_range_flocking_amd.learners.vdn import VDNLearner, reference_key
+
+    z = np.load(os.path.join(GOLD, "learn_vdn.npz"))
+    m = json.loads(str(z["meta"]))
+    A = m["n_agents"]
+    L = VDNLearner(A, m["k"], m["n_actions"], lr=m["lr"], gamma=m["gamma"], batch_size=m["batch"],
+                   chunk_size=m["chunk"], update_iter=m["update_iter"], grad_clip_norm=m["grad_clip_norm"],
+                   device=cuda, use_graph=use_graph)
+    L.q.load_reference_state_dict(_sd(z, "init_q"))
+    L.q.load_reference_state_dict(_sd(z, "init_target"), target=True)
+    # QNet forward (net.py:27-37) on the fixture batch
+    qo, ho = L.q(torch.tensor(z["fwd_obs"], device=cuda), torch.tensor(z["fwd_hidden"], device=cuda))
+    L.q.load_reference_state_dict(_sd(z, "init_q"))
+    for t in range(m["T"]):
+        L.put(z["s"][t], z["a"][t], z["r"][t], z["s_prime"][t], [int(z["done"][t])])
+    L.train(starts=z["starts"])
+    norm = L.norm.out[0].item()
+    np.testing.assert_allclose(norm, z["norms"][-1], rtol=1e-4)
+    final = L.q.state_dict()
+    for name in L.q.P.shapes:
+        for i in range(A):
+            key = reference_key(name, i)
+            grads = [z[f"grad{it}/{key}"] for it in range(m["update_iter"])]
+            _masked_close(final[key].numpy(), z[f"final_q/{key}"], grads, key, m["lr"])
+
+
+def test_vdn_forward_matches_reference_qnet(cuda):
+    from marl_range_flocking_amd.learners.vdn import BatchedQNet
+
+    z = np.load(os.path.join(GOLD, "learn_vdn.npz"))
+    m = json.loads(str(z["meta"]))
+    q = BatchedQNet(m["n_agents"], m["k"], m["n_actions"], device=cuda)
+    q.load_reference_state_dict(_sd(z, "final_q"))
+    qo, ho = q(torch.tensor(z["fwd_obs"], device=cuda), torch.tensor(z["fwd_hidden"], device=cuda))
+    np.testing.assert_allclose(qo.detach().cpu().numpy(), z["fwd_q"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(ho.detach().cpu().numpy(), z["fwd_h"], rtol=1e-4, atol=1e-5)
+    a, h = q.sample_action(torch.tensor(z["fwd_obs"], device=cuda), torch.tensor(z["fwd_hidden"], device=cuda), 0.0)
+    np.testing.assert_array_equal(a.cpu().numpy(), z["fwd_q"].argmax(-1).astype(np.float32))
