@@ -1,0 +1,316 @@
+"""MADDPG learners (reference: learners/maddpg_official_rnn/ and learners/maddpg_official/), batched over agents.
+
+Reference behaviour kept:
+  * networks (maddpg_official_rnn/net.py:14-146; maddpg_official/net.py:14-115): RNN actor fce(k->32)-GRUCell(32)-
+    fc1-ReLU-fc2-ReLU-[(tanh(linear)+1)/2, 1.5 tanh(angular)]; RNN critic fce(N*k->32)-GRUCell-fc1-ReLU-
+    fc2([h, a_1..a_N])-ReLU-fc3; feed-forward variants without fce/GRU and a tanh actor head; fanin_init on fc1/fc2
+    (U(+-1/sqrt(size[0]))), heads U(+-3e-3), everything else the torch defaults;
+  * SuperAgent.train() (rnn MADDPG.py:78-150, ff MADDPG.py:67-108): per agent y_i = r_i + gamma Q'_i(s', mu'(s'))
+    (1 - d_i) on the last chunk step, critic MSE, actor loss -mean Q_i(s, mu(s).detach()) with the critic hidden state
+    AFTER the last step (Q8); the detach means the actors never receive a gradient (Q6): their Adam steps are no-ops
+    and they stay bitwise frozen, while the actor loss does add to the critic gradient; hidden states reset to zero
+    where an agent is done; Adam(3e-3) on each critic; soft updates t*(1-tau) + p*tau of both targets;
+  * the replay's raw ``actors_action.reshape(B, C, 2N)`` of an [N, B, C, 2] tensor (MADDPG.py:86; ff :75), which
+    interleaves agents and batch rows, is reproduced (``reference_action_layout=True``) for parity;
+  * ReplayBufferMaddpg (memory_rnn.py:8-99; memory.py:8-99): rows at counter % capacity; minibatch starts drawn
+    without replacement from [0, min(counter, capacity) - chunk); chunks are physical row runs (no wrap);
+  * OrnsteinUhlenbeckProcess (utils.py:32-55): ONE process shared by all agents and sampled agent after agent (Q9).
+What changes: all N actors / critics / targets are stacked [N, ...] slices of flat buffers; every layer of every
+agent is one batched GEMM; the GRU elementwise work is flock_gru_fwd/bwd; the N critic Adam steps + target critic
+soft updates are ONE flock_adam_step launch; the update replays as one HIP graph; the N sequential OU samples are a
+closed-form prefix scan.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell
+
+HR = 32  # hidden_rnn (net.py:15,100)
+
+
+def actor_shapes(k, h1, h2, recurrent, n_actions=2):
+    if recurrent:
+        return {"fce.weight": (HR, k), "fce.bias": (HR,), "gru.weight_ih": (3 * HR, HR), "gru.weight_hh": (3 * HR, HR),
+                "gru.bias_ih": (3 * HR,), "gru.bias_hh": (3 * HR,), "fc1.weight": (h1, HR), "fc1.bias": (h1,),
+                "fc2.weight": (h2, h1), "fc2.bias": (h2,), "linear_speed.weight": (1, h2), "linear_speed.bias": (1,),
+                "angular_speed.weight": (1, h2), "angular_speed.bias": (1,)}
+    return {"fc1.weight": (h1, k), "fc1.bias": (h1,), "fc2.weight": (h2, h1), "fc2.bias": (h2,),
+            "fc3.weight": (n_actions, h2), "fc3.bias": (n_actions,)}
+
+
+def critic_shapes(n_agents, k, h1, h2, recurrent, n_actions=2):
+    s = {}
+    if recurrent:
+        s.update({"fce.weight": (HR, n_agents * k), "fce.bias": (HR,), "gru.weight_ih": (3 * HR, HR),
+                  "gru.weight_hh": (3 * HR, HR), "gru.bias_ih": (3 * HR,), "gru.bias_hh": (3 * HR,),
+                  "fc1.weight": (h1, HR), "fc1.bias": (h1,)})
+    else:
+        s.update({"fc1.weight": (h1, n_agents * k), "fc1.bias": (h1,)})
+    s.update({"fc2.weight": (h2, h1 + n_actions * n_agents), "fc2.bias": (h2,), "fc3.weight": (1, h2),
+              "fc3.bias": (1,)})
+    return s
+
+
+def _init(fp, generator):
+    """fanin_init (net.py:9-12) on fc1/fc2 weights, U(+-3e-3) on head weights, torch defaults elsewhere."""
+    with torch.no_grad():
+        for name, shp in fp.shapes.items():
+            layer, kind = name.split(".")
+            if layer == "gru":
+                b = 1.0 / math.sqrt(HR)
+                fp.view(fp.data, name).uniform_(-b, b, generator=generator)
+                continue
+            w = fp.shapes[layer + ".weight"]
+            if kind == "weight" and layer in ("fc1", "fc2"):
+                b = 1.0 / math.sqrt(w[0])
+            elif kind == "weight" and layer in ("fc3", "linear_speed", "angular_speed"):
+                b = 3e-3
+            else:
+                b = 1.0 / math.sqrt(w[1])
+            fp.view(fp.data, name).uniform_(-b, b, generator=generator)
+
+
+def actor_forward(P, x, h, recurrent):
+    """x [A,B,k], h [A,B,32] -> actions [A,B,2], h'."""
+    if recurrent:
+        y = gru_cell(blinear(x, P["fce.weight"], P["fce.bias"]), h, P["gru.weight_ih"], P["gru.weight_hh"],
+                     P["gru.bias_ih"], P["gru.bias_hh"])
+        h = y
+        y = F.relu(blinear(y, P["fc1.weight"], P["fc1.bias"]))
+        y = F.relu(blinear(y, P["fc2.weight"], P["fc2.bias"]))
+        lin = (torch.tanh(blinear(y, P["linear_speed.weight"], P["linear_speed.bias"])) + 1) / 2  # :65-66
+        ang = torch.tanh(blinear(y, P["angular_speed.weight"], P["angular_speed.bias"])) * 1.5       # :69-70
+        return torch.cat([lin, ang], dim=-1), h
+    y = F.relu(blinear(x, P["fc1.weight"], P["fc1.bias"]))
+    y = F.relu(blinear(y, P["fc2.weight"], P["fc2.bias"]))
+    return torch.tanh(blinear(y, P["fc3.weight"], P["fc3.bias"])), h
+
+
+def critic_forward(P, x, a, h, recurrent, h1):
+    """x [B, N*k] and a [B, 2N] shared by every agent's critic; h [A,B,32] -> q [A,B,1], h'.
+    fc2(cat([out, a])) is computed as out @ W[:, :h1]^T + a @ W[:, h1:]^T + b (same math, no [A,B,h1+2N] concat)."""
+    if recurrent:
+        y = gru_cell(blinear(x, P["fce.weight"], P["fce.bias"]), h, P["gru.weight_ih"], P["gru.weight_hh"],
+                     P["gru.bias_ih"], P["gru.bias_hh"])
+        h = y
+        y = F.relu(blinear(y, P["fc1.weight"], P["fc1.bias"]))
+    else:
+        y = F.relu(blinear(x, P["fc1.weight"], P["fc1.bias"]))
+    W = P["fc2.weight"]
+    z = blinear(y, W[:, :, :h1], P["fc2.bias"]) + blinear(a, W[:, :, h1:])
+    return blinear(F.relu(z), P["fc3.weight"], P["fc3.bias"]), h
+
+
+class SharedOU:
+    """OrnsteinUhlenbeckProcess shared by all agents, sampled agent after agent (utils.py:32-55, MADDPG.py:18,29),
+    for E independent envs at once: the N sequential samples are a closed-form prefix scan (float64)."""
+
+    def __init__(self, size, theta, mu, sigma, sigma_min, dt, device, generator, n_steps_annealing=1000,
+                 anneal_per_sample=False):
+        self.size, self.theta, self.mu, self.dt = size, theta, mu, dt
+        self.sigma, self.sigma_min = sigma, sigma_min
+        self.m = -float(sigma - sigma_min) / float(n_steps_annealing) if sigma_min is not None else 0.0
+        self.c = sigma
+        self.n_steps = 0
+        self.sample_sigma = sigma
+        self.anneal_per_sample = anneal_per_sample  # maddpg_official samples with current_sigma and n_steps += 1
+        self.device, self.gen = device, generator
+        self.x = None
+
+    @property
+    def current_sigma(self):
+        smin = self.sigma_min if self.sigma_min is not None else self.sigma
+        return max(smin, self.m * float(self.n_steps) + self.c)
+
+    def reset_states(self):
+        self.x = None
+
+    def update_sigma(self):
+        self.sample_sigma = self.current_sigma
+        self.n_steps += 1
+
+    def sample(self, n, envs=1):
+        """n sequential samples for each of ``envs`` processes -> [envs, n, size]."""
+        if self.x is None or self.x.shape[0] != envs:
+            self.x = torch.zeros((envs, self.size), dtype=torch.float64, device=self.device)
+        a = 1.0 - self.theta * self.dt
+        if self.anneal_per_sample:
+            sig = torch.tensor([self.current_sigma] * n, dtype=torch.float64, device=self.device)
+            self.n_steps += n
+        else:
+            sig = torch.full((n,), self.sample_sigma, dtype=torch.float64, device=self.device)
+        z = torch.randn((envs, n, self.size), generator=self.gen, device=self.device).double()
+        b = self.theta * self.mu * self.dt + sig.view(1, n, 1) * math.sqrt(self.dt) * z
+        j = torch.arange(1, n + 1, dtype=torch.float64, device=self.device).view(1, n, 1)
+        u = torch.cumsum(b * a ** (-j), dim=1)
+        x = a ** j * (self.x[:, None, :] + u)
+        self.x = x[:, -1]
+        return x.float()
+
+
+class MADDPGLearner:
+    """SuperAgent (both flavours) for N agents: batched acting, device replay, one-launch updates."""
+
+    def __init__(self, n_agents, k, recurrent=True, n_actions=2, hidden1=400, hidden2=300, actor_lr=3e-3,
+                 critic_lr=3e-3, gamma=0.99, tau=0.001, batch_size=128, chunk_size=10, buffer_capacity=45_000,
+                 min_size_buffer=8_000, ou_theta=0.15, ou_mu=0.0, ou_sigma=0.2, ou_sigma_min=0.001, device="cuda",
+                 seed=0, use_graph=True, reference_action_layout=True):
+        self.device = torch.device(device)
+        self.gen = torch.Generator(device=self.device).manual_seed(seed)
+        self.N, self.k, self.recurrent, self.h1 = n_agents, k, recurrent, hidden1
+        self.actor_lr, self.critic_lr, self.gamma, self.tau = actor_lr, critic_lr, gamma, tau
+        self.B, self.C = batch_size, (chunk_size if recurrent else 1)
+        self.min_size_buffer = min_size_buffer
+        self.reference_action_layout = reference_action_layout
+        self.actors = FlatParams(actor_shapes(k, hidden1, hidden2, recurrent, n_actions), self.device, n_agents,
+                                 target=True, adam=False)  # the actors never get a gradient (Q6)
+        self.critics = FlatParams(critic_shapes(n_agents, k, hidden1, hidden2, recurrent, n_actions), self.device,
+                                  n_agents, target=True)
+        _init(self.actors, self.gen)
+        _init(self.critics, self.gen)
+        self.actors.hard_update_target()    # agent.py:37-38
+        self.critics.hard_update_target()
+        self.replay = ReplayRing(buffer_capacity, {
+            "state": (n_agents, k), "next_state": (n_agents, k), "actor_state": (n_agents, k),
+            "actor_next_state": (n_agents, k), "action": (n_agents, n_actions), "reward": (n_agents,),
+            "done": (n_agents,)}, self.device)
+        self.n_games = 0
+        self.random_process = SharedOU(n_actions, ou_theta, ou_mu, ou_sigma, ou_sigma_min if recurrent else None,
+                                       1e-2, self.device, self.gen, anneal_per_sample=not recurrent)
+        self.critic_leaves = self.critics.new_leaves()
+        self.static_idx = torch.zeros((self.B, self.C), dtype=torch.int64, device=self.device)
+        self.losses = torch.zeros(2, device=self.device)
+        self.use_graph = use_graph
+        self.graph = None
+
+    # ---------------------------------------------------------------- acting
+    def init_hidden(self, envs=1):
+        return torch.zeros((self.N, envs, HR), device=self.device)
+
+    @torch.no_grad()
+    def get_actions(self, actor_states, hidden=None, test=False):
+        """actor_states [N, k] (one env) or [E, N, k]; hidden [N, E, 32] -> (actions like actor_states[..., :2],
+        hidden'). Noise: the shared OU process, sampled agent after agent (agent.py:53-64)."""
+        single = actor_states.dim() == 2
+        x = actor_states.reshape(-1, self.N, self.k).transpose(0, 1)  # [N, E, k]
+        E = x.shape[1]
+        if hidden is None:
+            hidden = self.init_hidden(E)
+        P = {n: self.actors.view(self.actors.data, n) for n in self.actors.shapes}
+        mu, h = actor_forward(P, x, hidden, self.recurrent)
+        mu = mu.transpose(0, 1)  # [E, N, 2]
+        if not test:
+            mu = mu + self.random_process.sample(self.N, E)
+        return (mu[0] if single else mu), h
+
+    def reset_random_process(self):
+        self.random_process.reset_states()
+
+    def update_random_process(self):
+        self.random_process.update_sigma()
+
+    # ---------------------------------------------------------------- replay
+    @property
+    def buffer_counter(self):
+        return self.replay.counter
+
+    def check_buffer_size(self):
+        return self.replay.counter >= self.B and self.replay.counter >= self.min_size_buffer
+
+    def add_record(self, actor_states, actor_next_states, actions, state, next_state, reward, done):
+        """ReplayBufferMaddpg.add_record (memory_rnn.py:53-67); a leading env dim stores one record per env."""
+        st = torch.as_tensor(state, device=self.device, dtype=torch.float32)
+        n = 1 if st.dim() == 2 else st.shape[0]
+        f = lambda t, *shape: torch.as_tensor(t, device=self.device, dtype=torch.float32).reshape(n, *shape)  # noqa
+        N, k = self.N, self.k
+        self.replay.store({"state": f(state, N, k), "next_state": f(next_state, N, k),
+                           "actor_state": f(actor_states, N, k), "actor_next_state": f(actor_next_states, N, k),
+                           "action": f(actions, N, 2), "reward": f(reward, N), "done": f(done, N)})
+
+    # ---------------------------------------------------------------- update
+    def _update(self):
+        N, B, C, k, h1 = self.N, self.B, self.C, self.k, self.h1
+        idx = self.static_idx
+        S = self.replay.gather("state", idx).reshape(B, C, N * k)
+        S2 = self.replay.gather("next_state", idx).reshape(B, C, N * k)
+        AS = self.replay.gather("actor_state", idx).permute(2, 1, 0, 3)        # [N, C, B, k]
+        AS2 = self.replay.gather("actor_next_state", idx).permute(2, 1, 0, 3)
+        act = self.replay.gather("action", idx)                                 # [B, C, N, 2]
+        if self.reference_action_layout:  # actors_action [N,B,C,2].reshape(B,C,2N) (MADDPG.py:86)
+            act = act.permute(2, 0, 1, 3).contiguous().reshape(B, C, 2 * N)
+        else:
+            act = act.reshape(B, C, 2 * N)
+        R = self.replay.gather("reward", idx)                                   # [B, C, N]
+        D = self.replay.gather("done", idx)
+        Pa = {n: self.actors.view(self.actors.data, n) for n in self.actors.shapes}
+        Pta = {n: self.actors.view(self.actors.target, n) for n in self.actors.shapes}
+        Ptc = {n: self.critics.view(self.critics.target, n) for n in self.critics.shapes}
+        Pc = self.critic_leaves
+        rec = self.recurrent
+        zero = lambda: torch.zeros((N, B, HR), device=self.device)  # noqa: E731
+        h_ta, h_tc, h_c, h_a = zero(), zero(), zero(), zero()
+        for t in range(C):
+            with torch.no_grad():
+                ta, h_ta = actor_forward(Pta, AS2[:, t], h_ta, rec)
+                cta = ta.transpose(0, 1).reshape(B, 2 * N)                       # torch.cat(..., dim=1)
+                tq, h_tc = critic_forward(Ptc, S2[:, t], cta, h_tc, rec, h1)
+            q, h_c = critic_forward(Pc, S[:, t], act[:, t], h_c, rec, h1)
+            with torch.no_grad():
+                pa, h_a = actor_forward(Pa, AS[:, t], h_a, rec)
+                cpa = pa.transpose(0, 1).reshape(B, 2 * N)
+            if rec:  # hidden[done_mask[:, i]] = 0 for the four hidden lists (MADDPG.py:117-132)
+                keep = (D[:, t] == 0).t().unsqueeze(-1)                         # [N, B, 1]
+                h_ta = torch.where(keep, h_ta, 0.0)
+                h_tc = torch.where(keep, h_tc, 0.0)
+                h_c = torch.where(keep, h_c, 0.0)
+                h_a = torch.where(keep, h_a, 0.0)
+        r = R[:, C - 1].t().unsqueeze(-1)
+        d = D[:, C - 1].t().unsqueeze(-1)
+        target = r + self.gamma * tq * (1 - d)                                  # MADDPG.py:135
+        critic_loss = ((target - q) ** 2).mean(dim=(1, 2))                      # F.mse_loss per agent (:136)
+        aq, _ = critic_forward(Pc, S[:, C - 1], cpa, h_c, rec, h1)              # (:137) hidden after the last step
+        actor_loss = -aq.mean(dim=(1, 2))
+        self.critics.grad.zero_()
+        torch.autograd.backward(critic_loss.sum() + actor_loss.sum(), inputs=list(Pc.values()))
+        # critic_optimizer.step() + update_target_networks() (:148-150): one launch for all agents
+        self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
+        self.actors.soft_update(self.tau, mode=0)                               # target actor (actor unchanged)
+        with torch.no_grad():
+            self.losses[0].copy_(critic_loss.detach().mean())
+            self.losses[1].copy_(actor_loss.detach().mean())
+
+    def train(self, starts=None):
+        """SuperAgent.train(): one update of every agent. starts: optional [B] physical chunk starts (parity)."""
+        if not self.check_buffer_size():
+            return None
+        rng = min(self.replay.counter, self.replay.capacity)
+        hi = rng - self.C if self.recurrent else rng
+        if starts is None:  # np.random.choice(hi, B, replace=False)
+            starts = torch.randperm(hi, device=self.device, generator=self.gen)[:self.B]
+        starts = torch.as_tensor(starts, device=self.device)
+        self.static_idx.copy_(starts[:, None] + torch.arange(self.C, device=self.device)[None])
+        if self.use_graph:
+            if self.graph is None:
+                self.graph = capture_graph(self._update, self.device,
+                                           self.critics.state_tensors() + self.actors.state_tensors()
+                                           + [self.losses])
+            self.graph.replay()
+        else:
+            self._update()
+        return self.losses
+
+    # ---------------------------------------------------------------- state dicts (reference names)
+    def load_reference_state(self, sds):
+        """sds: {"actor{i}"|"critic{i}"|"target_actor{i}"|"target_critic{i}": state_dict}."""
+        for key, sd in sds.items():
+            net = "actor" if "actor" in key else "critic"
+            i = int(key[len(key.rstrip("0123456789")):])
+            fp = self.actors if net == "actor" else self.critics
+            for n, v in sd.items():
+                fp.load(n, v, agent=i, target=key.startswith("target"))
+
+    def state_dict(self, net, i, target=False):
+        fp = self.actors if net == "actor" else self.critics
+        return {n: fp.export(n, i, target=target).cpu() for n in fp.shapes}

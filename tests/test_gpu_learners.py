@@ -125,3 +125,56 @@ def test_vdn_forward_matches_reference_qnet(cuda):
     np.testing.assert_allclose(ho.detach().cpu().numpy(), z["fwd_h"], rtol=1e-4, atol=1e-5)
     a, h = q.sample_action(torch.tensor(z["fwd_obs"], device=cuda), torch.tensor(z["fwd_hidden"], device=cuda), 0.0)
     np.testing.assert_array_equal(a.cpu().numpy(), z["fwd_q"].argmax(-1).astype(np.float32))
+
+
+@pytest.mark.parametrize("flavour", ["rnn", "ff"])
+@pytest.mark.parametrize("use_graph", [False, True], ids=["eager", "hipgraph"])
+def test_maddpg_train_matches_reference(flavour, use_graph, cuda):
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+    z = np.load(os.path.join(GOLD, f"learn_maddpg_{flavour}.npz"))
+    m = json.loads(str(z["meta"]))
+    N = m["n_agents"]
+    L = MADDPGLearner(N, m["k"], recurrent=flavour == "rnn", hidden1=m["hidden1"], hidden2=m["hidden2"],
+                      batch_size=m["batch"], chunk_size=m["chunk"], buffer_capacity=m["capacity"],
+                      min_size_buffer=m["batch"], device=cuda, use_graph=use_graph)
+    nets = ("actor", "critic", "target_actor", "target_critic")
+    L.load_reference_state({f"{nm}{i}": _sd(z, f"init/{nm}{i}") for i in range(N) for nm in nets})
+    for t in range(m["T"]):
+        L.add_record(z["obs"][t], z["obs"][t + 1], z["action"][t], z["obs"][t], z["obs"][t + 1], z["reward"][t],
+                     z["done"][t])
+    assert L.train(starts=z["starts"]) is not None
+    for i in range(N):
+        for n, v in L.state_dict("actor", i).items():  # frozen actors (Q6): bitwise unchanged
+            np.testing.assert_array_equal(v.numpy(), z[f"final/actor{i}/{n}"])
+        for n, v in L.state_dict("actor", i, target=True).items():  # t*(1-tau) + a*tau, same op order
+            np.testing.assert_array_equal(v.numpy(), z[f"final/target_actor{i}/{n}"])
+        for n, v in L.state_dict("critic", i).items():
+            g = [z[f"grad/critic{i}/{n}"]]
+            _masked_close(v.numpy(), z[f"final/critic{i}/{n}"], g, f"critic{i} {n}", m["lr"])
+        for n, v in L.state_dict("critic", i, target=True).items():
+            g = [z[f"grad/critic{i}/{n}"]]
+            _masked_close(v.numpy(), z[f"final/target_critic{i}/{n}"], g, f"target_critic{i} {n}", m["lr"])
+    # acting without noise (agent.choose_action, test=True)
+    obs0 = torch.tensor(z["obs"][0], device=cuda)
+    acts, hid = L.get_actions(obs0, None, test=True)
+    np.testing.assert_allclose(acts.cpu().numpy(), z["act_out"], rtol=1e-5, atol=1e-6)
+    if flavour == "rnn":
+        np.testing.assert_allclose(hid[:, 0].cpu().numpy(), z["act_hidden"], rtol=1e-5, atol=1e-6)
+
+
+def test_shared_ou_matches_sequential_process(cuda):
+    """The closed-form scan equals the reference's agent-after-agent OU recurrence (utils.py:43-47)."""
+    from marl_range_flocking_amd.learners.maddpg import SharedOU
+
+    g = torch.Generator(device=cuda).manual_seed(0)
+    ou = SharedOU(2, 0.15, 0.0, 0.2, 0.001, 1e-2, cuda, g)
+    xs = ou.sample(64, envs=3)
+    g2 = torch.Generator(device=cuda).manual_seed(0)
+    z = torch.randn((3, 64, 2), generator=g2, device=cuda).double()
+    x = torch.zeros(3, 2, dtype=torch.float64, device=cuda)
+    ref = []
+    for i in range(64):
+        x = x + 0.15 * (0.0 - x) * 1e-2 + 0.2 * np.sqrt(1e-2) * z[:, i]
+        ref.append(x)
+    torch.testing.assert_close(xs, torch.stack(ref, 1).float(), rtol=1e-5, atol=1e-7)
