@@ -25,6 +25,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from .. import dist
 from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell
 
 HR = 32  # hidden_rnn (net.py:15,100)
@@ -156,7 +157,7 @@ class MADDPGLearner:
     def __init__(self, n_agents, k, recurrent=True, n_actions=2, hidden1=400, hidden2=300, actor_lr=3e-3,
                  critic_lr=3e-3, gamma=0.99, tau=0.001, batch_size=128, chunk_size=10, buffer_capacity=45_000,
                  min_size_buffer=8_000, ou_theta=0.15, ou_mu=0.0, ou_sigma=0.2, ou_sigma_min=0.001, device="cuda",
-                 seed=0, use_graph=True, reference_action_layout=True):
+                 seed=0, use_graph=True, reference_action_layout=True, dist_group=None):
         self.device = torch.device(device)
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.N, self.k, self.recurrent, self.h1 = n_agents, k, recurrent, hidden1
@@ -184,6 +185,11 @@ class MADDPGLearner:
         self.losses = torch.zeros(2, device=self.device)
         self.use_graph = use_graph
         self.graph = None
+        self.group = dist_group
+        self.distributed = dist.active(dist_group)
+        if self.distributed:
+            dist.sync_params(self.actors, group=dist_group)
+            dist.sync_params(self.critics, group=dist_group)
 
     # ---------------------------------------------------------------- acting
     def init_hidden(self, envs=1):
@@ -231,6 +237,10 @@ class MADDPGLearner:
 
     # ---------------------------------------------------------------- update
     def _update(self):
+        self._fwd_bwd()
+        self._step()
+
+    def _fwd_bwd(self):
         N, B, C, k, h1 = self.N, self.B, self.C, self.k, self.h1
         idx = self.static_idx
         S = self.replay.gather("state", idx).reshape(B, C, N * k)
@@ -274,12 +284,14 @@ class MADDPGLearner:
         actor_loss = -aq.mean(dim=(1, 2))
         self.critics.grad.zero_()
         torch.autograd.backward(critic_loss.sum() + actor_loss.sum(), inputs=list(Pc.values()))
-        # critic_optimizer.step() + update_target_networks() (:148-150): one launch for all agents
-        self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
-        self.actors.soft_update(self.tau, mode=0)                               # target actor (actor unchanged)
         with torch.no_grad():
             self.losses[0].copy_(critic_loss.detach().mean())
             self.losses[1].copy_(actor_loss.detach().mean())
+
+    def _step(self):
+        # critic_optimizer.step() + update_target_networks() (:148-150): one launch for all agents
+        self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
+        self.actors.soft_update(self.tau, mode=0)                               # target actor (actor unchanged)
 
     def train(self, starts=None):
         """SuperAgent.train(): one update of every agent. starts: optional [B] physical chunk starts (parity)."""
@@ -291,14 +303,17 @@ class MADDPGLearner:
             starts = torch.randperm(hi, device=self.device, generator=self.gen)[:self.B]
         starts = torch.as_tensor(starts, device=self.device)
         self.static_idx.copy_(starts[:, None] + torch.arange(self.C, device=self.device)[None])
+        fn = self._fwd_bwd if self.distributed else self._update
         if self.use_graph:
             if self.graph is None:
-                self.graph = capture_graph(self._update, self.device,
-                                           self.critics.state_tensors() + self.actors.state_tensors()
-                                           + [self.losses])
+                self.graph = capture_graph(fn, self.device, self.critics.state_tensors()
+                                           + self.actors.state_tensors() + [self.losses])
             self.graph.replay()
         else:
-            self._update()
+            fn()
+        if self.distributed:  # critic-only all-reduce (the actors get no gradient, Q6), one bucket
+            dist.allreduce_mean_(self.critics.grad, self.group)
+            self._step()
         return self.losses
 
     # ---------------------------------------------------------------- state dicts (reference names)

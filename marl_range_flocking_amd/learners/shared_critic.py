@@ -17,6 +17,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from .. import dist
 from .core import FlatParams, ReplayRing, blayer_norm, blinear, capture_graph
 
 
@@ -74,7 +75,7 @@ def _init_mlp(fp, names_uniform, generator):
 class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
-                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True):
+                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -101,6 +102,12 @@ class SharedCriticLearner:
         self.graph = None
         self.critic_leaves = self.critic.new_leaves()
         self.scratch_leaves = self.scratch.new_leaves()
+        self.group = dist_group
+        self.distributed = dist.active(dist_group)
+        self.graphs = None
+        if self.distributed:
+            dist.sync_params(self.critic, group=dist_group)
+            dist.sync_params(self.actors, group=dist_group)
 
     # ------------------------------------------------------------------ acting
     def _stacked(self, fp, target=False):
@@ -144,17 +151,21 @@ class SharedCriticLearner:
 
     # ------------------------------------------------------------------ learning
     def _update(self):
-        """One Agent.learn() body on static tensors (agent_simple_shared_critic.py:118-150) for the actor in the
-        scratch slot; capturable."""
+        self._critic_phase()
+        self._critic_step()
+        self._actor_phase()
+        self._actor_step()
+
+    def _critic_phase(self):
+        """Sample, targets and critic backward (agent_simple_shared_critic.py:118-140); capturable."""
         B = self.batch_size
         idx = self.static_idx
-        state = self.replay.gather("state", idx)
+        self._state = state = self.replay.gather("state", idx)
         action = self.replay.gather("action", idx)
         reward = self.replay.gather("reward", idx)
         new_state = self.replay.gather("new_state", idx)
         terminal = self.replay.gather("terminal", idx)
         C = self.critic_leaves
-        S = self.scratch_leaves
         tgt = {n: self.scratch.view(self.scratch.target, n) for n in self.scratch.shapes}
         with torch.no_grad():
             target_actions = actor_forward(tgt, new_state)                    # :126
@@ -164,15 +175,45 @@ class SharedCriticLearner:
         q = critic_forward(C, state, action)[0]                               # :128
         critic_loss = F.mse_loss(target, q)                                   # :139
         torch.autograd.backward(critic_loss, inputs=list(C.values()))
+        with torch.no_grad():
+            self.losses[1].copy_(critic_loss.detach())
+
+    def _critic_step(self):
         self.critic.adam_step_dev(self.beta)                                  # :141
+
+    def _actor_phase(self):
+        """Actor loss through the UPDATED critic and its backward (:144-149); capturable."""
+        C, S = self.critic_leaves, self.scratch_leaves
         self.scratch.grad.zero_()                                             # :144
-        mu = actor_forward(S, state)                                          # :145
-        actor_loss = torch.mean(-critic_forward(C, state, mu))                # :147-148
+        mu = actor_forward(S, self._state)                                    # :145
+        actor_loss = torch.mean(-critic_forward(C, self._state, mu))          # :147-148
         torch.autograd.backward(actor_loss, inputs=list(S.values()))
-        self.scratch.adam_step_dev(self.alpha)                                # :150
         with torch.no_grad():
             self.losses[0].copy_(actor_loss.detach())
-            self.losses[1].copy_(critic_loss.detach())
+
+    def _actor_step(self):
+        self.scratch.adam_step_dev(self.alpha)                                # :150
+
+    def _run_update(self):
+        S = self.scratch
+        state = self.critic.state_tensors() + S.state_tensors() + [self.losses]
+        if not self.distributed:
+            if not self.use_graph:
+                return self._update()
+            if self.graph is None:
+                self.graph = capture_graph(self._update, self.device, state)
+            return self.graph.replay()
+        # data-parallel: graph-captured backward phases, RCCL all-reduce of each gradient bucket, identical steps
+        if self.use_graph and self.graphs is None:
+            self._critic_phase()  # materialise self._state before capturing the actor phase
+            self.graphs = (capture_graph(self._critic_phase, self.device, state),
+                           capture_graph(self._actor_phase, self.device, state))
+        (self.graphs[0].replay() if self.use_graph else self._critic_phase())
+        dist.allreduce_mean_(self.critic.grad, self.group)
+        self._critic_step()
+        (self.graphs[1].replay() if self.use_graph else self._actor_phase())
+        dist.allreduce_mean_(S.grad, self.group)
+        self._actor_step()
 
     def learn(self, agent, idx=None):
         """Agent.learn() of agent ``agent`` (agent_simple_shared_critic.py:115-155). Returns (actor_loss,
@@ -191,13 +232,7 @@ class SharedCriticLearner:
                              (A.exp_avg_sq, S.exp_avg_sq)):
                 dst.copy_(src[lo:hi])
             S.step_dev.copy_(self.actor_steps[agent:agent + 1])
-        if self.use_graph:
-            if self.graph is None:
-                self.graph = capture_graph(self._update, self.device,
-                                           self.critic.state_tensors() + S.state_tensors() + [self.losses])
-            self.graph.replay()
-        else:
-            self._update()
+        self._run_update()
         with torch.no_grad():
             for src, dst in ((S.data, A.data), (S.exp_avg, A.exp_avg), (S.exp_avg_sq, A.exp_avg_sq)):
                 dst[lo:hi].copy_(src)
@@ -233,15 +268,17 @@ class SharedCriticBench:
 
     def __init__(self, env, device, seed=0):
         self.env = env
+        group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
-                                           buffer_size=1_000_000)
+                                           buffer_size=1_000_000, dist_group=group)
         self.prev_obs = env.dnn.clone()
         self.prev_act = None
 
     def describe(self):
         return (f"maddpg_shared_critic learn() x1 per vectorized step (B={self.learner.batch_size}, agent = step mod "
                 f"{self.learner.n_agents}; all {self.env.E * self.env.N} transitions inserted into a 1e6-row "
-                f"device replay ring per step)")
+                f"device replay ring per step"
+                + ("; critic + actor gradient all-reduce over RCCL per learn)" if self.learner.distributed else ")"))
 
     def after_env_step(self, s, action):
         env = self.env

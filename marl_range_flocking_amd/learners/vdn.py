@@ -18,6 +18,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from .. import dist
 from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell
 
 HX = 32
@@ -102,7 +103,7 @@ class BatchedQNet:
 class VDNLearner:
     def __init__(self, n_agents, n_obs, n_actions, lr=1e-3, gamma=0.99, batch_size=32, chunk_size=10,
                  update_iter=10, grad_clip_norm=5.0, buffer_limit=50_000, recurrent=True, device="cuda", seed=0,
-                 use_graph=True):
+                 use_graph=True, dist_group=None):
         self.device = torch.device(device)
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.q = BatchedQNet(n_agents, n_obs, n_actions, recurrent, self.device, self.gen)
@@ -120,6 +121,10 @@ class VDNLearner:
         self.use_graph = use_graph
         self.graph = None
         self.train_leaves = self.q.P.new_leaves()
+        self.group = dist_group
+        self.distributed = dist.active(dist_group)
+        if self.distributed:  # identical replicas: rank 0's initial parameters everywhere
+            dist.sync_params(self.q.P, group=dist_group)
 
     def sync_target(self):
         """q_target.load_state_dict(q.state_dict()) (train_flock.py:84, :114-115)."""
@@ -142,7 +147,11 @@ class VDNLearner:
         return len(self.replay)
 
     def _iteration(self):
-        """One update iteration on static tensors (train_flock.py:18-43); capturable."""
+        self._fwd_bwd()
+        self._step()
+
+    def _fwd_bwd(self):
+        """Loss and backward of one update iteration on static tensors (train_flock.py:18-41); capturable."""
         A, B, C = self.A, self.B, self.chunk
         idx = self.static_idx
         s = self.replay.gather("s", idx).permute(1, 2, 0, 3)          # [C, A, B, n_obs]
@@ -169,10 +178,12 @@ class VDNLearner:
             ht = torch.where(keep, ht, torch.zeros((), device=self.device))
         self.q.P.grad.zero_()
         torch.autograd.backward(loss, inputs=list(Pq.values()))
-        scale = self.norm(self.q.P.grad, self.grad_clip_norm)           # clip_grad_norm_(5) (:42)
-        self.q.P.adam_step_dev(self.lr, grad_scale=scale[1:])          # Adam (:43)
         with torch.no_grad():
             self.loss.copy_(loss.detach())
+
+    def _step(self):
+        scale = self.norm(self.q.P.grad, self.grad_clip_norm)           # clip_grad_norm_(5) (:42)
+        self.q.P.adam_step_dev(self.lr, grad_scale=scale[1:])          # Adam (:43)
 
     def sample_starts(self):
         n = len(self.replay)
@@ -187,11 +198,15 @@ class VDNLearner:
         for it in range(self.update_iter):
             st = self.sample_starts() if starts is None else torch.as_tensor(starts[it], device=self.device)
             self.static_idx.copy_((base + st[:, None] + ar[None, :]) % self.replay.capacity)
+            fn = self._fwd_bwd if self.distributed else self._iteration
             if self.use_graph:
                 if self.graph is None:
-                    self.graph = capture_graph(self._iteration, self.device,
+                    self.graph = capture_graph(fn, self.device,
                                                self.q.P.state_tensors() + [self.loss, self.norm.out])
                 self.graph.replay()
             else:
-                self._iteration()
+                fn()
+            if self.distributed:  # one RCCL all-reduce of the whole flat gradient, then identical steps
+                dist.allreduce_mean_(self.q.P.grad, self.group)
+                self._step()
         return self.loss
