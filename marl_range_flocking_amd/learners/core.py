@@ -86,17 +86,39 @@ class FlatParams:
     def __getitem__(self, name):
         return self.params[name]
 
-    def new_leaves(self):
+    def new_leaves(self, squeeze=False):
         """A fresh set of leaf Parameters aliasing the same data/grad storage. Graph-captured updates use their own
         set, so an autograd graph a caller keeps alive on ``params`` (e.g. a grad-enabled forward outside the
         learner) never shares AccumulateGrad nodes with the captured backward (that combination crashed HIP graph
-        capture on ROCm 7.2)."""
+        capture on ROCm 7.2). squeeze (single network): leaves without the agent axis, so no select/unsqueeze
+        (and no zero-fill + copy in their backward) enters the graph."""
         d = OrderedDict()
         for name in self.shapes:
-            p = torch.nn.Parameter(self.view(self.data, name))
-            p.grad = self.view(self.grad, name)
+            v = self.view(self.data, name)
+            g = self.view(self.grad, name)
+            if squeeze:
+                assert self.agents == 1
+                v, g = v[0], g[0]
+            p = torch.nn.Parameter(v)
+            p.grad = g
             d[name] = p
         return d
+
+    def grads_into(self, loss, leaves):
+        """Gradients of ``loss`` w.r.t. ``leaves`` written straight into the flat grad buffer with one multi-tensor
+        copy (instead of zero-fill + one AccumulateGrad add per parameter)."""
+        names = list(leaves)
+        grads = torch.autograd.grad(loss, [leaves[n] for n in names], allow_unused=True)
+        dst, src = [], []
+        for n, g in zip(names, grads):
+            view = leaves[n].grad
+            if g is None:
+                view.zero_()
+            else:
+                dst.append(view)
+                src.append(g)
+        if dst:
+            torch._foreach_copy_(dst, src)
 
     def target_view(self, name, agent=None):
         return self.view(self.target, name, agent)
@@ -200,7 +222,10 @@ class GradNorm:
 
 def blinear(x, W, b=None):
     """Per-agent Linear: x [A,B,in] (or [B,in] shared by all agents), W [A,out,in], b [A,out] -> [A,B,out].
-    A == 1 goes through F.linear (one GEMM with the bias epilogue) instead of a batched GEMM."""
+    A single network (W [out,in]) is a plain F.linear on 2-D activations; A == 1 stacked also goes through F.linear
+    (one GEMM with the bias epilogue) instead of a batched GEMM."""
+    if W.dim() == 2:
+        return torch.nn.functional.linear(x, W, b)
     if W.shape[0] == 1:
         x2 = x if x.dim() == 2 else x[0]
         return torch.nn.functional.linear(x2, W[0], None if b is None else b[0]).unsqueeze(0)
@@ -214,6 +239,8 @@ def blinear(x, W, b=None):
 
 def blayer_norm(x, w, b, eps=1e-5):
     """Per-agent LayerNorm over the last dim: normalise, then w[A,F], b[A,F] affine."""
+    if w.dim() == 1:
+        return torch.nn.functional.layer_norm(x, (x.shape[-1],), w, b, eps=eps)
     if w.shape[0] == 1:  # one network: the fused affine LayerNorm kernel (forward and backward)
         return torch.nn.functional.layer_norm(x, (x.shape[-1],), w[0], b[0], eps=eps)
     y = torch.nn.functional.layer_norm(x, (x.shape[-1],), eps=eps)

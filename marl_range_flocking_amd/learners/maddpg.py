@@ -282,8 +282,7 @@ class MADDPGLearner:
         critic_loss = ((target - q) ** 2).mean(dim=(1, 2))                      # F.mse_loss per agent (:136)
         aq, _ = critic_forward(Pc, S[:, C - 1], cpa, h_c, rec, h1)              # (:137) hidden after the last step
         actor_loss = -aq.mean(dim=(1, 2))
-        self.critics.grad.zero_()
-        torch.autograd.backward(critic_loss.sum() + actor_loss.sum(), inputs=list(Pc.values()))
+        self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc)
         with torch.no_grad():
             self.losses[0].copy_(critic_loss.detach().mean())
             self.losses[1].copy_(actor_loss.detach().mean())

@@ -100,8 +100,8 @@ class SharedCriticLearner:
         self.losses = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.use_graph = use_graph
         self.graph = None
-        self.critic_leaves = self.critic.new_leaves()
-        self.scratch_leaves = self.scratch.new_leaves()
+        self.critic_leaves = self.critic.new_leaves(squeeze=True)
+        self.scratch_leaves = self.scratch.new_leaves(squeeze=True)
         self.group = dist_group
         self.distributed = dist.active(dist_group)
         self.graphs = None
@@ -166,15 +166,14 @@ class SharedCriticLearner:
         new_state = self.replay.gather("new_state", idx)
         terminal = self.replay.gather("terminal", idx)
         C = self.critic_leaves
-        tgt = {n: self.scratch.view(self.scratch.target, n) for n in self.scratch.shapes}
+        tgt = {n: self.scratch.view(self.scratch.target, n)[0] for n in self.scratch.shapes}
         with torch.no_grad():
             target_actions = actor_forward(tgt, new_state)                    # :126
-            q_next = critic_forward(C, new_state, target_actions)[0]          # :127 (target critic == critic)
+            q_next = critic_forward(C, new_state, target_actions)             # :127 (target critic == critic)
             target = reward.view(B, 1) + self.gamma * q_next * terminal.reshape(-1, 1)  # :130
-        self.critic.grad.zero_()                                              # :138
-        q = critic_forward(C, state, action)[0]                               # :128
+        q = critic_forward(C, state, action)                                  # :128
         critic_loss = F.mse_loss(target, q)                                   # :139
-        torch.autograd.backward(critic_loss, inputs=list(C.values()))
+        self.critic.grads_into(critic_loss, C)                                # zero_grad + backward (:138-140)
         with torch.no_grad():
             self.losses[1].copy_(critic_loss.detach())
 
@@ -184,10 +183,9 @@ class SharedCriticLearner:
     def _actor_phase(self):
         """Actor loss through the UPDATED critic and its backward (:144-149); capturable."""
         C, S = self.critic_leaves, self.scratch_leaves
-        self.scratch.grad.zero_()                                             # :144
         mu = actor_forward(S, self._state)                                    # :145
         actor_loss = torch.mean(-critic_forward(C, self._state, mu))          # :147-148
-        torch.autograd.backward(actor_loss, inputs=list(S.values()))
+        self.scratch.grads_into(actor_loss, S)                                # zero_grad + backward (:144-149)
         with torch.no_grad():
             self.losses[0].copy_(actor_loss.detach())
 

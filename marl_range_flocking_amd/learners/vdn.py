@@ -176,8 +176,7 @@ class VDNLearner:
             keep = (done[t] == 0).view(1, B, 1)                          # hidden[done_mask] = 0 (:36-38)
             h = torch.where(keep, h, torch.zeros((), device=self.device))
             ht = torch.where(keep, ht, torch.zeros((), device=self.device))
-        self.q.P.grad.zero_()
-        torch.autograd.backward(loss, inputs=list(Pq.values()))
+        self.q.P.grads_into(loss, Pq)
         with torch.no_grad():
             self.loss.copy_(loss.detach())
 
