@@ -2,8 +2,8 @@
 Euclidean kNN without range clamp, 4-frame observation memory, collision-only reward.
 One HIP launch per step (flock_step_flock, include/flock_amd.h).
 """
-from ..spaces import Box
-from ._base import SingleFlockEnv
+from marl_range_flocking_amd.spaces import Box
+from marl_range_flocking_amd.environments._base import SingleFlockEnv
 
 
 class MultiAgentEnv(SingleFlockEnv):

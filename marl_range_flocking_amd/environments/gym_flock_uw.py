@@ -2,8 +2,8 @@
 Euclidean kNN, 4-frame observation memory (N, 4, k), reward = collision + centre of mass + angular terms.
 One HIP launch per step (flock_step_uw, include/flock_amd.h).
 """
-from ..spaces import Box
-from ._base import SingleFlockEnv
+from marl_range_flocking_amd.spaces import Box
+from marl_range_flocking_amd.environments._base import SingleFlockEnv
 
 
 class MultiAgentEnv(SingleFlockEnv):

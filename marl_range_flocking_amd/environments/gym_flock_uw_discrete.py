@@ -6,8 +6,8 @@ syncs (:329-330) are gone.
 """
 import torch
 
-from ..spaces import Box, Discrete
-from ._base import SingleFlockEnv
+from marl_range_flocking_amd.spaces import Box, Discrete
+from marl_range_flocking_amd.environments._base import SingleFlockEnv
 
 
 class MultiAgentEnv(SingleFlockEnv):

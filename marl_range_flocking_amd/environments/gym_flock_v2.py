@@ -4,8 +4,8 @@ Same constructor, spaces, attributes and step/reset return types; the step runs 
 (flock_step_v2, include/flock_amd.h). ``periodic`` / ``v_min`` select the learners/maddpg_official_rnn fork
 (Euclidean distances, linear-speed floor 0.5) — see gym_flock_v2_rnn.py.
 """
-from ..spaces import Box
-from ._base import SingleFlockEnv
+from marl_range_flocking_amd.spaces import Box
+from marl_range_flocking_amd.environments._base import SingleFlockEnv
 
 
 class MultiAgentEnv(SingleFlockEnv):

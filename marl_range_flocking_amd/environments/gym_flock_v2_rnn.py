@@ -2,7 +2,7 @@
 directory is first on sys.path): step uses Euclidean _computeDistances (:75) and the linear speed is
 clamped to [0.5, max_linear_velocity] (:310). Everything else is gym_flock_v2.
 """
-from . import gym_flock_v2 as _v2
+from marl_range_flocking_amd.environments import gym_flock_v2 as _v2
 
 
 class MultiAgentEnv(_v2.MultiAgentEnv):

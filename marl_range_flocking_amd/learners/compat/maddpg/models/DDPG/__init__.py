@@ -1,0 +1,1 @@
+"""maddpg package shim (reference import paths of learners/maddpg_shared_critic)."""

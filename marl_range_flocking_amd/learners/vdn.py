@@ -126,6 +126,32 @@ class VDNLearner:
         if self.distributed:  # identical replicas: rank 0's initial parameters everywhere
             dist.sync_params(self.q.P, group=dist_group)
 
+    def attach(self, q, q_target, ring, lr=1e-3, gamma=0.99, batch_size=32, chunk_size=10, update_iter=10,
+               grad_clip_norm=5.0, use_graph=True, seed=0):
+        """Build the update engine over EXISTING networks (q, q_target: BatchedQNet) and replay ring — the
+        reference's train(q, q_target, memory, ...) signature (learners/dropin.py)."""
+        self.device = q.device
+        self.gen = torch.Generator(device=self.device).manual_seed(seed)
+        self.q, self.q_target = q, q_target
+        self.A, self.n_obs, self.n_actions = q.n_agents, q.n_obs, q.n_actions
+        self.lr, self.gamma, self.B, self.grad_clip_norm = lr, gamma, batch_size, grad_clip_norm
+        self.chunk = chunk_size if q.recurrent else 1
+        self.update_iter = update_iter
+        self.replay = ring
+        self.norm = GradNorm(self.device)
+        self.static_idx = torch.zeros((batch_size, self.chunk), dtype=torch.int64, device=self.device)
+        self.loss = torch.zeros((), device=self.device)
+        self.use_graph, self.graph = use_graph, None
+        self.train_leaves = q.P.new_leaves()
+        self.group, self.distributed = None, False
+        return self
+
+    def target_params(self):
+        qt = getattr(self, "q_target", None)
+        if qt is None:
+            return self.q.params(target=True)
+        return {n: qt.P.view(qt.P.data, n) for n in qt.P.shapes}
+
     def sync_target(self):
         """q_target.load_state_dict(q.state_dict()) (train_flock.py:84, :114-115)."""
         self.q.P.hard_update_target()
@@ -159,7 +185,7 @@ class VDNLearner:
         r = self.replay.gather("r", idx).permute(1, 0, 2)             # [C, B, A]
         s2 = self.replay.gather("s_prime", idx).permute(1, 2, 0, 3)
         done = self.replay.gather("done", idx).t()                      # [C, B]
-        Pq, Pt = self.train_leaves, self.q.params(target=True)
+        Pq, Pt = self.train_leaves, self.target_params()
         h = torch.zeros((A, B, HX), device=self.device)
         ht = torch.zeros((A, B, HX), device=self.device)
         loss = 0

