@@ -4,7 +4,7 @@
  * Device pointers, sizes, scalars; `stream` is a hipStream_t passed as an opaque pointer. Return 0 or a negative
  * code (flock_learn_last_error() holds the message). They replace, for ALL agents of a learner at once:
  *   flock_adam_step    torch.optim.Adam.step() per agent network (learners/maddpg_official_rnn/agent.py:32-33,
- *                      maddpg_shared_critic/ddpg_network.py:273,347, vdn/train_flock.py:265) fused with the
+ *                      maddpg_shared_critic/ddpg_network.py:53,127, vdn/train_flock.py:265) fused with the
  *                      target soft update (maddpg_official_rnn/net.py:305-309 mode 0,
  *                      maddpg_shared_critic/agent_simple_shared_critic.py:158-185 mode 1)
  *   flock_soft_update  the soft update alone (same two forms)
@@ -53,6 +53,53 @@ int flock_gru_bwd(void* stream, int64_t rows, int H, const float* dhout, const f
 /* gather: dst[r][:] = src[idx[r]][:]; scatter: dst[idx[r]][:] = src[r][:]; rows of `width` floats. */
 int flock_gather_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);
 int flock_scatter_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);
+
+/* Replay insert of n rows into ring rows start .. start+n-1 (mod capacity), every field in ONE launch (replaces the
+ * per-field row copies of ReplayBuffer.store_transitions, maddpg_shared_critic/utils.py:47-54, memory_rnn.py:53-67,
+ * vdn/utils.py:20-29). src: n * width contiguous values; dst: the field's [capacity][width] f32 ring.
+ * kind 0: f32 copy; 1: u8/bool -> 1 - x (the stored "terminal"); 2: u8/bool -> x. At most 8 fields; n <= capacity. */
+typedef struct FlockRingField {
+    const void* src;
+    float* dst;
+    int64_t width;
+    int kind;
+} FlockRingField;
+int flock_ring_store(void* stream, int64_t n, int64_t capacity, int64_t start, int nfields,
+                     const FlockRingField* fields);
+
+/* ---- fused shared-critic DDPG update ------------------------------------------------------------------------
+ * Replaces Agent.learn() of learners/maddpg_shared_critic/agent_simple_shared_critic.py:115-150 (the sample,
+ * target, critic MSE backward + Adam, actor -mean Q backward + Adam) for agent *agent, on the networks of
+ * learners/maddpg_shared_critic/ddpg_network.py:58-70 (critic) and :132-141 (actor). The soft updates
+ * (:152-185) stay separate (flock_soft_update). Parameter buffers are flat f32 in the reference's state_dict order:
+ *   critic: fc1.weight [fc1,in] fc1.bias bn1.weight bn1.bias fc2.weight [fc2,fc1] fc2.bias bn2.weight bn2.bias
+ *           action_value.weight [fc2,na] action_value.bias q.weight [1,fc2] q.bias [1]
+ *   actor:  fc1.weight fc1.bias bn1.weight bn1.bias fc2.weight fc2.bias bn2.weight bn2.bias mu.weight [na,fc2]
+ *           mu.bias [na]; agent a's actor at actors + a * actor_stride (same for grad / moments / target).
+ * Replay rows are read straight from the ring (rows idx[0..B)). workspace: flock_sc_workspace_floats() floats;
+ * counters: 2 zero-initialised uints (kept zero between calls). do_adam = 0 writes the gradients only (data-parallel
+ * callers all-reduce them and run flock_adam_step_dev themselves); step counters are incremented only with do_adam.
+ * Limits: in_dim <= 64, n_actions <= 8, fc1, fc2 <= 1024. losses[0] = actor loss, losses[1] = critic loss. */
+typedef struct FlockScUpdate {
+    int B, in_dim, n_actions, fc1, fc2, do_adam;
+    const int64_t* idx;   /* [B] replay rows */
+    const int64_t* agent; /* device scalar: the learning agent */
+    const float *ring_state, *ring_new_state, *ring_action, *ring_reward, *ring_terminal;
+    float *critic, *critic_grad, *critic_exp_avg, *critic_exp_avg_sq;
+    int64_t* critic_step;
+    float *actors, *actors_grad, *actors_exp_avg, *actors_exp_avg_sq, *actors_target;
+    int64_t* actor_steps; /* [n_agents] */
+    int64_t actor_stride;
+    float* losses;
+    float* workspace;
+    unsigned* counters;
+    float alpha, beta, gamma, beta1, beta2, eps;
+} FlockScUpdate;
+
+int64_t flock_sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2);
+int64_t flock_sc_update_size(void); /* sizeof(FlockScUpdate), for binding checks */
+int flock_sc_critic_update(void* stream, const FlockScUpdate* u); /* :118-141 */
+int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (after the critic update) */
 
 #ifdef __cplusplus
 }

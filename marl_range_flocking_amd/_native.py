@@ -40,7 +40,38 @@ SIGNATURES = {
     "flock_gather_rows": [_c_void_p, ctypes.c_int64, ctypes.c_int64, _c_void_p, _c_void_p, _c_void_p],
     "flock_scatter_rows": [_c_void_p, ctypes.c_int64, ctypes.c_int64, _c_void_p, _c_void_p, _c_void_p],
 }
-RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p}
+
+
+class FlockScUpdate(ctypes.Structure):
+    """Mirror of ``FlockScUpdate`` (include/flock_learn.h): all pointers are device pointers."""
+
+    _fields_ = ([(n, _c_int) for n in ("B", "in_dim", "n_actions", "fc1", "fc2", "do_adam")]
+                + [(n, _c_void_p) for n in ("idx", "agent", "ring_state", "ring_new_state", "ring_action",
+                                            "ring_reward", "ring_terminal", "critic", "critic_grad",
+                                            "critic_exp_avg", "critic_exp_avg_sq", "critic_step", "actors",
+                                            "actors_grad", "actors_exp_avg", "actors_exp_avg_sq", "actors_target",
+                                            "actor_steps")]
+                + [("actor_stride", ctypes.c_int64)]
+                + [(n, _c_void_p) for n in ("losses", "workspace", "counters")]
+                + [(n, _c_float) for n in ("alpha", "beta", "gamma", "beta1", "beta2", "eps")])
+
+
+class FlockRingField(ctypes.Structure):
+    """Mirror of ``FlockRingField`` (include/flock_learn.h)."""
+
+    _fields_ = [("src", _c_void_p), ("dst", _c_void_p), ("width", ctypes.c_int64), ("kind", _c_int)]
+
+
+SIGNATURES.update({
+    "flock_ring_store": [_c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_int,
+                         ctypes.POINTER(FlockRingField)],
+    "flock_sc_workspace_floats": [_c_int] * 5,
+    "flock_sc_update_size": [],
+    "flock_sc_critic_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
+    "flock_sc_actor_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
+})
+RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,
+            "flock_sc_workspace_floats": ctypes.c_int64, "flock_sc_update_size": ctypes.c_int64}
 
 _lib = None
 

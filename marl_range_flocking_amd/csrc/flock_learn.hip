@@ -12,11 +12,11 @@
 #include <stdio.h>
 
 #include "flock_learn.h"
+#include "learn_internal.h"
 
 #pragma clang fp contract(off)
 
-namespace {
-
+namespace flock_learn_internal {
 thread_local char g_err[256] = "";
 int fail(int code, const char* msg) {
     snprintf(g_err, sizeof(g_err), "%s", msg);
@@ -26,6 +26,11 @@ int launched() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : fail(-4, hipGetErrorString(e));
 }
+}  // namespace flock_learn_internal
+
+namespace {
+using flock_learn_internal::fail;
+using flock_learn_internal::launched;
 
 constexpr int kBlock = 256;
 
@@ -237,11 +242,83 @@ __global__ __launch_bounds__(kBlock) void gather_rows_kernel(int64_t rows, int64
     }
 }
 
+// replay-ring insert: every field of n rows at ring rows start .. start + n - 1 (mod cap), one launch for all fields
+// (grid.y = field). kind 0: f32 copy; 1: u8 (bool) -> 1 - x (the reference's stored "terminal", utils.py:52);
+// 2: u8 -> x. float4 / uchar4 vectors when the field's flat offsets are multiples of 4 (never straddling the wrap).
+struct RingStore {
+    FlockRingField f[8];
+    int nf;
+    int64_t n, cap, start;
+};
+
+__global__ __launch_bounds__(kBlock) void ring_store_kernel(RingStore rs) {
+    const FlockRingField F = rs.f[blockIdx.y];
+    const int64_t total = rs.n * F.width, wrap = rs.cap * F.width, d0 = rs.start * F.width;
+    const bool u8 = F.kind != 0;
+    const bool vec = ((total | wrap | d0) & 3) == 0 && ((uintptr_t)F.dst & 15) == 0 &&
+                     ((uintptr_t)F.src & (u8 ? 3 : 15)) == 0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    if (vec) {
+        for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < total / 4; q += stride) {
+            float4 v;
+            if (!u8) {
+                v = reinterpret_cast<const float4*>(F.src)[q];
+            } else {
+                const uchar4 b = reinterpret_cast<const uchar4*>(F.src)[q];
+                v = make_float4(b.x, b.y, b.z, b.w);
+                if (F.kind == 1) v = make_float4(1.0f - v.x, 1.0f - v.y, 1.0f - v.z, 1.0f - v.w);
+            }
+            int64_t d = d0 + 4 * q;
+            if (d >= wrap) d -= wrap;
+            *reinterpret_cast<float4*>(F.dst + d) = v;
+        }
+    } else {
+        for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < total; q += stride) {
+            float v;
+            if (!u8) {
+                v = reinterpret_cast<const float*>(F.src)[q];
+            } else {
+                v = (float)reinterpret_cast<const uint8_t*>(F.src)[q];
+                if (F.kind == 1) v = 1.0f - v;
+            }
+            int64_t d = d0 + q;
+            if (d >= wrap) d -= wrap;
+            F.dst[d] = v;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
 
-const char* flock_learn_last_error(void) { return g_err; }
+int flock_ring_store(void* stream, int64_t n, int64_t capacity, int64_t start, int nfields,
+                     const FlockRingField* fields) {
+    if (n <= 0) return 0;
+    if (!fields || nfields < 1 || nfields > 8) return fail(-5, "flock_ring_store: 1..8 fields");
+    if (n > capacity || start < 0 || start >= capacity)
+        return fail(-5, "flock_ring_store: need n <= capacity and 0 <= start < capacity");
+    RingStore rs;
+    int64_t widest = 0;
+    for (int i = 0; i < nfields; ++i) {
+        if (!fields[i].src || !fields[i].dst) return fail(-3, "flock_ring_store: NULL pointer");
+        if (fields[i].width < 1 || fields[i].kind < 0 || fields[i].kind > 2)
+            return fail(-5, "flock_ring_store: bad field");
+        rs.f[i] = fields[i];
+        if (fields[i].width > widest) widest = fields[i].width;
+    }
+    rs.nf = nfields;
+    rs.n = n;
+    rs.cap = capacity;
+    rs.start = start;
+    int64_t blocks = (n * widest / 4 + kBlock - 1) / kBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(ring_store_kernel, dim3((unsigned)blocks, nfields), dim3(kBlock), 0, (hipStream_t)stream, rs);
+    return launched();
+}
+
+const char* flock_learn_last_error(void) { return flock_learn_internal::g_err; }
 
 int flock_adam_step(void* stream, int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                     const float* grad_scale, float lr, float beta1, float beta2, float eps, int64_t step,

@@ -44,12 +44,15 @@ class FlatParams:
     updates one actor per learn() call; per-agent leaf views come from agent_params(i)).
     """
 
-    def __init__(self, shapes, device, agents=1, agent_major=False, target=False, adam=True):
+    def __init__(self, shapes, device, agents=1, agent_major=False, target=False, adam=True, agent_pad=1):
         self.shapes = OrderedDict((k, tuple(v)) for k, v in shapes.items())
         self.device = torch.device(device)
         self.agents = int(agents)
         self.agent_major = agent_major
-        self.per_agent = sum(math.prod(s) for s in self.shapes.values())
+        # agent_pad: each agent's block rounded up to a multiple of agent_pad floats (zero padding, never a
+        # parameter), so every agent's slice starts equally aligned (the fused kernels use 16-B vector loads)
+        raw = sum(math.prod(s) for s in self.shapes.values())
+        self.per_agent = -(-raw // agent_pad) * agent_pad
         n = self.per_agent * self.agents
         self.numel = n
         z = lambda: torch.zeros(n, dtype=torch.float32, device=self.device)  # noqa: E731
@@ -300,23 +303,38 @@ class ReplayRing:
     def _width(self, name):
         return math.prod(self.fields[name])
 
-    def store(self, rows: dict):
-        """Append n rows per field (all fields the same n) at positions counter..counter+n-1 (mod capacity): the
-        positions are consecutive, so each field is one or two contiguous streaming copies (split at the wrap)."""
+    def store(self, rows: dict, one_minus=()):
+        """Append n rows per field (all fields the same n) at positions counter..counter+n-1 (mod capacity), every
+        field in ONE flock_ring_store launch. rows[name]: [n, *row_shape] (converted to f32 if needed); a name in
+        ``one_minus`` takes a bool / 0-1 tensor [n] and stores 1 - x (the reference's terminal = 1 - done)."""
         n = next(iter(rows.values())).shape[0]
         if n > self.capacity:  # only the last `capacity` rows survive
             rows = {k: v[n - self.capacity:] for k, v in rows.items()}
             self.counter += n - self.capacity
             n = self.capacity
-        start = self.counter % self.capacity
-        first = min(n, self.capacity - start)
-        for name, val in rows.items():
-            dst = self.bufs[name].view(self.capacity, -1)
-            src = val.reshape(n, -1)
-            assert src.shape[1] == dst.shape[1], (name, src.shape, dst.shape)
-            dst[start:start + first].copy_(src[:first])
-            if first < n:
-                dst[:n - first].copy_(src[first:])
+        if n == 0:
+            return
+        fields = (_native.FlockRingField * len(rows))()
+        keep = []
+        for i, (name, val) in enumerate(rows.items()):
+            w = self._width(name)
+            val = torch.as_tensor(val, device=self.device)
+            kind = 0
+            if name in one_minus:
+                if val.dtype in (torch.bool, torch.uint8):
+                    src, kind = val.reshape(n).contiguous(), 1
+                else:
+                    src = (1.0 - val.reshape(n).float()).contiguous()
+            else:
+                src = val.reshape(n, -1)
+                assert src.shape[1] == w, (name, src.shape, w)
+                src = src.float().contiguous()
+            keep.append(src)
+            fields[i] = _native.FlockRingField(src.data_ptr(), self.bufs[name].data_ptr(), w, kind)
+        _require_cuda(self.bufs[next(iter(rows))])
+        rc = _native.lib().flock_ring_store(_stream(self.device), n, self.capacity, self.counter % self.capacity,
+                                            len(rows), fields)
+        _native.check(rc, "flock_ring_store", learn=True)
         self.counter += n
 
     def scatter(self, name, idx, rows):

@@ -1,9 +1,9 @@
 """Shared-critic DDPG learner (reference: learners/maddpg_shared_critic/), batched over agents on MI355X.
 
-Reference behaviour kept (agent_simple_shared_critic.py, ddpg_network.py, utils.py):
+Reference behaviour kept (learners/maddpg_shared_critic/{agent_simple_shared_critic,ddpg_network,utils}.py):
   * one CriticNetwork shared by every agent and used as its own target (Q11, :63,76); per-agent actors with target
-    copies; LayerNorm MLPs fc1 -> LN -> ReLU -> fc2 -> LN (+ ReLU(action_value(a))) -> ReLU -> q (ddpg_network.py:278-290),
-    actor fc1 -> LN -> ReLU -> fc2 -> LN -> ReLU -> mu -> tanh (:352-361); reference initialisations (:255-271, :326-346);
+    copies; LayerNorm MLPs fc1 -> LN -> ReLU -> fc2 -> LN (+ ReLU(action_value(a))) -> ReLU -> q (ddpg_network.py:58-70),
+    actor fc1 -> LN -> ReLU -> fc2 -> LN -> ReLU -> mu -> tanh (:132-141); reference initialisations (:35-53, :106-127);
   * learn(i) == Agent.learn() of agent i (:115-155): sample B rows with replacement, y = r + gamma Q(s', mu'_i(s')) *
     notdone, critic MSE + Adam(beta), actor loss -mean Q(s, mu_i(s)) + Adam(alpha), every update_rate-th call of that
     agent the soft update (critic with itself tau*c + (1-tau)*c, target actor tau*a + (1-tau)*t, :158-185);
@@ -11,14 +11,21 @@ Reference behaviour kept (agent_simple_shared_critic.py, ddpg_network.py, utils.
 What changes: all actors live in one agent-major flat buffer (per-agent Adam = one launch over the agent's slice),
 the replay ring is device-resident (HIP scatter/gather rows, no CPU round trip), choose_action runs every agent's
 actor in one batched GEMM chain, and the OU noise is a per-(env, agent) device process.
+
+learn() has two implementations with the same semantics:
+  * fused (default): flock_sc_critic_update + flock_sc_actor_update (csrc/flock_sc.hip) — 12 HIP launches reading
+    the replay ring, the agent's actor slice and the critic in place, Adam fused into the gradient kernels; the pair
+    is replayed as one HIP graph;
+  * autograd (fused=False): the same update written with torch ops and the batched helpers of core.py.
 """
+import ctypes
 import math
 
 import torch
 import torch.nn.functional as F
 
-from .. import dist
-from .core import FlatParams, ReplayRing, blayer_norm, blinear, capture_graph
+from .. import _native, dist
+from .core import FlatParams, ReplayRing, _p, _stream, blayer_norm, blinear, capture_graph
 
 
 def critic_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
@@ -35,7 +42,7 @@ def actor_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
 
 
 def critic_forward(P, state, action):
-    """ddpg_network.py:278-290. P: name -> [A, ...]; state [A,B,in] or [B,in]; action [A,B,n] or [B,n]."""
+    """ddpg_network.py:58-70. P: name -> [A, ...]; state [A,B,in] or [B,in]; action [A,B,n] or [B,n]."""
     sv = blinear(state, P["fc1.weight"], P["fc1.bias"])
     sv = F.relu(blayer_norm(sv, P["bn1.weight"], P["bn1.bias"]))
     sv = blinear(sv, P["fc2.weight"], P["fc2.bias"])
@@ -45,7 +52,7 @@ def critic_forward(P, state, action):
 
 
 def actor_forward(P, state):
-    """ddpg_network.py:352-361."""
+    """ddpg_network.py:132-141."""
     x = blinear(state, P["fc1.weight"], P["fc1.bias"])
     x = F.relu(blayer_norm(x, P["bn1.weight"], P["bn1.bias"]))
     x = blinear(x, P["fc2.weight"], P["fc2.bias"])
@@ -75,7 +82,7 @@ def _init_mlp(fp, names_uniform, generator):
 class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
-                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None):
+                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -83,7 +90,7 @@ class SharedCriticLearner:
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.critic = FlatParams(critic_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=1)
         self.actors = FlatParams(actor_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=n_agents,
-                                 agent_major=True, target=True)
+                                 agent_major=True, target=True, agent_pad=64)
         _init_mlp(self.critic, None, self.gen)
         _init_mlp(self.actors, None, self.gen)
         self.actors.hard_update_target()  # update_network_parameters(tau=1) (:81)
@@ -94,7 +101,8 @@ class SharedCriticLearner:
         self.ou_state = None
         # the update runs on static tensors so it can be replayed as one HIP graph: agent i's actor is copied into
         # a scratch slot (params, target, Adam moments, step) and back around the replay
-        self.scratch = FlatParams(actor_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=1, target=True)
+        self.scratch = FlatParams(actor_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=1, target=True,
+                                  agent_pad=64)
         self.actor_steps = torch.zeros(n_agents, dtype=torch.int64, device=self.device)
         self.static_idx = torch.zeros(batch_size, dtype=torch.int64, device=self.device)
         self.losses = torch.zeros(2, dtype=torch.float32, device=self.device)
@@ -108,6 +116,69 @@ class SharedCriticLearner:
         if self.distributed:
             dist.sync_params(self.critic, group=dist_group)
             dist.sync_params(self.actors, group=dist_group)
+        self.fused = fused
+        self.fc1, self.fc2 = fc1, fc2
+        if fused:
+            self._init_fused()
+
+    # ------------------------------------------------------------------ fused HIP update (csrc/flock_sc.hip)
+    def _init_fused(self):
+        lib = _native.lib()
+        dev = self.device
+        B, n_in, na = self.batch_size, self.input_dim, self.n_actions
+        self.static_agent = torch.zeros(1, dtype=torch.int64, device=dev)
+        n_ws = lib.flock_sc_workspace_floats(B, n_in, na, self.fc1, self.fc2)
+        self.sc_workspace = torch.zeros(int(n_ws), dtype=torch.float32, device=dev)
+        self.sc_counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        rb = self.replay.bufs
+        C, A = self.critic, self.actors
+        fields = dict(B=B, in_dim=n_in, n_actions=na, fc1=self.fc1, fc2=self.fc2, do_adam=1,
+                      idx=_p(self.static_idx), agent=_p(self.static_agent), ring_state=_p(rb["state"]),
+                      ring_new_state=_p(rb["new_state"]), ring_action=_p(rb["action"]), ring_reward=_p(rb["reward"]),
+                      ring_terminal=_p(rb["terminal"]), critic=_p(C.data), critic_grad=_p(C.grad),
+                      critic_exp_avg=_p(C.exp_avg), critic_exp_avg_sq=_p(C.exp_avg_sq), critic_step=_p(C.step_dev),
+                      actors=_p(A.data), actors_grad=_p(A.grad), actors_exp_avg=_p(A.exp_avg),
+                      actors_exp_avg_sq=_p(A.exp_avg_sq), actors_target=_p(A.target),
+                      actor_steps=_p(self.actor_steps), actor_stride=A.per_agent, losses=_p(self.losses),
+                      workspace=_p(self.sc_workspace), counters=_p(self.sc_counters), alpha=self.alpha,
+                      beta=self.beta, gamma=self.gamma, beta1=0.9, beta2=0.999, eps=1e-8)
+        self._sc = _native.FlockScUpdate(**fields)
+        self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0))  # data-parallel: grads only
+
+    def _fused_update(self, u=None):
+        lib = _native.lib()
+        u = ctypes.byref(self._sc if u is None else u)
+        st = _stream(self.device)
+        _native.check(lib.flock_sc_critic_update(st, u), "flock_sc_critic_update", learn=True)
+        _native.check(lib.flock_sc_actor_update(st, u), "flock_sc_actor_update", learn=True)
+
+    def _fused_state(self):
+        A = self.actors
+        return self.critic.state_tensors() + [A.data, A.exp_avg, A.exp_avg_sq, self.actor_steps, self.losses]
+
+    def _run_fused(self, agent):
+        if not self.distributed:
+            if not self.use_graph:
+                return self._fused_update()
+            if self.graph is None:
+                self.graph = capture_graph(self._fused_update, self.device, self._fused_state())
+            return self.graph.replay()
+        # data-parallel: gradient-only kernels, RCCL all-reduce of each network's gradient, then the Adam steps
+        lib = _native.lib()
+        st = _stream(self.device)
+        u = ctypes.byref(self._sc_grads)
+        _native.check(lib.flock_sc_critic_update(st, u), "flock_sc_critic_update", learn=True)
+        dist.allreduce_mean_(self.critic.grad, self.group)
+        self.critic.adam_step_dev(self.beta)
+        _native.check(lib.flock_sc_actor_update(st, u), "flock_sc_actor_update", learn=True)
+        A = self.actors
+        lo, hi = A.agent_range(agent)
+        dist.allreduce_mean_(A.grad[lo:hi], self.group)
+        self.actor_steps[agent:agent + 1].add_(1)
+        rc = lib.flock_adam_step_dev(st, hi - lo, _p(A.data[lo:hi]), _p(A.grad[lo:hi]), _p(A.exp_avg[lo:hi]),
+                                     _p(A.exp_avg_sq[lo:hi]), None, float(self.alpha), 0.9, 0.999, 1e-8,
+                                     _p(self.actor_steps[agent:agent + 1]), None, 0.0, 0)
+        _native.check(rc, "flock_adam_step_dev", learn=True)
 
     # ------------------------------------------------------------------ acting
     def _stacked(self, fp, target=False):
@@ -140,7 +211,7 @@ class SharedCriticLearner:
         n = state.shape[0]
         self.replay.store({"state": state.reshape(n, -1), "new_state": new_state.reshape(n, -1),
                            "action": action.reshape(n, -1), "reward": reward.reshape(n, 1),
-                           "terminal": 1.0 - done.reshape(n).float()})
+                           "terminal": done.reshape(n)}, one_minus=("terminal",))
 
     @property
     def mem_cntr(self):
@@ -223,6 +294,10 @@ class SharedCriticLearner:
             torch.randint(0, len(self.replay), (B,), device=self.device, generator=self.gen, out=self.static_idx)
         else:
             self.static_idx.copy_(torch.as_tensor(idx).to(self.device))
+        if self.fused:
+            self.static_agent.fill_(agent)
+            self._run_fused(agent)
+            return self._finish_learn(agent)
         lo, hi = self.actors.agent_range(agent)
         A, S = self.actors, self.scratch
         with torch.no_grad():
@@ -235,6 +310,9 @@ class SharedCriticLearner:
             for src, dst in ((S.data, A.data), (S.exp_avg, A.exp_avg), (S.exp_avg_sq, A.exp_avg_sq)):
                 dst[lo:hi].copy_(src)
             self.actor_steps[agent:agent + 1].copy_(S.step_dev)
+        return self._finish_learn(agent)
+
+    def _finish_learn(self, agent):
         if self.count[agent] % self.update_rate == 0:                         # :152-154
             self.critic.soft_update(self.tau, mode=1, self_update=True)       # :172-178 (critic is its own target)
             self.actors.soft_update(self.tau, mode=1, agent=agent)            # :180-185
@@ -264,16 +342,18 @@ class SharedCriticBench:
     """bench.py hook for BASELINE config 3: after each vectorized env step, insert every agent's transition into the
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
-    def __init__(self, env, device, seed=0):
+    def __init__(self, env, device, seed=0, fused=True):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
-                                           buffer_size=1_000_000, dist_group=group)
+                                           buffer_size=1_000_000, dist_group=group, fused=fused)
         self.prev_obs = env.dnn.clone()
         self.prev_act = None
 
     def describe(self):
-        return (f"maddpg_shared_critic learn() x1 per vectorized step (B={self.learner.batch_size}, agent = step mod "
+        return (f"maddpg_shared_critic learn() x1 per vectorized step ("
+                f"{'fused HIP update' if self.learner.fused else 'autograd update'}, B={self.learner.batch_size}, "
+                f"agent = step mod "
                 f"{self.learner.n_agents}; all {self.env.E * self.env.N} transitions inserted into a 1e6-row "
                 f"device replay ring per step"
                 + ("; critic + actor gradient all-reduce over RCCL per learn)" if self.learner.distributed else ")"))

@@ -16,7 +16,7 @@ def header_functions():
     src = "\n".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"^\s*(?:int|const char\*)\s+(flock_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.M | re.S):
+    for m in re.finditer(r"^\s*(?:int|int64_t|const char\*)\s+(flock_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.M | re.S):
         args = m.group(2).strip()
         out[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
     return out
@@ -32,7 +32,8 @@ def test_header_declares_expected_entry_points():
     fns = header_functions()
     for name in ("flock_step_v2", "flock_step_uw", "flock_step_uw_discrete", "flock_step_flock", "flock_knn",
                  "flock_reset", "flock_abi_version", "flock_last_error", "flock_adam_step", "flock_soft_update",
-                 "flock_grad_norm", "flock_gru_fwd", "flock_gru_bwd", "flock_gather_rows", "flock_scatter_rows"):
+                 "flock_grad_norm", "flock_gru_fwd", "flock_gru_bwd", "flock_gather_rows", "flock_scatter_rows",
+                 "flock_sc_workspace_floats", "flock_sc_critic_update", "flock_sc_actor_update"):
         assert name in fns, name
 
 
@@ -77,3 +78,15 @@ def test_ops_refuse_cpu_tensors():
 
     with pytest.raises(RuntimeError, match="HIP device"):
         ops.knn(torch.zeros(1, 8, 2), 4, 10.0)
+
+
+def test_shared_critic_update_struct_and_argument_checks(lib):
+    assert ctypes.sizeof(_native.FlockScUpdate) == lib.flock_sc_update_size()
+    n = lib.flock_sc_workspace_floats(256, 4, 2, 400, 300)
+    assert n >= 256 * (13 * 400 + 14 * 300) and n % 64 == 0
+    u = _native.FlockScUpdate(B=16, in_dim=4, n_actions=2, fc1=32, fc2=24, do_adam=1)
+    assert lib.flock_sc_critic_update(None, ctypes.byref(u)) == -3  # NULL pointers
+    assert lib.flock_sc_actor_update(None, None) == -3
+    u.fc1 = 2048
+    assert lib.flock_sc_critic_update(None, ctypes.byref(u)) == -2  # beyond the row-kernel limits
+    assert "fc1/fc2 <= 1024" in lib.flock_learn_last_error().decode()

@@ -97,3 +97,26 @@ def test_replay_ring_scatter_gather_wraps(cuda):
     assert got.shape == (2, 2, 3) and torch.equal(got, expect[idx])
     assert torch.equal(ring.gather("d", idx), expect[idx][..., 0])
     assert len(ring) == 10 and ring.counter == 16
+
+
+@pytest.mark.parametrize("cap,n,steps", [(64, 16, 7), (1000, 96, 13), (37, 5, 11)], ids=["vec", "vec-wrap", "scalar"])
+def test_ring_store_fused_matches_row_copies(cap, n, steps, cuda):
+    """flock_ring_store (all fields, one launch; float4 and scalar paths; bool -> 1 - x) against a python ring."""
+    ring = ReplayRing(cap, {"s": (4,), "a": (2,), "r": (1,), "t": ()}, cuda)
+    ref = {k: torch.zeros(cap, w, device=cuda) for k, w in (("s", 4), ("a", 2), ("r", 1), ("t", 1))}
+    g = torch.Generator(device=cuda).manual_seed(0)
+    pos = 0
+    for _ in range(steps):
+        s = torch.randn(n, 4, device=cuda, generator=g)
+        a = torch.randn(n, 2, device=cuda, generator=g)
+        r = torch.randn(n, 1, device=cuda, generator=g)
+        d = torch.rand(n, device=cuda, generator=g) < 0.3
+        ring.store({"s": s, "a": a, "r": r, "t": d}, one_minus=("t",))
+        for i in range(n):
+            p = (pos + i) % cap
+            ref["s"][p], ref["a"][p], ref["r"][p] = s[i], a[i], r[i]
+            ref["t"][p] = 1.0 - d[i].float()
+        pos += n
+    for k in ref:
+        assert torch.equal(ring.bufs[k].reshape(cap, -1), ref[k]), k
+    assert ring.counter == n * steps

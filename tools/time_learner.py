@@ -16,7 +16,7 @@ env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=4, range
                   device=dev)
 env.positions.uniform_(0, 253)
 a = torch.rand(E, N, 2, device=dev)
-hook = SharedCriticBench(env, dev)
+hook = SharedCriticBench(env, dev, fused=os.environ.get("FUSED", "1") != "0")
 for s in range(5):
     env.step(a)
     hook.after_env_step(s, a)
