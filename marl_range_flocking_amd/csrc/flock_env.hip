@@ -11,6 +11,16 @@
 //            key = (bits(d2) with the low IB mantissa bits cleared) | j  (IB = ceil(log2 N)),
 //            and keeps the L = k+2 smallest keys in registers with a branch-free insertion network
 //            (1 v_min_u32 + (L-1) v_med3_u32 per candidate; no divergence, no sort)
+//            Step variants with N >= 128 scan a CELL LIST instead of all N (phase 3c below).
+//   phase 3c agents are binned into a Gc x Gc grid over [0, box]^2 (Gc = floor(sqrt(N / 4))) by an LDS counting
+//            sort into an extended cell-sorted array of (x, y, j) in which every cell row also carries ghost copies
+//            of its last column (in front) and first column (behind) when the box is periodic, so each agent's 3x3
+//            neighbourhood is exactly 3 contiguous ranges (one per row). The lane runs the same insertion network
+//            over those ~9 cells (~36 candidates at 4 per cell instead of N) and keeps the result only if it is
+//            PROVABLY the full scan's: every unscanned agent lies at least m = the distance to the neighbourhood's
+//            edge away, so if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety factor) exceeds the L-th key,
+//            no unscanned key can enter the top L. Otherwise the lane falls back to the full scan. Keys carry j, so
+//            the order of agents within a cell (LDS atomics) never matters.
 //   phase 4  exactness: the k+1 winners are re-sorted by their exact (d2, j); if the (k+2)-th key shares the
 //            truncated-d2 bucket of the (k+1)-th, the lane falls back to an exact (d2, j) rescan (rare). The
 //            result is the ascending (d2, j) order — a valid tie resolution of the reference's
@@ -24,6 +34,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "flock_amd.h"
@@ -66,6 +77,9 @@ struct Params {
     uint8_t* done;
     uint8_t* any_done;
     int* status;
+    // cell list (step variants, N >= 128)
+    int cells, ecap;  // grid side Gc, extended-array capacity per env (2N)
+    float cw, inv_cw, cell_eps;
     // reset
     float range_lo, range_hi, head_hi, check_distance;
     int max_attempts;
@@ -148,24 +162,23 @@ __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0
 // phase 3/4: kNN of one agent against its env's LDS-resident positions.
 // Output: bd[0..W) / bj[0..W) = the W = L-1 smallest (d2, j) in ascending order (slots beyond N: +inf / INT_MAX).
 
+template <int L>
+__device__ __forceinline__ void key_insert(uint32_t (&key)[L], uint32_t kx) {
+    uint32_t nk[L];
+    nk[0] = min(key[0], kx);
+#pragma unroll
+    for (int s = 1; s < L; ++s) nk[s] = med3u(key[s - 1], kx, key[s]);
+#pragma unroll
+    for (int s = 0; s < L; ++s) key[s] = nk[s];
+}
+
+// phase 3: all N candidates (broadcast ds_read_b128, two per read)
 template <int L, bool PERIODIC>
-__device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N, int k, int ib, float xi, float yi,
-                                         float box, float (&bd)[L - 1], int (&bj)[L - 1]) {
-    constexpr int W = L - 1;
-    const uint32_t lo_mask = (1u << ib) - 1u, hi_mask = ~lo_mask;
-    uint32_t key[L];
+__device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __restrict__ cand, int N, int ib, float xi,
+                                         float yi, float box) {
+    const uint32_t hi_mask = ~((1u << ib) - 1u);
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
-
-    auto insert = [&](uint32_t kx) {
-        uint32_t nk[L];
-        nk[0] = min(key[0], kx);
-#pragma unroll
-        for (int s = 1; s < L; ++s) nk[s] = med3u(key[s - 1], kx, key[s]);
-#pragma unroll
-        for (int s = 0; s < L; ++s) key[s] = nk[s];
-    };
-
     const float4* cand4 = reinterpret_cast<const float4*>(cand);
     int j = 0;
 #pragma unroll 1
@@ -173,14 +186,63 @@ __device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N,
         const float4 c = cand4[j >> 1];  // broadcast: every lane of the env reads the same 16 B
         const float d0 = pair_d2<PERIODIC>(xi, yi, c.x, c.y, box);
         const float d1 = pair_d2<PERIODIC>(xi, yi, c.z, c.w, box);
-        insert((__float_as_uint(d0) & hi_mask) | (uint32_t)j);
-        insert((__float_as_uint(d1) & hi_mask) | (uint32_t)(j + 1));
+        key_insert<L>(key, (__float_as_uint(d0) & hi_mask) | (uint32_t)j);
+        key_insert<L>(key, (__float_as_uint(d1) & hi_mask) | (uint32_t)(j + 1));
     }
     if (j < N) {
         const float2 c = cand[j];
-        insert((__float_as_uint(pair_d2<PERIODIC>(xi, yi, c.x, c.y, box)) & hi_mask) | (uint32_t)j);
+        key_insert<L>(key, (__float_as_uint(pair_d2<PERIODIC>(xi, yi, c.x, c.y, box)) & hi_mask) | (uint32_t)j);
     }
+}
 
+// phase 3c: the 3x3 cell neighbourhood (3 contiguous ranges of the extended cell-sorted array); returns true when
+// the top-L keys are provably those of the full scan (see the file header)
+template <int L, bool PERIODIC>
+__device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __restrict__ ext,
+                                           const int* __restrict__ pre, int Gc, int cx, int cy, int ib, float xi,
+                                           float yi, float box, float cw, float eps) {
+    const uint32_t hi_mask = ~((1u << ib) - 1u);
+#pragma unroll
+    for (int s = 0; s < L; ++s) key[s] = kEmpty;
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r) {
+        int yr = cy + r - 1;
+        bool row = true;
+        if (PERIODIC)
+            yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
+        else
+            row = yr >= 0 && yr < Gc;
+        const int* pr = pre + (row ? yr : 0) * (Gc + 3);
+        const int s0 = row ? pr[cx] : 0, e0 = row ? pr[cx + 3] : 0;
+#pragma unroll 1
+        for (int c = s0;; c += 2) {
+            const bool a0 = c < e0, a1 = c + 1 < e0;
+            if (__ballot(a0) == 0) break;
+            const float4 q0 = ext[a0 ? c : 0];
+            const float4 q1 = ext[a1 ? c + 1 : 0];
+            const float d0 = pair_d2<PERIODIC>(xi, yi, q0.x, q0.y, box);
+            const float d1 = pair_d2<PERIODIC>(xi, yi, q1.x, q1.y, box);
+            const uint32_t k0 = (__float_as_uint(d0) & hi_mask) | (uint32_t)__float_as_int(q0.z);
+            const uint32_t k1 = (__float_as_uint(d1) & hi_mask) | (uint32_t)__float_as_int(q1.z);
+            key_insert<L>(key, a0 ? k0 : kEmpty);
+            key_insert<L>(key, a1 ? k1 : kEmpty);
+        }
+    }
+    // every agent outside the scanned 3x3 block is at least m away (periodic or not)
+    const float lx = (float)(cx - 1) * cw, rx = (float)(cx + 2) * cw;
+    const float ly = (float)(cy - 1) * cw, ry = (float)(cy + 2) * cw;
+    const float m = fminf(fminf(xi - lx, rx - xi), fminf(yi - ly, ry - yi)) - eps;
+    const float bound = m > 0.0f ? (m * m) * 0.99998f : 0.0f;
+    return (__float_as_uint(bound) & hi_mask) > key[L - 1];
+}
+
+// phase 4: exact (d2, j) order of the W best keys (or an exact rescan when the (k+1)/(k+2) bucket is ambiguous)
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void knn_finalize(const uint32_t (&key)[L], const float2* __restrict__ cand, int N, int k,
+                                             int ib, float xi, float yi, float box, float (&bd)[L - 1],
+                                             int (&bj)[L - 1]) {
+    constexpr int W = L - 1;
+    const uint32_t lo_mask = (1u << ib) - 1u, hi_mask = ~lo_mask;
     // (k+1)-th and (k+2)-th smallest keys (k is a runtime value <= L-2; static-index select, no scratch)
     uint32_t kk = kEmpty, kr = kEmpty;
 #pragma unroll
@@ -243,15 +305,29 @@ __device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N,
     }
 }
 
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N, int k, int ib, float xi, float yi,
+                                         float box, float (&bd)[L - 1], int (&bj)[L - 1]) {
+    uint32_t key[L];
+    scan_all<L, PERIODIC>(key, cand, N, ib, xi, yi, box);
+    knn_finalize<L, PERIODIC>(key, cand, N, k, ib, xi, yi, box, bd, bj);
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // the fused step kernel
 
-template <int L, bool PERIODIC>
+template <int L, bool PERIODIC, bool CELL>
 __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float2* lpos = reinterpret_cast<float2*>(smem);               // [G][S]
     float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
     int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G]
+    // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][Gc*Gc], pre [G][Gc][Gc+3], rowlen [G][Gc]
+    const int Gc = p.cells;
+    float4* ext_all = reinterpret_cast<float4*>(smem + ((((size_t)(flags + p.G) - (size_t)smem) + 15) & ~(size_t)15));
+    int* cnt_all = reinterpret_cast<int*>(ext_all + (CELL ? p.G * p.ecap : 0));
+    int* pre_all = cnt_all + (CELL ? p.G * Gc * Gc : 0);
+    int* rowlen_all = pre_all + (CELL ? p.G * Gc * (Gc + 3) : 0);
 
     const int t = threadIdx.x;
     const int g = t / p.N;
@@ -262,6 +338,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     const size_t a = (size_t)env * p.N + i;
     const int variant = p.variant;
     if (in_group && i == 0) flags[g] = 0;
+    if (CELL && in_group && i < Gc * Gc) cnt_all[g * Gc * Gc + i] = 0;  // published by the phase-2 barrier
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
@@ -373,10 +450,64 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         __syncthreads();
     }
 
+    // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
+    int cx = 0, cy = 0;
+    if (CELL) {
+        int* cnt = cnt_all + g * Gc * Gc;
+        int* pre = pre_all + g * Gc * (Gc + 3);
+        int* rowlen = rowlen_all + g * Gc;
+        float4* ext = ext_all + g * p.ecap;
+        int rank = 0;
+        if (active) {
+            cx = min((int)(x * p.inv_cw), Gc - 1);  // x, y in [0, box] after check_boundary
+            cy = min((int)(y * p.inv_cw), Gc - 1);
+            rank = atomicAdd(&cnt[cy * Gc + cx], 1);
+        }
+        __syncthreads();
+        if (in_group && i < Gc) {  // row i: [ghost of column Gc-1][columns 0..Gc-1][ghost of column 0]
+            const int* cr = cnt + i * Gc;
+            int* pr = pre + i * (Gc + 3);
+            int run = PERIODIC ? cr[Gc - 1] : 0;
+            pr[0] = 0;
+            for (int c = 0; c < Gc; ++c) {
+                pr[c + 1] = run;
+                run += cr[c];
+            }
+            pr[Gc + 1] = run;
+            run += PERIODIC ? cr[0] : 0;
+            pr[Gc + 2] = run;
+            rowlen[i] = run;
+        }
+        __syncthreads();
+        if (in_group && i < Gc) {
+            int off = 0;
+            for (int r = 0; r < i; ++r) off += rowlen[r];
+            int* pr = pre + i * (Gc + 3);
+            for (int e = 0; e < Gc + 3; ++e) pr[e] += off;
+        }
+        __syncthreads();
+        if (active) {
+            const float4 ent = make_float4(x, y, __int_as_float(i), 0.0f);
+            const int* pr = pre + cy * (Gc + 3);
+            ext[pr[cx + 1] + rank] = ent;
+            if (PERIODIC && cx == Gc - 1) ext[pr[0] + rank] = ent;
+            if (PERIODIC && cx == 0) ext[pr[Gc + 1] + rank] = ent;
+        }
+        __syncthreads();
+    }
+
     // ---- phase 3/4: kNN -------------------------------------------------------------------------------
     float bd[L - 1];
     int bj[L - 1];
-    if (active) knn_scan<L, PERIODIC>(lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);
+    if (active) {
+        uint32_t key[L];
+        bool ok = false;
+        if (CELL)
+            ok = scan_cells<L, PERIODIC>(key, ext_all + g * p.ecap, pre_all + g * Gc * (Gc + 3), Gc, cx, cy, p.ib,
+                                         x, y, p.box, p.cw, p.cell_eps);
+        if (!ok) scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
+        knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);
+    }
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
     int coll = 0;
@@ -530,7 +661,15 @@ struct Cfg {
     size_t lds;
 };
 
-Cfg make_cfg(int E, int N, bool reset) {
+// cell grid side for the step kernel's cell list (0 = full scan): ~4 agents per cell, >= 5 cells per side
+int cell_grid(int N, int variant) {
+    if (variant == kSense || N < 128) return 0;
+    int gc = 1;
+    while ((gc + 1) * (gc + 1) * 4 <= N) ++gc;
+    return gc >= 5 ? gc : 0;
+}
+
+Cfg make_cfg(int E, int N, bool reset, int cells) {
     Cfg c;
     c.S = (N + 1) & ~1;
     c.P = 1 << ceil_log2(N);
@@ -541,6 +680,10 @@ Cfg make_cfg(int E, int N, bool reset) {
         c.lds = (size_t)c.G * c.S * sizeof(float2) + 2 * c.G * sizeof(int);
     else
         c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + c.G * sizeof(int);
+    if (!reset && cells) {  // ext (2N float4, 16-B aligned) + cnt + pre + rowlen per env
+        c.lds = (c.lds + 15) & ~(size_t)15;
+        c.lds += (size_t)c.G * (2 * N * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 3) + cells) * 4);
+    }
     return c;
 }
 
@@ -554,10 +697,17 @@ int check_common(int E, int N, int k) {
 
 template <int L>
 void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
-    if (p.periodic)
-        hipLaunchKernelGGL((step_kernel<L, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
-    else
-        hipLaunchKernelGGL((step_kernel<L, false>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+    if (p.cells) {
+        if (p.periodic)
+            hipLaunchKernelGGL((step_kernel<L, true, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+        else
+            hipLaunchKernelGGL((step_kernel<L, false, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+    } else {
+        if (p.periodic)
+            hipLaunchKernelGGL((step_kernel<L, true, false>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+        else
+            hipLaunchKernelGGL((step_kernel<L, false, false>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+    }
 }
 
 template <int L>
@@ -567,7 +717,15 @@ void launch_reset_L(const Cfg& c, const Params& p, hipStream_t s) {
 
 int dispatch(Params& p, hipStream_t s, bool reset) {
     if (p.E == 0) return FLOCK_OK;
-    const Cfg c = make_cfg(p.E, p.N, reset);
+    p.cells = (reset || getenv("FLOCK_NO_CELLS")) ? 0 : cell_grid(p.N, p.variant);
+    if (p.cells) {
+        p.ecap = 2 * p.N;
+        p.cw = p.box / (float)p.cells;
+        p.inv_cw = (float)p.cells / p.box;
+        p.cell_eps = p.box * 1e-5f;
+        if (!(p.box > 0.0f)) p.cells = 0;
+    }
+    const Cfg c = make_cfg(p.E, p.N, reset, p.cells);
     p.G = c.G;
     p.S = c.S;
     p.P = c.P;

@@ -57,3 +57,12 @@ def allclose_rel(a, b, rtol=RTOL, atol=0.0):
     both_nan = np.isnan(a) & np.isnan(b)
     ok = np.isclose(a, b, rtol=rtol, atol=atol) | both_nan
     return bool(ok.all()), (np.nanmax(np.abs(a - b) / np.maximum(np.abs(b), 1e-30)) if a.size else 0.0)
+
+
+def _knn_exact(pos, k, box, sr, periodic, clamp, gdnn, gidx):
+    """GPU kNN (distances and indices) bitwise equal to the C oracle's exact (d2, j) order on the same positions."""
+    from oracle import oracle as O
+
+    dnn, idx = O.knn(pos, k, box, sr, periodic=periodic, clamp=clamp)
+    np.testing.assert_array_equal(gidx, idx)
+    np.testing.assert_array_equal(gdnn, dnn)

@@ -1,0 +1,101 @@
+"""The step kernel's cell-list kNN (N >= 128) against its own full scan (FLOCK_NO_CELLS=1) and the C oracle.
+
+The cell path must be indistinguishable from the all-pairs scan: every output of a step (positions, velocities,
+headings, neighbour distances and indices, reward, done) is compared BITWISE between the two paths from the same
+state, over uniform, clustered (many agents per cell, forcing long ranges and the full-scan fallback), box-edge
+(x = box / tiny x, cell clamping and periodic ghosts) and integer-lattice (exact distance ties, the ambiguous-bucket
+rescan) placements, N in 128..1024 and k up to 15; sampled envs are also checked against the oracle's exact kNN.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+from parity import _knn_exact
+
+pytestmark = pytest.mark.gpu
+
+
+def _positions(kind, E, N, box, rng):
+    if kind == "uniform":
+        return rng.uniform(0, box, (E, N, 2))
+    if kind == "clustered":  # 4 tight blobs: ~N/4 agents in one or two cells
+        centres = rng.uniform(0.1 * box, 0.9 * box, (E, 4, 2))
+        pick = rng.integers(0, 4, (E, N))
+        p = np.take_along_axis(centres, pick[..., None].repeat(2, -1), 1) + rng.normal(0, box / 60, (E, N, 2))
+        return np.clip(p, 0.001, box)
+    if kind == "edges":  # half the agents hugging the box edges and corners
+        p = rng.uniform(0, box, (E, N, 2))
+        m = rng.uniform(size=(E, N, 2)) < 0.25
+        p[m] = np.where(rng.uniform(size=m.sum()) < 0.5, rng.uniform(0.001, 0.5, m.sum()),
+                        rng.uniform(box - 0.5, box, m.sum()))
+        return p
+    if kind == "lattice":  # integer grid, equal spacing -> exact d2 ties
+        side = int(np.ceil(np.sqrt(N)))
+        g = np.stack(np.meshgrid(np.arange(side), np.arange(side)), -1).reshape(-1, 2)[:N].astype(np.float64)
+        g = g * (box / side) + 0.5
+        return np.broadcast_to(g, (E, N, 2)).copy()
+    raise ValueError(kind)
+
+
+def _step(variant, periodic, pos, head, prev, vel, mem, act, noise, N, k, box, cuda, cells):
+    E = pos.shape[0]
+    env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                  range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda)
+    env.set_state(positions=pos, headings=head, prev_headings=prev, velocities=vel,
+                  obs_memory=mem if variant in ("uw", "flock") else None)
+    if cells:
+        os.environ.pop("FLOCK_NO_CELLS", None)
+    else:
+        os.environ["FLOCK_NO_CELLS"] = "1"
+    try:
+        if variant == "uw_discrete":
+            out = env.step(torch.from_numpy(act), noise=torch.from_numpy(noise))
+        else:
+            out = env.step(torch.from_numpy(act))
+        torch.cuda.synchronize()
+    finally:
+        os.environ.pop("FLOCK_NO_CELLS", None)
+    obs, rew, (done, anyd), _ = out
+    res = {"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn, "idx": env.nn_idx,
+           "rew": rew, "done": done, "any": anyd}
+    return {k2: v.detach().cpu().numpy().copy() for k2, v in res.items()}
+
+
+CASES = [("v2", True, 256, 4, "uniform"), ("v2", True, 256, 4, "clustered"), ("v2", True, 256, 4, "edges"),
+         ("v2", True, 256, 4, "lattice"), ("v2", False, 256, 4, "edges"), ("v2", True, 128, 1, "uniform"),
+         ("v2", True, 500, 15, "uniform"), ("v2", True, 1024, 4, "uniform"), ("v2", True, 1024, 11, "clustered"),
+         ("uw", False, 256, 4, "uniform"), ("uw", False, 512, 4, "edges"), ("uw_discrete", False, 512, 4, "uniform"),
+         ("flock", False, 300, 6, "clustered"), ("v2", False, 1000, 9, "lattice")]
+
+
+@pytest.mark.parametrize("variant,periodic,N,k,kind", CASES,
+                         ids=[f"{v}-{'per' if p else 'euc'}-N{n}-k{k}-{d}" for v, p, n, k, d in CASES])
+def test_cell_list_step_is_bitwise_the_full_scan(variant, periodic, N, k, kind, cuda):
+    E = 64 if N <= 512 else 16
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(N * 31 + k)
+    pos = _positions(kind, E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    prev = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    vel = rng.standard_normal((E, N, 2)).astype(np.float32)
+    vel /= np.linalg.norm(vel, axis=-1, keepdims=True)
+    mem = rng.uniform(0, 14, (E, N, 4, k)).astype(np.float32)
+    noise = None
+    if variant == "uw_discrete":
+        act = rng.integers(0, 10, (E, N)).astype(np.int64)
+        noise = (0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)
+    else:
+        act = rng.uniform(-1.5, 2.5, (E, N, 2)).astype(np.float32)
+        if kind == "lattice":
+            act[..., 0] = 0.0  # keep the lattice (and its ties) intact through the step
+            act[..., 1] = 0.0
+    args = (variant, periodic, pos, head, prev, vel, mem, act, noise, N, k, box, cuda)
+    a = _step(*args, cells=True)
+    b = _step(*args, cells=False)
+    for key in a:
+        np.testing.assert_array_equal(a[key], b[key], err_msg=key)
+    sample = np.arange(0, E, max(1, E // 6))
+    _knn_exact(a["pos"][sample], k, box, 14.0, periodic, variant != "flock", a["dnn"][sample], a["idx"][sample])

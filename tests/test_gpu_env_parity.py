@@ -16,7 +16,7 @@ import torch
 
 from marl_range_flocking_amd import FlockConfig, VecFlockEnv, ops
 from oracle import oracle as O
-from parity import allclose_rel, d2_rows, knn_mismatch, meta
+from parity import _knn_exact, allclose_rel, d2_rows, knn_mismatch, meta
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -29,12 +29,6 @@ def _env(m, E, device):
                                    collision_distance=m["collision_distance"], range_start=(0, m["box"]),
                                    sensor_range=m.get("sensor_range", 14.0), periodic=(v == "v2"),
                                    v_min=m.get("v_min", 0.005)), device=device)
-
-
-def _knn_exact(pos, k, box, sr, periodic, clamp, gdnn, gidx):
-    dnn, idx = O.knn(pos, k, box, sr, periodic=periodic, clamp=clamp)
-    np.testing.assert_array_equal(gidx, idx)
-    np.testing.assert_array_equal(gdnn, dnn)
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "env_*.npz"))),
