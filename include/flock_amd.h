@@ -56,6 +56,30 @@ int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_ran
                   float* pos, float* heading, const float* action,
                   float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
 
+/* The same step fused with the replay insert of the training loop that drives it
+ * (learners/maddpg_shared_critic/train_flock.py:112-127: step, then store_transitions(state, action, reward,
+ * new_state, done), utils.py:47-54): agent a = env * N + i also writes ring row (start + a) mod capacity:
+ * state[k] = prev_obs[a][0..k), action[2] = the raw action, reward, new_state[k] = the new dnn row,
+ * terminal = 1 - done. When E * N > capacity only the last `capacity` transitions survive (as in a ring insert):
+ * agents a < skip write nothing and agent a >= skip writes row (start + a - skip) mod capacity.
+ * Requires 0 <= skip, E * N - skip <= capacity and 0 <= start < capacity. */
+typedef struct FlockRing {
+    float* state;
+    float* action;
+    float* reward;
+    float* new_state;
+    float* terminal;
+    const float* prev_obs;
+    int64_t capacity;
+    int64_t start;
+    int64_t skip;
+} FlockRing;
+int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                        float dt, float v_min, float v_max, int periodic, int rigid_boundary,
+                        float* pos, float* heading, const float* action,
+                        float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                        const FlockRing* ring);
+
 /* gym_flock_uw step: velocity actions; obs memory mem_in → mem_out (may alias); prev_heading (rw). nn_idx may be
  * NULL (the reference does not keep it for this env). */
 int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,

@@ -62,7 +62,15 @@ class FlockRingField(ctypes.Structure):
     _fields_ = [("src", _c_void_p), ("dst", _c_void_p), ("width", ctypes.c_int64), ("kind", _c_int)]
 
 
+class FlockRing(ctypes.Structure):
+    """Mirror of ``FlockRing`` (include/flock_amd.h): replay-ring targets of flock_step_v2_store."""
+
+    _fields_ = ([(n, _c_void_p) for n in ("state", "action", "reward", "new_state", "terminal", "prev_obs")]
+                + [("capacity", ctypes.c_int64), ("start", ctypes.c_int64), ("skip", ctypes.c_int64)])
+
+
 SIGNATURES.update({
+    "flock_step_v2_store": SIGNATURES["flock_step_v2"] + [ctypes.POINTER(FlockRing)],
     "flock_ring_store": [_c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_int,
                          ctypes.POINTER(FlockRingField)],
     "flock_sc_workspace_floats": [_c_int] * 5,

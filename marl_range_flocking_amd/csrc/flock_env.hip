@@ -77,6 +77,10 @@ struct Params {
     uint8_t* done;
     uint8_t* any_done;
     int* status;
+    // fused replay insert (flock_step_v2_store)
+    float *r_state, *r_action, *r_reward, *r_new, *r_term;
+    const float* r_prev;
+    int64_t r_cap, r_start, r_skip;
     // cell list (step variants, N >= 128)
     int cells, ecap;  // grid side Gc, extended-array capacity per env (2N)
     float cw, inv_cw, cell_eps;
@@ -342,12 +346,14 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
+    float2 act_in = make_float2(0.0f, 0.0f);
     if (active) {
         const float2 pp = reinterpret_cast<const float2*>(p.pos)[a];
         x = pp.x;
         y = pp.y;
         if (variant == FLOCK_VARIANT_V2) {  // gym_flock_v2.py:317-350 (heading=True)
             const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
+            act_in = ac;
             const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
             h = __fadd_rn(p.heading[a], __fmul_rn(ang, p.dt));               // :329
             const float lin = clamp_t(ac.x, p.v_min, p.v_max);               // :331
@@ -554,6 +560,20 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
                 r = coll ? -5.0f : 0.01f;  // gym_flock_v2.py:217-220, gym_flock.py:142-145
             }
             p.reward[a] = r;
+            if (p.r_state && (int64_t)a >= p.r_skip) {  // fused replay insert: row (start + a - skip) mod cap
+                int64_t row = p.r_start + (int64_t)a - p.r_skip;
+                if (row >= p.r_cap) row -= p.r_cap;
+                const float* po = p.r_prev + a * p.k;
+#pragma unroll
+                for (int s = 0; s < L - 2; ++s)
+                    if (s < p.k) {
+                        p.r_state[row * p.k + s] = po[s];
+                        p.r_new[row * p.k + s] = dv[s];
+                    }
+                reinterpret_cast<float2*>(p.r_action)[row] = act_in;
+                p.r_reward[row] = r;
+                p.r_term[row] = coll ? 0.0f : 1.0f;
+            }
         }
     }
     if (variant != kSense) {
@@ -808,6 +828,50 @@ int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_ran
     p.reward = reward;
     p.done = done;
     p.any_done = any_done;
+    return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                        float dt, float v_min, float v_max, int periodic, int rigid_boundary, float* pos,
+                        float* heading, const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward,
+                        uint8_t* done, uint8_t* any_done, const FlockRing* ring) {
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done || !ring))
+        return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL pointer");
+    if (E && (!ring->state || !ring->action || !ring->reward || !ring->new_state || !ring->terminal ||
+              !ring->prev_obs))
+        return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL ring pointer");
+    if (ring->skip < 0 || (int64_t)E * N - ring->skip > ring->capacity || ring->start < 0 ||
+        ring->start >= ring->capacity)
+        return fail(FLOCK_E_ARG, "flock_step_v2_store: need skip >= 0, E*N - skip <= capacity, 0 <= start < capacity");
+    Params p = base(E, N, k, box);
+    p.variant = FLOCK_VARIANT_V2;
+    p.periodic = periodic != 0;
+    p.rigid = rigid_boundary != 0;
+    p.sensor_range = sensor_range;
+    p.cd = collision_distance;
+    p.dt = dt;
+    p.v_min = v_min;
+    p.v_max = v_max;
+    p.pos = pos;
+    p.heading = heading;
+    p.action = action;
+    p.vel = vel;
+    p.dnn = dnn;
+    p.idx = nn_idx;
+    p.reward = reward;
+    p.done = done;
+    p.any_done = any_done;
+    p.r_state = ring->state;
+    p.r_action = ring->action;
+    p.r_reward = ring->reward;
+    p.r_new = ring->new_state;
+    p.r_term = ring->terminal;
+    p.r_prev = ring->prev_obs;
+    p.r_cap = ring->capacity;
+    p.r_start = ring->start;
+    p.r_skip = ring->skip;
     return dispatch(p, (hipStream_t)stream, false);
 }
 

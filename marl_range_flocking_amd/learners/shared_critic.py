@@ -213,6 +213,20 @@ class SharedCriticLearner:
                            "action": action.reshape(n, -1), "reward": reward.reshape(n, 1),
                            "terminal": done.reshape(n)}, one_minus=("terminal",))
 
+    def replay_slots(self, n):
+        """Reserve the next n replay rows for an env step that writes its transitions itself
+        (VecFlockEnv.step(ring=...) -> flock_step_v2_store); same rows and counter as store_transitions (when n
+        exceeds the capacity only the last `capacity` transitions are kept, as ReplayRing.store does)."""
+        R = self.replay
+        skip = max(0, n - R.capacity)
+        b = R.bufs
+        ring = _native.FlockRing(state=b["state"].data_ptr(), action=b["action"].data_ptr(),
+                                 reward=b["reward"].data_ptr(), new_state=b["new_state"].data_ptr(),
+                                 terminal=b["terminal"].data_ptr(), prev_obs=None, capacity=R.capacity,
+                                 start=(R.counter + skip) % R.capacity, skip=skip)
+        R.counter += n
+        return ring
+
     @property
     def mem_cntr(self):
         return self.replay.counter
@@ -355,8 +369,15 @@ class SharedCriticBench:
                 f"{'fused HIP update' if self.learner.fused else 'autograd update'}, B={self.learner.batch_size}, "
                 f"agent = step mod "
                 f"{self.learner.n_agents}; all {self.env.E * self.env.N} transitions inserted into a 1e6-row "
-                f"device replay ring per step"
+                f"device replay ring per step by the env kernel itself"
                 + ("; critic + actor gradient all-reduce over RCCL per learn)" if self.learner.distributed else ")"))
+
+    def step(self, s, action):
+        """One bench step with the replay insert fused into the env kernel (flock_step_v2_store), then learn()."""
+        env = self.env
+        ring = self.learner.replay_slots(env.E * env.N)
+        env.step(action, ring=ring)
+        self.learner.learn(s % self.learner.n_agents)
 
     def after_env_step(self, s, action):
         env = self.env

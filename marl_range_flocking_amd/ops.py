@@ -55,8 +55,10 @@ def _check_k(N, k):
 
 
 def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k, box, sensor_range,
-            collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False):
-    """gym_flock_v2.MultiAgentEnv.step (gym_flock_v2.py:71-83) for E envs; pos/heading updated in place."""
+            collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False, ring=None):
+    """gym_flock_v2.MultiAgentEnv.step (gym_flock_v2.py:71-83) for E envs; pos/heading updated in place.
+    ring (a _native.FlockRing): also write every transition into a replay ring in the same launch
+    (flock_step_v2_store; the store_transitions that follows each step in train_flock.py)."""
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -69,11 +71,13 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
     _need(reward, "reward", f32, (E, N), dev)
     _need(done, "done", torch.bool, (E, N), dev)
     _need(any_done, "any_done", torch.bool, (E,), dev)
-    rc = _native.lib().flock_step_v2(
-        _stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt), float(v_min),
-        float(v_max), int(bool(periodic)), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(action),
-        _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
-    _native.check(rc, "flock_step_v2")
+    args = (_stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
+            float(v_min), float(v_max), int(bool(periodic)), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading),
+            _ptr(action), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
+    if ring is None:
+        _native.check(_native.lib().flock_step_v2(*args), "flock_step_v2")
+    else:
+        _native.check(_native.lib().flock_step_v2_store(*args, ctypes.byref(ring)), "flock_step_v2_store")
 
 
 def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done, *, k, box,

@@ -141,9 +141,11 @@ class VecFlockEnv:
             self._bufs[self._cur]["mem"].copy_(torch.as_tensor(obs_memory).to(self.device))
 
     # ------------------------------------------------------------------ step
-    def step(self, action, noise=None, dt=None, copy=False):
+    def step(self, action, noise=None, dt=None, copy=False, ring=None):
         """One vectorized step. action: [E,N,2] f32 (v2: [lin, ang]; uw/flock: velocity/acceleration) or
-        [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info)."""
+        [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info).
+        ring (v2): a _native.FlockRing from a learner's replay_slots(); the step also stores every transition
+        (previous obs, action, reward, new obs, 1 - done) into that replay ring in the same launch."""
         c = self.cfg
         dt = c.dt if dt is None else float(dt)
         E, N, k = self.E, self.N, self.k
@@ -158,10 +160,14 @@ class VecFlockEnv:
             a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
         common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
                       rigid_boundary=c.rigid_boundary)
+        if ring is not None:
+            if c.variant != "v2":
+                raise NotImplementedError("the fused replay insert is built for the v2 step")
+            ring.prev_obs = src["dnn"].data_ptr()
         if c.variant == "v2":
             ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
                         self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
-                        v_max=c.max_linear_velocity, periodic=c.periodic, **common)
+                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, **common)
         elif c.variant == "uw":
             ops.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
                         dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, sensor_range=c.sensor_range,

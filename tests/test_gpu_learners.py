@@ -214,3 +214,39 @@ def test_shared_ou_matches_sequential_process(cuda):
         x = x + 0.15 * (0.0 - x) * 1e-2 + 0.2 * np.sqrt(1e-2) * z[:, i]
         ref.append(x)
     torch.testing.assert_close(xs, torch.stack(ref, 1).float(), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("cap", [10000, 5000], ids=["wrap", "step-larger-than-ring"])
+def test_fused_env_replay_insert_matches_store_transitions(cap, cuda):
+    """VecFlockEnv.step(ring=learner.replay_slots(n)) (flock_step_v2_store) leaves the replay ring, counter and
+    env outputs bitwise equal to step() followed by store_transitions(prev_obs, action, reward, obs, done), over
+    three steps with a ring wrap-around, and with a step larger than the whole ring (only the last rows kept)."""
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    E, N, k, box = 64, 128, 4, 179.0
+    envs, learners = [], []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0), device=cuda)
+        g = torch.Generator(device=cuda).manual_seed(5)
+        env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
+        env.headings.copy_(torch.rand(E, N, device=cuda, generator=g) * 4.7)
+        env.step(torch.zeros(E, N, 2, device=cuda))
+        envs.append(env)
+        learners.append(SharedCriticLearner(N, k, fc1=32, fc2=24, batch_size=16, buffer_size=cap, device=cuda))
+    g = torch.Generator(device=cuda).manual_seed(9)
+    for _ in range(3):
+        a = torch.stack([torch.rand(E, N, device=cuda, generator=g) * 3 - 0.5,
+                         torch.rand(E, N, device=cuda, generator=g) * 4 - 2], -1).contiguous()
+        fused_env, plain_env = envs
+        fused_env.step(a, ring=learners[0].replay_slots(E * N))
+        prev = plain_env.dnn.clone()
+        plain_env.step(a)
+        n = E * N
+        learners[1].store_transitions(prev.reshape(n, -1), a.reshape(n, -1), plain_env.reward.reshape(n, 1),
+                                      plain_env.dnn.reshape(n, -1), plain_env.done.reshape(n))
+        assert torch.equal(fused_env.dnn, plain_env.dnn) and torch.equal(fused_env.reward, plain_env.reward)
+    assert learners[0].replay.counter == learners[1].replay.counter == 3 * E * N
+    for name in learners[0].replay.bufs:
+        assert torch.equal(learners[0].replay.bufs[name], learners[1].replay.bufs[name]), name
