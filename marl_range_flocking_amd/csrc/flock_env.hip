@@ -216,12 +216,18 @@ __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __r
             yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
         else
             row = yr >= 0 && yr < Gc;
-        const int* pr = pre + (row ? yr : 0) * (Gc + 3);
+        const int* pr = pre + (row ? yr : 0) * (Gc + 2);
         const int s0 = row ? pr[cx] : 0, e0 = row ? pr[cx + 3] : 0;
+        // wave-uniform trip count (max range length over the wave) so the loop is a plain counted loop: a
+        // ballot-and-break loop made the compiler copy the whole key list around the back edge every iteration
+        int len = e0 - s0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) len = max(len, __shfl_xor(len, o, 64));
+        const int tmax = __builtin_amdgcn_readfirstlane(len);
 #pragma unroll 1
-        for (int c = s0;; c += 2) {
+        for (int t = 0; t < tmax; t += 2) {
+            const int c = s0 + t;
             const bool a0 = c < e0, a1 = c + 1 < e0;
-            if (__ballot(a0) == 0) break;
             const float4 q0 = ext[a0 ? c : 0];
             const float4 q1 = ext[a1 ? c + 1 : 0];
             const float d0 = pair_d2<PERIODIC>(xi, yi, q0.x, q0.y, box);
@@ -326,12 +332,12 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     float2* lpos = reinterpret_cast<float2*>(smem);               // [G][S]
     float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
     int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G]
-    // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][Gc*Gc], pre [G][Gc][Gc+3], rowlen [G][Gc]
-    const int Gc = p.cells;
+    // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][Gc*Gc], pre [G][npre]: exclusive prefix over
+    // the "virtual cells" of every row [ghost of column Gc-1, columns 0..Gc-1, ghost of column 0] (row-major)
+    const int Gc = p.cells, npre = Gc * (Gc + 2) + 1;
     float4* ext_all = reinterpret_cast<float4*>(smem + ((((size_t)(flags + p.G) - (size_t)smem) + 15) & ~(size_t)15));
     int* cnt_all = reinterpret_cast<int*>(ext_all + (CELL ? p.G * p.ecap : 0));
     int* pre_all = cnt_all + (CELL ? p.G * Gc * Gc : 0);
-    int* rowlen_all = pre_all + (CELL ? p.G * Gc * (Gc + 3) : 0);
 
     const int t = threadIdx.x;
     const int g = t / p.N;
@@ -347,6 +353,15 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
     float2 act_in = make_float2(0.0f, 0.0f);
+    float prev_obs[L - 2];  // fused replay insert: the previous observation row, loaded early (latency hidden)
+#pragma unroll
+    for (int s = 0; s < L - 2; ++s) prev_obs[s] = 0.0f;
+    if (active && p.r_state && (int64_t)a >= p.r_skip) {
+        const float* po = p.r_prev + a * p.k;
+#pragma unroll
+        for (int s = 0; s < L - 2; ++s)
+            if (s < p.k) prev_obs[s] = po[s];
+    }
     if (active) {
         const float2 pp = reinterpret_cast<const float2*>(p.pos)[a];
         x = pp.x;
@@ -460,8 +475,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     int cx = 0, cy = 0;
     if (CELL) {
         int* cnt = cnt_all + g * Gc * Gc;
-        int* pre = pre_all + g * Gc * (Gc + 3);
-        int* rowlen = rowlen_all + g * Gc;
+        int* pre = pre_all + g * npre;
         float4* ext = ext_all + g * p.ecap;
         int rank = 0;
         if (active) {
@@ -470,31 +484,38 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             rank = atomicAdd(&cnt[cy * Gc + cx], 1);
         }
         __syncthreads();
-        if (in_group && i < Gc) {  // row i: [ghost of column Gc-1][columns 0..Gc-1][ghost of column 0]
-            const int* cr = cnt + i * Gc;
-            int* pr = pre + i * (Gc + 3);
-            int run = PERIODIC ? cr[Gc - 1] : 0;
-            pr[0] = 0;
-            for (int c = 0; c < Gc; ++c) {
-                pr[c + 1] = run;
-                run += cr[c];
+        if (in_group && i < 64) {  // one wave per env (groups are wave-aligned whenever CELL): exclusive scan
+            const int W2 = Gc + 2, nv = npre - 1, per = (npre + 63) / 64;
+            auto vcount = [&](int f) {
+                const int yy = f / W2, e = f - yy * W2;
+                if (e == 0) return PERIODIC ? cnt[yy * Gc + Gc - 1] : 0;
+                if (e == W2 - 1) return PERIODIC ? cnt[yy * Gc] : 0;
+                return cnt[yy * Gc + e - 1];
+            };
+            int local = 0;
+            for (int q = 0; q < per; ++q) {
+                const int f = i * per + q;
+                if (f < nv) local += vcount(f);
             }
-            pr[Gc + 1] = run;
-            run += PERIODIC ? cr[0] : 0;
-            pr[Gc + 2] = run;
-            rowlen[i] = run;
-        }
-        __syncthreads();
-        if (in_group && i < Gc) {
-            int off = 0;
-            for (int r = 0; r < i; ++r) off += rowlen[r];
-            int* pr = pre + i * (Gc + 3);
-            for (int e = 0; e < Gc + 3; ++e) pr[e] += off;
+            int inc = local;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t2 = __shfl_up(inc, o, 64);
+                if (i >= o) inc += t2;
+            }
+            int run = inc - local;
+            for (int q = 0; q < per; ++q) {
+                const int f = i * per + q;
+                if (f < npre) {
+                    pre[f] = run;
+                    if (f < nv) run += vcount(f);
+                }
+            }
         }
         __syncthreads();
         if (active) {
             const float4 ent = make_float4(x, y, __int_as_float(i), 0.0f);
-            const int* pr = pre + cy * (Gc + 3);
+            const int* pr = pre + cy * (Gc + 2);
             ext[pr[cx + 1] + rank] = ent;
             if (PERIODIC && cx == Gc - 1) ext[pr[0] + rank] = ent;
             if (PERIODIC && cx == 0) ext[pr[Gc + 1] + rank] = ent;
@@ -509,8 +530,8 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         uint32_t key[L];
         bool ok = false;
         if (CELL)
-            ok = scan_cells<L, PERIODIC>(key, ext_all + g * p.ecap, pre_all + g * Gc * (Gc + 3), Gc, cx, cy, p.ib,
-                                         x, y, p.box, p.cw, p.cell_eps);
+            ok = scan_cells<L, PERIODIC>(key, ext_all + g * p.ecap, pre_all + g * npre, Gc, cx, cy, p.ib, x, y,
+                                         p.box, p.cw, p.cell_eps);
         if (!ok) scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
         knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);
     }
@@ -563,11 +584,10 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             if (p.r_state && (int64_t)a >= p.r_skip) {  // fused replay insert: row (start + a - skip) mod cap
                 int64_t row = p.r_start + (int64_t)a - p.r_skip;
                 if (row >= p.r_cap) row -= p.r_cap;
-                const float* po = p.r_prev + a * p.k;
 #pragma unroll
                 for (int s = 0; s < L - 2; ++s)
                     if (s < p.k) {
-                        p.r_state[row * p.k + s] = po[s];
+                        p.r_state[row * p.k + s] = prev_obs[s];
                         p.r_new[row * p.k + s] = dv[s];
                     }
                 reinterpret_cast<float2*>(p.r_action)[row] = act_in;
@@ -702,7 +722,7 @@ Cfg make_cfg(int E, int N, bool reset, int cells) {
         c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + c.G * sizeof(int);
     if (!reset && cells) {  // ext (2N float4, 16-B aligned) + cnt + pre + rowlen per env
         c.lds = (c.lds + 15) & ~(size_t)15;
-        c.lds += (size_t)c.G * (2 * N * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 3) + cells) * 4);
+        c.lds += (size_t)c.G * (2 * N * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 2) + 1) * 4);
     }
     return c;
 }
