@@ -94,10 +94,18 @@ typedef struct FlockScUpdate {
     float* workspace;
     unsigned* counters;
     float alpha, beta, gamma, beta1, beta2, eps;
+    float tau;       /* soft-update rate (update_network_parameters, :158-185) */
+    int update_rate; /* > 0 (with do_adam): flock_sc_actor_update also applies the soft updates when this agent's
+                        learn count (= actor_steps[agent] before the step) is a multiple of it, after both Adam
+                        steps, as Agent.learn() does (:152-154); 0: the caller runs them (flock_soft_update) */
 } FlockScUpdate;
 
 int64_t flock_sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2);
 int64_t flock_sc_update_size(void); /* sizeof(FlockScUpdate), for binding checks */
+/* learn() prologue in ONE launch: *agent_out = agent; idx[r] = Philox4x32-10(seed, counter, r) mod rows for
+ * r < B (uniform sampling with replacement, ReplayBuffer.sample_buffer, utils.py:65-76). idx may be NULL. */
+int flock_sc_prep(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
+                  int64_t* agent_out, int64_t agent);
 int flock_sc_critic_update(void* stream, const FlockScUpdate* u); /* :118-141 */
 int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (after the critic update) */
 

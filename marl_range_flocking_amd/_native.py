@@ -53,7 +53,8 @@ class FlockScUpdate(ctypes.Structure):
                                             "actor_steps")]
                 + [("actor_stride", ctypes.c_int64)]
                 + [(n, _c_void_p) for n in ("losses", "workspace", "counters")]
-                + [(n, _c_float) for n in ("alpha", "beta", "gamma", "beta1", "beta2", "eps")])
+                + [(n, _c_float) for n in ("alpha", "beta", "gamma", "beta1", "beta2", "eps", "tau")]
+                + [("update_rate", _c_int)])
 
 
 class FlockRingField(ctypes.Structure):
@@ -75,6 +76,7 @@ SIGNATURES.update({
                          ctypes.POINTER(FlockRingField)],
     "flock_sc_workspace_floats": [_c_int] * 5,
     "flock_sc_update_size": [],
+    "flock_sc_prep": [_c_void_p, _c_int, ctypes.c_int64, _c_u64, _c_u64, _c_void_p, _c_void_p, ctypes.c_int64],
     "flock_sc_critic_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_actor_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
 })

@@ -611,6 +611,8 @@ __global__ __launch_bounds__(256) void sc_a3(Ws w, RowArgs a) {
 // 2 = any strides (scalar).
 constexpr int kT = 32;
 constexpr int kKC = 512;
+constexpr int kGradKC = 128;  // the gradient kernels share one launch with ~400 LDS-free reduction blocks: a 34-KB
+                              // panel keeps 4 blocks per CU resident so the whole grid runs in one round
 constexpr int kPitch = 33;
 struct GemmP {
     const float* A;
@@ -620,6 +622,7 @@ struct GemmP {
     int M, N, K, sam, sak, sbk, sbn, ldc;
     int64_t relB;  // B and bias are agent-relative: + relB * (*agent)
     int tiles_n, tiles;
+    int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
 };
 struct GemmBatch {
     GemmP p[3];
@@ -627,13 +630,13 @@ struct GemmBatch {
     const int64_t* agent;
 };
 
-__host__ __device__ inline int gemm_kc(int K) {
-    const int k = K < kKC ? K : kKC;
+__host__ __device__ inline int gemm_kc(int K, int chunk = kKC) {
+    const int k = K < chunk ? K : chunk;
     return (k + 7) & ~7;
 }
 // A and B panels; the 4 partial tiles (4 x 16 x 64 floats) reuse the panel space once the MFMAs are done
-__host__ __device__ inline size_t gemm_lds_bytes(int K) {
-    const int panels = 2 * gemm_kc(K) * kPitch, red = 4 * 16 * 64;
+__host__ __device__ inline size_t gemm_lds_bytes(int K, int chunk = kKC) {
+    const int panels = 2 * gemm_kc(K, chunk) * kPitch, red = 4 * 16 * 64;
     return (size_t)(panels > red ? panels : red) * sizeof(float);
 }
 
@@ -713,15 +716,15 @@ template <int AV, int BV>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
                                           float (&out)[4]) {
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-    const int kcmax = gemm_kc(g.K);
+    const int kcmax = gemm_kc(g.K, g.kchunk);
     float* As = smem;
     float* Bs = smem + kcmax * kPitch;
     float* red = smem;  // after the last panel barrier
     f32x16 acc;
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
-    for (int k0 = 0; k0 < g.K; k0 += kKC) {
-        const int kc = gemm_kc(g.K - k0);
+    for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
+        const int kc = gemm_kc(g.K - k0, g.kchunk);
         load_panel<AV>(As, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k0, kc);
         load_panel<BV>(Bs, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k0, kc);
         __syncthreads();
@@ -794,26 +797,35 @@ struct GradAdam {
     unsigned* counter;
     float* loss;
     float lr, b1, b2, eps;
+    // soft updates after the Adam step (actor kernel): target = tau p + (1 - tau) target for every updated
+    // element, and the critic's self update (critic = tau c + (1 - tau) c) in soft_blocks extra blocks
+    float* target;
+    float* self_soft;
+    int64_t self_n;
+    int soft_rate, soft_blocks;
+    float tau, one_minus_tau;
 };
 
 struct AdamState {
-    float p, m, v;
+    float p, m, v, t;
 };
 __device__ __forceinline__ AdamState adam_load(const GradAdam& ga, int64_t i) {
-    return {ga.p[i], ga.m[i], ga.v[i]};
+    return {ga.p[i], ga.m[i], ga.v[i], ga.target ? ga.target[i] : 0.0f};
 }
 // torch.optim.Adam single-tensor path, identical to adam_dev_kernel (flock_learn.hip)
 __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamState s, float gi, float neg_step,
-                                           float bc2s) {
+                                           float bc2s, bool soft) {
     const float w1 = (float)(1.0 - (double)ga.b1), omb2 = (float)(1.0 - (double)ga.b2);
     float mi = s.m;
     mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
     float vi = s.v * ga.b2;
     vi = vi + (omb2 * gi) * gi;
     const float denom = __builtin_sqrtf(vi) / bc2s + ga.eps;
-    ga.p[i] = s.p + (neg_step * mi) / denom;
+    const float pn = s.p + (neg_step * mi) / denom;
+    ga.p[i] = pn;
     ga.m[i] = mi;
     ga.v[i] = vi;
+    if (soft && ga.target) ga.target[i] = ga.tau * pn + ga.one_minus_tau * s.t;  // soft_update_kernel mode 1
 }
 
 template <int AV, int BV>
@@ -821,15 +833,33 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     __shared__ float sh[2];
+    __shared__ int sh_soft;
     const int tid = threadIdx.x;
     const int64_t agent = ga.rel ? *ga.agent : 0;
     const int64_t base = ga.rel * agent;
-    if (ga.do_adam && tid == 0) {
-        const double st = (double)(ga.step[agent] + 1);
-        sh[0] = (float)(-(double)ga.lr / (1.0 - pow((double)ga.b1, st)));
-        sh[1] = (float)sqrt(1.0 - pow((double)ga.b2, st));
+    if (tid == 0) {
+        const int64_t step0 = ga.do_adam ? ga.step[agent] : 0;
+        sh_soft = ga.do_adam && ga.soft_rate > 0 && (step0 % ga.soft_rate) == 0;  // this learn's count
+        if (ga.do_adam) {
+            const double st = (double)(step0 + 1);
+            sh[0] = (float)(-(double)ga.lr / (1.0 - pow((double)ga.b1, st)));
+            sh[1] = (float)sqrt(1.0 - pow((double)ga.b2, st));
+        }
     }
-    if ((int)blockIdx.x < ga.g.tiles) {
+    if ((int)blockIdx.x >= ga.g.tiles + ga.nblk) {  // critic self soft update blocks (after its Adam step)
+        __syncthreads();
+        if (sh_soft && ga.self_soft) {
+            const int64_t b0 = (int64_t)(blockIdx.x - ga.g.tiles - ga.nblk) * 1024;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t e = b0 + q * 256 + tid;
+                if (e < ga.self_n) {
+                    const float c = ga.self_soft[e];
+                    ga.self_soft[e] = ga.tau * c + ga.one_minus_tau * c;
+                }
+            }
+        }
+    } else if ((int)blockIdx.x < ga.g.tiles) {
         {
             const int tm = blockIdx.x / ga.g.tiles_n, tn = blockIdx.x - tm * ga.g.tiles_n;
             const int wv = tid >> 6, l = tid & 63;
@@ -842,7 +872,7 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
                 const int mm = tm * kT + 8 * wv + 4 * (l >> 5) + q;
                 ok[q] = mm < ga.g.M && nn < ga.g.N;
                 e[q] = base + ga.w2_off + (int64_t)mm * ga.g.ldc + nn;
-                st[q] = (ok[q] && ga.do_adam) ? adam_load(ga, e[q]) : AdamState{0.f, 0.f, 0.f};
+                st[q] = (ok[q] && ga.do_adam) ? adam_load(ga, e[q]) : AdamState{0.f, 0.f, 0.f, 0.f};
             }
             float out[4];
             gemm_tile<AV, BV>(ga.g, ga.g.B, tm, tn, smem, out);  // (its barriers also publish sh[])
@@ -851,7 +881,7 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
             for (int q = 0; q < 4; ++q)
                 if (ok[q]) {
                     ga.grad[e[q]] = out[q];
-                    if (ga.do_adam) adam_store(ga, e[q], st[q], out[q], neg_step, bc2s);
+                    if (ga.do_adam) adam_store(ga, e[q], st[q], out[q], neg_step, bc2s, sh_soft != 0);
                 }
         }
     } else {
@@ -866,7 +896,7 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
         const bool prod = rp.mode == 1 || rp.mode == 2;
         const int64_t pe = base + rp.off + e;
         const AdamState st = (q == 0 && live && rp.mode != 3 && ga.do_adam) ? adam_load(ga, pe)
-                                                                              : AdamState{0.f, 0.f, 0.f};
+                                                                              : AdamState{0.f, 0.f, 0.f, 0.f};
         float acc = 0.0f;
         for (int r0 = q; r0 < ga.B; r0 += 16 * 16) {
             float dv[16], xv[16];
@@ -890,21 +920,18 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
                 *ga.loss = gsum * (1.0f / (float)ga.B);
             } else {
                 ga.grad[pe] = gsum;
-                if (ga.do_adam) adam_store(ga, pe, st, gsum, sh[0], sh[1]);
+                if (ga.do_adam) adam_store(ga, pe, st, gsum, sh[0], sh[1], sh_soft != 0);
             }
         }
     }
-    // the last block to finish advances the step counter (every block has read it by now)
-    if (ga.do_adam) {
-        __syncthreads();
-        if (tid == 0) {
-            __threadfence();
-            const unsigned prev = atomicAdd(ga.counter, 1u);
-            if (prev == gridDim.x - 1) {
-                ga.step[agent] += 1;
-                *ga.counter = 0u;
-                __threadfence();
-            }
+    // the last block to arrive advances the step counter. No fence: every block's thread 0 consumed its load of
+    // *step (the bias corrections) before its relaxed atomic add, and the increment only has to be visible to the
+    // NEXT launch (kernel boundary). A device-scope fence here costs an L2 writeback per block on gfx950.
+    if (ga.do_adam && tid == 0) {
+        const unsigned prev = atomicAdd(ga.counter, 1u);
+        if (prev == gridDim.x - 1) {
+            ga.step[agent] += 1;
+            *ga.counter = 0u;
         }
     }
 }
@@ -918,6 +945,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.M = M; g.N = N; g.K = K; g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc; g.relB = relB;
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
+    g.kchunk = kKC;
     return g;
 }
 
@@ -989,8 +1017,8 @@ int launch_grad_adam_v(hipStream_t st, const GradAdam& ga, dim3 grid, size_t lds
 
 int launch_grad_adam(hipStream_t st, const GradAdam& ga) {
     if (ga.nblk > kMaxRedBlocks) return fail(-2, "flock_sc: too many reduction blocks (fc1 * in_dim too large)");
-    const dim3 grid(ga.g.tiles + ga.nblk);
-    size_t lds = gemm_lds_bytes(ga.g.K);
+    const dim3 grid(ga.g.tiles + ga.nblk + ga.soft_blocks);
+    size_t lds = gemm_lds_bytes(ga.g.K, ga.g.kchunk);
     if (lds < 16 * kRedElems * sizeof(float)) lds = 16 * kRedElems * sizeof(float);
     return gemm_variant(ga.g) == 2 ? launch_grad_adam_v<1, 1>(st, ga, grid, lds)
                                    : launch_grad_adam_v<2, 2>(st, ga, grid, lds);
@@ -1078,9 +1106,48 @@ size_t tails_lds(int na, int H2) {
     return (size_t)(round4(crit_tail_len(na, H2)) + round4(act_tail_len(na, H2))) * sizeof(float);
 }
 
+// learn() prologue: the agent index and the minibatch rows (Philox4x32-10, counter = (learn counter, row))
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+
+__global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
+                                               int64_t* agent_out, int64_t agent) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r == 0) *agent_out = agent;
+    if (idx && r < B) {
+        const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
+        const uint64_t u = ((uint64_t)q.x << 32) | q.y;
+        idx[r] = (int64_t)(u % (uint64_t)rows);
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int flock_sc_prep(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
+                  int64_t* agent_out, int64_t agent) {
+    if (!agent_out) return fail(-3, "flock_sc_prep: NULL agent pointer");
+    if (idx && (B < 1 || rows < 1)) return fail(-5, "flock_sc_prep: need B >= 1 and rows >= 1");
+    const int blocks = idx ? (B + 255) / 256 : 1;
+    hipLaunchKernelGGL(sc_prep, dim3(blocks), dim3(256), 0, (hipStream_t)stream, B, rows, seed, counter, idx,
+                       agent_out, agent);
+    return launched();
+}
 
 int64_t flock_sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2) {
     return ws_layout(B, in_dim, n_actions, fc1, fc2, nullptr, nullptr);
@@ -1128,6 +1195,7 @@ int flock_sc_critic_update(void* stream, const FlockScUpdate* u) {
 
     GradAdam ga;
     ga.g = gemm_p(w.DZ2, w.H1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);  // dW2 = dZ2^T H1
+    ga.g.kchunk = kGradKC;
     ga.w2_off = co.W2;
     ga.nred = 0;
     ga.nblk = 0;
@@ -1152,6 +1220,8 @@ int flock_sc_critic_update(void* stream, const FlockScUpdate* u) {
     ga.counter = u->counters;
     ga.loss = u->losses + 1;
     ga.lr = u->beta; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    ga.target = nullptr; ga.self_soft = nullptr; ga.self_n = 0; ga.soft_rate = 0; ga.soft_blocks = 0;
+    ga.tau = 0.0f; ga.one_minus_tau = 1.0f;
     return launch_grad_adam(st, ga);
 }
 
@@ -1194,6 +1264,7 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
 
     GradAdam ga;
     ga.g = gemm_p(w.ADZ2, w.AH1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);
+    ga.g.kchunk = kGradKC;
     ga.w2_off = ao.W2;
     ga.nred = 0;
     ga.nblk = 0;
@@ -1216,6 +1287,14 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
     ga.counter = u->counters + 1;
     ga.loss = u->losses;
     ga.lr = u->alpha; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    const bool soft = u->do_adam && u->update_rate > 0;
+    ga.soft_rate = soft ? u->update_rate : 0;
+    ga.target = soft ? u->actors_target : nullptr;  // agent-relative like p
+    ga.self_soft = soft ? u->critic : nullptr;
+    ga.self_n = co.total;
+    ga.soft_blocks = soft ? (int)((co.total + 1023) / 1024) : 0;
+    ga.tau = u->tau;
+    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
     return launch_grad_adam(st, ga);
 }
 

@@ -88,6 +88,8 @@ class SharedCriticLearner:
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
         self.batch_size, self.update_rate = batch_size, update_rate
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
+        self.seed = int(seed)
+        self._learn_calls = 0
         self.critic = FlatParams(critic_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=1)
         self.actors = FlatParams(actor_shapes(input_dim, fc1, fc2, n_actions), self.device, agents=n_agents,
                                  agent_major=True, target=True, agent_pad=64)
@@ -141,9 +143,11 @@ class SharedCriticLearner:
                       actors_exp_avg_sq=_p(A.exp_avg_sq), actors_target=_p(A.target),
                       actor_steps=_p(self.actor_steps), actor_stride=A.per_agent, losses=_p(self.losses),
                       workspace=_p(self.sc_workspace), counters=_p(self.sc_counters), alpha=self.alpha,
-                      beta=self.beta, gamma=self.gamma, beta1=0.9, beta2=0.999, eps=1e-8)
+                      beta=self.beta, gamma=self.gamma, beta1=0.9, beta2=0.999, eps=1e-8, tau=self.tau,
+                      update_rate=self.update_rate)
+        # single GPU: the soft updates run inside the actor's gradient kernel (device-side count condition)
         self._sc = _native.FlockScUpdate(**fields)
-        self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0))  # data-parallel: grads only
+        self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0, update_rate=0))  # data-parallel
 
     def _fused_update(self, u=None):
         lib = _native.lib()
@@ -304,14 +308,21 @@ class SharedCriticLearner:
         B = self.batch_size
         if self.replay.counter < B:
             return 0, 0, False
+        self._learn_calls += 1
+        if self.fused:
+            # one launch: agent index + (unless given) B rows uniform with replacement (utils.py:65-76)
+            if idx is not None:
+                self.static_idx.copy_(torch.as_tensor(idx).to(self.device))
+            rc = _native.lib().flock_sc_prep(_stream(self.device), B, len(self.replay), self.seed,
+                                             self._learn_calls, None if idx is not None else _p(self.static_idx),
+                                             _p(self.static_agent), int(agent))
+            _native.check(rc, "flock_sc_prep", learn=True)
+            self._run_fused(agent)
+            return self._finish_learn(agent, soft_in_kernel=not self.distributed)
         if idx is None:                                                       # utils.py:65-76 (with replacement)
             torch.randint(0, len(self.replay), (B,), device=self.device, generator=self.gen, out=self.static_idx)
         else:
             self.static_idx.copy_(torch.as_tensor(idx).to(self.device))
-        if self.fused:
-            self.static_agent.fill_(agent)
-            self._run_fused(agent)
-            return self._finish_learn(agent)
         lo, hi = self.actors.agent_range(agent)
         A, S = self.actors, self.scratch
         with torch.no_grad():
@@ -326,8 +337,8 @@ class SharedCriticLearner:
             self.actor_steps[agent:agent + 1].copy_(S.step_dev)
         return self._finish_learn(agent)
 
-    def _finish_learn(self, agent):
-        if self.count[agent] % self.update_rate == 0:                         # :152-154
+    def _finish_learn(self, agent, soft_in_kernel=False):
+        if self.count[agent] % self.update_rate == 0 and not soft_in_kernel:                         # :152-154
             self.critic.soft_update(self.tau, mode=1, self_update=True)       # :172-178 (critic is its own target)
             self.actors.soft_update(self.tau, mode=1, agent=agent)            # :180-185
         self.count[agent] += 1
