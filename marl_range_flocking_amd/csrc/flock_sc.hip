@@ -141,10 +141,23 @@ struct RowArgs {
 
 // ---------------------------------------------------------------------------------------------------------------
 // helpers
+// wave64 all-reduce sum on DPP (quad_perm, row half-mirror, row mirror: every lane of a 16-lane row adds commutative
+// pairs, so the row sum is bitwise identical in all of its lanes) + readlane of the four row sums (a scalar, so the
+// result is identical in every lane). Replaces a 6-step ds_bpermute butterfly (LDS-path latency per step).
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    v = dpp_add<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add<0x141>(v);  // row_half_mirror
+    v = dpp_add<0x140>(v);  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 __device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
 __device__ __forceinline__ float rsqrt_rn(float x) { return 1.0f / __builtin_sqrtf(x); }
