@@ -1,14 +1,16 @@
 """Headline benchmark: agent-steps/sec, gym_flock_v2 (periodic) 256 agents x 4096 envs per MI355X (BASELINE config 3).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,4,5}]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
         bench.py --gpus N --steps K --warmup W
 
 One process per GPU. Envs are independent, so each rank steps its own 4096 envs with no data-path collective
 (weak scaling); the only collectives are the barrier around the timed region and the max-over-ranks of its time.
-A "step" = one vectorized env step of all the rank's envs (kinematics, boundary, all-pairs sensing, kNN obs,
-collision, reward, done: one HIP launch) plus, with --learner shared_critic, one shared-critic learn() (B=256).
-Inputs (state, a pool of synthetic actions) are resident in HBM before the timed region starts.
+A "step" = one vectorized env step of all the rank's envs (kinematics, boundary, sensing, kNN obs, collision,
+reward, done: one HIP launch) plus the config's learner: config 3 (default) inserts every transition into the
+shared-critic replay ring inside that same launch and runs one learn() (B=256); configs 4 / 5 insert every env's
+transition and run VDN / RNN-MADDPG train() every 150 / 250 steps. Inputs (state, a pool of synthetic actions)
+are resident in HBM before the timed region starts; the first update (graph capture) happens before it.
 
 Rank 0 prints ONE JSON line. Extra fields: roofline (dominant kernel, HIP events on the launch stream; algorithmic
 bytes 93 B/agent-step), valu (same kernel against the f32 VALU roof, which is what binds it), and
@@ -34,18 +36,37 @@ OPS_PER_PAIR = {True: 12, False: 7}  # algorithmic VALU ops per agent pair (SURV
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 200; configs 4/5: 300/500, "
+                                                                 "a multiple of the training cadence)")
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--agents", type=int, default=256)
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--k", type=int, default=4)
-    ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uw_discrete", "flock"])
-    ap.add_argument("--learner", default="shared_critic", choices=["none", "shared_critic"],
-                    help="config 3 pairs the env with the shared-critic update (default)")
+    ap.add_argument("--variant", default=None, choices=["v2", "uw", "uw_discrete", "flock"])
+    ap.add_argument("--learner", default=None, choices=["none", "shared_critic", "vdn", "maddpg_rnn"],
+                    help="default: the config's learner (config 3: shared_critic)")
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5],
+                    help="BASELINE.json config (per-GPU slice): 2 uw 64x1024 env only; 3 v2 256x4096 + shared "
+                         "critic (default); 4 uw_discrete 512x1024 + VDN every 150 steps; 5 v2 1024x2048 + "
+                         "RNN-MADDPG every 250 steps. --envs/--agents/--variant/--learner override it")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    c = CONFIGS[args.config]
+    for key in ("envs", "agents", "variant", "learner", "steps"):
+        if getattr(args, key) is None:
+            setattr(args, key, c[key])
+    return args
+
+
+# BASELINE.json configs, per-GPU slice (configs 4 and 5 are 8-GPU configs: 8192 / 16384 envs over 8 ranks)
+CONFIGS = {
+    2: dict(variant="uw", agents=64, envs=1024, learner="none", steps=200),
+    3: dict(variant="v2", agents=256, envs=4096, learner="shared_critic", steps=200),
+    4: dict(variant="uw_discrete", agents=512, envs=1024, learner="vdn", steps=300),
+    5: dict(variant="v2", agents=1024, envs=2048, learner="maddpg_rnn", steps=500),
+}
 
 
 def setup_dist(args):
@@ -106,6 +127,76 @@ def cpu_baseline(args, box, seconds):
                       f"vectorized steps ({el:.1f} s), single thread, on this box's host"}
 
 
+class VDNBench:
+    """BASELINE config 4 learner: every env's team transition (obs, action ids, rewards, next obs, any_done) is put
+    into the VDN replay ring each vectorized step (learners/vdn/train_flock.py:88-104), and VDN train() (10 updates
+    of B=32 chunks of 10, clip 5, Adam) runs every 150 vectorized steps (the reference's episode length, :98)."""
+
+    every = 150
+
+    def __init__(self, env, dev, seed=0):
+        from marl_range_flocking_amd.learners.vdn import VDNLearner
+
+        self.env = env
+        group = torch.distributed.group.WORLD if torch.distributed.is_initialized() else None
+        self.learner = VDNLearner(env.N, env.k, 10, device=dev, seed=seed, dist_group=group)
+        self.prev = None
+
+    def describe(self):
+        return (f"VDN train() every {self.every} vectorized steps (update_iter 10, B 32, chunk 10); all "
+                f"{self.env.E} team transitions per step inserted into a 50k-row device replay ring"
+                + ("; gradient all-reduce over RCCL" if self.learner.distributed else ""))
+
+    def before(self, s):
+        self.prev = self.env.dnn
+        return None
+
+    def after(self, s, a):
+        env = self.env
+        self.learner.put(self.prev, a, env.reward, env.dnn, env.any_done)
+        if (s + 1) % self.every == 0 and self.learner.size() > self.learner.chunk:
+            self.learner.train()
+
+    def prime(self):
+        self.learner.train()
+
+
+class MADDPGBench:
+    """BASELINE config 5 learner: each env's record (actor obs, next obs, actions, critic state, next state,
+    rewards, dones) goes into the RNN-MADDPG replay ring every vectorized step (main.py:24-59), and train()
+    (B=128 chunks of 10, per-agent recurrent critics over all agents' obs and actions) runs every 250 steps
+    (main.py:103)."""
+
+    every = 250
+
+    def __init__(self, env, dev, seed=0):
+        from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+        self.env = env
+        group = torch.distributed.group.WORLD if torch.distributed.is_initialized() else None
+        self.learner = MADDPGLearner(env.N, env.k, recurrent=True, device=dev, seed=seed, dist_group=group)
+        self.prev = None
+
+    def describe(self):
+        return (f"RNN-MADDPG train() every {self.every} vectorized steps (B 128, chunk 10, {self.env.N} critics "
+                f"400/300); all {self.env.E} env records per step inserted into a 45k-row device replay ring"
+                + ("; critic gradient all-reduce over RCCL" if self.learner.distributed else ""))
+
+    def before(self, s):
+        self.prev = self.env.dnn
+        return None
+
+    def after(self, s, a):
+        env, L = self.env, self.learner
+        L.add_record(self.prev, env.dnn, a, self.prev, env.dnn, env.reward, env.done)
+        if (s + 1) % self.every == 0 and L.check_buffer_size():
+            L.train()
+
+    def prime(self):
+        if self.learner.check_buffer_size():
+            self.learner.train()
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
@@ -132,40 +223,40 @@ def main():
         else:
             pool.append((torch.rand(E, N, 2, device=dev, generator=g) * 2 - 1).contiguous())
 
-    learner = None
+    hook = None
     if args.learner == "shared_critic":
         from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
-        learner = SharedCriticBench(env, device=dev, seed=1234 + rank)
+        hook = SharedCriticBench(env, device=dev, seed=1234 + rank)
+    elif args.learner == "vdn":
+        hook = VDNBench(env, dev, seed=1234 + rank)
+    elif args.learner == "maddpg_rnn":
+        hook = MADDPGBench(env, dev, seed=1234 + rank)
 
-    def one_step(s):
+    def one_step(s, ev=None):
         a = pool[s % len(pool)]
-        if learner is not None:
-            learner.step(s, a)
-        else:
-            env.step(a)
+        ring = hook.before(s) if hook is not None else None
+        if ev is not None:
+            ev[0].record(stream)
+        env.step(a, ring=ring) if ring is not None else env.step(a)
+        if ev is not None:
+            ev[1].record(stream)
+        if hook is not None:
+            hook.after(s, a)
 
+    stream = torch.cuda.current_stream(dev)
     for s in range(args.warmup):
         one_step(s)
+    if hook is not None:
+        hook.prime()  # graph capture / first update outside the timed region
     torch.cuda.synchronize(dev)
-    stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
 
     barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for s in range(args.steps):
-        a = pool[s % len(pool)]
-        if learner is not None:  # env step + fused replay insert (timed), then learn()
-            ring = learner.learner.replay_slots(E * N)
-            ev[s][0].record(stream)
-            env.step(a, ring=ring)
-            ev[s][1].record(stream)
-            learner.learner.learn(s % learner.learner.n_agents)
-        else:
-            ev[s][0].record(stream)
-            env.step(a)
-            ev[s][1].record(stream)
+        one_step(args.warmup + s, ev[s])
     torch.cuda.synchronize(dev)
     barrier(world)
     el = time.perf_counter() - t0
@@ -177,7 +268,7 @@ def main():
 
     total_agent_steps = world * E * N * args.steps
     value = total_agent_steps / el
-    fused_ring = learner is not None
+    fused_ring = args.learner == "shared_critic"
     bpa = BYTES_PER_AGENT_STEP[args.variant] + (RING_BYTES_PER_AGENT_STEP if fused_ring else 0)
     bytes_launch = bpa * E * N
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
@@ -190,6 +281,8 @@ def main():
     periodic = cfg.resolved().periodic
     ops_launch = OPS_PER_PAIR[periodic] * (N - 1) * E * N
     valu_t = ops_launch / (kern_ms * 1e-3) / 1e12
+    c = CONFIGS[args.config]
+    is_config = (args.variant, N, E, args.learner) == (c["variant"], c["agents"], c["envs"], c["learner"])
     line = {
         "metric": "agent-steps/sec at 256 agents x 4096 envs; 1/2/4/8 MI355X",
         "value": value,
@@ -205,14 +298,15 @@ def main():
         "data": "synthetic (uniform random positions/headings at main.py density, random actions; no checkpoints)",
         "config": {
             "workload": f"gym_flock_{args.variant} step, {N} agents x {E} envs per GPU"
-                        + (" (BASELINE config 3)" if (args.variant, N, E) == ("v2", 256, 4096) else ""),
+                        + (f" (BASELINE config {args.config})" if is_config else ""),
             "agents": N, "envs_per_gpu": E, "k": k, "box": box, "periodic": periodic,
-            "learner": ("none: env step only" if learner is None else learner.describe()),
+            "learner": ("none: env step only" if hook is None else hook.describe()),
             "parallelism": f"env-shard x{world}",
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "step_kernel<6,periodic>" + (" + fused replay insert" if fused_ring else ""),
+                     "kernel": f"step_kernel<{k + 2},{'periodic' if periodic else 'euclidean'}"
+                               f"{',cells' if N >= 128 else ''}>" + (" + fused replay insert" if fused_ring else ""),
                      "kernel_ms": kern_ms, "bytes_per_agent_step": bpa},
         "allpairs_equivalent": {"rate": valu_t, "unit": "Tlane-op/s", "ops_per_pair": OPS_PER_PAIR[periodic],
                                 "note": "all-pairs sensing work the step replaces per second; the cell-list kNN "

@@ -383,12 +383,20 @@ class SharedCriticBench:
                 f"device replay ring per step by the env kernel itself"
                 + ("; critic + actor gradient all-reduce over RCCL per learn)" if self.learner.distributed else ")"))
 
+    # bench.py hook interface: before(s) -> ring for the fused env step; after(s, a) -> learn(); prime()
+    def before(self, s):
+        return self.learner.replay_slots(self.env.E * self.env.N)
+
+    def after(self, s, action):
+        self.learner.learn(s % self.learner.n_agents)
+
+    def prime(self):
+        pass
+
     def step(self, s, action):
         """One bench step with the replay insert fused into the env kernel (flock_step_v2_store), then learn()."""
-        env = self.env
-        ring = self.learner.replay_slots(env.E * env.N)
-        env.step(action, ring=ring)
-        self.learner.learn(s % self.learner.n_agents)
+        self.env.step(action, ring=self.before(s))
+        self.after(s, action)
 
     def after_env_step(self, s, action):
         env = self.env
