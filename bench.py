@@ -86,12 +86,13 @@ def barrier(world):
         torch.distributed.barrier()
 
 
-def cpu_baseline(args, box, seconds):
-    """The C oracle (oracle/flock_oracle.c, 1 thread) stepping a sample of the same workload sequentially."""
+def _cpu_run(args, box, seconds, seed, E_s=8):
+    """One thread: the C oracle stepping E_s envs of the workload sequentially for `seconds` (ctypes releases the
+    GIL during each C call, so several of these run in parallel)."""
     from oracle import oracle
 
-    E_s, N, k = 8, args.agents, args.k
-    rng = np.random.default_rng(0)
+    N, k = args.agents, args.k
+    rng = np.random.default_rng(seed)
     pos = rng.uniform(0, box, (E_s, N, 2)).astype(np.float32)
     head = rng.uniform(0, 1.5 * np.pi, (E_s, N)).astype(np.float32)
     prev = np.zeros((E_s, N), np.float32)
@@ -121,10 +122,25 @@ def cpu_baseline(args, box, seconds):
         n += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": E_s * N * n / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/flock_oracle.c {args.variant} step, {E_s} envs x {N} agents, {n} sequential "
-                      f"vectorized steps ({el:.1f} s), single thread, on this box's host"}
+            return E_s * N * n, el
+
+
+def cpu_baseline(args, box, seconds, threads=16):
+    """The C oracle (oracle/flock_oracle.c) on the host: 1 thread, then `threads` threads (the GPU box's CPU share)
+    each stepping its own 8 envs; bounded sample of the same workload."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    half = seconds / 2
+    s1, t1 = _cpu_run(args, box, half, 0)
+    with ThreadPoolExecutor(threads) as ex:  # 32 envs per C call: the per-call Python work is negligible
+        res = list(ex.map(lambda i: _cpu_run(args, box, half, 1 + i, E_s=32), range(threads)))
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {"value": steps / wall, "unit": "agent-steps/s", "cores": threads, "kind": "port",
+            "value_1thread": s1 / t1,
+            "sample": f"oracle/flock_oracle.c {args.variant} step of {args.agents}-agent envs, sequential vectorized "
+                      f"steps for {half:.0f} s: 1 thread x 8 envs ({s1 / t1:.3g} agent-steps/s), {threads} threads x "
+                      f"32 envs ({steps / wall:.3g} agent-steps/s); this box's host"}
 
 
 class VDNBench:
