@@ -14,13 +14,15 @@
 //            Step variants with N >= 128 scan a CELL LIST instead of all N (phase 3c below).
 //   phase 3c agents are binned into a Gc x Gc grid over [0, box]^2 (Gc = floor(sqrt(N / 4))) by an LDS counting
 //            sort into an extended cell-sorted array of (x, y, j) in which every cell row also carries ghost copies
-//            of its last column (in front) and first column (behind) when the box is periodic, so each agent's 3x3
-//            neighbourhood is exactly 3 contiguous ranges (one per row). The lane runs the same insertion network
-//            over those ~9 cells (~36 candidates at 4 per cell instead of N) and keeps the result only if it is
-//            PROVABLY the full scan's: every unscanned agent lies at least m = the distance to the neighbourhood's
-//            edge away, so if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety factor) exceeds the L-th key,
-//            no unscanned key can enter the top L. Otherwise the lane falls back to the full scan. Keys carry j, so
-//            the order of agents within a cell (LDS atomics) never matters.
+//            of its last two columns (in front) and first two columns (behind) when the box is periodic, so each
+//            agent's 3x3 (or 5x5) neighbourhood is exactly 3 (5) contiguous ranges, one per row. The lane runs the
+//            same insertion network over its 3x3 cells (~36 candidates at 4 per cell instead of N) and keeps the
+//            result only if it is PROVABLY the full scan's: every unscanned agent lies at least m = the distance to
+//            the neighbourhood's edge away, so if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety factor)
+//            exceeds the L-th key, no unscanned key can enter the top L. Lanes whose proof fails take the 5x5 result
+//            (same proof, m >= 2 cells), and only then the full scan. An ambiguous bucket (phase 4) is rescanned
+//            exactly over the same neighbourhood, which the proof shows to contain every candidate of that bucket.
+//            Keys carry j, so the order of agents within a cell (LDS atomics) never matters.
 //   phase 4  exactness: the k+1 winners are re-sorted by their exact (d2, j); if the (k+2)-th key shares the
 //            truncated-d2 bucket of the (k+1)-th, the lane falls back to an exact (d2, j) rescan (rare). The
 //            result is the ascending (d2, j) order — a valid tie resolution of the reference's
@@ -199,25 +201,27 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
     }
 }
 
-// phase 3c: the 3x3 cell neighbourhood (3 contiguous ranges of the extended cell-sorted array); returns true when
-// the top-L keys are provably those of the full scan (see the file header)
+// phase 3c: the (2R+1) x (2R+1) cell neighbourhood (2R+1 contiguous ranges of the extended cell-sorted array, R = 1
+// or 2); returns true when the top-L keys are provably those of the full scan (see the file header). Uses
+// wave-wide reductions: call it with every lane of the wave active.
 template <int L, bool PERIODIC>
 __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __restrict__ ext,
-                                           const int* __restrict__ pre, int Gc, int cx, int cy, int ib, float xi,
-                                           float yi, float box, float cw, float eps) {
+                                           const int* __restrict__ pre, int Gc, int cx, int cy, int R, int ib,
+                                           float xi, float yi, float box, float cw, float eps) {
     const uint32_t hi_mask = ~((1u << ib) - 1u);
+    const int W2 = Gc + 4;
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #pragma unroll 1
-    for (int r = 0; r < 3; ++r) {
-        int yr = cy + r - 1;
+    for (int r = -R; r <= R; ++r) {
+        int yr = cy + r;
         bool row = true;
         if (PERIODIC)
             yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
         else
             row = yr >= 0 && yr < Gc;
-        const int* pr = pre + (row ? yr : 0) * (Gc + 2);
-        const int s0 = row ? pr[cx] : 0, e0 = row ? pr[cx + 3] : 0;
+        const int* pr = pre + (row ? yr : 0) * W2;
+        const int s0 = row ? pr[cx + 2 - R] : 0, e0 = row ? pr[cx + 3 + R] : 0;
         // wave-uniform trip count (max range length over the wave) so the loop is a plain counted loop: a
         // ballot-and-break loop made the compiler copy the whole key list around the back edge every iteration
         int len = e0 - s0;
@@ -238,19 +242,65 @@ __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __r
             key_insert<L>(key, a1 ? k1 : kEmpty);
         }
     }
-    // every agent outside the scanned 3x3 block is at least m away (periodic or not)
-    const float lx = (float)(cx - 1) * cw, rx = (float)(cx + 2) * cw;
-    const float ly = (float)(cy - 1) * cw, ry = (float)(cy + 2) * cw;
+    // every agent outside the scanned block is at least m away (periodic or not)
+    const float lx = (float)(cx - R) * cw, rx = (float)(cx + R + 1) * cw;
+    const float ly = (float)(cy - R) * cw, ry = (float)(cy + R + 1) * cw;
     const float m = fminf(fminf(xi - lx, rx - xi), fminf(yi - ly, ry - yi)) - eps;
     const float bound = m > 0.0f ? (m * m) * 0.99998f : 0.0f;
     return (__float_as_uint(bound) & hi_mask) > key[L - 1];
 }
 
-// phase 4: exact (d2, j) order of the W best keys (or an exact rescan when the (k+1)/(k+2) bucket is ambiguous)
+// exact ordered insertion of (d2, j) into the W best, lexicographic (any visiting order)
+template <int W>
+__device__ __forceinline__ void insert_exact(float (&bd)[W], int (&bj)[W], float d, int j) {
+    if (d < bd[W - 1] || (d == bd[W - 1] && j < bj[W - 1])) {
+        bool lt[W];
+#pragma unroll
+        for (int s = 0; s < W; ++s) lt[s] = d < bd[s] || (d == bd[s] && j < bj[s]);
+#pragma unroll
+        for (int s = W - 1; s >= 1; --s) {
+            bd[s] = lt[s - 1] ? bd[s - 1] : (lt[s] ? d : bd[s]);
+            bj[s] = lt[s - 1] ? bj[s - 1] : (lt[s] ? j : bj[s]);
+        }
+        bd[0] = lt[0] ? d : bd[0];
+        bj[0] = lt[0] ? j : bj[0];
+    }
+}
+
+// exact rescan of an ambiguous bucket over the scanned neighbourhood only: when scan_cells proved its top L, every
+// unscanned key exceeds the L-th key, so every unscanned d2 exceeds every d2 of the ambiguous bucket and the exact
+// top k+1 by (d2, j) lies in the scanned ranges (per-lane loops: no wave-wide operations)
 template <int L, bool PERIODIC>
-__device__ __forceinline__ void knn_finalize(const uint32_t (&key)[L], const float2* __restrict__ cand, int N, int k,
+__device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)[L - 1],
+                                                   const float4* __restrict__ ext, const int* __restrict__ pre,
+                                                   int Gc, int cx, int cy, int R, float xi, float yi, float box) {
+    constexpr int W = L - 1;
+    const int W2 = Gc + 4;
+#pragma unroll
+    for (int s = 0; s < W; ++s) {
+        bd[s] = __builtin_inff();
+        bj[s] = 0x7fffffff;
+    }
+    for (int r = -R; r <= R; ++r) {
+        int yr = cy + r;
+        if (PERIODIC)
+            yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
+        else if (yr < 0 || yr >= Gc)
+            continue;
+        const int* pr = pre + yr * W2;
+        for (int c = pr[cx + 2 - R]; c < pr[cx + 3 + R]; ++c) {
+            const float4 q = ext[c];
+            insert_exact<W>(bd, bj, pair_d2<PERIODIC>(xi, yi, q.x, q.y, box), __float_as_int(q.z));
+        }
+    }
+}
+
+// phase 4: exact (d2, j) order of the W best keys, or (ambiguous (k+1)/(k+2) bucket) an exact rescan of all N
+// candidates when full_rescan, else return true and let the caller rescan its neighbourhood
+template <int L, bool PERIODIC>
+__device__ __forceinline__ bool knn_finalize(const uint32_t (&key)[L], const float2* __restrict__ cand, int N, int k,
                                              int ib, float xi, float yi, float box, float (&bd)[L - 1],
-                                             int (&bj)[L - 1]) {
+                                             int (&bj)[L - 1], bool full_rescan = true) {
     constexpr int W = L - 1;
     const uint32_t lo_mask = (1u << ib) - 1u, hi_mask = ~lo_mask;
     // (k+1)-th and (k+2)-th smallest keys (k is a runtime value <= L-2; static-index select, no scratch)
@@ -289,7 +339,7 @@ __device__ __forceinline__ void knn_finalize(const uint32_t (&key)[L], const flo
                 bj[s] = tj;
             }
         }
-    } else {
+    } else if (full_rescan) {
         // exact rescan: branch-free ordered insertion of (d2, j); ascending j + strict '<' keeps lower j first
 #pragma unroll
         for (int s = 0; s < W; ++s) {
@@ -312,7 +362,10 @@ __device__ __forceinline__ void knn_finalize(const uint32_t (&key)[L], const flo
                 bj[0] = lt[0] ? jj : bj[0];
             }
         }
+    } else {
+        return true;
     }
+    return false;
 }
 
 template <int L, bool PERIODIC>
@@ -333,8 +386,8 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
     int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G]
     // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][Gc*Gc], pre [G][npre]: exclusive prefix over
-    // the "virtual cells" of every row [ghost of column Gc-1, columns 0..Gc-1, ghost of column 0] (row-major)
-    const int Gc = p.cells, npre = Gc * (Gc + 2) + 1;
+    // the "virtual cells" of every row [ghosts of columns Gc-2, Gc-1, columns 0..Gc-1, ghosts of columns 0, 1]
+    const int Gc = p.cells, npre = Gc * (Gc + 4) + 1;
     float4* ext_all = reinterpret_cast<float4*>(smem + ((((size_t)(flags + p.G) - (size_t)smem) + 15) & ~(size_t)15));
     int* cnt_all = reinterpret_cast<int*>(ext_all + (CELL ? p.G * p.ecap : 0));
     int* pre_all = cnt_all + (CELL ? p.G * Gc * Gc : 0);
@@ -485,12 +538,12 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         }
         __syncthreads();
         if (in_group && i < 64) {  // one wave per env (groups are wave-aligned whenever CELL): exclusive scan
-            const int W2 = Gc + 2, nv = npre - 1, per = (npre + 63) / 64;
+            const int W2 = Gc + 4, nv = npre - 1, per = (npre + 63) / 64;
             auto vcount = [&](int f) {
                 const int yy = f / W2, e = f - yy * W2;
-                if (e == 0) return PERIODIC ? cnt[yy * Gc + Gc - 1] : 0;
-                if (e == W2 - 1) return PERIODIC ? cnt[yy * Gc] : 0;
-                return cnt[yy * Gc + e - 1];
+                if (e < 2) return PERIODIC ? cnt[yy * Gc + Gc - 2 + e] : 0;        // ghosts of Gc-2, Gc-1
+                if (e >= Gc + 2) return PERIODIC ? cnt[yy * Gc + e - Gc - 2] : 0;  // ghosts of 0, 1
+                return cnt[yy * Gc + e - 2];
             };
             int local = 0;
             for (int q = 0; q < per; ++q) {
@@ -515,10 +568,10 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         __syncthreads();
         if (active) {
             const float4 ent = make_float4(x, y, __int_as_float(i), 0.0f);
-            const int* pr = pre + cy * (Gc + 2);
-            ext[pr[cx + 1] + rank] = ent;
-            if (PERIODIC && cx == Gc - 1) ext[pr[0] + rank] = ent;
-            if (PERIODIC && cx == 0) ext[pr[Gc + 1] + rank] = ent;
+            const int* pr = pre + cy * (Gc + 4);
+            ext[pr[cx + 2] + rank] = ent;
+            if (PERIODIC && cx >= Gc - 2) ext[pr[cx - Gc + 2] + rank] = ent;  // ghost in front (Gc >= 5)
+            if (PERIODIC && cx <= 1) ext[pr[Gc + 2 + cx] + rank] = ent;       // ghost behind
         }
         __syncthreads();
     }
@@ -529,11 +582,32 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     if (active) {
         uint32_t key[L];
         bool ok = false;
-        if (CELL)
-            ok = scan_cells<L, PERIODIC>(key, ext_all + g * p.ecap, pre_all + g * npre, Gc, cx, cy, p.ib, x, y,
-                                         p.box, p.cw, p.cell_eps);
-        if (!ok) scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
-        knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);
+        int R = 0;  // scanned neighbourhood radius (0: all N)
+        if (CELL) {
+            const float4* ext = ext_all + g * p.ecap;
+            const int* pre = pre_all + g * npre;
+            ok = scan_cells<L, PERIODIC>(key, ext, pre, Gc, cx, cy, 1, p.ib, x, y, p.box, p.cw, p.cell_eps);
+            R = 1;
+            if (__ballot(!ok) != 0) {  // wave-uniform: lanes whose 3x3 proof failed take the 5x5 result
+                uint32_t key2[L];
+                const bool ok2 =
+                    scan_cells<L, PERIODIC>(key2, ext, pre, Gc, cx, cy, 2, p.ib, x, y, p.box, p.cw, p.cell_eps);
+                if (!ok) {
+#pragma unroll
+                    for (int s = 0; s < L; ++s) key[s] = key2[s];
+                    ok = ok2;
+                    R = 2;
+                }
+            }
+        }
+        if (!ok) {
+            scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
+            R = 0;
+        }
+        const bool amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj, R == 0);
+        if (CELL && amb)
+            exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, Gc, cx, cy, R, x, y,
+                                            p.box);
     }
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
@@ -722,7 +796,7 @@ Cfg make_cfg(int E, int N, bool reset, int cells) {
         c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + c.G * sizeof(int);
     if (!reset && cells) {  // ext (2N float4, 16-B aligned) + cnt + pre + rowlen per env
         c.lds = (c.lds + 15) & ~(size_t)15;
-        c.lds += (size_t)c.G * (2 * N * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 2) + 1) * 4);
+        c.lds += (size_t)c.G * (2 * N * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 4) + 1) * 4);
     }
     return c;
 }

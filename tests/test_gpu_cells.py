@@ -4,7 +4,8 @@ The cell path must be indistinguishable from the all-pairs scan: every output of
 headings, neighbour distances and indices, reward, done) is compared BITWISE between the two paths from the same
 state, over uniform, clustered (many agents per cell, forcing long ranges and the full-scan fallback), box-edge
 (x = box / tiny x, cell clamping and periodic ghosts) and integer-lattice (exact distance ties, the ambiguous-bucket
-rescan) placements, N in 128..1024 and k up to 15; sampled envs are also checked against the oracle's exact kNN.
+rescan), and sparse (a blob plus isolated outliers: the 5x5 and full-scan fallbacks) placements, N in 128..1024
+and k up to 15; sampled envs are also checked against the oracle's exact kNN.
 """
 import os
 
@@ -32,6 +33,13 @@ def _positions(kind, E, N, box, rng):
         p[m] = np.where(rng.uniform(size=m.sum()) < 0.5, rng.uniform(0.001, 0.5, m.sum()),
                         rng.uniform(box - 0.5, box, m.sum()))
         return p
+    if kind == "sparse":  # a dense blob plus isolated outliers: blob-edge agents need the 5x5 neighbourhood, the
+        # outliers (fewer than L agents within 2 cells) the full scan
+        c = rng.uniform(0.3 * box, 0.7 * box, (E, 1, 2))
+        p = c + rng.normal(0, box / 25, (E, N, 2))
+        m = rng.uniform(size=(E, N)) < 0.08
+        p[m] = rng.uniform(0, box, (m.sum(), 2))
+        return np.clip(p, 0.001, box)
     if kind == "lattice":  # integer grid, equal spacing -> exact d2 ties
         side = int(np.ceil(np.sqrt(N)))
         g = np.stack(np.meshgrid(np.arange(side), np.arange(side)), -1).reshape(-1, 2)[:N].astype(np.float64)
@@ -68,7 +76,8 @@ CASES = [("v2", True, 256, 4, "uniform"), ("v2", True, 256, 4, "clustered"), ("v
          ("v2", True, 256, 4, "lattice"), ("v2", False, 256, 4, "edges"), ("v2", True, 128, 1, "uniform"),
          ("v2", True, 500, 15, "uniform"), ("v2", True, 1024, 4, "uniform"), ("v2", True, 1024, 11, "clustered"),
          ("uw", False, 256, 4, "uniform"), ("uw", False, 512, 4, "edges"), ("uw_discrete", False, 512, 4, "uniform"),
-         ("flock", False, 300, 6, "clustered"), ("v2", False, 1000, 9, "lattice")]
+         ("flock", False, 300, 6, "clustered"), ("v2", False, 1000, 9, "lattice"), ("v2", True, 256, 4, "sparse"),
+         ("v2", True, 1024, 4, "sparse"), ("uw", False, 512, 7, "sparse"), ("v2", True, 600, 15, "sparse")]
 
 
 @pytest.mark.parametrize("variant,periodic,N,k,kind", CASES,
