@@ -142,6 +142,39 @@ __device__ __forceinline__ float pair_d2(float xi, float yi, float xj, float yj,
     return __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
 }
 
+// max over the 64 lanes (every lane active), as a wave-uniform scalar: DPP max within each row of 16 (quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four row results by readlane. No LDS round trips.
+template <int CTRL>
+__device__ __forceinline__ int dpp_max(int v) {
+    return max(v, __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ int wave_max(int v) {
+    v = dpp_max<0xB1>(v);
+    v = dpp_max<0x4E>(v);
+    v = dpp_max<0x141>(v);
+    v = dpp_max<0x140>(v);
+    return __builtin_amdgcn_readfirstlane(max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+                                              max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48))));
+}
+
+// pair_d2 of two candidates at once: the squares and sums as packed f32 ops (v_pk_mul / v_pk_add, one candidate
+// per half; each half rounds exactly like the scalar mul, mul, add), so both packed issue slots do useful work.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool PERIODIC>
+__device__ __forceinline__ f32x2 pair_d2x2(float xi, float yi, float x0, float y0, float x1, float y1, float box) {
+    float dx0 = __fsub_rn(xi, x0), dx1 = __fsub_rn(xi, x1);
+    float dy0 = __fsub_rn(yi, y0), dy1 = __fsub_rn(yi, y1);
+    if (PERIODIC) {
+        const float ax0 = fabsf(dx0), ax1 = fabsf(dx1), ay0 = fabsf(dy0), ay1 = fabsf(dy1);
+        dx0 = fminf(ax0, __fsub_rn(box, ax0));
+        dx1 = fminf(ax1, __fsub_rn(box, ax1));
+        dy0 = fminf(ay0, __fsub_rn(box, ay0));
+        dy1 = fminf(ay1, __fsub_rn(box, ay1));
+    }
+    const f32x2 dx = {dx0, dx1}, dy = {dy0, dy1};
+    return dx * dx + dy * dy;
+}
+
 // Philox4x32-10 (Salmon et al. 2011), counter-based: (key = seed, counter = (c0, c1, c2, c3)).
 struct U4 {
     uint32_t x, y, z, w;
@@ -190,10 +223,9 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
 #pragma unroll 1
     for (; j + 1 < N; j += 2) {
         const float4 c = cand4[j >> 1];  // broadcast: every lane of the env reads the same 16 B
-        const float d0 = pair_d2<PERIODIC>(xi, yi, c.x, c.y, box);
-        const float d1 = pair_d2<PERIODIC>(xi, yi, c.z, c.w, box);
-        key_insert<L>(key, (__float_as_uint(d0) & hi_mask) | (uint32_t)j);
-        key_insert<L>(key, (__float_as_uint(d1) & hi_mask) | (uint32_t)(j + 1));
+        const f32x2 d = pair_d2x2<PERIODIC>(xi, yi, c.x, c.y, c.z, c.w, box);
+        key_insert<L>(key, (__float_as_uint(d.x) & hi_mask) | (uint32_t)j);
+        key_insert<L>(key, (__float_as_uint(d.y) & hi_mask) | (uint32_t)(j + 1));
     }
     if (j < N) {
         const float2 c = cand[j];
@@ -203,13 +235,18 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
 
 // phase 3c: the (2R+1) x (2R+1) cell neighbourhood (2R+1 contiguous ranges of the extended cell-sorted array, R = 1
 // or 2); returns true when the top-L keys are provably those of the full scan (see the file header). Uses
-// wave-wide reductions: call it with every lane of the wave active.
+// wave-wide reductions: call it with every lane of the wave active (lanes without an agent pass live = false:
+// empty ranges, result true).
 template <int L, bool PERIODIC>
 __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __restrict__ ext,
                                            const int* __restrict__ pre, int Gc, int cx, int cy, int R, int ib,
-                                           float xi, float yi, float box, float cw, float eps) {
+                                           float xi, float yi, float box, float cw, float eps, int ecap,
+                                           bool live) {
     const uint32_t hi_mask = ~((1u << ib) - 1u);
     const int W2 = Gc + 4;
+    // pair reads ext[c], ext[c + 1] from one clamped base: ext holds at most N + 4N/Gc <= 1.8N < ecap - 1 = 2N - 1
+    // entries, so a clamped pair is past every range end and both its keys are masked
+    const int cmax = ecap - 2;
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #pragma unroll 1
@@ -220,24 +257,21 @@ __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __r
             yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
         else
             row = yr >= 0 && yr < Gc;
+        row = row && live;
         const int* pr = pre + (row ? yr : 0) * W2;
         const int s0 = row ? pr[cx + 2 - R] : 0, e0 = row ? pr[cx + 3 + R] : 0;
         // wave-uniform trip count (max range length over the wave) so the loop is a plain counted loop: a
         // ballot-and-break loop made the compiler copy the whole key list around the back edge every iteration
-        int len = e0 - s0;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) len = max(len, __shfl_xor(len, o, 64));
-        const int tmax = __builtin_amdgcn_readfirstlane(len);
+        const int tmax = wave_max(e0 - s0);
 #pragma unroll 1
         for (int t = 0; t < tmax; t += 2) {
             const int c = s0 + t;
             const bool a0 = c < e0, a1 = c + 1 < e0;
-            const float4 q0 = ext[a0 ? c : 0];
-            const float4 q1 = ext[a1 ? c + 1 : 0];
-            const float d0 = pair_d2<PERIODIC>(xi, yi, q0.x, q0.y, box);
-            const float d1 = pair_d2<PERIODIC>(xi, yi, q1.x, q1.y, box);
-            const uint32_t k0 = (__float_as_uint(d0) & hi_mask) | (uint32_t)__float_as_int(q0.z);
-            const uint32_t k1 = (__float_as_uint(d1) & hi_mask) | (uint32_t)__float_as_int(q1.z);
+            const float4* q = ext + min(c, cmax);
+            const float4 q0 = q[0], q1 = q[1];
+            const f32x2 d = pair_d2x2<PERIODIC>(xi, yi, q0.x, q0.y, q1.x, q1.y, box);
+            const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
+            const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
             key_insert<L>(key, a0 ? k0 : kEmpty);
             key_insert<L>(key, a1 ? k1 : kEmpty);
         }
@@ -247,7 +281,7 @@ __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __r
     const float ly = (float)(cy - R) * cw, ry = (float)(cy + R + 1) * cw;
     const float m = fminf(fminf(xi - lx, rx - xi), fminf(yi - ly, ry - yi)) - eps;
     const float bound = m > 0.0f ? (m * m) * 0.99998f : 0.0f;
-    return (__float_as_uint(bound) & hi_mask) > key[L - 1];
+    return !live || (__float_as_uint(bound) & hi_mask) > key[L - 1];
 }
 
 // exact ordered insertion of (d2, j) into the W best, lexicographic (any visiting order)
@@ -579,27 +613,28 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     // ---- phase 3/4: kNN -------------------------------------------------------------------------------
     float bd[L - 1];
     int bj[L - 1];
-    if (active) {
-        uint32_t key[L];
-        bool ok = false;
-        int R = 0;  // scanned neighbourhood radius (0: all N)
-        if (CELL) {
-            const float4* ext = ext_all + g * p.ecap;
-            const int* pre = pre_all + g * npre;
-            ok = scan_cells<L, PERIODIC>(key, ext, pre, Gc, cx, cy, 1, p.ib, x, y, p.box, p.cw, p.cell_eps);
-            R = 1;
-            if (__ballot(!ok) != 0) {  // wave-uniform: lanes whose 3x3 proof failed take the 5x5 result
-                uint32_t key2[L];
-                const bool ok2 =
-                    scan_cells<L, PERIODIC>(key2, ext, pre, Gc, cx, cy, 2, p.ib, x, y, p.box, p.cw, p.cell_eps);
-                if (!ok) {
+    uint32_t key[L];
+    bool ok = false;
+    int R = 0;  // scanned neighbourhood radius (0: all N)
+    if (CELL) {  // every lane of the wave (the trip counts are wave-wide maxima); lanes without an agent scan nothing
+        const float4* ext = ext_all + g * p.ecap;
+        const int* pre = pre_all + g * npre;
+        ok = scan_cells<L, PERIODIC>(key, ext, pre, Gc, cx, cy, 1, p.ib, x, y, p.box, p.cw, p.cell_eps, p.ecap,
+                                     active);
+        R = 1;
+        if (__ballot(!ok) != 0) {  // wave-uniform: lanes whose 3x3 proof failed take the 5x5 result
+            uint32_t key2[L];
+            const bool ok2 = scan_cells<L, PERIODIC>(key2, ext, pre, Gc, cx, cy, 2, p.ib, x, y, p.box, p.cw,
+                                                     p.cell_eps, p.ecap, active);
+            if (!ok) {
 #pragma unroll
-                    for (int s = 0; s < L; ++s) key[s] = key2[s];
-                    ok = ok2;
-                    R = 2;
-                }
+                for (int s = 0; s < L; ++s) key[s] = key2[s];
+                ok = ok2;
+                R = 2;
             }
         }
+    }
+    if (active) {
         if (!ok) {
             scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
             R = 0;

@@ -49,78 +49,111 @@ __device__ __forceinline__ float sqrt_rn(float x) { return __builtin_sqrtf(x); }
 //   p = p + (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)     addcdiv_
 // then optionally the target network soft update (mode 0: t*(1-tau) + p*tau, maddpg nets net.py:305-309;
 // mode 1: tau*p + (1-tau)*t, shared critic agent_simple_shared_critic.py:172-185).
-__global__ __launch_bounds__(kBlock) void adam_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
-                                                      float* __restrict__ m, float* __restrict__ v,
-                                                      const float* __restrict__ grad_scale, float w1, float b2,
-                                                      float one_minus_b2, float neg_step_size, float bc2_sqrt,
-                                                      float eps, float* __restrict__ target, float tau,
-                                                      float one_minus_tau, int target_mode) {
-    const float gs = grad_scale ? *grad_scale : 1.0f;
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        float gi = g[i];
-        if (grad_scale) gi = gi * gs;
-        float mi = m[i];
-        mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
-        float vi = v[i] * b2;
-        vi = vi + (one_minus_b2 * gi) * gi;
-        const float denom = sqrt_rn(vi) / bc2_sqrt + eps;
-        float pi = p[i] + (neg_step_size * mi) / denom;
-        m[i] = mi;
-        v[i] = vi;
-        p[i] = pi;
-        if (target) {
-            const float t = target[i];
-            target[i] = target_mode == 0 ? t * one_minus_tau + pi * tau : tau * pi + one_minus_tau * t;
-        }
-    }
+struct AdamArgs {
+    int64_t n;
+    float *p, *m, *v, *target;
+    const float *g, *grad_scale;
+    const int64_t* step;  // device step count (graph-capturable path) or null: neg_step / bc2s given
+    float lr, beta1, beta2, w1, one_minus_b2, neg_step, bc2s, eps, tau, one_minus_tau;
+    int target_mode;
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float* t, const AdamArgs& a,
+                                          float gs, float neg_step, float bc2s) {
+    if (a.grad_scale) g = g * gs;
+    m = (a.w1 < 0.5f) ? m + a.w1 * (g - m) : g - (g - m) * (1.0f - a.w1);
+    v = v * a.beta2;
+    v = v + (a.one_minus_b2 * g) * g;
+    const float denom = sqrt_rn(v) / bc2s + a.eps;
+    p = p + (neg_step * m) / denom;
+    if (t) *t = a.target_mode == 0 ? *t * a.one_minus_tau + p * a.tau : a.tau * p + a.one_minus_tau * *t;
 }
 
-// Same update with the step count read from device memory (graph-capturable: the bias corrections are computed
-// in-kernel, once per block, from *step).
-__global__ __launch_bounds__(kBlock) void adam_dev_kernel(int64_t n, float* __restrict__ p, const float* __restrict__ g,
-                                                          float* __restrict__ m, float* __restrict__ v,
-                                                          const float* __restrict__ grad_scale,
-                                                          const int64_t* __restrict__ step, float lr, float beta1,
-                                                          float beta2, float eps, float* __restrict__ target,
-                                                          float tau, float one_minus_tau, int target_mode) {
+// VEC: every pointer 16-B aligned -> one float4 of each stream per thread and iteration (the update is HBM-bound:
+// 16 or 20 B read + 12 or 16 B written per parameter), the n % 4 tail by block 0. Same per-element arithmetic as
+// the scalar path, so both give identical bits.
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void adam_kernel(AdamArgs a) {
     __shared__ float sh[2];
-    if (threadIdx.x == 0) {
-        const double st = (double)*step;
-        const double bc1 = 1.0 - pow((double)beta1, st);
-        const double bc2 = 1.0 - pow((double)beta2, st);
-        sh[0] = (float)(-(double)lr / bc1);
-        sh[1] = (float)sqrt(bc2);
-    }
-    __syncthreads();
-    const float neg_step_size = sh[0], bc2_sqrt = sh[1];
-    const float w1 = (float)(1.0 - (double)beta1), one_minus_b2 = (float)(1.0 - (double)beta2);
-    const float gs = grad_scale ? *grad_scale : 1.0f;
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        float gi = g[i];
-        if (grad_scale) gi = gi * gs;
-        float mi = m[i];
-        mi = (w1 < 0.5f) ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.0f - w1);
-        float vi = v[i] * beta2;
-        vi = vi + (one_minus_b2 * gi) * gi;
-        const float denom = sqrt_rn(vi) / bc2_sqrt + eps;
-        const float pi = p[i] + (neg_step_size * mi) / denom;
-        m[i] = mi;
-        v[i] = vi;
-        p[i] = pi;
-        if (target) {
-            const float t = target[i];
-            target[i] = target_mode == 0 ? t * one_minus_tau + pi * tau : tau * pi + one_minus_tau * t;
+    float neg_step = a.neg_step, bc2s = a.bc2s;
+    if (a.step) {
+        if (threadIdx.x == 0) {
+            const double st = (double)*a.step;
+            const double bc1 = 1.0 - pow((double)a.beta1, st);
+            const double bc2 = 1.0 - pow((double)a.beta2, st);
+            sh[0] = (float)(-(double)a.lr / bc1);
+            sh[1] = (float)sqrt(bc2);
         }
+        __syncthreads();
+        neg_step = sh[0];
+        bc2s = sh[1];
+    }
+    const float gs = a.grad_scale ? *a.grad_scale : 1.0f;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    if (VEC) {
+        const int64_t nq = a.n >> 2;
+        for (int64_t q = i0; q < nq; q += stride) {
+            float4 p = reinterpret_cast<const float4*>(a.p)[q];
+            const float4 g = reinterpret_cast<const float4*>(a.g)[q];
+            float4 m = reinterpret_cast<const float4*>(a.m)[q];
+            float4 v = reinterpret_cast<const float4*>(a.v)[q];
+            float4 t = a.target ? reinterpret_cast<const float4*>(a.target)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            float* tp = a.target ? &t.x : nullptr;
+            adam_elem(p.x, g.x, m.x, v.x, tp, a, gs, neg_step, bc2s);
+            adam_elem(p.y, g.y, m.y, v.y, tp ? tp + 1 : nullptr, a, gs, neg_step, bc2s);
+            adam_elem(p.z, g.z, m.z, v.z, tp ? tp + 2 : nullptr, a, gs, neg_step, bc2s);
+            adam_elem(p.w, g.w, m.w, v.w, tp ? tp + 3 : nullptr, a, gs, neg_step, bc2s);
+            reinterpret_cast<float4*>(a.p)[q] = p;
+            reinterpret_cast<float4*>(a.m)[q] = m;
+            reinterpret_cast<float4*>(a.v)[q] = v;
+            if (a.target) reinterpret_cast<float4*>(a.target)[q] = t;
+        }
+        if (blockIdx.x != 0) return;
+        i0 = (nq << 2) + threadIdx.x;  // tail
+    }
+    for (int64_t i = i0; i < a.n; i += VEC ? a.n : stride) {
+        float p = a.p[i], m = a.m[i], v = a.v[i];
+        adam_elem(p, a.g[i], m, v, a.target ? a.target + i : nullptr, a, gs, neg_step, bc2s);
+        a.p[i] = p;
+        a.m[i] = m;
+        a.v[i] = v;
     }
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(kBlock) void soft_update_kernel(int64_t n, float* __restrict__ target,
                                                              const float* __restrict__ src, float tau,
                                                              float one_minus_tau, int mode) {
-    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-        const float t = target[i], s = src[i];
-        target[i] = mode == 0 ? t * one_minus_tau + s * tau : tau * s + one_minus_tau * t;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+    auto f = [&](float t, float s) { return mode == 0 ? t * one_minus_tau + s * tau : tau * s + one_minus_tau * t; };
+    if (VEC) {
+        const int64_t nq = n >> 2;
+        for (int64_t q = i0; q < nq; q += stride) {
+            float4 t = reinterpret_cast<const float4*>(target)[q];
+            const float4 s = reinterpret_cast<const float4*>(src)[q];
+            t.x = f(t.x, s.x);
+            t.y = f(t.y, s.y);
+            t.z = f(t.z, s.z);
+            t.w = f(t.w, s.w);
+            reinterpret_cast<float4*>(target)[q] = t;
+        }
+        if (blockIdx.x != 0) return;
+        i0 = (nq << 2) + threadIdx.x;
     }
+    for (int64_t i = i0; i < n; i += VEC ? n : stride) target[i] = f(target[i], src[i]);
+}
+
+bool aligned16(const void* p) { return p == nullptr || ((uintptr_t)p & 15u) == 0; }
+
+int launch_adam(void* stream, const AdamArgs& a) {
+    const bool vec = aligned16(a.p) && aligned16(a.g) && aligned16(a.m) && aligned16(a.v) && aligned16(a.target);
+    if (vec)
+        hipLaunchKernelGGL(adam_kernel<true>, dim3(grid_for(a.n, 4)), dim3(kBlock), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(adam_kernel<false>, dim3(grid_for(a.n, 4)), dim3(kBlock), 0, (hipStream_t)stream, a);
+    return launched();
 }
 
 // sum of squares: pass 1 per-block partials (f64 accumulation), pass 2 one block folds them and writes
@@ -329,12 +362,10 @@ int flock_adam_step(void* stream, int64_t n, float* param, const float* grad, fl
     // bias corrections in double then rounded, like the python-float math of _single_tensor_adam
     const double bc1 = 1.0 - pow((double)beta1, (double)step);
     const double bc2 = 1.0 - pow((double)beta2, (double)step);
-    const float neg_step = (float)(-(double)lr / bc1);
-    const float bc2s = (float)sqrt(bc2);
-    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, param, grad, exp_avg,
-                       exp_avg_sq, grad_scale, (float)(1.0 - (double)beta1), beta2, (float)(1.0 - (double)beta2),
-                       neg_step, bc2s, eps, target, tau, (float)(1.0 - (double)tau), target_mode);
-    return launched();
+    AdamArgs a{n, param, exp_avg, exp_avg_sq, target, grad, grad_scale, nullptr, lr, beta1, beta2,
+               (float)(1.0 - (double)beta1), (float)(1.0 - (double)beta2), (float)(-(double)lr / bc1),
+               (float)sqrt(bc2), eps, tau, (float)(1.0 - (double)tau), target_mode};
+    return launch_adam(stream, a);
 }
 
 int flock_adam_step_dev(void* stream, int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
@@ -342,17 +373,21 @@ int flock_adam_step_dev(void* stream, int64_t n, float* param, const float* grad
                         float* target, float tau, int target_mode) {
     if (n <= 0) return 0;
     if (!param || !grad || !exp_avg || !exp_avg_sq || !step) return fail(-3, "flock_adam_step_dev: NULL pointer");
-    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, param, grad,
-                       exp_avg, exp_avg_sq, grad_scale, step, lr, beta1, beta2, eps, target, tau,
-                       (float)(1.0 - (double)tau), target_mode);
-    return launched();
+    AdamArgs a{n, param, exp_avg, exp_avg_sq, target, grad, grad_scale, step, lr, beta1, beta2,
+               (float)(1.0 - (double)beta1), (float)(1.0 - (double)beta2), 0.0f, 1.0f, eps, tau,
+               (float)(1.0 - (double)tau), target_mode};
+    return launch_adam(stream, a);
 }
 
 int flock_soft_update(void* stream, int64_t n, float* target, const float* src, float tau, int mode) {
     if (n <= 0) return 0;
     if (!target || !src) return fail(-3, "flock_soft_update: NULL pointer");
-    hipLaunchKernelGGL(soft_update_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n, target, src,
-                       tau, (float)(1.0 - (double)tau), mode);
+    if (aligned16(target) && aligned16(src))
+        hipLaunchKernelGGL(soft_update_kernel<true>, dim3(grid_for(n, 4)), dim3(kBlock), 0, (hipStream_t)stream, n,
+                           target, src, tau, (float)(1.0 - (double)tau), mode);
+    else
+        hipLaunchKernelGGL(soft_update_kernel<false>, dim3(grid_for(n, 4)), dim3(kBlock), 0, (hipStream_t)stream, n,
+                           target, src, tau, (float)(1.0 - (double)tau), mode);
     return launched();
 }
 

@@ -825,7 +825,7 @@ struct AdamState {
 __device__ __forceinline__ AdamState adam_load(const GradAdam& ga, int64_t i) {
     return {ga.p[i], ga.m[i], ga.v[i], ga.target ? ga.target[i] : 0.0f};
 }
-// torch.optim.Adam single-tensor path, identical to adam_dev_kernel (flock_learn.hip)
+// torch.optim.Adam single-tensor path, identical to adam_elem (flock_learn.hip)
 __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamState s, float gi, float neg_step,
                                            float bc2s, bool soft) {
     const float w1 = (float)(1.0 - (double)ga.b1), omb2 = (float)(1.0 - (double)ga.b2);

@@ -233,11 +233,22 @@ def blinear(x, W, b=None):
         x2 = x if x.dim() == 2 else x[0]
         return torch.nn.functional.linear(x2, W[0], None if b is None else b[0]).unsqueeze(0)
     if x.dim() == 2:
-        x = x.unsqueeze(0).expand(W.shape[0], *x.shape)
+        return shared_linear(x, W, b)
     Wt = W.transpose(1, 2)
     if b is None:
         return torch.bmm(x, Wt)
     return torch.baddbmm(b.unsqueeze(1), x, Wt)
+
+
+def shared_linear(x, W, b=None):
+    """Every agent's Linear applied to ONE input shared by all agents: x [..., in], W [A,out,in] -> [A, ..., out].
+    One GEMM against the agent-stacked weight viewed as [A*out, in] (its weight gradient is then one GEMM landing in
+    W's own layout); the result is a permuted view."""
+    A, out, n_in = W.shape
+    y = torch.nn.functional.linear(x, W.reshape(A * out, n_in), None if b is None else b.reshape(A * out))
+    lead = x.shape[:-1]
+    y = y.view(*lead, A, out)
+    return y.movedim(-2, 0)
 
 
 def blayer_norm(x, w, b, eps=1e-5):

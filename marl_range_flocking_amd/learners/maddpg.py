@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell
+from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell, shared_linear
 
 HR = 32  # hidden_rnn (net.py:15,100)
 
@@ -49,9 +49,25 @@ def critic_shapes(n_agents, k, h1, h2, recurrent, n_actions=2):
                   "fc1.weight": (h1, HR), "fc1.bias": (h1,)})
     else:
         s.update({"fc1.weight": (h1, n_agents * k), "fc1.bias": (h1,)})
-    s.update({"fc2.weight": (h2, h1 + n_actions * n_agents), "fc2.bias": (h2,), "fc3.weight": (1, h2),
-              "fc3.bias": (1,)})
+    # fc2.weight [h2, h1 + 2N] is kept as its two column blocks (the fc1-output part and the all-agents action
+    # part) so each gets its own gradient GEMM (a sliced leaf costs a zero-filled full-size gradient per use);
+    # load_reference_state / state_dict split and join it (CRITIC_JOINED)
+    s.update({"fc2.weight_h": (h2, h1), "fc2.weight_a": (h2, n_actions * n_agents), "fc2.bias": (h2,),
+              "fc3.weight": (1, h2), "fc3.bias": (1,)})
     return s
+
+
+CRITIC_JOINED = {"fc2.weight": ("fc2.weight_h", "fc2.weight_a")}  # reference name -> stored column blocks
+
+
+def reference_names(fp):
+    """Parameter names in the reference state_dict order (stored column blocks joined back)."""
+    out = []
+    for n in fp.shapes:
+        ref = next((r for r, parts in CRITIC_JOINED.items() if n in parts), n)
+        if ref not in out:
+            out.append(ref)
+    return out
 
 
 def _init(fp, generator):
@@ -63,7 +79,12 @@ def _init(fp, generator):
                 b = 1.0 / math.sqrt(HR)
                 fp.view(fp.data, name).uniform_(-b, b, generator=generator)
                 continue
-            w = fp.shapes[layer + ".weight"]
+            kind = "weight" if kind.startswith("weight") else kind
+            if layer + ".weight" in fp.shapes:
+                w = fp.shapes[layer + ".weight"]
+            else:  # column blocks of one joined weight: [out, sum of the blocks' in]
+                parts = CRITIC_JOINED[layer + ".weight"]
+                w = (fp.shapes[parts[0]][0], sum(fp.shapes[q][1] for q in parts))
             if kind == "weight" and layer in ("fc1", "fc2"):
                 b = 1.0 / math.sqrt(w[0])
             elif kind == "weight" and layer in ("fc3", "linear_speed", "angular_speed"):
@@ -73,35 +94,58 @@ def _init(fp, generator):
             fp.view(fp.data, name).uniform_(-b, b, generator=generator)
 
 
+def actor_gru(P, x, h):
+    """The recurrent actor's GRU step only: x [A,B,k], h [A,B,32] -> h' (the action head is not evaluated)."""
+    return gru_cell(blinear(x, P["fce.weight"], P["fce.bias"]), h, P["gru.weight_ih"], P["gru.weight_hh"],
+                    P["gru.bias_ih"], P["gru.bias_hh"])
+
+
+def actor_head(P, h):
+    """The recurrent actor after its GRU: h [A,B,32] -> actions [A,B,2]."""
+    y = F.relu(blinear(h, P["fc1.weight"], P["fc1.bias"]))
+    y = F.relu(blinear(y, P["fc2.weight"], P["fc2.bias"]))
+    lin = (torch.tanh(blinear(y, P["linear_speed.weight"], P["linear_speed.bias"])) + 1) / 2  # :65-66
+    ang = torch.tanh(blinear(y, P["angular_speed.weight"], P["angular_speed.bias"])) * 1.5       # :69-70
+    return torch.cat([lin, ang], dim=-1)
+
+
 def actor_forward(P, x, h, recurrent):
     """x [A,B,k], h [A,B,32] -> actions [A,B,2], h'."""
     if recurrent:
-        y = gru_cell(blinear(x, P["fce.weight"], P["fce.bias"]), h, P["gru.weight_ih"], P["gru.weight_hh"],
-                     P["gru.bias_ih"], P["gru.bias_hh"])
-        h = y
-        y = F.relu(blinear(y, P["fc1.weight"], P["fc1.bias"]))
-        y = F.relu(blinear(y, P["fc2.weight"], P["fc2.bias"]))
-        lin = (torch.tanh(blinear(y, P["linear_speed.weight"], P["linear_speed.bias"])) + 1) / 2  # :65-66
-        ang = torch.tanh(blinear(y, P["angular_speed.weight"], P["angular_speed.bias"])) * 1.5       # :69-70
-        return torch.cat([lin, ang], dim=-1), h
+        h = actor_gru(P, x, h)
+        return actor_head(P, h), h
     y = F.relu(blinear(x, P["fc1.weight"], P["fc1.bias"]))
     y = F.relu(blinear(y, P["fc2.weight"], P["fc2.bias"]))
     return torch.tanh(blinear(y, P["fc3.weight"], P["fc3.bias"])), h
 
 
-def critic_forward(P, x, a, h, recurrent, h1):
-    """x [B, N*k] and a [B, 2N] shared by every agent's critic; h [A,B,32] -> q [A,B,1], h'.
-    fc2(cat([out, a])) is computed as out @ W[:, :h1]^T + a @ W[:, h1:]^T + b (same math, no [A,B,h1+2N] concat)."""
+def critic_fce(P, x):
+    """The recurrent critics' input layer for every agent and every chunk step at once: x [T,B,N*k] (shared by all
+    critics) -> T tensors [A,B,32]. One GEMM [T*B, N*k] x [N*k, A*32]; its weight gradient is one GEMM too."""
+    return shared_linear(x, P["fce.weight"], P["fce.bias"]).unbind(1)
+
+
+def critic_gru(P, fx, h):
+    """One GRUCell step of the recurrent critics from their fce output fx [A,B,32]: h [A,B,32] -> h'."""
+    return gru_cell(fx, h, P["gru.weight_ih"], P["gru.weight_hh"], P["gru.bias_ih"], P["gru.bias_hh"])
+
+
+def critic_head(P, y, a):
+    """fc2(cat([y, a])) -> ReLU -> fc3: y [A,B,h1] (post-ReLU fc1 output), a [B,2N] shared -> q [A,B,1].
+    fc2 runs as its two column blocks, y @ W_h^T + b + a @ W_a^T (same math, no [A,B,h1+2N] concat)."""
+    z = blinear(y, P["fc2.weight_h"], P["fc2.bias"]) + shared_linear(a, P["fc2.weight_a"])
+    return blinear(F.relu(z), P["fc3.weight"], P["fc3.bias"])
+
+
+def critic_forward(P, x, a, h, recurrent):
+    """One reference critic call (net.py:100-146 / :80-115): x [B, N*k] and a [B, 2N] shared by every agent's
+    critic; h [A,B,32] -> q [A,B,1], h'."""
     if recurrent:
-        y = gru_cell(blinear(x, P["fce.weight"], P["fce.bias"]), h, P["gru.weight_ih"], P["gru.weight_hh"],
-                     P["gru.bias_ih"], P["gru.bias_hh"])
-        h = y
+        y = h = critic_gru(P, shared_linear(x, P["fce.weight"], P["fce.bias"]), h)
         y = F.relu(blinear(y, P["fc1.weight"], P["fc1.bias"]))
     else:
-        y = F.relu(blinear(x, P["fc1.weight"], P["fc1.bias"]))
-    W = P["fc2.weight"]
-    z = blinear(y, W[:, :, :h1], P["fc2.bias"]) + blinear(a, W[:, :, h1:])
-    return blinear(F.relu(z), P["fc3.weight"], P["fc3.bias"]), h
+        y = F.relu(shared_linear(x, P["fc1.weight"], P["fc1.bias"]))
+    return critic_head(P, y, a), h
 
 
 class SharedOU:
@@ -241,46 +285,73 @@ class MADDPGLearner:
         self._step()
 
     def _fwd_bwd(self):
-        N, B, C, k, h1 = self.N, self.B, self.C, self.k, self.h1
+        N, B, C, k = self.N, self.B, self.C, self.k
         idx = self.static_idx
-        S = self.replay.gather("state", idx).reshape(B, C, N * k)
-        S2 = self.replay.gather("next_state", idx).reshape(B, C, N * k)
+        tidx = idx.t().contiguous()                                             # [C, B]: chunk step major
+        S = self.replay.gather("state", tidx).reshape(C, B, N * k)
+        S2 = self.replay.gather("next_state", tidx).reshape(C, B, N * k)
         AS = self.replay.gather("actor_state", idx).permute(2, 1, 0, 3)        # [N, C, B, k]
         AS2 = self.replay.gather("actor_next_state", idx).permute(2, 1, 0, 3)
-        act = self.replay.gather("action", idx)                                 # [B, C, N, 2]
+        act = self.replay.gather("action", tidx)                                # [C, B, N, 2]
         if self.reference_action_layout:  # actors_action [N,B,C,2].reshape(B,C,2N) (MADDPG.py:86)
-            act = act.permute(2, 0, 1, 3).contiguous().reshape(B, C, 2 * N)
+            act = act.permute(2, 1, 0, 3).contiguous().reshape(B, C, 2 * N).transpose(0, 1)
         else:
-            act = act.reshape(B, C, 2 * N)
+            act = act.reshape(C, B, 2 * N)
         R = self.replay.gather("reward", idx)                                   # [B, C, N]
         D = self.replay.gather("done", idx)
         Pa = {n: self.actors.view(self.actors.data, n) for n in self.actors.shapes}
         Pta = {n: self.actors.view(self.actors.target, n) for n in self.actors.shapes}
         Ptc = {n: self.critics.view(self.critics.target, n) for n in self.critics.shapes}
         Pc = self.critic_leaves
-        rec = self.recurrent
-        zero = lambda: torch.zeros((N, B, HR), device=self.device)  # noqa: E731
-        h_ta, h_tc, h_c, h_a = zero(), zero(), zero(), zero()
-        for t in range(C):
+        last = C - 1
+        if self.recurrent:
+            # MADDPG.py:95-132. critic_values, target_critic_values and the actions are overwritten at every chunk
+            # step and read only after the loop, so before the last step only the four GRU recurrences reach the
+            # loss: the heads run once, on the last step's hidden states (identical results, C x less head work).
+            # The critics' input layer does not depend on the recurrence: one GEMM for all steps and agents.
+            zero = lambda: torch.zeros((N, B, HR), device=self.device)  # noqa: E731
+            h_ta, h_tc, h_c, h_a = zero(), zero(), zero(), zero()
             with torch.no_grad():
-                ta, h_ta = actor_forward(Pta, AS2[:, t], h_ta, rec)
-                cta = ta.transpose(0, 1).reshape(B, 2 * N)                       # torch.cat(..., dim=1)
-                tq, h_tc = critic_forward(Ptc, S2[:, t], cta, h_tc, rec, h1)
-            q, h_c = critic_forward(Pc, S[:, t], act[:, t], h_c, rec, h1)
-            with torch.no_grad():
-                pa, h_a = actor_forward(Pa, AS[:, t], h_a, rec)
-                cpa = pa.transpose(0, 1).reshape(B, 2 * N)
-            if rec:  # hidden[done_mask[:, i]] = 0 for the four hidden lists (MADDPG.py:117-132)
+                fx_t = critic_fce(Ptc, S2)
+            fx = critic_fce(Pc, S)
+            for t in range(C):
+                with torch.no_grad():
+                    h_ta = actor_gru(Pta, AS2[:, t], h_ta)
+                    h_tc = critic_gru(Ptc, fx_t[t], h_tc)
+                    h_a = actor_gru(Pa, AS[:, t], h_a)
+                h_c = critic_gru(Pc, fx[t], h_c)
+                if t == last:
+                    y_ta, y_tc, y_c, y_a = h_ta, h_tc, h_c, h_a                # the heads see the pre-reset state
+                # hidden[done_mask[:, i]] = 0 for the four hidden lists (MADDPG.py:117-132)
                 keep = (D[:, t] == 0).t().unsqueeze(-1)                         # [N, B, 1]
                 h_ta = torch.where(keep, h_ta, 0.0)
                 h_tc = torch.where(keep, h_tc, 0.0)
                 h_c = torch.where(keep, h_c, 0.0)
                 h_a = torch.where(keep, h_a, 0.0)
-        r = R[:, C - 1].t().unsqueeze(-1)
-        d = D[:, C - 1].t().unsqueeze(-1)
+            with torch.no_grad():
+                cta = actor_head(Pta, y_ta).transpose(0, 1).reshape(B, 2 * N)   # torch.cat(..., dim=1)
+                tq = critic_head(Ptc, F.relu(blinear(y_tc, Ptc["fc1.weight"], Ptc["fc1.bias"])), cta)
+                cpa = actor_head(Pa, y_a).transpose(0, 1).reshape(B, 2 * N)
+            # the actor-loss critic call (:137) steps the GRU once more from the reset hidden state; its head and
+            # the critic-loss head share one pass over a 2B batch
+            h_aq = critic_gru(Pc, fx[last], h_c)
+            y = F.relu(blinear(torch.cat([y_c, h_aq], 1), Pc["fc1.weight"], Pc["fc1.bias"]))
+            qq = critic_head(Pc, y, torch.cat([act[last], cpa], 0))
+            q, aq = qq[:, :B], qq[:, B:]
+        else:  # maddpg_official/MADDPG.py:67-108 (C == 1)
+            zero = torch.zeros((N, B, HR), device=self.device)
+            with torch.no_grad():
+                ta, _ = actor_forward(Pta, AS2[:, 0], zero, False)
+                tq, _ = critic_forward(Ptc, S2[0], ta.transpose(0, 1).reshape(B, 2 * N), zero, False)
+                pa, _ = actor_forward(Pa, AS[:, 0], zero, False)
+                cpa = pa.transpose(0, 1).reshape(B, 2 * N)
+            y = F.relu(shared_linear(S[0], Pc["fc1.weight"], Pc["fc1.bias"]))
+            qq = critic_head(Pc, torch.cat([y, y], 1), torch.cat([act[0], cpa], 0))
+            q, aq = qq[:, :B], qq[:, B:]
+        r = R[:, last].t().unsqueeze(-1)
+        d = D[:, last].t().unsqueeze(-1)
         target = r + self.gamma * tq * (1 - d)                                  # MADDPG.py:135
         critic_loss = ((target - q) ** 2).mean(dim=(1, 2))                      # F.mse_loss per agent (:136)
-        aq, _ = critic_forward(Pc, S[:, C - 1], cpa, h_c, rec, h1)              # (:137) hidden after the last step
         actor_loss = -aq.mean(dim=(1, 2))
         self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc)
         with torch.no_grad():
@@ -322,9 +393,24 @@ class MADDPGLearner:
             net = "actor" if "actor" in key else "critic"
             i = int(key[len(key.rstrip("0123456789")):])
             fp = self.actors if net == "actor" else self.critics
+            tgt = key.startswith("target")
             for n, v in sd.items():
-                fp.load(n, v, agent=i, target=key.startswith("target"))
+                if n in CRITIC_JOINED and net == "critic":
+                    v = torch.as_tensor(v)
+                    lo = 0
+                    for part in CRITIC_JOINED[n]:
+                        w = fp.shapes[part][1]
+                        fp.load(part, v[:, lo:lo + w], agent=i, target=tgt)
+                        lo += w
+                else:
+                    fp.load(n, v, agent=i, target=tgt)
 
     def state_dict(self, net, i, target=False):
         fp = self.actors if net == "actor" else self.critics
-        return {n: fp.export(n, i, target=target).cpu() for n in fp.shapes}
+        out = {}
+        for n in reference_names(fp):
+            if n in CRITIC_JOINED and n not in fp.shapes:
+                out[n] = torch.cat([fp.export(p, i, target=target) for p in CRITIC_JOINED[n]], -1).cpu()
+            else:
+                out[n] = fp.export(n, i, target=target).cpu()
+        return out
