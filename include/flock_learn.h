@@ -50,6 +50,19 @@ int flock_gru_fwd(void* stream, int64_t rows, int H, const float* gi, const floa
 int flock_gru_bwd(void* stream, int64_t rows, int H, const float* dhout, const float* h, const float* ws, float* dgi,
                   float* dgh, float* dh);
 
+/* GRUCell recurrence of A networks over a whole chunk of C steps in one launch (one block per network; replaces the
+ * per-step GRUCell calls of vdn/train_flock.py:23-36 and maddpg_official_rnn/MADDPG.py:95-132). gi: [A][C][B][3H]
+ * input-side pre-activations x W_ih^T + b_ih of every step; w_hh [A][3H][H], b_hh [A][3H]; keep: uint8 mask at
+ * keep[t*keep_st + a*keep_sa + b*keep_sb] (0: the hidden state is reset to zero after step t, the done reset);
+ * initial hidden state zero. Out: hs [A][C][B][H] (each step's output before its reset), ws [A][C][B][4H] (saved
+ * gates for the backward; may be NULL). H = 32; B <= 256.
+ * bwd: dhs = dLoss/dhs -> dgi [A][C][B][3H], dw_hh [A][3H][H], db_hh [A][3H] (written, not accumulated). */
+int flock_gru_seq_fwd(void* stream, int A, int C, int B, int H, const float* gi, const float* w_hh, const float* b_hh,
+                      const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb, float* hs, float* ws);
+int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs, const float* hs, const float* ws,
+                      const float* w_hh, const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb,
+                      float* dgi, float* dw_hh, float* db_hh);
+
 /* gather: dst[r][:] = src[idx[r]][:]; scatter: dst[idx[r]][:] = src[r][:]; rows of `width` floats. */
 int flock_gather_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);
 int flock_scatter_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);

@@ -254,6 +254,168 @@ __global__ __launch_bounds__(kBlock) void gru_bwd_kernel(int64_t rows, int H, co
 }
 
 // dst[r, :] = src[idx[r], :]  (replay minibatch / chunk gather); one wave per row, 16-B vectors when aligned
+// GRUCell recurrence of A independent networks over a whole chunk of C steps, ONE block per network (replaces
+// C x (hidden GEMM + gate kernel + reset) launches per network: vdn/train_flock.py:23-36 and
+// maddpg_official_rnn/MADDPG.py:95-132 step their GRUCells once per chunk step). Step t:
+//   gh = h W_hh^T + b_hh;  r, z, n, h' as gru_fwd_kernel;  hs[t] = h';  h = keep[t] ? h' : 0 (the done reset)
+// gi: [A][C][B][3H] input-side pre-activations of every step (computed for all steps by one GEMM beforehand);
+// keep: uint8 at keep[t*kt + a*ka + b*kb]; the initial hidden state is zero (every reference chunk starts from
+// init_hidden). Thread (j, b): hidden unit j = tid % H of rows b = tid / H + (256 / H) * q; its three W_hh rows
+// live in registers, the hidden states in LDS (ping-pong). ws [A][C][B][4H] = (r, z, n, gh_n) for the backward.
+template <int H>
+__global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const float* __restrict__ gi,
+                                                             const float* __restrict__ W, const float* __restrict__ bias,
+                                                             const uint8_t* __restrict__ keep, int64_t kt, int64_t ka,
+                                                             int64_t kb, float* __restrict__ hs,
+                                                             float* __restrict__ ws) {
+    extern __shared__ float4 seq_smem[];
+    float* hcur = reinterpret_cast<float*>(seq_smem);
+    float* hnxt = hcur + B * H;
+    const int64_t a = blockIdx.x;
+    const int tid = threadIdx.x, j = tid % H, bstep = kBlock / H;
+    const float* Wa = W + a * 3 * H * H;
+    float wr[H], wz[H], wn[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        wr[i] = Wa[j * H + i];
+        wz[i] = Wa[(H + j) * H + i];
+        wn[i] = Wa[(2 * H + j) * H + i];
+    }
+    const float br = bias[a * 3 * H + j], bz = bias[a * 3 * H + H + j], bn = bias[a * 3 * H + 2 * H + j];
+    for (int e = tid; e < B * H; e += kBlock) hcur[e] = 0.0f;
+    __syncthreads();
+    for (int t = 0; t < C; ++t) {
+        for (int b = tid / H; b < B; b += bstep) {
+            const float4* hp = reinterpret_cast<const float4*>(hcur + b * H);
+            float sr = 0.0f, sz = 0.0f, sn = 0.0f;
+#pragma unroll
+            for (int i4 = 0; i4 < H / 4; ++i4) {
+                const float4 v = hp[i4];
+                sr = fmaf(wr[4 * i4], v.x, sr); sz = fmaf(wz[4 * i4], v.x, sz); sn = fmaf(wn[4 * i4], v.x, sn);
+                sr = fmaf(wr[4 * i4 + 1], v.y, sr); sz = fmaf(wz[4 * i4 + 1], v.y, sz); sn = fmaf(wn[4 * i4 + 1], v.y, sn);
+                sr = fmaf(wr[4 * i4 + 2], v.z, sr); sz = fmaf(wz[4 * i4 + 2], v.z, sz); sn = fmaf(wn[4 * i4 + 2], v.z, sn);
+                sr = fmaf(wr[4 * i4 + 3], v.w, sr); sz = fmaf(wz[4 * i4 + 3], v.w, sz); sn = fmaf(wn[4 * i4 + 3], v.w, sn);
+            }
+            const int64_t row = (a * C + t) * B + b;
+            const float* g = gi + row * 3 * H;
+            const float r = sigmoidf_((sr + br) + g[j]);
+            const float z = sigmoidf_((sz + bz) + g[H + j]);
+            const float ghn = sn + bn;
+            const float nn = tanhf(g[2 * H + j] + ghn * r);
+            const float hv = hcur[b * H + j];
+            const float ho = (hv - nn) * z + nn;
+            hs[row * H + j] = ho;
+            if (ws) {
+                float* w = ws + row * 4 * H;
+                w[j] = r;
+                w[H + j] = z;
+                w[2 * H + j] = nn;
+                w[3 * H + j] = ghn;
+            }
+            hnxt[b * H + j] = keep[t * kt + a * ka + b * kb] ? ho : 0.0f;
+        }
+        __syncthreads();
+        float* tmp = hcur;
+        hcur = hnxt;
+        hnxt = tmp;
+    }
+}
+
+// Backpropagation through gru_seq_fwd_kernel's chunk, one block per network, t = C-1 .. 0:
+//   go = dhs[t] + carry;  gate gradients as gru_bwd_kernel -> dgi[t] (= dgh for the r, z gates; dgh_n = dan r)
+//   dh_prev = go z + dgh W_hh;  carry = keep[t-1] ? dh_prev : 0
+//   dW_hh += dgh^T h_prev, db_hh += sum_b dgh   (h_prev = keep[t-1] ? hs[t-1] : 0, zero at t = 0)
+// dW / db are written (this recurrence is their only use inside the chunk). LDS: dgh [B][3H], h_prev and carry
+// [B][H]. Thread (i, b) for dh_prev keeps column i of W_hh in registers; dW entries e = tid + 256 q are per thread.
+template <int H>
+__global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const float* __restrict__ dhs,
+                                                             const float* __restrict__ hs, const float* __restrict__ ws,
+                                                             const float* __restrict__ W,
+                                                             const uint8_t* __restrict__ keep, int64_t kt, int64_t ka,
+                                                             int64_t kb, float* __restrict__ dgi,
+                                                             float* __restrict__ dW, float* __restrict__ db) {
+    constexpr int G = 3 * H, NW = G * H / kBlock;  // dW entries per thread
+    extern __shared__ float4 seq_smem[];
+    float* dgh = reinterpret_cast<float*>(seq_smem);  // [B][G]
+    float* hprev = dgh + B * G;                        // [B][H]
+    float* carry = hprev + B * H;                      // [B][H]
+    const int64_t a = blockIdx.x;
+    const int tid = threadIdx.x, i = tid % H, bstep = kBlock / H;
+    const float* Wa = W + a * G * H;
+    float wc[G];  // column i of W_hh
+#pragma unroll
+    for (int g = 0; g < G; ++g) wc[g] = Wa[g * H + i];
+    float accw[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) accw[q] = 0.0f;
+    float accb = 0.0f;
+    for (int e = tid; e < B * H; e += kBlock) carry[e] = 0.0f;
+    for (int t = C - 1; t >= 0; --t) {
+        // h_prev of step t (the reset previous output), and the gate gradients
+        for (int e = tid; e < B * H; e += kBlock) {
+            const int b = e / H;
+            float v = 0.0f;
+            if (t > 0 && keep[(t - 1) * kt + a * ka + b * kb]) v = hs[((a * C + t - 1) * B + b) * H + (e - b * H)];
+            hprev[e] = v;
+        }
+        __syncthreads();  // carry (previous iteration) and hprev visible
+        for (int b = tid / H; b < B; b += bstep) {
+            const int64_t row = (a * C + t) * B + b;
+            const float* w = ws + row * 4 * H;
+            const float r = w[i], z = w[H + i], nn = w[2 * H + i], ghn = w[3 * H + i];
+            const float go = dhs[row * H + i] + carry[b * H + i];
+            const float hv = hprev[b * H + i];
+            const float dn = go * (1.0f - z);
+            const float dz = go * (hv - nn);
+            const float dan = dn * (1.0f - nn * nn);
+            const float dr = dan * ghn;
+            const float dar = dr * (r * (1.0f - r));
+            const float daz = dz * (z * (1.0f - z));
+            float* gi_ = dgi + row * G;
+            gi_[i] = dar;
+            gi_[H + i] = daz;
+            gi_[2 * H + i] = dan;
+            dgh[b * G + i] = dar;
+            dgh[b * G + H + i] = daz;
+            dgh[b * G + 2 * H + i] = dan * r;
+            carry[b * H + i] = go * z;  // the direct term of dh_prev; the W_hh term is added below
+        }
+        __syncthreads();
+        // dW_hh / db_hh partial sums of this step
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            const int e = tid + kBlock * q, g = e / H, ii = e - g * H;
+            float s = 0.0f;
+            for (int b = 0; b < B; ++b) s = fmaf(dgh[b * G + g], hprev[b * H + ii], s);
+            accw[q] += s;
+        }
+        if (tid < G) {
+            float s = 0.0f;
+            for (int b = 0; b < B; ++b) s += dgh[b * G + tid];
+            accb += s;
+        }
+        // dh_prev = go z + dgh W_hh, masked by the reset that produced h_prev
+        for (int b = tid / H; b < B; b += bstep) {
+            const float4* d4 = reinterpret_cast<const float4*>(dgh + b * G);
+            float s = 0.0f;
+#pragma unroll
+            for (int g4 = 0; g4 < G / 4; ++g4) {
+                const float4 v = d4[g4];
+                s = fmaf(v.x, wc[4 * g4], s);
+                s = fmaf(v.y, wc[4 * g4 + 1], s);
+                s = fmaf(v.z, wc[4 * g4 + 2], s);
+                s = fmaf(v.w, wc[4 * g4 + 3], s);
+            }
+            const bool kept = t > 0 && keep[(t - 1) * kt + a * ka + b * kb];
+            carry[b * H + i] = kept ? carry[b * H + i] + s : 0.0f;
+        }
+        __syncthreads();  // dgh / hprev reads done before the next step overwrites them
+    }
+#pragma unroll
+    for (int q = 0; q < NW; ++q) dW[a * G * H + tid + kBlock * q] = accw[q];
+    if (tid < G) db[a * G + tid] = accb;
+}
+
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(int64_t rows, int64_t width, const float* __restrict__ src,
                                                              const int64_t* __restrict__ idx, float* __restrict__ dst,
                                                              int scatter) {
@@ -416,6 +578,38 @@ int flock_gru_bwd(void* stream, int64_t rows, int H, const float* dhout, const f
     if (!dhout || !h || !ws || !dgi || !dgh || !dh) return fail(-3, "flock_gru_bwd: NULL pointer");
     hipLaunchKernelGGL(gru_bwd_kernel, dim3(grid_for(rows * H)), dim3(kBlock), 0, (hipStream_t)stream, rows, H, dhout,
                        h, ws, dgi, dgh, dh);
+    return launched();
+}
+
+int flock_gru_seq_fwd(void* stream, int A, int C, int B, int H, const float* gi, const float* w_hh, const float* b_hh,
+                      const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb, float* hs, float* ws) {
+    if (A <= 0 || C <= 0 || B <= 0) return 0;
+    if (!gi || !w_hh || !b_hh || !keep || !hs) return fail(-3, "flock_gru_seq_fwd: NULL pointer");
+    if (H != 32) return fail(-2, "flock_gru_seq_fwd: hidden size must be 32");
+    const size_t lds = (size_t)2 * B * H * sizeof(float);
+    if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_fwd: B too large for LDS");
+    if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(gru_seq_fwd_kernel<32>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(-4, "flock_gru_seq_fwd: cannot raise the LDS limit");
+    hipLaunchKernelGGL(gru_seq_fwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, gi, w_hh, b_hh,
+                       keep, keep_st, keep_sa, keep_sb, hs, ws);
+    return launched();
+}
+
+int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs, const float* hs, const float* ws,
+                      const float* w_hh, const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb,
+                      float* dgi, float* dw_hh, float* db_hh) {
+    if (A <= 0 || C <= 0 || B <= 0) return 0;
+    if (!dhs || !hs || !ws || !w_hh || !keep || !dgi || !dw_hh || !db_hh)
+        return fail(-3, "flock_gru_seq_bwd: NULL pointer");
+    if (H != 32) return fail(-2, "flock_gru_seq_bwd: hidden size must be 32");
+    const size_t lds = (size_t)B * (3 * H + 2 * H) * sizeof(float);
+    if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_bwd: B too large for LDS");
+    if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(gru_seq_bwd_kernel<32>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(-4, "flock_gru_seq_bwd: cannot raise the LDS limit");
+    hipLaunchKernelGGL(gru_seq_bwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dhs, hs, ws,
+                       w_hh, keep, keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh);
     return launched();
 }
 

@@ -292,7 +292,55 @@ class _GRUCellFn(torch.autograd.Function):
 
 def gru_cell(x, h, W_ih, W_hh, b_ih, b_hh):
     """nn.GRUCell for A agents at once: x [A,B,in] (or shared [B,in]), h [A,B,H] -> h' [A,B,H]."""
-    gi = blinear(x, W_ih, b_ih)
+    return gru_cell_gi(blinear(x, W_ih, b_ih), h, W_hh, b_hh)
+
+
+class _GRUSeqFn(torch.autograd.Function):
+    """A chunk of GRUCell steps for A networks in one launch each way (flock_gru_seq_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, gi, W_hh, b_hh, keep, save):
+        A, C, B, G = gi.shape
+        H = G // 3
+        gi, W_hh, b_hh = gi.contiguous(), W_hh.contiguous(), b_hh.contiguous()
+        k8 = keep.view(torch.uint8) if keep.dtype == torch.bool else keep
+        hs = torch.empty((A, C, B, H), dtype=gi.dtype, device=gi.device)
+        ws = torch.empty((A, C, B, 4 * H), dtype=gi.dtype, device=gi.device) if save else None
+        st = k8.stride()
+        rc = _native.lib().flock_gru_seq_fwd(_stream(gi.device), A, C, B, H, _p(gi), _p(W_hh), _p(b_hh), _p(k8),
+                                             st[0], st[1], st[2], _p(hs), _p(ws))
+        _native.check(rc, "flock_gru_seq_fwd", learn=True)
+        if save:
+            ctx.save_for_backward(hs, ws, W_hh, k8)
+        return hs
+
+    @staticmethod
+    def backward(ctx, dhs):
+        hs, ws, W_hh, k8 = ctx.saved_tensors
+        A, C, B, H = hs.shape
+        dhs = dhs.contiguous()
+        dgi = torch.empty((A, C, B, 3 * H), dtype=hs.dtype, device=hs.device)
+        dW = torch.empty_like(W_hh)
+        db = torch.empty((A, 3 * H), dtype=hs.dtype, device=hs.device)
+        st = k8.stride()
+        rc = _native.lib().flock_gru_seq_bwd(_stream(hs.device), A, C, B, H, _p(dhs), _p(hs), _p(ws), _p(W_hh),
+                                             _p(k8), st[0], st[1], st[2], _p(dgi), _p(dW), _p(db))
+        _native.check(rc, "flock_gru_seq_bwd", learn=True)
+        return dgi, dW, db, None, None
+
+
+def gru_seq(gi, W_hh, b_hh, keep):
+    """GRUCell recurrence of A networks over a chunk of C steps from a zero hidden state: gi [A,C,B,3H] (every
+    step's x W_ih^T + b_ih), W_hh [A,3H,H], b_hh [A,3H], keep [C,A,B] bool (False: reset the hidden state after
+    that step; may be an expanded view) -> hs [A,C,B,H], each step's output before its reset."""
+    assert keep.dim() == 3 and keep.shape == (gi.shape[1], gi.shape[0], gi.shape[2])
+    save = torch.is_grad_enabled() and any(t.requires_grad for t in (gi, W_hh, b_hh))
+    return _GRUSeqFn.apply(gi, W_hh, b_hh, keep, save)
+
+
+def gru_cell_gi(gi, h, W_hh, b_hh):
+    """gru_cell from precomputed input-side gate pre-activations gi = x W_ih^T + b_ih [A,B,3H] (a recurrence can
+    compute them for every step at once)."""
     gh = blinear(h, W_hh, b_hh)
     return _GRUCellFn.apply(gi, gh, h)
 

@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell, shared_linear
+from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell, gru_seq, shared_linear
 
 HR = 32  # hidden_rnn (net.py:15,100)
 
@@ -119,10 +119,25 @@ def actor_forward(P, x, h, recurrent):
     return torch.tanh(blinear(y, P["fc3.weight"], P["fc3.bias"])), h
 
 
-def critic_fce(P, x):
-    """The recurrent critics' input layer for every agent and every chunk step at once: x [T,B,N*k] (shared by all
-    critics) -> T tensors [A,B,32]. One GEMM [T*B, N*k] x [N*k, A*32]; its weight gradient is one GEMM too."""
-    return shared_linear(x, P["fce.weight"], P["fce.bias"]).unbind(1)
+def actor_seq(P, x, keep):
+    """The recurrent actors' GRU over a whole chunk: x [A,C,B,k], keep [C,A,B] -> hidden outputs [A,C,B,32]
+    (each step's, before its done reset). fce and the GRU input GEMM run once for all steps; the recurrence is one
+    gru_seq launch."""
+    A, C, B, k = x.shape
+    y = blinear(x.reshape(A, C * B, k), P["fce.weight"], P["fce.bias"])
+    gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, 3 * HR)
+    return gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep)
+
+
+def critic_seq(P, x, keep):
+    """The recurrent critics' GRU over a whole chunk: x [C,B,N*k] shared by every critic, keep [C,A,B] ->
+    (hidden outputs [A,C,B,32], fce outputs [A,C,B,32]). fce is one GEMM [C*B, N*k] x [N*k, A*32] for every agent
+    and step (its weight gradient one GEMM too), the GRU input GEMM one batched GEMM, the recurrence one gru_seq."""
+    C, B, _ = x.shape
+    fx = shared_linear(x, P["fce.weight"], P["fce.bias"])               # [A, C, B, 32] (a permuted view)
+    A = fx.shape[0]
+    gi = blinear(fx.reshape(A, C * B, HR), P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, 3 * HR)
+    return gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep), fx
 
 
 def critic_gru(P, fx, h):
@@ -307,34 +322,23 @@ class MADDPGLearner:
         if self.recurrent:
             # MADDPG.py:95-132. critic_values, target_critic_values and the actions are overwritten at every chunk
             # step and read only after the loop, so before the last step only the four GRU recurrences reach the
-            # loss: the heads run once, on the last step's hidden states (identical results, C x less head work).
-            # The critics' input layer does not depend on the recurrence: one GEMM for all steps and agents.
-            zero = lambda: torch.zeros((N, B, HR), device=self.device)  # noqa: E731
-            h_ta, h_tc, h_c, h_a = zero(), zero(), zero(), zero()
+            # loss: each runs as one whole-chunk gru_seq, and the heads run once, on the last step's hidden states
+            # (identical results, C x less head work). hidden[done_mask[:, i]] = 0 is the keep mask (:117-132).
+            keep = (D == 0).permute(1, 2, 0)                                # [C, N, B]
             with torch.no_grad():
-                fx_t = critic_fce(Ptc, S2)
-            fx = critic_fce(Pc, S)
-            for t in range(C):
-                with torch.no_grad():
-                    h_ta = actor_gru(Pta, AS2[:, t], h_ta)
-                    h_tc = critic_gru(Ptc, fx_t[t], h_tc)
-                    h_a = actor_gru(Pa, AS[:, t], h_a)
-                h_c = critic_gru(Pc, fx[t], h_c)
-                if t == last:
-                    y_ta, y_tc, y_c, y_a = h_ta, h_tc, h_c, h_a                # the heads see the pre-reset state
-                # hidden[done_mask[:, i]] = 0 for the four hidden lists (MADDPG.py:117-132)
-                keep = (D[:, t] == 0).t().unsqueeze(-1)                         # [N, B, 1]
-                h_ta = torch.where(keep, h_ta, 0.0)
-                h_tc = torch.where(keep, h_tc, 0.0)
-                h_c = torch.where(keep, h_c, 0.0)
-                h_a = torch.where(keep, h_a, 0.0)
+                y_ta = actor_seq(Pta, AS2, keep)[:, last]
+                y_tc = critic_seq(Ptc, S2, keep)[0][:, last]
+                y_a = actor_seq(Pa, AS, keep)[:, last]
+            hs_c, fx = critic_seq(Pc, S, keep)
+            y_c = hs_c[:, last]                                             # the heads see the pre-reset state
+            h_c = torch.where(keep[last].unsqueeze(-1), y_c, 0.0)
             with torch.no_grad():
                 cta = actor_head(Pta, y_ta).transpose(0, 1).reshape(B, 2 * N)   # torch.cat(..., dim=1)
                 tq = critic_head(Ptc, F.relu(blinear(y_tc, Ptc["fc1.weight"], Ptc["fc1.bias"])), cta)
                 cpa = actor_head(Pa, y_a).transpose(0, 1).reshape(B, 2 * N)
             # the actor-loss critic call (:137) steps the GRU once more from the reset hidden state; its head and
             # the critic-loss head share one pass over a 2B batch
-            h_aq = critic_gru(Pc, fx[last], h_c)
+            h_aq = critic_gru(Pc, fx[:, last], h_c)
             y = F.relu(blinear(torch.cat([y_c, h_aq], 1), Pc["fc1.weight"], Pc["fc1.bias"]))
             qq = critic_head(Pc, y, torch.cat([act[last], cpa], 0))
             q, aq = qq[:, :B], qq[:, B:]

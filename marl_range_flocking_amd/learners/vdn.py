@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell
+from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell, gru_seq
 
 HX = 32
 
@@ -66,6 +66,22 @@ class BatchedQNet:
             y = gru_cell(y, h, P["gru.weight_ih"], P["gru.weight_hh"], P["gru.bias_ih"], P["gru.bias_hh"])
             h = y
         return blinear(y, P["q.weight"], P["q.bias"]), h
+
+    def forward_seq(self, x, keep, P=None):
+        """A whole chunk, agent-major: x [A,C,B,n_obs], keep [C,B] (False: the hidden state is reset after that
+        step, train_flock.py:34-36) -> q [A,C,B,n_actions] from zero initial hidden states. The feature layers, the
+        GRU input GEMM and the q head do not depend on the recurrence, so each runs ONCE over all C steps (one
+        batched GEMM of C*B rows per agent); the recurrence itself (hidden GEMM, gates, resets) is one gru_seq
+        launch. Same per-step math as forward_am."""
+        P = self.P.params if P is None else P
+        A, C, B, n = x.shape
+        y = F.relu(blinear(x.reshape(A, C * B, n), P["feat1.weight"], P["feat1.bias"]))
+        y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
+        if self.recurrent:  # the whole chunk's recurrence in one launch each way (flock_gru_seq_fwd / _bwd)
+            gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
+            hs = gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep.unsqueeze(1).expand(C, A, B))
+            y = hs.view(A, C * B, self.hx_size)
+        return blinear(y, P["q.weight"], P["q.bias"]).view(A, C, B, -1)
 
     def __call__(self, obs, hidden):
         """Reference layout: obs [B,A,n_obs], hidden [B,A,H] -> (q [B,A,n_actions], hidden [B,A,H])."""
@@ -186,22 +202,21 @@ class VDNLearner:
         s2 = self.replay.gather("s_prime", idx).permute(1, 2, 0, 3)
         done = self.replay.gather("done", idx).t()                      # [C, B]
         Pq, Pt = self.train_leaves, self.target_params()
-        h = torch.zeros((A, B, HX), device=self.device)
-        ht = torch.zeros((A, B, HX), device=self.device)
-        loss = 0
-        for t in range(C):
-            q_out, h = self.q.forward_am(s[t], h, Pq)                    # [A, B, n_act]
-            q_a = q_out.gather(2, a[t].unsqueeze(-1)).squeeze(-1)        # [A, B]
-            sum_q = q_a.sum(dim=0).unsqueeze(1)                          # [B, 1]
-            with torch.no_grad():
-                qp, ht = self.q.forward_am(s2[t], ht, Pt)
-                max_q = qp.max(dim=2)[0]                                 # [A, B]
-                target_q = r[t].sum(dim=1, keepdim=True)
-                target_q = target_q + self.gamma * max_q.sum(dim=0).unsqueeze(1) * (1 - done[t]).unsqueeze(1)
-            loss = loss + F.smooth_l1_loss(sum_q, target_q)
-            keep = (done[t] == 0).view(1, B, 1)                          # hidden[done_mask] = 0 (:36-38)
-            h = torch.where(keep, h, torch.zeros((), device=self.device))
-            ht = torch.where(keep, ht, torch.zeros((), device=self.device))
+        keep = done == 0                                                # hidden[done_mask] = 0 (:34-36)
+        # agent-major whole-chunk tensors [A, C, B, ...] (one GEMM per layer for all steps, BatchedQNet.forward_seq)
+        q_out = self.q.forward_seq(s.permute(1, 0, 2, 3), keep, Pq)      # [A, C, B, n_act]
+        q_a = q_out.gather(3, a.permute(1, 0, 2).unsqueeze(-1)).squeeze(-1)
+        sum_q = q_a.sum(dim=0)                                          # [C, B]
+        with torch.no_grad():
+            qp = self.q.forward_seq(s2.permute(1, 0, 2, 3), keep, Pt)
+            max_q = qp.max(dim=3)[0]                                    # [A, C, B]
+            target_q = r.sum(dim=2)                                     # [C, B]
+            target_q = target_q + self.gamma * max_q.sum(dim=0) * (1 - done)
+        # loss += smooth_l1_loss(sum_q_t, target_q_t) over the chunk steps (:29): per-step means, summed in order
+        per_step = F.smooth_l1_loss(sum_q, target_q, reduction="none").mean(dim=1)
+        loss = per_step[0]
+        for t in range(1, C):
+            loss = loss + per_step[t]
         self.q.P.grads_into(loss, Pq)
         with torch.no_grad():
             self.loss.copy_(loss.detach())

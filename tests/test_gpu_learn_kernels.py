@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 import torch
 
-from marl_range_flocking_amd.learners.core import FlatParams, GradNorm, ReplayRing, gru_cell
+from marl_range_flocking_amd.learners.core import FlatParams, GradNorm, ReplayRing, gru_cell, gru_cell_gi, gru_seq
 
 pytestmark = pytest.mark.gpu
 
@@ -120,3 +120,34 @@ def test_ring_store_fused_matches_row_copies(cap, n, steps, cuda):
     for k in ref:
         assert torch.equal(ring.bufs[k].reshape(cap, -1), ref[k]), k
     assert ring.counter == n * steps
+
+
+@pytest.mark.parametrize("A,C,B,per_agent", [(3, 10, 32, False), (5, 10, 128, True), (2, 1, 7, True), (4, 4, 200, False)])
+def test_gru_seq_matches_per_step_grucell(A, C, B, per_agent, cuda):
+    """flock_gru_seq_fwd/_bwd (one launch per chunk) against the per-step loop the learners used before: gru_cell
+    per step (hidden GEMM + gate kernel) with the done reset between steps, fp32 autograd, same inputs."""
+    g = torch.Generator(device=cuda).manual_seed(A * 100 + B)
+    H = 32
+    gi = torch.randn(A, C, B, 3 * H, device=cuda, generator=g, requires_grad=True)
+    W = (0.3 * torch.randn(A, 3 * H, H, device=cuda, generator=g)).requires_grad_()
+    b = (0.3 * torch.randn(A, 3 * H, device=cuda, generator=g)).requires_grad_()
+    if per_agent:   # MADDPG: a done flag per agent, strided view [C, A, B]
+        keep = (torch.rand(B, C, A, device=cuda, generator=g) > 0.2).permute(1, 2, 0)
+    else:           # VDN: one flag per batch row, expanded over agents
+        keep = (torch.rand(C, B, device=cuda, generator=g) > 0.2).unsqueeze(1).expand(C, A, B)
+    hs = gru_seq(gi, W, b, keep)
+    h = torch.zeros(A, B, H, device=cuda)
+    ref = []
+    for t in range(C):
+        h = gru_cell_gi(gi[:, t], h, W, b)
+        ref.append(h)
+        h = torch.where(keep[t].unsqueeze(-1), h, 0.0)
+    ref = torch.stack(ref, 1)
+    torch.testing.assert_close(hs, ref, rtol=1e-5, atol=1e-6)
+    dout = torch.randn(A, C, B, H, device=cuda, generator=g)
+    d1 = torch.autograd.grad(hs, (gi, W, b), dout)
+    d2 = torch.autograd.grad(ref, (gi, W, b), dout)
+    for x, y, name in zip(d1, d2, ("dgi", "dW_hh", "db_hh")):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5, msg=name)
+    with torch.no_grad():  # no saved gates without grad
+        torch.testing.assert_close(gru_seq(gi, W, b, keep), ref, rtol=1e-5, atol=1e-6)
