@@ -27,9 +27,10 @@ import torch
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_TLANEOPS = 78.6        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (f32 non-packed lane-ops/s, /1e12)
 BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
-# fused replay insert (flock_step_v2_store): + previous obs read (k=4 floats) + ring row written
-# (state 16 + action 8 + reward 4 + new_state 16 + terminal 4 bytes)
-RING_BYTES_PER_AGENT_STEP = 16 + 48
+# fused replay insert (flock_step_v2_store), per agent-step: + previous obs read (k=4 floats) + the ring fields
+# written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG record: state,
+# next_state, actor_state, actor_next_state 16 each + action 8 + reward 4 + done 4
+RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80}
 OPS_PER_PAIR = {True: 12, False: 7}  # algorithmic VALU ops per agent pair: periodic / Euclidean
 
 
@@ -195,16 +196,16 @@ class MADDPGBench:
 
     def describe(self):
         return (f"RNN-MADDPG train() every {self.every} vectorized steps (B 128, chunk 10, {self.env.N} critics "
-                f"400/300); all {self.env.E} env records per step inserted into a 45k-row device replay ring"
+                f"400/300); all {self.env.E} env records per step inserted into a 45k-row device replay ring by the "
+                f"env kernel itself"
                 + ("; critic gradient all-reduce over RCCL" if self.learner.distributed else ""))
 
     def before(self, s):
-        self.prev = self.env.dnn
-        return None
+        # the env kernel writes every env's record itself (flock_step_v2_store, one ring row per env)
+        return self.learner.replay_slots(self.env.E)
 
     def after(self, s, a):
-        env, L = self.env, self.learner
-        L.add_record(self.prev, env.dnn, a, self.prev, env.dnn, env.reward, env.done)
+        L = self.learner
         if (s + 1) % self.every == 0 and L.check_buffer_size():
             L.train()
 
@@ -284,8 +285,8 @@ def main():
 
     total_agent_steps = world * E * N * args.steps
     value = total_agent_steps / el
-    fused_ring = args.learner == "shared_critic"
-    bpa = BYTES_PER_AGENT_STEP[args.variant] + (RING_BYTES_PER_AGENT_STEP if fused_ring else 0)
+    fused_ring = args.learner in RING_BYTES_PER_AGENT_STEP
+    bpa = BYTES_PER_AGENT_STEP[args.variant] + RING_BYTES_PER_AGENT_STEP.get(args.learner, 0)
     bytes_launch = bpa * E * N
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = None

@@ -56,13 +56,20 @@ int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_ran
                   float* pos, float* heading, const float* action,
                   float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
 
-/* The same step fused with the replay insert of the training loop that drives it
- * (learners/maddpg_shared_critic/train_flock.py:112-127: step, then store_transitions(state, action, reward,
- * new_state, done), utils.py:47-54): agent a = env * N + i also writes ring row (start + a) mod capacity:
- * state[k] = prev_obs[a][0..k), action[2] = the raw action, reward, new_state[k] = the new dnn row,
- * terminal = 1 - done. When E * N > capacity only the last `capacity` transitions survive (as in a ring insert):
- * agents a < skip write nothing and agent a >= skip writes row (start + a - skip) mod capacity.
- * Requires 0 <= skip, E * N - skip <= capacity and 0 <= start < capacity. */
+/* The same step fused with the replay insert of the training loop that drives it. Two row layouts:
+ *  group = 1 (learners/maddpg_shared_critic/train_flock.py:112-127: step, then store_transitions(state, action,
+ *   reward, new_state, done), utils.py:47-54): agent a = env * N + i owns ring row (start + a) mod capacity:
+ *   state[k] = prev_obs[a][0..k), action[2] = the raw action, reward, new_state[k] = the new dnn row,
+ *   terminal = 1 - done;
+ *  group = N (main.py:41 / learners/maddpg_official_rnn/train_flock.py:45: add_record(obs["actors"],
+ *   next_obs["actors"], actions, state, next_state, reward, done[0]), memory_rnn.py:53-67): env e owns ring row
+ *   (start + e) mod capacity and agent i its slot i of that row: state[row][i][k], action[row][i][2],
+ *   reward[row][i], new_state[row][i][k], terminal[row][i]; actor_state / actor_new_state (may be NULL) receive
+ *   the same observation rows again (the record's actor copies).
+ * store_done: 0 stores 1 - done (the shared critic's terminal), 1 stores done (the RNN-MADDPG record).
+ * When the step produces more rows than capacity only the last `capacity` survive (as in a ring insert): units
+ * (agents or envs) u < skip write nothing and unit u >= skip writes row (start + u - skip) mod capacity.
+ * Requires 0 <= skip, rows - skip <= capacity and 0 <= start < capacity. */
 typedef struct FlockRing {
     float* state;
     float* action;
@@ -73,6 +80,10 @@ typedef struct FlockRing {
     int64_t capacity;
     int64_t start;
     int64_t skip;
+    float* actor_state;
+    float* actor_new_state;
+    int64_t group;
+    int store_done;
 } FlockRing;
 int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
                         float dt, float v_min, float v_max, int periodic, int rigid_boundary,

@@ -71,7 +71,9 @@ class FlockRing(ctypes.Structure):
     """Mirror of ``FlockRing`` (include/flock_amd.h): replay-ring targets of flock_step_v2_store."""
 
     _fields_ = ([(n, _c_void_p) for n in ("state", "action", "reward", "new_state", "terminal", "prev_obs")]
-                + [("capacity", ctypes.c_int64), ("start", ctypes.c_int64), ("skip", ctypes.c_int64)])
+                + [("capacity", ctypes.c_int64), ("start", ctypes.c_int64), ("skip", ctypes.c_int64)]
+                + [("actor_state", _c_void_p), ("actor_new_state", _c_void_p), ("group", ctypes.c_int64),
+                   ("store_done", _c_int)])
 
 
 SIGNATURES.update({

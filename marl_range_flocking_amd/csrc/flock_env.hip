@@ -80,9 +80,10 @@ struct Params {
     uint8_t* any_done;
     int* status;
     // fused replay insert (flock_step_v2_store)
-    float *r_state, *r_action, *r_reward, *r_new, *r_term;
+    float *r_state, *r_action, *r_reward, *r_new, *r_term, *r_astate, *r_anew;
     const float* r_prev;
     int64_t r_cap, r_start, r_skip;
+    int r_group, r_done;  // agents per ring row (1 or N); stored flag: 0 -> 1 - done, 1 -> done
     // cell list (step variants, N >= 128)
     int cells, ecap;  // grid side Gc, extended-array capacity per env (2N)
     float cw, inv_cw, cell_eps;
@@ -443,7 +444,11 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     float prev_obs[L - 2];  // fused replay insert: the previous observation row, loaded early (latency hidden)
 #pragma unroll
     for (int s = 0; s < L - 2; ++s) prev_obs[s] = 0.0f;
-    if (active && p.r_state && (int64_t)a >= p.r_skip) {
+    // fused replay insert: ring unit (row) of this agent and its slot within the row (one row per agent, or one
+    // row per env holding every agent's fields, group = N)
+    const int64_t r_unit = p.r_group == 1 ? (int64_t)a : (int64_t)env;
+    const int r_slot = p.r_group == 1 ? 0 : i;
+    if (active && p.r_state && r_unit >= p.r_skip) {
         const float* po = p.r_prev + a * p.k;
 #pragma unroll
         for (int s = 0; s < L - 2; ++s)
@@ -690,18 +695,21 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
                 r = coll ? -5.0f : 0.01f;  // gym_flock_v2.py:217-220, gym_flock.py:142-145
             }
             p.reward[a] = r;
-            if (p.r_state && (int64_t)a >= p.r_skip) {  // fused replay insert: row (start + a - skip) mod cap
-                int64_t row = p.r_start + (int64_t)a - p.r_skip;
+            if (p.r_state && r_unit >= p.r_skip) {  // fused replay insert: row (start + unit - skip) mod cap
+                int64_t row = p.r_start + r_unit - p.r_skip;
                 if (row >= p.r_cap) row -= p.r_cap;
+                const int64_t e = row * p.r_group + r_slot;  // this agent's element of the row
 #pragma unroll
                 for (int s = 0; s < L - 2; ++s)
                     if (s < p.k) {
-                        p.r_state[row * p.k + s] = prev_obs[s];
-                        p.r_new[row * p.k + s] = dv[s];
+                        p.r_state[e * p.k + s] = prev_obs[s];
+                        p.r_new[e * p.k + s] = dv[s];
+                        if (p.r_astate) p.r_astate[e * p.k + s] = prev_obs[s];
+                        if (p.r_anew) p.r_anew[e * p.k + s] = dv[s];
                     }
-                reinterpret_cast<float2*>(p.r_action)[row] = act_in;
-                p.r_reward[row] = r;
-                p.r_term[row] = coll ? 0.0f : 1.0f;
+                reinterpret_cast<float2*>(p.r_action)[e] = act_in;
+                p.r_reward[e] = r;
+                p.r_term[e] = (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f;
             }
         }
     }
@@ -971,9 +979,11 @@ int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sens
     if (E && (!ring->state || !ring->action || !ring->reward || !ring->new_state || !ring->terminal ||
               !ring->prev_obs))
         return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL ring pointer");
-    if (ring->skip < 0 || (int64_t)E * N - ring->skip > ring->capacity || ring->start < 0 ||
-        ring->start >= ring->capacity)
-        return fail(FLOCK_E_ARG, "flock_step_v2_store: need skip >= 0, E*N - skip <= capacity, 0 <= start < capacity");
+    if (ring->group != 1 && ring->group != N)
+        return fail(FLOCK_E_ARG, "flock_step_v2_store: ring group must be 1 (a row per agent) or N (a row per env)");
+    const int64_t units = ring->group == 1 ? (int64_t)E * N : (int64_t)E;
+    if (ring->skip < 0 || units - ring->skip > ring->capacity || ring->start < 0 || ring->start >= ring->capacity)
+        return fail(FLOCK_E_ARG, "flock_step_v2_store: need skip >= 0, rows - skip <= capacity, 0 <= start < capacity");
     Params p = base(E, N, k, box);
     p.variant = FLOCK_VARIANT_V2;
     p.periodic = periodic != 0;
@@ -1001,6 +1011,10 @@ int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sens
     p.r_cap = ring->capacity;
     p.r_start = ring->start;
     p.r_skip = ring->skip;
+    p.r_astate = ring->actor_state;
+    p.r_anew = ring->actor_new_state;
+    p.r_group = (int)ring->group;
+    p.r_done = ring->store_done;
     return dispatch(p, (hipStream_t)stream, false);
 }
 

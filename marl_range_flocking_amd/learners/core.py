@@ -396,6 +396,23 @@ class ReplayRing:
         _native.check(rc, "flock_ring_store", learn=True)
         self.counter += n
 
+    def step_slots(self, n, state, action, reward, new_state, terminal, actor_state=None, actor_new_state=None,
+                   group=1, store_done=False):
+        """Reserve the next n rows for an env step that writes them itself (VecFlockEnv.step(ring=...) ->
+        flock_step_v2_store) and return the kernel's FlockRing: same rows and counter as store() (when n exceeds
+        the capacity only the last `capacity` rows are kept). Field names map the kernel's targets to this ring's
+        fields; group = agents per row (1, or N for one row per env); store_done: store done (else 1 - done)."""
+        skip = max(0, n - self.capacity)
+        b = self.bufs
+        ptr = lambda name: None if name is None else b[name].data_ptr()  # noqa: E731
+        ring = _native.FlockRing(state=ptr(state), action=ptr(action), reward=ptr(reward), new_state=ptr(new_state),
+                                 terminal=ptr(terminal), prev_obs=None, capacity=self.capacity,
+                                 start=(self.counter + skip) % self.capacity, skip=skip,
+                                 actor_state=ptr(actor_state), actor_new_state=ptr(actor_new_state), group=group,
+                                 store_done=int(bool(store_done)))
+        self.counter += n
+        return ring
+
     def scatter(self, name, idx, rows):
         """Write rows at arbitrary positions idx (HIP row scatter)."""
         idx = idx.to(device=self.device, dtype=torch.int64).contiguous()

@@ -294,6 +294,14 @@ class MADDPGLearner:
                            "actor_state": f(actor_states, N, k), "actor_next_state": f(actor_next_states, N, k),
                            "action": f(actions, N, 2), "reward": f(reward, N), "done": f(done, N)})
 
+    def replay_slots(self, n_envs):
+        """Reserve the next n_envs records for an env step that writes them itself (VecFlockEnv.step(ring=...)):
+        the record add_record(obs, next_obs, actions, obs, next_obs, reward, done) of every env, one ring row per
+        env (critic and actor observations are the same dnn rows here, as main.py:34-41 passes for v2)."""
+        return self.replay.step_slots(n_envs, "state", "action", "reward", "next_state", "done",
+                                      actor_state="actor_state", actor_new_state="actor_next_state", group=self.N,
+                                      store_done=True)
+
     # ---------------------------------------------------------------- update
     def _update(self):
         self._fwd_bwd()

@@ -221,15 +221,7 @@ class SharedCriticLearner:
         """Reserve the next n replay rows for an env step that writes its transitions itself
         (VecFlockEnv.step(ring=...) -> flock_step_v2_store); same rows and counter as store_transitions (when n
         exceeds the capacity only the last `capacity` transitions are kept, as ReplayRing.store does)."""
-        R = self.replay
-        skip = max(0, n - R.capacity)
-        b = R.bufs
-        ring = _native.FlockRing(state=b["state"].data_ptr(), action=b["action"].data_ptr(),
-                                 reward=b["reward"].data_ptr(), new_state=b["new_state"].data_ptr(),
-                                 terminal=b["terminal"].data_ptr(), prev_obs=None, capacity=R.capacity,
-                                 start=(R.counter + skip) % R.capacity, skip=skip)
-        R.counter += n
-        return ring
+        return self.replay.step_slots(n, "state", "action", "reward", "new_state", "terminal")
 
     @property
     def mem_cntr(self):

@@ -216,6 +216,42 @@ def test_shared_ou_matches_sequential_process(cuda):
     torch.testing.assert_close(xs, torch.stack(ref, 1).float(), rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("cap", [100, 40], ids=["wrap", "step-larger-than-ring"])
+def test_fused_env_record_insert_matches_add_record(cap, cuda):
+    """The RNN-MADDPG record layout (one ring row per env, memory_rnn.py:53-67): VecFlockEnv.step(ring=
+    learner.replay_slots(E)) leaves every replay field and the counter bitwise equal to step() followed by
+    add_record(obs, next_obs, actions, obs, next_obs, reward, done) for every env, across a ring wrap and with a
+    step of more envs than the ring holds."""
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+    E, N, k, box = 64, 12, 4, 55.0
+    envs, learners = [], []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0), device=cuda)
+        g = torch.Generator(device=cuda).manual_seed(5)
+        env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
+        env.headings.copy_(torch.rand(E, N, device=cuda, generator=g) * 4.7)
+        env.step(torch.zeros(E, N, 2, device=cuda))
+        envs.append(env)
+        learners.append(MADDPGLearner(N, k, recurrent=True, hidden1=16, hidden2=8, batch_size=8, chunk_size=4,
+                                      buffer_capacity=cap, min_size_buffer=8, device=cuda, use_graph=False))
+    g = torch.Generator(device=cuda).manual_seed(9)
+    for _ in range(3):
+        a = torch.stack([torch.rand(E, N, device=cuda, generator=g) * 3 - 0.5,
+                         torch.rand(E, N, device=cuda, generator=g) * 4 - 2], -1).contiguous()
+        fused_env, plain_env = envs
+        fused_env.step(a, ring=learners[0].replay_slots(E))
+        prev = plain_env.dnn.clone()
+        plain_env.step(a)
+        learners[1].add_record(prev, plain_env.dnn, a, prev, plain_env.dnn, plain_env.reward, plain_env.done)
+        assert torch.equal(fused_env.dnn, plain_env.dnn) and torch.equal(fused_env.reward, plain_env.reward)
+    assert learners[0].replay.counter == learners[1].replay.counter == 3 * E
+    for name in learners[0].replay.bufs:
+        assert torch.equal(learners[0].replay.bufs[name], learners[1].replay.bufs[name]), name
+
+
 @pytest.mark.parametrize("cap", [10000, 5000], ids=["wrap", "step-larger-than-ring"])
 def test_fused_env_replay_insert_matches_store_transitions(cap, cuda):
     """VecFlockEnv.step(ring=learner.replay_slots(n)) (flock_step_v2_store) leaves the replay ring, counter and
