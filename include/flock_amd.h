@@ -11,6 +11,10 @@
  *   action_id [E][N] i64 · noise [E][N][2] f32 · dnn [E][N][k] f32 · nn_idx [E][N][k] i64
  *   reward [E][N] f32 · done [E][N] u8 · any_done [E] u8 · obs memory [E][N][4][k] f32
  * State arrays marked (rw) are updated in place, as the reference mutates self.positions / self.headings.
+ * nn_idx of the step entry points is read before it is written: on entry it may hold anything; when it holds an
+ * earlier step's indices of the same envs (e.g. the previous step's output) the N >= 128 cell-list kNN uses them as
+ * search seeds. The results never depend on its content (seeds that are out of range or repeated are ignored, and
+ * every seeded search is exact by construction).
  *
  * Each entry point replaces one reference step()/reset() (paths relative to RetamalVictor/marl-range-flocking):
  *   flock_step_v2          environments/gym_flock_v2.py:71-83  (periodic=1; the RNN fork

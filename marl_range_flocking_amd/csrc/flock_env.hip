@@ -95,6 +95,40 @@ struct Params {
 };
 
 // ---------------------------------------------------------------------------------------------------------------
+// phase timing (diagnostics build only: tools/phase_prof.py compiles this file with -DFLOCK_PHASE_PROF into a
+// separate library; the product build has no counters)
+#ifdef FLOCK_PHASE_PROF
+// 64 slots x 32 counters (slot = blockIdx mod 64) so the end-of-kernel atomics do not pile onto one address
+__device__ unsigned long long g_phase[64 * 32];
+#define PHASE(n)                                                             \
+    do {                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+        ph_acc[n] += t_ - t_prev;                                            \
+        t_prev = t_;                                                         \
+    } while (0)
+#define PHASE_COUNT(n, v) \
+    do {                  \
+        ph_acc[n] += (v); \
+    } while (0)
+#define PHASE_FLUSH()                                                                               \
+    do {                                                                                            \
+        if ((threadIdx.x & 63) == 0)                                                                \
+            _Pragma("unroll") for (int q_ = 0; q_ < 24; ++q_)                                       \
+                if (ph_acc[q_]) atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + q_], ph_acc[q_]);       \
+    } while (0)
+#else
+#define PHASE_FLUSH() \
+    do {              \
+    } while (0)
+#define PHASE(n) \
+    do {         \
+    } while (0)
+#define PHASE_COUNT(n, v) \
+    do {                  \
+    } while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------------------------------
 // small helpers
 
 // Correctly-rounded sqrt. NOTE: HIP's __fsqrt_rn is ocml's *native* (1-ulp) sqrt unless OCML_BASIC_ROUNDED_OPERATIONS
@@ -234,20 +268,113 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
     }
 }
 
-// phase 3c: the (2R+1) x (2R+1) cell neighbourhood (2R+1 contiguous ranges of the extended cell-sorted array, R = 1
-// or 2); returns true when the top-L keys are provably those of the full scan (see the file header). Uses
-// wave-wide reductions: call it with every lane of the wave active (lanes without an agent pass live = false:
-// empty ranges, result true).
+// Cell-list scans (step variants, N >= 128). The env's agents are binned into a Gc x Gc grid (Gc = floor(sqrt N),
+// about one agent per cell) and stored cell-sorted in an extended array ext of (x, y, j, sx) in which every cell
+// row also carries ghost copies of its last kRg columns (in front) and first kRg columns (behind) when the box is
+// periodic, so any run of up to 2*kRg+1 columns of a row is ONE contiguous range. sx = box for a ghost copy, else 0.
+constexpr int kRg = 3;
+
+// d2 of two candidates of one row range, bit-identical to the reference's periodic/Euclidean d2 in op order: with
+// Gc >= 11 and at most kRg(+1) cells between the lane's cell and a scanned cell, a regular entry has |d| < B/2 (the
+// reference keeps |d|, and (0 - |d|)^2 == d^2 bit for bit) and a ghost entry (sx = B) or a wrapped row (sy = B) has
+// |d| > B/2 (the reference takes B - |d|). So min(|d|, B - |d|) becomes one subtraction with an |.| modifier.
+__device__ __forceinline__ f32x2 pair_d2_shift(float xi, float yi, float sy, const float4& q0, const float4& q1) {
+    const float dx0 = __fsub_rn(q0.w, fabsf(__fsub_rn(xi, q0.x))), dx1 = __fsub_rn(q1.w, fabsf(__fsub_rn(xi, q1.x)));
+    const float dy0 = __fsub_rn(sy, fabsf(__fsub_rn(yi, q0.y))), dy1 = __fsub_rn(sy, fabsf(__fsub_rn(yi, q1.y)));
+    const f32x2 dx = {dx0, dx1}, dy = {dy0, dy1};
+    return dx * dx + dy * dy;
+}
+
+// one row range [s, e) of ext into the insertion network; tmax = the wave-wide maximum of e - s (a plain counted
+// loop: every lane of the wave runs it, lanes with an empty range insert nothing). Pairs are read from one
+// clamped base: ext holds at most 2N entries (an agent has at most one ghost copy, Gc >= 2 kRg) and
+// ecap = 2N + 2, so a clamped pair lies past every range end and both its keys are masked.
+template <int L>
+__device__ __forceinline__ void scan_range(uint32_t (&key)[L], const float4* __restrict__ ext, int s, int e, int tmax,
+                                           uint32_t hi_mask, float xi, float yi, float sy, int cmax) {
+#ifdef FLOCK_PHASE_PROF
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 21], (unsigned long long)((tmax + 1) / 2));
+        atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 22], 1ull);
+    }
+#endif
+#pragma unroll 1
+    for (int t = 0; t < tmax; t += 2) {
+        const int c = s + t;
+        const bool a0 = c < e, a1 = c + 1 < e;
+        const float4* q = ext + min(c, cmax);
+        const float4 q0 = q[0], q1 = q[1];
+        const f32x2 d = pair_d2_shift(xi, yi, sy, q0, q1);
+        const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
+        const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
+        key_insert<L>(key, a0 ? k0 : kEmpty);
+        key_insert<L>(key, a1 ? k1 : kEmpty);
+    }
+}
+
+__device__ __forceinline__ int wrap_row(int yy, int Gc) { return yy < 0 ? yy + Gc : (yy >= Gc ? yy - Gc : yy); }
+
+// Seeded disk scan: every cell that meets the disk of radius r around the lane's agent, row by row (rows cy + q for
+// q in [-kRg, kRg]; in each row the columns under the disk's chord, one contiguous range). The caller guarantees
+// that the disk holds k+1 distinct agents (the lane itself and its previous neighbours) and that r exceeds their
+// largest distance by a factor that moves it >= 16 truncated-d2 buckets up, so every agent outside the disk has a
+// larger key than the (k+1)-th smallest, and every agent sharing that key's bucket is inside: the top k+1 keys
+// (and the ambiguity test of knn_finalize) are exactly the full scan's. Call with every lane of the wave active;
+// lanes with use = false scan nothing.
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void scan_disk(uint32_t (&key)[L], const float4* __restrict__ ext,
+                                          const int* __restrict__ pre, int Gc, int cx, int cy, bool use, float r,
+                                          int ib, float xi, float yi, float box, float cw, float inv_cw, int cmax) {
+    const uint32_t hi_mask = ~((1u << ib) - 1u);
+    const int W2 = Gc + 2 * kRg;
+#pragma unroll
+    for (int s = 0; s < L; ++s) key[s] = kEmpty;
+    int qlo = kRg + 1, qhi = -kRg - 1;
+    if (use) {
+        qlo = max((int)floorf((yi - r) * inv_cw) - cy, -kRg);
+        qhi = min((int)floorf((yi + r) * inv_cw) - cy, kRg);
+        if (!PERIODIC) {
+            qlo = max(qlo, -cy);
+            qhi = min(qhi, Gc - 1 - cy);
+        }
+    }
+    const int wlo = -wave_max(-qlo), whi = wave_max(qhi);
+    const float r2 = r * r;
+#pragma unroll 1
+    for (int q = wlo; q <= whi; ++q) {
+        const int yy = cy + q;
+        int s = 0, e = 0;
+        float sy = 0.0f;
+        if (q >= qlo && q <= qhi) {
+            const float ylo = (float)yy * cw, yhi = (float)(yy + 1) * cw;
+            const float dy = fmaxf(fmaxf(ylo - yi, yi - yhi), 0.0f);
+            if (dy <= r) {
+                // chord half-width, rounded up (the r2 * 1e-6 term dominates the rounding of r2 - dy^2)
+                const float hw = sqrtf(fmaxf(r2 - dy * dy, 0.0f) + r2 * 1e-6f);
+                const int xa = max((int)floorf((xi - hw) * inv_cw), -kRg);
+                const int xb = min((int)floorf((xi + hw) * inv_cw), Gc + kRg - 1);
+                const int yw = PERIODIC ? wrap_row(yy, Gc) : yy;
+                if (PERIODIC && yw != yy) sy = box;
+                const int* pr = pre + yw * W2;
+                s = pr[xa + kRg];
+                e = pr[xb + kRg + 1];
+            }
+        }
+        scan_range<L>(key, ext, s, e, wave_max(e - s), hi_mask, xi, yi, sy, cmax);
+    }
+}
+
+// Square scan with proof (lanes without usable seeds): the (2R+1) x (2R+1) cells around the lane's cell (R <= kRg);
+// returns true when the top-L keys are provably those of the full scan: every agent outside the square lies at
+// least m = the distance to the square's edge away, so if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety
+// factor) exceeds the L-th key, no unscanned key can enter the top L. Call with every lane of the wave active
+// (lanes with live = false scan nothing and return true).
 template <int L, bool PERIODIC>
 __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __restrict__ ext,
                                            const int* __restrict__ pre, int Gc, int cx, int cy, int R, int ib,
-                                           float xi, float yi, float box, float cw, float eps, int ecap,
-                                           bool live) {
+                                           float xi, float yi, float box, float cw, float eps, int cmax, bool live) {
     const uint32_t hi_mask = ~((1u << ib) - 1u);
-    const int W2 = Gc + 4;
-    // pair reads ext[c], ext[c + 1] from one clamped base: ext holds at most N + 4N/Gc <= 1.8N < ecap - 1 = 2N - 1
-    // entries, so a clamped pair is past every range end and both its keys are masked
-    const int cmax = ecap - 2;
+    const int W2 = Gc + 2 * kRg;
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #pragma unroll 1
@@ -255,27 +382,14 @@ __device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __r
         int yr = cy + r;
         bool row = true;
         if (PERIODIC)
-            yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
+            yr = wrap_row(yr, Gc);
         else
             row = yr >= 0 && yr < Gc;
         row = row && live;
         const int* pr = pre + (row ? yr : 0) * W2;
-        const int s0 = row ? pr[cx + 2 - R] : 0, e0 = row ? pr[cx + 3 + R] : 0;
-        // wave-uniform trip count (max range length over the wave) so the loop is a plain counted loop: a
-        // ballot-and-break loop made the compiler copy the whole key list around the back edge every iteration
-        const int tmax = wave_max(e0 - s0);
-#pragma unroll 1
-        for (int t = 0; t < tmax; t += 2) {
-            const int c = s0 + t;
-            const bool a0 = c < e0, a1 = c + 1 < e0;
-            const float4* q = ext + min(c, cmax);
-            const float4 q0 = q[0], q1 = q[1];
-            const f32x2 d = pair_d2x2<PERIODIC>(xi, yi, q0.x, q0.y, q1.x, q1.y, box);
-            const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
-            const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
-            key_insert<L>(key, a0 ? k0 : kEmpty);
-            key_insert<L>(key, a1 ? k1 : kEmpty);
-        }
+        const int s0 = row ? pr[cx + kRg - R] : 0, e0 = row ? pr[cx + kRg + R + 1] : 0;
+        const float sy = (PERIODIC && yr != cy + r) ? box : 0.0f;
+        scan_range<L>(key, ext, s0, e0, wave_max(e0 - s0), hi_mask, xi, yi, sy, cmax);
     }
     // every agent outside the scanned block is at least m away (periodic or not)
     const float lx = (float)(cx - R) * cw, rx = (float)(cx + R + 1) * cw;
@@ -310,7 +424,7 @@ __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)
                                                    const float4* __restrict__ ext, const int* __restrict__ pre,
                                                    int Gc, int cx, int cy, int R, float xi, float yi, float box) {
     constexpr int W = L - 1;
-    const int W2 = Gc + 4;
+    const int W2 = Gc + 2 * kRg;
 #pragma unroll
     for (int s = 0; s < W; ++s) {
         bd[s] = __builtin_inff();
@@ -323,7 +437,7 @@ __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)
         else if (yr < 0 || yr >= Gc)
             continue;
         const int* pr = pre + yr * W2;
-        for (int c = pr[cx + 2 - R]; c < pr[cx + 3 + R]; ++c) {
+        for (int c = pr[cx + kRg - R]; c < pr[cx + kRg + R + 1]; ++c) {
             const float4 q = ext[c];
             insert_exact<W>(bd, bj, pair_d2<PERIODIC>(xi, yi, q.x, q.y, box), __float_as_int(q.z));
         }
@@ -348,7 +462,11 @@ __device__ __forceinline__ bool knn_finalize(const uint32_t (&key)[L], const flo
     const bool ambiguous = (kr != kEmpty) && ((kr & hi_mask) == (kk & hi_mask));
 
     if (!ambiguous) {
-        // exact (d2, j) for the W best keys, then an odd-even transposition sort (only same-bucket keys move)
+        // exact (d2, j) for the W best keys; keys of different truncated buckets are already in exact d2 order, so
+        // the odd-even transposition sort (only same-bucket keys move) runs only when two adjacent keys share one
+        bool same = false;
+#pragma unroll
+        for (int s = 0; s + 1 < W; ++s) same |= (key[s] & hi_mask) == (key[s + 1] & hi_mask);
 #pragma unroll
         for (int s = 0; s < W; ++s) {
             if (key[s] == kEmpty) {
@@ -361,6 +479,7 @@ __device__ __forceinline__ bool knn_finalize(const uint32_t (&key)[L], const flo
                 bj[s] = jj;
             }
         }
+        if (same) {
 #pragma unroll
         for (int pass = 0; pass < W; ++pass) {
 #pragma unroll
@@ -373,6 +492,7 @@ __device__ __forceinline__ bool knn_finalize(const uint32_t (&key)[L], const flo
                 bd[s] = td;
                 bj[s] = tj;
             }
+        }
         }
     } else if (full_rescan) {
         // exact rescan: branch-free ordered insertion of (d2, j); ascending j + strict '<' keeps lower j first
@@ -415,15 +535,16 @@ __device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N,
 // the fused step kernel
 
 template <int L, bool PERIODIC, bool CELL>
-__global__ __launch_bounds__(1024) void step_kernel(const Params p) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float2* lpos = reinterpret_cast<float2*>(smem);               // [G][S]
     float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
-    int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G]
+    int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G] collision flags, [G] arrivals (G = 1)
     // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][Gc*Gc], pre [G][npre]: exclusive prefix over
-    // the "virtual cells" of every row [ghosts of columns Gc-2, Gc-1, columns 0..Gc-1, ghosts of columns 0, 1]
-    const int Gc = p.cells, npre = Gc * (Gc + 4) + 1;
-    float4* ext_all = reinterpret_cast<float4*>(smem + ((((size_t)(flags + p.G) - (size_t)smem) + 15) & ~(size_t)15));
+    // the "virtual cells" of every row [ghosts of columns Gc-kRg..Gc-1, columns 0..Gc-1, ghosts of columns 0..kRg-1]
+    const int Gc = p.cells, W2 = Gc + 2 * kRg, npre = Gc * W2 + 1;
+    float4* ext_all =
+        reinterpret_cast<float4*>(smem + ((((size_t)(flags + 2 * p.G) - (size_t)smem) + 15) & ~(size_t)15));
     int* cnt_all = reinterpret_cast<int*>(ext_all + (CELL ? p.G * p.ecap : 0));
     int* pre_all = cnt_all + (CELL ? p.G * Gc * Gc : 0);
 
@@ -435,7 +556,15 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     const bool active = in_group && env < p.E;
     const size_t a = (size_t)env * p.N + i;
     const int variant = p.variant;
+#ifdef FLOCK_PHASE_PROF
+    unsigned long long ph_acc[24];
+#pragma unroll
+    for (int q_ = 0; q_ < 24; ++q_) ph_acc[q_] = 0;
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+    PHASE_COUNT(20, 1);
+#endif
     if (in_group && i == 0) flags[g] = 0;
+    if (t == 0) flags[p.G] = 0;  // arrival counter of the G = 1 any_done (published by the phase-2 barrier)
     if (CELL && in_group && i < Gc * Gc) cnt_all[g * Gc * Gc + i] = 0;  // published by the phase-2 barrier
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
@@ -448,6 +577,30 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     // row per env holding every agent's fields, group = N)
     const int64_t r_unit = p.r_group == 1 ? (int64_t)a : (int64_t)env;
     const int r_slot = p.r_group == 1 ? 0 : i;
+    // cell path: previous neighbour indices (nn_idx on entry, a search hint only), loaded early
+    int seed[L - 2];
+    bool seeds_ok = CELL && active && p.idx != nullptr;
+#pragma unroll
+    for (int s = 0; s < L - 2; ++s) seed[s] = 0;
+    if (seeds_ok) {
+        const int64_t* hp = p.idx + a * p.k;
+#pragma unroll
+        for (int s = 0; s < L - 2; ++s)
+            if (s < p.k) {
+                const int64_t v = hp[s];
+                seeds_ok = seeds_ok && v >= 0 && v < p.N && v != i;
+                seed[s] = (int)v;
+            }
+#pragma unroll
+        for (int s = 0; s < L - 2; ++s)
+#pragma unroll
+            for (int u = s + 1; u < L - 2; ++u)
+                if (u < p.k) seeds_ok = seeds_ok && seed[s] != seed[u];
+        if (!seeds_ok) {
+#pragma unroll
+            for (int s = 0; s < L - 2; ++s) seed[s] = 0;
+        }
+    }
     if (active && p.r_state && r_unit >= p.r_skip) {
         const float* po = p.r_prev + a * p.k;
 #pragma unroll
@@ -534,6 +687,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         lpos[g * p.S + i] = make_float2(x, y);
     }
 
+    PHASE(0);
     // ---- phase 2: per-env sums in a fixed tree order (same order as oracle tree_sum) -------------------------
     float s0 = 0.0f, s1 = 0.0f;
     if (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_UW_DISCRETE) {
@@ -563,6 +717,7 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         __syncthreads();
     }
 
+    PHASE(1);
     // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
     int cx = 0, cy = 0;
     if (CELL) {
@@ -577,12 +732,12 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         }
         __syncthreads();
         if (in_group && i < 64) {  // one wave per env (groups are wave-aligned whenever CELL): exclusive scan
-            const int W2 = Gc + 4, nv = npre - 1, per = (npre + 63) / 64;
+            const int nv = npre - 1, per = (npre + 63) / 64;
             auto vcount = [&](int f) {
                 const int yy = f / W2, e = f - yy * W2;
-                if (e < 2) return PERIODIC ? cnt[yy * Gc + Gc - 2 + e] : 0;        // ghosts of Gc-2, Gc-1
-                if (e >= Gc + 2) return PERIODIC ? cnt[yy * Gc + e - Gc - 2] : 0;  // ghosts of 0, 1
-                return cnt[yy * Gc + e - 2];
+                if (e < kRg) return PERIODIC ? cnt[yy * Gc + Gc - kRg + e] : 0;          // ghosts of the last columns
+                if (e >= Gc + kRg) return PERIODIC ? cnt[yy * Gc + e - Gc - kRg] : 0;    // ghosts of the first columns
+                return cnt[yy * Gc + e - kRg];
             };
             int local = 0;
             for (int q = 0; q < per; ++q) {
@@ -607,14 +762,16 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
         __syncthreads();
         if (active) {
             const float4 ent = make_float4(x, y, __int_as_float(i), 0.0f);
-            const int* pr = pre + cy * (Gc + 4);
-            ext[pr[cx + 2] + rank] = ent;
-            if (PERIODIC && cx >= Gc - 2) ext[pr[cx - Gc + 2] + rank] = ent;  // ghost in front (Gc >= 5)
-            if (PERIODIC && cx <= 1) ext[pr[Gc + 2 + cx] + rank] = ent;       // ghost behind
+            const float4 ghost = make_float4(x, y, __int_as_float(i), p.box);  // sx = B: see pair_d2_shift
+            const int* pr = pre + cy * W2;
+            ext[pr[cx + kRg] + rank] = ent;
+            if (PERIODIC && cx >= Gc - kRg) ext[pr[cx - Gc + kRg] + rank] = ghost;  // in front (Gc >= 2 kRg)
+            if (PERIODIC && cx < kRg) ext[pr[Gc + kRg + cx] + rank] = ghost;        // behind
         }
         __syncthreads();
     }
 
+    PHASE(2);
     // ---- phase 3/4: kNN -------------------------------------------------------------------------------
     float bd[L - 1];
     int bj[L - 1];
@@ -624,31 +781,69 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
     if (CELL) {  // every lane of the wave (the trip counts are wave-wide maxima); lanes without an agent scan nothing
         const float4* ext = ext_all + g * p.ecap;
         const int* pre = pre_all + g * npre;
-        ok = scan_cells<L, PERIODIC>(key, ext, pre, Gc, cx, cy, 1, p.ib, x, y, p.box, p.cw, p.cell_eps, p.ecap,
-                                     active);
-        R = 1;
-        if (__ballot(!ok) != 0) {  // wave-uniform: lanes whose 3x3 proof failed take the 5x5 result
+        const int cmax = p.ecap - 2;
+        // seeds: the lane itself and its k previous neighbours (nn_idx on entry) are k+1 distinct agents, so their
+        // largest distance bounds the (k+1)-th nearest; r adds 2^(ib-20) relative (>= 16 truncated-d2 buckets) and
+        // a 1e-5 box margin. Seeds that are out of range or repeated (a stale or uninitialised buffer) fall back.
+        bool use = false;
+        float r = 0.0f;
+        if (active && seeds_ok) {
+            const float2* cand = lpos + g * p.S;
+            float rho2 = 0.0f;
+#pragma unroll
+            for (int s = 0; s < L - 2; ++s)
+                if (s < p.k) {
+                    const float2 c = cand[seed[s]];
+                    rho2 = fmaxf(rho2, pair_d2<PERIODIC>(x, y, c.x, c.y, p.box));
+                }
+            r = sqrtf(rho2) * (1.0f + __int_as_float((127 + p.ib - 20) << 23)) + p.cell_eps;
+            use = r <= ((float)kRg - 0.5f) * p.cw;  // the disk stays within kRg cells (see pair_d2_shift)
+        }
+#ifdef FLOCK_DIAG_NOSCAN  // diagnostics only: cost of everything but the cell scans (results are wrong)
+        use = false;
+#pragma unroll
+        for (int s = 0; s < L; ++s) key[s] = kEmpty;
+#else
+        scan_disk<L, PERIODIC>(key, ext, pre, Gc, cx, cy, use, r, p.ib, x, y, p.box, p.cw, p.inv_cw, cmax);
+#endif
+        ok = use;
+        R = kRg;
+        PHASE(3);
+#ifdef FLOCK_DIAG_NOSCAN
+        ok = true;
+        if (false) {
+#else
+        if (__ballot(active && !use) != 0) {  // wave-uniform: lanes without a usable disk take the proved square
+#endif
+            PHASE_COUNT(16, 1);
             uint32_t key2[L];
-            const bool ok2 = scan_cells<L, PERIODIC>(key2, ext, pre, Gc, cx, cy, 2, p.ib, x, y, p.box, p.cw,
-                                                     p.cell_eps, p.ecap, active);
-            if (!ok) {
+            const bool ok2 = scan_cells<L, PERIODIC>(key2, ext, pre, Gc, cx, cy, kRg, p.ib, x, y, p.box, p.cw,
+                                                     p.cell_eps, cmax, active && !use);
+            if (!use) {
 #pragma unroll
                 for (int s = 0; s < L; ++s) key[s] = key2[s];
                 ok = ok2;
-                R = 2;
             }
         }
+        PHASE(4);
     }
+#ifdef FLOCK_PHASE_PROF
+    if (__ballot(active && !ok) != 0) PHASE_COUNT(17, 1);
+#endif
     if (active) {
         if (!ok) {
             scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
             R = 0;
         }
         const bool amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj, R == 0);
+#ifdef FLOCK_PHASE_PROF
+        if (__ballot(amb) != 0) PHASE_COUNT(18, 1);
+#endif
         if (CELL && amb)
             exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, Gc, cx, cy, R, x, y,
                                             p.box);
     }
+    PHASE(5);
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
     int coll = 0;
@@ -713,11 +908,29 @@ __global__ __launch_bounds__(1024) void step_kernel(const Params p) {
             }
         }
     }
-    if (variant != kSense) {
-        if (active && coll) atomicOr(&flags[g], 1);
-        __syncthreads();
-        if (active && i == 0) p.any_done[env] = (uint8_t)flags[g];  // _computeDone :306-315
+    PHASE(6);
+    if (variant != kSense) {  // _computeDone :306-315
+        if (p.G == 1) {
+            // one env per block: no trailing barrier. Each wave ORs its collisions into flags[0] and then adds its
+            // agent count to the arrival counter (release); the wave that completes the count (acquire) has seen
+            // every OR and publishes any_done
+            const bool coll_w = __ballot(active && coll) != 0;
+            const int na = __popcll(__ballot(active));
+            if ((t & 63) == 0 && na) {
+                if (coll_w) __hip_atomic_fetch_or(&flags[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int old = __hip_atomic_fetch_add(&flags[1], na, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old + na == p.N)
+                    p.any_done[env] =
+                        (uint8_t)__hip_atomic_load(&flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {
+            if (active && coll) atomicOr(&flags[g], 1);
+            __syncthreads();
+            if (active && i == 0) p.any_done[env] = (uint8_t)flags[g];
+        }
     }
+    PHASE(7);
+    PHASE_FLUSH();
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -818,12 +1031,12 @@ struct Cfg {
     size_t lds;
 };
 
-// cell grid side for the step kernel's cell list (0 = full scan): ~4 agents per cell, >= 5 cells per side
+// cell grid side for the step kernel's cell list (0 = full scan): ~1 agent per cell, >= 11 cells per side
 int cell_grid(int N, int variant) {
     if (variant == kSense || N < 128) return 0;
     int gc = 1;
-    while ((gc + 1) * (gc + 1) * 4 <= N) ++gc;
-    return gc >= 5 ? gc : 0;
+    while ((gc + 1) * (gc + 1) <= N) ++gc;  // about one agent per cell
+    return gc >= 11 ? gc : 0;               // pair_d2_shift needs Gc >= 11 (kRg = 3)
 }
 
 Cfg make_cfg(int E, int N, bool reset, int cells) {
@@ -836,10 +1049,10 @@ Cfg make_cfg(int E, int N, bool reset, int cells) {
     if (reset)
         c.lds = (size_t)c.G * c.S * sizeof(float2) + 2 * c.G * sizeof(int);
     else
-        c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + c.G * sizeof(int);
-    if (!reset && cells) {  // ext (2N float4, 16-B aligned) + cnt + pre + rowlen per env
+        c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + 2 * c.G * sizeof(int);
+    if (!reset && cells) {  // ext (2N + 2 float4, 16-B aligned) + cnt + pre per env
         c.lds = (c.lds + 15) & ~(size_t)15;
-        c.lds += (size_t)c.G * (2 * N * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 4) + 1) * 4);
+        c.lds += (size_t)c.G * ((2 * N + 2) * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 2 * kRg) + 1) * 4);
     }
     return c;
 }
@@ -876,7 +1089,7 @@ int dispatch(Params& p, hipStream_t s, bool reset) {
     if (p.E == 0) return FLOCK_OK;
     p.cells = (reset || getenv("FLOCK_NO_CELLS")) ? 0 : cell_grid(p.N, p.variant);
     if (p.cells) {
-        p.ecap = 2 * p.N;
+        p.ecap = 2 * p.N + 2;
         p.cw = p.box / (float)p.cells;
         p.inv_cw = (float)p.cells / p.box;
         p.cell_eps = p.box * 1e-5f;
@@ -936,6 +1149,20 @@ Params base(int E, int N, int k, float box) {
 extern "C" {
 
 int flock_abi_version(void) { return FLOCK_ABI_VERSION; }
+
+#ifdef FLOCK_PHASE_PROF
+// diagnostics build only: copy out and clear the phase counters (32 x u64)
+int flock_phase_read(unsigned long long* host) {
+    static unsigned long long buf[64 * 32];
+    if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_phase), sizeof(buf)) != hipSuccess) return 1;
+    for (int q = 0; q < 32; ++q) {
+        host[q] = 0;
+        for (int s = 0; s < 64; ++s) host[q] += buf[s * 32 + q];
+    }
+    memset(buf, 0, sizeof(buf));
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), buf, sizeof(buf)) != hipSuccess;
+}
+#endif
 
 const char* flock_last_error(void) { return g_err; }
 

@@ -1,0 +1,96 @@
+"""Per-phase cycle breakdown of the env step kernel (diagnostics, not the product).
+
+    python tools/phase_prof.py --build            # here (CPU): hipcc flock_env.hip -DFLOCK_PHASE_PROF
+    python tools/phase_prof.py [--E 4096 --N 256]  # GPU box: run steps, print mean cycles per wave per phase
+
+Every wave's lane 0 adds s_memtime deltas between phase marks of step_kernel into device counters (see the
+PHASE() marks in flock_env.hip); counts: waves taking the 5x5 scan, the full scan, an ambiguous-bucket rescan.
+"""
+import argparse
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+SO = os.path.join(ROOT, "marl_range_flocking_amd", "_build", "libflock_env_prof.so")
+NAMES = ["kinematics", "phase2 barrier", "cell binning", "3x3 scan", "5x5 scan", "finalize/fallback",
+         "outputs", "any_done barrier"]
+
+
+def build():
+    from marl_range_flocking_amd.build import HIPCC_FLAGS, INCLUDE, CSRC, hipcc
+
+    os.makedirs(os.path.dirname(SO), exist_ok=True)
+    cmd = [hipcc()] + HIPCC_FLAGS + ["-DFLOCK_PHASE_PROF", "-shared", "-I", INCLUDE, "-o", SO,
+                                     os.path.join(CSRC, "flock_env.hip")]
+    print(" ".join(cmd))
+    subprocess.check_call(cmd)
+
+
+def run(E, N, k, steps):
+    import numpy as np
+    import torch
+
+    lib = ctypes.CDLL(SO)
+    lib.flock_phase_read.argtypes = [ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    box = float(round(np.sqrt(250.0 * N)))
+    g = torch.Generator(device=dev).manual_seed(0)
+    pos = torch.rand(E, N, 2, device=dev, generator=g) * box
+    head = torch.rand(E, N, device=dev, generator=g) * 4.71
+    act = torch.stack([torch.rand(E, N, device=dev, generator=g),
+                       torch.rand(E, N, device=dev, generator=g) * 3 - 1.5], -1).contiguous()
+    vel = torch.empty(E, N, 2, device=dev)
+    dnn = torch.empty(E, N, k, device=dev)
+    idx = torch.empty(E, N, k, dtype=torch.int64, device=dev)
+    rew = torch.empty(E, N, device=dev)
+    done = torch.empty(E, N, dtype=torch.uint8, device=dev)
+    anyd = torch.empty(E, dtype=torch.uint8, device=dev)
+    f = lib.flock_step_v2
+    f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 6 + [ctypes.c_int] * 2 + \
+        [ctypes.c_void_p] * 9
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        rc = f(stream, E, N, k, box, 14.0, 2.5, 0.1, 0.0, 2.5, 1, 0, pos.data_ptr(), head.data_ptr(),
+               act.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(), rew.data_ptr(), done.data_ptr(),
+               anyd.data_ptr())
+        assert rc == 0, rc
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 32)()
+    lib.flock_phase_read(buf)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    lib.flock_phase_read(buf)
+    waves = buf[20]
+    tot = sum(buf[i] for i in range(8))
+    print(f"E={E} N={N} k={k}: kernel {e0.elapsed_time(e1) / steps * 1e3:.1f} us/launch, waves/launch "
+          f"{waves / steps:.0f}")
+    for i, n in enumerate(NAMES):
+        print(f"  {n:20s} {buf[i] / waves:9.0f} cycles/wave  {100.0 * buf[i] / tot:5.1f} %")
+    print(f"  waves taking 5x5: {buf[16] / waves:.4f}, full scan: {buf[17] / waves:.5f}, "
+          f"ambiguous rescan: {buf[18] / waves:.5f}")
+    print(f"  cell-scan pair iterations per wave: {buf[21] / waves:.1f} over {buf[22] / waves:.2f} row ranges")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--E", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=256)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    if a.build:
+        build()
+    else:
+        run(a.E, a.N, a.k, a.steps)
