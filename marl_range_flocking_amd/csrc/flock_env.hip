@@ -12,17 +12,24 @@
 //            and keeps the L = k+2 smallest keys in registers with a branch-free insertion network
 //            (1 v_min_u32 + (L-1) v_med3_u32 per candidate; no divergence, no sort)
 //            Step variants with N >= 128 scan a CELL LIST instead of all N (phase 3c below).
-//   phase 3c agents are binned into a Gc x Gc grid over [0, box]^2 (Gc = floor(sqrt(N / 4))) by an LDS counting
-//            sort into an extended cell-sorted array of (x, y, j) in which every cell row also carries ghost copies
-//            of its last two columns (in front) and first two columns (behind) when the box is periodic, so each
-//            agent's 3x3 (or 5x5) neighbourhood is exactly 3 (5) contiguous ranges, one per row. The lane runs the
-//            same insertion network over its 3x3 cells (~36 candidates at 4 per cell instead of N) and keeps the
-//            result only if it is PROVABLY the full scan's: every unscanned agent lies at least m = the distance to
-//            the neighbourhood's edge away, so if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety factor)
-//            exceeds the L-th key, no unscanned key can enter the top L. Lanes whose proof fails take the 5x5 result
-//            (same proof, m >= 2 cells), and only then the full scan. An ambiguous bucket (phase 4) is rescanned
-//            exactly over the same neighbourhood, which the proof shows to contain every candidate of that bucket.
-//            Keys carry j, so the order of agents within a cell (LDS atomics) never matters.
+//   phase 3c agents are binned into a Gx x Gy grid (about one agent per cell, rows about twice the typical
+//            (k+1)-th neighbour distance tall) by an LDS counting sort (block-wide DPP prefix scan) into an extended
+//            cell-sorted array of (x, y, j, sx) in which every cell row also carries ghost copies of its last and first
+//            kRg columns when the box is periodic, so any run of up to 2 kRg + 1 columns of a row is one contiguous
+//            range. SEEDED scan (the usual case): nn_idx holds the previous step's neighbours on entry; the lane's
+//            own agent and those k seeds are k+1 distinct agents, so their largest current distance bounds the
+//            (k+1)-th nearest, and every agent inside the disk of that radius (widened by >= 16 truncated-d2
+//            buckets) is scanned: the cells under the disk, at most kRows rows, each row's chord one range, all
+//            rows streamed as ONE sequence per lane (the wave loops max-over-lanes(total) slots, not a per-row
+//            maximum per row). Every agent outside the disk has a larger key than the (k+1)-th smallest, so the
+//            top k+1 keys and the ambiguity test of phase 4 are exactly the full scan's. Lanes without usable
+//            seeds (first step, stale or invalid indices, too large a radius) take a SQUARE scan (rows cy +- 1,
+//            columns cx +- kRg) kept only if PROVABLY the full scan's: every unscanned agent lies at least m = the
+//            distance to the block's edge away (no agents beyond a box edge without wrap), so if the truncated-d2
+//            bucket of m^2 (shrunk by a 1e-5 safety factor) exceeds the L-th key, no unscanned key can enter the top
+//            L; only then the full scan. An ambiguous bucket (phase 4) is rescanned exactly over the square, which
+//            contains every candidate of that bucket in both cases. Keys carry j, so the order of agents within a
+//            cell (LDS atomics) never matters.
 //   phase 4  exactness: the k+1 winners are re-sorted by their exact (d2, j); if the (k+2)-th key shares the
 //            truncated-d2 bucket of the (k+1)-th, the lane falls back to an exact (d2, j) rescan (rare). The
 //            result is the ascending (d2, j) order — a valid tie resolution of the reference's
@@ -31,7 +38,7 @@
 //            (LDS atomic OR), reward, observation memory roll.
 //
 // Float arithmetic: every op is rounded separately (__fmul_rn / __fadd_rn / __fdiv_rn / sqrt_rn, and the file
-// is built with -ffp-contract=off), in the reference's op order; cosf/sinf are ocml's.
+// is built with -ffp-contract=off), in the reference's op order; cosf/sinf are ocml's (sincosf: the same bits).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -85,8 +92,8 @@ struct Params {
     int64_t r_cap, r_start, r_skip;
     int r_group, r_done;  // agents per ring row (1 or N); stored flag: 0 -> 1 - done, 1 -> done
     // cell list (step variants, N >= 128)
-    int cells, ecap;  // grid side Gc, extended-array capacity per env (2N)
-    float cw, inv_cw, cell_eps;
+    int cells, gx, gy, ecap;  // cells != 0: cell list on a gx x gy grid; extended-array capacity per env (2N + 2)
+    float cwx, cwy, inv_cwx, inv_cwy, cell_eps, r_lim;
     // reset
     float range_lo, range_hi, head_hi, check_distance;
     int max_attempts;
@@ -192,6 +199,18 @@ __device__ __forceinline__ int wave_max(int v) {
                                               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48))));
 }
 
+// inclusive prefix sum over the 64 lanes (every lane active): DPP row_shr 1/2/4/8 within rows of 16, then
+// row_bcast 15 / 31 across rows (lanes without a source read the 0 of `old`)
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+
 // pair_d2 of two candidates at once: the squares and sums as packed f32 ops (v_pk_mul / v_pk_add, one candidate
 // per half; each half rounds exactly like the scalar mul, mul, add), so both packed issue slots do useful work.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -268,134 +287,156 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
     }
 }
 
-// Cell-list scans (step variants, N >= 128). The env's agents are binned into a Gc x Gc grid (Gc = floor(sqrt N),
-// about one agent per cell) and stored cell-sorted in an extended array ext of (x, y, j, sx) in which every cell
-// row also carries ghost copies of its last kRg columns (in front) and first kRg columns (behind) when the box is
-// periodic, so any run of up to 2*kRg+1 columns of a row is ONE contiguous range. sx = box for a ghost copy, else 0.
-constexpr int kRg = 3;
+// Cell-list scans (step variants, N >= 128). The env's agents are binned into a Gx x Gy grid of cells about as
+// tall as twice the typical (k+1)-th neighbour distance and about one agent per cell (Gy = max(kRows, 0.38 sqrt N),
+// Gx = max(2 kRg + 4, N / Gy)), and stored cell-sorted, row by row, in an extended array ext of (x, y, j, sx): every
+// cell row also carries ghost copies of its last kRg columns (in front) and its first kRg columns (behind) when the
+// box is periodic, so any run of up to 2 kRg + 1 columns of a row is ONE contiguous range. sx = box for a ghost
+// copy, else 0.
+constexpr int kRg = 8;    // ghost columns per side of a row
+constexpr int kRows = 3;  // rows of a seeded scan (its radius is at most one row height)
 
-// d2 of two candidates of one row range, bit-identical to the reference's periodic/Euclidean d2 in op order: with
-// Gc >= 11 and at most kRg(+1) cells between the lane's cell and a scanned cell, a regular entry has |d| < B/2 (the
-// reference keeps |d|, and (0 - |d|)^2 == d^2 bit for bit) and a ghost entry (sx = B) or a wrapped row (sy = B) has
-// |d| > B/2 (the reference takes B - |d|). So min(|d|, B - |d|) becomes one subtraction with an |.| modifier.
-__device__ __forceinline__ f32x2 pair_d2_shift(float xi, float yi, float sy, const float4& q0, const float4& q1) {
+// d2 of two candidates, bit-identical to the reference's periodic / Euclidean d2 in op order (gym_flock_v2.py:140-144,
+// :160-165). x: with Gx >= 2 kRg + 4 and every scanned cell at most kRg(+1) columns from the lane's cell, a regular
+// entry has |dx| < B/2 (the reference keeps |dx|, and (0 - |dx|)^2 == dx^2 bit for bit) and a ghost entry (sx = B)
+// has |dx| > B/2 (the reference takes B - |dx|), so min(|dx|, B - |dx|) is one subtraction with an |.| modifier.
+// y: the reference formula (rows wrap by index).
+template <bool PERIODIC>
+__device__ __forceinline__ f32x2 cand_d2x2(float xi, float yi, float box, const float4& q0, const float4& q1) {
     const float dx0 = __fsub_rn(q0.w, fabsf(__fsub_rn(xi, q0.x))), dx1 = __fsub_rn(q1.w, fabsf(__fsub_rn(xi, q1.x)));
-    const float dy0 = __fsub_rn(sy, fabsf(__fsub_rn(yi, q0.y))), dy1 = __fsub_rn(sy, fabsf(__fsub_rn(yi, q1.y)));
+    float dy0 = __fsub_rn(yi, q0.y), dy1 = __fsub_rn(yi, q1.y);
+    if (PERIODIC) {
+        const float a0 = fabsf(dy0), a1 = fabsf(dy1);
+        dy0 = fminf(a0, __fsub_rn(box, a0));
+        dy1 = fminf(a1, __fsub_rn(box, a1));
+    }
     const f32x2 dx = {dx0, dx1}, dy = {dy0, dy1};
     return dx * dx + dy * dy;
 }
 
-// one row range [s, e) of ext into the insertion network; tmax = the wave-wide maximum of e - s (a plain counted
-// loop: every lane of the wave runs it, lanes with an empty range insert nothing). Pairs are read from one
-// clamped base: ext holds at most 2N entries (an agent has at most one ghost copy, Gc >= 2 kRg) and
-// ecap = 2N + 2, so a clamped pair lies past every range end and both its keys are masked.
-template <int L>
-__device__ __forceinline__ void scan_range(uint32_t (&key)[L], const float4* __restrict__ ext, int s, int e, int tmax,
-                                           uint32_t hi_mask, float xi, float yi, float sy, int cmax) {
+__device__ __forceinline__ int wrap_row(int yy, int G) { return yy < 0 ? yy + G : (yy >= G ? yy - G : yy); }
+
+// Seeded scan, flattened. The caller guarantees that the disk of radius r around the lane's agent holds k+1
+// distinct agents (the lane itself and its previous neighbours) and that r exceeds their largest distance by a factor
+// that moves it >= 16 truncated-d2 buckets up, so every agent outside the disk has a larger key than the (k+1)-th
+// smallest and every agent sharing that key's bucket is inside: the top k+1 keys (and the ambiguity test of
+// knn_finalize) are exactly the full scan's. The lane's candidates are the cells under the disk, row by row (at most
+// kRows rows, r <= one row height; per row the columns under the disk's chord, one contiguous range of ext), taken
+// as ONE sequence: candidate t of the lane is ext[t + b_q] for the row q with P_q <= t < P_{q+1} (P = running row
+// totals). The wave runs max-over-lanes(total) slots, two per iteration, with the slot index t wave-uniform.
+// Call with every lane of the wave active; lanes with use = false scan nothing.
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __restrict__ ext,
+                                            const int* __restrict__ pre, int gx, int gy, int cy, bool use, float r,
+                                            int ib, float xi, float yi, float box, float cwy, float inv_cwx,
+                                            float inv_cwy, int cmax) {
+    const uint32_t hi_mask = ~((1u << ib) - 1u);
+    const int W2 = gx + 2 * kRg;
+#pragma unroll
+    for (int s = 0; s < L; ++s) key[s] = kEmpty;
+    int b[kRows], P[kRows];  // P[u]: candidates before row slot u; b[u]: ext index of candidate t in slot u minus t
+    int tot = 0;
+    int qlo = 1, qhi = 0;
+    if (use) {
+        qlo = (int)floorf((yi - r) * inv_cwy) - cy;
+        qhi = (int)floorf((yi + r) * inv_cwy) - cy;
+        if (!PERIODIC) {
+            qlo = max(qlo, -cy);
+            qhi = min(qhi, gy - 1 - cy);
+        }
+    }
+    const float r2 = r * r;
+#pragma unroll
+    for (int u = 0; u < kRows; ++u) {
+        const int q = qlo + u;
+        P[u] = tot;
+        b[u] = 0;
+        if (q <= qhi) {
+            const int yy = cy + q;
+            const float ylo = (float)yy * cwy;
+            const float dy = fmaxf(fmaxf(ylo - yi, yi - (ylo + cwy)), 0.0f);
+            if (dy <= r) {
+                // chord half-width, rounded up (raw v_sqrt_f32 is within 1 ulp; the r * 2^-10 term covers the
+                // rounding of r2 - dy^2 near a grazing row and of the cell assignment)
+                const float hw = __builtin_amdgcn_sqrtf(fmaxf(r2 - dy * dy, 0.0f)) * 1.000001f + r * 0.0009765625f;
+                const int xa = max((int)floorf((xi - hw) * inv_cwx), -kRg);
+                const int xb = min((int)floorf((xi + hw) * inv_cwx), gx + kRg - 1);
+                const int* pr = pre + (PERIODIC ? wrap_row(yy, gy) : yy) * W2;
+                const int s0 = pr[xa + kRg], e0 = pr[xb + kRg + 1];
+                b[u] = s0 - tot;
+                tot += e0 - s0;
+            }
+        }
+    }
+    const int slots = wave_max(tot);
 #ifdef FLOCK_PHASE_PROF
     if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 21], (unsigned long long)((tmax + 1) / 2));
+        atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 21], (unsigned long long)((slots + 1) / 2));
         atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 22], 1ull);
     }
 #endif
 #pragma unroll 1
-    for (int t = 0; t < tmax; t += 2) {
-        const int c = s + t;
-        const bool a0 = c < e, a1 = c + 1 < e;
-        const float4* q = ext + min(c, cmax);
-        const float4 q0 = q[0], q1 = q[1];
-        const f32x2 d = pair_d2_shift(xi, yi, sy, q0, q1);
+    for (int t = 0; t < slots; t += 2) {
+        int c0 = t + b[0], c1 = t + 1 + b[0];
+#pragma unroll
+        for (int u = 1; u < kRows; ++u) {
+            c0 = (t >= P[u]) ? t + b[u] : c0;
+            c1 = (t + 1 >= P[u]) ? t + 1 + b[u] : c1;
+        }
+        const float4 q0 = ext[min(c0, cmax)], q1 = ext[min(c1, cmax)];
+        const f32x2 d = cand_d2x2<PERIODIC>(xi, yi, box, q0, q1);
         const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
         const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
-        key_insert<L>(key, a0 ? k0 : kEmpty);
-        key_insert<L>(key, a1 ? k1 : kEmpty);
+        key_insert<L>(key, t < tot ? k0 : kEmpty);
+        key_insert<L>(key, t + 1 < tot ? k1 : kEmpty);
     }
 }
 
-__device__ __forceinline__ int wrap_row(int yy, int Gc) { return yy < 0 ? yy + Gc : (yy >= Gc ? yy - Gc : yy); }
-
-// Seeded disk scan: every cell that meets the disk of radius r around the lane's agent, row by row (rows cy + q for
-// q in [-kRg, kRg]; in each row the columns under the disk's chord, one contiguous range). The caller guarantees
-// that the disk holds k+1 distinct agents (the lane itself and its previous neighbours) and that r exceeds their
-// largest distance by a factor that moves it >= 16 truncated-d2 buckets up, so every agent outside the disk has a
-// larger key than the (k+1)-th smallest, and every agent sharing that key's bucket is inside: the top k+1 keys
-// (and the ambiguity test of knn_finalize) are exactly the full scan's. Call with every lane of the wave active;
-// lanes with use = false scan nothing.
+// Square scan with proof (lanes without usable seeds): rows cy-Ry..cy+Ry, columns cx-kRg..cx+kRg, one row range at
+// a time (tmax = the wave-wide maximum of the row's range lengths); returns true when the top-L keys are provably
+// those of the full scan: every agent outside the block lies at least m = the distance to the block's edge away, so
+// if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety factor) exceeds the L-th key, no unscanned key can enter
+// the top L. Call with every lane of the wave active (lanes with live = false scan nothing and return true).
 template <int L, bool PERIODIC>
-__device__ __forceinline__ void scan_disk(uint32_t (&key)[L], const float4* __restrict__ ext,
-                                          const int* __restrict__ pre, int Gc, int cx, int cy, bool use, float r,
-                                          int ib, float xi, float yi, float box, float cw, float inv_cw, int cmax) {
+__device__ __forceinline__ bool scan_square(uint32_t (&key)[L], const float4* __restrict__ ext,
+                                            const int* __restrict__ pre, int gx, int gy, int cx, int cy, int Ry,
+                                            int ib, float xi, float yi, float box, float cwx, float cwy, float eps,
+                                            int cmax, bool live) {
     const uint32_t hi_mask = ~((1u << ib) - 1u);
-    const int W2 = Gc + 2 * kRg;
-#pragma unroll
-    for (int s = 0; s < L; ++s) key[s] = kEmpty;
-    int qlo = kRg + 1, qhi = -kRg - 1;
-    if (use) {
-        qlo = max((int)floorf((yi - r) * inv_cw) - cy, -kRg);
-        qhi = min((int)floorf((yi + r) * inv_cw) - cy, kRg);
-        if (!PERIODIC) {
-            qlo = max(qlo, -cy);
-            qhi = min(qhi, Gc - 1 - cy);
-        }
-    }
-    const int wlo = -wave_max(-qlo), whi = wave_max(qhi);
-    const float r2 = r * r;
-#pragma unroll 1
-    for (int q = wlo; q <= whi; ++q) {
-        const int yy = cy + q;
-        int s = 0, e = 0;
-        float sy = 0.0f;
-        if (q >= qlo && q <= qhi) {
-            const float ylo = (float)yy * cw, yhi = (float)(yy + 1) * cw;
-            const float dy = fmaxf(fmaxf(ylo - yi, yi - yhi), 0.0f);
-            if (dy <= r) {
-                // chord half-width, rounded up (the r2 * 1e-6 term dominates the rounding of r2 - dy^2)
-                const float hw = sqrtf(fmaxf(r2 - dy * dy, 0.0f) + r2 * 1e-6f);
-                const int xa = max((int)floorf((xi - hw) * inv_cw), -kRg);
-                const int xb = min((int)floorf((xi + hw) * inv_cw), Gc + kRg - 1);
-                const int yw = PERIODIC ? wrap_row(yy, Gc) : yy;
-                if (PERIODIC && yw != yy) sy = box;
-                const int* pr = pre + yw * W2;
-                s = pr[xa + kRg];
-                e = pr[xb + kRg + 1];
-            }
-        }
-        scan_range<L>(key, ext, s, e, wave_max(e - s), hi_mask, xi, yi, sy, cmax);
-    }
-}
-
-// Square scan with proof (lanes without usable seeds): the (2R+1) x (2R+1) cells around the lane's cell (R <= kRg);
-// returns true when the top-L keys are provably those of the full scan: every agent outside the square lies at
-// least m = the distance to the square's edge away, so if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety
-// factor) exceeds the L-th key, no unscanned key can enter the top L. Call with every lane of the wave active
-// (lanes with live = false scan nothing and return true).
-template <int L, bool PERIODIC>
-__device__ __forceinline__ bool scan_cells(uint32_t (&key)[L], const float4* __restrict__ ext,
-                                           const int* __restrict__ pre, int Gc, int cx, int cy, int R, int ib,
-                                           float xi, float yi, float box, float cw, float eps, int cmax, bool live) {
-    const uint32_t hi_mask = ~((1u << ib) - 1u);
-    const int W2 = Gc + 2 * kRg;
+    const int W2 = gx + 2 * kRg;
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #pragma unroll 1
-    for (int r = -R; r <= R; ++r) {
-        int yr = cy + r;
-        bool row = true;
+    for (int rr = -Ry; rr <= Ry; ++rr) {
+        int yr = cy + rr;
+        bool row = live;
         if (PERIODIC)
-            yr = wrap_row(yr, Gc);
+            yr = wrap_row(yr, gy);
         else
-            row = yr >= 0 && yr < Gc;
-        row = row && live;
+            row = row && yr >= 0 && yr < gy;
         const int* pr = pre + (row ? yr : 0) * W2;
-        const int s0 = row ? pr[cx + kRg - R] : 0, e0 = row ? pr[cx + kRg + R + 1] : 0;
-        const float sy = (PERIODIC && yr != cy + r) ? box : 0.0f;
-        scan_range<L>(key, ext, s0, e0, wave_max(e0 - s0), hi_mask, xi, yi, sy, cmax);
+        const int s0 = row ? pr[cx] : 0, e0 = row ? pr[cx + 2 * kRg + 1] : 0;
+        const int tmax = wave_max(e0 - s0);
+#pragma unroll 1
+        for (int t = 0; t < tmax; t += 2) {
+            const int c = s0 + t;
+            const float4 q0 = ext[min(c, cmax)], q1 = ext[min(c + 1, cmax)];
+            const f32x2 d = cand_d2x2<PERIODIC>(xi, yi, box, q0, q1);
+            const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
+            const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
+            key_insert<L>(key, c < e0 ? k0 : kEmpty);
+            key_insert<L>(key, c + 1 < e0 ? k1 : kEmpty);
+        }
     }
-    // every agent outside the scanned block is at least m away (periodic or not)
-    const float lx = (float)(cx - R) * cw, rx = (float)(cx + R + 1) * cw;
-    const float ly = (float)(cy - R) * cw, ry = (float)(cy + R + 1) * cw;
-    const float m = fminf(fminf(xi - lx, rx - xi), fminf(yi - ly, ry - yi)) - eps;
-    const float bound = m > 0.0f ? (m * m) * 0.99998f : 0.0f;
+    // every agent outside the scanned block is at least m away; without wrap, a side of the block that reaches the
+    // box edge has no agents beyond it
+    const float inf = __builtin_inff();
+    const float lx = (float)(cx - kRg) * cwx, rx = (float)(cx + kRg + 1) * cwx;
+    const float ly = (float)(cy - Ry) * cwy, ry = (float)(cy + Ry + 1) * cwy;
+    const float ml = (!PERIODIC && cx - kRg <= 0) ? inf : xi - lx, mr = (!PERIODIC && cx + kRg >= gx - 1) ? inf : rx - xi;
+    const float mb = (!PERIODIC && cy - Ry <= 0) ? inf : yi - ly, mt = (!PERIODIC && cy + Ry >= gy - 1) ? inf : ry - yi;
+    const float m = fminf(fminf(ml, mr), fminf(mb, mt)) - eps;
+    const float bound = m > 0.0f ? fminf((m * m) * 0.99998f, 3.0e38f) : 0.0f;
     return !live || (__float_as_uint(bound) & hi_mask) > key[L - 1];
 }
 
@@ -416,28 +457,29 @@ __device__ __forceinline__ void insert_exact(float (&bd)[W], int (&bj)[W], float
     }
 }
 
-// exact rescan of an ambiguous bucket over the scanned neighbourhood only: when scan_cells proved its top L, every
-// unscanned key exceeds the L-th key, so every unscanned d2 exceeds every d2 of the ambiguous bucket and the exact
-// top k+1 by (d2, j) lies in the scanned ranges (per-lane loops: no wave-wide operations)
+// exact rescan of an ambiguous bucket over the scanned neighbourhood only (rows cy-Ry..cy+Ry, columns cx-kRg..cx+kRg,
+// which contains a seeded lane's disk and a square lane's proved block): every unscanned d2 exceeds every d2 of the
+// ambiguous bucket, so the exact top k+1 by (d2, j) lies in the scanned ranges (per-lane loops: no wave-wide ops)
 template <int L, bool PERIODIC>
 __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)[L - 1],
                                                    const float4* __restrict__ ext, const int* __restrict__ pre,
-                                                   int Gc, int cx, int cy, int R, float xi, float yi, float box) {
+                                                   int gx, int gy, int cx, int cy, int Ry, float xi, float yi,
+                                                   float box) {
     constexpr int W = L - 1;
-    const int W2 = Gc + 2 * kRg;
+    const int W2 = gx + 2 * kRg;
 #pragma unroll
     for (int s = 0; s < W; ++s) {
         bd[s] = __builtin_inff();
         bj[s] = 0x7fffffff;
     }
-    for (int r = -R; r <= R; ++r) {
+    for (int r = -Ry; r <= Ry; ++r) {
         int yr = cy + r;
         if (PERIODIC)
-            yr = yr < 0 ? yr + Gc : (yr >= Gc ? yr - Gc : yr);
-        else if (yr < 0 || yr >= Gc)
+            yr = wrap_row(yr, gy);
+        else if (yr < 0 || yr >= gy)
             continue;
         const int* pr = pre + yr * W2;
-        for (int c = pr[cx + kRg - R]; c < pr[cx + kRg + R + 1]; ++c) {
+        for (int c = pr[cx]; c < pr[cx + 2 * kRg + 1]; ++c) {
             const float4 q = ext[c];
             insert_exact<W>(bd, bj, pair_d2<PERIODIC>(xi, yi, q.x, q.y, box), __float_as_int(q.z));
         }
@@ -540,13 +582,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     float2* lpos = reinterpret_cast<float2*>(smem);               // [G][S]
     float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
     int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G] collision flags, [G] arrivals (G = 1)
-    // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][Gc*Gc], pre [G][npre]: exclusive prefix over
-    // the "virtual cells" of every row [ghosts of columns Gc-kRg..Gc-1, columns 0..Gc-1, ghosts of columns 0..kRg-1]
-    const int Gc = p.cells, W2 = Gc + 2 * kRg, npre = Gc * W2 + 1;
+    // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][gx*gy], pre [G][npre]: exclusive prefix over
+    // the "virtual cells" of every row [ghosts of columns gx-kRg..gx-1, columns 0..gx-1, ghosts of columns 0..kRg-1]
+    const int gx = p.gx, gy = p.gy, ncell = gx * gy, W2 = gx + 2 * kRg, npre = gy * W2 + 1;
     float4* ext_all =
         reinterpret_cast<float4*>(smem + ((((size_t)(flags + 2 * p.G) - (size_t)smem) + 15) & ~(size_t)15));
     int* cnt_all = reinterpret_cast<int*>(ext_all + (CELL ? p.G * p.ecap : 0));
-    int* pre_all = cnt_all + (CELL ? p.G * Gc * Gc : 0);
+    int* pre_all = cnt_all + (CELL ? p.G * ncell : 0);
+    int* wtot_all = pre_all + (CELL ? p.G * npre : 0);  // [G][16] per-wave totals of the binning scan
 
     const int t = threadIdx.x;
     const int g = t / p.N;
@@ -565,7 +608,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #endif
     if (in_group && i == 0) flags[g] = 0;
     if (t == 0) flags[p.G] = 0;  // arrival counter of the G = 1 any_done (published by the phase-2 barrier)
-    if (CELL && in_group && i < Gc * Gc) cnt_all[g * Gc * Gc + i] = 0;  // published by the phase-2 barrier
+    if (CELL && in_group)  // published by the phase-2 barrier
+        for (int c = i; c < ncell; c += p.N) cnt_all[g * ncell + c] = 0;
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
@@ -577,29 +621,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     // row per env holding every agent's fields, group = N)
     const int64_t r_unit = p.r_group == 1 ? (int64_t)a : (int64_t)env;
     const int r_slot = p.r_group == 1 ? 0 : i;
-    // cell path: previous neighbour indices (nn_idx on entry, a search hint only), loaded early
-    int seed[L - 2];
-    bool seeds_ok = CELL && active && p.idx != nullptr;
+    // cell path: previous neighbour indices (nn_idx on entry, a search hint only), loaded early and checked at use
+    int64_t hint[L - 2];
+    const bool has_hint = CELL && active && p.idx != nullptr;
 #pragma unroll
-    for (int s = 0; s < L - 2; ++s) seed[s] = 0;
-    if (seeds_ok) {
+    for (int s = 0; s < L - 2; ++s) hint[s] = -1;
+    if (has_hint) {
         const int64_t* hp = p.idx + a * p.k;
 #pragma unroll
         for (int s = 0; s < L - 2; ++s)
-            if (s < p.k) {
-                const int64_t v = hp[s];
-                seeds_ok = seeds_ok && v >= 0 && v < p.N && v != i;
-                seed[s] = (int)v;
-            }
-#pragma unroll
-        for (int s = 0; s < L - 2; ++s)
-#pragma unroll
-            for (int u = s + 1; u < L - 2; ++u)
-                if (u < p.k) seeds_ok = seeds_ok && seed[s] != seed[u];
-        if (!seeds_ok) {
-#pragma unroll
-            for (int s = 0; s < L - 2; ++s) seed[s] = 0;
-        }
+            if (s < p.k) hint[s] = hp[s];
     }
     if (active && p.r_state && r_unit >= p.r_skip) {
         const float* po = p.r_prev + a * p.k;
@@ -617,8 +648,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
             h = __fadd_rn(p.heading[a], __fmul_rn(ang, p.dt));               // :329
             const float lin = clamp_t(ac.x, p.v_min, p.v_max);               // :331
-            float vx = __fmul_rn(lin, cosf(h));                              // :335
-            float vy = __fmul_rn(lin, sinf(h));                              // :336
+            float sn, cs;
+            sincosf(h, &sn, &cs);                                            // ocml: the sinf / cosf bits
+            float vx = __fmul_rn(lin, cs);                                   // :335
+            float vy = __fmul_rn(lin, sn);                                   // :336
             vx = __fmul_rn(nan_to_num(vx), p.dt);                            // :346, :349
             vy = __fmul_rn(nan_to_num(vy), p.dt);
             x = __fadd_rn(x, vx);                                            // :350
@@ -658,8 +691,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             const float ang = clamp_t(__fadd_rn(mean.y, na), -0.025f, 0.025f);  // :343
             h = __fadd_rn(p.heading[a], __fmul_rn(ang, p.dt));                   // :345
             lin = clamp_t(lin, 5e-6f, p.v_max);                                   // :347
-            float vx = __fmul_rn(lin, cosf(h));                                   // :351
-            float vy = __fmul_rn(lin, sinf(h));                                   // :352
+            float sn, cs;
+            sincosf(h, &sn, &cs);
+            float vx = __fmul_rn(lin, cs);                                        // :351
+            float vy = __fmul_rn(lin, sn);                                        // :352
             const float n = sqrt_rn(__fadd_rn(__fmul_rn(vx, vx), __fmul_rn(vy, vy)));  // :358
             vx = __fmul_rn(nan_to_num(__fdiv_rn(vx, n)), p.dt);                  // :358-365
             vy = __fmul_rn(nan_to_num(__fdiv_rn(vy, n)), p.dt);
@@ -721,41 +756,50 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
     int cx = 0, cy = 0;
     if (CELL) {
-        int* cnt = cnt_all + g * Gc * Gc;
+        int* cnt = cnt_all + g * ncell;
         int* pre = pre_all + g * npre;
         float4* ext = ext_all + g * p.ecap;
         int rank = 0;
         if (active) {
-            cx = min((int)(x * p.inv_cw), Gc - 1);  // x, y in [0, box] after check_boundary
-            cy = min((int)(y * p.inv_cw), Gc - 1);
-            rank = atomicAdd(&cnt[cy * Gc + cx], 1);
+            cx = min((int)(x * p.inv_cwx), gx - 1);  // x, y in [0, box] after check_boundary
+            cy = min((int)(y * p.inv_cwy), gy - 1);
+            rank = atomicAdd(&cnt[cy * gx + cx], 1);
         }
         __syncthreads();
-        if (in_group && i < 64) {  // one wave per env (groups are wave-aligned whenever CELL): exclusive scan
-            const int nv = npre - 1, per = (npre + 63) / 64;
-            auto vcount = [&](int f) {
-                const int yy = f / W2, e = f - yy * W2;
-                if (e < kRg) return PERIODIC ? cnt[yy * Gc + Gc - kRg + e] : 0;          // ghosts of the last columns
-                if (e >= Gc + kRg) return PERIODIC ? cnt[yy * Gc + e - Gc - kRg] : 0;    // ghosts of the first columns
-                return cnt[yy * Gc + e - kRg];
+        // exclusive prefix over the env's virtual cells by all of its lanes (envs are wave-aligned whenever CELL):
+        // `per` consecutive virtual cells per lane, a DPP wave scan, the wave totals through LDS
+        {
+            const int nv = npre - 1, per = (npre + p.N - 1) / p.N;
+            const int f0 = in_group ? i * per : npre;
+            const int y0 = f0 / W2, e0 = f0 - y0 * W2;
+            auto vcount = [&](int yy, int e) {
+                if (e < kRg) return PERIODIC ? cnt[yy * gx + gx - kRg + e] : 0;          // ghosts of the last columns
+                if (e >= gx + kRg) return PERIODIC ? cnt[yy * gx + e - gx - kRg] : 0;    // ghosts of the first columns
+                return cnt[yy * gx + e - kRg];
             };
             int local = 0;
-            for (int q = 0; q < per; ++q) {
-                const int f = i * per + q;
-                if (f < nv) local += vcount(f);
+            for (int q = 0, yy = y0, e = e0; q < per && f0 + q < nv; ++q) {
+                local += vcount(yy, e);
+                if (++e == W2) {
+                    e = 0;
+                    ++yy;
+                }
             }
-            int inc = local;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int t2 = __shfl_up(inc, o, 64);
-                if (i >= o) inc += t2;
-            }
+            const int inc = wave_incl_scan(local);
+            const int wv = i >> 6;
+            int* wtot = wtot_all + g * 16;
+            const int wsum = __builtin_amdgcn_readlane(inc, 63);
+            if (in_group && (i & 63) == 0) wtot[wv] = wsum;
+            __syncthreads();
             int run = inc - local;
-            for (int q = 0; q < per; ++q) {
-                const int f = i * per + q;
-                if (f < npre) {
-                    pre[f] = run;
-                    if (f < nv) run += vcount(f);
+            if (in_group)
+                for (int w = 0; w < wv; ++w) run += wtot[w];
+            for (int q = 0, yy = y0, e = e0; q < per && f0 + q < npre; ++q) {
+                pre[f0 + q] = run;
+                if (f0 + q < nv) run += vcount(yy, e);
+                if (++e == W2) {
+                    e = 0;
+                    ++yy;
                 }
             }
         }
@@ -765,8 +809,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             const float4 ghost = make_float4(x, y, __int_as_float(i), p.box);  // sx = B: see pair_d2_shift
             const int* pr = pre + cy * W2;
             ext[pr[cx + kRg] + rank] = ent;
-            if (PERIODIC && cx >= Gc - kRg) ext[pr[cx - Gc + kRg] + rank] = ghost;  // in front (Gc >= 2 kRg)
-            if (PERIODIC && cx < kRg) ext[pr[Gc + kRg + cx] + rank] = ghost;        // behind
+            if (PERIODIC && cx >= gx - kRg) ext[pr[cx - gx + kRg] + rank] = ghost;  // in front (gx >= 2 kRg)
+            if (PERIODIC && cx < kRg) ext[pr[gx + kRg + cx] + rank] = ghost;        // behind
         }
         __syncthreads();
     }
@@ -787,6 +831,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         // a 1e-5 box margin. Seeds that are out of range or repeated (a stale or uninitialised buffer) fall back.
         bool use = false;
         float r = 0.0f;
+        bool seeds_ok = has_hint;
+        int seed[L - 2];
+#pragma unroll
+        for (int s = 0; s < L - 2; ++s) {
+            seed[s] = (int)min((uint64_t)hint[s], (uint64_t)(p.N - 1));  // in range for the LDS read either way
+            if (s < p.k) seeds_ok = seeds_ok && (uint64_t)hint[s] < (uint64_t)p.N && seed[s] != i;
+        }
+#pragma unroll
+        for (int s = 0; s < L - 2; ++s)
+#pragma unroll
+            for (int u = s + 1; u < L - 2; ++u)
+                if (u < p.k) seeds_ok = seeds_ok && seed[s] != seed[u];
         if (active && seeds_ok) {
             const float2* cand = lpos + g * p.S;
             float rho2 = 0.0f;
@@ -797,17 +853,25 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                     rho2 = fmaxf(rho2, pair_d2<PERIODIC>(x, y, c.x, c.y, p.box));
                 }
             r = sqrtf(rho2) * (1.0f + __int_as_float((127 + p.ib - 20) << 23)) + p.cell_eps;
-            use = r <= ((float)kRg - 0.5f) * p.cw;  // the disk stays within kRg cells (see pair_d2_shift)
+            // at most kRows rows; periodic: at most kRg - 1 columns either side (see cand_d2x2). Without wrap, rows
+            // and columns beyond the box are empty, so only the rows inside it count
+            int q0 = (int)floorf((y - r) * p.inv_cwy), q1 = (int)floorf((y + r) * p.inv_cwy);
+            if (!PERIODIC) {
+                q0 = max(q0, 0);
+                q1 = min(q1, gy - 1);
+            }
+            use = (!PERIODIC || r <= p.r_lim) && q1 - q0 < kRows;
         }
 #ifdef FLOCK_DIAG_NOSCAN  // diagnostics only: cost of everything but the cell scans (results are wrong)
         use = false;
 #pragma unroll
         for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #else
-        scan_disk<L, PERIODIC>(key, ext, pre, Gc, cx, cy, use, r, p.ib, x, y, p.box, p.cw, p.inv_cw, cmax);
+        scan_seeded<L, PERIODIC>(key, ext, pre, gx, gy, cy, use, r, p.ib, x, y, p.box, p.cwy, p.inv_cwx, p.inv_cwy,
+                                 cmax);
 #endif
         ok = use;
-        R = kRg;
+        R = 1;  // rows of the exact rescan
         PHASE(3);
 #ifdef FLOCK_DIAG_NOSCAN
         ok = true;
@@ -817,8 +881,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #endif
             PHASE_COUNT(16, 1);
             uint32_t key2[L];
-            const bool ok2 = scan_cells<L, PERIODIC>(key2, ext, pre, Gc, cx, cy, kRg, p.ib, x, y, p.box, p.cw,
-                                                     p.cell_eps, cmax, active && !use);
+            const bool ok2 = scan_square<L, PERIODIC>(key2, ext, pre, gx, gy, cx, cy, 1, p.ib, x, y, p.box, p.cwx,
+                                                      p.cwy, p.cell_eps, cmax, active && !use);
             if (!use) {
 #pragma unroll
                 for (int s = 0; s < L; ++s) key[s] = key2[s];
@@ -840,7 +904,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (__ballot(amb) != 0) PHASE_COUNT(18, 1);
 #endif
         if (CELL && amb)
-            exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, Gc, cx, cy, R, x, y,
+            exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, gx, gy, cx, cy, R, x, y,
                                             p.box);
     }
     PHASE(5);
@@ -1031,15 +1095,17 @@ struct Cfg {
     size_t lds;
 };
 
-// cell grid side for the step kernel's cell list (0 = full scan): ~1 agent per cell, >= 11 cells per side
-int cell_grid(int N, int variant) {
-    if (variant == kSense || N < 128) return 0;
-    int gc = 1;
-    while ((gc + 1) * (gc + 1) <= N) ++gc;  // about one agent per cell
-    return gc >= 11 ? gc : 0;               // pair_d2_shift needs Gc >= 11 (kRg = 3)
+// cell grid of the step kernel's cell list (N >= 128): about one agent per cell, rows about twice the typical
+// (k+1)-th neighbour distance tall (0.38 sqrt N rows: 5 agents within r_typ means r_typ = box sqrt(5 / (pi N))), at
+// least kRows distinct rows and gx >= 2 kRg + 4 columns (cand_d2x2). Returns false for the full-scan path.
+bool cell_grid(int N, int variant, int* gx, int* gy) {
+    if (variant == kSense || N < 128) return false;
+    *gy = max(kRows, (int)(0.38f * sqrtf((float)N)));
+    *gx = max(2 * kRg + 4, N / *gy);
+    return true;
 }
 
-Cfg make_cfg(int E, int N, bool reset, int cells) {
+Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy) {
     Cfg c;
     c.S = (N + 1) & ~1;
     c.P = 1 << ceil_log2(N);
@@ -1052,7 +1118,7 @@ Cfg make_cfg(int E, int N, bool reset, int cells) {
         c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + 2 * c.G * sizeof(int);
     if (!reset && cells) {  // ext (2N + 2 float4, 16-B aligned) + cnt + pre per env
         c.lds = (c.lds + 15) & ~(size_t)15;
-        c.lds += (size_t)c.G * ((2 * N + 2) * sizeof(float4) + (size_t)(cells * cells + cells * (cells + 2 * kRg) + 1) * 4);
+        c.lds += (size_t)c.G * ((2 * N + 2) * sizeof(float4) + (size_t)(gx * gy + gy * (gx + 2 * kRg) + 1 + 16) * 4);
     }
     return c;
 }
@@ -1087,15 +1153,18 @@ void launch_reset_L(const Cfg& c, const Params& p, hipStream_t s) {
 
 int dispatch(Params& p, hipStream_t s, bool reset) {
     if (p.E == 0) return FLOCK_OK;
-    p.cells = (reset || getenv("FLOCK_NO_CELLS")) ? 0 : cell_grid(p.N, p.variant);
+    p.cells = (reset || getenv("FLOCK_NO_CELLS")) ? 0 : cell_grid(p.N, p.variant, &p.gx, &p.gy);
     if (p.cells) {
         p.ecap = 2 * p.N + 2;
-        p.cw = p.box / (float)p.cells;
-        p.inv_cw = (float)p.cells / p.box;
+        p.cwx = p.box / (float)p.gx;
+        p.cwy = p.box / (float)p.gy;
+        p.inv_cwx = (float)p.gx / p.box;
+        p.inv_cwy = (float)p.gy / p.box;
         p.cell_eps = p.box * 1e-5f;
+        p.r_lim = fminf(0.999f * p.cwy, (float)(kRg - 1) * p.cwx);  // kRows rows, kRg - 1 columns each side
         if (!(p.box > 0.0f)) p.cells = 0;
     }
-    const Cfg c = make_cfg(p.E, p.N, reset, p.cells);
+    const Cfg c = make_cfg(p.E, p.N, reset, p.cells, p.gx, p.gy);
     p.G = c.G;
     p.S = c.S;
     p.P = c.P;

@@ -14,22 +14,22 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-SO = os.path.join(ROOT, "marl_range_flocking_amd", "_build", "libflock_env_prof.so")
+SO = os.environ.get("FLOCK_PROF_SO") or os.path.join(ROOT, "marl_range_flocking_amd", "_build", "libflock_env_prof.so")
 NAMES = ["kinematics", "phase2 barrier", "cell binning", "3x3 scan", "5x5 scan", "finalize/fallback",
          "outputs", "any_done barrier"]
 
 
 def build():
-    from marl_range_flocking_amd.build import HIPCC_FLAGS, INCLUDE, CSRC, hipcc
+    from marl_range_flocking_amd.build import CSRC, FILE_FLAGS, HIPCC_FLAGS, INCLUDE, hipcc
 
     os.makedirs(os.path.dirname(SO), exist_ok=True)
-    cmd = [hipcc()] + HIPCC_FLAGS + ["-DFLOCK_PHASE_PROF", "-shared", "-I", INCLUDE, "-o", SO,
+    cmd = [hipcc()] + HIPCC_FLAGS + FILE_FLAGS["flock_env.hip"] + ["-DFLOCK_PHASE_PROF", "-shared", "-I", INCLUDE, "-o", SO,
                                      os.path.join(CSRC, "flock_env.hip")]
     print(" ".join(cmd))
     subprocess.check_call(cmd)
 
 
-def run(E, N, k, steps):
+def run(E, N, k, steps, variant="v2"):
     import numpy as np
     import torch
 
@@ -52,11 +52,23 @@ def run(E, N, k, steps):
     f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 6 + [ctypes.c_int] * 2 + \
         [ctypes.c_void_p] * 9
     stream = torch.cuda.current_stream(dev).cuda_stream
+    gd = lib.flock_step_uw_discrete
+    gd.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 5 + [ctypes.c_int] + \
+        [ctypes.c_void_p] * 5 + [ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int] + \
+        [ctypes.c_void_p] * 7
+    aid = torch.randint(0, 10, (E, N), device=dev, generator=g)
+    table = torch.rand(10, 2, device=dev, generator=g)
+    prev = torch.zeros(E, N, device=dev)
 
     def step():
-        rc = f(stream, E, N, k, box, 14.0, 2.5, 0.1, 0.0, 2.5, 1, 0, pos.data_ptr(), head.data_ptr(),
-               act.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(), rew.data_ptr(), done.data_ptr(),
-               anyd.data_ptr())
+        if variant == "v2":
+            rc = f(stream, E, N, k, box, 14.0, 2.5, 0.1, 0.0, 2.5, 1, 0, pos.data_ptr(), head.data_ptr(),
+                   act.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(), rew.data_ptr(), done.data_ptr(),
+                   anyd.data_ptr())
+        else:
+            rc = gd(stream, E, N, k, box, 14.0, 2.5, 0.1, 2.5, 0, pos.data_ptr(), head.data_ptr(), prev.data_ptr(),
+                    aid.data_ptr(), None, 0.1, 7, 0, table.data_ptr(), 10, vel.data_ptr(), dnn.data_ptr(),
+                    idx.data_ptr(), rew.data_ptr(), done.data_ptr(), anyd.data_ptr(), None)
         assert rc == 0, rc
 
     for _ in range(5):
@@ -89,8 +101,9 @@ if __name__ == "__main__":
     ap.add_argument("--N", type=int, default=256)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--variant", default="v2", choices=["v2", "uwd"])
     a = ap.parse_args()
     if a.build:
         build()
     else:
-        run(a.E, a.N, a.k, a.steps)
+        run(a.E, a.N, a.k, a.steps, a.variant)
