@@ -119,6 +119,20 @@ int64_t flock_sc_update_size(void); /* sizeof(FlockScUpdate), for binding checks
  * r < B (uniform sampling with replacement, ReplayBuffer.sample_buffer, utils.py:65-76). idx may be NULL. */
 int flock_sc_prep(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
                   int64_t* agent_out, int64_t agent);
+/* The same prologue with a minibatch snapshot: staging row r (r < B) receives every field of replay row
+ * Philox4x32-10(seed, counter, r) mod rows (the row flock_sc_prep samples; written to idx_out when non-NULL).
+ * An update whose ring pointers are the staging fields and whose idx is 0..B-1 computes exactly the update on
+ * the sampled ring rows, and no longer reads the ring: the next env step may rewrite it concurrently. */
+typedef struct FlockScRows {
+    float* state;      /* [rows][in_dim] */
+    float* new_state;  /* [rows][in_dim] */
+    float* action;     /* [rows][n_actions] */
+    float* reward;     /* [rows] */
+    float* terminal;   /* [rows] (1 - done) */
+} FlockScRows;
+int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
+                           int64_t* agent_out, int64_t agent, int in_dim, int n_actions, const FlockScRows* ring,
+                           const FlockScRows* staging);
 int flock_sc_critic_update(void* stream, const FlockScUpdate* u); /* :118-141 */
 int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (after the critic update) */
 

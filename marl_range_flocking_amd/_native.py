@@ -46,6 +46,12 @@ SIGNATURES = {
 }
 
 
+class FlockScRows(ctypes.Structure):
+    """Mirror of ``FlockScRows`` (include/flock_learn.h): replay fields of a ring or of its minibatch snapshot."""
+
+    _fields_ = [(n, _c_void_p) for n in ("state", "new_state", "action", "reward", "terminal")]
+
+
 class FlockScUpdate(ctypes.Structure):
     """Mirror of ``FlockScUpdate`` (include/flock_learn.h): all pointers are device pointers."""
 
@@ -82,6 +88,8 @@ SIGNATURES.update({
                          ctypes.POINTER(FlockRingField)],
     "flock_sc_workspace_floats": [_c_int] * 5,
     "flock_sc_update_size": [],
+    "flock_sc_prep_snapshot": [_c_void_p, _c_int, ctypes.c_int64, _c_u64, _c_u64, _c_void_p, _c_void_p,
+                               ctypes.c_int64, _c_int, _c_int, _c_void_p, _c_void_p],
     "flock_sc_prep": [_c_void_p, _c_int, ctypes.c_int64, _c_u64, _c_u64, _c_void_p, _c_void_p, ctypes.c_int64],
     "flock_sc_critic_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_actor_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],

@@ -1148,9 +1148,46 @@ __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t see
     }
 }
 
+// learn() prologue with a minibatch snapshot: the sampled rows of every replay field are copied to staging rows
+// 0..B-1, so the update can read the staging copy (with the identity index) while the next env step rewrites the ring
+__global__ __launch_bounds__(256) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
+                                                        int64_t* idx_out, int64_t* agent_out, int64_t agent,
+                                                        int in_dim, int n_actions, FlockScRows src,
+                                                        FlockScRows dst) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r == 0) *agent_out = agent;
+    if (r >= B) return;
+    const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
+    const uint64_t u = ((uint64_t)q.x << 32) | q.y;
+    const int64_t row = (int64_t)(u % (uint64_t)rows);  // the row sc_prep samples for r
+    if (idx_out) idx_out[r] = row;
+    for (int c = 0; c < in_dim; ++c) {
+        dst.state[(int64_t)r * in_dim + c] = src.state[row * in_dim + c];
+        dst.new_state[(int64_t)r * in_dim + c] = src.new_state[row * in_dim + c];
+    }
+    for (int c = 0; c < n_actions; ++c) dst.action[(int64_t)r * n_actions + c] = src.action[row * n_actions + c];
+    dst.reward[r] = src.reward[row];
+    dst.terminal[r] = src.terminal[row];
+}
+
 }  // namespace
 
 extern "C" {
+
+int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
+                           int64_t* agent_out, int64_t agent, int in_dim, int n_actions, const FlockScRows* ring,
+                           const FlockScRows* staging) {
+    if (!agent_out || !ring || !staging) return fail(-3, "flock_sc_prep_snapshot: NULL pointer");
+    if (B < 1 || rows < 1 || in_dim < 1 || n_actions < 1)
+        return fail(-5, "flock_sc_prep_snapshot: need B, rows, in_dim, n_actions >= 1");
+    const FlockScRows* rs[2] = {ring, staging};
+    for (const FlockScRows* x : rs)
+        if (!x->state || !x->new_state || !x->action || !x->reward || !x->terminal)
+            return fail(-3, "flock_sc_prep_snapshot: NULL field pointer");
+    hipLaunchKernelGGL(sc_prep_snapshot, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, B, rows, seed,
+                       counter, idx_out, agent_out, agent, in_dim, n_actions, *ring, *staging);
+    return launched();
+}
 
 int flock_sc_prep(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
                   int64_t* agent_out, int64_t agent) {

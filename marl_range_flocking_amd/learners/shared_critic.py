@@ -82,7 +82,8 @@ def _init_mlp(fp, names_uniform, generator):
 class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
-                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True):
+                 ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
+                 snapshot=False):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -120,6 +121,10 @@ class SharedCriticLearner:
             dist.sync_params(self.actors, group=dist_group)
         self.fused = fused
         self.fc1, self.fc2 = fc1, fc2
+        # snapshot (fused only): learn() first copies its B sampled rows out of the ring (flock_sc_prep_snapshot)
+        # into one of two staging slots and the update reads that copy, so the ring may be rewritten while the
+        # update runs (snapshot_into / update_slot: the copy on the env stream, the update on another one)
+        self.snapshot = bool(snapshot and fused)
         if fused:
             self._init_fused()
 
@@ -148,6 +153,23 @@ class SharedCriticLearner:
         # single GPU: the soft updates run inside the actor's gradient kernel (device-side count condition)
         self._sc = _native.FlockScUpdate(**fields)
         self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0, update_rate=0))  # data-parallel
+        self._slots = []
+        if self.snapshot:
+            self.identity_idx = torch.arange(B, dtype=torch.int64, device=dev)
+            names = ("state", "new_state", "action", "reward", "terminal")
+            self._rows_ring = _native.FlockScRows(**{n: _p(rb[n]) for n in names})
+            for _ in range(2):
+                stg = {"state": torch.zeros(B, n_in, device=dev), "new_state": torch.zeros(B, n_in, device=dev),
+                       "action": torch.zeros(B, na, device=dev), "reward": torch.zeros(B, device=dev),
+                       "terminal": torch.zeros(B, device=dev)}
+                agent_t = torch.zeros(1, dtype=torch.int64, device=dev)
+                f = dict(fields, idx=_p(self.identity_idx), agent=_p(agent_t),
+                         **{"ring_" + n: _p(stg[n]) for n in names})
+                self._slots.append(dict(staging=stg, agent=agent_t, graph=None,
+                                        rows=_native.FlockScRows(**{n: _p(stg[n]) for n in names}),
+                                        sc=_native.FlockScUpdate(**f),
+                                        sc_grads=_native.FlockScUpdate(**dict(f, do_adam=0, update_rate=0))))
+            self.staging = self._slots[0]["staging"]
 
     def _fused_update(self, u=None):
         lib = _native.lib()
@@ -157,20 +179,30 @@ class SharedCriticLearner:
         _native.check(lib.flock_sc_actor_update(st, u), "flock_sc_actor_update", learn=True)
 
     def _fused_state(self):
+        """Everything one fused update writes (graph-capture warm-ups are undone on these): the actor targets too,
+        which the in-kernel soft update moves."""
         A = self.actors
-        return self.critic.state_tensors() + [A.data, A.exp_avg, A.exp_avg_sq, self.actor_steps, self.losses]
+        return self.critic.state_tensors() + [A.data, A.target, A.exp_avg, A.exp_avg_sq, self.actor_steps,
+                                              self.losses]
 
-    def _run_fused(self, agent):
+    def _run_fused(self, agent, slot=None):
+        S = self._slots[slot] if slot is not None else None
         if not self.distributed:
+            u = S["sc"] if S is not None else self._sc
             if not self.use_graph:
-                return self._fused_update()
-            if self.graph is None:
-                self.graph = capture_graph(self._fused_update, self.device, self._fused_state())
-            return self.graph.replay()
+                return self._fused_update(u)
+            g = S["graph"] if S is not None else self.graph
+            if g is None:
+                g = capture_graph(lambda: self._fused_update(u), self.device, self._fused_state())
+                if S is not None:
+                    S["graph"] = g
+                else:
+                    self.graph = g
+            return g.replay()
         # data-parallel: gradient-only kernels, RCCL all-reduce of each network's gradient, then the Adam steps
         lib = _native.lib()
         st = _stream(self.device)
-        u = ctypes.byref(self._sc_grads)
+        u = ctypes.byref(S["sc_grads"] if S is not None else self._sc_grads)
         _native.check(lib.flock_sc_critic_update(st, u), "flock_sc_critic_update", learn=True)
         dist.allreduce_mean_(self.critic.grad, self.group)
         self.critic.adam_step_dev(self.beta)
@@ -305,10 +337,21 @@ class SharedCriticLearner:
             # one launch: agent index + (unless given) B rows uniform with replacement (utils.py:65-76)
             if idx is not None:
                 self.static_idx.copy_(torch.as_tensor(idx).to(self.device))
-            rc = _native.lib().flock_sc_prep(_stream(self.device), B, len(self.replay), self.seed,
-                                             self._learn_calls, None if idx is not None else _p(self.static_idx),
-                                             _p(self.static_agent), int(agent))
-            _native.check(rc, "flock_sc_prep", learn=True)
+            if self.snapshot:  # slot 0, one stream
+                if idx is not None:  # injected rows: copy them out of the ring by index
+                    S = self._slots[0]
+                    for n, v in S["staging"].items():
+                        v.copy_(self.replay.bufs[n][self.static_idx].reshape(v.shape))
+                    S["agent"].fill_(int(agent))
+                else:
+                    self._learn_calls -= 1
+                    self.snapshot_into(0, agent)
+                return self.update_slot(0, agent)
+            else:
+                rc = _native.lib().flock_sc_prep(_stream(self.device), B, len(self.replay), self.seed,
+                                                 self._learn_calls, None if idx is not None else _p(self.static_idx),
+                                                 _p(self.static_agent), int(agent))
+                _native.check(rc, "flock_sc_prep", learn=True)
             self._run_fused(agent)
             return self._finish_learn(agent, soft_in_kernel=not self.distributed)
         if idx is None:                                                       # utils.py:65-76 (with replacement)
@@ -328,6 +371,29 @@ class SharedCriticLearner:
                 dst[lo:hi].copy_(src)
             self.actor_steps[agent:agent + 1].copy_(S.step_dev)
         return self._finish_learn(agent)
+
+    def snapshot_into(self, slot, agent):
+        """learn() prologue of ``agent`` into staging slot 0 or 1, enqueued on the current stream: sample the B rows
+        (utils.py:65-76) and copy them out of the ring. Returns False (nothing enqueued) before the buffer holds a
+        batch. The ring may be rewritten once this has run; update_slot(slot) must follow before the slot is reused."""
+        B = self.batch_size
+        if not self.snapshot:
+            raise RuntimeError("snapshot_into needs SharedCriticLearner(snapshot=True)")
+        if self.replay.counter < B:
+            return False
+        self._learn_calls += 1
+        S = self._slots[slot]
+        rc = _native.lib().flock_sc_prep_snapshot(
+            _stream(self.device), B, len(self.replay), self.seed, self._learn_calls, _p(self.static_idx),
+            _p(S["agent"]), int(agent), self.input_dim, self.n_actions, ctypes.byref(self._rows_ring),
+            ctypes.byref(S["rows"]))
+        _native.check(rc, "flock_sc_prep_snapshot", learn=True)
+        return True
+
+    def update_slot(self, slot, agent):
+        """The rest of learn() on the rows snapshot_into(slot, agent) copied, enqueued on the current stream."""
+        self._run_fused(agent, slot)
+        return self._finish_learn(agent, soft_in_kernel=not self.distributed)
 
     def _finish_learn(self, agent, soft_in_kernel=False):
         if self.count[agent] % self.update_rate == 0 and not soft_in_kernel:                         # :152-154
@@ -359,11 +425,22 @@ class SharedCriticBench:
     """bench.py hook for BASELINE config 3: after each vectorized env step, insert every agent's transition into the
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
-    def __init__(self, env, device, seed=0, fused=True):
+    def __init__(self, env, device, seed=0, fused=True, overlap=True):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
+        # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
+        # s+1 (which rewrites the ring); in this loop the actions do not come from the actor (random-action
+        # exploration), so step s+1 does not depend on learn(s) and every kernel still sees the same data
+        # (single GPU only: with data-parallel replicas the update's all-reduces stay on the main stream)
+        self.overlap = bool(overlap and fused and not dist.active())
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
-                                           buffer_size=1_000_000, dist_group=group, fused=fused)
+                                           buffer_size=1_000_000, dist_group=group, fused=fused,
+                                           snapshot=self.overlap)
+        if self.overlap:
+            self.stream = torch.cuda.Stream(device=device)
+            self.snap_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self.learn_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self._used = [False, False]
         self.prev_obs = env.dnn.clone()
         self.prev_act = None
 
@@ -380,10 +457,34 @@ class SharedCriticBench:
         return self.learner.replay_slots(self.env.E * self.env.N)
 
     def after(self, s, action):
-        self.learner.learn(s % self.learner.n_agents)
+        L = self.learner
+        agent = s % L.n_agents
+        if not self.overlap:
+            L.learn(agent)
+            return
+        # the snapshot goes on the env stream right behind the env step (the next env step follows it in order);
+        # the update runs on the learner stream; staging slots alternate, and a slot is refilled only after the
+        # update that read it two steps ago has finished
+        main = torch.cuda.current_stream(L.device)
+        slot = s & 1
+        if self._used[slot]:
+            main.wait_event(self.learn_done[slot])
+        if not L.snapshot_into(slot, agent):
+            return
+        self.snap_done[slot].record(main)
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(self.snap_done[slot])
+            L.update_slot(slot, agent)
+            self.learn_done[slot].record(self.stream)
+        self._used[slot] = True
+
+    def finish(self):
+        """Join the learner stream into the current one (end of a timed region)."""
+        if self.overlap:
+            torch.cuda.current_stream(self.learner.device).wait_stream(self.stream)
 
     def prime(self):
-        pass
+        self.finish()
 
     def step(self, s, action):
         """One bench step with the replay insert fused into the env kernel (flock_step_v2_store), then learn()."""

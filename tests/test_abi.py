@@ -33,7 +33,8 @@ def test_header_declares_expected_entry_points():
     for name in ("flock_step_v2", "flock_step_uw", "flock_step_uw_discrete", "flock_step_flock", "flock_knn",
                  "flock_reset", "flock_abi_version", "flock_last_error", "flock_adam_step", "flock_soft_update",
                  "flock_grad_norm", "flock_gru_fwd", "flock_gru_bwd", "flock_gather_rows", "flock_scatter_rows",
-                 "flock_sc_workspace_floats", "flock_sc_critic_update", "flock_sc_actor_update"):
+                 "flock_sc_workspace_floats", "flock_sc_critic_update", "flock_sc_actor_update",
+                 "flock_sc_prep_snapshot"):
         assert name in fns, name
 
 
