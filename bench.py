@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")
+    ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
+                    help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
+                         "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
     args = ap.parse_args()
     c = CONFIGS[args.config]
     for key in ("envs", "agents", "variant", "learner", "steps"):
@@ -244,7 +247,7 @@ def main():
     if args.learner == "shared_critic":
         from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
-        hook = SharedCriticBench(env, device=dev, seed=1234 + rank)
+        hook = SharedCriticBench(env, device=dev, seed=1234 + rank, overlap=bool(args.overlap))
     elif args.learner == "vdn":
         hook = VDNBench(env, dev, seed=1234 + rank)
     elif args.learner == "maddpg_rnn":

@@ -95,6 +95,22 @@ int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sens
                         float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
                         const FlockRing* ring);
 
+/* Optional extras of the *_ext entry points (each equals its plain entry point when ext is NULL or all-NULL):
+ *  ring  (v2 only; may be NULL): the fused replay insert of flock_step_v2_store;
+ *  seeds (may be NULL): [E][N][k] u16 (rw), a compact side buffer of kNN search seeds. When set, the N >= 128
+ *        cell-list kNN reads its seeds here instead of from nn_idx on entry (2 B instead of 8 B per seed) and
+ *        writes this step's neighbour indices back for the next step. Any content is valid (out-of-range or repeated
+ *        seeds are ignored; results never depend on it); zeroes or a reset simply fall back to a proved scan. */
+typedef struct FlockStepExt {
+    const FlockRing* ring;
+    uint16_t* seeds;
+} FlockStepExt;
+int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                      float dt, float v_min, float v_max, int periodic, int rigid_boundary,
+                      float* pos, float* heading, const float* action,
+                      float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                      const FlockStepExt* ext);
+
 /* gym_flock_uw step: velocity actions; obs memory mem_in → mem_out (may alias); prev_heading (rw). nn_idx may be
  * NULL (the reference does not keep it for this env). */
 int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
@@ -120,6 +136,24 @@ int flock_step_flock(void* stream, int E, int N, int k, float box, float collisi
                      int rigid_boundary, float* pos, float* vel, const float* action,
                      const float* mem_in, float* mem_out,
                      float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
+int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                      float dt, int rigid_boundary,
+                      float* pos, const float* heading, float* prev_heading, const float* action,
+                      const float* mem_in, float* mem_out,
+                      float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                      const FlockStepExt* ext);
+int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, float sensor_range,
+                               float collision_distance, float dt, float v_max, int rigid_boundary,
+                               float* pos, float* heading, float* prev_heading, const int64_t* action_id,
+                               const float* noise, float noise_std, uint64_t seed, uint64_t rng_offset,
+                               const float* table, int n_actions,
+                               float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
+                               uint8_t* any_done, int* status, const FlockStepExt* ext);
+int flock_step_flock_ext(void* stream, int E, int N, int k, float box, float collision_distance, float dt,
+                         int rigid_boundary, float* pos, float* vel, const float* action,
+                         const float* mem_in, float* mem_out,
+                         float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                         const FlockStepExt* ext);
 
 /* Sensing only: kNN of every agent from positions (no state change). clamp != 0 clamps to [0, sensor_range]. */
 int flock_knn(void* stream, int E, int N, int k, float box, float sensor_range, int periodic, int clamp,

@@ -24,6 +24,15 @@ SIGNATURES = {
                                _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_float, _c_u64,
                                _c_u64, _c_void_p, _c_int] + [_c_void_p] * 7,
     "flock_step_flock": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_int] + [_c_void_p] * 10,
+    "flock_step_v2_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_float,
+                          _c_float, _c_int, _c_int] + [_c_void_p] * 10,
+    "flock_step_uw_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_int]
+                         + [_c_void_p] * 13,
+    "flock_step_uw_discrete_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float,
+                                   _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                   _c_float, _c_u64, _c_u64, _c_void_p, _c_int] + [_c_void_p] * 8,
+    "flock_step_flock_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_int]
+                            + [_c_void_p] * 11,
     "flock_knn": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int] + [_c_void_p] * 3,
     "flock_reset": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_float,
                     _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9,
@@ -81,6 +90,15 @@ class FlockRing(ctypes.Structure):
                 + [("actor_state", _c_void_p), ("actor_new_state", _c_void_p), ("group", ctypes.c_int64),
                    ("store_done", _c_int)])
 
+
+class FlockStepExt(ctypes.Structure):
+    """Mirror of ``FlockStepExt`` (include/flock_amd.h): optional extras of the *_ext step entry points."""
+
+    _fields_ = [("ring", ctypes.POINTER(FlockRing)), ("seeds", _c_void_p)]
+
+
+for _name in ("flock_step_v2_ext", "flock_step_uw_ext", "flock_step_uw_discrete_ext", "flock_step_flock_ext"):
+    SIGNATURES[_name] = SIGNATURES[_name][:-1] + [ctypes.POINTER(FlockStepExt)]
 
 SIGNATURES.update({
     "flock_step_v2_store": SIGNATURES["flock_step_v2"] + [ctypes.POINTER(FlockRing)],

@@ -91,6 +91,7 @@ struct Params {
     const float* r_prev;
     int64_t r_cap, r_start, r_skip;
     int r_group, r_done;  // agents per ring row (1 or N); stored flag: 0 -> 1 - done, 1 -> done
+    uint16_t* seeds;      // [E][N][k] compact kNN search seeds (rw), or NULL: nn_idx on entry is the hint
     // cell list (step variants, N >= 128)
     int cells, gx, gy, ecap;  // cells != 0: cell list on a gx x gy grid; extended-array capacity per env (2N + 2)
     float cwx, cwy, inv_cwx, inv_cwy, cell_eps, r_lim;
@@ -623,10 +624,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     const int r_slot = p.r_group == 1 ? 0 : i;
     // cell path: previous neighbour indices (nn_idx on entry, a search hint only), loaded early and checked at use
     int64_t hint[L - 2];
-    const bool has_hint = CELL && active && p.idx != nullptr;
+    const bool has_hint = CELL && active && (p.seeds != nullptr || p.idx != nullptr);
 #pragma unroll
     for (int s = 0; s < L - 2; ++s) hint[s] = -1;
-    if (has_hint) {
+    if (has_hint && p.seeds) {
+        const uint16_t* hp = p.seeds + a * p.k;
+        if (L - 2 == 4 && p.k == 4) {  // one 8-B load (a * k u16 is 8-B aligned)
+            const uint2 v = *reinterpret_cast<const uint2*>(hp);
+            hint[0] = v.x & 0xFFFFu;
+            hint[1] = v.x >> 16;
+            hint[2 % (L - 2)] = v.y & 0xFFFFu;
+            hint[3 % (L - 2)] = v.y >> 16;
+        } else {
+#pragma unroll
+            for (int s = 0; s < L - 2; ++s)
+                if (s < p.k) hint[s] = hp[s];
+        }
+    } else if (has_hint) {
         const int64_t* hp = p.idx + a * p.k;
 #pragma unroll
         for (int s = 0; s < L - 2; ++s)
@@ -923,6 +937,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 p.dnn[a * p.k + (s - 1)] = d;
                 if (p.idx) p.idx[a * p.k + (s - 1)] = (int64_t)bj[s];
             }
+        }
+        if (CELL && p.seeds) {  // this step's neighbours: the next step's search seeds
+            uint16_t* sp = p.seeds + a * p.k;
+            if (L - 2 == 4 && p.k == 4)
+                *reinterpret_cast<uint2*>(sp) = make_uint2((uint32_t)bj[1] | ((uint32_t)bj[2 % (L - 1)] << 16),
+                                                           (uint32_t)bj[3 % (L - 1)] | ((uint32_t)bj[4 % (L - 1)] << 16));
+            else
+#pragma unroll
+                for (int s = 1; s < L - 1; ++s)
+                    if (s <= p.k) sp[s - 1] = (uint16_t)bj[s];
         }
         if (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK) {  // torch.roll + insert (:120-123)
             const float* mi = p.mem_in + a * kMem * p.k;
@@ -1235,15 +1259,46 @@ int flock_phase_read(unsigned long long* host) {
 
 const char* flock_last_error(void) { return g_err; }
 
-int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
-                  float dt, float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
-                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
-                  uint8_t* any_done) {
+}  // extern "C"
+
+namespace {
+
+// ring (may be NULL): the fused replay insert; seeds (may be NULL): compact kNN search seeds
+int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance, float dt,
+                 float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
+                 const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
+                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds) {
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done))
         return fail(FLOCK_E_NULL, "flock_step_v2: NULL pointer");
     Params p = base(E, N, k, box);
+    if (ring) {
+        if (E && (!ring->state || !ring->action || !ring->reward || !ring->new_state || !ring->terminal ||
+                  !ring->prev_obs))
+            return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL ring pointer");
+        if (ring->group != 1 && ring->group != N)
+            return fail(FLOCK_E_ARG,
+                        "flock_step_v2_store: ring group must be 1 (a row per agent) or N (a row per env)");
+        const int64_t units = ring->group == 1 ? (int64_t)E * N : (int64_t)E;
+        if (ring->skip < 0 || units - ring->skip > ring->capacity || ring->start < 0 ||
+            ring->start >= ring->capacity)
+            return fail(FLOCK_E_ARG,
+                        "flock_step_v2_store: need skip >= 0, rows - skip <= capacity, 0 <= start < capacity");
+        p.r_state = ring->state;
+        p.r_action = ring->action;
+        p.r_reward = ring->reward;
+        p.r_new = ring->new_state;
+        p.r_term = ring->terminal;
+        p.r_prev = ring->prev_obs;
+        p.r_cap = ring->capacity;
+        p.r_start = ring->start;
+        p.r_skip = ring->skip;
+        p.r_astate = ring->actor_state;
+        p.r_anew = ring->actor_new_state;
+        p.r_group = (int)ring->group;
+        p.r_done = ring->store_done;
+    }
     p.variant = FLOCK_VARIANT_V2;
     p.periodic = periodic != 0;
     p.rigid = rigid_boundary != 0;
@@ -1261,63 +1316,47 @@ int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_ran
     p.reward = reward;
     p.done = done;
     p.any_done = any_done;
+    p.seeds = seeds;
     return dispatch(p, (hipStream_t)stream, false);
+}
+
+}  // namespace
+
+extern "C" {
+
+int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                  float dt, float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
+                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
+                  uint8_t* any_done) {
+    return step_v2_impl(stream, E, N, k, box, sensor_range, collision_distance, dt, v_min, v_max, periodic,
+                        rigid_boundary, pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, nullptr,
+                        nullptr);
 }
 
 int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
                         float dt, float v_min, float v_max, int periodic, int rigid_boundary, float* pos,
                         float* heading, const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward,
                         uint8_t* done, uint8_t* any_done, const FlockRing* ring) {
-    int rc = check_common(E, N, k);
-    if (rc) return rc;
-    if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done || !ring))
-        return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL pointer");
-    if (E && (!ring->state || !ring->action || !ring->reward || !ring->new_state || !ring->terminal ||
-              !ring->prev_obs))
-        return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL ring pointer");
-    if (ring->group != 1 && ring->group != N)
-        return fail(FLOCK_E_ARG, "flock_step_v2_store: ring group must be 1 (a row per agent) or N (a row per env)");
-    const int64_t units = ring->group == 1 ? (int64_t)E * N : (int64_t)E;
-    if (ring->skip < 0 || units - ring->skip > ring->capacity || ring->start < 0 || ring->start >= ring->capacity)
-        return fail(FLOCK_E_ARG, "flock_step_v2_store: need skip >= 0, rows - skip <= capacity, 0 <= start < capacity");
-    Params p = base(E, N, k, box);
-    p.variant = FLOCK_VARIANT_V2;
-    p.periodic = periodic != 0;
-    p.rigid = rigid_boundary != 0;
-    p.sensor_range = sensor_range;
-    p.cd = collision_distance;
-    p.dt = dt;
-    p.v_min = v_min;
-    p.v_max = v_max;
-    p.pos = pos;
-    p.heading = heading;
-    p.action = action;
-    p.vel = vel;
-    p.dnn = dnn;
-    p.idx = nn_idx;
-    p.reward = reward;
-    p.done = done;
-    p.any_done = any_done;
-    p.r_state = ring->state;
-    p.r_action = ring->action;
-    p.r_reward = ring->reward;
-    p.r_new = ring->new_state;
-    p.r_term = ring->terminal;
-    p.r_prev = ring->prev_obs;
-    p.r_cap = ring->capacity;
-    p.r_start = ring->start;
-    p.r_skip = ring->skip;
-    p.r_astate = ring->actor_state;
-    p.r_anew = ring->actor_new_state;
-    p.r_group = (int)ring->group;
-    p.r_done = ring->store_done;
-    return dispatch(p, (hipStream_t)stream, false);
+    if (E && !ring) return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL pointer");
+    return step_v2_impl(stream, E, N, k, box, sensor_range, collision_distance, dt, v_min, v_max, periodic,
+                        rigid_boundary, pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, ring,
+                        nullptr);
 }
 
-int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
-                  float dt, int rigid_boundary, float* pos, const float* heading, float* prev_heading,
-                  const float* action, const float* mem_in, float* mem_out, float* vel, float* dnn, int64_t* nn_idx,
-                  float* reward, uint8_t* done, uint8_t* any_done) {
+int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                      float dt, float v_min, float v_max, int periodic, int rigid_boundary, float* pos,
+                      float* heading, const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward,
+                      uint8_t* done, uint8_t* any_done, const FlockStepExt* ext) {
+    return step_v2_impl(stream, E, N, k, box, sensor_range, collision_distance, dt, v_min, v_max, periodic,
+                        rigid_boundary, pos, heading, action, vel, dnn, nn_idx, reward, done, any_done,
+                        ext ? ext->ring : nullptr, ext ? ext->seeds : nullptr);
+}
+
+int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                      float dt, int rigid_boundary, float* pos, const float* heading, float* prev_heading,
+                      const float* action, const float* mem_in, float* mem_out, float* vel, float* dnn,
+                      int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done, const FlockStepExt* ext) {
+    if (ext && ext->ring) return fail(FLOCK_E_ARG, "flock_step_uw_ext: the fused replay insert is v2 only");
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !prev_heading || !action || !mem_in || !mem_out || !vel || !dnn || !reward ||
@@ -1329,6 +1368,7 @@ int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_ran
     p.sensor_range = sensor_range;
     p.cd = collision_distance;
     p.com_r = (float)((double)collision_distance * 4.0);  // collision_distance*4 (gym_flock_uw.py:197)
+    p.seeds = ext ? ext->seeds : nullptr;
     p.dt = dt;
     p.pos = pos;
     p.heading = const_cast<float*>(heading);
@@ -1345,12 +1385,22 @@ int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_ran
     return dispatch(p, (hipStream_t)stream, false);
 }
 
-int flock_step_uw_discrete(void* stream, int E, int N, int k, float box, float sensor_range,
-                           float collision_distance, float dt, float v_max, int rigid_boundary, float* pos,
-                           float* heading, float* prev_heading, const int64_t* action_id, const float* noise,
-                           float noise_std, uint64_t seed, uint64_t rng_offset, const float* table, int n_actions,
-                           float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
-                           int* status) {
+int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                  float dt, int rigid_boundary, float* pos, const float* heading, float* prev_heading,
+                  const float* action, const float* mem_in, float* mem_out, float* vel, float* dnn, int64_t* nn_idx,
+                  float* reward, uint8_t* done, uint8_t* any_done) {
+    return flock_step_uw_ext(stream, E, N, k, box, sensor_range, collision_distance, dt, rigid_boundary, pos, heading,
+                             prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
+                             nullptr);
+}
+
+int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, float sensor_range,
+                               float collision_distance, float dt, float v_max, int rigid_boundary, float* pos,
+                               float* heading, float* prev_heading, const int64_t* action_id, const float* noise,
+                               float noise_std, uint64_t seed, uint64_t rng_offset, const float* table,
+                               int n_actions, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
+                               uint8_t* any_done, int* status, const FlockStepExt* ext) {
+    if (ext && ext->ring) return fail(FLOCK_E_ARG, "flock_step_uw_discrete_ext: the fused replay insert is v2 only");
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !prev_heading || !action_id || !table || !vel || !dnn || !reward || !done ||
@@ -1381,12 +1431,27 @@ int flock_step_uw_discrete(void* stream, int E, int N, int k, float box, float s
     p.done = done;
     p.any_done = any_done;
     p.status = status;
+    p.seeds = ext ? ext->seeds : nullptr;
     return dispatch(p, (hipStream_t)stream, false);
 }
 
-int flock_step_flock(void* stream, int E, int N, int k, float box, float collision_distance, float dt,
-                     int rigid_boundary, float* pos, float* vel, const float* action, const float* mem_in,
-                     float* mem_out, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done) {
+int flock_step_uw_discrete(void* stream, int E, int N, int k, float box, float sensor_range,
+                           float collision_distance, float dt, float v_max, int rigid_boundary, float* pos,
+                           float* heading, float* prev_heading, const int64_t* action_id, const float* noise,
+                           float noise_std, uint64_t seed, uint64_t rng_offset, const float* table, int n_actions,
+                           float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done,
+                           int* status) {
+    return flock_step_uw_discrete_ext(stream, E, N, k, box, sensor_range, collision_distance, dt, v_max,
+                                      rigid_boundary, pos, heading, prev_heading, action_id, noise, noise_std, seed,
+                                      rng_offset, table, n_actions, vel, dnn, nn_idx, reward, done, any_done, status,
+                                      nullptr);
+}
+
+int flock_step_flock_ext(void* stream, int E, int N, int k, float box, float collision_distance, float dt,
+                         int rigid_boundary, float* pos, float* vel, const float* action, const float* mem_in,
+                         float* mem_out, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
+                         uint8_t* any_done, const FlockStepExt* ext) {
+    if (ext && ext->ring) return fail(FLOCK_E_ARG, "flock_step_flock_ext: the fused replay insert is v2 only");
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !vel || !action || !mem_in || !mem_out || !dnn || !reward || !done || !any_done))
@@ -1395,6 +1460,7 @@ int flock_step_flock(void* stream, int E, int N, int k, float box, float collisi
     p.variant = FLOCK_VARIANT_FLOCK;
     p.rigid = rigid_boundary != 0;
     p.clamp = 0;  // gym_flock.py:105: no clamp
+    p.seeds = ext ? ext->seeds : nullptr;
     p.cd = collision_distance;
     p.dt = dt;
     p.pos = pos;
@@ -1408,6 +1474,13 @@ int flock_step_flock(void* stream, int E, int N, int k, float box, float collisi
     p.done = done;
     p.any_done = any_done;
     return dispatch(p, (hipStream_t)stream, false);
+}
+
+int flock_step_flock(void* stream, int E, int N, int k, float box, float collision_distance, float dt,
+                     int rigid_boundary, float* pos, float* vel, const float* action, const float* mem_in,
+                     float* mem_out, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done) {
+    return flock_step_flock_ext(stream, E, N, k, box, collision_distance, dt, rigid_boundary, pos, vel, action,
+                                mem_in, mem_out, dnn, nn_idx, reward, done, any_done, nullptr);
 }
 
 int flock_knn(void* stream, int E, int N, int k, float box, float sensor_range, int periodic, int clamp,

@@ -54,11 +54,23 @@ def _check_k(N, k):
         raise RuntimeError("selected index k out of range")
 
 
+def _ext(ring=None, seeds=None, E=0, N=0, k=0, dev=None):
+    """FlockStepExt for the *_ext entry points, or None when there is nothing extra."""
+    if ring is None and seeds is None:
+        return None
+    if seeds is not None:
+        _need(seeds, "seeds", torch.int16, (E, N, k), dev)
+    return _native.FlockStepExt(ring=ctypes.pointer(ring) if ring is not None else None,
+                                seeds=_ptr(seeds) if seeds is not None else None)
+
+
 def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k, box, sensor_range,
-            collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False, ring=None):
+            collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False, ring=None,
+            seeds=None):
     """gym_flock_v2.MultiAgentEnv.step (gym_flock_v2.py:71-83) for E envs; pos/heading updated in place.
     ring (a _native.FlockRing): also write every transition into a replay ring in the same launch
-    (flock_step_v2_store; the store_transitions that follows each step in train_flock.py)."""
+    (flock_step_v2_store; the store_transitions that follows each step in train_flock.py).
+    seeds ([E, N, k] int16, rw, optional): compact kNN search seeds (flock_step_v2_ext; see include/flock_amd.h)."""
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -74,14 +86,15 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
     args = (_stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
             float(v_min), float(v_max), int(bool(periodic)), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading),
             _ptr(action), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
-    if ring is None:
+    ext = _ext(ring, seeds, E, N, k, dev)
+    if ext is None:
         _native.check(_native.lib().flock_step_v2(*args), "flock_step_v2")
     else:
-        _native.check(_native.lib().flock_step_v2_store(*args, ctypes.byref(ring)), "flock_step_v2_store")
+        _native.check(_native.lib().flock_step_v2_ext(*args, ctypes.byref(ext)), "flock_step_v2_ext")
 
 
 def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done, *, k, box,
-            sensor_range, collision_distance, dt=0.1, rigid_boundary=False):
+            sensor_range, collision_distance, dt=0.1, rigid_boundary=False, seeds=None):
     """gym_flock_uw.MultiAgentEnv.step (gym_flock_uw.py:69-81); mem_out = rolled 4-frame observation."""
     E, N, dev = _dims(pos)
     _check_k(N, k)
@@ -98,16 +111,19 @@ def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_id
     _need(reward, "reward", f32, (E, N), dev)
     _need(done, "done", torch.bool, (E, N), dev)
     _need(any_done, "any_done", torch.bool, (E,), dev)
-    rc = _native.lib().flock_step_uw(
-        _stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
-        int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action), _ptr(mem_in),
-        _ptr(mem_out), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
-    _native.check(rc, "flock_step_uw")
+    args = (_stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
+            int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action), _ptr(mem_in),
+            _ptr(mem_out), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
+    ext = _ext(None, seeds, E, N, k, dev)
+    if ext is None:
+        _native.check(_native.lib().flock_step_uw(*args), "flock_step_uw")
+    else:
+        _native.check(_native.lib().flock_step_uw_ext(*args, ctypes.byref(ext)), "flock_step_uw_ext")
 
 
 def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                      status=None, *, k, box, sensor_range, collision_distance, dt=0.1, v_max=2.5, rigid_boundary=False,
-                     noise_std=0.1, seed=0, rng_offset=0):
+                     noise_std=0.1, seed=0, rng_offset=0, seeds=None):
     """gym_flock_uw_discrete.MultiAgentEnv.step (gym_flock_uw_discrete.py:110-122). noise=None → in-kernel
     Philox N(0, noise_std) draws; otherwise noise [E,N,2] is added to the action-table means (parity mode)."""
     E, N, dev = _dims(pos)
@@ -128,16 +144,20 @@ def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, d
     _need(done, "done", torch.bool, (E, N), dev)
     _need(any_done, "any_done", torch.bool, (E,), dev)
     _opt(status, "status", torch.int32, (1,), dev)
-    rc = _native.lib().flock_step_uw_discrete(
-        _stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt), float(v_max),
-        int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action_id), _ptr(noise),
-        float(noise_std), int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(table), int(table.shape[0]),
-        _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done), _ptr(status))
-    _native.check(rc, "flock_step_uw_discrete")
+    args = (_stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
+            float(v_max), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action_id),
+            _ptr(noise), float(noise_std), int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(table),
+            int(table.shape[0]), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done),
+            _ptr(status))
+    ext = _ext(None, seeds, E, N, k, dev)
+    if ext is None:
+        _native.check(_native.lib().flock_step_uw_discrete(*args), "flock_step_uw_discrete")
+    else:
+        _native.check(_native.lib().flock_step_uw_discrete_ext(*args, ctypes.byref(ext)), "flock_step_uw_discrete_ext")
 
 
 def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, *, k, box, collision_distance,
-               dt=0.1, rigid_boundary=False):
+               dt=0.1, rigid_boundary=False, seeds=None):
     """gym_flock.MultiAgentEnv.step (gym_flock.py:48-60); vel is the unit-velocity state (rw)."""
     E, N, dev = _dims(pos)
     _check_k(N, k)
@@ -152,11 +172,14 @@ def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any
     _need(reward, "reward", f32, (E, N), dev)
     _need(done, "done", torch.bool, (E, N), dev)
     _need(any_done, "any_done", torch.bool, (E,), dev)
-    rc = _native.lib().flock_step_flock(
-        _stream(pos), E, N, k, float(box), float(collision_distance), float(dt), int(bool(rigid_boundary)), _ptr(pos),
-        _ptr(vel), _ptr(action), _ptr(mem_in), _ptr(mem_out), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done),
-        _ptr(any_done))
-    _native.check(rc, "flock_step_flock")
+    args = (_stream(pos), E, N, k, float(box), float(collision_distance), float(dt), int(bool(rigid_boundary)),
+            _ptr(pos), _ptr(vel), _ptr(action), _ptr(mem_in), _ptr(mem_out), _ptr(dnn), _ptr(nn_idx), _ptr(reward),
+            _ptr(done), _ptr(any_done))
+    ext = _ext(None, seeds, E, N, k, dev)
+    if ext is None:
+        _native.check(_native.lib().flock_step_flock(*args), "flock_step_flock")
+    else:
+        _native.check(_native.lib().flock_step_flock_ext(*args, ctypes.byref(ext)), "flock_step_flock_ext")
 
 
 def knn(pos, k, box, sensor_range=14.0, periodic=True, clamp=True, dnn=None, nn_idx=None):

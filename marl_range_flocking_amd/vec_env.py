@@ -83,6 +83,9 @@ class VecFlockEnv:
                 mem=z(E, N, 4, k) if has_mem else None,
             ))
         self._cur = 0
+        # compact kNN search seeds for the cell-list path (N >= 128): this step's neighbour indices, read by the
+        # next step (flock_step_*_ext; results never depend on them)
+        self.seeds = z(E, N, k, dtype=torch.int16) if N >= 128 else None
         self.status = z(1, dtype=torch.int32)
         self.valid = z(E, dtype=torch.bool)
         self.table = torch.tensor(ops.UWD_TABLE, dtype=f32, device=dev)
@@ -123,6 +126,8 @@ class VecFlockEnv:
                   rigid_boundary=c.rigid_boundary, max_attempts=c.max_reset_attempts, seed=c.seed,
                   rng_offset=self._rng_offset)
         self._rng_offset += c.max_reset_attempts
+        if self.seeds is not None and b["idx"] is not None:  # the reset's neighbours seed the first step
+            self.seeds.copy_(b["idx"])
         if env_mask is None:
             self.done.zero_()
             self.any_done.zero_()
@@ -167,22 +172,22 @@ class VecFlockEnv:
         if c.variant == "v2":
             ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
                         self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
-                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, **common)
+                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, seeds=self.seeds, **common)
         elif c.variant == "uw":
             ops.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
                         dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, sensor_range=c.sensor_range,
-                        **common)
+                        seeds=self.seeds, **common)
         elif c.variant == "uw_discrete":
             if noise is not None:
                 noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
             ops.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
                                  self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
                                  self.status, sensor_range=c.sensor_range, v_max=c.max_linear_velocity,
-                                 seed=c.seed, rng_offset=self._rng_offset, **common)
+                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, **common)
             self._rng_offset += 1
         else:
             ops.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
-                           self.reward, self.done, self.any_done, **common)
+                           self.reward, self.done, self.any_done, seeds=self.seeds, **common)
         self._cur = nxt
         self.steps += 1
         return self.observation(copy), self.reward, (self.done, self.any_done), {}

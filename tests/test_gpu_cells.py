@@ -108,3 +108,58 @@ def test_cell_list_step_is_bitwise_the_full_scan(variant, periodic, N, k, kind, 
         np.testing.assert_array_equal(a[key], b[key], err_msg=key)
     sample = np.arange(0, E, max(1, E // 6))
     _knn_exact(a["pos"][sample], k, box, 14.0, periodic, variant != "flock", a["dnn"][sample], a["idx"][sample])
+
+
+ROLLOUTS = [("v2", True, 256, 4, "uniform"), ("v2", True, 1024, 4, "uniform"), ("v2", True, 256, 4, "clustered"),
+            ("v2", False, 300, 6, "sparse"), ("uw", False, 256, 4, "edges"), ("uw_discrete", False, 512, 4, "uniform"),
+            ("flock", False, 256, 4, "uniform"), ("v2", True, 500, 15, "uniform")]
+
+
+@pytest.mark.parametrize("variant,periodic,N,k,kind", ROLLOUTS,
+                         ids=[f"{v}-{'per' if p else 'euc'}-N{n}-k{k}-{d}" for v, p, n, k, d in ROLLOUTS])
+def test_seeded_rollout_is_bitwise_the_full_scan(variant, periodic, N, k, kind, cuda):
+    """Multi-step rollouts, where the cell path takes its seeded scan (the previous step's neighbours from the compact
+    seed buffer): every step's outputs equal the full scan's bit for bit, also after the seeds are overwritten with
+    garbage (negative, out-of-range and repeated indices) mid-rollout."""
+    E = 32 if N <= 512 else 8
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(N * 7 + k)
+    pos = _positions(kind, E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    vel = rng.standard_normal((E, N, 2)).astype(np.float32)
+    vel /= np.linalg.norm(vel, axis=-1, keepdims=True)
+    mem = rng.uniform(0, 14, (E, N, 4, k)).astype(np.float32)
+    envs = []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda)
+        env.set_state(positions=pos, headings=head, velocities=vel,
+                      obs_memory=mem if variant in ("uw", "flock") else None)
+        envs.append(env)
+    assert envs[0].seeds is not None
+    for t in range(7):
+        if variant == "uw_discrete":
+            act = torch.from_numpy(rng.integers(0, 10, (E, N)).astype(np.int64))
+            kw = dict(noise=torch.from_numpy((0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)))
+        else:
+            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
+            kw = {}
+        if t == 4:  # garbage seeds: both signs, beyond N, repeats
+            g = rng.integers(-40000, 40000, (E, N, k)).astype(np.int16)
+            g[:, : N // 3] = 3
+            envs[0].seeds.copy_(torch.from_numpy(g))
+        outs = []
+        for i, env in enumerate(envs):
+            if i == 1:
+                os.environ["FLOCK_NO_CELLS"] = "1"
+            try:
+                obs, rew, (done, anyd), _ = env.step(act, **kw)
+                torch.cuda.synchronize()
+            finally:
+                os.environ.pop("FLOCK_NO_CELLS", None)
+            outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
+                         "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd})
+        for key in outs[0]:
+            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+        if t >= 1 and t != 4:  # the seed buffer holds this step's neighbours
+            assert torch.equal(envs[0].seeds.to(torch.int64), envs[0].nn_idx)
