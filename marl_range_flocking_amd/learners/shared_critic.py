@@ -431,8 +431,8 @@ class SharedCriticBench:
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
         # s+1 (which rewrites the ring); in this loop the actions do not come from the actor (random-action
         # exploration), so step s+1 does not depend on learn(s) and every kernel still sees the same data
-        # (single GPU only: with data-parallel replicas the update's all-reduces stay on the main stream)
-        self.overlap = bool(overlap and fused and not dist.active())
+        # (with data-parallel replicas the update's two all-reduces run on the learner stream too)
+        self.overlap = bool(overlap and fused)
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
                                            buffer_size=1_000_000, dist_group=group, fused=fused,
                                            snapshot=self.overlap)

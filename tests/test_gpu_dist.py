@@ -115,3 +115,63 @@ def test_two_ranks_equal_union_batch(kind, cuda):
         # ~0 may flip sign between the two summation orders and move by 2 lr: allow a small fraction of those
         bad = err > 1e-6 + 1e-4 * np.abs(want)
         assert bad.mean() < 0.01, (kind, int(bad.sum()), float(err.max()))
+
+
+def _bench_worker(rank, port, q):
+    """Both config-3 loops (serial, overlapped) on 2 data-parallel ranks (gloo, cuda:0): the overlapped one, whose
+    update and its two all-reduces run on the learner stream, must end bitwise equal to the serial one."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", RANK=str(rank))
+    try:
+        torch.distributed.init_process_group("gloo")
+        from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+        from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
+
+        dev = torch.device("cuda", 0)
+        E, Na = 32, 16
+        states = []
+        for overlap in (False, True):
+            env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
+                                          range_start=(0, 63.0), sensor_range=14.0), device=dev)
+            g = torch.Generator(device=dev).manual_seed(3 + rank)
+            env.positions.copy_(torch.rand(E, Na, 2, device=dev, generator=g) * 63.0)
+            env.headings.copy_(torch.rand(E, Na, device=dev, generator=g) * 4.7)
+            hook = SharedCriticBench(env, device=dev, seed=11, overlap=overlap)
+            assert hook.overlap == overlap and hook.learner.distributed
+            ga = torch.Generator(device=dev).manual_seed(7 + rank)
+            for s in range(6):
+                a = torch.stack([torch.rand(E, Na, device=dev, generator=ga),
+                                 torch.rand(E, Na, device=dev, generator=ga) * 3 - 1.5], -1).contiguous()
+                ring = hook.before(s)
+                env.step(a, ring=ring)
+                hook.after(s, a)
+            hook.finish()
+            torch.cuda.synchronize()
+            L = hook.learner
+            states.append([L.critic.data.cpu().numpy(), L.actors.data.cpu().numpy(), L.losses.cpu().numpy()])
+        q.put((rank, states))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc() + repr(e)))
+
+
+def test_two_ranks_overlapped_bench_loop_equals_serial(cuda):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bench_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(2)], key=lambda o: o[0])
+    for p in ps:
+        p.join(timeout=60)
+    for o in out:
+        assert not isinstance(o[1], str), o
+    for rank, (serial, overlapped) in out:
+        for x, y in zip(serial, overlapped):
+            np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(out[0][1][1][0], out[1][1][1][0])  # replicas identical
