@@ -652,6 +652,34 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         for (int s = 0; s < L - 2; ++s)
             if (s < p.k) prev_obs[s] = po[s];
     }
+    // small-N Euclidean kernels (uw / flock observation memory): the three frames the roll keeps, loaded now so
+    // their latency hides behind the step (only in the !CELL, !PERIODIC instantiation: no register cost elsewhere)
+    constexpr bool kMemEarly = !CELL && !PERIODIC;
+    constexpr int kMemKeep = kMemEarly ? (kMem - 1) * (L - 2) : 1;
+    float mrow[kMemKeep];
+#pragma unroll
+    for (int s = 0; s < kMemKeep; ++s) mrow[s] = 0.0f;
+    float prev_h = 0.0f;  // uw reward: the previous heading (:202-204), loaded early
+    if (active && variant == FLOCK_VARIANT_UW) prev_h = p.prev_heading[a];
+    if (kMemEarly && active && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
+        const float* mi = p.mem_in + a * kMem * p.k;
+        if (L - 2 == 4 && p.k == 4) {  // 3 x float4 (rows are 64-B aligned)
+#pragma unroll
+            for (int f = 0; f < kMem - 1; ++f) {
+                const float4 v = reinterpret_cast<const float4*>(mi)[f];
+                mrow[(f * (L - 2) + 0) % kMemKeep] = v.x;
+                mrow[(f * (L - 2) + 1) % kMemKeep] = v.y;
+                mrow[(f * (L - 2) + 2) % kMemKeep] = v.z;
+                mrow[(f * (L - 2) + 3) % kMemKeep] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int f = 0; f < kMem - 1; ++f)
+#pragma unroll
+                for (int c = 0; c < L - 2; ++c)
+                    if (c < p.k) mrow[(f * (L - 2) + c) % kMemKeep] = mi[f * p.k + c];
+        }
+    }
     if (active) {
         const float2 pp = reinterpret_cast<const float2*>(p.pos)[a];
         x = pp.x;
@@ -949,14 +977,32 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                     if (s <= p.k) sp[s - 1] = (uint16_t)bj[s];
         }
         if (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK) {  // torch.roll + insert (:120-123)
-            const float* mi = p.mem_in + a * kMem * p.k;
             float* mo = p.mem_out + a * kMem * p.k;
-            for (int c = 0; c < p.k; ++c) {
-                for (int s = kMem - 1; s >= 1; --s) mo[s * p.k + c] = mi[(s - 1) * p.k + c];
-            }
+            if (kMemEarly && L - 2 == 4 && p.k == 4) {  // the prefetched frames, 4 x float4 stores
+                float4* mo4 = reinterpret_cast<float4*>(mo);
+                mo4[0] = make_float4(dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]);
 #pragma unroll
-            for (int s = 0; s < L - 2; ++s)
-                if (s < p.k) mo[s] = dv[s];
+                for (int f = 0; f < kMem - 1; ++f)
+                    mo4[f + 1] = make_float4(mrow[(f * (L - 2)) % kMemKeep], mrow[(f * (L - 2) + 1) % kMemKeep],
+                                             mrow[(f * (L - 2) + 2) % kMemKeep], mrow[(f * (L - 2) + 3) % kMemKeep]);
+            } else if (kMemEarly) {
+#pragma unroll
+                for (int f = 0; f < kMem - 1; ++f)
+#pragma unroll
+                    for (int c = 0; c < L - 2; ++c)
+                        if (c < p.k) mo[(f + 1) * p.k + c] = mrow[(f * (L - 2) + c) % kMemKeep];
+#pragma unroll
+                for (int s = 0; s < L - 2; ++s)
+                    if (s < p.k) mo[s] = dv[s];
+            } else {
+                const float* mi = p.mem_in + a * kMem * p.k;
+                for (int c = 0; c < p.k; ++c) {
+                    for (int s = kMem - 1; s >= 1; --s) mo[s * p.k + c] = mi[(s - 1) * p.k + c];
+                }
+#pragma unroll
+                for (int s = 0; s < L - 2; ++s)
+                    if (s < p.k) mo[s] = dv[s];
+            }
         }
         if (variant != kSense) {
             p.done[a] = (uint8_t)coll;
@@ -965,7 +1011,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
                 const float dist = sqrt_rn(__fadd_rn(__fmul_rn(com_x, com_x), __fmul_rn(com_y, com_y)));
                 const float com = (dist < p.com_r) ? 0.01f : 0.0f;                  // :197
-                const float prev = p.prev_heading[a];
+                const float prev = prev_h;
                 const float angp = (fabsf(__fsub_rn(prev, h)) > 0.27f) ? -0.01f : 0.001f;  // :202-204
                 p.prev_heading[a] = h;
                 r = __fadd_rn(__fadd_rn(coll ? -5.0f : 0.01f, com), angp);          // :220

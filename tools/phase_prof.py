@@ -56,6 +56,10 @@ def run(E, N, k, steps, variant="v2"):
     gd.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 5 + [ctypes.c_int] + \
         [ctypes.c_void_p] * 5 + [ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int] + \
         [ctypes.c_void_p] * 7
+    gu = lib.flock_step_uw
+    gu.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 4 + [ctypes.c_int] + \
+        [ctypes.c_void_p] * 12
+    mem = torch.zeros(E, N, 4, k, device=dev)
     aid = torch.randint(0, 10, (E, N), device=dev, generator=g)
     table = torch.rand(10, 2, device=dev, generator=g)
     prev = torch.zeros(E, N, device=dev)
@@ -65,6 +69,10 @@ def run(E, N, k, steps, variant="v2"):
             rc = f(stream, E, N, k, box, 14.0, 2.5, 0.1, 0.0, 2.5, 1, 0, pos.data_ptr(), head.data_ptr(),
                    act.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(), rew.data_ptr(), done.data_ptr(),
                    anyd.data_ptr())
+        elif variant == "uw":
+            rc = gu(stream, E, N, k, box, 14.0, 2.5, 0.1, 0, pos.data_ptr(), head.data_ptr(), prev.data_ptr(),
+                    act.data_ptr(), mem.data_ptr(), mem.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(),
+                    rew.data_ptr(), done.data_ptr(), anyd.data_ptr())
         else:
             rc = gd(stream, E, N, k, box, 14.0, 2.5, 0.1, 2.5, 0, pos.data_ptr(), head.data_ptr(), prev.data_ptr(),
                     aid.data_ptr(), None, 0.1, 7, 0, table.data_ptr(), 10, vel.data_ptr(), dnn.data_ptr(),
@@ -101,7 +109,7 @@ if __name__ == "__main__":
     ap.add_argument("--N", type=int, default=256)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--variant", default="v2", choices=["v2", "uwd"])
+    ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uwd"])
     a = ap.parse_args()
     if a.build:
         build()
