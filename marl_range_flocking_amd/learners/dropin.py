@@ -9,6 +9,7 @@ VDN QNet keys ``agent_feature_{i}.0.weight`` ...), written and read with torch.s
 """
 import json
 import os
+import random
 import time
 
 import numpy as np
@@ -99,6 +100,7 @@ class SuperAgent:
         rnn = self.recurrent
         self.learner = MADDPGLearner(
             self.n_agents, k, recurrent=rnn, n_actions=env.action_space[0].shape[0],
+            hidden1=getattr(args, "hidden1", 400), hidden2=getattr(args, "hidden2", 300),
             batch_size=getattr(args, "batch_size", 128), chunk_size=10,
             buffer_capacity=getattr(args, "buffer_size", 1_000_000) if rnn else 1_000_000,
             min_size_buffer=getattr(args, "min_size_buffer", 8_000) if rnn else 8_000,
@@ -142,9 +144,19 @@ class SuperAgent:
                 sds[f"{net}{i}"] = torch.load(self._ckpt(i, net), weights_only=True)
         self.learner.load_reference_state(sds)
 
+    def load_replay_buffer(self):
+        """MADDPG.py:56-58: the replay saved by save() under path_load."""
+        self.replay_buffer.load(self.path_load)
+
     def load_single_checkpoint(self, path):
         sd = torch.load(path, weights_only=True)
         self.learner.load_reference_state({f"actor{i}": sd for i in range(self.n_agents)})
+
+    def load_scaled_checkpoint(self, ch_path, total=5):
+        """MADDPG.py:67-76: every agent takes the actor of a random saved agent (randint is inclusive)."""
+        self.learner.load_reference_state({
+            f"actor{i}": torch.load(os.path.join(ch_path, f"agent_number_{random.randint(0, total)}_actor_ddpg.pt"),
+                                    weights_only=True) for i in range(self.n_agents)})
 
 
 class SuperAgentFF(SuperAgent):
@@ -302,7 +314,7 @@ class Agent:
         self.critic = self.target_critic = shared_critic
         self.alpha, self.gamma, self.tau, self.batch_size, self.update_rate = alpha, gamma, tau, batch_size, update_rate
         self.index, self.memory, self.noise = index, replay_buffer, noise
-        self.checkpoint_dir = checkpoint_dir
+        self.checkpoint_dir, self.checkpoint_best = checkpoint_dir, checkpoint_best
         shared_critic.agents.append(self)
 
     def choose_action(self, observation):
@@ -317,10 +329,24 @@ class Agent:
     def learn(self):
         return self.critic._build().learn(self.index)
 
-    def save_models(self):
+    def _files(self, best):
+        d = self.checkpoint_best if best else self.checkpoint_dir
+        return [os.path.join(d, f"{n}_ddpg.pt") for n in ("Actor", "TargetActor", "Critic")]
+
+    def save_models(self, best=False):
+        """train_flock.py:143 (every 300 s) / :151 (save_models_best); agent_simple.py:200-210 file naming."""
         L = self.critic._build()
-        os.makedirs(self.checkpoint_dir, exist_ok=True)
-        torch.save(L.actor_state_dict(self.index), os.path.join(self.checkpoint_dir, "Actor_ddpg.pt"))
-        torch.save(L.actor_state_dict(self.index, target=True),
-                   os.path.join(self.checkpoint_dir, "TargetActor_ddpg.pt"))
-        torch.save(L.critic_state_dict(), os.path.join(self.checkpoint_dir, "Critic_ddpg.pt"))
+        files = self._files(best)
+        os.makedirs(os.path.dirname(files[0]), exist_ok=True)
+        for f, sd in zip(files, (L.actor_state_dict(self.index), L.actor_state_dict(self.index, target=True),
+                                 L.critic_state_dict())):
+            torch.save(sd, f)
+
+    def save_models_best(self):
+        self.save_models(best=True)
+
+    def load_models(self, silent=False, best=False):
+        """agent_simple.py:212-216: this agent's actor + target actor, and the shared critic."""
+        L = self.critic._build()
+        actor, target, critic = (torch.load(f, weights_only=True) for f in self._files(best))
+        L.load_reference_state(critic, {self.index: actor}, {self.index: target})

@@ -404,15 +404,13 @@ class SharedCriticLearner:
 
     # ------------------------------------------------------------------ state dicts (reference key names)
     def load_reference_state(self, critic_sd, actor_sds, target_actor_sds=None):
+        """actor_sds / target_actor_sds: a list over agents, or {agent index: state_dict} for a subset."""
         for n, v in critic_sd.items():
             self.critic.load(n, v, agent=0)
-        for i, sd in enumerate(actor_sds):
-            for n, v in sd.items():
-                self.actors.load(n, v, agent=i)
-        if target_actor_sds is not None:
-            for i, sd in enumerate(target_actor_sds):
+        for sds, target in ((actor_sds, False), (target_actor_sds, True)):
+            for i, sd in (sds.items() if isinstance(sds, dict) else enumerate(sds or ())):
                 for n, v in sd.items():
-                    self.actors.load(n, v, agent=i, target=True)
+                    self.actors.load(n, v, agent=i, target=target)
 
     def critic_state_dict(self):
         return {n: self.critic.export(n, 0).cpu() for n in self.critic.shapes}
