@@ -44,7 +44,9 @@ def _super_agent(flavour, m, tmp, cuda):
                                  buffer_size=m["capacity"], min_size_buffer=m["batch"], hidden1=m["hidden1"],
                                  hidden2=m["hidden2"], save_dir=os.path.join(tmp, "ckpt"))
     cls = SuperAgent if flavour == "rnn" else SuperAgentFF
-    return cls(args, env, path_save=tmp, path_load=tmp)
+    agent = cls(args, env, path_save=tmp, path_load=tmp)
+    agent.learner.min_size_buffer = m["batch"]  # the feed-forward SuperAgent hard-codes 8000 (memory.py)
+    return agent
 
 
 def _assert_same_learner(a, b, N):
@@ -83,7 +85,7 @@ def test_maddpg_checkpoint_files_round_trip(flavour, tmp_path, cuda):
                 assert v.dtype == torch.float32 and tuple(v.shape) == gold[n].shape
                 assert torch.equal(v, mine[n])
     (folder,) = glob.glob(os.path.join(tmp, "save_agent_*"))
-    cap, k = m["capacity"], m["k"]
+    cap, k = a.replay_buffer.buffer_capacity, m["k"]  # ff: memory.py:12 fixes 1e6 rows
     shapes = {"states": (cap, N, k), "next_states": (cap, N, k), "rewards": (cap, N, 1), "dones": (cap, N, 1)}
     for i in range(N):
         shapes.update({f"states_actor_{i}": (cap, k), f"next_states_actor_{i}": (cap, k),
@@ -110,7 +112,8 @@ def test_maddpg_checkpoint_files_round_trip(flavour, tmp_path, cuda):
     # the Adam moments are not part of the reference checkpoint: copy a's, then train both once more
     for pa, pb in ((a.learner.actors, b.learner.actors), (a.learner.critics, b.learner.critics)):
         for name in ("exp_avg", "exp_avg_sq", "step_dev"):
-            getattr(pb, name).copy_(getattr(pa, name))
+            if getattr(pa, name) is not None:  # the frozen MADDPG actors carry no Adam state
+                getattr(pb, name).copy_(getattr(pa, name))
         pb.step_count, pb.agent_steps = pa.step_count, list(pa.agent_steps)
     a.learner.train(starts=z["starts"])
     b.learner.train(starts=z["starts"])
