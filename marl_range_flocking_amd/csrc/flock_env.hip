@@ -577,8 +577,33 @@ __device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N,
 // ---------------------------------------------------------------------------------------------------------------
 // the fused step kernel
 
-template <int L, bool PERIODIC, bool CELL>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params p) {
+constexpr int clog2c(int n) {
+    int b = 0;
+    while ((1 << b) < n) ++b;
+    return b;
+}
+
+// VAR >= 0, NC > 0: an instantiation specialised on the variant, N (k = L - 2) and the cell grid (GXC x GYC) of one
+// hot configuration. The launch's Params copy gets those fields as compile-time constants, so the variant branches,
+// the env/lane split (t / N), the LDS carve-up and every trip count that depends on them fold away (fewer SGPRs
+// live across the kernel). Same code, same results as the generic instantiation.
+template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params pin) {
+    Params p = pin;
+    if (VAR >= 0) p.variant = VAR;
+    if (NC > 0) {  // make_cfg / dispatch values for N = NC
+        p.N = NC;
+        p.k = L - 2;
+        p.G = NC <= 256 ? 256 / NC : 1;
+        p.S = (NC + 1) & ~1;
+        p.P = 1 << clog2c(NC);
+        p.ib = clog2c(NC) < 1 ? 1 : clog2c(NC);
+        if (CELL) {
+            p.gx = GXC;
+            p.gy = GYC;
+            p.ecap = 2 * NC + 2;
+        }
+    }
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float2* lpos = reinterpret_cast<float2*>(smem);               // [G][S]
     float* red = reinterpret_cast<float*>(lpos + p.G * p.S);      // [G][2][P]
@@ -1201,8 +1226,25 @@ int check_common(int E, int N, int k) {
     return FLOCK_OK;
 }
 
+// the specialised instantiations (step_kernel VAR / NC): the BASELINE configurations' per-GPU shapes
+template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC>
+bool launch_spec(const Cfg& c, const Params& p, hipStream_t s) {
+    if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL)
+        return false;
+    if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
+    if (getenv("FLOCK_NO_SPEC")) return false;  // A/B diagnostics: the generic instantiation
+    hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+    return true;
+}
+
 template <int L>
 void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
+    if constexpr (L == 6) {
+        if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6>(c, p, s)) return;         // config 3
+        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12>(c, p, s)) return;       // config 5
+        if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
+        if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0>(c, p, s)) return;          // config 2
+    }
     if (p.cells) {
         if (p.periodic)
             hipLaunchKernelGGL((step_kernel<L, true, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);

@@ -163,3 +163,49 @@ def test_seeded_rollout_is_bitwise_the_full_scan(variant, periodic, N, k, kind, 
             assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
         if t >= 1 and t != 4:  # the seed buffer holds this step's neighbours
             assert torch.equal(envs[0].seeds.to(torch.int64), envs[0].nn_idx)
+
+
+SPEC = [("v2", True, 256, "uniform"), ("v2", True, 1024, "clustered"), ("uw_discrete", False, 512, "edges"),
+        ("uw", False, 64, "uniform")]
+
+
+@pytest.mark.parametrize("variant,periodic,N,kind", SPEC, ids=[f"{v}-N{n}-{d}" for v, _, n, d in SPEC])
+def test_specialised_kernel_is_bitwise_the_generic_one(variant, periodic, N, kind, cuda):
+    """The BASELINE configurations' shapes launch step_kernel instantiations specialised on (variant, N, k = 4, cell
+    grid); FLOCK_NO_SPEC=1 launches the generic instantiation. Four-step rollouts agree bit for bit on every output,
+    the observation memory and the seed buffer."""
+    k, E = 4, (16 if N >= 512 else 64)
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(N + 5)
+    pos = _positions(kind, E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    mem = rng.uniform(0, 14, (E, N, 4, k)).astype(np.float32)
+    envs = []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda)
+        env.set_state(positions=pos, headings=head, obs_memory=mem if variant == "uw" else None)
+        envs.append(env)
+    for t in range(4):
+        if variant == "uw_discrete":
+            act = torch.from_numpy(rng.integers(0, 4, (E, N)).astype(np.int64))
+            kw = dict(noise=torch.from_numpy((0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)))
+        else:
+            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
+            kw = {}
+        outs = []
+        for i, env in enumerate(envs):
+            if i == 1:
+                os.environ["FLOCK_NO_SPEC"] = "1"
+            try:
+                obs, rew, (done, anyd), _ = env.step(act, **kw)
+                torch.cuda.synchronize()
+            finally:
+                os.environ.pop("FLOCK_NO_SPEC", None)
+            o = obs["actors"] if isinstance(obs, dict) else obs
+            outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
+                         "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd, "obs": o.clone()})
+            if env.seeds is not None:
+                outs[-1]["seeds"] = env.seeds.clone()
+        for key in outs[0]:
+            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
