@@ -215,6 +215,31 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 // pair_d2 of two candidates at once: the squares and sums as packed f32 ops (v_pk_mul / v_pk_add, one candidate
 // per half; each half rounds exactly like the scalar mul, mul, add), so both packed issue slots do useful work.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// Accessors of the step kernel's per-agent streams (state in, state / observation / replay record out). Plain
+// accesses by default; -DFLOCK_NT makes them non-temporal (measured: the env kernel 51.4 -> 52.2 us and the
+// overlapped config-3 step 159.5 -> 162.5 us, so keeping the streams out of L2 does not help the co-running update).
+#ifdef FLOCK_NT
+template <typename T>
+__device__ __forceinline__ T ldnt(const T* p) {
+    return __builtin_nontemporal_load(p);
+}
+template <typename T>
+__device__ __forceinline__ void stnt(T* p, T v) {
+    __builtin_nontemporal_store(v, p);
+}
+#else
+template <typename T>
+__device__ __forceinline__ T ldnt(const T* p) {
+    return *p;
+}
+template <typename T>
+__device__ __forceinline__ void stnt(T* p, T v) {
+    *p = v;
+}
+#endif
 template <bool PERIODIC>
 __device__ __forceinline__ f32x2 pair_d2x2(float xi, float yi, float x0, float y0, float x1, float y1, float box) {
     float dx0 = __fsub_rn(xi, x0), dx1 = __fsub_rn(xi, x1);
@@ -652,31 +677,48 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     const bool has_hint = CELL && active && (p.seeds != nullptr || p.idx != nullptr);
 #pragma unroll
     for (int s = 0; s < L - 2; ++s) hint[s] = -1;
-    if (has_hint && p.seeds) {
-        const uint16_t* hp = p.seeds + a * p.k;
-        if (L - 2 == 4 && p.k == 4) {  // one 8-B load (a * k u16 is 8-B aligned)
-            const uint2 v = *reinterpret_cast<const uint2*>(hp);
-            hint[0] = v.x & 0xFFFFu;
-            hint[1] = v.x >> 16;
-            hint[2 % (L - 2)] = v.y & 0xFFFFu;
-            hint[3 % (L - 2)] = v.y >> 16;
-        } else {
+    // k = 4 seeds: one 8-B load (a * k u16 is 8-B aligned), unpacked only at the seeded scan
+    const bool seed_packed = has_hint && p.seeds && L - 2 == 4 && p.k == 4;
+    uint2 seed_raw = make_uint2(0u, 0u);
+    // the inputs needed only after phase 1 (seeds, the previous observation of the fused insert) are loaded after
+    // the kinematics inputs, so that at kernel start, when every resident block loads at once, the loads the
+    // kinematics waits on are not queued behind them
+    auto load_late = [&]() {
+        if (seed_packed) {
+            const u32x2 sv = ldnt(reinterpret_cast<const u32x2*>(p.seeds + a * p.k));
+            seed_raw = make_uint2(sv.x, sv.y);
+        } else if (has_hint && p.seeds) {
+            const uint16_t* hp = p.seeds + a * p.k;
+#pragma unroll
+            for (int s = 0; s < L - 2; ++s)
+                if (s < p.k) hint[s] = hp[s];
+        } else if (has_hint) {
+            const int64_t* hp = p.idx + a * p.k;
 #pragma unroll
             for (int s = 0; s < L - 2; ++s)
                 if (s < p.k) hint[s] = hp[s];
         }
-    } else if (has_hint) {
-        const int64_t* hp = p.idx + a * p.k;
+        if (active && p.r_state && r_unit >= p.r_skip) {
+            const float* po = p.r_prev + a * p.k;
+            if (L - 2 == 4 && p.k == 4) {  // one 16-B load (rows of 4 floats are 16-B aligned)
+                const f32x4 v = ldnt(reinterpret_cast<const f32x4*>(po));
+                prev_obs[0] = v.x;
+                prev_obs[1 % (L - 2)] = v.y;
+                prev_obs[2 % (L - 2)] = v.z;
+                prev_obs[3 % (L - 2)] = v.w;
+            } else {
 #pragma unroll
-        for (int s = 0; s < L - 2; ++s)
-            if (s < p.k) hint[s] = hp[s];
-    }
-    if (active && p.r_state && r_unit >= p.r_skip) {
-        const float* po = p.r_prev + a * p.k;
-#pragma unroll
-        for (int s = 0; s < L - 2; ++s)
-            if (s < p.k) prev_obs[s] = po[s];
-    }
+                for (int s = 0; s < L - 2; ++s)
+                    if (s < p.k) prev_obs[s] = po[s];
+            }
+        }
+    };
+#ifndef FLOCK_LOAD_LATE_FIRST
+    constexpr bool kLateAfter = true;
+#else
+    constexpr bool kLateAfter = false;
+#endif
+    if (!kLateAfter) load_late();
     // small-N Euclidean kernels (uw / flock observation memory): the three frames the roll keeps, loaded now so
     // their latency hides behind the step (only in the !CELL, !PERIODIC instantiation: no register cost elsewhere)
     constexpr bool kMemEarly = !CELL && !PERIODIC;
@@ -706,14 +748,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
     }
     if (active) {
-        const float2 pp = reinterpret_cast<const float2*>(p.pos)[a];
+        const f32x2 pp = ldnt(reinterpret_cast<const f32x2*>(p.pos) + a);
         x = pp.x;
         y = pp.y;
         if (variant == FLOCK_VARIANT_V2) {  // gym_flock_v2.py:317-350 (heading=True)
-            const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
-            act_in = ac;
+            const f32x2 ac = ldnt(reinterpret_cast<const f32x2*>(p.action) + a);
+            act_in = make_float2(ac.x, ac.y);
             const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
-            h = __fadd_rn(p.heading[a], __fmul_rn(ang, p.dt));               // :329
+            h = __fadd_rn(ldnt(p.heading + a), __fmul_rn(ang, p.dt));        // :329
             const float lin = clamp_t(ac.x, p.v_min, p.v_max);               // :331
             float sn, cs;
             sincosf(h, &sn, &cs);                                            // ocml: the sinf / cosf bits
@@ -723,8 +765,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             vy = __fmul_rn(nan_to_num(vy), p.dt);
             x = __fadd_rn(x, vx);                                            // :350
             y = __fadd_rn(y, vy);
-            p.heading[a] = h;
-            reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
+            stnt(p.heading + a, h);
+            stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
         } else if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:269-302 (heading=False)
             const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
             const float n = sqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
@@ -784,10 +826,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (variant != kSense) {
             x = boundary(x, p.box, p.rigid);  // check_boundary :271-304
             y = boundary(y, p.box, p.rigid);
-            reinterpret_cast<float2*>(p.pos)[a] = make_float2(x, y);
+            stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
         }
         lpos[g * p.S + i] = make_float2(x, y);
     }
+    if (kLateAfter) load_late();
 
     PHASE(0);
     // ---- phase 2: per-env sums in a fixed tree order (same order as oracle tree_sum) -------------------------
@@ -899,6 +942,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         bool use = false;
         float r = 0.0f;
         bool seeds_ok = has_hint;
+        if (seed_packed) {
+            hint[0] = seed_raw.x & 0xFFFFu;
+            hint[1 % (L - 2)] = seed_raw.x >> 16;
+            hint[2 % (L - 2)] = seed_raw.y & 0xFFFFu;
+            hint[3 % (L - 2)] = seed_raw.y >> 16;
+        }
         int seed[L - 2];
 #pragma unroll
         for (int s = 0; s < L - 2; ++s) {
@@ -987,15 +1036,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);  // gym_flock_v2.py:151
                 dv[s - 1] = d;
                 coll |= (d < p.cd);                                   // :212-215
-                p.dnn[a * p.k + (s - 1)] = d;
+                if (!(L - 2 == 4 && p.k == 4)) p.dnn[a * p.k + (s - 1)] = d;
                 if (p.idx) p.idx[a * p.k + (s - 1)] = (int64_t)bj[s];
             }
         }
+        if (L - 2 == 4 && p.k == 4)  // one 16-B store
+            stnt(reinterpret_cast<f32x4*>(p.dnn + a * p.k), f32x4{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]});
         if (CELL && p.seeds) {  // this step's neighbours: the next step's search seeds
             uint16_t* sp = p.seeds + a * p.k;
             if (L - 2 == 4 && p.k == 4)
-                *reinterpret_cast<uint2*>(sp) = make_uint2((uint32_t)bj[1] | ((uint32_t)bj[2 % (L - 1)] << 16),
-                                                           (uint32_t)bj[3 % (L - 1)] | ((uint32_t)bj[4 % (L - 1)] << 16));
+                stnt(reinterpret_cast<u32x2*>(sp), u32x2{(uint32_t)bj[1] | ((uint32_t)bj[2 % (L - 1)] << 16),
+                                                         (uint32_t)bj[3 % (L - 1)] | ((uint32_t)bj[4 % (L - 1)] << 16)});
             else
 #pragma unroll
                 for (int s = 1; s < L - 1; ++s)
@@ -1030,7 +1081,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             }
         }
         if (variant != kSense) {
-            p.done[a] = (uint8_t)coll;
+            stnt(p.done + a, (uint8_t)coll);
             float r;
             if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:206-221
                 const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
@@ -1048,22 +1099,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             } else {
                 r = coll ? -5.0f : 0.01f;  // gym_flock_v2.py:217-220, gym_flock.py:142-145
             }
-            p.reward[a] = r;
+            stnt(p.reward + a, r);
             if (p.r_state && r_unit >= p.r_skip) {  // fused replay insert: row (start + unit - skip) mod cap
                 int64_t row = p.r_start + r_unit - p.r_skip;
                 if (row >= p.r_cap) row -= p.r_cap;
                 const int64_t e = row * p.r_group + r_slot;  // this agent's element of the row
+                if (L - 2 == 4 && p.k == 4 && !p.r_astate && !p.r_anew) {  // 16-B stores
+                    stnt(reinterpret_cast<f32x4*>(p.r_state + e * p.k),
+                         f32x4{prev_obs[0], prev_obs[1 % (L - 2)], prev_obs[2 % (L - 2)], prev_obs[3 % (L - 2)]});
+                    stnt(reinterpret_cast<f32x4*>(p.r_new + e * p.k),
+                         f32x4{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]});
+                } else {
 #pragma unroll
-                for (int s = 0; s < L - 2; ++s)
-                    if (s < p.k) {
-                        p.r_state[e * p.k + s] = prev_obs[s];
-                        p.r_new[e * p.k + s] = dv[s];
-                        if (p.r_astate) p.r_astate[e * p.k + s] = prev_obs[s];
-                        if (p.r_anew) p.r_anew[e * p.k + s] = dv[s];
-                    }
-                reinterpret_cast<float2*>(p.r_action)[e] = act_in;
-                p.r_reward[e] = r;
-                p.r_term[e] = (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f;
+                    for (int s = 0; s < L - 2; ++s)
+                        if (s < p.k) {
+                            p.r_state[e * p.k + s] = prev_obs[s];
+                            p.r_new[e * p.k + s] = dv[s];
+                            if (p.r_astate) p.r_astate[e * p.k + s] = prev_obs[s];
+                            if (p.r_anew) p.r_anew[e * p.k + s] = dv[s];
+                        }
+                }
+                stnt(reinterpret_cast<f32x2*>(p.r_action) + e, f32x2{act_in.x, act_in.y});
+                stnt(p.r_reward + e, r);
+                stnt(p.r_term + e, (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f);
             }
         }
     }

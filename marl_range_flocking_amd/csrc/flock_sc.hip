@@ -724,6 +724,67 @@ __device__ __forceinline__ void load_panel(float* __restrict__ P, const float* _
     }
 }
 
+// Split panel load for the vectorised layouts (V = 0, 1: one round of at most 16 float4 per thread, kc <= 512):
+// panel_fetch issues the global loads into registers, panel_store writes them to LDS. gemm_tile fetches the A and
+// B panels of a chunk together (one memory round trip instead of two) and the next chunk's panels before the
+// current chunk's MFMAs.
+template <int V>
+__device__ __forceinline__ void panel_fetch(float4 (&v)[16], const float* __restrict__ X, int R, int Kd, int sr,
+                                            int sk, int r0, int k0, int kc) {
+    const int tid = threadIdx.x;
+    if (V == 0) {
+        const int q = kc >> 2, items = 32 * q;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int t = tid + 256 * i;
+            const int rr = t / q, k = k0 + 4 * (t - rr * q), rw = r0 + rr;
+            v[i] = (t < items && rw < R && k < Kd) ? *reinterpret_cast<const float4*>(X + (int64_t)rw * sr + k)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    } else {
+        const int items = 8 * kc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int t = tid + 256 * i;
+            const int kk = t >> 3, rr = 4 * (t & 7), k = k0 + kk, rw = r0 + rr;
+            v[i] = (t < items && rw < R && k < Kd) ? *reinterpret_cast<const float4*>(X + (int64_t)k * sk + rw)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+}
+template <int V>
+__device__ __forceinline__ void panel_store(float* __restrict__ P, const float4 (&v)[16], int kc) {
+    const int tid = threadIdx.x;
+    if (V == 0) {
+        const int q = kc >> 2, items = 32 * q;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int t = tid + 256 * i;
+            if (t < items) {
+                const int rr = t / q, kk = 4 * (t - rr * q);
+                P[(kk + 0) * kPitch + rr] = v[i].x;
+                P[(kk + 1) * kPitch + rr] = v[i].y;
+                P[(kk + 2) * kPitch + rr] = v[i].z;
+                P[(kk + 3) * kPitch + rr] = v[i].w;
+            }
+        }
+    } else {
+        const int items = 8 * kc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int t = tid + 256 * i;
+            if (t < items) {
+                const int kk = t >> 3, rr = 4 * (t & 7);
+                float* d = P + kk * kPitch + rr;
+                d[0] = v[i].x;
+                d[1] = v[i].y;
+                d[2] = v[i].z;
+                d[3] = v[i].w;
+            }
+        }
+    }
+}
+
 // the 4 outputs of thread (wave w, lane l): rows 8w + 4(l >> 5) + q (q < 4), column l & 31
 template <int AV, int BV>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
@@ -736,17 +797,41 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
     f32x16 acc;
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
-    for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
-        const int kc = gemm_kc(g.K - k0, g.kchunk);
-        load_panel<AV>(As, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k0, kc);
-        load_panel<BV>(Bs, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k0, kc);
-        __syncthreads();
-        const int kq = kc >> 2;  // multiple of 2
-        const float* a = As + (wv * kq + (l >> 5)) * kPitch + (l & 31);
-        const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
-        for (int kk = 0; kk < kq; kk += 2)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk * kPitch], b[kk * kPitch], acc, 0, 0, 0);
-        __syncthreads();
+    if constexpr (AV != 2 && BV != 2) {
+        float4 va[16], vb[16];
+        int kc = gemm_kc(g.K, g.kchunk);
+        panel_fetch<AV>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
+        panel_fetch<BV>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, 0, kc);
+        for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
+            panel_store<AV>(As, va, kc);
+            panel_store<BV>(Bs, vb, kc);
+            __syncthreads();
+            const int k1 = k0 + g.kchunk, kc1 = k1 < g.K ? gemm_kc(g.K - k1, g.kchunk) : 0;
+            if (k1 < g.K) {  // the next chunk's loads fly during this chunk's MFMAs
+                panel_fetch<AV>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
+                panel_fetch<BV>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k1, kc1);
+            }
+            const int kq = kc >> 2;  // multiple of 2
+            const float* a = As + (wv * kq + (l >> 5)) * kPitch + (l & 31);
+            const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
+            for (int kk = 0; kk < kq; kk += 2)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk * kPitch], b[kk * kPitch], acc, 0, 0, 0);
+            __syncthreads();
+            kc = kc1;
+        }
+    } else {
+        for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
+            const int kc = gemm_kc(g.K - k0, g.kchunk);
+            load_panel<AV>(As, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k0, kc);
+            load_panel<BV>(Bs, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k0, kc);
+            __syncthreads();
+            const int kq = kc >> 2;  // multiple of 2
+            const float* a = As + (wv * kq + (l >> 5)) * kPitch + (l & 31);
+            const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
+            for (int kk = 0; kk < kq; kk += 2)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk * kPitch], b[kk * kPitch], acc, 0, 0, 0);
+            __syncthreads();
+        }
     }
 #pragma unroll
     for (int v = 0; v < 16; ++v) red[(wv * 16 + v) * 64 + l] = acc[v];

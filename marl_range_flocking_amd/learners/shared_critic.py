@@ -21,6 +21,8 @@ learn() has two implementations with the same semantics:
 import ctypes
 import math
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -435,7 +437,10 @@ class SharedCriticBench:
                                            buffer_size=1_000_000, dist_group=group, fused=fused,
                                            snapshot=self.overlap)
         if self.overlap:
-            self.stream = torch.cuda.Stream(device=device)
+            # high priority: when the env kernel holds every CU slot, the update's blocks are dispatched first as
+            # env blocks retire, so the update chain (the step's critical path) is not stretched by the env step
+            prio = 0 if os.environ.get("FLOCK_LEARNER_PRIORITY") == "0" else torch.cuda.Stream.priority_range()[1]
+            self.stream = torch.cuda.Stream(device=device, priority=prio)
             self.snap_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.learn_done = [torch.cuda.Event(), torch.cuda.Event()]
             self._used = [False, False]
