@@ -401,15 +401,22 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
         atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 22], 1ull);
     }
 #endif
-#pragma unroll 1
-    for (int t = 0; t < slots; t += 2) {
-        int c0 = t + b[0], c1 = t + 1 + b[0];
+    auto cand_index = [&](int tt, int& c0, int& c1) {
+        c0 = tt + b[0];
+        c1 = tt + 1 + b[0];
 #pragma unroll
         for (int u = 1; u < kRows; ++u) {
-            c0 = (t >= P[u]) ? t + b[u] : c0;
-            c1 = (t + 1 >= P[u]) ? t + 1 + b[u] : c1;
+            c0 = (tt >= P[u]) ? tt + b[u] : c0;
+            c1 = (tt + 1 >= P[u]) ? tt + 1 + b[u] : c1;
         }
-        const float4 q0 = ext[min(c0, cmax)], q1 = ext[min(c1, cmax)];
+        c0 = min(c0, cmax);
+        c1 = min(c1, cmax);
+    };
+#pragma unroll 1
+    for (int t = 0; t < slots; t += 2) {
+        int c0, c1;
+        cand_index(t, c0, c1);
+        const float4 q0 = ext[c0], q1 = ext[c1];
         const f32x2 d = cand_d2x2<PERIODIC>(xi, yi, box, q0, q1);
         const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
         const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
@@ -656,6 +663,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     for (int q_ = 0; q_ < 24; ++q_) ph_acc[q_] = 0;
     unsigned long long t_prev = __builtin_amdgcn_s_memtime();
     PHASE_COUNT(20, 1);
+#endif
+#ifdef FLOCK_STAGGER  // diagnostics: offset the phases of the first-round blocks sharing a CU (b, b + 256, ...)
+    if (blockIdx.x < 2048) {
+        const int m = (blockIdx.x >> 8) & 7;
+        for (int q = 0; q < m * FLOCK_STAGGER; ++q) __builtin_amdgcn_s_sleep(1);
+    }
 #endif
     if (in_group && i == 0) flags[g] = 0;
     if (t == 0) flags[p.G] = 0;  // arrival counter of the G = 1 any_done (published by the phase-2 barrier)

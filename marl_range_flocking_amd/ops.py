@@ -64,13 +64,60 @@ def _ext(ring=None, seeds=None, E=0, N=0, k=0, dev=None):
                                 seeds=_ptr(seeds) if seeds is not None else None)
 
 
+class StepPlan:
+    """A validated step launch over fixed buffers (VecFlockEnv allocates its state once, so every call with the
+    same buffer parity passes the same pointers). The first call through a plan checks every tensor and records
+    the argument tuple; later calls check only the per-call action tensor and substitute the stream, the action
+    pointer, dt and (uw_discrete) the RNG offset: the Python cost of a step drops to about one ctypes call."""
+
+    __slots__ = ("fn", "name", "args", "ext", "i_action", "i_dt", "i_rng")
+
+    def __init__(self):
+        self.fn = None
+
+    def record(self, fn, name, args, ext, i_action, i_dt, i_rng=None):
+        self.fn, self.name, self.args, self.ext = fn, name, list(args), ext
+        self.i_action, self.i_dt, self.i_rng = i_action, i_dt, i_rng
+
+    def launch(self, stream, action, dt, rng_offset=None):
+        a = self.args
+        a[0] = stream
+        a[self.i_action] = ctypes.c_void_p(action.data_ptr())
+        a[self.i_dt] = float(dt)
+        if self.i_rng is not None:
+            a[self.i_rng] = int(rng_offset) & (2**64 - 1)
+        rc = self.fn(*a) if self.ext is None else self.fn(*a, ctypes.byref(self.ext))
+        _native.check(rc, self.name)
+
+
+def _planned(plan, pos, action, name, dtype, shape, dt, rng_offset=None):
+    """Run a recorded plan (True) after checking the per-call action tensor, or return False."""
+    if plan is None or plan.fn is None:
+        return False
+    _need(action, name, dtype, shape, pos.device)
+    plan.launch(_stream(pos), action, dt, rng_offset)
+    return True
+
+
+def _record(plan, lib_fn, name, args, ext, i_action, i_dt, i_rng=None):
+    if ext is None:
+        _native.check(lib_fn(*args), name)
+    else:
+        _native.check(lib_fn(*args, ctypes.byref(ext)), name)
+    if plan is not None:
+        plan.record(lib_fn, name, args, ext, i_action, i_dt, i_rng)
+
+
 def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k, box, sensor_range,
             collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False, ring=None,
-            seeds=None):
+            seeds=None, plan=None):
     """gym_flock_v2.MultiAgentEnv.step (gym_flock_v2.py:71-83) for E envs; pos/heading updated in place.
     ring (a _native.FlockRing): also write every transition into a replay ring in the same launch
     (flock_step_v2_store; the store_transitions that follows each step in train_flock.py).
-    seeds ([E, N, k] int16, rw, optional): compact kNN search seeds (flock_step_v2_ext; see include/flock_amd.h)."""
+    seeds ([E, N, k] int16, rw, optional): compact kNN search seeds (flock_step_v2_ext; see include/flock_amd.h).
+    plan (StepPlan, optional; not with ring): record / replay the validated launch over the same buffers."""
+    if ring is None and _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
+        return
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -87,15 +134,16 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
             float(v_min), float(v_max), int(bool(periodic)), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading),
             _ptr(action), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
     ext = _ext(ring, seeds, E, N, k, dev)
-    if ext is None:
-        _native.check(_native.lib().flock_step_v2(*args), "flock_step_v2")
-    else:
-        _native.check(_native.lib().flock_step_v2_ext(*args, ctypes.byref(ext)), "flock_step_v2_ext")
+    L = _native.lib()
+    _record(plan if ring is None else None, L.flock_step_v2 if ext is None else L.flock_step_v2_ext,
+            "flock_step_v2" if ext is None else "flock_step_v2_ext", args, ext, 14, 7)
 
 
 def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done, *, k, box,
-            sensor_range, collision_distance, dt=0.1, rigid_boundary=False, seeds=None):
+            sensor_range, collision_distance, dt=0.1, rigid_boundary=False, seeds=None, plan=None):
     """gym_flock_uw.MultiAgentEnv.step (gym_flock_uw.py:69-81); mem_out = rolled 4-frame observation."""
+    if _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
+        return
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -115,17 +163,20 @@ def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_id
             int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action), _ptr(mem_in),
             _ptr(mem_out), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
     ext = _ext(None, seeds, E, N, k, dev)
-    if ext is None:
-        _native.check(_native.lib().flock_step_uw(*args), "flock_step_uw")
-    else:
-        _native.check(_native.lib().flock_step_uw_ext(*args, ctypes.byref(ext)), "flock_step_uw_ext")
+    L = _native.lib()
+    _record(plan, L.flock_step_uw if ext is None else L.flock_step_uw_ext,
+            "flock_step_uw" if ext is None else "flock_step_uw_ext", args, ext, 12, 7)
 
 
 def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                      status=None, *, k, box, sensor_range, collision_distance, dt=0.1, v_max=2.5, rigid_boundary=False,
-                     noise_std=0.1, seed=0, rng_offset=0, seeds=None):
+                     noise_std=0.1, seed=0, rng_offset=0, seeds=None, plan=None):
     """gym_flock_uw_discrete.MultiAgentEnv.step (gym_flock_uw_discrete.py:110-122). noise=None → in-kernel
-    Philox N(0, noise_std) draws; otherwise noise [E,N,2] is added to the action-table means (parity mode)."""
+    Philox N(0, noise_std) draws; otherwise noise [E,N,2] is added to the action-table means (parity mode).
+    plan (StepPlan, optional; in-kernel noise only): record / replay the validated launch over the same buffers."""
+    if noise is None and _planned(plan, pos, action_id, "action_id", torch.int64, tuple(pos.shape[:2]), dt,
+                                  rng_offset):
+        return
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -150,15 +201,16 @@ def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, d
             int(table.shape[0]), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done),
             _ptr(status))
     ext = _ext(None, seeds, E, N, k, dev)
-    if ext is None:
-        _native.check(_native.lib().flock_step_uw_discrete(*args), "flock_step_uw_discrete")
-    else:
-        _native.check(_native.lib().flock_step_uw_discrete_ext(*args, ctypes.byref(ext)), "flock_step_uw_discrete_ext")
+    L = _native.lib()
+    _record(plan if noise is None else None, L.flock_step_uw_discrete if ext is None else L.flock_step_uw_discrete_ext,
+            "flock_step_uw_discrete" if ext is None else "flock_step_uw_discrete_ext", args, ext, 13, 7, 17)
 
 
 def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, *, k, box, collision_distance,
-               dt=0.1, rigid_boundary=False, seeds=None):
+               dt=0.1, rigid_boundary=False, seeds=None, plan=None):
     """gym_flock.MultiAgentEnv.step (gym_flock.py:48-60); vel is the unit-velocity state (rw)."""
+    if _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
+        return
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -176,10 +228,9 @@ def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any
             _ptr(pos), _ptr(vel), _ptr(action), _ptr(mem_in), _ptr(mem_out), _ptr(dnn), _ptr(nn_idx), _ptr(reward),
             _ptr(done), _ptr(any_done))
     ext = _ext(None, seeds, E, N, k, dev)
-    if ext is None:
-        _native.check(_native.lib().flock_step_flock(*args), "flock_step_flock")
-    else:
-        _native.check(_native.lib().flock_step_flock_ext(*args, ctypes.byref(ext)), "flock_step_flock_ext")
+    L = _native.lib()
+    _record(plan, L.flock_step_flock if ext is None else L.flock_step_flock_ext,
+            "flock_step_flock" if ext is None else "flock_step_flock_ext", args, ext, 10, 6)
 
 
 def knn(pos, k, box, sensor_range=14.0, periodic=True, clamp=True, dnn=None, nn_idx=None):

@@ -163,8 +163,13 @@ class VecFlockEnv:
             a = a.reshape(E, N).contiguous()
         else:
             a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
+        # launch plan of this buffer parity (ops.StepPlan): fixed buffers, so later steps skip the tensor checks
+        plans = self.__dict__.setdefault("_plans", {})
+        plan = plans.get(nxt)
+        if plan is None:
+            plan = plans[nxt] = ops.StepPlan()
         common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
-                      rigid_boundary=c.rigid_boundary)
+                      rigid_boundary=c.rigid_boundary, plan=plan)
         if ring is not None:
             if c.variant != "v2":
                 raise NotImplementedError("the fused replay insert is built for the v2 step")

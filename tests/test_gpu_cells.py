@@ -209,3 +209,46 @@ def test_specialised_kernel_is_bitwise_the_generic_one(variant, periodic, N, kin
                 outs[-1]["seeds"] = env.seeds.clone()
         for key in outs[0]:
             assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+
+
+class _NoPlans(dict):
+    """VecFlockEnv plan cache that never keeps a plan: every step takes the fully checked launch path."""
+
+    def __setitem__(self, key, value):
+        pass
+
+
+@pytest.mark.parametrize("variant,periodic,N", [("v2", True, 256), ("uw", False, 64), ("uw_discrete", False, 512),
+                                                ("flock", False, 128)])
+def test_step_plan_replay_is_bitwise_the_checked_launch(variant, periodic, N, cuda):
+    """ops.StepPlan (recorded launch per buffer parity, replayed with a new stream / action / dt / RNG offset)
+    against the checked launch on every step of a 6-step rollout, including a dt change mid-rollout."""
+    k, E = 4, 16
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(N + 11)
+    pos = _positions("uniform", E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    envs = []
+    for i in range(2):
+        env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda)
+        env.set_state(positions=pos, headings=head)
+        if i == 1:
+            env.__dict__["_plans"] = _NoPlans()
+        envs.append(env)
+    for t in range(6):
+        if variant == "uw_discrete":
+            act = torch.from_numpy(rng.integers(0, 4, (E, N)).astype(np.int64)).to(cuda)
+        else:
+            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32)).to(cuda)
+        dt = 0.1 if t < 4 else 0.05
+        outs = []
+        for env in envs:
+            obs, rew, (done, anyd), _ = env.step(act, dt=dt)
+            o = obs["actors"] if isinstance(obs, dict) else obs
+            outs.append([env.positions.clone(), env.headings.clone(), env.dnn.clone(), env.nn_idx.clone(),
+                         rew.clone(), done.clone(), anyd.clone(), o.clone()])
+        torch.cuda.synchronize()
+        for x, y in zip(*outs):
+            assert torch.equal(x, y), f"step {t}"
+    assert envs[0]._plans and all(p.fn is not None for p in envs[0]._plans.values())
