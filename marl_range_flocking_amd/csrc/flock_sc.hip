@@ -785,6 +785,25 @@ __device__ __forceinline__ void panel_store(float* __restrict__ P, const float4 
     }
 }
 
+// acc += the wave's K slice of the staged panels: operand k of MFMA kk/2 is a[kk * kPitch] / b[kk * kPitch]. The
+// LDS reads of 8 MFMAs are issued together, so the loop pays one LDS latency per 8 MFMAs instead of one per MFMA;
+// the accumulation order (and so every bit of the result) is the plain loop's.
+__device__ __forceinline__ f32x16 mfma_panel(f32x16 acc, const float* a, const float* b, int kq) {
+    int kk = 0;
+    for (; kk + 16 <= kq; kk += 16) {
+        float av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            av[u] = a[(kk + 2 * u) * kPitch];
+            bv[u] = b[(kk + 2 * u) * kPitch];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+    for (; kk < kq; kk += 2) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk * kPitch], b[kk * kPitch], acc, 0, 0, 0);
+    return acc;
+}
+
 // the 4 outputs of thread (wave w, lane l): rows 8w + 4(l >> 5) + q (q < 4), column l & 31
 template <int AV, int BV>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
@@ -814,8 +833,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
             const int kq = kc >> 2;  // multiple of 2
             const float* a = As + (wv * kq + (l >> 5)) * kPitch + (l & 31);
             const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
-            for (int kk = 0; kk < kq; kk += 2)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk * kPitch], b[kk * kPitch], acc, 0, 0, 0);
+            acc = mfma_panel(acc, a, b, kq);
             __syncthreads();
             kc = kc1;
         }
@@ -828,8 +846,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
             const int kq = kc >> 2;  // multiple of 2
             const float* a = As + (wv * kq + (l >> 5)) * kPitch + (l & 31);
             const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
-            for (int kk = 0; kk < kq; kk += 2)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk * kPitch], b[kk * kPitch], acc, 0, 0, 0);
+            acc = mfma_panel(acc, a, b, kq);
             __syncthreads();
         }
     }
