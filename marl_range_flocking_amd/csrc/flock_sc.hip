@@ -26,6 +26,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "flock_learn.h"
 #include "learn_internal.h"
@@ -1053,6 +1054,18 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
 
 // ---------------------------------------------------------------------------------------------------------------
 // host side
+// K-panel depth of the forward / input-gradient GEMMs: whole panels (kKC) by default; FLOCK_GEMM_KC (a multiple
+// of 8 in [8, 512]) stages them in chunks (smaller LDS footprint per block; A/B diagnostics)
+int fwd_kc() {
+    static int kc = -1;
+    if (kc < 0) {
+        const char* e = getenv("FLOCK_GEMM_KC");
+        const int v = e ? atoi(e) : 0;
+        kc = (v >= 8 && v <= kKC && (v & 7) == 0) ? v : kKC;
+    }
+    return kc;
+}
+
 GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int sam, int sak,
              int sbk, int sbn, int ldc, int64_t relB) {
     GemmP g;
@@ -1060,7 +1073,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.M = M; g.N = N; g.K = K; g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc; g.relB = relB;
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
-    g.kchunk = kKC;
+    g.kchunk = fwd_kc();
     return g;
 }
 
@@ -1105,7 +1118,7 @@ int launch_gemm(hipStream_t st, const GemmBatch& gb) {
         if (gemm_variant(gb.p[i]) != var) var = 3;
     }
     const dim3 grid(tiles, gb.n);
-    const size_t lds = gemm_lds_bytes(K);
+    const size_t lds = gemm_lds_bytes(K, fwd_kc());
     switch (var) {
         case 0: return launch_gemm_v<0, 0>(st, gb, grid, lds);
         case 1: return launch_gemm_v<0, 1>(st, gb, grid, lds);
