@@ -300,6 +300,20 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
     const float4* cand4 = reinterpret_cast<const float4*>(cand);
     int j = 0;
+    // 8 candidates per trip, their 4 LDS reads issued together: small-N steps run one wave per SIMD, where a
+    // read per candidate pair leaves the LDS latency exposed on every pair
+#pragma unroll 1
+    for (; j + 7 < N; j += 8) {
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = cand4[(j >> 1) + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const f32x2 d = pair_d2x2<PERIODIC>(xi, yi, c[u].x, c[u].y, c[u].z, c[u].w, box);
+            key_insert<L>(key, (__float_as_uint(d.x) & hi_mask) | (uint32_t)(j + 2 * u));
+            key_insert<L>(key, (__float_as_uint(d.y) & hi_mask) | (uint32_t)(j + 2 * u + 1));
+        }
+    }
 #pragma unroll 1
     for (; j + 1 < N; j += 2) {
         const float4 c = cand4[j >> 1];  // broadcast: every lane of the env reads the same 16 B
