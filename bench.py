@@ -13,8 +13,9 @@ transition and run VDN / RNN-MADDPG train() every 150 / 250 steps. Inputs (state
 are resident in HBM before the timed region starts; the first update (graph capture) happens before it.
 
 Rank 0 prints ONE JSON line. Extra fields: roofline (dominant kernel, HIP events on the launch stream; algorithmic
-bytes 93 B/agent-step), valu (same kernel against the f32 VALU roof, which is what binds it), and
-cpu_baseline (the C oracle port, 1 thread, on a bounded sample of the same workload; N=1 only).
+bytes per agent-step from SURVEY §8(d): v2 93, uw 149, uw_discrete 69, plus the fused replay insert; PMC traffic
+from profiles/pmc_*.json), allpairs_equivalent (the all-pairs sensing work the step replaces), and cpu_baseline (the
+C oracle port on 16 host threads and on 1, a bounded sample of the same workload; N=1 only).
 """
 import argparse
 import json
@@ -226,7 +227,8 @@ def main():
     E, N, k = args.envs, args.agents, args.k
     box = float(round(np.sqrt(250.0 * N)))  # main.py density: 10 agents in 50x50
     cfg = FlockConfig(variant=args.variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
-                      range_start=(0, box), sensor_range=14.0, seed=1234 + rank)
+                      range_start=(0, box), sensor_range=14.0, seed=1234 + rank,
+                      track_indices=args.variant == "v2")  # the reference returns neighbour indices for v2 only
     env = VecFlockEnv(cfg, device=dev)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     env.positions.copy_(torch.rand(E, N, 2, device=dev, generator=g) * box)

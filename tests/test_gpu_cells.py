@@ -252,3 +252,42 @@ def test_step_plan_replay_is_bitwise_the_checked_launch(variant, periodic, N, cu
         for x, y in zip(*outs):
             assert torch.equal(x, y), f"step {t}"
     assert envs[0]._plans and all(p.fn is not None for p in envs[0]._plans.values())
+
+
+@pytest.mark.parametrize("variant,periodic,N,kind", SPEC, ids=[f"{v}-N{n}-{d}" for v, _, n, d in SPEC])
+def test_untracked_indices_change_nothing_else(variant, periodic, N, kind, cuda):
+    """track_indices=False (bench.py's uw / uw_discrete configs: the reference returns no neighbour indices there)
+    skips the int64 index stores; four-step rollouts agree bit for bit with the tracked run on every other output,
+    the observation memory and the seed buffer."""
+    k, E = 4, (16 if N >= 512 else 64)
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(N + 9)
+    pos = _positions(kind, E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    mem = rng.uniform(0, 14, (E, N, 4, k)).astype(np.float32)
+    envs = []
+    for track in (True, False):
+        env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, periodic=periodic,
+                                      track_indices=track), device=cuda)
+        env.set_state(positions=pos, headings=head, obs_memory=mem if variant == "uw" else None)
+        envs.append(env)
+    assert envs[1].nn_idx is None
+    for t in range(4):
+        if variant == "uw_discrete":
+            act = torch.from_numpy(rng.integers(0, 4, (E, N)).astype(np.int64))
+            kw = dict(noise=torch.from_numpy((0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)))
+        else:
+            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
+            kw = {}
+        outs = []
+        for env in envs:
+            obs, rew, (done, anyd), _ = env.step(act, **kw)
+            torch.cuda.synchronize()
+            o = obs["actors"] if isinstance(obs, dict) else obs
+            outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
+                         "rew": rew, "done": done, "any": anyd, "obs": o.clone()})
+            if env.seeds is not None:
+                outs[-1]["seeds"] = env.seeds.clone()
+        for key in outs[0]:
+            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
