@@ -66,6 +66,7 @@ int fail(int code, const char* msg) {
 
 struct Params {
     int E, N, k, G, S, P, ib;
+    int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
     int variant, periodic, rigid, clamp;
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
     uint64_t seed, rng_offset;
@@ -666,7 +667,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     const int t = threadIdx.x;
     const int g = t / p.N;
     const int i = t - g * p.N;
-    const int env = blockIdx.x * p.G + g;
+    const int env = p.env0 + blockIdx.x * p.G + g;
     const bool in_group = g < p.G;
     const bool active = in_group && env < p.E;
     const size_t a = (size_t)env * p.N + i;
@@ -1311,6 +1312,13 @@ int check_common(int E, int N, int k) {
     return FLOCK_OK;
 }
 
+// FLOCK_ENV_LAUNCHES=n (diagnostics): split a step into n launches over consecutive env ranges
+int env_launches(int blocks) {
+    const char* e = getenv("FLOCK_ENV_LAUNCHES");
+    const int n = e ? atoi(e) : 1;
+    return n < 1 ? 1 : (n > blocks ? blocks : n);
+}
+
 // the specialised instantiations (step_kernel VAR / NC): the BASELINE configurations' per-GPU shapes
 template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC>
 bool launch_spec(const Cfg& c, const Params& p, hipStream_t s) {
@@ -1318,7 +1326,19 @@ bool launch_spec(const Cfg& c, const Params& p, hipStream_t s) {
         return false;
     if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
     if (getenv("FLOCK_NO_SPEC")) return false;  // A/B diagnostics: the generic instantiation
-    hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+    const int parts = env_launches(c.blocks);
+    if (parts <= 1) {
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+        return true;
+    }
+    // the step as `parts` back-to-back launches over consecutive env ranges (same results: envs are independent)
+    const int per = (c.blocks + parts - 1) / parts;
+    Params q = p;
+    for (int b0 = 0; b0 < c.blocks; b0 += per) {
+        q.env0 = b0 * c.G;
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC>), dim3(min(per, c.blocks - b0)),
+                           dim3(c.T), c.lds, s, q);
+    }
     return true;
 }
 
