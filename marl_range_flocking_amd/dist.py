@@ -53,6 +53,14 @@ def allreduce_mean_(t, group=None):
     return t
 
 
+def allreduce_sum_(t, group=None):
+    """In-place sum over ranks (no-op on one rank); the caller folds 1 / world into its consumer (the Adam
+    kernels' device-side grad_scale), one elementwise launch fewer than allreduce_mean_."""
+    if active(group):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
 def broadcast_(t, src=0, group=None):
     if active(group):
         dist.broadcast(t, src=src, group=group)

@@ -117,6 +117,10 @@ class SharedCriticLearner:
         self.scratch_leaves = self.scratch.new_leaves(squeeze=True)
         self.group = dist_group
         self.distributed = dist.active(dist_group)
+        # fused data-parallel path: gradients are all-reduced as sums and the Adam kernels scale them by 1 / world
+        # (bitwise the mean for power-of-two worlds)
+        self.inv_world = (torch.full((1,), 1.0 / torch.distributed.get_world_size(dist_group), device=device)
+                          if self.distributed else None)
         self.graphs = None
         if self.distributed:
             dist.sync_params(self.critic, group=dist_group)
@@ -201,21 +205,25 @@ class SharedCriticLearner:
                 else:
                     self.graph = g
             return g.replay()
-        # data-parallel: gradient-only kernels, RCCL all-reduce of each network's gradient, then the Adam steps
+        # data-parallel: gradient-only kernels, RCCL all-reduce (sum) of each network's gradient, then the Adam
+        # steps with grad_scale = 1 / world; the actor's target soft update (:180-185) rides in its Adam launch
         lib = _native.lib()
         st = _stream(self.device)
         u = ctypes.byref(S["sc_grads"] if S is not None else self._sc_grads)
         _native.check(lib.flock_sc_critic_update(st, u), "flock_sc_critic_update", learn=True)
-        dist.allreduce_mean_(self.critic.grad, self.group)
-        self.critic.adam_step_dev(self.beta)
+        dist.allreduce_sum_(self.critic.grad, self.group)
+        self.critic.adam_step_dev(self.beta, grad_scale=self.inv_world)
         _native.check(lib.flock_sc_actor_update(st, u), "flock_sc_actor_update", learn=True)
         A = self.actors
         lo, hi = A.agent_range(agent)
-        dist.allreduce_mean_(A.grad[lo:hi], self.group)
+        dist.allreduce_sum_(A.grad[lo:hi], self.group)
         self.actor_steps[agent:agent + 1].add_(1)
+        soft = self.count[agent] % self.update_rate == 0
         rc = lib.flock_adam_step_dev(st, hi - lo, _p(A.data[lo:hi]), _p(A.grad[lo:hi]), _p(A.exp_avg[lo:hi]),
-                                     _p(A.exp_avg_sq[lo:hi]), None, float(self.alpha), 0.9, 0.999, 1e-8,
-                                     _p(self.actor_steps[agent:agent + 1]), None, 0.0, 0)
+                                     _p(A.exp_avg_sq[lo:hi]), _p(self.inv_world), float(self.alpha), 0.9, 0.999,
+                                     1e-8, _p(self.actor_steps[agent:agent + 1]),
+                                     _p(A.target[lo:hi]) if soft else None, float(self.tau) if soft else 0.0,
+                                     1 if soft else 0)
         _native.check(rc, "flock_adam_step_dev", learn=True)
 
     # ------------------------------------------------------------------ acting
@@ -355,7 +363,7 @@ class SharedCriticLearner:
                                                  _p(self.static_agent), int(agent))
                 _native.check(rc, "flock_sc_prep", learn=True)
             self._run_fused(agent)
-            return self._finish_learn(agent, soft_in_kernel=not self.distributed)
+            return self._finish_learn(agent, soft_in_kernel=not self.distributed, actor_soft_done=self.distributed)
         if idx is None:                                                       # utils.py:65-76 (with replacement)
             torch.randint(0, len(self.replay), (B,), device=self.device, generator=self.gen, out=self.static_idx)
         else:
@@ -395,12 +403,13 @@ class SharedCriticLearner:
     def update_slot(self, slot, agent):
         """The rest of learn() on the rows snapshot_into(slot, agent) copied, enqueued on the current stream."""
         self._run_fused(agent, slot)
-        return self._finish_learn(agent, soft_in_kernel=not self.distributed)
+        return self._finish_learn(agent, soft_in_kernel=not self.distributed, actor_soft_done=self.distributed)
 
-    def _finish_learn(self, agent, soft_in_kernel=False):
+    def _finish_learn(self, agent, soft_in_kernel=False, actor_soft_done=False):
         if self.count[agent] % self.update_rate == 0 and not soft_in_kernel:                         # :152-154
             self.critic.soft_update(self.tau, mode=1, self_update=True)       # :172-178 (critic is its own target)
-            self.actors.soft_update(self.tau, mode=1, agent=agent)            # :180-185
+            if not actor_soft_done:
+                self.actors.soft_update(self.tau, mode=1, agent=agent)        # :180-185
         self.count[agent] += 1
         return self.losses[0], self.losses[1], True
 
