@@ -291,3 +291,34 @@ def test_untracked_indices_change_nothing_else(variant, periodic, N, kind, cuda)
                 outs[-1]["seeds"] = env.seeds.clone()
         for key in outs[0]:
             assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+
+
+def test_env_range_launches_are_bitwise_one_launch(cuda):
+    """FLOCK_ENV_LAUNCHES=n splits a step into n launches over consecutive env ranges (Params.env0): a four-step
+    config-3-shape rollout (v2, N = 256, seeds, every output) is bit for bit the one-launch rollout."""
+    k, E, N = 4, 37, 256  # E not a multiple of the split: the last range is short
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(11)
+    pos = rng.uniform(0, box, (E, N, 2)).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    envs = []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0), device=cuda)
+        env.set_state(positions=pos, headings=head)
+        envs.append(env)
+    try:
+        for t in range(4):
+            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
+            outs = []
+            for i, env in enumerate(envs):
+                os.environ["FLOCK_ENV_LAUNCHES"] = "4" if i else "1"
+                obs, rew, (done, anyd), _ = env.step(act)
+                torch.cuda.synchronize()
+                outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
+                             "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd,
+                             "seeds": env.seeds.clone() if env.seeds is not None else rew})
+            for key in outs[0]:
+                assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+    finally:
+        os.environ.pop("FLOCK_ENV_LAUNCHES", None)
