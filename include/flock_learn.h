@@ -70,7 +70,8 @@ int flock_scatter_rows(void* stream, int64_t rows, int64_t width, const float* s
 /* Replay insert of n rows into ring rows start .. start+n-1 (mod capacity), every field in ONE launch (replaces the
  * per-field row copies of ReplayBuffer.store_transitions, maddpg_shared_critic/utils.py:47-54, memory_rnn.py:53-67,
  * vdn/utils.py:20-29). src: n * width contiguous values; dst: the field's [capacity][width] f32 ring.
- * kind 0: f32 copy; 1: u8/bool -> 1 - x (the stored "terminal"); 2: u8/bool -> x. At most 8 fields; n <= capacity. */
+ * kind 0: f32 copy; 1: u8/bool -> 1 - x (the stored "terminal"); 2: u8/bool -> x; 3: int64 -> f32 (round to
+ * nearest, as torch's .float(): discrete action ids). At most 8 fields; n <= capacity. */
 typedef struct FlockRingField {
     const void* src;
     float* dst;

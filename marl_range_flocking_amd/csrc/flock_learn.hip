@@ -449,8 +449,9 @@ struct RingStore {
 __global__ __launch_bounds__(kBlock) void ring_store_kernel(RingStore rs) {
     const FlockRingField F = rs.f[blockIdx.y];
     const int64_t total = rs.n * F.width, wrap = rs.cap * F.width, d0 = rs.start * F.width;
-    const bool u8 = F.kind != 0;
-    const bool vec = ((total | wrap | d0) & 3) == 0 && ((uintptr_t)F.dst & 15) == 0 &&
+    const bool i64 = F.kind == 3;  // int64 -> f32 (torch .float(): round to nearest)
+    const bool u8 = F.kind == 1 || F.kind == 2;
+    const bool vec = !i64 && ((total | wrap | d0) & 3) == 0 && ((uintptr_t)F.dst & 15) == 0 &&
                      ((uintptr_t)F.src & (u8 ? 3 : 15)) == 0;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     if (vec) {
@@ -470,7 +471,9 @@ __global__ __launch_bounds__(kBlock) void ring_store_kernel(RingStore rs) {
     } else {
         for (int64_t q = blockIdx.x * (int64_t)kBlock + threadIdx.x; q < total; q += stride) {
             float v;
-            if (!u8) {
+            if (i64) {
+                v = (float)reinterpret_cast<const int64_t*>(F.src)[q];
+            } else if (!u8) {
                 v = reinterpret_cast<const float*>(F.src)[q];
             } else {
                 v = (float)reinterpret_cast<const uint8_t*>(F.src)[q];
@@ -497,7 +500,7 @@ int flock_ring_store(void* stream, int64_t n, int64_t capacity, int64_t start, i
     int64_t widest = 0;
     for (int i = 0; i < nfields; ++i) {
         if (!fields[i].src || !fields[i].dst) return fail(-3, "flock_ring_store: NULL pointer");
-        if (fields[i].width < 1 || fields[i].kind < 0 || fields[i].kind > 2)
+        if (fields[i].width < 1 || fields[i].kind < 0 || fields[i].kind > 3)
             return fail(-5, "flock_ring_store: bad field");
         rs.f[i] = fields[i];
         if (fields[i].width > widest) widest = fields[i].width;

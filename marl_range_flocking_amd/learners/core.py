@@ -364,7 +364,8 @@ class ReplayRing:
 
     def store(self, rows: dict, one_minus=()):
         """Append n rows per field (all fields the same n) at positions counter..counter+n-1 (mod capacity), every
-        field in ONE flock_ring_store launch. rows[name]: [n, *row_shape] (converted to f32 if needed); a name in
+        field in ONE flock_ring_store launch. rows[name]: [n, *row_shape] (u8 / bool / int64 converted to f32 by the
+        kernel, other dtypes by torch); a name in
         ``one_minus`` takes a bool / 0-1 tensor [n] and stores 1 - x (the reference's terminal = 1 - done)."""
         n = next(iter(rows.values())).shape[0]
         if n > self.capacity:  # only the last `capacity` rows survive
@@ -387,7 +388,12 @@ class ReplayRing:
             else:
                 src = val.reshape(n, -1)
                 assert src.shape[1] == w, (name, src.shape, w)
-                src = src.float().contiguous()
+                if src.dtype in (torch.bool, torch.uint8):  # converted in the store kernel
+                    src, kind = src.contiguous(), 2
+                elif src.dtype == torch.int64:
+                    src, kind = src.contiguous(), 3
+                else:
+                    src = src.float().contiguous()
             keep.append(src)
             fields[i] = _native.FlockRingField(src.data_ptr(), self.bufs[name].data_ptr(), w, kind)
         _require_cuda(self.bufs[next(iter(rows))])

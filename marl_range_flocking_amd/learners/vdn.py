@@ -180,10 +180,11 @@ class VDNLearner:
             s, a, r, s_prime = s[None], torch.as_tensor(a)[None], torch.as_tensor(r)[None], torch.as_tensor(s_prime)[None]
             done = torch.as_tensor(done, dtype=torch.float32).reshape(1)
         n = s.shape[0]
-        self.replay.store({"s": s, "a": torch.as_tensor(a, device=self.device).float().reshape(n, self.A),
+        # action ids (int64) and done flags (u8 / bool) are converted to f32 inside the one store launch
+        self.replay.store({"s": s, "a": torch.as_tensor(a, device=self.device).reshape(n, self.A),
                            "r": torch.as_tensor(r, device=self.device).float().reshape(n, self.A),
                            "s_prime": torch.as_tensor(s_prime, device=self.device).float(),
-                           "done": torch.as_tensor(done, device=self.device).float().reshape(n)})
+                           "done": torch.as_tensor(done, device=self.device).reshape(n)})
 
     def size(self):
         return len(self.replay)
