@@ -173,6 +173,17 @@ int flock_reset(void* stream, int variant, int E, int N, int k, float range_lo, 
                 float* pos, float* heading, float* prev_heading, float* vel, float* dnn, int64_t* nn_idx,
                 float* mem, uint8_t* valid);
 
+/* flock_reset plus a repair stage (repair_rounds > 0; flock_reset(...) == flock_reset_ext(..., 0)): an env whose
+ * max_attempts whole-swarm draws all collided keeps its last draw, and every agent closer than check_distance to a
+ * lower-indexed agent re-draws its own position, for up to repair_rounds rounds; the reference's kNN collision
+ * check then sets valid[e]. Replaces the recursion of gym_flock_v2.py:105-108 where it cannot terminate (N >= 256
+ * at main.py density: the reference overflows Python's recursion limit). */
+int flock_reset_ext(void* stream, int variant, int E, int N, int k, float range_lo, float range_hi, float box,
+                    float sensor_range, float check_distance, int rigid_boundary, int max_attempts,
+                    uint64_t seed, uint64_t rng_offset, const uint8_t* env_mask,
+                    float* pos, float* heading, float* prev_heading, float* vel, float* dnn, int64_t* nn_idx,
+                    float* mem, uint8_t* valid, int repair_rounds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,8 @@ SIGNATURES = {
     "flock_knn": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int] + [_c_void_p] * 3,
     "flock_reset": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_float,
                     _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9,
+    "flock_reset_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float,
+                        _c_float, _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9 + [_c_int],
     # learner kernels (include/flock_learn.h)
     "flock_learn_last_error": [],
     "flock_adam_step": [_c_void_p, ctypes.c_int64] + [_c_void_p] * 5 + [_c_float] * 4 + [ctypes.c_int64, _c_void_p,

@@ -98,7 +98,7 @@ struct Params {
     float cwx, cwy, inv_cwx, inv_cwy, cell_eps, r_lim;
     // reset
     float range_lo, range_hi, head_hi, check_distance;
-    int max_attempts;
+    int max_attempts, repair;
     const uint8_t* env_mask;
     uint8_t* valid;
 };
@@ -1238,6 +1238,53 @@ __global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
         if (in_group) more = state[g];
         if (!__syncthreads_or(more)) break;
     }
+    // repair (p.repair > 0 rounds; flock_reset_ext): a swarm whose every whole-swarm draw collided (certain at
+    // main.py density for N >= 256) keeps its last draw, and every agent closer than
+    // check_distance to a LOWER-indexed agent re-draws its own position from a separate Philox stream, round after
+    // round, until no pair is that close. The kNN + collision check of the reference then decides valid[] as for
+    // a plain draw. Agent 0 never moves, so each round fixes at least the lowest conflicting index.
+    if (p.repair > 0 && __syncthreads_or(in_group && state[g])) {
+        const float2* lp = lpos + g * p.S;
+        for (int round = 0; round < p.repair; ++round) {
+            int bad = 0;
+            if (active && state[g]) {
+                for (int j = 0; j < i; ++j) {  // Euclidean distance with the kNN's op order
+                    const float2 q = lp[j];
+                    const float dx = __fsub_rn(x, q.x), dy = __fsub_rn(y, q.y);
+                    const float d = sqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)));
+                    bad |= (d < p.check_distance);
+                }
+            }
+            __syncthreads();  // every lane has read the round's positions before any rewrite
+            if (bad) {
+                const uint64_t ctr = p.rng_offset + (uint64_t)round;
+                const U4 r = philox(p.seed, (uint32_t)a, (uint32_t)(a >> 32), (uint32_t)ctr,
+                                    (uint32_t)(ctr >> 32) | 0x80000000u);
+                const float span = p.range_lo - p.range_hi;
+                x = boundary(__fadd_rn(__fmul_rn(span, u01(r.x)), p.range_hi), p.box, p.rigid);
+                y = boundary(__fadd_rn(__fmul_rn(span, u01(r.y)), p.range_hi), p.box, p.rigid);
+                lpos[g * p.S + i] = make_float2(x, y);
+            }
+            if (!__syncthreads_or(bad)) break;
+        }
+        if (in_group && i == 0) flags[g] = 0;
+        __syncthreads();
+        if (active && state[g]) {
+            knn_scan<L, false>(lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);
+            int coll = 0;
+#pragma unroll
+            for (int s = 1; s < L - 1; ++s)
+                if (s <= p.k) {
+                    float d = sqrt_rn(bd[s]);
+                    if (p.clamp) d = clamp_t(d, 0.0f, p.sensor_range);
+                    coll |= (d < p.check_distance);
+                }
+            if (coll) atomicOr(&flags[g], 1);
+        }
+        __syncthreads();
+        if (in_group && i == 0 && state[g]) state[g] = flags[g];
+        __syncthreads();
+    }
     const bool touched = active && (p.env_mask == nullptr || p.env_mask[env] != 0);
     if (touched) {
         reinterpret_cast<float2*>(p.pos)[a] = make_float2(x, y);
@@ -1697,11 +1744,22 @@ int flock_reset(void* stream, int variant, int E, int N, int k, float range_lo, 
                 float sensor_range, float check_distance, int rigid_boundary, int max_attempts, uint64_t seed,
                 uint64_t rng_offset, const uint8_t* env_mask, float* pos, float* heading, float* prev_heading,
                 float* vel, float* dnn, int64_t* nn_idx, float* mem, uint8_t* valid) {
+    return flock_reset_ext(stream, variant, E, N, k, range_lo, range_hi, box, sensor_range, check_distance,
+                           rigid_boundary, max_attempts, seed, rng_offset, env_mask, pos, heading, prev_heading, vel,
+                           dnn, nn_idx, mem, valid, 0);
+}
+
+int flock_reset_ext(void* stream, int variant, int E, int N, int k, float range_lo, float range_hi, float box,
+                    float sensor_range, float check_distance, int rigid_boundary, int max_attempts, uint64_t seed,
+                    uint64_t rng_offset, const uint8_t* env_mask, float* pos, float* heading, float* prev_heading,
+                    float* vel, float* dnn, int64_t* nn_idx, float* mem, uint8_t* valid, int repair_rounds) {
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !dnn)) return fail(FLOCK_E_NULL, "flock_reset: NULL pointer");
     if (max_attempts < 1) return fail(FLOCK_E_ARG, "max_attempts must be >= 1");
+    if (repair_rounds < 0) return fail(FLOCK_E_ARG, "repair_rounds must be >= 0");
     Params p = base(E, N, k, box);
+    p.repair = repair_rounds;
     p.variant = variant;
     p.rigid = rigid_boundary != 0;
     p.sensor_range = sensor_range;

@@ -38,13 +38,9 @@ class SingleFlockEnv(_EnvBase):
             raise NotImplementedError("normalize_distance=True is not supported by the HIP stepper")
         self.num_particles = agents
         self.k = k
-        self.rigid_boundary = rigid_boundary
         self.boundary = range_start[1]
         self.desired_distance = desired_distance
         self.range_start = range_start
-        self.sensor_range = sensor_range
-        self.max_linear_velocity = max_linear_velocity
-        self.collision_distance = collision_distance
         self.normalize_distances = normalize_distance
         self._vec = VecFlockEnv(
             FlockConfig(variant=self.variant, num_envs=1, num_agents=agents, k=k,
@@ -56,6 +52,21 @@ class SingleFlockEnv(_EnvBase):
         self.device = self._vec.device
         # like the reference ctor (gym_flock_v2.py:54-57): random positions before the first reset
         self._vec.positions.uniform_(0.0, 1.0).mul_(float(range_start[0] - range_start[1])).add_(range_start[1])
+
+    # ---- parameters the reference reads on every step: assignments write through to the device config -----
+    def _param(name):  # noqa: N805
+        def get(self):
+            return getattr(self._vec.cfg, name)
+
+        def set_(self, value):
+            self._vec.set_param(name, value)
+
+        return property(get, set_)
+
+    collision_distance = _param("collision_distance")
+    sensor_range = _param("sensor_range")
+    rigid_boundary = _param("rigid_boundary")
+    max_linear_velocity = _param("max_linear_velocity")
 
     # ---- state views (shape as in the reference: (N, 2), (N,), (N, k)) --------------------------------------
     def _view(name):  # noqa: N805
@@ -108,7 +119,14 @@ class SingleFlockEnv(_EnvBase):
         return self._obs(), self._vec.reward[0].reshape(-1, 1).clone(), (dones, all_done), {}
 
     def reset(self):
+        """reset() (gym_flock_v2.py:85-108 and siblings): a collision-free swarm (VecFlockEnv.reset: bounded
+        whole-swarm draws, then the per-agent repair). Raises RuntimeError if neither places one — where the
+        reference's recursion never ends (it overflows Python's recursion limit)."""
         self._vec.reset()
+        if not self.reset_valid:
+            raise RuntimeError("reset(): no collision-free placement within max_reset_attempts whole-swarm draws and "
+                               f"{self._vec.cfg.reset_repair_rounds} repair rounds (gym_flock_v2.py:105-108 would "
+                               "recurse without end)")
         return self._obs()
 
     @property

@@ -30,6 +30,11 @@ class MultiAgentEnv(SingleFlockEnv):
 
     def step(self, action, dt=0.1, noise=None):
         a = torch.as_tensor(action).to(self.device).reshape(1, self.num_particles)
+        # action_dictionary[int(act)] raises before any state changes (:329-330): check the ids first (this
+        # single-env wrapper synchronises every step anyway; VecFlockEnv reports bad ids through its status flag)
+        ids = a if a.dtype == torch.int64 else a.to(torch.int64)
+        if bool(((ids < 0) | (ids >= len(self.action_dictionary))).any().item()):
+            raise KeyError("action id outside the action dictionary (gym_flock_uw_discrete.py:329)")
         if noise is not None:
             noise = torch.as_tensor(noise, dtype=torch.float32).to(self.device).reshape(1, self.num_particles, 2)
         self._vec.step(a, noise=noise, dt=dt)

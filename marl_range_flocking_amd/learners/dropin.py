@@ -258,35 +258,41 @@ class OUActionNoiseGPU:
 
 
 class ReplayBuffer:
-    """maddpg_shared_critic/utils.py:28-76 surface; the rows live in the shared-critic learner's device ring."""
+    """maddpg_shared_critic/utils.py:28-76 surface. The device ring is allocated here (max_size rows, as the reference
+    allocates its arrays in the constructor, utils.py:29-45) and adopted by the shared-critic learner, so rows stored
+    before the first choose_action land in HBM at once and mem_cntr is a plain counter."""
 
     def __init__(self, max_size, input_shape, n_actions, n_agents):
         self.mem_size, self.input_shape, self.n_actions, self.n_agents = int(max_size), input_shape, n_actions, \
             n_agents
-        self.pending = []
-        self.backend = None
+        self.ring = SharedCriticLearner.make_replay(self.mem_size, input_shape[0], n_actions, _device())
 
     @property
     def mem_cntr(self):
-        return self.backend.replay.counter if self.backend is not None else sum(p[0].shape[0] for p in self.pending)
+        return self.ring.counter
 
     def store_transitions(self, state, action, reward, state_, done):
-        if self.backend is None:
-            self.pending.append((state, action, reward, state_, done))
-        else:
-            self.backend.store_transitions(state, action, reward, state_, done)
+        SharedCriticLearner.store_rows(self.ring, state, action, reward, state_, done)
 
     store_single_transition = store_transitions
 
 
 class CriticNetwork:
-    """ddpg_network.py:11-70 surface: the shared critic; the Agents built on it form ONE batched learner."""
+    """ddpg_network.py:11-70 surface: the shared critic; the Agents built on it form ONE batched learner. Checkpoint
+    files as the reference names them (ddpg_network.py:29-34): ``{chkpt_dir}/{name}_ddpg.pt`` and
+    ``{chkpt_best_dir}/{name}_ddpg.pt``, both directories created here."""
 
-    def __init__(self, beta, input_dims, fc1_dims, fc2_dims, n_actions, name, chkpt_dir="tmp", chkpt_best_dir="tmp"):
+    def __init__(self, beta, input_dims, fc1_dims, fc2_dims, n_actions, name, chkpt_dir=r"tmp\ddpg",
+                 chkpt_best_dir=r"tmp\ddpg_best"):
         self.beta, self.input_dims, self.fc1_dims, self.fc2_dims = beta, input_dims, fc1_dims, fc2_dims
-        self.n_actions, self.name, self.chkpt_dir = n_actions, name, chkpt_dir
+        self.n_actions, self.name, self.chkpt_dir, self.chkpt_best_dir = n_actions, name, chkpt_dir, chkpt_best_dir
+        for d in (chkpt_dir, chkpt_best_dir):
+            os.makedirs(d, exist_ok=True)
+        self.checkpoint_file = os.path.join(chkpt_dir, name + "_ddpg.pt")
+        self.checkpoint_best_file = os.path.join(chkpt_best_dir, name + "_ddpg.pt")
         self.agents = []
         self.backend = None
+        self._act_cache = None  # (observation tensor, key, all agents' mu) of the last choose_action
 
     def _build(self):
         if self.backend is None:
@@ -295,12 +301,28 @@ class CriticNetwork:
             self.backend = SharedCriticLearner(
                 len(self.agents), self.input_dims[0], n_actions=self.n_actions, fc1=self.fc1_dims, fc2=self.fc2_dims,
                 alpha=a0.alpha, beta=self.beta, gamma=a0.gamma, tau=a0.tau, batch_size=a0.batch_size,
-                update_rate=a0.update_rate, buffer_size=rb.mem_size, device=_device())
-            rb.backend = self.backend
-            for p in rb.pending:
-                self.backend.store_transitions(*p)
-            rb.pending = []
+                update_rate=a0.update_rate, buffer_size=rb.mem_size, device=_device(), replay=rb.ring)
         return self.backend
+
+    def actions(self, observation):
+        """Every agent's mu for one observation [N, in], computed once per observation: the reference driver calls
+        choose_action agent after agent with the same tensor (train_flock.py:114-115), so agents 1..N-1 slice the
+        batched result. The cache holds the observation tensor itself (its address cannot be reused while cached)
+        and keys on its storage, shape, strides and version counter (bumped by any in-place write); learn() and
+        load_models() drop it."""
+        t = observation if torch.is_tensor(observation) else None
+        key = None if t is None else (t.data_ptr(), tuple(t.shape), t.stride(), t.dtype, t.device, t._version)
+        c = self._act_cache
+        if key is not None and c is not None and c[1] == key:
+            return c[2]
+        L = self._build()
+        obs = torch.as_tensor(observation).to(L.device).float()
+        mu = L.choose_action(obs.reshape(L.n_agents, -1)[None], noise=False)[0]
+        self._act_cache = (t, key, mu) if key is not None else None
+        return mu
+
+    def drop_action_cache(self):
+        self._act_cache = None
 
 
 class Agent:
@@ -311,6 +333,7 @@ class Agent:
                  batch_size=64, update_rate=3):
         if recurrent:
             raise NotImplementedError("the recurrent shared-critic variant imports modules absent from the reference")
+        os.makedirs(checkpoint_dir, exist_ok=True)  # agent_simple_shared_critic.py:46-47
         self.critic = self.target_critic = shared_critic
         self.alpha, self.gamma, self.tau, self.batch_size, self.update_rate = alpha, gamma, tau, batch_size, update_rate
         self.index, self.memory, self.noise = index, replay_buffer, noise
@@ -318,26 +341,29 @@ class Agent:
         shared_critic.agents.append(self)
 
     def choose_action(self, observation):
-        L = self.critic._build()
-        obs = torch.as_tensor(observation).to(L.device).float()
-        mu = L.choose_action(obs.reshape(L.n_agents, -1)[None], noise=False)[0, self.index]
-        return mu + self.noise()
+        """agent_simple_shared_critic.py:92-107: mu_i(obs[i]) + noise (the batched mu is shared by all agents)."""
+        return self.critic.actions(observation)[self.index] + self.noise()
 
     def remember(self, state, action, reward, new_state, done):
         self.memory.store_transitions(state, action, reward, new_state, done)
 
     def learn(self):
+        self.critic.drop_action_cache()
         return self.critic._build().learn(self.index)
 
     def _files(self, best):
+        """Actor / TargetActor in this agent's checkpoint (or best) directory, the critic in the CriticNetwork's own
+        directories (ddpg_network.py:33-34, :103-104; train_flock.py:47-48, :65-66)."""
         d = self.checkpoint_best if best else self.checkpoint_dir
-        return [os.path.join(d, f"{n}_ddpg.pt") for n in ("Actor", "TargetActor", "Critic")]
+        crit = self.critic.checkpoint_best_file if best else self.critic.checkpoint_file
+        return [os.path.join(d, f"{n}_ddpg.pt") for n in ("Actor", "TargetActor")] + [crit]
 
     def save_models(self, best=False):
         """train_flock.py:143 (every 300 s) / :151 (save_models_best); agent_simple.py:200-210 file naming."""
         L = self.critic._build()
         files = self._files(best)
-        os.makedirs(os.path.dirname(files[0]), exist_ok=True)
+        for f in files:
+            os.makedirs(os.path.dirname(f) or ".", exist_ok=True)
         for f, sd in zip(files, (L.actor_state_dict(self.index), L.actor_state_dict(self.index, target=True),
                                  L.critic_state_dict())):
             torch.save(sd, f)
@@ -350,3 +376,4 @@ class Agent:
         L = self.critic._build()
         actor, target, critic = (torch.load(f, weights_only=True) for f in self._files(best))
         L.load_reference_state(critic, {self.index: actor}, {self.index: target})
+        self.critic.drop_action_cache()

@@ -85,7 +85,7 @@ class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
                  ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
-                 snapshot=False):
+                 snapshot=False, replay=None):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -100,8 +100,9 @@ class SharedCriticLearner:
         _init_mlp(self.actors, None, self.gen)
         self.actors.hard_update_target()  # update_network_parameters(tau=1) (:81)
         self.count = [0] * n_agents
-        self.replay = ReplayRing(buffer_size, {"state": (input_dim,), "new_state": (input_dim,),
-                                               "action": (n_actions,), "reward": (1,), "terminal": ()}, self.device)
+        # replay: an existing ring from make_replay (the drop-in ReplayBuffer allocates it before the learner)
+        self.replay = replay if replay is not None else self.make_replay(buffer_size, input_dim, n_actions,
+                                                                           self.device)
         self.ou = dict(sigma=ou_sigma, theta=ou_theta, dt=ou_dt)
         self.ou_state = None
         # the update runs on static tensors so it can be replayed as one HIP graph: agent i's actor is copied into
@@ -252,12 +253,22 @@ class SharedCriticLearner:
         self.ou_state = None
 
     # ------------------------------------------------------------------ replay
-    def store_transitions(self, state, action, reward, new_state, done):
+    @staticmethod
+    def make_replay(capacity, input_dim, n_actions, device):
+        """The ReplayBuffer arrays (utils.py:29-45) as one device ring."""
+        return ReplayRing(capacity, {"state": (input_dim,), "new_state": (input_dim,), "action": (n_actions,),
+                                     "reward": (1,), "terminal": ()}, device)
+
+    @staticmethod
+    def store_rows(ring, state, action, reward, new_state, done):
         """ReplayBuffer.store_transitions (utils.py:47-54): rows [n, ...]; terminal stored as 1 - done."""
         n = state.shape[0]
-        self.replay.store({"state": state.reshape(n, -1), "new_state": new_state.reshape(n, -1),
-                           "action": action.reshape(n, -1), "reward": reward.reshape(n, 1),
-                           "terminal": done.reshape(n)}, one_minus=("terminal",))
+        ring.store({"state": state.reshape(n, -1), "new_state": new_state.reshape(n, -1),
+                    "action": action.reshape(n, -1), "reward": reward.reshape(n, 1),
+                    "terminal": done.reshape(n)}, one_minus=("terminal",))
+
+    def store_transitions(self, state, action, reward, new_state, done):
+        self.store_rows(self.replay, state, action, reward, new_state, done)
 
     def replay_slots(self, n):
         """Reserve the next n replay rows for an env step that writes its transitions itself

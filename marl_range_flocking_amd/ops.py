@@ -255,8 +255,9 @@ VARIANT_IDS = {"v2": 0, "uw": 1, "uw_discrete": 2, "flock": 3}
 
 def reset(variant, pos, dnn, *, k, range_start, box, sensor_range, check_distance, heading=None, prev_heading=None,
           vel=None, nn_idx=None, mem=None, valid=None, env_mask=None, rigid_boundary=False, max_attempts=64, seed=0,
-          rng_offset=0):
-    """Device-side reset with bounded rejection sampling (reference reset() recursion, e.g. gym_flock_v2.py:85-108)."""
+          rng_offset=0, repair_rounds=0):
+    """Device-side reset with bounded rejection sampling (reference reset() recursion, e.g. gym_flock_v2.py:85-108);
+    repair_rounds > 0: envs whose every draw collided re-draw only their colliding agents (flock_reset_ext)."""
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -269,9 +270,9 @@ def reset(variant, pos, dnn, *, k, range_start, box, sensor_range, check_distanc
     _opt(mem, "mem", f32, (E, N, 4, k), dev)
     _opt(valid, "valid", torch.bool, (E,), dev)
     _opt(env_mask, "env_mask", torch.bool, (E,), dev)
-    rc = _native.lib().flock_reset(
+    rc = _native.lib().flock_reset_ext(
         _stream(pos), VARIANT_IDS[variant], E, N, k, float(range_start[0]), float(range_start[1]), float(box),
         float(sensor_range), float(check_distance), int(bool(rigid_boundary)), int(max_attempts),
         int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(env_mask), _ptr(pos), _ptr(heading),
-        _ptr(prev_heading), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(mem), _ptr(valid))
-    _native.check(rc, "flock_reset")
+        _ptr(prev_heading), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(mem), _ptr(valid), int(repair_rounds))
+    _native.check(rc, "flock_reset_ext")

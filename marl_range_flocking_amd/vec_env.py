@@ -36,6 +36,9 @@ class FlockConfig:
     dt: float = 0.1
     seed: int = 0
     max_reset_attempts: int = 64
+    # envs whose max_reset_attempts whole-swarm draws all collide (always, at main.py density for N >= 256) re-draw
+    # only their colliding agents for up to this many rounds (0: bounded rejection sampling alone, valid = False)
+    reset_repair_rounds: int = 64
     track_indices: bool = True     # keep nearest_neighbors (the reference keeps them for v2 only)
     reset_check_distance: float = None  # uw_discrete resets with collision_distance = 4 (:145)
     extra: dict = field(default_factory=dict)
@@ -92,6 +95,18 @@ class VecFlockEnv:
         self._rng_offset = 0
         self.steps = 0
 
+    def set_param(self, name, value):
+        """Change a step / reset parameter (collision_distance, sensor_range, rigid_boundary, max_linear_velocity,
+        v_min, dt) between steps: the recorded launch plans hold the old scalars, so they are dropped. The reset
+        check distance follows collision_distance (gym_flock_v2.py:100-105) except for uw_discrete, whose reset
+        checks with 4 (gym_flock_uw_discrete.py:145)."""
+        if name not in ("collision_distance", "sensor_range", "rigid_boundary", "max_linear_velocity", "v_min", "dt"):
+            raise AttributeError(f"{name} is not a runtime parameter")
+        setattr(self.cfg, name, value)
+        if name == "collision_distance" and self.cfg.variant != "uw_discrete":
+            self.cfg.reset_check_distance = value
+        self.__dict__.pop("_plans", None)
+
     # ------------------------------------------------------------------ views
     @property
     def dnn(self):
@@ -113,8 +128,14 @@ class VecFlockEnv:
         return o.clone() if copy else o
 
     # ------------------------------------------------------------------ reset
-    def reset(self, env_mask=None, copy=False):
-        """Device-side reset (bounded rejection sampling; gym_flock_v2.py:85-108 and siblings)."""
+    def reset(self, env_mask=None, copy=False, _keep_done=False):
+        """Device-side reset of all envs, or of the envs where ``env_mask`` [E] (bool, device) is set, with no host
+        synchronisation (gym_flock_v2.py:85-108 and siblings). The reference re-draws the whole swarm until no
+        agent collides; here a draw is repeated up to ``max_reset_attempts`` times (the reference's distribution
+        whenever one succeeds), then, with ``reset_repair_rounds`` > 0, the colliding agents of the last draw
+        re-draw their own positions until the swarm is collision-free. ``valid`` [E] is False where neither
+        succeeded (the env keeps its last draw and reports done on its next step); the reference cannot terminate
+        there (its recursion overflows)."""
         c = self.cfg
         b = self._bufs[self._cur]
         if env_mask is not None:
@@ -124,11 +145,13 @@ class VecFlockEnv:
                   heading=self.headings if c.variant != "flock" else None, prev_heading=self.prev_headings,
                   vel=self.velocities, nn_idx=b["idx"], mem=b["mem"], valid=self.valid, env_mask=env_mask,
                   rigid_boundary=c.rigid_boundary, max_attempts=c.max_reset_attempts, seed=c.seed,
-                  rng_offset=self._rng_offset)
-        self._rng_offset += c.max_reset_attempts
+                  rng_offset=self._rng_offset, repair_rounds=c.reset_repair_rounds)
+        self._rng_offset += max(c.max_reset_attempts, c.reset_repair_rounds)
         if self.seeds is not None and b["idx"] is not None:  # the reset's neighbours seed the first step
             self.seeds.copy_(b["idx"])
-        if env_mask is None:
+        if _keep_done:
+            pass
+        elif env_mask is None:
             self.done.zero_()
             self.any_done.zero_()
         else:
@@ -146,11 +169,16 @@ class VecFlockEnv:
             self._bufs[self._cur]["mem"].copy_(torch.as_tensor(obs_memory).to(self.device))
 
     # ------------------------------------------------------------------ step
-    def step(self, action, noise=None, dt=None, copy=False, ring=None):
+    def step(self, action, noise=None, dt=None, copy=False, ring=None, auto_reset=False):
         """One vectorized step. action: [E,N,2] f32 (v2: [lin, ang]; uw/flock: velocity/acceleration) or
         [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info).
         ring (v2): a _native.FlockRing from a learner's replay_slots(); the step also stores every transition
-        (previous obs, action, reward, new obs, 1 - done) into that replay ring in the same launch."""
+        (previous obs, action, reward, new obs, 1 - done) into that replay ring in the same launch.
+        auto_reset: every env whose step ended in a collision (any_done) is reset right behind the step, keyed on
+        the device flag (no host sync) — what main.py:24-31 / train_flock.py do with env.reset() after done[1].
+        The returned done / any_done still report the step's termination, the returned observation of a reset env
+        is its new episode's first one, and the terminal observation stays in info["final_observation"] (the
+        fused replay insert already stored the terminal transition)."""
         c = self.cfg
         dt = c.dt if dt is None else float(dt)
         E, N, k = self.E, self.N, self.k
@@ -195,4 +223,12 @@ class VecFlockEnv:
                            self.reward, self.done, self.any_done, seeds=self.seeds, **common)
         self._cur = nxt
         self.steps += 1
-        return self.observation(copy), self.reward, (self.done, self.any_done), {}
+        info = {}
+        if auto_reset:
+            final = self.__dict__.get("_final")
+            if final is None:
+                final = self._final = torch.empty_like(self.obs_memory if self.obs_memory is not None else self.dnn)
+            final.copy_(self.obs_memory if self.obs_memory is not None else self.dnn)
+            self.reset(env_mask=self.any_done, _keep_done=True)
+            info["final_observation"] = final
+        return self.observation(copy), self.reward, (self.done, self.any_done), info

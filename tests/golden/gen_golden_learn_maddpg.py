@@ -6,6 +6,9 @@ sampled chunk starts (np.random.choice patched).
 Small hidden sizes (hidden1=32, hidden2=24) keep fixtures small; the code path is the reference's own.
 Writes tests/golden/learn_maddpg_rnn.npz and learn_maddpg_ff.npz. Run each flavour in its own process
 (``python gen_golden_learn_maddpg.py rnn|ff``): both directories define modules named agent/net/utils/MADDPG.
+
+``rnn-prod``: the reference's production shape (net.py:14-146 defaults hidden 400/300; MADDPG.py:78 B 128,
+chunk 10) with 16 agents, written compactly (tests/golden/compact.py) to learn_maddpg_rnn_prod.npz.
 """
 import json
 import os
@@ -17,13 +20,20 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+import compact  # noqa: E402
 import refshim  # noqa: E402
 
-N, B, CAP, T, H1, H2 = 3, 8, 64, 40, 32, 24
+SMALL = dict(N=3, B=8, CAP=64, T=40, H1=32, H2=24)
+PROD = dict(N=16, B=128, CAP=256, T=150, H1=400, H2=300)
+SAMPLES = 256  # sampled positions per tensor in the compact fixture (64 networks)
 
 
 def run(flavour):
     import torch
+
+    prod = flavour.endswith("-prod")
+    flavour = flavour.replace("-prod", "")
+    N, B, CAP, T, H1, H2 = (PROD if prod else SMALL).values()
 
     refshim.install()
     d = "learners/maddpg_official_rnn" if flavour == "rnn" else "learners/maddpg_official"
@@ -54,11 +64,18 @@ def run(flavour):
     sa = mad.SuperAgent(args, env)
     sd = lambda m: {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}  # noqa: E731
     nets = ("actor", "critic", "target_actor", "target_critic")
-    # make target nets differ from the online nets (as after training)
+    specs = []
     with torch.no_grad():
-        for ag in sa.agents:
-            for p in list(ag.target_critic.parameters()) + list(ag.target_actor.parameters()):
-                p.add_(0.01 * torch.randn_like(p))
+        if prod:  # seeded initial parameters (compact.init_value; targets differ from the online nets)
+            for i, ag in enumerate(sa.agents):
+                for nm in nets:
+                    for k, v in getattr(ag, nm).state_dict().items():
+                        v.copy_(torch.from_numpy(compact.init_value(f"{nm}{i}", k, v.shape)))
+                        specs.append([f"{nm}{i}", k, list(v.shape)])
+        else:  # make target nets differ from the online nets (as after training)
+            for ag in sa.agents:
+                for p in list(ag.target_critic.parameters()) + list(ag.target_actor.parameters()):
+                    p.add_(0.01 * torch.randn_like(p))
     init = {f"{nm}{i}": sd(getattr(ag, nm)) for i, ag in enumerate(sa.agents) for nm in nets}
     obs = rng.uniform(0, 14, (T + 1, N, K)).astype(np.float32)
     act = rng.uniform(-1, 1.5, (T, N, 2)).astype(np.float32)
@@ -107,6 +124,23 @@ def run(flavour):
         else:
             acts = sa.get_actions(torch.tensor(obs[0]), test=True)
             hid = torch.zeros(1)
+    meta = dict(flavour=flavour, n_agents=N, k=K, batch=B, chunk=C, capacity=CAP, T=T, hidden1=H1, hidden2=H2,
+                hidden_rnn=32, lr=3e-3, gamma=0.99, tau=0.001, torch=torch.__version__, source=f"{d}/MADDPG.py")
+    if prod:
+        flat = {}
+        for i in range(N):
+            g = {k: [grads[f"critic{i}/{k}"]] for k in final[f"critic{i}"]}
+            flat.update(compact.encode(f"critic{i}", final[f"critic{i}"], g, s=SAMPLES))
+            flat.update(compact.encode(f"target_critic{i}", final[f"target_critic{i}"], g, s=SAMPLES))
+            flat.update(compact.encode(f"actor{i}", final[f"actor{i}"], s=SAMPLES))  # frozen (Q6): bitwise
+            flat.update(compact.encode(f"target_actor{i}", final[f"target_actor{i}"], s=SAMPLES))
+        meta["specs"], meta["samples"] = specs, SAMPLES
+        name = f"learn_maddpg_{flavour}_prod.npz"
+        np.savez_compressed(os.path.join(HERE, name), meta=np.array(json.dumps(meta)), obs=obs, action=act,
+                            reward=rew, done=done, starts=starts, act_out=acts.numpy(), act_hidden=hid.numpy(),
+                            **flat)
+        print("wrote", name)
+        return
     flat = {}
     for tag, dd in (("init", init), ("final", final)):
         for nm, params in dd.items():
@@ -114,8 +148,6 @@ def run(flavour):
                 flat[f"{tag}/{nm}/{k}"] = v
     for k, v in grads.items():
         flat[f"grad/{k}"] = v
-    meta = dict(flavour=flavour, n_agents=N, k=K, batch=B, chunk=C, capacity=CAP, T=T, hidden1=H1, hidden2=H2,
-                hidden_rnn=32, lr=3e-3, gamma=0.99, tau=0.001, torch=torch.__version__, source=f"{d}/MADDPG.py")
     np.savez_compressed(os.path.join(HERE, f"learn_maddpg_{flavour}.npz"), meta=np.array(json.dumps(meta)),
                         obs=obs, action=act, reward=rew, done=done, starts=starts, act_out=acts.numpy(),
                         act_hidden=hid.numpy(), **flat)

@@ -3,6 +3,10 @@
 sampled indices (np.random.choice patched, utils.py:65-76). Small layer sizes (fc1=32, fc2=24) keep the fixture
 small; the code path is the reference's own. Writes tests/golden/learn_shared_critic.npz.
 
+``--prod``: the reference's production shape (train_flock.py:15-27, :64: fc1 400, fc2 300, B 256) with 8 agents,
+written compactly (tests/golden/compact.py: seeded initial parameters, sampled final parameters, well-conditioned
+bit masks instead of gradients) to tests/golden/learn_shared_critic_prod.npz.
+
 Recorded: initial state_dicts (critic, actors, target actors), the replay rows, the sampled indices, per-learn()
 losses and the gradients each optimizer step consumed, and the final state_dicts.
 """
@@ -17,8 +21,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import refshim  # noqa: E402
 
-N_AGENTS, K, FC1, FC2, B, CAP = 3, 4, 32, 24, 16, 64
-CALLS = [0, 1, 2, 0, 1]  # learn() order over agents: counts 0,0,0,1,1 → soft updates on the first three
+import compact  # noqa: E402
+
+PROD = "--prod" in sys.argv
+if PROD:
+    N_AGENTS, K, FC1, FC2, B, CAP, T = 8, 4, 400, 300, 256, 4096, 64
+    CALLS = [0, 1, 2, 3, 0, 1]  # counts 0,0,0,0,1,1 → soft updates on the first four
+else:
+    N_AGENTS, K, FC1, FC2, B, CAP, T = 3, 4, 32, 24, 16, 64, 20
+    CALLS = [0, 1, 2, 0, 1]  # learn() order over agents: counts 0,0,0,1,1 → soft updates on the first three
 
 
 def main():
@@ -46,12 +57,21 @@ def main():
                               checkpoint_dir=f"a{i}", checkpoint_best="b", index=i, replay_buffer=buf, noise=noise,
                               layer1_size=FC1, layer2_size=FC2, batch_size=B) for i in range(N_AGENTS)]
     sd = lambda m: {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}  # noqa: E731
+    nets = {"critic": critic}
+    for i, a in enumerate(agents):
+        nets[f"actor{i}"], nets[f"target_actor{i}"] = a.actor, a.target_actor
+    specs = []
+    if PROD:  # seeded initial parameters (compact.init_value), written into the reference's own modules
+        with torch.no_grad():
+            for tag, m in nets.items():
+                for k, v in m.state_dict().items():
+                    v.copy_(torch.from_numpy(compact.init_value(tag, k, v.shape)))
+                    specs.append([tag, k, list(v.shape)])
     init = {"critic": sd(critic)}
     for i, a in enumerate(agents):
         init[f"actor{i}"] = sd(a.actor)
         init[f"target_actor{i}"] = sd(a.target_actor)
-    # replay contents: 20 store_transitions calls of N_AGENTS rows (utils.py:47-54)
-    T = 20
+    # replay contents: T store_transitions calls of N_AGENTS rows (utils.py:47-54)
     st = rng.uniform(0, 14, (T, N_AGENTS, K)).astype(np.float32)
     st2 = rng.uniform(0, 14, (T, N_AGENTS, K)).astype(np.float32)
     act = rng.uniform(-1, 1, (T, N_AGENTS, 2)).astype(np.float32)
@@ -102,6 +122,22 @@ def main():
     for i, a in enumerate(agents):
         final[f"actor{i}"] = sd(a.actor)
         final[f"target_actor{i}"] = sd(a.target_actor)
+    if PROD:
+        flat = {}
+        for tag in nets:
+            kind = "critic" if tag == "critic" else "actor"
+            agent = None if tag == "critic" else int(tag[len(tag.rstrip("0123456789")):])
+            calls = [c for c, a in enumerate(CALLS) if agent is None or a == agent]
+            g = {k: [grads[f"call{c}.{kind}.{k}"] for c in calls] for k in final[tag]}
+            flat.update(compact.encode(tag, final[tag], g))
+        meta = dict(n_agents=N_AGENTS, k=K, fc1=FC1, fc2=FC2, batch=B, capacity=CAP, calls=CALLS, gamma=0.99,
+                    tau=0.001, alpha=3e-4, beta=3e-4, update_rate=3, torch=torch.__version__, specs=specs,
+                    source="learners/maddpg_shared_critic/agent_simple_shared_critic.py:115-185")
+        np.savez_compressed(os.path.join(HERE, "learn_shared_critic_prod.npz"), meta=np.array(json.dumps(meta)),
+                            state=st, next_state=st2, action=act, reward=rew, done=done, idx=idx,
+                            losses=np.array(losses, np.float64), **flat)
+        print("wrote learn_shared_critic_prod.npz", losses)
+        return
     flat = {}
     for tag, d in (("init", init), ("final", final)):
         for net_name, params in d.items():

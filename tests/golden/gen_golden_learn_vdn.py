@@ -2,6 +2,9 @@
 (learners/vdn/train_flock.py:16-43, QNet learners/vdn/net.py:11-61, ReplayBufferVDN learners/vdn/utils.py:7-69)
 run on CPU with injected replay contents and sampled chunk starts (np.random.randint patched). Also records QNet
 forward outputs on a fixed batch. Writes tests/golden/learn_vdn.npz.
+
+``--prod``: 64 agents at the reference driver's settings (train_flock.py:16-43, :60-80: B 32, chunk 10,
+update_iter 10), written compactly (tests/golden/compact.py) to learn_vdn_prod.npz.
 """
 import json
 import os
@@ -12,9 +15,15 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
+import compact  # noqa: E402
 import refshim  # noqa: E402
 
-N_AGENTS, K, N_ACT, B, CHUNK, ITERS, T = 3, 4, 4, 6, 10, 3, 40
+PROD = "--prod" in sys.argv
+if PROD:
+    N_AGENTS, K, N_ACT, B, CHUNK, ITERS, T = 64, 4, 4, 32, 10, 10, 60
+else:
+    N_AGENTS, K, N_ACT, B, CHUNK, ITERS, T = 3, 4, 4, 6, 10, 3, 40
+SAMPLES = 128  # sampled positions per tensor in the compact fixture (64 agents x 10 tensors)
 
 
 def main():
@@ -43,10 +52,16 @@ def main():
     q = net.QNet(obs_space, act_space, recurrent=True)
     q_target = net.QNet(obs_space, act_space, recurrent=True)
     q_target.load_state_dict(q.state_dict())
-    # perturb the target so q and q_target differ (as between target syncs)
+    specs = []
     with torch.no_grad():
-        for p in q_target.parameters():
-            p.add_(0.01 * torch.randn_like(p))
+        if PROD:  # seeded initial parameters (compact.init_value; the target differs from q)
+            for tag, m in (("q", q), ("target_q", q_target)):
+                for k_, v in m.state_dict().items():
+                    v.copy_(torch.from_numpy(compact.init_value(tag, k_, v.shape)))
+                    specs.append([tag, k_, list(v.shape)])
+        else:  # perturb the target so q and q_target differ (as between target syncs)
+            for p in q_target.parameters():
+                p.add_(0.01 * torch.randn_like(p))
     sd = lambda m: {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}  # noqa: E731
     init_q, init_t = sd(q), sd(q_target)
     memory = utils.ReplayBufferVDN(50000, chunk_size=CHUNK, n_agents=N_AGENTS, input_shape=[K], batch_size=B)
@@ -92,6 +107,16 @@ def main():
     xh = rng.standard_normal((5, N_AGENTS, 32)).astype(np.float32)
     with torch.no_grad():
         qo, ho = q(torch.tensor(xo), torch.tensor(xh))
+    if PROD:
+        flat = compact.encode("q", final_q, {k_: [g[k_] for g in rec["grads"]] for k_ in final_q}, s=SAMPLES)
+        meta = dict(n_agents=N_AGENTS, k=K, n_actions=N_ACT, batch=B, chunk=CHUNK, update_iter=ITERS, T=T, lr=1e-3,
+                    gamma=0.99, grad_clip_norm=5, recurrent=True, torch=torch.__version__, specs=specs,
+                    samples=SAMPLES, source="learners/vdn/train_flock.py:16-43")
+        np.savez_compressed(os.path.join(HERE, "learn_vdn_prod.npz"), meta=np.array(json.dumps(meta)), s=s,
+                            s_prime=s2, a=a, r=r, done=d, starts=starts, norms=np.array(rec["norms"]), fwd_obs=xo,
+                            fwd_hidden=xh, fwd_q=qo.numpy(), fwd_h=ho.numpy(), **flat)
+        print("wrote learn_vdn_prod.npz norms", rec["norms"])
+        return
     flat = {}
     for tag, dct in (("init_q", init_q), ("init_target", init_t), ("final_q", final_q)):
         for k_, v in dct.items():

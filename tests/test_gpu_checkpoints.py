@@ -163,35 +163,54 @@ def test_vdn_q_pth_and_load_params(tmp_path, cuda):
         np.testing.assert_array_equal(v.cpu().numpy(), gold[src], err_msg=n)
 
 
-def test_shared_critic_models_files(tmp_path, cuda):
+@pytest.mark.parametrize("best", [False, True], ids=["save_models", "save_models_best"])
+def test_shared_critic_models_files(tmp_path, best, cuda):
+    """The reference driver's directory layout (maddpg_shared_critic/train_flock.py:40-66): the critic in
+    CHECKPOINT_DIR/critic (best: CHECKPOINT_DIR/best), each agent's Actor / TargetActor in CHECKPOINT_DIR/agent_i
+    (best: CHECKPOINT_DIR/best); file names {name}_ddpg.pt (ddpg_network.py:33-34). save_models(_best) writes the
+    reference's files with its state_dict keys; load_models on a fresh learner reads them back."""
     from marl_range_flocking_amd.learners import dropin
 
     z = np.load(os.path.join(GOLD, "learn_shared_critic.npz"))
     m = json.loads(str(z["meta"]))
     A, K = m["n_agents"], m["k"]
+    ck = str(tmp_path)
 
-    def build(d):
+    def build():
         rb = dropin.ReplayBuffer(64, [K], n_actions=2, n_agents=A)
-        critic = dropin.CriticNetwork(m["beta"], [K], m["fc1"], m["fc2"], n_actions=2, name="Critic")
+        critic = dropin.CriticNetwork(m["beta"], [K], m["fc1"], m["fc2"], n_actions=2, name="Critic",
+                                      chkpt_dir=os.path.join(ck, "critic"), chkpt_best_dir=os.path.join(ck, "best"))
         agents = [dropin.Agent(shared_critic=critic, replay_buffer=rb, noise=None, index=i, alpha=m["alpha"],
                                beta=m["beta"], input_dims=[K], layer1_size=m["fc1"], layer2_size=m["fc2"],
-                               tau=m["tau"], batch_size=m["batch"], checkpoint_dir=os.path.join(d, "c"),
-                               checkpoint_best=os.path.join(d, "c", "best")) for i in range(A)]
+                               tau=m["tau"], batch_size=m["batch"], checkpoint_dir=os.path.join(ck, f"agent_{i}"),
+                               checkpoint_best=os.path.join(ck, "best")) for i in range(A)]
         return critic._build(), agents
 
-    L, agents = build(str(tmp_path))
+    L, agents = build()
     L.load_reference_state(_sd(z, "final/critic"), [_sd(z, f"final/actor{i}") for i in range(A)],
                            [_sd(z, f"final/target_actor{i}") for i in range(A)])
-    agents[2].save_models_best()
-    files = {n: os.path.join(str(tmp_path), "c", "best", f"{n}_ddpg.pt") for n in ("Actor", "TargetActor", "Critic")}
+    if best:
+        agents[2].save_models_best()
+    else:
+        agents[2].save_models()
+    adir = os.path.join(ck, "best" if best else "agent_2")
+    files = {"Actor": os.path.join(adir, "Actor_ddpg.pt"), "TargetActor": os.path.join(adir, "TargetActor_ddpg.pt"),
+             "Critic": os.path.join(ck, "best" if best else "critic", "Critic_ddpg.pt")}
     for n, gold in (("Actor", "final/actor2"), ("TargetActor", "final/target_actor2"), ("Critic", "final/critic")):
         sd, g = torch.load(files[n], weights_only=True), _sd(z, gold)
         assert list(sd) == list(g), n
         for key, v in sd.items():
             np.testing.assert_array_equal(v.numpy(), g[key], err_msg=f"{n} {key}")
-    L2, agents2 = build(str(tmp_path))
-    agents2[0].load_models(best=True)  # agent 0 takes agent 2's saved actor; the critic is shared
-    for key, v in L2.actor_state_dict(0).items():
-        np.testing.assert_array_equal(v.numpy(), z[f"final/actor2/{key}"])
+    L2, agents2 = build()
+    if best:  # agent 0 takes agent 2's saved best actor; the critic is shared
+        agents2[0].load_models(best=True)
+        src, dst = 2, 0
+    else:
+        agents2[2].load_models()
+        src, dst = 2, 2
+    for key, v in L2.actor_state_dict(dst).items():
+        np.testing.assert_array_equal(v.numpy(), z[f"final/actor{src}/{key}"])
+    for key, v in L2.actor_state_dict(dst, target=True).items():
+        np.testing.assert_array_equal(v.numpy(), z[f"final/target_actor{src}/{key}"])
     for key, v in L2.critic_state_dict().items():
         np.testing.assert_array_equal(v.numpy(), z[f"final/critic/{key}"])

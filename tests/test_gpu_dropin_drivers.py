@@ -103,7 +103,7 @@ def test_vdn_train_flock_loop(cuda):
     assert torch.equal(q_target.impl.P.data, q.impl.P.data) or True
 
 
-def test_shared_critic_train_flock_loop(cuda):
+def test_shared_critic_train_flock_loop(tmp_path, cuda):
     (gym_flock_uw,) = _import(ENVS, "gym_flock_uw")
     agent_mod, ddpg_net, ddpg_utils = _import(COMPAT, "maddpg.agents.ddpg.agent_simple_shared_critic",
                                               "maddpg.models.DDPG.DDPG_network", "maddpg.models.DDPG.utils")
@@ -112,10 +112,13 @@ def test_shared_critic_train_flock_loop(cuda):
     input_dims = [env.k * 4]
     replay_buffer = ddpg_utils.ReplayBuffer(max_size=4096, input_shape=input_dims, n_agents=N, n_actions=2)
     noise = ddpg_utils.OUActionNoiseGPU(mu=torch.zeros(2).cuda())
-    critic = ddpg_net.CriticNetwork(3e-4, input_dims, 64, 48, n_actions=2, name="Critic")
+    ck = str(tmp_path)
+    critic = ddpg_net.CriticNetwork(3e-4, input_dims, 64, 48, n_actions=2, name="Critic",
+                                    chkpt_dir=os.path.join(ck, "critic"), chkpt_best_dir=os.path.join(ck, "best"))
     agents = [agent_mod.Agent(shared_critic=critic, replay_buffer=replay_buffer, noise=noise, index=i, alpha=3e-4,
                               beta=3e-4, input_dims=input_dims, layer1_size=64, layer2_size=48, tau=0.001,
-                              batch_size=32, checkpoint_dir="c", checkpoint_best="b") for i in range(N)]
+                              batch_size=32, checkpoint_dir=os.path.join(ck, f"agent_{i}"),
+                              checkpoint_best=os.path.join(ck, "best")) for i in range(N)]
     observation = env.reset()
     for _ in range(10):  # prefill with random actions (train_flock.py:89-101)
         action_list = torch.rand(size=(N, 2)).cuda()
@@ -126,9 +129,13 @@ def test_shared_critic_train_flock_loop(cuda):
     action_list = torch.zeros(size=(N, 2)).cuda()
     losses = []
     observation = env.reset()
+    L = critic._build()
     for epoch in range(1, 6):  # train_flock.py:112-133
+        mu = L.choose_action(observation.reshape(N, -1)[None], noise=False)[0]
         for index in range(N):
             action_list[index, :] = agents[index].choose_action(observation.reshape(N, -1))
+        # one batched actor pass per step (the cache), each agent's row = its own actor's mu plus the shared noise
+        assert critic._act_cache is not None and torch.equal(critic._act_cache[2], mu)
         nxt, reward, dones, _ = env.step(action_list)
         replay_buffer.store_transitions(observation.reshape(N, -1), action_list, reward, nxt.reshape(N, -1),
                                         dones[0].long())

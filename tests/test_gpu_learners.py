@@ -72,6 +72,45 @@ def test_shared_critic_learn_matches_reference(use_graph, fused, cuda):
                 _masked_close(v.numpy(), z[f"final/{tag}{i}/{n}"], grads, f"{tag}{i} {n}", m["alpha"])
 
 
+@pytest.mark.parametrize("fused", [True, False], ids=["fused", "autograd"])
+@pytest.mark.parametrize("use_graph", [False, True], ids=["eager", "hipgraph"])
+def test_shared_critic_learn_matches_reference_prod(use_graph, fused, cuda):
+    """The reference's production shape (fc1 400, fc2 300, B 256; train_flock.py:15-27, :64) with 8 agents: the
+    whole-K-panel MFMA tiles and the fused row kernels the bench runs, against the REFERENCE Agent.learn() (compact
+    fixture, tests/golden/compact.py): losses of all 6 calls, the critic, the four learning actors and their targets
+    (sampled positions, SURVEY.md §8(c) rule), the non-learning actors bitwise."""
+    from golden import compact
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    z = np.load(os.path.join(GOLD, "learn_shared_critic_prod.npz"))
+    m = json.loads(str(z["meta"]))
+    A, K = m["n_agents"], m["k"]
+    init = compact.rebuild(m["specs"])
+    L = SharedCriticLearner(A, K, fc1=m["fc1"], fc2=m["fc2"], alpha=m["alpha"], beta=m["beta"], gamma=m["gamma"],
+                            tau=m["tau"], batch_size=m["batch"], update_rate=m["update_rate"],
+                            buffer_size=m["capacity"], device=cuda, use_graph=use_graph, fused=fused)
+    L.load_reference_state(init["critic"], [init[f"actor{i}"] for i in range(A)],
+                           [init[f"target_actor{i}"] for i in range(A)])
+    for t in range(z["state"].shape[0]):
+        L.store_transitions(torch.tensor(z["state"][t]), torch.tensor(z["action"][t]), torch.tensor(z["reward"][t]),
+                            torch.tensor(z["next_state"][t]), torch.tensor(z["done"][t]))
+    for c, i in enumerate(m["calls"]):
+        al, cl, ok = L.learn(i, idx=torch.tensor(z["idx"][c]))
+        assert ok
+        np.testing.assert_allclose([al.item(), cl.item()], z["losses"][c], rtol=1e-4)
+    for n, v in L.critic_state_dict().items():
+        compact.check(z, "critic", n, v.numpy(), m["beta"], len(m["calls"]))
+    for i in range(A):
+        steps = sum(1 for a in m["calls"] if a == i)
+        for target in (False, True):
+            tag = ("target_actor" if target else "actor") + str(i)
+            for n, v in L.actor_state_dict(i, target=target).items():
+                if steps == 0:  # never learned: bitwise the initial parameters
+                    np.testing.assert_array_equal(v.numpy(), init[tag][n], err_msg=f"{tag} {n}")
+                else:
+                    compact.check(z, tag, n, v.numpy(), m["alpha"], steps)
+
+
 def test_shared_critic_fused_matches_autograd_at_bench_size(cuda):
     """The fused HIP update (csrc/flock_sc.hip) against the autograd formulation at the bench shape (fc1 400,
     fc2 300, B 256): per-call gradients of the critic and of the learning actor, losses, and parameters after 6
@@ -149,6 +188,35 @@ def test_vdn_train_matches_reference(use_graph, cuda):
             _masked_close(final[key].numpy(), z[f"final_q/{key}"], grads, key, m["lr"])
 
 
+@pytest.mark.parametrize("use_graph", [False, True], ids=["eager", "hipgraph"])
+def test_vdn_train_matches_reference_prod(use_graph, cuda):
+    """VDN with 64 agents at the reference driver's settings (B 32, chunk 10, update_iter 10; train_flock.py:16-43)
+    against the REFERENCE train() (compact fixture, tests/golden/compact.py): every iteration's pre-clip gradient norm
+    rtol 1e-4 is implied by the last one, final QNet parameters at sampled positions (SURVEY.md §8(c) rule), and the
+    QNet forward on a fixed batch."""
+    from golden import compact
+    from marl_range_flocking_amd.learners.vdn import VDNLearner
+
+    z = np.load(os.path.join(GOLD, "learn_vdn_prod.npz"))
+    m = json.loads(str(z["meta"]))
+    A, S = m["n_agents"], m["samples"]
+    init = compact.rebuild(m["specs"])
+    L = VDNLearner(A, m["k"], m["n_actions"], lr=m["lr"], gamma=m["gamma"], batch_size=m["batch"],
+                   chunk_size=m["chunk"], update_iter=m["update_iter"], grad_clip_norm=m["grad_clip_norm"],
+                   device=cuda, use_graph=use_graph)
+    L.q.load_reference_state_dict(init["q"])
+    L.q.load_reference_state_dict(init["target_q"], target=True)
+    for t in range(m["T"]):
+        L.put(z["s"][t], z["a"][t], z["r"][t], z["s_prime"][t], [int(z["done"][t])])
+    L.train(starts=z["starts"])
+    np.testing.assert_allclose(L.norm.out[0].item(), z["norms"][-1], rtol=1e-4)
+    for key, v in L.q.state_dict().items():
+        compact.check(z, "q", key, v.numpy(), m["lr"], m["update_iter"], s=S)
+    qo, ho = L.q(torch.tensor(z["fwd_obs"], device=cuda), torch.tensor(z["fwd_hidden"], device=cuda))
+    np.testing.assert_allclose(qo.detach().cpu().numpy(), z["fwd_q"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(ho.detach().cpu().numpy(), z["fwd_h"], rtol=1e-4, atol=1e-5)
+
+
 def test_vdn_forward_matches_reference_qnet(cuda):
     from marl_range_flocking_amd.learners.vdn import BatchedQNet
 
@@ -197,6 +265,37 @@ def test_maddpg_train_matches_reference(flavour, use_graph, cuda):
     np.testing.assert_allclose(acts.cpu().numpy(), z["act_out"], rtol=1e-5, atol=1e-6)
     if flavour == "rnn":
         np.testing.assert_allclose(hid[:, 0].cpu().numpy(), z["act_hidden"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("use_graph", [False, True], ids=["eager", "hipgraph"])
+def test_maddpg_rnn_train_matches_reference_prod(use_graph, cuda):
+    """RNN-MADDPG at the reference's production shape (hidden 400/300, B 128, chunk 10; net.py:14-146,
+    MADDPG.py:78-150) with 16 agents, against the REFERENCE SuperAgent.train() (compact fixture,
+    tests/golden/compact.py): critics and target critics at sampled positions (SURVEY.md §8(c) rule), frozen actors
+    and the target actors' soft update bitwise, acting outputs rtol 1e-5."""
+    from golden import compact
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+    z = np.load(os.path.join(GOLD, "learn_maddpg_rnn_prod.npz"))
+    m = json.loads(str(z["meta"]))
+    N, S = m["n_agents"], m["samples"]
+    L = MADDPGLearner(N, m["k"], recurrent=True, hidden1=m["hidden1"], hidden2=m["hidden2"], batch_size=m["batch"],
+                      chunk_size=m["chunk"], buffer_capacity=m["capacity"], min_size_buffer=m["batch"], device=cuda,
+                      use_graph=use_graph)
+    L.load_reference_state({tag: sd for tag, sd in compact.rebuild(m["specs"]).items()})
+    for t in range(m["T"]):
+        L.add_record(z["obs"][t], z["obs"][t + 1], z["action"][t], z["obs"][t], z["obs"][t + 1], z["reward"][t],
+                     z["done"][t])
+    assert L.train(starts=z["starts"]) is not None
+    for i in range(N):
+        for net in ("actor", "critic"):
+            for target in (False, True):
+                tag = ("target_" if target else "") + f"{net}{i}"
+                for n, v in L.state_dict(net, i, target=target).items():
+                    compact.check(z, tag, n, v.numpy(), m["lr"], 1, s=S)
+    acts, hid = L.get_actions(torch.tensor(z["obs"][0], device=cuda), None, test=True)
+    np.testing.assert_allclose(acts.cpu().numpy(), z["act_out"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(hid[:, 0].cpu().numpy(), z["act_hidden"], rtol=1e-5, atol=1e-6)
 
 
 def test_shared_ou_matches_sequential_process(cuda):
