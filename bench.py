@@ -12,10 +12,19 @@ shared-critic replay ring inside that same launch and runs one learn() (B=256); 
 transition and run VDN / RNN-MADDPG train() every 150 / 250 steps. Inputs (state, a pool of synthetic actions)
 are resident in HBM before the timed region starts; the first update (graph capture) happens before it.
 
-Rank 0 prints ONE JSON line. Extra fields: roofline (dominant kernel, HIP events on the launch stream; algorithmic
-bytes per agent-step from SURVEY §8(d): v2 93, uw 149, uw_discrete 69, plus the fused replay insert; PMC traffic
-from profiles/pmc_*.json), allpairs_equivalent (the all-pairs sensing work the step replaces), and cpu_baseline (the
-C oracle port on 16 host threads and on 1, a bounded sample of the same workload; N=1 only).
+Rank 0 prints ONE JSON line. Extra fields:
+  roofline      the env step kernel (the dominant kernel), timed with HIP events on its launch stream.
+                HBM side: achieved = algorithmic bytes per agent-step (v2 93, uw 149,
+                uw_discrete 69) x agent-steps per launch / kernel time, frac = achieved / 8 TB/s; the fused replay
+                insert's bytes are reported beside it (insert_bytes_per_agent_step), not in frac; traffic = measured
+                HBM bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_*.json).
+                VALU side: executed VALU lane-ops per launch (64 x SQ_INSTS_VALU, profiles/pmc_sq_*.json) / kernel
+                time / 39.3 T lane-ops/s (256 CU x 4 SIMD x 16 lanes x 2.4 GHz, non-packed). "binding" names the
+                larger of the two fractions.
+  cpu_baseline  the C oracle port on every host CPU this process may use (sched_getaffinity, capped by the
+                cgroup CPU quota) and on 1 thread, a bounded sample of the same workload; N=1 only.
+Configs 4 and 5 are 8-GPU configs: their GLOBAL env count (8192 / 16384) is split over the ranks (strong scaling);
+config 3 (the headline) keeps 4096 envs per GPU (weak scaling).
 """
 import argparse
 import json
@@ -26,13 +35,12 @@ import numpy as np
 import torch
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-VALU_PEAK_TLANEOPS = 78.6        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (f32 non-packed lane-ops/s, /1e12)
+VALU_PEAK_LANEOPS = 39.3e12      # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz: non-packed f32 lane-ops/s (packed: 78.6e12)
 BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
 # fused replay insert (flock_step_v2_store), per agent-step: + previous obs read (k=4 floats) + the ring fields
 # written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG record: state,
 # next_state, actor_state, actor_next_state 16 each + action 8 + reward 4 + done 4
 RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80}
-OPS_PER_PAIR = {True: 12, False: 7}  # algorithmic VALU ops per agent pair: periodic / Euclidean
 EV_EVERY = 4  # steps between HIP-event-timed env launches inside the timed region
 
 
@@ -42,16 +50,18 @@ def parse():
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 200; configs 4/5: 300/500, "
                                                                  "a multiple of the training cadence)")
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--envs", type=int, default=None, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's; configs 4 / 5: "
+                                                         "their global env count / world size)")
     ap.add_argument("--agents", type=int, default=None)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--variant", default=None, choices=["v2", "uw", "uw_discrete", "flock"])
     ap.add_argument("--learner", default=None, choices=["none", "shared_critic", "vdn", "maddpg_rnn"],
                     help="default: the config's learner (config 3: shared_critic)")
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5],
-                    help="BASELINE.json config (per-GPU slice): 2 uw 64x1024 env only; 3 v2 256x4096 + shared "
-                         "critic (default); 4 uw_discrete 512x1024 + VDN every 150 steps; 5 v2 1024x2048 + "
-                         "RNN-MADDPG every 250 steps. --envs/--agents/--variant/--learner override it")
+                    help="BASELINE.json config: 2 uw 64x1024 env only; 3 v2 256x4096 per GPU + shared critic "
+                         "(default); 4 uw_discrete 512x8192 (global, split over the ranks) + VDN every 150 steps; "
+                         "5 v2 1024x16384 (global) + RNN-MADDPG every 250 steps. --envs/--agents/--variant/--learner "
+                         "override it")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")
@@ -60,18 +70,24 @@ def parse():
                          "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
     args = ap.parse_args()
     c = CONFIGS[args.config]
+    args.global_split = args.envs is None and "global_envs" in c
+    if args.global_split:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if c["global_envs"] % world:
+            raise SystemExit(f"config {args.config}: {c['global_envs']} envs do not split over {world} ranks")
+        args.envs = c["global_envs"] // world
     for key in ("envs", "agents", "variant", "learner", "steps"):
         if getattr(args, key) is None:
             setattr(args, key, c[key])
     return args
 
 
-# BASELINE.json configs, per-GPU slice (configs 4 and 5 are 8-GPU configs: 8192 / 16384 envs over 8 ranks)
+# BASELINE.json configs. 2 and 3: per GPU. 4 and 5 are 8-GPU configs: a global env count split over the ranks.
 CONFIGS = {
     2: dict(variant="uw", agents=64, envs=1024, learner="none", steps=200),
     3: dict(variant="v2", agents=256, envs=4096, learner="shared_critic", steps=200),
-    4: dict(variant="uw_discrete", agents=512, envs=1024, learner="vdn", steps=300),
-    5: dict(variant="v2", agents=1024, envs=2048, learner="maddpg_rnn", steps=500),
+    4: dict(variant="uw_discrete", agents=512, global_envs=8192, learner="vdn", steps=300),
+    5: dict(variant="v2", agents=1024, global_envs=16384, learner="maddpg_rnn", steps=500),
 }
 
 
@@ -131,11 +147,33 @@ def _cpu_run(args, box, seconds, seed, E_s=8):
             return E_s * N * n, el
 
 
-def cpu_baseline(args, box, seconds, threads=16):
-    """The C oracle (oracle/flock_oracle.c) on the host: 1 thread, then `threads` threads (the GPU box's CPU share)
-    each stepping its own 8 envs; bounded sample of the same workload."""
+def host_cpus():
+    """CPUs this process may run on: the affinity mask, capped by the cgroup v2 CPU quota (a container's share of a
+    large host), and the host's CPU model string."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, model
+
+
+def cpu_baseline(args, box, seconds):
+    """The C oracle (oracle/flock_oracle.c) on the host: 1 thread, then one thread per usable host CPU, each
+    stepping its own envs; a bounded sample of the same workload."""
     from concurrent.futures import ThreadPoolExecutor
 
+    threads, model = host_cpus()
     half = seconds / 2
     s1, t1 = _cpu_run(args, box, half, 0)
     with ThreadPoolExecutor(threads) as ex:  # 32 envs per C call: the per-call Python work is negligible
@@ -143,10 +181,10 @@ def cpu_baseline(args, box, seconds, threads=16):
     steps = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     return {"value": steps / wall, "unit": "agent-steps/s", "cores": threads, "kind": "port",
-            "value_1thread": s1 / t1,
+            "value_1thread": s1 / t1, "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": f"oracle/flock_oracle.c {args.variant} step of {args.agents}-agent envs, sequential vectorized "
-                      f"steps for {half:.0f} s: 1 thread x 8 envs ({s1 / t1:.3g} agent-steps/s), {threads} threads x "
-                      f"32 envs ({steps / wall:.3g} agent-steps/s); this box's host"}
+                      f"steps for {half:.0f} s: 1 thread x 8 envs ({s1 / t1:.3g} agent-steps/s), {threads} threads "
+                      f"(the CPUs this process may use) x 32 envs ({steps / wall:.3g} agent-steps/s); {model}"}
 
 
 class VDNBench:
@@ -295,20 +333,39 @@ def main():
     total_agent_steps = world * E * N * args.steps
     value = total_agent_steps / el
     fused_ring = args.learner in RING_BYTES_PER_AGENT_STEP
-    bpa = BYTES_PER_AGENT_STEP[args.variant] + RING_BYTES_PER_AGENT_STEP.get(args.learner, 0)
-    bytes_launch = bpa * E * N
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = args.pmc or os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                        f"pmc_{args.variant}{'_ring' if fused_ring else ''}_N{N}_E{E}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    bpa = BYTES_PER_AGENT_STEP[args.variant]
+    ins = RING_BYTES_PER_AGENT_STEP.get(args.learner, 0)
+    kern_s = kern_ms * 1e-3
+    achieved = bpa * E * N / kern_s / 1e9
+    tag = f"{args.variant}{'_ring' if fused_ring else ''}_N{N}_E{E}"
+    prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+
+    def pmc(name):
+        path = os.path.join(prof, name)
+        if not os.path.exists(path):
+            return None
+        with open(path) as f:
+            return json.load(f)
+
+    pt = pmc(os.path.basename(args.pmc)) if args.pmc else pmc(f"pmc_{tag}.json")
+    traffic = pt.get("hbm_bytes_per_launch") if pt else None
+    sq = pmc(f"pmc_sq_{tag}.json")
+    valu = None
+    if sq and "SQ_INSTS_VALU" in sq:
+        lane_ops = 64.0 * sq["SQ_INSTS_VALU"]
+        valu = {"insts_per_launch": sq["SQ_INSTS_VALU"], "insts_per_wave": sq.get("valu_insts_per_wave"),
+                "lane_ops_per_s": lane_ops / kern_s, "peak": VALU_PEAK_LANEOPS, "unit": "lane-op/s",
+                "frac": lane_ops / kern_s / VALU_PEAK_LANEOPS, "source": f"profiles/pmc_sq_{tag}.json"}
+    hbm_frac = achieved / HBM_PEAK_GBS
     periodic = cfg.resolved().periodic
-    ops_launch = OPS_PER_PAIR[periodic] * (N - 1) * E * N
-    valu_t = ops_launch / (kern_ms * 1e-3) / 1e12
     c = CONFIGS[args.config]
-    is_config = (args.variant, N, E, args.learner) == (c["variant"], c["agents"], c["envs"], c["learner"])
+    is_config = (args.variant, N, args.learner) == (c["variant"], c["agents"], c["learner"]) and (
+        E == c.get("envs") or (args.global_split and E * world == c["global_envs"]))
+    workload = f"gym_flock_{args.variant} step, {N} agents x {E} envs per GPU"
+    if args.global_split:
+        workload += f" ({E * world} envs split over {world} GPU{'s' if world > 1 else ''})"
+    if is_config:
+        workload += f" (BASELINE config {args.config})"
     line = {
         "metric": "agent-steps/sec at 256 agents x 4096 envs; 1/2/4/8 MI355X",
         "value": value,
@@ -318,25 +375,25 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_split else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (uniform random positions/headings at main.py density, random actions; no checkpoints)",
         "config": {
-            "workload": f"gym_flock_{args.variant} step, {N} agents x {E} envs per GPU"
-                        + (f" (BASELINE config {args.config})" if is_config else ""),
+            "workload": workload,
             "agents": N, "envs_per_gpu": E, "k": k, "box": box, "periodic": periodic,
             "learner": ("none: env step only" if hook is None else hook.describe()),
             "parallelism": f"env-shard x{world}",
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": hbm_frac, "traffic": traffic,
                      "kernel": f"step_kernel<{k + 2},{'periodic' if periodic else 'euclidean'}"
                                f"{',cells' if N >= 128 else ''}>" + (" + fused replay insert" if fused_ring else ""),
-                     "kernel_ms": kern_ms, "bytes_per_agent_step": bpa},
-        "allpairs_equivalent": {"rate": valu_t, "unit": "Tlane-op/s", "ops_per_pair": OPS_PER_PAIR[periodic],
-                                "note": "all-pairs sensing work the step replaces per second; the cell-list kNN "
-                                        "evaluates ~36 candidates per agent instead of N-1 (DESIGN.md)"},
+                     "kernel_ms": kern_ms, "bytes_per_agent_step": bpa,
+                     "insert_bytes_per_agent_step": ins,
+                     "achieved_incl_insert": (bpa + ins) * E * N / kern_s / 1e9,
+                     "valu": valu,
+                     "binding": "valu" if valu and valu["frac"] > hbm_frac else "hbm"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, box, args.cpu_seconds)
