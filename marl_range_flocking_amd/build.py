@@ -19,6 +19,10 @@ ARCH = os.environ.get("FLOCK_OFFLOAD_ARCH", "gfx950")
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}"]
 
 
+TORCH_OPS_SRC = os.path.join(CSRC, "flock_torch.cpp")
+TORCH_OPS_LIB = os.path.join(BUILD_DIR, "libflock_torch.so")
+
+
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
@@ -43,8 +47,34 @@ def hipcc():
 FILE_FLAGS = {"flock_env.hip": ["-fno-slp-vectorize"]}
 
 
+def build_torch_ops(force=False, verbose=False):
+    """libflock_torch.so: the TORCH_LIBRARY(flock) custom ops (csrc/flock_torch.cpp), host C++ over libflock_amd.so,
+    compiled against this interpreter's torch headers and linked with rpath $ORIGIN."""
+    deps = [TORCH_OPS_SRC, LIB_PATH] + glob.glob(os.path.join(INCLUDE, "*.h"))
+    if not force and os.path.exists(TORCH_OPS_LIB) and all(os.path.getmtime(d) <= os.path.getmtime(TORCH_OPS_LIB)
+                                                           for d in deps):
+        return TORCH_OPS_LIB
+    import torch
+
+    tdir = os.path.dirname(torch.__file__)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    tmp = TORCH_OPS_LIB + ".tmp"
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+           f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}", "-I", INCLUDE,
+           "-I", os.path.join(rocm, "include"), "-I", os.path.join(tdir, "include"),
+           "-I", os.path.join(tdir, "include", "torch", "csrc", "api", "include"), TORCH_OPS_SRC, "-o", tmp,
+           "-L", BUILD_DIR, "-lflock_amd", "-L", os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch",
+           "-ltorch_cpu", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, TORCH_OPS_LIB)
+    return TORCH_OPS_LIB
+
+
 def build(force=False, verbose=False):
     if not force and not _stale():
+        build_torch_ops(False, verbose)
         return LIB_PATH
     os.makedirs(BUILD_DIR, exist_ok=True)
     objs = []
@@ -66,6 +96,7 @@ def build(force=False, verbose=False):
         print(" ".join(cmd))
     subprocess.check_call(cmd)
     os.replace(tmp, LIB_PATH)
+    build_torch_ops(True, verbose)
     return LIB_PATH
 
 

@@ -57,8 +57,22 @@ class FlockConfig:
 
 
 class VecFlockEnv:
-    def __init__(self, config: FlockConfig = None, device="cuda", **kw):
+    """launch: "torch" (default) dispatches the torch.ops.flock custom ops (csrc/flock_torch.cpp): the kernels behind
+    the PyTorch dispatcher, traceable by FakeTensor / torch.compile, and the cheaper host path (7.8-8.1 us per step
+    against 10-11 us at configs 2 / 3, tools/host_cost_ops.py); "plan" launches through the C ABI with a recorded
+    launch plan (ops.StepPlan: one ctypes call per step). Both run the same kernels with bitwise-equal results. A step
+    with a fused replay insert (ring=...) takes the C ABI path (the ring is a struct of device pointers)."""
+
+    def __init__(self, config: FlockConfig = None, device="cuda", launch="torch", **kw):
         cfg = (config or FlockConfig(**kw)).resolved()
+        if launch not in ("plan", "torch"):
+            raise ValueError('launch must be "plan" or "torch"')
+        self.launch = launch
+        self._torch_ops = None
+        if launch == "torch":
+            from . import torch_ops
+
+            self._torch_ops = torch_ops.load()
         self.cfg = cfg
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -140,12 +154,20 @@ class VecFlockEnv:
         b = self._bufs[self._cur]
         if env_mask is not None:
             env_mask = env_mask.to(device=self.device, dtype=torch.bool).contiguous()
-        ops.reset(c.variant, self.positions, b["dnn"], k=self.k, range_start=c.range_start, box=self.box,
-                  sensor_range=c.sensor_range, check_distance=c.reset_check_distance,
-                  heading=self.headings if c.variant != "flock" else None, prev_heading=self.prev_headings,
-                  vel=self.velocities, nn_idx=b["idx"], mem=b["mem"], valid=self.valid, env_mask=env_mask,
-                  rigid_boundary=c.rigid_boundary, max_attempts=c.max_reset_attempts, seed=c.seed,
-                  rng_offset=self._rng_offset, repair_rounds=c.reset_repair_rounds)
+        heading = self.headings if c.variant != "flock" else None
+        if self._torch_ops is not None:
+            self._torch_ops.reset(self.positions, b["dnn"], heading, self.prev_headings, self.velocities, b["idx"],
+                                  b["mem"], self.valid, env_mask, ops.VARIANT_IDS[c.variant], self.k,
+                                  float(c.range_start[0]), float(c.range_start[1]), self.box, c.sensor_range,
+                                  c.reset_check_distance, c.rigid_boundary, c.max_reset_attempts,
+                                  c.seed & (2**63 - 1), self._rng_offset, c.reset_repair_rounds)
+        else:
+            ops.reset(c.variant, self.positions, b["dnn"], k=self.k, range_start=c.range_start, box=self.box,
+                      sensor_range=c.sensor_range, check_distance=c.reset_check_distance, heading=heading,
+                      prev_heading=self.prev_headings, vel=self.velocities, nn_idx=b["idx"], mem=b["mem"],
+                      valid=self.valid, env_mask=env_mask, rigid_boundary=c.rigid_boundary,
+                      max_attempts=c.max_reset_attempts, seed=c.seed, rng_offset=self._rng_offset,
+                      repair_rounds=c.reset_repair_rounds)
         self._rng_offset += max(c.max_reset_attempts, c.reset_repair_rounds)
         if self.seeds is not None and b["idx"] is not None:  # the reset's neighbours seed the first step
             self.seeds.copy_(b["idx"])
@@ -169,6 +191,33 @@ class VecFlockEnv:
             self._bufs[self._cur]["mem"].copy_(torch.as_tensor(obs_memory).to(self.device))
 
     # ------------------------------------------------------------------ step
+    def _step_torch(self, T, a, noise, dt, src, dst):
+        """The step through torch.ops.flock (VecFlockEnv(launch="torch"))."""
+        c = self.cfg
+        common = (self.k, self.box)
+        if c.variant == "v2":
+            T.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
+                      self.done, self.any_done, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
+                      c.v_min, c.max_linear_velocity, c.periodic, c.rigid_boundary)
+        elif c.variant == "uw":
+            T.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
+                      dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, self.seeds, *common,
+                      c.sensor_range, c.collision_distance, dt, c.rigid_boundary)
+        elif c.variant == "uw_discrete":
+            if noise is not None:
+                noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(
+                    self.E, self.N, 2).contiguous()
+            T.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
+                               self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
+                               self.status, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
+                               c.max_linear_velocity, c.rigid_boundary, 0.1, c.seed & (2**63 - 1),
+                               self._rng_offset & (2**63 - 1))
+            self._rng_offset += 1
+        else:
+            T.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
+                         self.reward, self.done, self.any_done, self.seeds, *common, c.collision_distance, dt,
+                         c.rigid_boundary)
+
     def step(self, action, noise=None, dt=None, copy=False, ring=None, auto_reset=False):
         """One vectorized step. action: [E,N,2] f32 (v2: [lin, ang]; uw/flock: velocity/acceleration) or
         [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info).
@@ -202,7 +251,10 @@ class VecFlockEnv:
             if c.variant != "v2":
                 raise NotImplementedError("the fused replay insert is built for the v2 step")
             ring.prev_obs = src["dnn"].data_ptr()
-        if c.variant == "v2":
+        T = self._torch_ops if ring is None else None
+        if T is not None:
+            self._step_torch(T, a, noise, dt, src, dst)
+        elif c.variant == "v2":
             ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
                         self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
                         v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, seeds=self.seeds, **common)
