@@ -41,7 +41,7 @@ BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  #
 # written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG record: state,
 # next_state, actor_state, actor_next_state 16 each + action 8 + reward 4 + done 4
 RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80}
-EV_EVERY = 4  # steps between HIP-event-timed env launches inside the timed region
+EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 4))  # steps between HIP-event-timed env launches (timed region)
 
 
 def parse():

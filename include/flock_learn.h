@@ -112,6 +112,13 @@ typedef struct FlockScUpdate {
     int update_rate; /* > 0 (with do_adam): flock_sc_actor_update also applies the soft updates when this agent's
                         learn count (= actor_steps[agent] before the step) is a multiple of it, after both Adam
                         steps, as Agent.learn() does (:152-154); 0: the caller runs them (flock_soft_update) */
+    float* critic_view; /* may be NULL. With do_adam: flock_sc_critic_update writes the critic's post-Adam
+                           parameters here and, when this learn() soft-updates (update_rate above), the critic's
+                           self soft update tau c + (1 - tau) c (the shared critic is its own target, :172-178)
+                           straight into `critic`; flock_sc_actor_update then reads the critic from critic_view.
+                           Results are bitwise those of critic_view = NULL; what it buys is that the critic phase of
+                           the NEXT learn() (which reads `critic`) may run while this actor phase still reads the
+                           critic it was given (two views, alternated by the caller). */
 } FlockScUpdate;
 
 int64_t flock_sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2);

@@ -75,7 +75,7 @@ class FlockScUpdate(ctypes.Structure):
                 + [("actor_stride", ctypes.c_int64)]
                 + [(n, _c_void_p) for n in ("losses", "workspace", "counters")]
                 + [(n, _c_float) for n in ("alpha", "beta", "gamma", "beta1", "beta2", "eps", "tau")]
-                + [("update_rate", _c_int)])
+                + [("update_rate", _c_int), ("critic_view", _c_void_p)])
 
 
 class FlockRingField(ctypes.Structure):

@@ -920,6 +920,10 @@ struct GradAdam {
     int64_t self_n;
     int soft_rate, soft_blocks;
     float tau, one_minus_tau;
+    // critic kernel with a view (FlockScUpdate.critic_view): the post-Adam value also goes to p_copy, and when
+    // soft_count[*agent] (this learn's count) is a multiple of soft_rate, p receives the self soft update of it
+    float* p_copy;
+    const int64_t* soft_count;
 };
 
 struct AdamState {
@@ -938,7 +942,12 @@ __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamSt
     vi = vi + (omb2 * gi) * gi;
     const float denom = __builtin_sqrtf(vi) / bc2s + ga.eps;
     const float pn = s.p + (neg_step * mi) / denom;
-    ga.p[i] = pn;
+    if (ga.p_copy) {  // critic with a view: view = post-Adam, p = its self soft update on soft learns
+        ga.p_copy[i] = pn;
+        ga.p[i] = soft ? ga.tau * pn + ga.one_minus_tau * pn : pn;
+    } else {
+        ga.p[i] = pn;
+    }
     ga.m[i] = mi;
     ga.v[i] = vi;
     if (soft && ga.target) ga.target[i] = ga.tau * pn + ga.one_minus_tau * s.t;  // soft_update_kernel mode 1
@@ -955,7 +964,8 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
     const int64_t base = ga.rel * agent;
     if (tid == 0) {
         const int64_t step0 = ga.do_adam ? ga.step[agent] : 0;
-        sh_soft = ga.do_adam && ga.soft_rate > 0 && (step0 % ga.soft_rate) == 0;  // this learn's count
+        const int64_t count = ga.soft_count ? ga.soft_count[*ga.agent] : step0;
+        sh_soft = ga.do_adam && ga.soft_rate > 0 && (count % ga.soft_rate) == 0;  // this learn's count
         if (ga.do_adam) {
             const double st = (double)(step0 + 1);
             sh[0] = (float)(-(double)ga.lr / (1.0 - pow((double)ga.b1, st)));
@@ -1385,8 +1395,14 @@ int flock_sc_critic_update(void* stream, const FlockScUpdate* u) {
     ga.counter = u->counters;
     ga.loss = u->losses + 1;
     ga.lr = u->beta; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
-    ga.target = nullptr; ga.self_soft = nullptr; ga.self_n = 0; ga.soft_rate = 0; ga.soft_blocks = 0;
-    ga.tau = 0.0f; ga.one_minus_tau = 1.0f;
+    ga.target = nullptr; ga.self_soft = nullptr; ga.self_n = 0; ga.soft_blocks = 0;
+    // with a critic view the self soft update of this learn() rides in the critic's Adam (see FlockScUpdate)
+    const bool view = u->do_adam && u->critic_view;
+    ga.p_copy = view ? u->critic_view : nullptr;
+    ga.soft_count = view ? u->actor_steps : nullptr;
+    ga.soft_rate = view ? u->update_rate : 0;
+    ga.tau = u->tau;
+    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
     return launch_grad_adam(st, ga);
 }
 
@@ -1397,7 +1413,10 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
     const int B = u->B, in = u->in_dim, na = u->n_actions, H1 = u->fc1, H2 = u->fc2;
     Ws w;
     ws_layout(B, in, na, H1, H2, u->workspace, &w);
-    const RowArgs a = row_args(u);
+    RowArgs a = row_args(u);
+    const bool view = u->do_adam && u->critic_view;
+    float* const critic = view ? u->critic_view : u->critic;  // the critic this actor step sees (post-Adam)
+    a.critic = critic;
     const CriticOff co = critic_off(in, na, H1, H2);
     const ActorOff ao = actor_off(in, na, H1, H2);
     const int C = chunks(u);
@@ -1408,8 +1427,8 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
         GemmBatch gb;
         gb.p[0] = gemm_p(w.AH1, u->actors + ao.W2, w.Z2b, u->actors + ao.b2, B, H2, H1, H1, 1, 1, H1, H2,
                          u->actor_stride);
-        gb.p[1] = gemm_p(w.CH1, u->critic + co.W2, w.Z2b + (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1, 1,
-                         H1, H2, 0);
+        gb.p[1] = gemm_p(w.CH1, critic + co.W2, w.Z2b + (int64_t)B * H2, critic + co.b2, B, H2, H1, H1, 1, 1, H1,
+                         H2, 0);
         gb.n = 2;
         gb.agent = u->agent;
         if ((rc = launch_gemm(st, gb))) return rc;
@@ -1455,11 +1474,13 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
     const bool soft = u->do_adam && u->update_rate > 0;
     ga.soft_rate = soft ? u->update_rate : 0;
     ga.target = soft ? u->actors_target : nullptr;  // agent-relative like p
-    ga.self_soft = soft ? u->critic : nullptr;
+    ga.self_soft = (soft && !view) ? u->critic : nullptr;  // with a view the critic kernel did it
     ga.self_n = co.total;
-    ga.soft_blocks = soft ? (int)((co.total + 1023) / 1024) : 0;
+    ga.soft_blocks = (soft && !view) ? (int)((co.total + 1023) / 1024) : 0;
     ga.tau = u->tau;
     ga.one_minus_tau = (float)(1.0 - (double)u->tau);
+    ga.p_copy = nullptr;
+    ga.soft_count = nullptr;
     return launch_grad_adam(st, ga);
 }
 

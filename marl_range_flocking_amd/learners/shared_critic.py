@@ -144,6 +144,11 @@ class SharedCriticLearner:
         n_ws = lib.flock_sc_workspace_floats(B, n_in, na, self.fc1, self.fc2)
         self.sc_workspace = torch.zeros(int(n_ws), dtype=torch.float32, device=dev)
         self.sc_counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        # critic views (FlockScUpdate.critic_view): the critic phase writes the post-Adam critic into a view and the
+        # self soft update into critic.data; the actor phase reads the view. Two views and two workspaces (one per
+        # staging slot) let the critic phase of learn t+1 run beside the actor phase of learn t (pipelined()).
+        self.critic_views = [torch.zeros_like(self.critic.data) for _ in range(2)]
+        self.sc_workspaces = [self.sc_workspace, torch.zeros_like(self.sc_workspace)]
         rb = self.replay.bufs
         C, A = self.critic, self.actors
         fields = dict(B=B, in_dim=n_in, n_actions=na, fc1=self.fc1, fc2=self.fc2, do_adam=1,
@@ -157,24 +162,24 @@ class SharedCriticLearner:
                       workspace=_p(self.sc_workspace), counters=_p(self.sc_counters), alpha=self.alpha,
                       beta=self.beta, gamma=self.gamma, beta1=0.9, beta2=0.999, eps=1e-8, tau=self.tau,
                       update_rate=self.update_rate)
-        # single GPU: the soft updates run inside the actor's gradient kernel (device-side count condition)
-        self._sc = _native.FlockScUpdate(**fields)
+        # single GPU: the soft updates run inside the gradient kernels (device-side count condition)
+        self._sc = _native.FlockScUpdate(**fields, critic_view=_p(self.critic_views[0]))
         self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0, update_rate=0))  # data-parallel
         self._slots = []
         if self.snapshot:
             self.identity_idx = torch.arange(B, dtype=torch.int64, device=dev)
             names = ("state", "new_state", "action", "reward", "terminal")
             self._rows_ring = _native.FlockScRows(**{n: _p(rb[n]) for n in names})
-            for _ in range(2):
+            for i in range(2):
                 stg = {"state": torch.zeros(B, n_in, device=dev), "new_state": torch.zeros(B, n_in, device=dev),
                        "action": torch.zeros(B, na, device=dev), "reward": torch.zeros(B, device=dev),
                        "terminal": torch.zeros(B, device=dev)}
                 agent_t = torch.zeros(1, dtype=torch.int64, device=dev)
-                f = dict(fields, idx=_p(self.identity_idx), agent=_p(agent_t),
+                f = dict(fields, idx=_p(self.identity_idx), agent=_p(agent_t), workspace=_p(self.sc_workspaces[i]),
                          **{"ring_" + n: _p(stg[n]) for n in names})
-                self._slots.append(dict(staging=stg, agent=agent_t, graph=None,
+                self._slots.append(dict(staging=stg, agent=agent_t, graph=None, graph_c=None, graph_a=None,
                                         rows=_native.FlockScRows(**{n: _p(stg[n]) for n in names}),
-                                        sc=_native.FlockScUpdate(**f),
+                                        sc=_native.FlockScUpdate(**f, critic_view=_p(self.critic_views[i])),
                                         sc_grads=_native.FlockScUpdate(**dict(f, do_adam=0, update_rate=0))))
             self.staging = self._slots[0]["staging"]
 
@@ -190,7 +195,7 @@ class SharedCriticLearner:
         which the in-kernel soft update moves."""
         A = self.actors
         return self.critic.state_tensors() + [A.data, A.target, A.exp_avg, A.exp_avg_sq, self.actor_steps,
-                                              self.losses]
+                                              self.losses] + self.critic_views
 
     def _run_fused(self, agent, slot=None):
         S = self._slots[slot] if slot is not None else None
@@ -411,6 +416,46 @@ class SharedCriticLearner:
         _native.check(rc, "flock_sc_prep_snapshot", learn=True)
         return True
 
+    def _phase(self, slot, phase):
+        """Enqueue the critic ("c": flock_sc_critic_update) or actor ("a": flock_sc_actor_update) phase of the
+        update on staging slot ``slot`` on the current stream (one HIP graph replay per phase)."""
+        S = self._slots[slot]
+        lib = _native.lib()
+        fn, name = ((lib.flock_sc_critic_update, "flock_sc_critic_update") if phase == "c"
+                    else (lib.flock_sc_actor_update, "flock_sc_actor_update"))
+        u = ctypes.byref(S["sc"])
+
+        def run():
+            _native.check(fn(_stream(self.device), u), name, learn=True)
+
+        if not self.use_graph:
+            return run()
+        key = "graph_" + phase
+        if S[key] is None:
+            S[key] = capture_graph(run, self.device, self._fused_state())
+        S[key].replay()
+
+    def update_slot_pipelined(self, slot, agent, critic_stream, actor_stream, after_actor=None, critic_done=None):
+        """update_slot as two phases on two streams (single GPU): the critic phase on critic_stream, the actor
+        phase on actor_stream behind it. The critic phase of the NEXT learn() may then run beside this actor phase:
+        it reads critic.data (post-soft) while this actor phase reads critic_views[slot] (post-Adam), and each slot
+        has its own workspace. Ordering the caller must provide: the critic phase of a learn whose agent equals the
+        previous learn's waits for that actor phase (it reads the target actor that actor phase soft-updates), and
+        a slot is reused only after its previous actor phase (``after_actor``: an event recorded behind it).
+        Results are bitwise those of update_slot."""
+        if self.distributed:
+            raise RuntimeError("update_slot_pipelined is the single-GPU path")
+        done_c = critic_done if critic_done is not None else torch.cuda.Event()
+        with torch.cuda.stream(critic_stream):
+            self._phase(slot, "c")
+            done_c.record(critic_stream)
+        with torch.cuda.stream(actor_stream):
+            actor_stream.wait_event(done_c)
+            self._phase(slot, "a")
+            if after_actor is not None:
+                after_actor.record(actor_stream)
+        return self._finish_learn(agent, soft_in_kernel=True)
+
     def update_slot(self, slot, agent):
         """The rest of learn() on the rows snapshot_into(slot, agent) copied, enqueued on the current stream."""
         self._run_fused(agent, slot)
@@ -457,13 +502,20 @@ class SharedCriticBench:
                                            buffer_size=1_000_000, dist_group=group, fused=fused,
                                            snapshot=self.overlap)
         if self.overlap:
-            # high priority: when the env kernel holds every CU slot, the update's blocks are dispatched first as
-            # env blocks retire, so the update chain (the step's critical path) is not stretched by the env step
-            prio = 0 if os.environ.get("FLOCK_LEARNER_PRIORITY") == "0" else torch.cuda.Stream.priority_range()[1]
+            # single GPU: learn() runs as two phases on two streams, the actor phase of learn s beside the critic
+            # phase of learn s+1 (SharedCriticLearner.update_slot_pipelined); FLOCK_LEARN_PIPELINE=0 keeps one
+            self.pipelined = not self.learner.distributed and os.environ.get("FLOCK_LEARN_PIPELINE") != "0"
+            # stream priority (FLOCK_LEARNER_PRIORITY=1): the one-stream learner ran at high priority; with the two
+            # pipelined streams high priority made steps 2-3x slower in fresh processes (tools/pipe_bench_probe.py)
+            hi = os.environ.get("FLOCK_LEARNER_PRIORITY", "0" if self.pipelined else "1") == "1"
+            prio = torch.cuda.Stream.priority_range()[1] if hi else 0
             self.stream = torch.cuda.Stream(device=device, priority=prio)
+            self.actor_stream = torch.cuda.Stream(device=device, priority=prio) if self.pipelined else None
+            self.critic_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.snap_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.learn_done = [torch.cuda.Event(), torch.cuda.Event()]
             self._used = [False, False]
+            self._prev_agent = None
         self.prev_obs = env.dnn.clone()
         self.prev_act = None
 
@@ -495,16 +547,29 @@ class SharedCriticBench:
         if not L.snapshot_into(slot, agent):
             return
         self.snap_done[slot].record(main)
-        with torch.cuda.stream(self.stream):
+        if self.pipelined:
+            # critic phase on self.stream, actor phase on self.actor_stream; learn_done[slot] = its actor phase.
+            # Slot reuse waits above (snapshot behind learn_done[slot]) cover the view and workspace of the slot.
             self.stream.wait_event(self.snap_done[slot])
-            L.update_slot(slot, agent)
-            self.learn_done[slot].record(self.stream)
+            if agent == self._prev_agent:  # same agent: its target actor is soft-updated by the previous actor phase
+                self.stream.wait_event(self.learn_done[slot ^ 1])
+            L.update_slot_pipelined(slot, agent, self.stream, self.actor_stream, after_actor=self.learn_done[slot],
+                                    critic_done=self.critic_done[slot])
+            self._prev_agent = agent
+        else:
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(self.snap_done[slot])
+                L.update_slot(slot, agent)
+                self.learn_done[slot].record(self.stream)
         self._used[slot] = True
 
     def finish(self):
-        """Join the learner stream into the current one (end of a timed region)."""
+        """Join the learner stream(s) into the current one (end of a timed region)."""
         if self.overlap:
-            torch.cuda.current_stream(self.learner.device).wait_stream(self.stream)
+            cur = torch.cuda.current_stream(self.learner.device)
+            cur.wait_stream(self.stream)
+            if self.actor_stream is not None:
+                cur.wait_stream(self.actor_stream)
 
     def prime(self):
         self.finish()

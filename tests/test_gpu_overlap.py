@@ -43,11 +43,16 @@ def test_snapshot_prologue_copies_the_sampled_rows(cuda):
         assert torch.equal(x, y)
 
 
-def test_overlapped_bench_loop_equals_serial(cuda):
-    runs = [_pair(cuda, overlap) for overlap in (False, True)]
+@pytest.mark.parametrize("N,steps", [(16, 8), (6, 14)], ids=["distinct-agents", "repeated-agents"])
+def test_overlapped_bench_loop_equals_serial(N, steps, cuda):
+    """The default overlapped hook runs learn() as a critic phase and an actor phase on two streams, the actor phase
+    of learn s beside the critic phase of learn s+1 (update_slot_pipelined). With 6 agents each agent learns 2-3
+    times, so soft and non-soft learns (count % 3) alternate in the pipeline."""
+    runs = [_pair(cuda, overlap, N=N) for overlap in (False, True)]
+    assert runs[1][1].pipelined
     g = torch.Generator(device=cuda).manual_seed(7)
     E, N = runs[0][0].E, runs[0][0].N
-    for s in range(8):
+    for s in range(steps):
         a = torch.stack([torch.rand(E, N, device=cuda, generator=g),
                          torch.rand(E, N, device=cuda, generator=g) * 3 - 1.5], -1).contiguous()
         for env, hook in runs:
@@ -67,3 +72,42 @@ def test_overlapped_bench_loop_equals_serial(cuda):
         assert torch.equal(x, y)
     for name in L0.replay.bufs:
         assert torch.equal(L0.replay.bufs[name], L1.replay.bufs[name]), name
+
+
+def test_pipelined_phases_same_agent_equal_serial(cuda):
+    """update_slot_pipelined with the SAME agent learning back to back (its critic phase must wait for the previous
+    actor phase, which soft-updates that agent's target actor): bitwise the serial learn() sequence."""
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    Ls = [SharedCriticLearner(1, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=True)
+          for _ in range(2)]
+    g = torch.Generator(device=cuda).manual_seed(2)
+    n = 300
+    rows = (torch.rand(n, 4, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g),
+            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, 4, device=cuda, generator=g),
+            torch.rand(n, device=cuda, generator=g) > 0.5)
+    for L in Ls:
+        L.store_transitions(*rows)
+    ser, pip = Ls
+    sc, sa = torch.cuda.Stream(device=cuda), torch.cuda.Stream(device=cuda)
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    main = torch.cuda.current_stream(cuda)
+    for t in range(7):
+        ser.learn(0)
+        slot = t & 1
+        if t >= 2:
+            main.wait_event(done[slot])
+        assert pip.snapshot_into(slot, 0)
+        ev = torch.cuda.Event()
+        ev.record(main)
+        sc.wait_event(ev)
+        if t >= 1:
+            sc.wait_event(done[slot ^ 1])  # same agent as the previous learn
+        pip.update_slot_pipelined(slot, 0, sc, sa, after_actor=done[slot])
+    main.wait_stream(sc)
+    main.wait_stream(sa)
+    torch.cuda.synchronize()
+    for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg, pip.critic.exp_avg),
+                 (ser.actors.data, pip.actors.data), (ser.actors.target, pip.actors.target),
+                 (ser.actor_steps, pip.actor_steps), (ser.critic.step_dev, pip.critic.step_dev)):
+        assert torch.equal(x, y)
