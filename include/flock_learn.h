@@ -144,6 +144,25 @@ int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uin
 int flock_sc_critic_update(void* stream, const FlockScUpdate* u); /* :118-141 */
 int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (after the critic update) */
 
+/* learn() pipeline of a training loop that calls Agent.learn() once per env step (train_flock.py:120-121, one agent
+ * per call): two staging slots, each with its own FlockScUpdate (do_adam, own critic_view, own workspace; ring
+ * fields = that slot's staging rows, idx = 0..B-1), whose critic and actor phases are captured once as HIP graphs.
+ * flock_sc_pipeline_learn enqueues one learn() of `agent` with no host synchronisation:
+ *   env_stream:    [wait for the slot's previous learn] minibatch snapshot (flock_sc_prep_snapshot, rows sampled
+ *                  with Philox(seed, counter)) -> event
+ *   critic_stream: wait snapshot [, wait the previous learn when wait_previous: same agent] -> critic phase graph
+ *   actor_stream:  wait critic phase -> actor phase graph
+ * so the actor phase of learn t runs beside the critic phase of learn t+1 and beside the next env step (which may
+ * rewrite the ring once the snapshot ran). Results are bitwise those of the serial update. Slots alternate per
+ * call. Returns NULL (create) or a negative code; flock_learn_last_error() has the message. */
+typedef struct FlockScPipeline FlockScPipeline;
+FlockScPipeline* flock_sc_pipeline_create(const FlockScUpdate* slot0, const FlockScUpdate* slot1,
+                                          const FlockScRows* ring, const FlockScRows* staging0,
+                                          const FlockScRows* staging1);
+int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* critic_stream, void* actor_stream,
+                            int64_t rows, uint64_t seed, uint64_t counter, int64_t agent, int wait_previous);
+void flock_sc_pipeline_destroy(FlockScPipeline* p);
+
 #ifdef __cplusplus
 }
 #endif

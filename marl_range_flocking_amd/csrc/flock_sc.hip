@@ -1484,4 +1484,113 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
     return launch_grad_adam(st, ga);
 }
 
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------------------------
+// learn() pipeline: the config-3 loop's per-step learner work in one call (see include/flock_learn.h)
+struct FlockScPipeline {
+    FlockScUpdate u[2];
+    FlockScRows ring, staging[2];
+    hipGraphExec_t gc[2], ga[2];
+    hipEvent_t snap_done[2], critic_done[2], learn_done[2];
+    bool used[2];
+    int slot;
+};
+
+namespace {
+int capture_phase(const FlockScUpdate* u, bool critic, hipGraphExec_t* out) {
+    hipStream_t cs;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return fail(-4, "flock_sc_pipeline: stream");
+    hipGraph_t g = nullptr;
+    int rc = 0;
+    if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        rc = fail(-4, "flock_sc_pipeline: begin capture");
+    } else {
+        rc = critic ? flock_sc_critic_update(cs, u) : flock_sc_actor_update(cs, u);
+        const hipError_t e = hipStreamEndCapture(cs, &g);
+        if (!rc && e != hipSuccess) rc = fail(-4, hipGetErrorString(e));
+        if (!rc && hipGraphInstantiate(out, g, nullptr, nullptr, 0) != hipSuccess)
+            rc = fail(-4, "flock_sc_pipeline: graph instantiate");
+    }
+    if (g) hipGraphDestroy(g);
+    hipStreamDestroy(cs);
+    return rc;
+}
+}  // namespace
+
+extern "C" {
+
+FlockScPipeline* flock_sc_pipeline_create(const FlockScUpdate* slot0, const FlockScUpdate* slot1,
+                                          const FlockScRows* ring, const FlockScRows* staging0,
+                                          const FlockScRows* staging1) {
+    if (!slot0 || !slot1 || !ring || !staging0 || !staging1) {
+        fail(-3, "flock_sc_pipeline_create: NULL argument");
+        return nullptr;
+    }
+    if (check(slot0) || check(slot1)) return nullptr;
+    if (!slot0->do_adam || !slot1->do_adam || !slot0->critic_view || !slot1->critic_view ||
+        slot0->critic_view == slot1->critic_view || slot0->workspace == slot1->workspace) {
+        fail(-5, "flock_sc_pipeline_create: each slot needs do_adam, its own critic_view and its own workspace");
+        return nullptr;
+    }
+    FlockScPipeline* p = new FlockScPipeline();
+    p->u[0] = *slot0;
+    p->u[1] = *slot1;
+    p->ring = *ring;
+    p->staging[0] = *staging0;
+    p->staging[1] = *staging1;
+    int rc = 0;
+    for (int i = 0; i < 2 && !rc; ++i) {
+        rc = capture_phase(&p->u[i], true, &p->gc[i]);
+        if (!rc) rc = capture_phase(&p->u[i], false, &p->ga[i]);
+        hipEvent_t* evs[3] = {&p->snap_done[i], &p->critic_done[i], &p->learn_done[i]};
+        for (hipEvent_t* e : evs)
+            if (!rc && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
+                rc = fail(-4, "flock_sc_pipeline_create: event");
+        p->used[i] = false;
+    }
+    p->slot = 0;
+    if (rc) {
+        delete p;  // (a failed create leaks at most the objects made before the failure)
+        return nullptr;
+    }
+    return p;
+}
+
+int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* critic_stream, void* actor_stream,
+                            int64_t rows, uint64_t seed, uint64_t counter, int64_t agent, int wait_previous) {
+    if (!p) return fail(-3, "flock_sc_pipeline_learn: NULL pipeline");
+    hipStream_t es = (hipStream_t)env_stream, cs = (hipStream_t)critic_stream, as = (hipStream_t)actor_stream;
+    const int s = p->slot;
+    const FlockScUpdate& u = p->u[s];
+    if (p->used[s] && hipStreamWaitEvent(es, p->learn_done[s], 0) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_learn: wait");
+    int rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
+                                    u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
+    if (rc) return rc;
+    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
+              hipStreamWaitEvent(cs, p->snap_done[s], 0) == hipSuccess;
+    if (ok && wait_previous && p->used[s ^ 1]) ok = hipStreamWaitEvent(cs, p->learn_done[s ^ 1], 0) == hipSuccess;
+    ok = ok && hipGraphLaunch(p->gc[s], cs) == hipSuccess && hipEventRecord(p->critic_done[s], cs) == hipSuccess &&
+         hipStreamWaitEvent(as, p->critic_done[s], 0) == hipSuccess && hipGraphLaunch(p->ga[s], as) == hipSuccess &&
+         hipEventRecord(p->learn_done[s], as) == hipSuccess;
+    if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
+    p->used[s] = true;
+    p->slot = s ^ 1;
+    return 0;
+}
+
+void flock_sc_pipeline_destroy(FlockScPipeline* p) {
+    if (!p) return;
+    for (int i = 0; i < 2; ++i) {
+        hipGraphExecDestroy(p->gc[i]);
+        hipGraphExecDestroy(p->ga[i]);
+        hipEventDestroy(p->snap_done[i]);
+        hipEventDestroy(p->critic_done[i]);
+        hipEventDestroy(p->learn_done[i]);
+    }
+    delete p;
+}
+
 }  // extern "C"

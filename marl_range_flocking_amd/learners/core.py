@@ -409,13 +409,20 @@ class ReplayRing:
         the capacity only the last `capacity` rows are kept). Field names map the kernel's targets to this ring's
         fields; group = agents per row (1, or N for one row per env); store_done: store done (else 1 - done)."""
         skip = max(0, n - self.capacity)
-        b = self.bufs
-        ptr = lambda name: None if name is None else b[name].data_ptr()  # noqa: E731
-        ring = _native.FlockRing(state=ptr(state), action=ptr(action), reward=ptr(reward), new_state=ptr(new_state),
-                                 terminal=ptr(terminal), prev_obs=None, capacity=self.capacity,
-                                 start=(self.counter + skip) % self.capacity, skip=skip,
-                                 actor_state=ptr(actor_state), actor_new_state=ptr(actor_new_state), group=group,
-                                 store_done=int(bool(store_done)))
+        # one FlockRing object per field mapping, updated in place: the env step's launch plan keeps a pointer to it
+        key = (state, action, reward, new_state, terminal, actor_state, actor_new_state, group, bool(store_done))
+        rings = self.__dict__.setdefault("_rings", {})
+        ring = rings.get(key)
+        if ring is None:
+            b = self.bufs
+            ptr = lambda name: None if name is None else b[name].data_ptr()  # noqa: E731
+            ring = rings[key] = _native.FlockRing(
+                state=ptr(state), action=ptr(action), reward=ptr(reward), new_state=ptr(new_state),
+                terminal=ptr(terminal), prev_obs=None, capacity=self.capacity, start=0, skip=0,
+                actor_state=ptr(actor_state), actor_new_state=ptr(actor_new_state), group=group,
+                store_done=int(bool(store_done)))
+        ring.start = (self.counter + skip) % self.capacity
+        ring.skip = skip
         self.counter += n
         return ring
 

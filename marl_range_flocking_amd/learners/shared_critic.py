@@ -456,6 +456,45 @@ class SharedCriticLearner:
                 after_actor.record(actor_stream)
         return self._finish_learn(agent, soft_in_kernel=True)
 
+    def pipeline(self):
+        """The native learn() pipeline (flock_sc_pipeline_*, include/flock_learn.h) over the two staging slots:
+        snapshot, critic-phase graph and actor-phase graph of one learn() enqueued by ONE C call, the actor phase
+        of learn t beside the critic phase of learn t+1 (the update_slot_pipelined schedule without its per-step
+        Python and graph-replay host cost)."""
+        if self.__dict__.get("_pipe") is None:
+            if not (self.snapshot and self.fused) or self.distributed:
+                raise RuntimeError("the native pipeline needs a single-GPU fused learner with snapshot=True")
+            lib = _native.lib()
+            S0, S1 = self._slots
+            h = lib.flock_sc_pipeline_create(ctypes.byref(S0["sc"]), ctypes.byref(S1["sc"]),
+                                             ctypes.byref(self._rows_ring), ctypes.byref(S0["rows"]),
+                                             ctypes.byref(S1["rows"]))
+            if not h:
+                raise RuntimeError("flock_sc_pipeline_create: " + lib.flock_learn_last_error().decode())
+            self._pipe = h
+        return self._pipe
+
+    def pipeline_learn(self, agent, env_stream, critic_stream, actor_stream, wait_previous):
+        """Enqueue learn(agent) through the native pipeline (raw stream handles). Returns False (nothing enqueued)
+        before the buffer holds a batch, like snapshot_into."""
+        if self.replay.counter < self.batch_size:
+            return False
+        self._learn_calls += 1
+        rc = _native.lib().flock_sc_pipeline_learn(self.pipeline(), env_stream, critic_stream, actor_stream,
+                                                   len(self.replay), self.seed, self._learn_calls, int(agent),
+                                                   int(bool(wait_previous)))
+        _native.check(rc, "flock_sc_pipeline_learn", learn=True)
+        self._finish_learn(agent, soft_in_kernel=True)
+        return True
+
+    def __del__(self):
+        h = self.__dict__.get("_pipe")
+        if h:
+            try:
+                _native.lib().flock_sc_pipeline_destroy(h)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+
     def update_slot(self, slot, agent):
         """The rest of learn() on the rows snapshot_into(slot, agent) copied, enqueued on the current stream."""
         self._run_fused(agent, slot)
@@ -512,6 +551,7 @@ class SharedCriticBench:
             self.stream = torch.cuda.Stream(device=device, priority=prio)
             self.actor_stream = torch.cuda.Stream(device=device, priority=prio) if self.pipelined else None
             self.critic_done = [torch.cuda.Event(), torch.cuda.Event()]
+            self._handles = None
             self.snap_done = [torch.cuda.Event(), torch.cuda.Event()]
             self.learn_done = [torch.cuda.Event(), torch.cuda.Event()]
             self._used = [False, False]
@@ -540,6 +580,16 @@ class SharedCriticBench:
         # the snapshot goes on the env stream right behind the env step (the next env step follows it in order);
         # the update runs on the learner stream; staging slots alternate, and a slot is refilled only after the
         # update that read it two steps ago has finished
+        if self.pipelined and L.use_graph:
+            # the native pipeline: snapshot on the env stream, critic phase on self.stream, actor phase on
+            # self.actor_stream, all enqueued by one C call (stream handles cached at the first call: the env
+            # stream is the stream current then)
+            if self._handles is None:
+                self._handles = (torch.cuda.current_stream(L.device).cuda_stream, self.stream.cuda_stream,
+                                 self.actor_stream.cuda_stream)
+            L.pipeline_learn(agent, *self._handles, wait_previous=agent == self._prev_agent)
+            self._prev_agent = agent
+            return
         main = torch.cuda.current_stream(L.device)
         slot = s & 1
         if self._used[slot]:

@@ -70,10 +70,11 @@ class StepPlan:
     the argument tuple; later calls check only the per-call action tensor and substitute the stream, the action
     pointer, dt and (uw_discrete) the RNG offset: the Python cost of a step drops to about one ctypes call."""
 
-    __slots__ = ("fn", "name", "args", "ext", "i_action", "i_dt", "i_rng")
+    __slots__ = ("fn", "name", "args", "ext", "i_action", "i_dt", "i_rng", "ring")
 
     def __init__(self):
         self.fn = None
+        self.ring = None
 
     def record(self, fn, name, args, ext, i_action, i_dt, i_rng=None):
         self.fn, self.name, self.args, self.ext = fn, name, list(args), ext
@@ -115,8 +116,11 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
     ring (a _native.FlockRing): also write every transition into a replay ring in the same launch
     (flock_step_v2_store; the store_transitions that follows each step in train_flock.py).
     seeds ([E, N, k] int16, rw, optional): compact kNN search seeds (flock_step_v2_ext; see include/flock_amd.h).
-    plan (StepPlan, optional; not with ring): record / replay the validated launch over the same buffers."""
-    if ring is None and _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
+    plan (StepPlan, optional): record / replay the validated launch over the same buffers; with a ring, the plan
+    holds that FlockRing object (ReplayRing.step_slots updates one object in place) and serves only that ring."""
+    if plan is not None and plan.ring is not ring:
+        plan.fn = None  # recorded for another ring (or none): record again
+    if _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
         return
     E, N, dev = _dims(pos)
     _check_k(N, k)
@@ -135,8 +139,10 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
             _ptr(action), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
     ext = _ext(ring, seeds, E, N, k, dev)
     L = _native.lib()
-    _record(plan if ring is None else None, L.flock_step_v2 if ext is None else L.flock_step_v2_ext,
+    _record(plan, L.flock_step_v2 if ext is None else L.flock_step_v2_ext,
             "flock_step_v2" if ext is None else "flock_step_v2_ext", args, ext, 14, 7)
+    if plan is not None:
+        plan.ring = ring  # a strong reference: the recorded ext points into it
 
 
 def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done, *, k, box,

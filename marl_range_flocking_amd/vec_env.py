@@ -242,9 +242,10 @@ class VecFlockEnv:
             a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
         # launch plan of this buffer parity (ops.StepPlan): fixed buffers, so later steps skip the tensor checks
         plans = self.__dict__.setdefault("_plans", {})
-        plan = plans.get(nxt)
+        pkey = nxt if ring is None else (nxt, id(ring))  # ring steps: one plan per (parity, ring object)
+        plan = plans.get(pkey)
         if plan is None:
-            plan = plans[nxt] = ops.StepPlan()
+            plan = plans[pkey] = ops.StepPlan()
         common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
                       rigid_boundary=c.rigid_boundary, plan=plan)
         if ring is not None:

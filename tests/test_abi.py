@@ -16,7 +16,8 @@ def header_functions():
     src = "\n".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"^\s*(?:int|int64_t|const char\*)\s+(flock_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.M | re.S):
+    for m in re.finditer(r"^\s*(?:int|int64_t|const char\*|void|\w+\*)\s+(flock_\w+)\s*\(([^;]*?)\)\s*;", src,
+                         flags=re.M | re.S):
         args = m.group(2).strip()
         out[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
     return out

@@ -231,7 +231,8 @@ def test_step_plan_replay_is_bitwise_the_checked_launch(variant, periodic, N, cu
     envs = []
     for i in range(2):
         env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
-                                      range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda)
+                                      range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda,
+                          launch="plan")
         env.set_state(positions=pos, headings=head)
         if i == 1:
             env.__dict__["_plans"] = _NoPlans()
