@@ -321,6 +321,8 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         one_step(args.warmup + s, ev.get(s))
+    if hook is not None and hasattr(hook, "finish"):
+        hook.finish()  # the learner work still pending (the last learn's actor phase) runs inside the timed region
     torch.cuda.synchronize(dev)
     barrier(world)
     el = time.perf_counter() - t0

@@ -143,24 +143,32 @@ int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uin
                            const FlockScRows* staging);
 int flock_sc_critic_update(void* stream, const FlockScUpdate* u); /* :118-141 */
 int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (after the critic update) */
+/* One round of six launches: the critic phase of critic_u and the actor phase of actor_u (either may be NULL; each
+ * alone is flock_sc_critic_update / flock_sc_actor_update). For two learn() calls of DIFFERENT agents, round(critic
+ * of call t+1, actor of call t) is bitwise the actor phase of t followed by the critic phase of t+1: the phases share
+ * no written state (actor_u must carry a critic_view, critic_u its own workspace and critic_view). The two updates
+ * must have the same shapes. */
+int flock_sc_round(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u);
 
 /* learn() pipeline of a training loop that calls Agent.learn() once per env step (train_flock.py:120-121, one agent
- * per call): two staging slots, each with its own FlockScUpdate (do_adam, own critic_view, own workspace; ring
- * fields = that slot's staging rows, idx = 0..B-1), whose critic and actor phases are captured once as HIP graphs.
- * flock_sc_pipeline_learn enqueues one learn() of `agent` with no host synchronisation:
- *   env_stream:    [wait for the slot's previous learn] minibatch snapshot (flock_sc_prep_snapshot, rows sampled
- *                  with Philox(seed, counter)) -> event
- *   critic_stream: wait snapshot [, wait the previous learn when wait_previous: same agent] -> critic phase graph
- *   actor_stream:  wait critic phase -> actor phase graph
- * so the actor phase of learn t runs beside the critic phase of learn t+1 and beside the next env step (which may
- * rewrite the ring once the snapshot ran). Results are bitwise those of the serial update. Slots alternate per
- * call. Returns NULL (create) or a negative code; flock_learn_last_error() has the message. */
+ * per call): n_slots (2..8) staging slots, each with its own FlockScUpdate (do_adam, own critic_view, own workspace;
+ * ring fields = that slot's staging rows, idx = 0..B-1). Rounds (flock_sc_round) are captured once as HIP graphs.
+ * flock_sc_pipeline_learn enqueues learn() t of `agent` with no host synchronisation:
+ *   env_stream:     [wait until the slot's previous learn() has finished] minibatch snapshot (flock_sc_prep_snapshot,
+ *                   rows sampled with Philox(seed, counter)) -> event
+ *   learner_stream: wait for the snapshot -> ONE round: the critic phase of learn t with the actor phase of learn t-1
+ *                   (if learn t-1 had the same agent: its actor phase, then this critic phase)
+ * so the learner runs one six-launch round per env step beside the next env step (which may rewrite the ring once
+ * the snapshot ran), with no cross-stream wait between the two phases. The actor phase of the last learn() stays
+ * pending until the next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise
+ * those of the serial learn() sequence. Returns NULL (create) or a negative code; flock_learn_last_error() has the
+ * message. */
 typedef struct FlockScPipeline FlockScPipeline;
-FlockScPipeline* flock_sc_pipeline_create(const FlockScUpdate* slot0, const FlockScUpdate* slot1,
-                                          const FlockScRows* ring, const FlockScRows* staging0,
-                                          const FlockScRows* staging1);
-int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* critic_stream, void* actor_stream,
-                            int64_t rows, uint64_t seed, uint64_t counter, int64_t agent, int wait_previous);
+FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slots, const FlockScRows* ring,
+                                          const FlockScRows* staging);
+int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
+                            uint64_t counter, int64_t agent);
+int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);
 
 #ifdef __cplusplus

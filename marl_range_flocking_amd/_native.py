@@ -113,10 +113,11 @@ SIGNATURES.update({
     "flock_sc_prep": [_c_void_p, _c_int, ctypes.c_int64, _c_u64, _c_u64, _c_void_p, _c_void_p, ctypes.c_int64],
     "flock_sc_critic_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_actor_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
-    "flock_sc_pipeline_create": [ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScUpdate),
-                                 ctypes.POINTER(FlockScRows), ctypes.POINTER(FlockScRows),
+    "flock_sc_round": [_c_void_p, ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScUpdate)],
+    "flock_sc_pipeline_create": [_c_int, ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScRows),
                                  ctypes.POINTER(FlockScRows)],
-    "flock_sc_pipeline_learn": [_c_void_p] * 4 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64, _c_int],
+    "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],
+    "flock_sc_pipeline_flush": [_c_void_p, _c_void_p],
     "flock_sc_pipeline_destroy": [_c_void_p],
 })
 RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,

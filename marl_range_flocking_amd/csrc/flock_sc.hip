@@ -302,13 +302,12 @@ __device__ __forceinline__ void ln_backward(const float (&dy)[C], const float (&
 // ---------------------------------------------------------------------------------------------------------------
 // c1 (grid.y = path): 0 target actor on s', 1 critic on s', 2 critic on s (+ the gathered minibatch rows)
 template <int C>
-__global__ __launch_bounds__(256) void sc_c1(Ws w, RowArgs a) {
+__device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, int path) {
     extern __shared__ float4 smem4[];
     float* xs = reinterpret_cast<float*>(smem4);  // [4 rows][kMaxIn] inputs, then the fc1 image
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int path = blockIdx.y;
-    const int r = blockIdx.x * kRowsPerBlock + wv;
+    const int r = bx * kRowsPerBlock + wv;
     const float* net = path == 0 ? a.actors_target + (*a.agent) * a.stride : a.critic;  // fc1 block at offset 0
     const bool live = r < a.B;
     if (live) {
@@ -346,13 +345,13 @@ __global__ __launch_bounds__(256) void sc_c1(Ws w, RowArgs a) {
 
 // c3: heads, TD target, MSE and the critic backward down to the fc2 pre-activation
 template <int C>
-__global__ __launch_bounds__(256) void sc_c3(Ws w, RowArgs a) {
+__device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);  // critic tail
     const int H2 = a.H2, na = a.na;
     float* at = ct + round4(crit_tail_len(na, H2));  // target actor tail
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
     const bool live = r < a.B;
     const CriticOff co = critic_off(a.in, na, a.H1, H2);
     const ActorOff ao = actor_off(a.in, na, a.H1, H2);
@@ -458,37 +457,42 @@ __global__ __launch_bounds__(256) void sc_c3(Ws w, RowArgs a) {
 }
 
 // c5 / a5: ReLU + LN1 backward: dy = dh * [h > 0]; dz = LN backward(dy)
+struct Ln1Args {
+    int B, F;
+    const float *DH, *XH, *RS, *H, *g_base;
+    const int64_t* agent;  // g_base is agent-relative (+ stride * (*agent)) when non-NULL
+    int64_t stride;
+    float *DY, *DZ;
+};
 template <int C>
-__global__ __launch_bounds__(256) void sc_ln1_bwd(int B, int F, const float* DH, const float* XH, const float* RS,
-                                                  const float* H, const float* g_base, const int64_t* agent,
-                                                  int64_t stride, float* DY, float* DZ) {
+__device__ __forceinline__ void ln1_body(const Ln1Args& l, int bx) {
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
-    if (r >= B) return;
-    const float* g = g_base + (agent ? (*agent) * stride : 0);
+    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
+    const int F = l.F;
+    if (r >= l.B) return;
+    const float* g = l.g_base + (l.agent ? (*l.agent) * l.stride : 0);
     const int64_t ro = (int64_t)r * F;
     float dh[C], xh[C], h[C], gv[C], dy[C], dz[C];
-    load_row<C>(dh, DH + ro, F, lane);
-    load_row<C>(xh, XH + ro, F, lane);
-    load_row<C>(h, H + ro, F, lane);
+    load_row<C>(dh, l.DH + ro, F, lane);
+    load_row<C>(xh, l.XH + ro, F, lane);
+    load_row<C>(h, l.H + ro, F, lane);
     load_row<C>(gv, g, F, lane);
-    const float rs = RS[r];
+    const float rs = l.RS[r];
 #pragma unroll
     for (int c = 0; c < C; ++c) dy[c] = h[c] > 0.0f ? dh[c] : 0.0f;
     ln_backward<C>(dy, xh, gv, rs, F, dz);
-    store_row<C>(DY + ro, dy, F, lane);
-    store_row<C>(DZ + ro, dz, F, lane);
+    store_row<C>(l.DY + ro, dy, F, lane);
+    store_row<C>(l.DZ + ro, dz, F, lane);
 }
 
 // a1 (grid.y = path): 0 the agent's actor fc1/LN/ReLU on s (saved for backward), 1 the updated critic's on s
 template <int C>
-__global__ __launch_bounds__(256) void sc_a1(Ws w, RowArgs a) {
+__device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, int path) {
     extern __shared__ float4 smem4[];
     float* xs = reinterpret_cast<float*>(smem4);
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int path = blockIdx.y;
-    const int r = blockIdx.x * kRowsPerBlock + wv;
+    const int r = bx * kRowsPerBlock + wv;
     const bool live = r < a.B;
     const float* net = path == 0 ? a.actors + (*a.agent) * a.stride : a.critic;
     if (live && lane < a.in) xs[wv * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
@@ -510,13 +514,13 @@ __global__ __launch_bounds__(256) void sc_a1(Ws w, RowArgs a) {
 // a3: actor LN2/ReLU/mu/tanh, Q(s, mu) with the updated critic, actor loss -mean Q, and the backward through the
 // critic's action branch (dQ/dmu) and the actor head down to the actor's fc2 pre-activation
 template <int C>
-__global__ __launch_bounds__(256) void sc_a3(Ws w, RowArgs a) {
+__device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);
     const int H2 = a.H2, na = a.na;
     float* at = ct + round4(crit_tail_len(na, H2));
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
     const bool live = r < a.B;
     const CriticOff co = critic_off(a.in, na, a.H1, H2);
     const ActorOff ao = actor_off(a.in, na, a.H1, H2);
@@ -616,6 +620,31 @@ __global__ __launch_bounds__(256) void sc_a3(Ws w, RowArgs a) {
     if (lane == 0) w.ARS2[r] = rs;
 }
 
+// Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
+// the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
+// blocks past them).
+template <int C>
+__global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
+    if ((int)blockIdx.y < npc)
+        c1_body<C>(wc, ac, blockIdx.x, blockIdx.y);
+    else
+        a1_body<C>(wa, aa, blockIdx.x, blockIdx.y - npc);
+}
+template <int C>
+__global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
+    if ((int)blockIdx.x < nbc)
+        c3_body<C>(wc, ac, blockIdx.x);
+    else
+        a3_body<C>(wa, aa, blockIdx.x - nbc);
+}
+template <int C>
+__global__ __launch_bounds__(256) void sc_ln1_bwd(Ln1Args l0, int nb0, Ln1Args l1) {
+    if ((int)blockIdx.x < nb0)
+        ln1_body<C>(l0, blockIdx.x);
+    else
+        ln1_body<C>(l1, blockIdx.x - nb0);
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // f32 GEMM tile on MFMA: C[m, n] = sum_k A(m, k) B(k, n) for one 32x32 output tile; A(m, k) = A[m*sam + k*sak],
 // B(k, n) = B[k*sbk + n*sbn]. K is processed in panels of up to kKC: the 32 x kc A panel and kc x 32 B panel are
@@ -625,6 +654,8 @@ __global__ __launch_bounds__(256) void sc_a3(Ws w, RowArgs a) {
 // 2 = any strides (scalar).
 constexpr int kT = 32;
 constexpr int kKC = 512;
+constexpr int kFwdKC = 200;   // forward / input-gradient GEMM K chunk (FLOCK_GEMM_KC overrides): 0.098 ms per config-3
+                              // step vs 0.117 with whole 400-deep panels (lighter blocks co-run with the env kernel)
 constexpr int kGradKC = 128;  // the gradient kernels share one launch with ~400 LDS-free reduction blocks: a 34-KB
                               // panel keeps 4 blocks per CU resident so the whole grid runs in one round
 constexpr int kPitch = 33;
@@ -635,13 +666,14 @@ struct GemmP {
     const float* bias;
     int M, N, K, sam, sak, sbk, sbn, ldc;
     int64_t relB;  // B and bias are agent-relative: + relB * (*agent)
+    const int64_t* agent;
     int tiles_n, tiles;
     int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
 };
+constexpr int kMaxBatch = 5;  // a round's forward GEMMs: 3 (critic phase) + 2 (actor phase)
 struct GemmBatch {
-    GemmP p[3];
+    GemmP p[kMaxBatch];
     int n;
-    const int64_t* agent;
 };
 
 __host__ __device__ inline int gemm_kc(int K, int chunk = kKC) {
@@ -729,14 +761,14 @@ __device__ __forceinline__ void load_panel(float* __restrict__ P, const float* _
 // panel_fetch issues the global loads into registers, panel_store writes them to LDS. gemm_tile fetches the A and
 // B panels of a chunk together (one memory round trip instead of two) and the next chunk's panels before the
 // current chunk's MFMAs.
-template <int V>
-__device__ __forceinline__ void panel_fetch(float4 (&v)[16], const float* __restrict__ X, int R, int Kd, int sr,
+template <int V, int NF>
+__device__ __forceinline__ void panel_fetch(float4 (&v)[NF], const float* __restrict__ X, int R, int Kd, int sr,
                                             int sk, int r0, int k0, int kc) {
     const int tid = threadIdx.x;
     if (V == 0) {
         const int q = kc >> 2, items = 32 * q;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < NF; ++i) {
             const int t = tid + 256 * i;
             const int rr = t / q, k = k0 + 4 * (t - rr * q), rw = r0 + rr;
             v[i] = (t < items && rw < R && k < Kd) ? *reinterpret_cast<const float4*>(X + (int64_t)rw * sr + k)
@@ -745,7 +777,7 @@ __device__ __forceinline__ void panel_fetch(float4 (&v)[16], const float* __rest
     } else {
         const int items = 8 * kc;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < NF; ++i) {
             const int t = tid + 256 * i;
             const int kk = t >> 3, rr = 4 * (t & 7), k = k0 + kk, rw = r0 + rr;
             v[i] = (t < items && rw < R && k < Kd) ? *reinterpret_cast<const float4*>(X + (int64_t)k * sk + rw)
@@ -753,13 +785,13 @@ __device__ __forceinline__ void panel_fetch(float4 (&v)[16], const float* __rest
         }
     }
 }
-template <int V>
-__device__ __forceinline__ void panel_store(float* __restrict__ P, const float4 (&v)[16], int kc) {
+template <int V, int NF>
+__device__ __forceinline__ void panel_store(float* __restrict__ P, const float4 (&v)[NF], int kc) {
     const int tid = threadIdx.x;
     if (V == 0) {
         const int q = kc >> 2, items = 32 * q;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < NF; ++i) {
             const int t = tid + 256 * i;
             if (t < items) {
                 const int rr = t / q, kk = 4 * (t - rr * q);
@@ -772,7 +804,7 @@ __device__ __forceinline__ void panel_store(float* __restrict__ P, const float4 
     } else {
         const int items = 8 * kc;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < NF; ++i) {
             const int t = tid + 256 * i;
             if (t < items) {
                 const int kk = t >> 3, rr = 4 * (t & 7);
@@ -806,7 +838,7 @@ __device__ __forceinline__ f32x16 mfma_panel(f32x16 acc, const float* a, const f
 }
 
 // the 4 outputs of thread (wave w, lane l): rows 8w + 4(l >> 5) + q (q < 4), column l & 31
-template <int AV, int BV>
+template <int AV, int BV, int NF>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
                                           float (&out)[4]) {
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
@@ -818,18 +850,18 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
     if constexpr (AV != 2 && BV != 2) {
-        float4 va[16], vb[16];
+        float4 va[NF], vb[NF];
         int kc = gemm_kc(g.K, g.kchunk);
-        panel_fetch<AV>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
-        panel_fetch<BV>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, 0, kc);
+        panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
+        panel_fetch<BV, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, 0, kc);
         for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
-            panel_store<AV>(As, va, kc);
-            panel_store<BV>(Bs, vb, kc);
+            panel_store<AV, NF>(As, va, kc);
+            panel_store<BV, NF>(Bs, vb, kc);
             __syncthreads();
             const int k1 = k0 + g.kchunk, kc1 = k1 < g.K ? gemm_kc(g.K - k1, g.kchunk) : 0;
             if (k1 < g.K) {  // the next chunk's loads fly during this chunk's MFMAs
-                panel_fetch<AV>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
-                panel_fetch<BV>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k1, kc1);
+                panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
+                panel_fetch<BV, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k1, kc1);
             }
             const int kq = kc >> 2;  // multiple of 2
             const float* a = As + (wv * kq + (l >> 5)) * kPitch + (l & 31);
@@ -863,7 +895,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
 }
 
 // grid (max tiles, problems): block (x, y) computes tile x of problem y
-template <int AV, int BV>
+template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
@@ -871,12 +903,12 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     const int t = blockIdx.x;
     if (t >= g.tiles) return;
     const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    const int64_t rel = g.relB ? g.relB * (*gb.agent) : 0;
+    const int64_t rel = g.relB ? g.relB * (*g.agent) : 0;
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int n = tn * kT + (l & 31);
     const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
     float out[4];
-    gemm_tile<AV, BV>(g, g.B + rel, tm, tn, smem, out);
+    gemm_tile<AV, BV, NF>(g, g.B + rel, tm, tn, smem, out);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
@@ -886,7 +918,8 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
 
 // ---------------------------------------------------------------------------------------------------------------
 // gradients + Adam for one network. Blocks [0, tiles): the fc2.weight gradient (a K = B GEMM) with Adam in the
-// epilogue; the next blocks: reduction red_of[b] over the B rows, 16 elements per block (16 row groups per block):
+// epilogue; the next blocks: reduction red[q] (the last q with red[q].blk0 <= block) over the B rows, 16 elements per
+// block (16 row groups per block):
 //   mode 0: g[o] = sum_b D[b, o]         (biases, LayerNorm beta)
 //   mode 1: g[o] = sum_b D[b, o] X[b, o] (LayerNorm gamma)
 //   mode 2: g[o*in + i] = sum_b D[b, o] X[b, i]  (fc1 / action_value / head weights)
@@ -899,13 +932,12 @@ struct RedP {
 };
 constexpr int kMaxRed = 12;
 constexpr int kRedElems = 16;
-constexpr int kMaxRedBlocks = 2048;
+constexpr int kMaxRedBlocks = 4096;
 struct GradAdam {
     GemmP g;  // C unused: the gradient goes to grad + w2_off
     int64_t w2_off;
     int nred, nblk, B, do_adam;
     RedP red[kMaxRed];
-    uint8_t red_of[kMaxRedBlocks];  // reduction block -> descriptor (one kernarg load instead of a search)
     float *p, *grad, *m, *v;
     int64_t rel;  // p/grad/m/v are agent-relative: + rel * (*agent)
     const int64_t* agent;
@@ -953,8 +985,9 @@ __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamSt
     if (soft && ga.target) ga.target[i] = ga.tau * pn + ga.one_minus_tau * s.t;  // soft_update_kernel mode 1
 }
 
-template <int AV, int BV>
-__global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
+// one job's blocks: bx in [0, nb), nb = g.tiles + nblk + soft_blocks
+template <int AV, int BV, int NF>
+__device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int nb) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     __shared__ float sh[2];
@@ -972,10 +1005,10 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
             sh[1] = (float)sqrt(1.0 - pow((double)ga.b2, st));
         }
     }
-    if ((int)blockIdx.x >= ga.g.tiles + ga.nblk) {  // critic self soft update blocks (after its Adam step)
+    if (bx >= ga.g.tiles + ga.nblk) {  // critic self soft update blocks (after its Adam step)
         __syncthreads();
         if (sh_soft && ga.self_soft) {
-            const int64_t b0 = (int64_t)(blockIdx.x - ga.g.tiles - ga.nblk) * 1024;
+            const int64_t b0 = (int64_t)(bx - ga.g.tiles - ga.nblk) * 1024;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t e = b0 + q * 256 + tid;
@@ -985,9 +1018,9 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
                 }
             }
         }
-    } else if ((int)blockIdx.x < ga.g.tiles) {
+    } else if (bx < ga.g.tiles) {
         {
-            const int tm = blockIdx.x / ga.g.tiles_n, tn = blockIdx.x - tm * ga.g.tiles_n;
+            const int tm = bx / ga.g.tiles_n, tn = bx - tm * ga.g.tiles_n;
             const int wv = tid >> 6, l = tid & 63;
             const int nn = tn * kT + (l & 31);
             AdamState st[4];
@@ -1001,7 +1034,7 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
                 st[q] = (ok[q] && ga.do_adam) ? adam_load(ga, e[q]) : AdamState{0.f, 0.f, 0.f, 0.f};
             }
             float out[4];
-            gemm_tile<AV, BV>(ga.g, ga.g.B, tm, tn, smem, out);  // (its barriers also publish sh[])
+            gemm_tile<AV, BV, NF>(ga.g, ga.g.B, tm, tn, smem, out);  // (its barriers also publish sh[])
             const float neg_step = sh[0], bc2s = sh[1];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -1012,8 +1045,11 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
         }
     } else {
         float* part = smem;  // [16 row groups][16 elements]
-        const int b = blockIdx.x - ga.g.tiles;
-        const RedP& rp = ga.red[ga.red_of[b]];
+        const int b = bx - ga.g.tiles;
+        int q0 = 0;  // descriptor of this block: a wave-uniform search over <= kMaxRed scalars
+        for (int q = 1; q < ga.nred; ++q)
+            if (b >= ga.red[q].blk0) q0 = q;
+        const RedP& rp = ga.red[q0];
         const int el = tid & (kRedElems - 1), q = tid >> 4;
         const int e = (b - rp.blk0) * kRedElems + el;
         const bool live = e < rp.n;
@@ -1055,35 +1091,61 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam ga) {
     // NEXT launch (kernel boundary). A device-scope fence here costs an L2 writeback per block on gfx950.
     if (ga.do_adam && tid == 0) {
         const unsigned prev = atomicAdd(ga.counter, 1u);
-        if (prev == gridDim.x - 1) {
+        if (prev == (unsigned)nb - 1u) {
             ga.step[agent] += 1;
             *ga.counter = 0u;
         }
     }
 }
 
+// a round's gradient + Adam launch: blocks [0, nb0) run job j0, the rest job j1 (when there are any)
+struct GradAdam2 {
+    GradAdam j0, j1;
+    int nb0;
+};
+template <int AV, int BV, int NF>
+__global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
+    if ((int)blockIdx.x < gg.nb0)
+        grad_adam_body<AV, BV, NF>(gg.j0, blockIdx.x, gg.nb0);
+    else
+        grad_adam_body<AV, BV, NF>(gg.j1, blockIdx.x - gg.nb0, gridDim.x - gg.nb0);
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // host side
 // K-panel depth of the forward / input-gradient GEMMs: whole panels (kKC) by default; FLOCK_GEMM_KC (a multiple
 // of 8 in [8, 512]) stages them in chunks (smaller LDS footprint per block; A/B diagnostics)
+int kc_knob(const char* name, int dflt) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : 0;
+    return (v >= 8 && v <= kKC && (v & 7) == 0) ? v : dflt;
+}
 int fwd_kc() {
-    static int kc = -1;
-    if (kc < 0) {
-        const char* e = getenv("FLOCK_GEMM_KC");
-        const int v = e ? atoi(e) : 0;
-        kc = (v >= 8 && v <= kKC && (v & 7) == 0) ? v : kKC;
-    }
+    static const int kc = kc_knob("FLOCK_GEMM_KC", kFwdKC);
     return kc;
 }
+int grad_kc() {
+    static const int kc = kc_knob("FLOCK_GRAD_KC", kGradKC);
+    return kc;
+}
+// K chunk for a K-deep GEMM with at most kcmax per chunk: the chunks balanced, a multiple of 8
+int balanced_kc(int K, int kcmax) {
+    const int n = (K + kcmax - 1) / kcmax;
+    const int kc = ((K + n - 1) / n + 7) & ~7;
+    return kc < kcmax ? kc : kcmax;
+}
+// float4 registers per thread per operand of a chunk (kc <= 32 NF): the instantiated depths
+int nf_of(int kc) { return kc <= 128 ? 4 : kc <= 224 ? 7 : kc <= 320 ? 10 : 16; }
 
 GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int sam, int sak,
-             int sbk, int sbn, int ldc, int64_t relB) {
+             int sbk, int sbn, int ldc, int64_t relB, const int64_t* agent = nullptr) {
     GemmP g;
     g.A = A; g.B = B; g.C = C; g.bias = bias;
     g.M = M; g.N = N; g.K = K; g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc; g.relB = relB;
+    g.agent = agent;
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
-    g.kchunk = fwd_kc();
+    g.kchunk = balanced_kc(K, fwd_kc());
     return g;
 }
 
@@ -1113,27 +1175,39 @@ int allow_lds(F* kernel, size_t bytes) {
     return 0;
 }
 
-template <int AV, int BV>
+template <int AV, int BV, int NF>
 int launch_gemm_v(hipStream_t st, const GemmBatch& gb, dim3 grid, size_t lds) {
-    if (int rc = allow_lds(sc_gemm<AV, BV>, lds)) return rc;
-    hipLaunchKernelGGL((sc_gemm<AV, BV>), grid, dim3(256), lds, st, gb);
+    if (int rc = allow_lds(sc_gemm<AV, BV, NF>, lds)) return rc;
+    hipLaunchKernelGGL((sc_gemm<AV, BV, NF>), grid, dim3(256), lds, st, gb);
     return launched();
+}
+template <int AV, int BV>
+int launch_gemm_nf(hipStream_t st, const GemmBatch& gb, dim3 grid, size_t lds, int nf) {
+    switch (nf) {
+        case 4: return launch_gemm_v<AV, BV, 4>(st, gb, grid, lds);
+        case 7: return launch_gemm_v<AV, BV, 7>(st, gb, grid, lds);
+        case 10: return launch_gemm_v<AV, BV, 10>(st, gb, grid, lds);
+        default: return launch_gemm_v<AV, BV, 16>(st, gb, grid, lds);
+    }
 }
 
 int launch_gemm(hipStream_t st, const GemmBatch& gb) {
-    int K = 0, tiles = 0, var = gemm_variant(gb.p[0]);
+    int K = 0, kc = 8, tiles = 0, var = gemm_variant(gb.p[0]);
     for (int i = 0; i < gb.n; ++i) {
         K = gb.p[i].K > K ? gb.p[i].K : K;
+        const int c = gemm_kc(gb.p[i].K, gb.p[i].kchunk);
+        kc = c > kc ? c : kc;
         tiles = gb.p[i].tiles > tiles ? gb.p[i].tiles : tiles;
         if (gemm_variant(gb.p[i]) != var) var = 3;
     }
     const dim3 grid(tiles, gb.n);
-    const size_t lds = gemm_lds_bytes(K, fwd_kc());
+    const size_t lds = gemm_lds_bytes(kc, kc);
+    const int nf = nf_of(kc);
     switch (var) {
-        case 0: return launch_gemm_v<0, 0>(st, gb, grid, lds);
-        case 1: return launch_gemm_v<0, 1>(st, gb, grid, lds);
-        case 2: return launch_gemm_v<1, 1>(st, gb, grid, lds);
-        default: return launch_gemm_v<2, 2>(st, gb, grid, lds);
+        case 0: return launch_gemm_nf<0, 0>(st, gb, grid, lds, nf);
+        case 1: return launch_gemm_nf<0, 1>(st, gb, grid, lds, nf);
+        case 2: return launch_gemm_nf<1, 1>(st, gb, grid, lds, nf);
+        default: return launch_gemm_v<2, 2, 16>(st, gb, grid, lds);
     }
 }
 
@@ -1142,24 +1216,19 @@ void add_red(GradAdam& ga, const float* D, int ldd, const float* X, int ldx, int
     RedP& r = ga.red[j];
     r.D = D; r.X = X; r.ldd = ldd; r.ldx = ldx; r.mode = mode; r.in = in; r.n = n; r.off = off;
     r.blk0 = ga.nblk;
-    for (int b = 0; b < (n + kRedElems - 1) / kRedElems; ++b)
-        if (ga.nblk < kMaxRedBlocks) ga.red_of[ga.nblk++] = (uint8_t)j; else ga.nblk = kMaxRedBlocks + 1;
+    ga.nblk += (n + kRedElems - 1) / kRedElems;
+}
+int grad_blocks(const GradAdam& ga) { return ga.g.tiles + ga.nblk + ga.soft_blocks; }
+size_t grad_lds(const GradAdam& ga) {
+    const size_t lds = gemm_lds_bytes(ga.g.K, ga.g.kchunk);
+    return lds < 16 * kRedElems * sizeof(float) ? 16 * kRedElems * sizeof(float) : lds;
 }
 
-template <int AV, int BV>
-int launch_grad_adam_v(hipStream_t st, const GradAdam& ga, dim3 grid, size_t lds) {
-    if (int rc = allow_lds(sc_grad_adam<AV, BV>, lds)) return rc;
-    hipLaunchKernelGGL((sc_grad_adam<AV, BV>), grid, dim3(256), lds, st, ga);
+template <int AV, int BV, int NF>
+int launch_grad_adam_v(hipStream_t st, const GradAdam2& gg, dim3 grid, size_t lds) {
+    if (int rc = allow_lds(sc_grad_adam<AV, BV, NF>, lds)) return rc;
+    hipLaunchKernelGGL((sc_grad_adam<AV, BV, NF>), grid, dim3(256), lds, st, gg);
     return launched();
-}
-
-int launch_grad_adam(hipStream_t st, const GradAdam& ga) {
-    if (ga.nblk > kMaxRedBlocks) return fail(-2, "flock_sc: too many reduction blocks (fc1 * in_dim too large)");
-    const dim3 grid(ga.g.tiles + ga.nblk + ga.soft_blocks);
-    size_t lds = gemm_lds_bytes(ga.g.K, ga.g.kchunk);
-    if (lds < 16 * kRedElems * sizeof(float)) lds = 16 * kRedElems * sizeof(float);
-    return gemm_variant(ga.g) == 2 ? launch_grad_adam_v<1, 1>(st, ga, grid, lds)
-                                   : launch_grad_adam_v<2, 2>(st, ga, grid, lds);
 }
 
 int check(const FlockScUpdate* u) {
@@ -1199,49 +1268,242 @@ RowArgs row_args(const FlockScUpdate* u) {
     return a;
 }
 
-// row kernel launch with the C (features per lane / 64) instantiation and its dynamic LDS
-#define SC_ROWS_CASE(NAME, CC)                                                           \
-    case CC:                                                                             \
-        if (int rc = allow_lds(NAME<CC>, lds)) return rc;                                \
-        hipLaunchKernelGGL(NAME<CC>, grid, dim3(256), lds, st, w, a);                    \
-        break;
-#define SC_ROWS(NAME)                                                                    \
-    int launch_##NAME(int C, dim3 grid, size_t lds, hipStream_t st, Ws w, RowArgs a) {  \
-        switch (C) {                                                                     \
-            SC_ROWS_CASE(NAME, 1)                                                        \
-            SC_ROWS_CASE(NAME, 2)                                                        \
-            SC_ROWS_CASE(NAME, 4)                                                        \
-            SC_ROWS_CASE(NAME, 8)                                                        \
-            default: SC_ROWS_CASE(NAME, 16)                                              \
-        }                                                                                \
-        return launched();                                                               \
-    }
-SC_ROWS(sc_c1)
-SC_ROWS(sc_c3)
-SC_ROWS(sc_a1)
-SC_ROWS(sc_a3)
-
-#define SC_LN1_CASE(CC)                                                                                          \
-    case CC:                                                                                                     \
-        hipLaunchKernelGGL(sc_ln1_bwd<CC>, dim3(rb), dim3(256), 0, st, B, F, DH, XH, RS, H, g, agent, stride, DY, \
-                           DZ);                                                                                  \
-        break;
-int launch_ln1_bwd(int C, int rb, hipStream_t st, int B, int F, const float* DH, const float* XH, const float* RS,
-                   const float* H, const float* g, const int64_t* agent, int64_t stride, float* DY, float* DZ) {
-    switch (C) {
-        SC_LN1_CASE(1)
-        SC_LN1_CASE(2)
-        SC_LN1_CASE(4)
-        SC_LN1_CASE(8)
-        default: SC_LN1_CASE(16)
-    }
-    return launched();
-}
-
 size_t fc1_lds(int in, int H1) { return (size_t)(kRowsPerBlock * kMaxIn + round4(H1 * (in + 3))) * sizeof(float); }
 
 size_t tails_lds(int na, int H2) {
     return (size_t)(round4(crit_tail_len(na, H2)) + round4(act_tail_len(na, H2))) * sizeof(float);
+}
+
+// One phase of one learn() as the arguments of the six launches of a round (launch_round):
+//   1 rows: fc1 + LN + ReLU (critic c1: 3 paths, actor a1: 2 paths)   2 forward fc2 GEMMs (critic 3, actor 2)
+//   3 rows: heads, losses, backward to the fc2 pre-activation (c3 / a3)   4 dH1 = dZ2 W2 GEMM
+//   5 ReLU + LN1 backward   6 gradient + Adam (+ soft updates)
+struct Job {
+    Ws w;
+    RowArgs a;
+    int C, rb, B, in, na, H1, H2;
+    size_t lds1, lds3;
+    GemmP fwd[3];
+    int nfwd;
+    GemmP dh;
+    Ln1Args l;
+    GradAdam ga;
+};
+
+void job_common(const FlockScUpdate* u, Job& j) {
+    j.B = u->B; j.in = u->in_dim; j.na = u->n_actions; j.H1 = u->fc1; j.H2 = u->fc2;
+    ws_layout(j.B, j.in, j.na, j.H1, j.H2, u->workspace, &j.w);
+    j.a = row_args(u);
+    j.C = chunks(u);
+    j.rb = (j.B + kRowsPerBlock - 1) / kRowsPerBlock;
+    j.lds1 = fc1_lds(j.in, j.H1);
+    j.lds3 = tails_lds(j.na, j.H2);
+}
+
+// critic phase (agent_simple_shared_critic.py:118-141)
+void critic_job(const FlockScUpdate* u, Job& j) {
+    job_common(u, j);
+    const int B = j.B, in = j.in, na = j.na, H1 = j.H1, H2 = j.H2;
+    const Ws& w = j.w;
+    const CriticOff co = critic_off(in, na, H1, H2);
+    const ActorOff ao = actor_off(in, na, H1, H2);
+    // fc2 of target actor(s'), critic(s'), critic(s)
+    j.fwd[0] = gemm_p(w.TH1, u->actors_target + ao.W2, w.Z2, u->actors_target + ao.b2, B, H2, H1, H1, 1, 1, H1, H2,
+                      u->actor_stride, u->agent);
+    j.fwd[1] = gemm_p(w.NH1, u->critic + co.W2, w.Z2 + (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1, 1, H1,
+                      H2, 0);
+    j.fwd[2] = gemm_p(w.H1, u->critic + co.W2, w.Z2 + 2 * (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1, 1,
+                      H1, H2, 0);
+    j.nfwd = 3;
+    j.dh = gemm_p(w.DZ2, u->critic + co.W2, w.DH1, nullptr, B, H1, H2, H2, 1, H1, 1, H1, 0);  // dH1 = dZ2 W2
+    j.l = Ln1Args{B, H1, w.DH1, w.XH1, w.RS1, w.H1, u->critic + co.g1, nullptr, 0, w.DY1, w.DZ1};
+    GradAdam& ga = j.ga;
+    ga.g = gemm_p(w.DZ2, w.H1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);  // dW2 = dZ2^T H1
+    ga.g.kchunk = balanced_kc(B, grad_kc());
+    ga.w2_off = co.W2;
+    ga.nred = 0;
+    ga.nblk = 0;
+    ga.B = B;
+    ga.do_adam = u->do_adam;
+    add_red(ga, w.DZ1, H1, w.S, in, 2, in, H1 * in, co.W1);
+    add_red(ga, w.DZ1, H1, nullptr, 0, 0, 1, H1, co.b1);
+    add_red(ga, w.DY1, H1, w.XH1, H1, 1, 1, H1, co.g1);
+    add_red(ga, w.DY1, H1, nullptr, 0, 0, 1, H1, co.be1);
+    add_red(ga, w.DZ2, H2, nullptr, 0, 0, 1, H2, co.b2);
+    add_red(ga, w.DY2, H2, w.XH2, H2, 1, 1, H2, co.g2);
+    add_red(ga, w.DY2, H2, nullptr, 0, 0, 1, H2, co.be2);
+    add_red(ga, w.DZA, H2, w.A, na, 2, na, H2 * na, co.Wa);
+    add_red(ga, w.DZA, H2, nullptr, 0, 0, 1, H2, co.ba);
+    add_red(ga, w.DQ, 1, w.HQ, H2, 2, H2, H2, co.Wq);
+    add_red(ga, w.DQ, 1, nullptr, 0, 0, 1, 1, co.bq);
+    add_red(ga, w.LOSS, 1, nullptr, 0, 3, 1, 1, 0);
+    ga.p = u->critic; ga.grad = u->critic_grad; ga.m = u->critic_exp_avg; ga.v = u->critic_exp_avg_sq;
+    ga.rel = 0;
+    ga.agent = u->agent;
+    ga.step = u->critic_step;
+    ga.counter = u->counters;
+    ga.loss = u->losses + 1;
+    ga.lr = u->beta; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    ga.target = nullptr; ga.self_soft = nullptr; ga.self_n = 0; ga.soft_blocks = 0;
+    // with a critic view the self soft update of this learn() rides in the critic's Adam (see FlockScUpdate)
+    const bool view = u->do_adam && u->critic_view;
+    ga.p_copy = view ? u->critic_view : nullptr;
+    ga.soft_count = view ? u->actor_steps : nullptr;
+    ga.soft_rate = view ? u->update_rate : 0;
+    ga.tau = u->tau;
+    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
+}
+
+// actor phase (:144-150), through the UPDATED critic (critic_view when given)
+void actor_job(const FlockScUpdate* u, Job& j) {
+    job_common(u, j);
+    const int B = j.B, in = j.in, na = j.na, H1 = j.H1, H2 = j.H2;
+    const Ws& w = j.w;
+    const bool view = u->do_adam && u->critic_view;
+    float* const critic = view ? u->critic_view : u->critic;  // the critic this actor step sees (post-Adam)
+    j.a.critic = critic;
+    const CriticOff co = critic_off(in, na, H1, H2);
+    const ActorOff ao = actor_off(in, na, H1, H2);
+    // fc2 of the actor and of the updated critic
+    j.fwd[0] = gemm_p(w.AH1, u->actors + ao.W2, w.Z2b, u->actors + ao.b2, B, H2, H1, H1, 1, 1, H1, H2,
+                      u->actor_stride, u->agent);
+    j.fwd[1] = gemm_p(w.CH1, critic + co.W2, w.Z2b + (int64_t)B * H2, critic + co.b2, B, H2, H1, H1, 1, 1, H1, H2,
+                      0);
+    j.nfwd = 2;
+    j.dh = gemm_p(w.ADZ2, u->actors + ao.W2, w.ADH1, nullptr, B, H1, H2, H2, 1, H1, 1, H1, u->actor_stride,
+                  u->agent);  // dH1 = dZ2 W2 (actor)
+    j.l = Ln1Args{B, H1, w.ADH1, w.AXH1, w.ARS1, w.AH1, u->actors + ao.g1, u->agent, u->actor_stride, w.ADY1,
+                  w.ADZ1};
+    GradAdam& ga = j.ga;
+    ga.g = gemm_p(w.ADZ2, w.AH1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);
+    ga.g.kchunk = balanced_kc(B, grad_kc());
+    ga.w2_off = ao.W2;
+    ga.nred = 0;
+    ga.nblk = 0;
+    ga.B = B;
+    ga.do_adam = u->do_adam;
+    add_red(ga, w.ADZ1, H1, w.S, in, 2, in, H1 * in, ao.W1);
+    add_red(ga, w.ADZ1, H1, nullptr, 0, 0, 1, H1, ao.b1);
+    add_red(ga, w.ADY1, H1, w.AXH1, H1, 1, 1, H1, ao.g1);
+    add_red(ga, w.ADY1, H1, nullptr, 0, 0, 1, H1, ao.be1);
+    add_red(ga, w.ADZ2, H2, nullptr, 0, 0, 1, H2, ao.b2);
+    add_red(ga, w.ADY2, H2, w.AXH2, H2, 1, 1, H2, ao.g2);
+    add_red(ga, w.ADY2, H2, nullptr, 0, 0, 1, H2, ao.be2);
+    add_red(ga, w.DM, na, w.AH2, H2, 2, H2, na * H2, ao.Wmu);
+    add_red(ga, w.DM, na, nullptr, 0, 0, 1, na, ao.bmu);
+    add_red(ga, w.ALOSS, 1, nullptr, 0, 3, 1, 1, 0);
+    ga.p = u->actors; ga.grad = u->actors_grad; ga.m = u->actors_exp_avg; ga.v = u->actors_exp_avg_sq;
+    ga.rel = u->actor_stride;
+    ga.agent = u->agent;
+    ga.step = u->actor_steps;
+    ga.counter = u->counters + 1;
+    ga.loss = u->losses;
+    ga.lr = u->alpha; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    const bool soft = u->do_adam && u->update_rate > 0;
+    ga.soft_rate = soft ? u->update_rate : 0;
+    ga.target = soft ? u->actors_target : nullptr;  // agent-relative like p
+    ga.self_soft = (soft && !view) ? u->critic : nullptr;  // with a view the critic kernel did it
+    ga.self_n = co.total;
+    ga.soft_blocks = (soft && !view) ? (int)((co.total + 1023) / 1024) : 0;
+    ga.tau = u->tau;
+    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
+    ga.p_copy = nullptr;
+    ga.soft_count = nullptr;
+}
+
+// the C (features per lane / 64) instantiation of a row kernel launch
+#define SC_C_SWITCH(C, ...)                  \
+    switch (C) {                             \
+        case 1: {                            \
+            constexpr int CC = 1;            \
+            __VA_ARGS__;                     \
+        } break;                             \
+        case 2: {                            \
+            constexpr int CC = 2;            \
+            __VA_ARGS__;                     \
+        } break;                             \
+        case 4: {                            \
+            constexpr int CC = 4;            \
+            __VA_ARGS__;                     \
+        } break;                             \
+        case 8: {                            \
+            constexpr int CC = 8;            \
+            __VA_ARGS__;                     \
+        } break;                             \
+        default: {                           \
+            constexpr int CC = 16;           \
+            __VA_ARGS__;                     \
+        } break;                             \
+    }
+
+size_t zmax(size_t a, size_t b) { return a > b ? a : b; }
+
+// One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in six launches; either may be
+// NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
+// computes exactly what the actor phase followed by the critic phase would.
+int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
+    const Job& A = jc ? *jc : *ja;  // the first job (placeholder arguments for an absent one)
+    const Job& Z = ja ? *ja : *jc;
+    if (jc && ja && (jc->B != ja->B || jc->in != ja->in || jc->na != ja->na || jc->H1 != ja->H1 || jc->H2 != ja->H2))
+        return fail(-5, "flock_sc_round: the two updates must have the same shapes");
+    const int C = A.C, rb = A.rb;
+    int rc = 0;
+    {  // 1: fc1 rows
+        const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
+        const size_t lds = zmax(A.lds1, Z.lds1);
+        const dim3 grid(rb, npc + npa);
+        SC_C_SWITCH(C, if ((rc = allow_lds(sc_k1<CC>, lds))) return rc;
+                    hipLaunchKernelGGL(sc_k1<CC>, grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a))
+        if ((rc = launched())) return rc;
+    }
+    {  // 2: forward fc2 GEMMs
+        GemmBatch gb;
+        gb.n = 0;
+        if (jc)
+            for (int i = 0; i < jc->nfwd; ++i) gb.p[gb.n++] = jc->fwd[i];
+        if (ja)
+            for (int i = 0; i < ja->nfwd; ++i) gb.p[gb.n++] = ja->fwd[i];
+        if ((rc = launch_gemm(st, gb))) return rc;
+    }
+    {  // 3: heads, losses, backward to the fc2 pre-activation
+        const int nbc = jc ? rb : 0;
+        const size_t lds = zmax(A.lds3, Z.lds3);
+        const dim3 grid(nbc + (ja ? rb : 0));
+        SC_C_SWITCH(C, if ((rc = allow_lds(sc_k3<CC>, lds))) return rc;
+                    hipLaunchKernelGGL(sc_k3<CC>, grid, dim3(256), lds, st, A.w, A.a, nbc, Z.w, Z.a))
+        if ((rc = launched())) return rc;
+    }
+    {  // 4: dH1 = dZ2 W2
+        GemmBatch gb;
+        gb.n = 0;
+        if (jc) gb.p[gb.n++] = jc->dh;
+        if (ja) gb.p[gb.n++] = ja->dh;
+        if ((rc = launch_gemm(st, gb))) return rc;
+    }
+    {  // 5: ReLU + LN1 backward
+        const int two = (jc && ja) ? 2 : 1;
+        const dim3 grid(rb * two);
+        SC_C_SWITCH(C, hipLaunchKernelGGL(sc_ln1_bwd<CC>, grid, dim3(256), 0, st, A.l, rb, Z.l))
+        if ((rc = launched())) return rc;
+    }
+    // 6: gradients + Adam
+    GradAdam2 gg;
+    gg.j0 = A.ga;
+    gg.j1 = Z.ga;
+    gg.nb0 = grad_blocks(A.ga);
+    const int nb = gg.nb0 + ((jc && ja) ? grad_blocks(Z.ga) : 0);
+    if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks)
+        return fail(-2, "flock_sc: too many reduction blocks (fc1 * in_dim too large)");
+    const size_t lds = zmax(grad_lds(A.ga), grad_lds(Z.ga));
+    const bool v11 = gemm_variant(A.ga.g) == 2 && gemm_variant(Z.ga.g) == 2;
+    if (!v11) return launch_grad_adam_v<2, 2, 16>(st, gg, dim3(nb), lds);
+    const int kc0 = gemm_kc(A.ga.g.K, A.ga.g.kchunk), kc1 = gemm_kc(Z.ga.g.K, Z.ga.g.kchunk);
+    switch (nf_of(kc0 > kc1 ? kc0 : kc1)) {
+        case 4: return launch_grad_adam_v<1, 1, 4>(st, gg, dim3(nb), lds);
+        case 7: return launch_grad_adam_v<1, 1, 7>(st, gg, dim3(nb), lds);
+        case 10: return launch_grad_adam_v<1, 1, 10>(st, gg, dim3(nb), lds);
+        default: return launch_grad_adam_v<1, 1, 16>(st, gg, dim3(nb), lds);
+    }
 }
 
 // learn() prologue: the agent index and the minibatch rows (Philox4x32-10, counter = (learn counter, row))
@@ -1330,176 +1592,45 @@ int64_t flock_sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int
 
 int64_t flock_sc_update_size(void) { return (int64_t)sizeof(FlockScUpdate); }
 
-int flock_sc_critic_update(void* stream, const FlockScUpdate* u) {
-    int rc = check(u);
-    if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    const int B = u->B, in = u->in_dim, na = u->n_actions, H1 = u->fc1, H2 = u->fc2;
-    Ws w;
-    ws_layout(B, in, na, H1, H2, u->workspace, &w);
-    const RowArgs a = row_args(u);
-    const CriticOff co = critic_off(in, na, H1, H2);
-    const ActorOff ao = actor_off(in, na, H1, H2);
-    const int C = chunks(u);
-    const int rb = (B + kRowsPerBlock - 1) / kRowsPerBlock;
+int flock_sc_critic_update(void* stream, const FlockScUpdate* u) { return flock_sc_round(stream, u, nullptr); }
 
-    if ((rc = launch_sc_c1(C, dim3(rb, 3), fc1_lds(in, H1), st, w, a))) return rc;
-    {  // fc2 of target actor(s'), critic(s'), critic(s)
-        GemmBatch gb;
-        gb.p[0] = gemm_p(w.TH1, u->actors_target + ao.W2, w.Z2, u->actors_target + ao.b2, B, H2, H1, H1, 1, 1,
-                         H1, H2, u->actor_stride);
-        gb.p[1] = gemm_p(w.NH1, u->critic + co.W2, w.Z2 + (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1, 1,
-                         H1, H2, 0);
-        gb.p[2] = gemm_p(w.H1, u->critic + co.W2, w.Z2 + 2 * (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1,
-                         1, H1, H2, 0);
-        gb.n = 3;
-        gb.agent = u->agent;
-        if ((rc = launch_gemm(st, gb))) return rc;
-    }
-    if ((rc = launch_sc_c3(C, dim3(rb), tails_lds(na, H2), st, w, a))) return rc;
-    {  // dH1 = dZ2 W2
-        GemmBatch gb;
-        gb.p[0] = gemm_p(w.DZ2, u->critic + co.W2, w.DH1, nullptr, B, H1, H2, H2, 1, H1, 1, H1, 0);
-        gb.n = 1;
-        gb.agent = u->agent;
-        if ((rc = launch_gemm(st, gb))) return rc;
-    }
-    if ((rc = launch_ln1_bwd(C, rb, st, B, H1, w.DH1, w.XH1, w.RS1, w.H1, u->critic + co.g1, nullptr, 0, w.DY1,
-                             w.DZ1)))
-        return rc;
+int flock_sc_actor_update(void* stream, const FlockScUpdate* u) { return flock_sc_round(stream, nullptr, u); }
 
-    GradAdam ga;
-    ga.g = gemm_p(w.DZ2, w.H1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);  // dW2 = dZ2^T H1
-    ga.g.kchunk = kGradKC;
-    ga.w2_off = co.W2;
-    ga.nred = 0;
-    ga.nblk = 0;
-    ga.B = B;
-    ga.do_adam = u->do_adam;
-    add_red(ga, w.DZ1, H1, w.S, in, 2, in, H1 * in, co.W1);
-    add_red(ga, w.DZ1, H1, nullptr, 0, 0, 1, H1, co.b1);
-    add_red(ga, w.DY1, H1, w.XH1, H1, 1, 1, H1, co.g1);
-    add_red(ga, w.DY1, H1, nullptr, 0, 0, 1, H1, co.be1);
-    add_red(ga, w.DZ2, H2, nullptr, 0, 0, 1, H2, co.b2);
-    add_red(ga, w.DY2, H2, w.XH2, H2, 1, 1, H2, co.g2);
-    add_red(ga, w.DY2, H2, nullptr, 0, 0, 1, H2, co.be2);
-    add_red(ga, w.DZA, H2, w.A, na, 2, na, H2 * na, co.Wa);
-    add_red(ga, w.DZA, H2, nullptr, 0, 0, 1, H2, co.ba);
-    add_red(ga, w.DQ, 1, w.HQ, H2, 2, H2, H2, co.Wq);
-    add_red(ga, w.DQ, 1, nullptr, 0, 0, 1, 1, co.bq);
-    add_red(ga, w.LOSS, 1, nullptr, 0, 3, 1, 1, 0);
-    ga.p = u->critic; ga.grad = u->critic_grad; ga.m = u->critic_exp_avg; ga.v = u->critic_exp_avg_sq;
-    ga.rel = 0;
-    ga.agent = u->agent;
-    ga.step = u->critic_step;
-    ga.counter = u->counters;
-    ga.loss = u->losses + 1;
-    ga.lr = u->beta; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
-    ga.target = nullptr; ga.self_soft = nullptr; ga.self_n = 0; ga.soft_blocks = 0;
-    // with a critic view the self soft update of this learn() rides in the critic's Adam (see FlockScUpdate)
-    const bool view = u->do_adam && u->critic_view;
-    ga.p_copy = view ? u->critic_view : nullptr;
-    ga.soft_count = view ? u->actor_steps : nullptr;
-    ga.soft_rate = view ? u->update_rate : 0;
-    ga.tau = u->tau;
-    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
-    return launch_grad_adam(st, ga);
-}
-
-int flock_sc_actor_update(void* stream, const FlockScUpdate* u) {
-    int rc = check(u);
-    if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    const int B = u->B, in = u->in_dim, na = u->n_actions, H1 = u->fc1, H2 = u->fc2;
-    Ws w;
-    ws_layout(B, in, na, H1, H2, u->workspace, &w);
-    RowArgs a = row_args(u);
-    const bool view = u->do_adam && u->critic_view;
-    float* const critic = view ? u->critic_view : u->critic;  // the critic this actor step sees (post-Adam)
-    a.critic = critic;
-    const CriticOff co = critic_off(in, na, H1, H2);
-    const ActorOff ao = actor_off(in, na, H1, H2);
-    const int C = chunks(u);
-    const int rb = (B + kRowsPerBlock - 1) / kRowsPerBlock;
-
-    if ((rc = launch_sc_a1(C, dim3(rb, 2), fc1_lds(in, H1), st, w, a))) return rc;
-    {  // fc2 of the actor and of the updated critic
-        GemmBatch gb;
-        gb.p[0] = gemm_p(w.AH1, u->actors + ao.W2, w.Z2b, u->actors + ao.b2, B, H2, H1, H1, 1, 1, H1, H2,
-                         u->actor_stride);
-        gb.p[1] = gemm_p(w.CH1, critic + co.W2, w.Z2b + (int64_t)B * H2, critic + co.b2, B, H2, H1, H1, 1, 1, H1,
-                         H2, 0);
-        gb.n = 2;
-        gb.agent = u->agent;
-        if ((rc = launch_gemm(st, gb))) return rc;
-    }
-    if ((rc = launch_sc_a3(C, dim3(rb), tails_lds(na, H2), st, w, a))) return rc;
-    {  // dH1 = dZ2 W2 (actor)
-        GemmBatch gb;
-        gb.p[0] = gemm_p(w.ADZ2, u->actors + ao.W2, w.ADH1, nullptr, B, H1, H2, H2, 1, H1, 1, H1,
-                         u->actor_stride);
-        gb.n = 1;
-        gb.agent = u->agent;
-        if ((rc = launch_gemm(st, gb))) return rc;
-    }
-    if ((rc = launch_ln1_bwd(C, rb, st, B, H1, w.ADH1, w.AXH1, w.ARS1, w.AH1, u->actors + ao.g1, u->agent,
-                             u->actor_stride, w.ADY1, w.ADZ1)))
-        return rc;
-
-    GradAdam ga;
-    ga.g = gemm_p(w.ADZ2, w.AH1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);
-    ga.g.kchunk = kGradKC;
-    ga.w2_off = ao.W2;
-    ga.nred = 0;
-    ga.nblk = 0;
-    ga.B = B;
-    ga.do_adam = u->do_adam;
-    add_red(ga, w.ADZ1, H1, w.S, in, 2, in, H1 * in, ao.W1);
-    add_red(ga, w.ADZ1, H1, nullptr, 0, 0, 1, H1, ao.b1);
-    add_red(ga, w.ADY1, H1, w.AXH1, H1, 1, 1, H1, ao.g1);
-    add_red(ga, w.ADY1, H1, nullptr, 0, 0, 1, H1, ao.be1);
-    add_red(ga, w.ADZ2, H2, nullptr, 0, 0, 1, H2, ao.b2);
-    add_red(ga, w.ADY2, H2, w.AXH2, H2, 1, 1, H2, ao.g2);
-    add_red(ga, w.ADY2, H2, nullptr, 0, 0, 1, H2, ao.be2);
-    add_red(ga, w.DM, na, w.AH2, H2, 2, H2, na * H2, ao.Wmu);
-    add_red(ga, w.DM, na, nullptr, 0, 0, 1, na, ao.bmu);
-    add_red(ga, w.ALOSS, 1, nullptr, 0, 3, 1, 1, 0);
-    ga.p = u->actors; ga.grad = u->actors_grad; ga.m = u->actors_exp_avg; ga.v = u->actors_exp_avg_sq;
-    ga.rel = u->actor_stride;
-    ga.agent = u->agent;
-    ga.step = u->actor_steps;
-    ga.counter = u->counters + 1;
-    ga.loss = u->losses;
-    ga.lr = u->alpha; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
-    const bool soft = u->do_adam && u->update_rate > 0;
-    ga.soft_rate = soft ? u->update_rate : 0;
-    ga.target = soft ? u->actors_target : nullptr;  // agent-relative like p
-    ga.self_soft = (soft && !view) ? u->critic : nullptr;  // with a view the critic kernel did it
-    ga.self_n = co.total;
-    ga.soft_blocks = (soft && !view) ? (int)((co.total + 1023) / 1024) : 0;
-    ga.tau = u->tau;
-    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
-    ga.p_copy = nullptr;
-    ga.soft_count = nullptr;
-    return launch_grad_adam(st, ga);
+int flock_sc_round(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u) {
+    if (!critic_u && !actor_u) return fail(-3, "flock_sc_round: NULL argument");
+    int rc = 0;
+    if (critic_u && (rc = check(critic_u))) return rc;
+    if (actor_u && (rc = check(actor_u))) return rc;
+    Job jc, ja;
+    if (critic_u) critic_job(critic_u, jc);
+    if (actor_u) actor_job(actor_u, ja);
+    return launch_round((hipStream_t)stream, critic_u ? &jc : nullptr, actor_u ? &ja : nullptr);
 }
 
 
 }  // extern "C"
 
 // ---------------------------------------------------------------------------------------------------------------
-// learn() pipeline: the config-3 loop's per-step learner work in one call (see include/flock_learn.h)
+// learn() pipeline: the config-3 loop's per-step learner work in one call (see include/flock_learn.h). Rounds are
+// replayed from HIP graphs captured once: merged[s] = critic phase of slot s + actor phase of slot s - 1 (mod n),
+// conly[s] / aonly[s] = one phase alone.
+constexpr int kMaxSlots = 8;
 struct FlockScPipeline {
-    FlockScUpdate u[2];
-    FlockScRows ring, staging[2];
-    hipGraphExec_t gc[2], ga[2];
-    hipEvent_t snap_done[2], critic_done[2], learn_done[2];
-    bool used[2];
+    int n;
+    FlockScUpdate u[kMaxSlots];
+    FlockScRows ring, staging[kMaxSlots];
+    hipGraphExec_t merged[kMaxSlots], conly[kMaxSlots], aonly[kMaxSlots];
+    Job jc[kMaxSlots], ja[kMaxSlots];  // direct launches (graphs == false): the rounds' arguments, built once
+    bool graphs;
+    hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
+    bool used[kMaxSlots];
     int slot;
+    int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
+    int64_t pending_agent;
 };
 
 namespace {
-int capture_phase(const FlockScUpdate* u, bool critic, hipGraphExec_t* out) {
+int capture_round(const FlockScUpdate* uc, const FlockScUpdate* ua, hipGraphExec_t* out) {
     hipStream_t cs;
     if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return fail(-4, "flock_sc_pipeline: stream");
     hipGraph_t g = nullptr;
@@ -1507,88 +1638,139 @@ int capture_phase(const FlockScUpdate* u, bool critic, hipGraphExec_t* out) {
     if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
         rc = fail(-4, "flock_sc_pipeline: begin capture");
     } else {
-        rc = critic ? flock_sc_critic_update(cs, u) : flock_sc_actor_update(cs, u);
+        rc = flock_sc_round(cs, uc, ua);
         const hipError_t e = hipStreamEndCapture(cs, &g);
         if (!rc && e != hipSuccess) rc = fail(-4, hipGetErrorString(e));
         if (!rc && hipGraphInstantiate(out, g, nullptr, nullptr, 0) != hipSuccess)
             rc = fail(-4, "flock_sc_pipeline: graph instantiate");
     }
-    if (g) hipGraphDestroy(g);
-    hipStreamDestroy(cs);
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipStreamDestroy(cs);
     return rc;
+}
+// one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none)
+int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a) {
+    if (!p->graphs) return launch_round(ls, c >= 0 ? &p->jc[c] : nullptr, a >= 0 ? &p->ja[a] : nullptr);
+    hipGraphExec_t g = c >= 0 && a >= 0 ? p->merged[c] : (c >= 0 ? p->conly[c] : p->aonly[a]);
+    return hipGraphLaunch(g, ls) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: graph launch failed");
 }
 }  // namespace
 
 extern "C" {
 
-FlockScPipeline* flock_sc_pipeline_create(const FlockScUpdate* slot0, const FlockScUpdate* slot1,
-                                          const FlockScRows* ring, const FlockScRows* staging0,
-                                          const FlockScRows* staging1) {
-    if (!slot0 || !slot1 || !ring || !staging0 || !staging1) {
+FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slots, const FlockScRows* ring,
+                                          const FlockScRows* staging) {
+    if (!slots || !ring || !staging) {
         fail(-3, "flock_sc_pipeline_create: NULL argument");
         return nullptr;
     }
-    if (check(slot0) || check(slot1)) return nullptr;
-    if (!slot0->do_adam || !slot1->do_adam || !slot0->critic_view || !slot1->critic_view ||
-        slot0->critic_view == slot1->critic_view || slot0->workspace == slot1->workspace) {
-        fail(-5, "flock_sc_pipeline_create: each slot needs do_adam, its own critic_view and its own workspace");
+    if (n_slots < 2 || n_slots > kMaxSlots) {
+        fail(-5, "flock_sc_pipeline_create: 2 <= n_slots <= 8");
         return nullptr;
     }
+    for (int i = 0; i < n_slots; ++i) {
+        if (check(&slots[i])) return nullptr;
+        if (!slots[i].do_adam || !slots[i].critic_view) {
+            fail(-5, "flock_sc_pipeline_create: each slot needs do_adam and a critic_view");
+            return nullptr;
+        }
+        for (int j = 0; j < i; ++j)
+            if (slots[i].critic_view == slots[j].critic_view || slots[i].workspace == slots[j].workspace) {
+                fail(-5, "flock_sc_pipeline_create: each slot needs its own critic_view and workspace");
+                return nullptr;
+            }
+    }
     FlockScPipeline* p = new FlockScPipeline();
-    p->u[0] = *slot0;
-    p->u[1] = *slot1;
+    p->n = n_slots;
     p->ring = *ring;
-    p->staging[0] = *staging0;
-    p->staging[1] = *staging1;
+    for (int i = 0; i < n_slots; ++i) {
+        p->u[i] = slots[i];
+        p->staging[i] = staging[i];
+    }
+    // rounds launched directly from arguments built here (6 hipLaunchKernel per round), or replayed as HIP graphs
+    // (FLOCK_SC_PIPELINE_GRAPHS=1, read here once): config-3 step 0.117 ms direct vs 0.125 ms with graphs
+    const char* ge = getenv("FLOCK_SC_PIPELINE_GRAPHS");
+    p->graphs = ge && ge[0] == '1';
     int rc = 0;
-    for (int i = 0; i < 2 && !rc; ++i) {
-        rc = capture_phase(&p->u[i], true, &p->gc[i]);
-        if (!rc) rc = capture_phase(&p->u[i], false, &p->ga[i]);
-        hipEvent_t* evs[3] = {&p->snap_done[i], &p->critic_done[i], &p->learn_done[i]};
+    for (int i = 0; i < n_slots && !rc; ++i) {
+        critic_job(&p->u[i], p->jc[i]);
+        actor_job(&p->u[i], p->ja[i]);
+        if (p->graphs) {
+            rc = capture_round(&p->u[i], nullptr, &p->conly[i]);
+            if (!rc) rc = capture_round(nullptr, &p->u[i], &p->aonly[i]);
+            if (!rc) rc = capture_round(&p->u[i], &p->u[(i + n_slots - 1) % n_slots], &p->merged[i]);
+        }
+        hipEvent_t* evs[2] = {&p->snap_done[i], &p->slot_free[i]};
         for (hipEvent_t* e : evs)
             if (!rc && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
                 rc = fail(-4, "flock_sc_pipeline_create: event");
         p->used[i] = false;
     }
     p->slot = 0;
+    p->pending = -1;
+    p->pending_agent = -1;
     if (rc) {
-        delete p;  // (a failed create leaks at most the objects made before the failure)
+        flock_sc_pipeline_destroy(p);
         return nullptr;
     }
     return p;
 }
 
-int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* critic_stream, void* actor_stream,
-                            int64_t rows, uint64_t seed, uint64_t counter, int64_t agent, int wait_previous) {
+int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
+                            uint64_t counter, int64_t agent) {
     if (!p) return fail(-3, "flock_sc_pipeline_learn: NULL pipeline");
-    hipStream_t es = (hipStream_t)env_stream, cs = (hipStream_t)critic_stream, as = (hipStream_t)actor_stream;
-    const int s = p->slot;
+    hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
+    const int s = p->slot, n = p->n;
     const FlockScUpdate& u = p->u[s];
-    if (p->used[s] && hipStreamWaitEvent(es, p->learn_done[s], 0) != hipSuccess)
+    if (p->used[s] && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
     int rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                     u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
     if (rc) return rc;
-    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
-              hipStreamWaitEvent(cs, p->snap_done[s], 0) == hipSuccess;
-    if (ok && wait_previous && p->used[s ^ 1]) ok = hipStreamWaitEvent(cs, p->learn_done[s ^ 1], 0) == hipSuccess;
-    ok = ok && hipGraphLaunch(p->gc[s], cs) == hipSuccess && hipEventRecord(p->critic_done[s], cs) == hipSuccess &&
-         hipStreamWaitEvent(as, p->critic_done[s], 0) == hipSuccess && hipGraphLaunch(p->ga[s], as) == hipSuccess &&
-         hipEventRecord(p->learn_done[s], as) == hipSuccess;
+    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess && hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess;
     if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
+    const int q = p->pending;
+    if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
+        // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
+        if ((rc = pipeline_round(p, ls, s, q))) return rc;
+        ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
+    } else {
+        // same agent (this critic phase reads the target actor that actor phase soft-updates): one after the other
+        if (q >= 0) {
+            if ((rc = pipeline_round(p, ls, -1, q))) return rc;
+            ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
+        }
+        if (ok && (rc = pipeline_round(p, ls, s, -1))) return rc;
+    }
+    if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
+    p->pending = s;
+    p->pending_agent = agent;
     p->used[s] = true;
-    p->slot = s ^ 1;
+    p->slot = (s + 1) % n;
+    return 0;
+}
+
+int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream) {
+    if (!p) return fail(-3, "flock_sc_pipeline_flush: NULL pipeline");
+    const int q = p->pending;
+    if (q < 0) return 0;
+    hipStream_t ls = (hipStream_t)learner_stream;
+    if (int rc = pipeline_round(p, ls, -1, q)) return rc;
+    if (hipEventRecord(p->slot_free[q], ls) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_flush: stream operation failed");
+    p->pending = -1;
     return 0;
 }
 
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;
-    for (int i = 0; i < 2; ++i) {
-        hipGraphExecDestroy(p->gc[i]);
-        hipGraphExecDestroy(p->ga[i]);
-        hipEventDestroy(p->snap_done[i]);
-        hipEventDestroy(p->critic_done[i]);
-        hipEventDestroy(p->learn_done[i]);
+    for (int i = 0; i < p->n; ++i) {
+        hipGraphExec_t* gs[3] = {&p->merged[i], &p->conly[i], &p->aonly[i]};
+        for (hipGraphExec_t* g : gs)
+            if (*g) (void)hipGraphExecDestroy(*g);
+        hipEvent_t* evs[2] = {&p->snap_done[i], &p->slot_free[i]};
+        for (hipEvent_t* e : evs)
+            if (*e) (void)hipEventDestroy(*e);
     }
     delete p;
 }

@@ -85,7 +85,7 @@ class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
                  ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
-                 snapshot=False, replay=None):
+                 snapshot=False, replay=None, n_slots=2):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -132,6 +132,7 @@ class SharedCriticLearner:
         # into one of two staging slots and the update reads that copy, so the ring may be rewritten while the
         # update runs (snapshot_into / update_slot: the copy on the env stream, the update on another one)
         self.snapshot = bool(snapshot and fused)
+        self.n_slots = max(2, int(n_slots))
         if fused:
             self._init_fused()
 
@@ -145,10 +146,11 @@ class SharedCriticLearner:
         self.sc_workspace = torch.zeros(int(n_ws), dtype=torch.float32, device=dev)
         self.sc_counters = torch.zeros(2, dtype=torch.int32, device=dev)
         # critic views (FlockScUpdate.critic_view): the critic phase writes the post-Adam critic into a view and the
-        # self soft update into critic.data; the actor phase reads the view. Two views and two workspaces (one per
-        # staging slot) let the critic phase of learn t+1 run beside the actor phase of learn t (pipelined()).
-        self.critic_views = [torch.zeros_like(self.critic.data) for _ in range(2)]
-        self.sc_workspaces = [self.sc_workspace, torch.zeros_like(self.sc_workspace)]
+        # self soft update into critic.data; the actor phase reads the view. One view and one workspace per staging
+        # slot let the critic phase of learn t+1 run beside the actor phase of learn t (pipeline(), flock_sc_round).
+        ns = self.n_slots if self.snapshot else 2
+        self.critic_views = [torch.zeros_like(self.critic.data) for _ in range(ns)]
+        self.sc_workspaces = [self.sc_workspace] + [torch.zeros_like(self.sc_workspace) for _ in range(ns - 1)]
         rb = self.replay.bufs
         C, A = self.critic, self.actors
         fields = dict(B=B, in_dim=n_in, n_actions=na, fc1=self.fc1, fc2=self.fc2, do_adam=1,
@@ -170,7 +172,7 @@ class SharedCriticLearner:
             self.identity_idx = torch.arange(B, dtype=torch.int64, device=dev)
             names = ("state", "new_state", "action", "reward", "terminal")
             self._rows_ring = _native.FlockScRows(**{n: _p(rb[n]) for n in names})
-            for i in range(2):
+            for i in range(self.n_slots):
                 stg = {"state": torch.zeros(B, n_in, device=dev), "new_state": torch.zeros(B, n_in, device=dev),
                        "action": torch.zeros(B, na, device=dev), "reward": torch.zeros(B, device=dev),
                        "terminal": torch.zeros(B, device=dev)}
@@ -457,35 +459,40 @@ class SharedCriticLearner:
         return self._finish_learn(agent, soft_in_kernel=True)
 
     def pipeline(self):
-        """The native learn() pipeline (flock_sc_pipeline_*, include/flock_learn.h) over the two staging slots:
-        snapshot, critic-phase graph and actor-phase graph of one learn() enqueued by ONE C call, the actor phase
-        of learn t beside the critic phase of learn t+1 (the update_slot_pipelined schedule without its per-step
-        Python and graph-replay host cost)."""
+        """The native learn() pipeline (flock_sc_pipeline_*, include/flock_learn.h) over the n_slots staging slots:
+        snapshot plus ONE six-launch round (this learn's critic phase with the previous learn's actor phase,
+        flock_sc_round) enqueued by one C call, no cross-stream wait between the phases."""
         if self.__dict__.get("_pipe") is None:
             if not (self.snapshot and self.fused) or self.distributed:
                 raise RuntimeError("the native pipeline needs a single-GPU fused learner with snapshot=True")
             lib = _native.lib()
-            S0, S1 = self._slots
-            h = lib.flock_sc_pipeline_create(ctypes.byref(S0["sc"]), ctypes.byref(S1["sc"]),
-                                             ctypes.byref(self._rows_ring), ctypes.byref(S0["rows"]),
-                                             ctypes.byref(S1["rows"]))
+            n = len(self._slots)
+            us = (_native.FlockScUpdate * n)(*[S["sc"] for S in self._slots])
+            rows = (_native.FlockScRows * n)(*[S["rows"] for S in self._slots])
+            h = lib.flock_sc_pipeline_create(n, us, ctypes.byref(self._rows_ring), rows)
             if not h:
                 raise RuntimeError("flock_sc_pipeline_create: " + lib.flock_learn_last_error().decode())
             self._pipe = h
         return self._pipe
 
-    def pipeline_learn(self, agent, env_stream, critic_stream, actor_stream, wait_previous):
-        """Enqueue learn(agent) through the native pipeline (raw stream handles). Returns False (nothing enqueued)
-        before the buffer holds a batch, like snapshot_into."""
+    def pipeline_learn(self, agent, env_stream, learner_stream):
+        """Enqueue learn(agent) through the native pipeline (raw stream handles): the snapshot on env_stream, the
+        round on learner_stream. The actor phase stays pending until the next call or pipeline_flush. Returns False
+        (nothing enqueued) before the buffer holds a batch, like snapshot_into."""
         if self.replay.counter < self.batch_size:
             return False
         self._learn_calls += 1
-        rc = _native.lib().flock_sc_pipeline_learn(self.pipeline(), env_stream, critic_stream, actor_stream,
-                                                   len(self.replay), self.seed, self._learn_calls, int(agent),
-                                                   int(bool(wait_previous)))
+        rc = _native.lib().flock_sc_pipeline_learn(self.pipeline(), env_stream, learner_stream, len(self.replay),
+                                                   self.seed, self._learn_calls, int(agent))
         _native.check(rc, "flock_sc_pipeline_learn", learn=True)
         self._finish_learn(agent, soft_in_kernel=True)
         return True
+
+    def pipeline_flush(self, learner_stream):
+        """Enqueue the pending actor phase of the last pipeline_learn (no-op when none)."""
+        if self.__dict__.get("_pipe") is not None:
+            _native.check(_native.lib().flock_sc_pipeline_flush(self._pipe, learner_stream),
+                          "flock_sc_pipeline_flush", learn=True)
 
     def __del__(self):
         h = self.__dict__.get("_pipe")
@@ -529,7 +536,7 @@ class SharedCriticBench:
     """bench.py hook for BASELINE config 3: after each vectorized env step, insert every agent's transition into the
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
-    def __init__(self, env, device, seed=0, fused=True, overlap=True):
+    def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=3):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
@@ -539,10 +546,12 @@ class SharedCriticBench:
         self.overlap = bool(overlap and fused)
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
                                            buffer_size=1_000_000, dist_group=group, fused=fused,
-                                           snapshot=self.overlap)
+                                           snapshot=self.overlap, n_slots=n_slots)
         if self.overlap:
-            # single GPU: learn() runs as two phases on two streams, the actor phase of learn s beside the critic
-            # phase of learn s+1 (SharedCriticLearner.update_slot_pipelined); FLOCK_LEARN_PIPELINE=0 keeps one
+            # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
+            # with graphs, the native pipeline (one merged six-launch round per step on self.stream,
+            # SharedCriticLearner.pipeline_learn); without, two streams (update_slot_pipelined).
+            # FLOCK_LEARN_PIPELINE=0 keeps one serial learn() per step on self.stream.
             self.pipelined = not self.learner.distributed and os.environ.get("FLOCK_LEARN_PIPELINE") != "0"
             # stream priority (FLOCK_LEARNER_PRIORITY=1): the one-stream learner ran at high priority; with the two
             # pipelined streams high priority made steps 2-3x slower in fresh processes (tools/pipe_bench_probe.py)
@@ -581,14 +590,12 @@ class SharedCriticBench:
         # the update runs on the learner stream; staging slots alternate, and a slot is refilled only after the
         # update that read it two steps ago has finished
         if self.pipelined and L.use_graph:
-            # the native pipeline: snapshot on the env stream, critic phase on self.stream, actor phase on
-            # self.actor_stream, all enqueued by one C call (stream handles cached at the first call: the env
-            # stream is the stream current then)
+            # the native pipeline: snapshot on the env stream, then one round (this critic phase + the previous
+            # learn's actor phase) on self.stream, enqueued by one C call (stream handles cached at the first call:
+            # the env stream is the stream current then)
             if self._handles is None:
-                self._handles = (torch.cuda.current_stream(L.device).cuda_stream, self.stream.cuda_stream,
-                                 self.actor_stream.cuda_stream)
-            L.pipeline_learn(agent, *self._handles, wait_previous=agent == self._prev_agent)
-            self._prev_agent = agent
+                self._handles = (torch.cuda.current_stream(L.device).cuda_stream, self.stream.cuda_stream)
+            L.pipeline_learn(agent, *self._handles)
             return
         main = torch.cuda.current_stream(L.device)
         slot = s & 1
@@ -614,8 +621,11 @@ class SharedCriticBench:
         self._used[slot] = True
 
     def finish(self):
-        """Join the learner stream(s) into the current one (end of a timed region)."""
+        """Enqueue the pending actor phase (native pipeline) and join the learner stream(s) into the current one
+        (end of a timed region)."""
         if self.overlap:
+            if self._handles is not None:
+                self.learner.pipeline_flush(self._handles[1])
             cur = torch.cuda.current_stream(self.learner.device)
             cur.wait_stream(self.stream)
             if self.actor_stream is not None:

@@ -35,7 +35,8 @@ def test_header_declares_expected_entry_points():
                  "flock_reset", "flock_abi_version", "flock_last_error", "flock_adam_step", "flock_soft_update",
                  "flock_grad_norm", "flock_gru_fwd", "flock_gru_bwd", "flock_gather_rows", "flock_scatter_rows",
                  "flock_sc_workspace_floats", "flock_sc_critic_update", "flock_sc_actor_update",
-                 "flock_sc_prep_snapshot"):
+                 "flock_sc_prep_snapshot", "flock_sc_round", "flock_sc_pipeline_create", "flock_sc_pipeline_learn",
+                 "flock_sc_pipeline_flush"):
         assert name in fns, name
 
 
@@ -92,3 +93,14 @@ def test_shared_critic_update_struct_and_argument_checks(lib):
     u.fc1 = 2048
     assert lib.flock_sc_critic_update(None, ctypes.byref(u)) == -2  # beyond the row-kernel limits
     assert "fc1/fc2 <= 1024" in lib.flock_learn_last_error().decode()
+
+
+def test_shared_critic_round_and_pipeline_argument_checks(lib):
+    assert lib.flock_sc_round(None, None, None) == -3
+    u = _native.FlockScUpdate(B=16, in_dim=4, n_actions=2, fc1=32, fc2=24, do_adam=1)
+    assert lib.flock_sc_round(None, ctypes.byref(u), None) == -3  # NULL pointers, checked before any launch
+    rows = _native.FlockScRows()
+    assert not lib.flock_sc_pipeline_create(1, ctypes.byref(u), ctypes.byref(rows), ctypes.byref(rows))
+    assert "n_slots" in lib.flock_learn_last_error().decode()
+    assert lib.flock_sc_pipeline_flush(None, None) == -3
+    assert lib.flock_sc_pipeline_learn(None, None, None, 1, 0, 0, 0) == -3

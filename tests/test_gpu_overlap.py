@@ -111,3 +111,42 @@ def test_pipelined_phases_same_agent_equal_serial(cuda):
                  (ser.actors.data, pip.actors.data), (ser.actors.target, pip.actors.target),
                  (ser.actor_steps, pip.actor_steps), (ser.critic.step_dev, pip.critic.step_dev)):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("agents,n_slots", [((0, 0, 0, 1, 1, 0, 2, 1, 1, 2), 2), ((0, 1, 2, 0, 0, 1, 2, 2, 1, 0), 3),
+                                            ((3, 1, 4, 1, 5, 9, 2, 6, 5, 3), 4)],
+                         ids=["same-agent-runs-2slots", "mixed-3slots", "distinct-4slots"])
+def test_native_pipeline_rounds_equal_serial(agents, n_slots, cuda):
+    """The native pipeline (flock_sc_pipeline_learn): one six-launch round per learn() = its critic phase merged
+    with the previous learn's actor phase (flock_sc_round), or the two phases one after the other when both learns
+    have the same agent; the last actor phase is enqueued by flock_sc_pipeline_flush. After a sequence with runs of
+    the same agent, every parameter, moment, target, step counter and loss is bitwise the serial learn() sequence."""
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    ser = SharedCriticLearner(10, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=False)
+    pip = SharedCriticLearner(10, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=True,
+                              n_slots=n_slots)
+    g = torch.Generator(device=cuda).manual_seed(4)
+    n = 300
+    rows = (torch.rand(n, 4, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g),
+            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, 4, device=cuda, generator=g),
+            torch.rand(n, device=cuda, generator=g) > 0.5)
+    for L in (ser, pip):
+        L.store_transitions(*rows)
+    ls = torch.cuda.Stream(device=cuda)
+    main = torch.cuda.current_stream(cuda)
+    losses = []
+    for a in agents:
+        ser.learn(a)
+        losses.append(ser.losses.clone())
+        assert pip.pipeline_learn(a, main.cuda_stream, ls.cuda_stream)
+    pip.pipeline_flush(ls.cuda_stream)
+    pip.pipeline_flush(ls.cuda_stream)  # nothing pending: a no-op
+    main.wait_stream(ls)
+    torch.cuda.synchronize()
+    for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg, pip.critic.exp_avg),
+                 (ser.critic.exp_avg_sq, pip.critic.exp_avg_sq), (ser.actors.data, pip.actors.data),
+                 (ser.actors.exp_avg, pip.actors.exp_avg), (ser.actors.target, pip.actors.target),
+                 (ser.actor_steps, pip.actor_steps), (ser.critic.step_dev, pip.critic.step_dev),
+                 (ser.losses, pip.losses)):
+        assert torch.equal(x, y)

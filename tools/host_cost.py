@@ -35,7 +35,14 @@ def host(name, fn, n=200):
     print(f"{name:14s} host {1e6 * (t1 - t0) / n:8.1f} us/call   wall {1e6 * (t2 - t0) / n:8.1f} us/call")
 
 
+def after_only(i):
+    L.replay_slots(E * N)
+    hook.after(i, a)
+
+
 host("replay_slots", lambda i: L.replay_slots(E * N))
 host("env.step+ring", lambda i: env.step(a, ring=L.replay_slots(E * N)))
-host("learn", lambda i: L.learn(i % N))
+host("hook.after", after_only)
+hook.finish()
 host("bench step", lambda i: hook.step(i, a))
+hook.finish()
