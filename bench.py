@@ -323,6 +323,7 @@ def main():
         one_step(args.warmup + s, ev.get(s))
     if hook is not None and hasattr(hook, "finish"):
         hook.finish()  # the learner work still pending (the last learn's actor phase) runs inside the timed region
+    host_el = time.perf_counter() - t0  # host enqueue time of the timed steps (no synchronisation inside)
     torch.cuda.synchronize(dev)
     barrier(world)
     el = time.perf_counter() - t0
@@ -376,6 +377,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
+        "host_ms_per_step": host_el / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong" if args.global_split else "weak",
         "vs_baseline": None,

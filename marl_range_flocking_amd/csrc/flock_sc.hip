@@ -96,11 +96,11 @@ struct Ws {
     float *TH1, *NH1, *XH1, *RS1, *H1;     // fc1 outputs: target actor(s'), critic(s'), critic(s) xhat/rstd/h
     float* Z2;                             // [3][B][H2] fc2 pre-LN: target actor(s'), critic(s'), critic(s)
     float *XH2, *RS2, *HQ, *DZA, *DY2, *DZ2, *DQ, *LOSS;
-    float *DH1, *DY1, *DZ1;
+    float *DY1, *DXH1, *PS1;               // LN1 backward: dy, dxh = dy g1, row sums per dH tile [B][tiles][2]
     float *AXH1, *ARS1, *AH1, *CH1;        // actor phase fc1: actor xhat/rstd/h, updated critic h
     float* Z2b;                            // [2][B][H2] actor fc2, critic fc2
     float *AXH2, *ARS2, *AH2, *DM, *ADY2, *ADZ2, *ALOSS;
-    float *ADH1, *ADY1, *ADZ1;
+    float *ADY1, *ADXH1, *APS1;
 };
 
 int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
@@ -117,12 +117,13 @@ int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
     x.Z2 = take(3 * (int64_t)H2);
     x.XH2 = take(H2); x.RS2 = take(1); x.HQ = take(H2); x.DZA = take(H2); x.DY2 = take(H2); x.DZ2 = take(H2);
     x.DQ = take(1); x.LOSS = take(1);
-    x.DH1 = take(H1); x.DY1 = take(H1); x.DZ1 = take(H1);
+    const int ps = 2 * ((H1 + 31) / 32);  // (sum dxh, sum dxh xh) per 32-column tile of a dH1 row
+    x.DY1 = take(H1); x.DXH1 = take(H1); x.PS1 = take(ps);
     x.AXH1 = take(H1); x.ARS1 = take(1); x.AH1 = take(H1); x.CH1 = take(H1);
     x.Z2b = take(2 * (int64_t)H2);
     x.AXH2 = take(H2); x.ARS2 = take(1); x.AH2 = take(H2); x.DM = take(na); x.ADY2 = take(H2); x.ADZ2 = take(H2);
     x.ALOSS = take(1);
-    x.ADH1 = take(H1); x.ADY1 = take(H1); x.ADZ1 = take(H1);
+    x.ADY1 = take(H1); x.ADXH1 = take(H1); x.APS1 = take(ps);
     if (w) *w = x;
     return off;
 }
@@ -457,34 +458,6 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
 }
 
 // c5 / a5: ReLU + LN1 backward: dy = dh * [h > 0]; dz = LN backward(dy)
-struct Ln1Args {
-    int B, F;
-    const float *DH, *XH, *RS, *H, *g_base;
-    const int64_t* agent;  // g_base is agent-relative (+ stride * (*agent)) when non-NULL
-    int64_t stride;
-    float *DY, *DZ;
-};
-template <int C>
-__device__ __forceinline__ void ln1_body(const Ln1Args& l, int bx) {
-    const int lane = threadIdx.x & 63;
-    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
-    const int F = l.F;
-    if (r >= l.B) return;
-    const float* g = l.g_base + (l.agent ? (*l.agent) * l.stride : 0);
-    const int64_t ro = (int64_t)r * F;
-    float dh[C], xh[C], h[C], gv[C], dy[C], dz[C];
-    load_row<C>(dh, l.DH + ro, F, lane);
-    load_row<C>(xh, l.XH + ro, F, lane);
-    load_row<C>(h, l.H + ro, F, lane);
-    load_row<C>(gv, g, F, lane);
-    const float rs = l.RS[r];
-#pragma unroll
-    for (int c = 0; c < C; ++c) dy[c] = h[c] > 0.0f ? dh[c] : 0.0f;
-    ln_backward<C>(dy, xh, gv, rs, F, dz);
-    store_row<C>(l.DY + ro, dy, F, lane);
-    store_row<C>(l.DZ + ro, dz, F, lane);
-}
-
 // a1 (grid.y = path): 0 the agent's actor fc1/LN/ReLU on s (saved for backward), 1 the updated critic's on s
 template <int C>
 __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, int path) {
@@ -637,14 +610,6 @@ __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, 
     else
         a3_body<C>(wa, aa, blockIdx.x - nbc);
 }
-template <int C>
-__global__ __launch_bounds__(256) void sc_ln1_bwd(Ln1Args l0, int nb0, Ln1Args l1) {
-    if ((int)blockIdx.x < nb0)
-        ln1_body<C>(l0, blockIdx.x);
-    else
-        ln1_body<C>(l1, blockIdx.x - nb0);
-}
-
 // ---------------------------------------------------------------------------------------------------------------
 // f32 GEMM tile on MFMA: C[m, n] = sum_k A(m, k) B(k, n) for one 32x32 output tile; A(m, k) = A[m*sam + k*sak],
 // B(k, n) = B[k*sbk + n*sbn]. K is processed in panels of up to kKC: the 32 x kc A panel and kc x 32 B panel are
@@ -917,13 +882,20 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// gradients + Adam for one network. Blocks [0, tiles): the fc2.weight gradient (a K = B GEMM) with Adam in the
-// epilogue; the next blocks: reduction red[q] (the last q with red[q].blk0 <= block) over the B rows, 16 elements per
-// block (16 row groups per block):
+// Backward and update, the last two launches of a round.
+//   bwd  (sc_bwd): dH1 = dZ2 W2 tiles with the ReLU + LN1-backward epilogue (dy = dH1 [h > 0], dxh = dy g1, and per
+//        row and 32-column tile the partial sums of dxh and dxh xhat), the fc2.weight gradient dW2 = dZ2^T H1 tiles,
+//        and the reductions whose inputs the row kernels already wrote (fc2.bias, LN2, heads, loss): gradients only.
+//   late (sc_grad_adam): the fc1 / LN1 reductions, with dz = rstd (dxh - mean(dxh) - xhat mean(dxh xhat)) formed on
+//        the fly from those row sums (no LN1-backward launch), Adam inline; Adam of the parameters whose gradients
+//        the bwd launch wrote; the step counter; the critic's self soft update when it has no view.
+// Reductions: red[q] (the last q with red[q].blk0 <= block) over the B rows, 16 elements per block (16 row groups):
 //   mode 0: g[o] = sum_b D[b, o]         (biases, LayerNorm beta)
 //   mode 1: g[o] = sum_b D[b, o] X[b, o] (LayerNorm gamma)
-//   mode 2: g[o*in + i] = sum_b D[b, o] X[b, i]  (fc1 / action_value / head weights)
+//   mode 2: g[o*in + i] = sum_b D[b, o] X[b, i]  (action_value / head weights)
 //   mode 3: loss = sum_b D[b] / B        (written to *loss, no Adam)
+//   mode 4: g[o*in + i] = sum_b dz[b, o] X[b, i], dz from D = dxh (fc1.weight)
+//   mode 5: g[o] = sum_b dz[b, o]                  (fc1.bias)
 struct RedP {
     const float* D;
     const float* X;
@@ -933,17 +905,201 @@ struct RedP {
 constexpr int kMaxRed = 12;
 constexpr int kRedElems = 16;
 constexpr int kMaxRedBlocks = 4096;
-struct GradAdam {
-    GemmP g;  // C unused: the gradient goes to grad + w2_off
+
+// LN1 row statistics for modes 4 / 5, from the bwd launch's per-tile row sums
+struct DzArgs {
+    const float *XH, *RS, *PS;  // xhat [B][F], rstd [B], row sums [B][ntn][2]
+    int F, ntn;
+};
+
+// One block's reduction: the 16-element slice of rp for block b (thread el = tid & 15, row group q = tid >> 4);
+// returns the sum in threads q == 0 (0 elsewhere). part: 256 floats of LDS; mst: [B][2] LDS (modes 4 / 5)
+__device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const DzArgs& dz, float* part, float* mst,
+                                           int& e_out, bool& live_out) {
+    const int tid = threadIdx.x;
+    const bool dzm = rp.mode == 4 || rp.mode == 5;
+    if (dzm) {  // mean(dxh), mean(dxh xhat) of every row: its tiles' partial sums in a fixed order
+        for (int r = tid; r < B; r += 256) {
+            const float* ps = dz.PS + (int64_t)r * 2 * dz.ntn;
+            float s1 = 0.0f, s2 = 0.0f;
+            for (int t = 0; t < dz.ntn; ++t) {
+                s1 += ps[2 * t];
+                s2 += ps[2 * t + 1];
+            }
+            mst[2 * r] = s1 / (float)dz.F;
+            mst[2 * r + 1] = s2 / (float)dz.F;
+        }
+        __syncthreads();
+    }
+    const int el = tid & (kRedElems - 1), q = tid >> 4;
+    const int e = (b - rp.blk0) * kRedElems + el;
+    const bool live = e < rp.n;
+    const bool per_in = rp.mode == 2 || rp.mode == 4;
+    const int o = per_in ? e / rp.in : e;
+    const int i = per_in ? e - o * rp.in : e;
+    const bool prod = rp.mode == 1 || rp.mode == 2 || rp.mode == 4;
+    float acc = 0.0f;
+    constexpr int kRB = 8;  // rows per batch of loads (row group q takes rows q, q + 16, ...)
+    for (int r0 = q; r0 < B; r0 += 16 * kRB) {
+        float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
+#pragma unroll
+        for (int k = 0; k < kRB; ++k) {
+            const int r = r0 + 16 * k;
+            const bool in = live && r < B;
+            dv[k] = in ? rp.D[(int64_t)r * rp.ldd + o] : 0.0f;
+            xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
+            xh[k] = (in && dzm) ? dz.XH[(int64_t)r * dz.F + o] : 0.0f;
+            rs[k] = (in && dzm) ? dz.RS[r] : 0.0f;
+        }
+        if (dzm) {
+#pragma unroll
+            for (int k = 0; k < kRB; ++k) {
+                const int r = min(r0 + 16 * k, B - 1);
+                dv[k] = rs[k] * (dv[k] - mst[2 * r] - xh[k] * mst[2 * r + 1]);  // ln_backward's dz
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kRB; ++k) acc = prod ? fmaf(dv[k], xv[k], acc) : acc + dv[k];
+    }
+    part[q * kRedElems + el] = acc;
+    __syncthreads();
+    float gsum = 0.0f;
+    if (q == 0 && live) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gsum += part[k * kRedElems + el];
+    }
+    e_out = e;
+    live_out = live && q == 0;
+    return gsum;
+}
+
+struct BwdJob {
+    GemmP dh;                    // dH1 = dZ2 W2 (B x H1, K = H2); W2 agent-relative through dh.relB / dh.agent
+    GemmP dw;                    // dW2 = dZ2^T H1 (H2 x H1, K = B) -> grad + w2_off
+    const float *H1, *XH1, *g1;  // LN1-backward epilogue of the dH tiles (g1 agent-relative like grad)
+    float *DY1, *DXH1, *PS1;
+    int F, ntn;
     int64_t w2_off;
+    int nred, nblk, B;
+    RedP red[kMaxRed];
+    float* grad;
+    int64_t rel;  // grad / g1 are agent-relative: + rel * (*agent)
+    const int64_t* agent;
+    float* loss;
+};
+__host__ __device__ inline int bwd_blocks(const BwdJob& j) { return j.dh.tiles + j.dw.tiles + j.nblk; }
+
+// the 4 rows of thread (wave w, lane l) in a 32 x 32 tile: 8w + 4(l >> 5) + q; its column: l & 31
+template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
+__device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
+    extern __shared__ float4 smem4[];
+    float* smem = reinterpret_cast<float*>(smem4);
+    const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
+    const int64_t base = j.rel ? j.rel * (*j.agent) : 0;
+    if (bx < j.dh.tiles) {
+        const GemmP& g = j.dh;
+        const int tm = bx / g.tiles_n, tn = bx - tm * g.tiles_n;
+        const int64_t relB = g.relB ? g.relB * (*g.agent) : 0;
+        const int n = tn * kT + (l & 31);
+        const bool nok = n < g.N;
+        // the epilogue's inputs, loaded before the GEMM
+        const float gam = nok ? j.g1[base + n] : 0.0f;
+        float hv[4], xv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
+            const bool ok = m < g.M && nok;
+            hv[q] = ok ? j.H1[(int64_t)m * j.F + n] : 0.0f;
+            xv[q] = ok ? j.XH1[(int64_t)m * j.F + n] : 0.0f;
+        }
+        float out[4];
+        gemm_tile<AVH, BVH, NFH>(g, g.B + relB, tm, tn, smem, out);
+        float s1[4], s2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
+            const bool ok = m < g.M && nok;
+            const float dy = hv[q] > 0.0f ? out[q] : 0.0f;  // through the ReLU
+            const float dxh = dy * gam;
+            if (ok) {
+                j.DY1[(int64_t)m * j.F + n] = dy;
+                j.DXH1[(int64_t)m * j.F + n] = dxh;
+            }
+            s1[q] = ok ? dxh : 0.0f;
+            s2[q] = ok ? dxh * xv[q] : 0.0f;
+        }
+        // row sums over the tile's 32 columns (the 32 lanes of a half-wave): xor butterfly, bitwise equal in all lanes
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                s1[q] += __shfl_xor(s1[q], off);
+                s2[q] += __shfl_xor(s2[q], off);
+            }
+        if ((l & 31) == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
+                if (m < g.M) {
+                    j.PS1[((int64_t)m * j.ntn + tn) * 2] = s1[q];
+                    j.PS1[((int64_t)m * j.ntn + tn) * 2 + 1] = s2[q];
+                }
+            }
+        }
+    } else if (bx < j.dh.tiles + j.dw.tiles) {
+        const GemmP& g = j.dw;
+        const int t = bx - j.dh.tiles;
+        const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
+        float out[4];
+        gemm_tile<AVW, BVW, NFW>(g, g.B, tm, tn, smem, out);
+        const int nn = tn * kT + (l & 31);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int mm = tm * kT + 8 * wv + 4 * (l >> 5) + q;
+            if (mm < g.M && nn < g.N) j.grad[base + j.w2_off + (int64_t)mm * g.ldc + nn] = out[q];
+        }
+    } else {
+        const int b = bx - j.dh.tiles - j.dw.tiles;
+        int q0 = 0;  // descriptor of this block: a wave-uniform search over <= kMaxRed scalars
+        for (int q = 1; q < j.nred; ++q)
+            if (b >= j.red[q].blk0) q0 = q;
+        const RedP& rp = j.red[q0];
+        int e;
+        bool wr;
+        const DzArgs none{nullptr, nullptr, nullptr, 0, 0};
+        const float gsum = red_block(rp, b, j.B, none, smem, nullptr, e, wr);
+        if (wr) {
+            if (rp.mode == 3)
+                *j.loss = gsum * (1.0f / (float)j.B);
+            else
+                j.grad[base + rp.off + e] = gsum;
+        }
+    }
+}
+
+struct Bwd2 {
+    BwdJob j0, j1;
+    int nb0;
+};
+template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
+__global__ __launch_bounds__(256) void sc_bwd(Bwd2 bb) {
+    if ((int)blockIdx.x < bb.nb0)
+        bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
+    else
+        bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j1, blockIdx.x - bb.nb0);
+}
+
+struct GradAdam {
     int nred, nblk, B, do_adam;
     RedP red[kMaxRed];
+    DzArgs dz;
+    int64_t adam_lo, adam_n;  // Adam-only region (gradients written by the bwd launch), relative to the agent base
+    int adam_blocks;
     float *p, *grad, *m, *v;
     int64_t rel;  // p/grad/m/v are agent-relative: + rel * (*agent)
     const int64_t* agent;
     int64_t* step;  // step[0], or step[*agent] when rel != 0
     unsigned* counter;
-    float* loss;
     float lr, b1, b2, eps;
     // soft updates after the Adam step (actor kernel): target = tau p + (1 - tau) target for every updated
     // element, and the critic's self update (critic = tau c + (1 - tau) c) in soft_blocks extra blocks
@@ -957,6 +1113,7 @@ struct GradAdam {
     float* p_copy;
     const int64_t* soft_count;
 };
+__host__ __device__ inline int late_blocks(const GradAdam& ga) { return ga.nblk + ga.adam_blocks + ga.soft_blocks; }
 
 struct AdamState {
     float p, m, v, t;
@@ -985,8 +1142,8 @@ __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamSt
     if (soft && ga.target) ga.target[i] = ga.tau * pn + ga.one_minus_tau * s.t;  // soft_update_kernel mode 1
 }
 
-// one job's blocks: bx in [0, nb), nb = g.tiles + nblk + soft_blocks
-template <int AV, int BV, int NF>
+// one job's blocks of the late launch: [0, nblk) reductions, [nblk, + adam_blocks) Adam of the bwd launch's
+// gradients, then soft_blocks self soft update blocks
 __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int nb) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
@@ -1005,10 +1162,11 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
             sh[1] = (float)sqrt(1.0 - pow((double)ga.b2, st));
         }
     }
-    if (bx >= ga.g.tiles + ga.nblk) {  // critic self soft update blocks (after its Adam step)
+    const int adam0 = ga.nblk, soft0 = ga.nblk + ga.adam_blocks;
+    if (bx >= soft0) {  // critic self soft update blocks (after its Adam step)
         __syncthreads();
         if (sh_soft && ga.self_soft) {
-            const int64_t b0 = (int64_t)(bx - ga.g.tiles - ga.nblk) * 1024;
+            const int64_t b0 = (int64_t)(bx - soft0) * 1024;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t e = b0 + q * 256 + tid;
@@ -1018,72 +1176,38 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
                 }
             }
         }
-    } else if (bx < ga.g.tiles) {
-        {
-            const int tm = bx / ga.g.tiles_n, tn = bx - tm * ga.g.tiles_n;
-            const int wv = tid >> 6, l = tid & 63;
-            const int nn = tn * kT + (l & 31);
-            AdamState st[4];
-            int64_t e[4];
-            bool ok[4];
+    } else if (bx >= adam0) {  // Adam of gradients the bwd launch wrote: every load first, then the updates
+        __syncthreads();
+        const int64_t e0 = ga.adam_lo + (int64_t)(bx - adam0) * 1024, end = ga.adam_lo + ga.adam_n;
+        AdamState st[4];
+        float gi[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {  // prefetch the Adam state of this thread's 4 outputs
-                const int mm = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-                ok[q] = mm < ga.g.M && nn < ga.g.N;
-                e[q] = base + ga.w2_off + (int64_t)mm * ga.g.ldc + nn;
-                st[q] = (ok[q] && ga.do_adam) ? adam_load(ga, e[q]) : AdamState{0.f, 0.f, 0.f, 0.f};
-            }
-            float out[4];
-            gemm_tile<AV, BV, NF>(ga.g, ga.g.B, tm, tn, smem, out);  // (its barriers also publish sh[])
-            const float neg_step = sh[0], bc2s = sh[1];
+        for (int q = 0; q < 4; ++q) {
+            const int64_t e = e0 + q * 256 + tid;
+            st[q] = e < end ? adam_load(ga, base + e) : AdamState{0.f, 0.f, 0.f, 0.f};
+            gi[q] = e < end ? ga.grad[base + e] : 0.0f;
+        }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (ok[q]) {
-                    ga.grad[e[q]] = out[q];
-                    if (ga.do_adam) adam_store(ga, e[q], st[q], out[q], neg_step, bc2s, sh_soft != 0);
-                }
+        for (int q = 0; q < 4; ++q) {
+            const int64_t e = e0 + q * 256 + tid;
+            if (e < end) adam_store(ga, base + e, st[q], gi[q], sh[0], sh[1], sh_soft != 0);
         }
     } else {
-        float* part = smem;  // [16 row groups][16 elements]
-        const int b = bx - ga.g.tiles;
+        const int b = bx;
         int q0 = 0;  // descriptor of this block: a wave-uniform search over <= kMaxRed scalars
         for (int q = 1; q < ga.nred; ++q)
             if (b >= ga.red[q].blk0) q0 = q;
         const RedP& rp = ga.red[q0];
-        const int el = tid & (kRedElems - 1), q = tid >> 4;
-        const int e = (b - rp.blk0) * kRedElems + el;
-        const bool live = e < rp.n;
-        const int o = rp.mode == 2 ? e / rp.in : e;
-        const int i = rp.mode == 2 ? e - o * rp.in : e;
-        const bool prod = rp.mode == 1 || rp.mode == 2;
-        const int64_t pe = base + rp.off + e;
-        const AdamState st = (q == 0 && live && rp.mode != 3 && ga.do_adam) ? adam_load(ga, pe)
-                                                                              : AdamState{0.f, 0.f, 0.f, 0.f};
-        float acc = 0.0f;
-        for (int r0 = q; r0 < ga.B; r0 += 16 * 16) {
-            float dv[16], xv[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int r = r0 + 16 * k;
-                const bool in = live && r < ga.B;
-                dv[k] = in ? rp.D[(int64_t)r * rp.ldd + o] : 0.0f;
-                xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; ++k) acc = prod ? fmaf(dv[k], xv[k], acc) : acc + dv[k];
-        }
-        part[q * kRedElems + el] = acc;
-        __syncthreads();
-        if (q == 0 && live) {
-            float gsum = 0.0f;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) gsum += part[k * kRedElems + el];
-            if (rp.mode == 3) {
-                *ga.loss = gsum * (1.0f / (float)ga.B);
-            } else {
-                ga.grad[pe] = gsum;
-                if (ga.do_adam) adam_store(ga, pe, st, gsum, sh[0], sh[1], sh_soft != 0);
-            }
+        const int e1 = (b - rp.blk0) * kRedElems + (tid & (kRedElems - 1));
+        const bool ad = (tid >> 4) == 0 && e1 < rp.n && rp.mode != 3 && ga.do_adam;
+        const AdamState st = ad ? adam_load(ga, base + rp.off + e1) : AdamState{0.f, 0.f, 0.f, 0.f};
+        int e;
+        bool wr;
+        const float gsum = red_block(rp, b, ga.B, ga.dz, smem, smem + 256, e, wr);
+        if (wr) {
+            const int64_t pe = base + rp.off + e;
+            ga.grad[pe] = gsum;
+            if (ga.do_adam) adam_store(ga, pe, st, gsum, sh[0], sh[1], sh_soft != 0);
         }
     }
     // the last block to arrive advances the step counter. No fence: every block's thread 0 consumed its load of
@@ -1098,17 +1222,16 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
     }
 }
 
-// a round's gradient + Adam launch: blocks [0, nb0) run job j0, the rest job j1 (when there are any)
+// a round's late launch: blocks [0, nb0) run job j0, the rest job j1 (when there are any)
 struct GradAdam2 {
     GradAdam j0, j1;
     int nb0;
 };
-template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
     if ((int)blockIdx.x < gg.nb0)
-        grad_adam_body<AV, BV, NF>(gg.j0, blockIdx.x, gg.nb0);
+        grad_adam_body(gg.j0, blockIdx.x, gg.nb0);
     else
-        grad_adam_body<AV, BV, NF>(gg.j1, blockIdx.x - gg.nb0, gridDim.x - gg.nb0);
+        grad_adam_body(gg.j1, blockIdx.x - gg.nb0, gridDim.x - gg.nb0);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1211,23 +1334,26 @@ int launch_gemm(hipStream_t st, const GemmBatch& gb) {
     }
 }
 
-void add_red(GradAdam& ga, const float* D, int ldd, const float* X, int ldx, int mode, int in, int n, int64_t off) {
+// append reduction descriptor n elements (mode: see RedP) to a bwd or late job
+template <typename J>
+void add_red(J& ga, const float* D, int ldd, const float* X, int ldx, int mode, int in, int n, int64_t off) {
     const int j = ga.nred++;
     RedP& r = ga.red[j];
     r.D = D; r.X = X; r.ldd = ldd; r.ldx = ldx; r.mode = mode; r.in = in; r.n = n; r.off = off;
     r.blk0 = ga.nblk;
     ga.nblk += (n + kRedElems - 1) / kRedElems;
 }
-int grad_blocks(const GradAdam& ga) { return ga.g.tiles + ga.nblk + ga.soft_blocks; }
-size_t grad_lds(const GradAdam& ga) {
-    const size_t lds = gemm_lds_bytes(ga.g.K, ga.g.kchunk);
-    return lds < 16 * kRedElems * sizeof(float) ? 16 * kRedElems * sizeof(float) : lds;
+size_t red_lds(int B) { return (size_t)(16 * kRedElems + 2 * B) * sizeof(float); }  // part + LN1 row statistics
+size_t bwd_lds(const BwdJob& j) {
+    const size_t a = gemm_lds_bytes(j.dh.K, j.dh.kchunk), b = gemm_lds_bytes(j.dw.K, j.dw.kchunk);
+    const size_t r = 16 * kRedElems * sizeof(float);
+    return a > b ? (a > r ? a : r) : (b > r ? b : r);
 }
 
-template <int AV, int BV, int NF>
-int launch_grad_adam_v(hipStream_t st, const GradAdam2& gg, dim3 grid, size_t lds) {
-    if (int rc = allow_lds(sc_grad_adam<AV, BV, NF>, lds)) return rc;
-    hipLaunchKernelGGL((sc_grad_adam<AV, BV, NF>), grid, dim3(256), lds, st, gg);
+template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
+int launch_bwd_v(hipStream_t st, const Bwd2& bb, dim3 grid, size_t lds) {
+    if (int rc = allow_lds(sc_bwd<AVH, BVH, AVW, BVW, NFH, NFW>, lds)) return rc;
+    hipLaunchKernelGGL((sc_bwd<AVH, BVH, AVW, BVW, NFH, NFW>), grid, dim3(256), lds, st, bb);
     return launched();
 }
 
@@ -1285,8 +1411,7 @@ struct Job {
     size_t lds1, lds3;
     GemmP fwd[3];
     int nfwd;
-    GemmP dh;
-    Ln1Args l;
+    BwdJob bw;
     GradAdam ga;
 };
 
@@ -1298,6 +1423,46 @@ void job_common(const FlockScUpdate* u, Job& j) {
     j.rb = (j.B + kRowsPerBlock - 1) / kRowsPerBlock;
     j.lds1 = fc1_lds(j.in, j.H1);
     j.lds3 = tails_lds(j.na, j.H2);
+}
+
+// the bwd launch's job: dH1 = dZ2 W2 (+ LN1 epilogue), dW2 = dZ2^T H1, then the caller's early reductions
+void bwd_common(Job& j, const float* W2, int64_t rel_w2, const int64_t* agent, const float* H1, const float* XH1,
+                const float* g1, float* DY1, float* DXH1, float* PS1, const float* DZ2, int64_t w2_off, float* grad,
+                int64_t rel, float* loss) {
+    const int B = j.B, H1n = j.H1, H2 = j.H2;
+    BwdJob& bw = j.bw;
+    bw.dh = gemm_p(DZ2, W2, nullptr, nullptr, B, H1n, H2, H2, 1, H1n, 1, H1n, rel_w2, agent);
+    bw.dw = gemm_p(DZ2, H1, nullptr, nullptr, H2, H1n, B, 1, H2, H1n, 1, H1n, 0);
+    bw.dw.kchunk = balanced_kc(B, grad_kc());
+    bw.H1 = H1; bw.XH1 = XH1; bw.g1 = g1; bw.DY1 = DY1; bw.DXH1 = DXH1; bw.PS1 = PS1;
+    bw.F = H1n; bw.ntn = bw.dh.tiles_n;
+    bw.w2_off = w2_off;
+    bw.nred = 0; bw.nblk = 0; bw.B = B;
+    bw.grad = grad; bw.rel = rel; bw.agent = agent; bw.loss = loss;
+}
+
+// the late launch's job: fc1 / LN1 reductions (+ Adam), Adam of [W2, total)
+void late_common(Job& j, const FlockScUpdate* u, const float* DXH1, const float* DY1, const float* XH1,
+                 const float* RS1, const float* PS1, int64_t W1, int64_t b1, int64_t g1, int64_t be1, int64_t W2,
+                 int64_t total) {
+    const int in = j.in, H1 = j.H1;
+    GradAdam& ga = j.ga;
+    ga.nred = 0;
+    ga.nblk = 0;
+    ga.B = j.B;
+    ga.do_adam = u->do_adam;
+    add_red(ga, DXH1, H1, j.w.S, in, 4, in, H1 * in, W1);
+    add_red(ga, DXH1, H1, nullptr, 0, 5, 1, H1, b1);
+    add_red(ga, DY1, H1, XH1, H1, 1, 1, H1, g1);
+    add_red(ga, DY1, H1, nullptr, 0, 0, 1, H1, be1);
+    ga.dz = DzArgs{XH1, RS1, PS1, H1, j.bw.ntn};
+    ga.adam_lo = W2;
+    ga.adam_n = total - W2;
+    ga.adam_blocks = u->do_adam ? (int)((ga.adam_n + 1023) / 1024) : 0;
+    ga.lr = 0.0f;
+    ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    ga.tau = u->tau;
+    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
 }
 
 // critic phase (agent_simple_shared_critic.py:118-141)
@@ -1315,43 +1480,31 @@ void critic_job(const FlockScUpdate* u, Job& j) {
     j.fwd[2] = gemm_p(w.H1, u->critic + co.W2, w.Z2 + 2 * (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1, 1,
                       H1, H2, 0);
     j.nfwd = 3;
-    j.dh = gemm_p(w.DZ2, u->critic + co.W2, w.DH1, nullptr, B, H1, H2, H2, 1, H1, 1, H1, 0);  // dH1 = dZ2 W2
-    j.l = Ln1Args{B, H1, w.DH1, w.XH1, w.RS1, w.H1, u->critic + co.g1, nullptr, 0, w.DY1, w.DZ1};
+    BwdJob& bw = j.bw;
+    bwd_common(j, u->critic + co.W2, 0, u->agent, w.H1, w.XH1, u->critic + co.g1, w.DY1, w.DXH1, w.PS1, w.DZ2, co.W2,
+               u->critic_grad, 0, u->losses + 1);
+    add_red(bw, w.DZ2, H2, nullptr, 0, 0, 1, H2, co.b2);
+    add_red(bw, w.DY2, H2, w.XH2, H2, 1, 1, H2, co.g2);
+    add_red(bw, w.DY2, H2, nullptr, 0, 0, 1, H2, co.be2);
+    add_red(bw, w.DZA, H2, w.A, na, 2, na, H2 * na, co.Wa);
+    add_red(bw, w.DZA, H2, nullptr, 0, 0, 1, H2, co.ba);
+    add_red(bw, w.DQ, 1, w.HQ, H2, 2, H2, H2, co.Wq);
+    add_red(bw, w.DQ, 1, nullptr, 0, 0, 1, 1, co.bq);
+    add_red(bw, w.LOSS, 1, nullptr, 0, 3, 1, 1, 0);
+    late_common(j, u, w.DXH1, w.DY1, w.XH1, w.RS1, w.PS1, co.W1, co.b1, co.g1, co.be1, co.W2, co.total);
     GradAdam& ga = j.ga;
-    ga.g = gemm_p(w.DZ2, w.H1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);  // dW2 = dZ2^T H1
-    ga.g.kchunk = balanced_kc(B, grad_kc());
-    ga.w2_off = co.W2;
-    ga.nred = 0;
-    ga.nblk = 0;
-    ga.B = B;
-    ga.do_adam = u->do_adam;
-    add_red(ga, w.DZ1, H1, w.S, in, 2, in, H1 * in, co.W1);
-    add_red(ga, w.DZ1, H1, nullptr, 0, 0, 1, H1, co.b1);
-    add_red(ga, w.DY1, H1, w.XH1, H1, 1, 1, H1, co.g1);
-    add_red(ga, w.DY1, H1, nullptr, 0, 0, 1, H1, co.be1);
-    add_red(ga, w.DZ2, H2, nullptr, 0, 0, 1, H2, co.b2);
-    add_red(ga, w.DY2, H2, w.XH2, H2, 1, 1, H2, co.g2);
-    add_red(ga, w.DY2, H2, nullptr, 0, 0, 1, H2, co.be2);
-    add_red(ga, w.DZA, H2, w.A, na, 2, na, H2 * na, co.Wa);
-    add_red(ga, w.DZA, H2, nullptr, 0, 0, 1, H2, co.ba);
-    add_red(ga, w.DQ, 1, w.HQ, H2, 2, H2, H2, co.Wq);
-    add_red(ga, w.DQ, 1, nullptr, 0, 0, 1, 1, co.bq);
-    add_red(ga, w.LOSS, 1, nullptr, 0, 3, 1, 1, 0);
     ga.p = u->critic; ga.grad = u->critic_grad; ga.m = u->critic_exp_avg; ga.v = u->critic_exp_avg_sq;
     ga.rel = 0;
     ga.agent = u->agent;
     ga.step = u->critic_step;
     ga.counter = u->counters;
-    ga.loss = u->losses + 1;
-    ga.lr = u->beta; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    ga.lr = u->beta;
     ga.target = nullptr; ga.self_soft = nullptr; ga.self_n = 0; ga.soft_blocks = 0;
     // with a critic view the self soft update of this learn() rides in the critic's Adam (see FlockScUpdate)
     const bool view = u->do_adam && u->critic_view;
     ga.p_copy = view ? u->critic_view : nullptr;
     ga.soft_count = view ? u->actor_steps : nullptr;
     ga.soft_rate = view ? u->update_rate : 0;
-    ga.tau = u->tau;
-    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
 }
 
 // actor phase (:144-150), through the UPDATED critic (critic_view when given)
@@ -1370,43 +1523,29 @@ void actor_job(const FlockScUpdate* u, Job& j) {
     j.fwd[1] = gemm_p(w.CH1, critic + co.W2, w.Z2b + (int64_t)B * H2, critic + co.b2, B, H2, H1, H1, 1, 1, H1, H2,
                       0);
     j.nfwd = 2;
-    j.dh = gemm_p(w.ADZ2, u->actors + ao.W2, w.ADH1, nullptr, B, H1, H2, H2, 1, H1, 1, H1, u->actor_stride,
-                  u->agent);  // dH1 = dZ2 W2 (actor)
-    j.l = Ln1Args{B, H1, w.ADH1, w.AXH1, w.ARS1, w.AH1, u->actors + ao.g1, u->agent, u->actor_stride, w.ADY1,
-                  w.ADZ1};
+    BwdJob& bw = j.bw;
+    bwd_common(j, u->actors + ao.W2, u->actor_stride, u->agent, w.AH1, w.AXH1, u->actors + ao.g1, w.ADY1, w.ADXH1,
+               w.APS1, w.ADZ2, ao.W2, u->actors_grad, u->actor_stride, u->losses);
+    add_red(bw, w.ADZ2, H2, nullptr, 0, 0, 1, H2, ao.b2);
+    add_red(bw, w.ADY2, H2, w.AXH2, H2, 1, 1, H2, ao.g2);
+    add_red(bw, w.ADY2, H2, nullptr, 0, 0, 1, H2, ao.be2);
+    add_red(bw, w.DM, na, w.AH2, H2, 2, H2, na * H2, ao.Wmu);
+    add_red(bw, w.DM, na, nullptr, 0, 0, 1, na, ao.bmu);
+    add_red(bw, w.ALOSS, 1, nullptr, 0, 3, 1, 1, 0);
+    late_common(j, u, w.ADXH1, w.ADY1, w.AXH1, w.ARS1, w.APS1, ao.W1, ao.b1, ao.g1, ao.be1, ao.W2, ao.total);
     GradAdam& ga = j.ga;
-    ga.g = gemm_p(w.ADZ2, w.AH1, nullptr, nullptr, H2, H1, B, 1, H2, H1, 1, H1, 0);
-    ga.g.kchunk = balanced_kc(B, grad_kc());
-    ga.w2_off = ao.W2;
-    ga.nred = 0;
-    ga.nblk = 0;
-    ga.B = B;
-    ga.do_adam = u->do_adam;
-    add_red(ga, w.ADZ1, H1, w.S, in, 2, in, H1 * in, ao.W1);
-    add_red(ga, w.ADZ1, H1, nullptr, 0, 0, 1, H1, ao.b1);
-    add_red(ga, w.ADY1, H1, w.AXH1, H1, 1, 1, H1, ao.g1);
-    add_red(ga, w.ADY1, H1, nullptr, 0, 0, 1, H1, ao.be1);
-    add_red(ga, w.ADZ2, H2, nullptr, 0, 0, 1, H2, ao.b2);
-    add_red(ga, w.ADY2, H2, w.AXH2, H2, 1, 1, H2, ao.g2);
-    add_red(ga, w.ADY2, H2, nullptr, 0, 0, 1, H2, ao.be2);
-    add_red(ga, w.DM, na, w.AH2, H2, 2, H2, na * H2, ao.Wmu);
-    add_red(ga, w.DM, na, nullptr, 0, 0, 1, na, ao.bmu);
-    add_red(ga, w.ALOSS, 1, nullptr, 0, 3, 1, 1, 0);
     ga.p = u->actors; ga.grad = u->actors_grad; ga.m = u->actors_exp_avg; ga.v = u->actors_exp_avg_sq;
     ga.rel = u->actor_stride;
     ga.agent = u->agent;
     ga.step = u->actor_steps;
     ga.counter = u->counters + 1;
-    ga.loss = u->losses;
-    ga.lr = u->alpha; ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
+    ga.lr = u->alpha;
     const bool soft = u->do_adam && u->update_rate > 0;
     ga.soft_rate = soft ? u->update_rate : 0;
     ga.target = soft ? u->actors_target : nullptr;  // agent-relative like p
     ga.self_soft = (soft && !view) ? u->critic : nullptr;  // with a view the critic kernel did it
     ga.self_n = co.total;
     ga.soft_blocks = (soft && !view) ? (int)((co.total + 1023) / 1024) : 0;
-    ga.tau = u->tau;
-    ga.one_minus_tau = (float)(1.0 - (double)u->tau);
     ga.p_copy = nullptr;
     ga.soft_count = nullptr;
 }
@@ -1438,7 +1577,7 @@ void actor_job(const FlockScUpdate* u, Job& j) {
 
 size_t zmax(size_t a, size_t b) { return a > b ? a : b; }
 
-// One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in six launches; either may be
+// One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in five launches; either may be
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
 // computes exactly what the actor phase followed by the critic phase would.
 int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
@@ -1473,37 +1612,46 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
                     hipLaunchKernelGGL(sc_k3<CC>, grid, dim3(256), lds, st, A.w, A.a, nbc, Z.w, Z.a))
         if ((rc = launched())) return rc;
     }
-    {  // 4: dH1 = dZ2 W2
-        GemmBatch gb;
-        gb.n = 0;
-        if (jc) gb.p[gb.n++] = jc->dh;
-        if (ja) gb.p[gb.n++] = ja->dh;
-        if ((rc = launch_gemm(st, gb))) return rc;
+    {  // 4: dH1 = dZ2 W2 with the LN1-backward epilogue, dW2, early reductions
+        Bwd2 bb;
+        bb.j0 = A.bw;
+        bb.j1 = Z.bw;
+        bb.nb0 = bwd_blocks(A.bw);
+        const int nb = bb.nb0 + ((jc && ja) ? bwd_blocks(Z.bw) : 0);
+        const size_t lds = zmax(bwd_lds(A.bw), bwd_lds(Z.bw));
+        bool fast = true;
+        int kh = 8, kw = 8;
+        for (const BwdJob* b : {&A.bw, &Z.bw}) {
+            fast = fast && gemm_variant(b->dh) == 1 && gemm_variant(b->dw) == 2;
+            const int ch = gemm_kc(b->dh.K, b->dh.kchunk), cw = gemm_kc(b->dw.K, b->dw.kchunk);
+            kh = ch > kh ? ch : kh;
+            kw = cw > kw ? cw : kw;
+        }
+        const int nfh = nf_of(kh), nfw = nf_of(kw);
+        const dim3 grid(nb);
+        if (!fast)
+            rc = launch_bwd_v<2, 2, 2, 2, 16, 16>(st, bb, grid, lds);
+        else if (nfw <= 4)
+            rc = nfh <= 4 ? launch_bwd_v<0, 1, 1, 1, 4, 4>(st, bb, grid, lds)
+                          : nfh <= 7 ? launch_bwd_v<0, 1, 1, 1, 7, 4>(st, bb, grid, lds)
+                                     : launch_bwd_v<0, 1, 1, 1, 16, 4>(st, bb, grid, lds);
+        else
+            rc = nfh <= 7 ? launch_bwd_v<0, 1, 1, 1, 7, 16>(st, bb, grid, lds)
+                          : launch_bwd_v<0, 1, 1, 1, 16, 16>(st, bb, grid, lds);
+        if (rc) return rc;
     }
-    {  // 5: ReLU + LN1 backward
-        const int two = (jc && ja) ? 2 : 1;
-        const dim3 grid(rb * two);
-        SC_C_SWITCH(C, hipLaunchKernelGGL(sc_ln1_bwd<CC>, grid, dim3(256), 0, st, A.l, rb, Z.l))
-        if ((rc = launched())) return rc;
-    }
-    // 6: gradients + Adam
+    // 5: fc1 / LN1 gradients + every Adam step
+    if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks || A.bw.nblk > kMaxRedBlocks)
+        return fail(-2, "flock_sc: too many reduction blocks (fc1 * in_dim too large)");
     GradAdam2 gg;
     gg.j0 = A.ga;
     gg.j1 = Z.ga;
-    gg.nb0 = grad_blocks(A.ga);
-    const int nb = gg.nb0 + ((jc && ja) ? grad_blocks(Z.ga) : 0);
-    if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks)
-        return fail(-2, "flock_sc: too many reduction blocks (fc1 * in_dim too large)");
-    const size_t lds = zmax(grad_lds(A.ga), grad_lds(Z.ga));
-    const bool v11 = gemm_variant(A.ga.g) == 2 && gemm_variant(Z.ga.g) == 2;
-    if (!v11) return launch_grad_adam_v<2, 2, 16>(st, gg, dim3(nb), lds);
-    const int kc0 = gemm_kc(A.ga.g.K, A.ga.g.kchunk), kc1 = gemm_kc(Z.ga.g.K, Z.ga.g.kchunk);
-    switch (nf_of(kc0 > kc1 ? kc0 : kc1)) {
-        case 4: return launch_grad_adam_v<1, 1, 4>(st, gg, dim3(nb), lds);
-        case 7: return launch_grad_adam_v<1, 1, 7>(st, gg, dim3(nb), lds);
-        case 10: return launch_grad_adam_v<1, 1, 10>(st, gg, dim3(nb), lds);
-        default: return launch_grad_adam_v<1, 1, 16>(st, gg, dim3(nb), lds);
-    }
+    gg.nb0 = late_blocks(A.ga);
+    const int nb = gg.nb0 + ((jc && ja) ? late_blocks(Z.ga) : 0);
+    const size_t lds = red_lds(A.B);
+    if ((rc = allow_lds(sc_grad_adam, lds))) return rc;
+    hipLaunchKernelGGL(sc_grad_adam, dim3(nb), dim3(256), lds, st, gg);
+    return launched();
 }
 
 // learn() prologue: the agent index and the minibatch rows (Philox4x32-10, counter = (learn counter, row))
@@ -1537,24 +1685,40 @@ __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t see
 
 // learn() prologue with a minibatch snapshot: the sampled rows of every replay field are copied to staging rows
 // 0..B-1, so the update can read the staging copy (with the identity index) while the next env step rewrites the ring
-__global__ __launch_bounds__(256) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
+__global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
                                                         int64_t* idx_out, int64_t* agent_out, int64_t agent,
                                                         int in_dim, int n_actions, FlockScRows src,
-                                                        FlockScRows dst) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
+                                                        FlockScRows dst, int vec) {
+    const int r = blockIdx.x * 64 + threadIdx.x;
     if (r == 0) *agent_out = agent;
     if (r >= B) return;
     const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
     const uint64_t u = ((uint64_t)q.x << 32) | q.y;
     const int64_t row = (int64_t)(u % (uint64_t)rows);  // the row sc_prep samples for r
     if (idx_out) idx_out[r] = row;
+    // every load of the row first, then the stores (src and dst may alias as far as the compiler knows: interleaved,
+    // each store would wait for its load, one memory round trip per field)
+    if (vec) {  // the v2 shapes (in_dim 4, n_actions 2) with aligned fields: 16-B / 8-B rows
+        const float4 st = *reinterpret_cast<const float4*>(src.state + row * 4);
+        const float4 ns = *reinterpret_cast<const float4*>(src.new_state + row * 4);
+        const float2 ac = *reinterpret_cast<const float2*>(src.action + row * 2);
+        const float rw = src.reward[row], te = src.terminal[row];
+        *reinterpret_cast<float4*>(dst.state + (int64_t)r * 4) = st;
+        *reinterpret_cast<float4*>(dst.new_state + (int64_t)r * 4) = ns;
+        *reinterpret_cast<float2*>(dst.action + (int64_t)r * 2) = ac;
+        dst.reward[r] = rw;
+        dst.terminal[r] = te;
+        return;
+    }
     for (int c = 0; c < in_dim; ++c) {
-        dst.state[(int64_t)r * in_dim + c] = src.state[row * in_dim + c];
-        dst.new_state[(int64_t)r * in_dim + c] = src.new_state[row * in_dim + c];
+        const float a = src.state[row * in_dim + c], b = src.new_state[row * in_dim + c];
+        dst.state[(int64_t)r * in_dim + c] = a;
+        dst.new_state[(int64_t)r * in_dim + c] = b;
     }
     for (int c = 0; c < n_actions; ++c) dst.action[(int64_t)r * n_actions + c] = src.action[row * n_actions + c];
-    dst.reward[r] = src.reward[row];
-    dst.terminal[r] = src.terminal[row];
+    const float rw = src.reward[row], te = src.terminal[row];
+    dst.reward[r] = rw;
+    dst.terminal[r] = te;
 }
 
 }  // namespace
@@ -1571,8 +1735,11 @@ int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uin
     for (const FlockScRows* x : rs)
         if (!x->state || !x->new_state || !x->action || !x->reward || !x->terminal)
             return fail(-3, "flock_sc_prep_snapshot: NULL field pointer");
-    hipLaunchKernelGGL(sc_prep_snapshot, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, B, rows, seed,
-                       counter, idx_out, agent_out, agent, in_dim, n_actions, *ring, *staging);
+    int vec = in_dim == 4 && n_actions == 2;
+    for (const FlockScRows* x : rs)
+        vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
+    hipLaunchKernelGGL(sc_prep_snapshot, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, B, rows, seed,
+                       counter, idx_out, agent_out, agent, in_dim, n_actions, *ring, *staging, vec);
     return launched();
 }
 
@@ -1622,6 +1789,8 @@ struct FlockScPipeline {
     hipGraphExec_t merged[kMaxSlots], conly[kMaxSlots], aonly[kMaxSlots];
     Job jc[kMaxSlots], ja[kMaxSlots];  // direct launches (graphs == false): the rounds' arguments, built once
     bool graphs;
+    int diag;  // FLOCK_SC_PIPELINE_DIAG (timing diagnostics only; results are wrong): 1 no learner wait on the
+               // snapshot, 2 no env wait on the slot, 3 neither
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
     bool used[kMaxSlots];
     int slot;
@@ -1691,6 +1860,8 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     // (FLOCK_SC_PIPELINE_GRAPHS=1, read here once): config-3 step 0.117 ms direct vs 0.125 ms with graphs
     const char* ge = getenv("FLOCK_SC_PIPELINE_GRAPHS");
     p->graphs = ge && ge[0] == '1';
+    const char* de = getenv("FLOCK_SC_PIPELINE_DIAG");
+    p->diag = de ? atoi(de) : 0;
     int rc = 0;
     for (int i = 0; i < n_slots && !rc; ++i) {
         critic_job(&p->u[i], p->jc[i]);
@@ -1722,12 +1893,13 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
     const int s = p->slot, n = p->n;
     const FlockScUpdate& u = p->u[s];
-    if (p->used[s] && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
+    if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
     int rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                     u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
     if (rc) return rc;
-    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess && hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess;
+    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
+              ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
     if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     const int q = p->pending;
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {

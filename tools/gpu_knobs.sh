@@ -7,5 +7,5 @@ i=0
 for kv in "$@"; do
   i=$((i+1))
   env $kv timeout -k 10 200 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/run$i.json 2> $OUT/run$i.err || { echo "FAIL $kv"; tail -5 $OUT/run$i.err; exit 1; }
-  echo "$kv -> $(grep -o '"ms_per_step": [0-9.]*' $OUT/run$i.json) $(grep -o '"kernel_ms": [0-9.]*' $OUT/run$i.json)"
+  echo "$kv -> $(grep -o "\"ms_per_step\": [0-9.]*\|\"host_ms_per_step\": [0-9.]*\|\"kernel_ms\": [0-9.]*" $OUT/run$i.json | tr "\n" " ")"
 done
