@@ -53,6 +53,11 @@ enum { FLOCK_VARIANT_V2 = 0, FLOCK_VARIANT_UW = 1, FLOCK_VARIANT_UW_DISCRETE = 2
 
 int flock_abi_version(void);
 const char* flock_last_error(void);
+/* Diagnostics (A/B tests and tools only; the defaults are the product paths): "env_launches" (n launches over env
+ * ranges per step), "no_spec" (generic step instantiations), "no_split" (one lane per agent in the split-scan
+ * instantiations), "no_cells" (full scans instead of the cell list). Initialised once from FLOCK_ENV_LAUNCHES,
+ * FLOCK_NO_SPEC, FLOCK_NO_SPLIT, FLOCK_NO_CELLS; not thread-safe against concurrent launches. */
+int flock_set_diag(const char* name, int value);
 
 /* gym_flock_v2 step: pos (rw), heading (rw), action [lin, ang] → vel, dnn, nn_idx, reward, done, any_done. */
 int flock_step_v2(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,

@@ -16,6 +16,7 @@ _c_void_p, _c_int, _c_float, _c_u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_fl
 SIGNATURES = {
     "flock_abi_version": [],
     "flock_last_error": [],
+    "flock_set_diag": [ctypes.c_char_p, _c_int],
     "flock_step_v2": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_float, _c_float,
                       _c_int, _c_int] + [_c_void_p] * 9,
     "flock_step_uw": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_int]

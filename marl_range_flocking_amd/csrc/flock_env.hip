@@ -328,6 +328,34 @@ __device__ __forceinline__ void scan_all(uint32_t (&key)[L], const float2* __res
     }
 }
 
+// phase 3 over candidates [j0, j1) only (j0 even): one quarter of a split scan (step_kernel SPL > 1)
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void scan_range(uint32_t (&key)[L], const float2* __restrict__ cand, int j0, int j1, int ib,
+                                           float xi, float yi, float box) {
+    const uint32_t hi_mask = ~((1u << ib) - 1u);
+#pragma unroll
+    for (int s = 0; s < L; ++s) key[s] = kEmpty;
+    const float4* cand4 = reinterpret_cast<const float4*>(cand);
+    int j = j0;
+#pragma unroll 1
+    for (; j + 7 < j1; j += 8) {
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = cand4[(j >> 1) + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const f32x2 d = pair_d2x2<PERIODIC>(xi, yi, c[u].x, c[u].y, c[u].z, c[u].w, box);
+            key_insert<L>(key, (__float_as_uint(d.x) & hi_mask) | (uint32_t)(j + 2 * u));
+            key_insert<L>(key, (__float_as_uint(d.y) & hi_mask) | (uint32_t)(j + 2 * u + 1));
+        }
+    }
+#pragma unroll 1
+    for (; j < j1; ++j) {
+        const float2 c = cand[j];
+        key_insert<L>(key, (__float_as_uint(pair_d2<PERIODIC>(xi, yi, c.x, c.y, box)) & hi_mask) | (uint32_t)j);
+    }
+}
+
 // Cell-list scans (step variants, N >= 128). The env's agents are binned into a Gx x Gy grid of cells about as
 // tall as twice the typical (k+1)-th neighbour distance and about one agent per cell (Gy = max(kRows, 0.38 sqrt N),
 // Gx = max(2 kRg + 4, N / Gy)), and stored cell-sorted, row by row, in an extended array ext of (x, y, j, sx): every
@@ -634,14 +662,20 @@ constexpr int clog2c(int n) {
 // hot configuration. The launch's Params copy gets those fields as compile-time constants, so the variant branches,
 // the env/lane split (t / N), the LDS carve-up and every trip count that depends on them fold away (fewer SGPRs
 // live across the kernel). Same code, same results as the generic instantiation.
-template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0>
+// SPL > 1 (small N without cells, SPL * N threads per block): one env per block, SPL waves-worth of lanes per env.
+// The first N lanes are the env's agents for every phase; the candidate scan alone is split: lane group q scans
+// candidates [q N / SPL, (q + 1) N / SPL) for agent (t mod N), and the agents' lanes merge the SPL partial top-L
+// key lists through LDS (the same key set, hence the same result, as the one-lane scan). At N = 64 this gives 4x the
+// waves of one lane per agent, where one wave per SIMD left every latency exposed.
+template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params pin) {
+    static_assert(SPL == 1 || (NC > 0 && !CELL && (NC % (2 * SPL)) == 0), "split scans: specialised N, no cells");
     Params p = pin;
     if (VAR >= 0) p.variant = VAR;
     if (NC > 0) {  // make_cfg / dispatch values for N = NC
         p.N = NC;
         p.k = L - 2;
-        p.G = NC <= 256 ? 256 / NC : 1;
+        p.G = SPL > 1 ? 1 : (NC <= 256 ? 256 / NC : 1);
         p.S = (NC + 1) & ~1;
         p.P = 1 << clog2c(NC);
         p.ib = clog2c(NC) < 1 ? 1 : clog2c(NC);
@@ -756,7 +790,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     for (int s = 0; s < kMemKeep; ++s) mrow[s] = 0.0f;
     float prev_h = 0.0f;  // uw reward: the previous heading (:202-204), loaded early
     if (active && variant == FLOCK_VARIANT_UW) prev_h = p.prev_heading[a];
-    if (kMemEarly && active && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
+    if constexpr (SPL > 1 && kMemEarly) {  // split instantiation: lane groups 1..3 roll memory frames 0..2 (k = 4)
+        const int q = t / NC, ia = t - q * NC;
+        const int envb = p.env0 + (int)blockIdx.x;
+        if (q >= 1 && q < kMem && envb < p.E && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
+            const size_t ab = (size_t)envb * NC + ia;
+            reinterpret_cast<float4*>(p.mem_out + ab * kMem * 4)[q] =
+                reinterpret_cast<const float4*>(p.mem_in + ab * kMem * 4)[q - 1];
+        }
+    }
+    if (kMemEarly && SPL == 1 && active && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
         const float* mi = p.mem_in + a * kMem * p.k;
         if (L - 2 == 4 && p.k == 4) {  // 3 x float4 (rows are 64-B aligned)
 #pragma unroll
@@ -1038,6 +1081,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #ifdef FLOCK_PHASE_PROF
     if (__ballot(active && !ok) != 0) PHASE_COUNT(17, 1);
 #endif
+    if constexpr (SPL > 1) {  // split scan: every lane group takes 1 / SPL of the candidates, then the merge
+        constexpr int Q = NC / SPL;
+        const int q = t / NC, ia = t - q * NC;
+        const bool live = p.env0 + (int)blockIdx.x < p.E;
+        uint32_t part[L];
+        if (live) {
+            const float2 me = lpos[ia];  // published by the phase-2 barrier
+            scan_range<L, PERIODIC>(part, lpos, q * Q, q * Q + Q, p.ib, me.x, me.y, p.box);
+        }
+        uint32_t* mk = reinterpret_cast<uint32_t*>(ext_all);  // [SPL - 1][L][NC] (no cell list here)
+        if (q > 0 && live)
+#pragma unroll
+            for (int s = 0; s < L; ++s) mk[((q - 1) * L + s) * NC + ia] = part[s];
+        __syncthreads();
+        if (q == 0 && live) {
+#pragma unroll
+            for (int s = 0; s < L; ++s) key[s] = part[s];
+            for (int r = 0; r < SPL - 1; ++r)
+#pragma unroll
+                for (int s = 0; s < L; ++s) key_insert<L>(key, mk[(r * L + s) * NC + ia]);
+        }
+        ok = true;
+    }
     if (active) {
         if (!ok) {
             scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
@@ -1086,7 +1152,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 float4* mo4 = reinterpret_cast<float4*>(mo);
                 mo4[0] = make_float4(dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]);
 #pragma unroll
-                for (int f = 0; f < kMem - 1; ++f)
+                for (int f = 0; f < (SPL > 1 ? 0 : kMem - 1); ++f)  // (split: the other lane groups rolled them)
                     mo4[f + 1] = make_float4(mrow[(f * (L - 2)) % kMemKeep], mrow[(f * (L - 2) + 1) % kMemKeep],
                                              mrow[(f * (L - 2) + 2) % kMemKeep], mrow[(f * (L - 2) + 3) % kMemKeep]);
             } else if (kMemEarly) {
@@ -1333,11 +1399,11 @@ bool cell_grid(int N, int variant, int* gx, int* gy) {
     return true;
 }
 
-Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy) {
+Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy, int G = 0) {
     Cfg c;
     c.S = (N + 1) & ~1;
     c.P = 1 << ceil_log2(N);
-    c.G = (N <= 256) ? (256 / N) : 1;
+    c.G = G > 0 ? G : ((N <= 256) ? (256 / N) : 1);
     c.T = ((c.G * N + 63) / 64) * 64;
     c.blocks = (E + c.G - 1) / c.G;
     if (reset)
@@ -1359,23 +1425,45 @@ int check_common(int E, int N, int k) {
     return FLOCK_OK;
 }
 
-// FLOCK_ENV_LAUNCHES=n (diagnostics): split a step into n launches over consecutive env ranges
+// diagnostics knobs, read once (first launch): FLOCK_ENV_LAUNCHES=n splits a step into n launches over consecutive
+// env ranges; FLOCK_NO_SPEC=1 takes the generic instantiations; FLOCK_NO_SPLIT=1 the one-lane-per-agent scan of the
+// split (SPL > 1) instantiations; FLOCK_NO_CELLS=1 the full scan instead of the cell list (A/B tests)
+struct Knobs {
+    int env_launches;
+    bool no_spec, no_split, no_cells;
+};
+Knobs& knobs_mut() {
+    static Knobs k = [] {
+        const char* e = getenv("FLOCK_ENV_LAUNCHES");
+        return Knobs{e ? atoi(e) : 1, getenv("FLOCK_NO_SPEC") != nullptr, getenv("FLOCK_NO_SPLIT") != nullptr,
+                     getenv("FLOCK_NO_CELLS") != nullptr};
+    }();
+    return k;
+}
+const Knobs& knobs() { return knobs_mut(); }
 int env_launches(int blocks) {
-    const char* e = getenv("FLOCK_ENV_LAUNCHES");
-    const int n = e ? atoi(e) : 1;
+    const int n = knobs().env_launches;
     return n < 1 ? 1 : (n > blocks ? blocks : n);
 }
 
-// the specialised instantiations (step_kernel VAR / NC): the BASELINE configurations' per-GPU shapes
-template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC>
-bool launch_spec(const Cfg& c, const Params& p, hipStream_t s) {
+// the specialised instantiations (step_kernel VAR / NC / SPL): the BASELINE configurations' per-GPU shapes
+template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1>
+bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL)
         return false;
     if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
-    if (getenv("FLOCK_NO_SPEC")) return false;  // A/B diagnostics: the generic instantiation
+    if (knobs().no_spec) return false;  // A/B diagnostics: the generic instantiation
+    Cfg c = c0;
+    if (SPL > 1) {  // one env per block of SPL * NC lanes; LDS: the G = 1 layout + the merge lists in place of ext
+        if (knobs().no_split) return false;
+        c = make_cfg(p.E, NC, false, 0, 0, 0, 1);
+        c.T = SPL * NC;
+        c.lds = ((c.lds + 15) & ~(size_t)15) + (size_t)(SPL - 1) * 6 * NC * sizeof(uint32_t);
+    }
     const int parts = env_launches(c.blocks);
     if (parts <= 1) {
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks), dim3(c.T), c.lds, s,
+                           p);
         return true;
     }
     // the step as `parts` back-to-back launches over consecutive env ranges (same results: envs are independent)
@@ -1383,7 +1471,7 @@ bool launch_spec(const Cfg& c, const Params& p, hipStream_t s) {
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC>), dim3(min(per, c.blocks - b0)),
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
                            dim3(c.T), c.lds, s, q);
     }
     return true;
@@ -1395,7 +1483,7 @@ void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
         if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6>(c, p, s)) return;         // config 3
         if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12>(c, p, s)) return;       // config 5
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
-        if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0>(c, p, s)) return;          // config 2
+        if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
     }
     if (p.cells) {
         if (p.periodic)
@@ -1417,7 +1505,7 @@ void launch_reset_L(const Cfg& c, const Params& p, hipStream_t s) {
 
 int dispatch(Params& p, hipStream_t s, bool reset) {
     if (p.E == 0) return FLOCK_OK;
-    p.cells = (reset || getenv("FLOCK_NO_CELLS")) ? 0 : cell_grid(p.N, p.variant, &p.gx, &p.gy);
+    p.cells = (reset || knobs().no_cells) ? 0 : cell_grid(p.N, p.variant, &p.gx, &p.gy);
     if (p.cells) {
         p.ecap = 2 * p.N + 2;
         p.cwx = p.box / (float)p.gx;
@@ -1482,6 +1570,22 @@ Params base(int E, int N, int k, float box) {
 extern "C" {
 
 int flock_abi_version(void) { return FLOCK_ABI_VERSION; }
+
+int flock_set_diag(const char* name, int value) {
+    if (!name) return fail(FLOCK_E_NULL, "flock_set_diag: NULL name");
+    Knobs& k = knobs_mut();
+    if (!strcmp(name, "env_launches"))
+        k.env_launches = value;
+    else if (!strcmp(name, "no_spec"))
+        k.no_spec = value != 0;
+    else if (!strcmp(name, "no_split"))
+        k.no_split = value != 0;
+    else if (!strcmp(name, "no_cells"))
+        k.no_cells = value != 0;
+    else
+        return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
+    return FLOCK_OK;
+}
 
 #ifdef FLOCK_PHASE_PROF
 // diagnostics build only: copy out and clear the phase counters (32 x u64)

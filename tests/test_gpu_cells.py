@@ -7,13 +7,13 @@ state, over uniform, clustered (many agents per cell, forcing long ranges and th
 rescan), and sparse (a blob plus isolated outliers: the 5x5 and full-scan fallbacks) placements, N in 128..1024
 and k up to 15; sampled envs are also checked against the oracle's exact kNN.
 """
-import os
+import contextlib
 
 import numpy as np
 import pytest
 import torch
 
-from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+from marl_range_flocking_amd import FlockConfig, VecFlockEnv, _native
 from parity import _knn_exact
 
 pytestmark = pytest.mark.gpu
@@ -48,24 +48,29 @@ def _positions(kind, E, N, box, rng):
     raise ValueError(kind)
 
 
+@contextlib.contextmanager
+def diag(name, value, default=0):
+    """Set one diagnostics knob of the step library (flock_set_diag) for the body, then restore its default."""
+    lib = _native.lib()
+    assert lib.flock_set_diag(name.encode(), int(value)) == 0
+    try:
+        yield
+    finally:
+        lib.flock_set_diag(name.encode(), int(default))
+
+
 def _step(variant, periodic, pos, head, prev, vel, mem, act, noise, N, k, box, cuda, cells):
     E = pos.shape[0]
     env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
                                   range_start=(0, box), sensor_range=14.0, periodic=periodic), device=cuda)
     env.set_state(positions=pos, headings=head, prev_headings=prev, velocities=vel,
                   obs_memory=mem if variant in ("uw", "flock") else None)
-    if cells:
-        os.environ.pop("FLOCK_NO_CELLS", None)
-    else:
-        os.environ["FLOCK_NO_CELLS"] = "1"
-    try:
+    with diag("no_cells", 0 if cells else 1):
         if variant == "uw_discrete":
             out = env.step(torch.from_numpy(act), noise=torch.from_numpy(noise))
         else:
             out = env.step(torch.from_numpy(act))
         torch.cuda.synchronize()
-    finally:
-        os.environ.pop("FLOCK_NO_CELLS", None)
     obs, rew, (done, anyd), _ = out
     res = {"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn, "idx": env.nn_idx,
            "rew": rew, "done": done, "any": anyd}
@@ -150,13 +155,9 @@ def test_seeded_rollout_is_bitwise_the_full_scan(variant, periodic, N, k, kind, 
             envs[0].seeds.copy_(torch.from_numpy(g))
         outs = []
         for i, env in enumerate(envs):
-            if i == 1:
-                os.environ["FLOCK_NO_CELLS"] = "1"
-            try:
+            with diag("no_cells", i):
                 obs, rew, (done, anyd), _ = env.step(act, **kw)
                 torch.cuda.synchronize()
-            finally:
-                os.environ.pop("FLOCK_NO_CELLS", None)
             outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
                          "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd})
         for key in outs[0]:
@@ -169,10 +170,12 @@ SPEC = [("v2", True, 256, "uniform"), ("v2", True, 1024, "clustered"), ("uw_disc
         ("uw", False, 64, "uniform")]
 
 
+@pytest.mark.parametrize("knob", ["no_spec", "no_split"])
 @pytest.mark.parametrize("variant,periodic,N,kind", SPEC, ids=[f"{v}-N{n}-{d}" for v, _, n, d in SPEC])
-def test_specialised_kernel_is_bitwise_the_generic_one(variant, periodic, N, kind, cuda):
+def test_specialised_kernel_is_bitwise_the_generic_one(variant, periodic, N, kind, knob, cuda):
     """The BASELINE configurations' shapes launch step_kernel instantiations specialised on (variant, N, k = 4, cell
-    grid); FLOCK_NO_SPEC=1 launches the generic instantiation. Four-step rollouts agree bit for bit on every output,
+    grid); no_spec launches the generic instantiation. The config-2 shape (uw, N = 64) also splits its candidate scan
+    over 4 lanes per agent; no_split takes the one-lane scan. Four-step rollouts agree bit for bit on every output,
     the observation memory and the seed buffer."""
     k, E = 4, (16 if N >= 512 else 64)
     box = float(round(np.sqrt(250 * N)))
@@ -195,13 +198,9 @@ def test_specialised_kernel_is_bitwise_the_generic_one(variant, periodic, N, kin
             kw = {}
         outs = []
         for i, env in enumerate(envs):
-            if i == 1:
-                os.environ["FLOCK_NO_SPEC"] = "1"
-            try:
+            with diag(knob, i):
                 obs, rew, (done, anyd), _ = env.step(act, **kw)
                 torch.cuda.synchronize()
-            finally:
-                os.environ.pop("FLOCK_NO_SPEC", None)
             o = obs["actors"] if isinstance(obs, dict) else obs
             outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
                          "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd, "obs": o.clone()})
@@ -308,18 +307,15 @@ def test_env_range_launches_are_bitwise_one_launch(cuda):
                                       range_start=(0, box), sensor_range=14.0), device=cuda)
         env.set_state(positions=pos, headings=head)
         envs.append(env)
-    try:
-        for t in range(4):
-            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
-            outs = []
-            for i, env in enumerate(envs):
-                os.environ["FLOCK_ENV_LAUNCHES"] = "4" if i else "1"
+    for t in range(4):
+        act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
+        outs = []
+        for i, env in enumerate(envs):
+            with diag("env_launches", 4 if i else 1, default=1):
                 obs, rew, (done, anyd), _ = env.step(act)
                 torch.cuda.synchronize()
-                outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
-                             "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd,
-                             "seeds": env.seeds.clone() if env.seeds is not None else rew})
-            for key in outs[0]:
-                assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
-    finally:
-        os.environ.pop("FLOCK_ENV_LAUNCHES", None)
+            outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
+                         "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd,
+                         "seeds": env.seeds.clone() if env.seeds is not None else rew})
+        for key in outs[0]:
+            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
