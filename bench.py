@@ -92,14 +92,17 @@ CONFIGS = {
 
 
 def setup_dist(args):
+    """One process per GPU over RCCL ("nccl"). FLOCK_DIST_BACKEND=gloo rehearses the N > 1 code path with several
+    ranks on one GPU (device = LOCAL_RANK mod the visible GPUs); its numbers are not scaling results."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    backend = os.environ.get("FLOCK_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % torch.cuda.device_count() if backend != "nccl" else local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        torch.distributed.init_process_group(backend, **kw)
     return world, rank, dev
 
 
@@ -234,14 +237,19 @@ class MADDPGBench:
 
         self.env = env
         group = torch.distributed.group.WORLD if torch.distributed.is_initialized() else None
-        self.learner = MADDPGLearner(env.N, env.k, recurrent=True, device=dev, seed=seed, dist_group=group)
+        # under torchrun: agent-sharded critics (each rank owns N / world critics; the minibatches and the actor
+        # heads' actions are all-gathered instead of all-reducing the 3.6-GB critic gradient)
+        self.learner = MADDPGLearner(env.N, env.k, recurrent=True, device=dev, seed=seed, dist_group=group,
+                                     agent_shard=group is not None and env.N % torch.distributed.get_world_size() == 0)
         self.prev = None
 
     def describe(self):
+        L = self.learner
         return (f"RNN-MADDPG train() every {self.every} vectorized steps (B 128, chunk 10, {self.env.N} critics "
                 f"400/300); all {self.env.E} env records per step inserted into a 45k-row device replay ring by the "
                 f"env kernel itself"
-                + ("; critic gradient all-reduce over RCCL" if self.learner.distributed else ""))
+                + ("; agent-sharded critics, minibatch + action all-gathers over RCCL" if L.shard else
+                   "; critic gradient all-reduce over RCCL" if L.distributed else ""))
 
     def before(self, s):
         # the env kernel writes every env's record itself (flock_step_v2_store, one ring row per env)

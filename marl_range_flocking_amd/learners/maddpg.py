@@ -19,14 +19,21 @@ What changes: all N actors / critics / targets are stacked [N, ...] slices of fl
 agent is one batched GEMM; the GRU elementwise work is flock_gru_fwd/bwd; the N critic Adam steps + target critic
 soft updates are ONE flock_adam_step launch; the update replays as one HIP graph; the N sequential OU samples are a
 closed-form prefix scan.
+
+Multi-GPU: data-parallel replicas all-reduce the critics' flat gradient (907 M floats at config 5,
+3.6 GB per update), or, with agent_shard=True, each rank owns the critics and target actors of N / world agents:
+the ranks' sampled minibatches are all-gathered into the union batch (~2 x 21 MB of observations per rank at
+config 5), every rank runs its agents' actor heads and critics on it, and the [B', 2] action columns of the actor
+heads are all-gathered (every critic reads every agent's action). Per-agent results equal the replicated update on
+the union batch; no gradient crosses xGMI.
 """
 import math
 
 import torch
 import torch.nn.functional as F
 
-from .. import dist
-from .core import FlatParams, ReplayRing, blinear, capture_graph, gru_cell, gru_seq, shared_linear
+from .. import _native, dist
+from .core import FlatParams, ReplayRing, _p, _stream, blinear, capture_graph, gru_cell, gru_seq, shared_linear
 
 HR = 32  # hidden_rnn (net.py:15,100)
 
@@ -216,7 +223,7 @@ class MADDPGLearner:
     def __init__(self, n_agents, k, recurrent=True, n_actions=2, hidden1=400, hidden2=300, actor_lr=3e-3,
                  critic_lr=3e-3, gamma=0.99, tau=0.001, batch_size=128, chunk_size=10, buffer_capacity=45_000,
                  min_size_buffer=8_000, ou_theta=0.15, ou_mu=0.0, ou_sigma=0.2, ou_sigma_min=0.001, device="cuda",
-                 seed=0, use_graph=True, reference_action_layout=True, dist_group=None):
+                 seed=0, use_graph=True, reference_action_layout=True, dist_group=None, agent_shard=False):
         self.device = torch.device(device)
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.N, self.k, self.recurrent, self.h1 = n_agents, k, recurrent, hidden1
@@ -232,6 +239,26 @@ class MADDPGLearner:
         _init(self.critics, self.gen)
         self.actors.hard_update_target()    # agent.py:37-38
         self.critics.hard_update_target()
+        self.group = dist_group
+        self.distributed = dist.active(dist_group)
+        self.shard = bool(agent_shard) and self.distributed
+        if self.shard:
+            # this rank's agents [a0, a0 + na): their critics (params, targets, Adam) only; the actors stay whole
+            # (frozen, Q6: every rank acts for all agents of its envs), their targets are advanced for [a0, a0 + na)
+            W, r = torch.distributed.get_world_size(dist_group), torch.distributed.get_rank(dist_group)
+            if not recurrent:
+                raise NotImplementedError("agent_shard is built for the recurrent MADDPG (config 5)")
+            if n_agents % W:
+                raise ValueError(f"agent_shard needs n_agents ({n_agents}) divisible by the world size ({W})")
+            self.na, self.a0 = n_agents // W, r * (n_agents // W)
+            dist.sync_params(self.critics, group=dist_group)
+            full = self.critics
+            self.critics = FlatParams(full.shapes, self.device, self.na, target=True)
+            with torch.no_grad():
+                for n in full.shapes:
+                    for buf, dst in ((full.data, self.critics.data), (full.target, self.critics.target)):
+                        self.critics.view(dst, n).copy_(full.view(buf, n)[self.a0:self.a0 + self.na])
+            del full
         self.replay = ReplayRing(buffer_capacity, {
             "state": (n_agents, k), "next_state": (n_agents, k), "actor_state": (n_agents, k),
             "actor_next_state": (n_agents, k), "action": (n_agents, n_actions), "reward": (n_agents,),
@@ -244,11 +271,10 @@ class MADDPGLearner:
         self.losses = torch.zeros(2, device=self.device)
         self.use_graph = use_graph
         self.graph = None
-        self.group = dist_group
-        self.distributed = dist.active(dist_group)
         if self.distributed:
             dist.sync_params(self.actors, group=dist_group)
-            dist.sync_params(self.critics, group=dist_group)
+            if not self.shard:
+                dist.sync_params(self.critics, group=dist_group)
 
     # ---------------------------------------------------------------- acting
     def init_hidden(self, envs=1):
@@ -370,6 +396,76 @@ class MADDPGLearner:
             self.losses[0].copy_(critic_loss.detach().mean())
             self.losses[1].copy_(actor_loss.detach().mean())
 
+    # ---------------------------------------------------------------- agent-sharded update (agent_shard=True)
+    def _local_batch(self):
+        """This rank's sampled rows, in the layouts the update reads (the reference action layout per rank)."""
+        N, B, C, k = self.N, self.B, self.C, self.k
+        idx = self.static_idx
+        tidx = idx.t().contiguous()
+        act = self.replay.gather("action", tidx)                                # [C, B, N, 2]
+        if self.reference_action_layout:  # actors_action [N,B,C,2].reshape(B,C,2N) (MADDPG.py:86), per rank
+            act = act.permute(2, 1, 0, 3).contiguous().reshape(B, C, 2 * N).transpose(0, 1)
+        else:
+            act = act.reshape(C, B, 2 * N)
+        return {"S": self.replay.gather("state", tidx).reshape(C, B, N * k),
+                "S2": self.replay.gather("next_state", tidx).reshape(C, B, N * k),
+                "AS": self.replay.gather("actor_state", idx).permute(2, 1, 0, 3),   # [N, C, B, k]
+                "AS2": self.replay.gather("actor_next_state", idx).permute(2, 1, 0, 3),
+                "act": act.contiguous(),                                         # [C, B, 2N]
+                "R": self.replay.gather("reward", idx), "D": self.replay.gather("done", idx)}  # [B, C, N]
+
+    # batch dimension of each field: the union batch is every rank's rows, rank after rank
+    _BATCH_DIM = {"S": 1, "S2": 1, "AS": 2, "AS2": 2, "act": 1, "R": 0, "D": 0}
+
+    def _gather_cat(self, t, dim):
+        parts = [torch.empty_like(t) for _ in range(torch.distributed.get_world_size(self.group))]
+        torch.distributed.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, dim)
+
+    def _train_shard(self):
+        """One train() of this rank's agents on the union batch (MADDPG.py:78-150 per agent)."""
+        lo, hi = self.a0, self.a0 + self.na
+        U = {n: self._gather_cat(v, self._BATCH_DIM[n]) for n, v in self._local_batch().items()}
+        C = self.C
+        Bu = U["S"].shape[1]
+        last = C - 1
+        sl = lambda fp, buf: {n: fp.view(buf, n)[lo:hi] for n in fp.shapes}  # noqa: E731
+        Pa, Pta = sl(self.actors, self.actors.data), sl(self.actors, self.actors.target)
+        Ptc = {n: self.critics.view(self.critics.target, n) for n in self.critics.shapes}
+        Pc = self.critic_leaves
+        keep = (U["D"] == 0).permute(1, 2, 0)[:, lo:hi]                      # [C, na, Bu]
+        with torch.no_grad():
+            y_ta = actor_seq(Pta, U["AS2"][lo:hi], keep)[:, last]
+            y_a = actor_seq(Pa, U["AS"][lo:hi], keep)[:, last]
+            heads = torch.stack([actor_head(Pta, y_ta), actor_head(Pa, y_a)])  # [2, na, Bu, 2]
+            heads = self._gather_cat(heads, 1)                                 # every agent's actions
+            cta = heads[0].transpose(0, 1).reshape(Bu, 2 * self.N)
+            cpa = heads[1].transpose(0, 1).reshape(Bu, 2 * self.N)
+            y_tc = critic_seq(Ptc, U["S2"], keep)[0][:, last]
+            tq = critic_head(Ptc, F.relu(blinear(y_tc, Ptc["fc1.weight"], Ptc["fc1.bias"])), cta)
+        hs_c, fx = critic_seq(Pc, U["S"], keep)
+        y_c = hs_c[:, last]
+        h_c = torch.where(keep[last].unsqueeze(-1), y_c, 0.0)
+        h_aq = critic_gru(Pc, fx[:, last], h_c)
+        y = F.relu(blinear(torch.cat([y_c, h_aq], 1), Pc["fc1.weight"], Pc["fc1.bias"]))
+        qq = critic_head(Pc, y, torch.cat([U["act"][last], cpa], 0))
+        q, aq = qq[:, :Bu], qq[:, Bu:]
+        r = U["R"][:, last, lo:hi].t().unsqueeze(-1)
+        d = U["D"][:, last, lo:hi].t().unsqueeze(-1)
+        target = r + self.gamma * tq * (1 - d)                                  # MADDPG.py:135
+        critic_loss = ((target - q) ** 2).mean(dim=(1, 2))
+        actor_loss = -aq.mean(dim=(1, 2))
+        self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc)
+        self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
+        for n in self.actors.shapes:  # the target actors of this rank's agents (mode 0, as _step)
+            t, p_ = self.actors.view(self.actors.target, n)[lo:hi], self.actors.view(self.actors.data, n)[lo:hi]
+            _native.check(_native.lib().flock_soft_update(_stream(self.device), t.numel(), _p(t), _p(p_),
+                                                          float(self.tau), 0), "flock_soft_update", learn=True)
+        with torch.no_grad():
+            sums = torch.stack([critic_loss.detach().sum(), actor_loss.detach().sum()])
+            torch.distributed.all_reduce(sums, group=self.group)
+            self.losses.copy_(sums / self.N)
+
     def _step(self):
         # critic_optimizer.step() + update_target_networks() (:148-150): one launch for all agents
         self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
@@ -385,6 +481,9 @@ class MADDPGLearner:
             starts = torch.randperm(hi, device=self.device, generator=self.gen)[:self.B]
         starts = torch.as_tensor(starts, device=self.device)
         self.static_idx.copy_(starts[:, None] + torch.arange(self.C, device=self.device)[None])
+        if self.shard:  # collectives between the phases: eager
+            self._train_shard()
+            return self.losses
         fn = self._fwd_bwd if self.distributed else self._update
         if self.use_graph:
             if self.graph is None:
@@ -406,6 +505,10 @@ class MADDPGLearner:
             i = int(key[len(key.rstrip("0123456789")):])
             fp = self.actors if net == "actor" else self.critics
             tgt = key.startswith("target")
+            if net == "critic" and self.shard:  # agent_shard: this rank's critics only
+                if not self.a0 <= i < self.a0 + self.na:
+                    continue
+                i -= self.a0
             for n, v in sd.items():
                 if n in CRITIC_JOINED and net == "critic":
                     v = torch.as_tensor(v)
@@ -418,7 +521,12 @@ class MADDPGLearner:
                     fp.load(n, v, agent=i, target=tgt)
 
     def state_dict(self, net, i, target=False):
+        """Reference state_dict of agent i's actor / critic (agent_shard: critics of this rank's agents only)."""
         fp = self.actors if net == "actor" else self.critics
+        if net == "critic" and self.shard:
+            if not self.a0 <= i < self.a0 + self.na:
+                raise KeyError(f"critic {i} lives on another rank (this rank holds {self.a0}..{self.a0 + self.na - 1})")
+            i -= self.a0
         out = {}
         for n in reference_names(fp):
             if n in CRITIC_JOINED and n not in fp.shapes:

@@ -175,3 +175,87 @@ def test_two_ranks_overlapped_bench_loop_equals_serial(cuda):
         for x, y in zip(serial, overlapped):
             np.testing.assert_array_equal(x, y)
     np.testing.assert_array_equal(out[0][1][1][0], out[1][1][1][0])  # replicas identical
+
+
+NS = 4  # agents of the sharded test (divisible by the world size)
+
+
+def _shard_make(batch, group=None, shard=False):
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+    return MADDPGLearner(NS, K, recurrent=True, hidden1=32, hidden2=24, batch_size=batch, chunk_size=C,
+                         buffer_capacity=128, min_size_buffer=batch, device="cuda:0", seed=0, dist_group=group,
+                         reference_action_layout=False, agent_shard=shard)
+
+
+def _shard_fill(L):
+    rng = np.random.default_rng(1)
+    obs = rng.uniform(0, 14, (T + 1, NS, K)).astype(np.float32)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (NS, 2)).astype(np.float32)
+        r = rng.choice([-5.0, 0.01], (NS,)).astype(np.float32)
+        d = (rng.uniform(size=NS) < 0.1).astype(np.float32)
+        L.add_record(obs[t], obs[t + 1], a, obs[t], obs[t + 1], r, d)
+
+
+def _layers(fp, buf, lo, hi):
+    return np.concatenate([fp.view(buf, n)[lo:hi].detach().cpu().numpy().ravel() for n in fp.shapes])
+
+
+def _shard_worker(rank, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", RANK=str(rank))
+    try:
+        torch.distributed.init_process_group("gloo")
+        L = _shard_make(B, torch.distributed.group.WORLD, shard=True)
+        assert L.shard and L.na == NS // 2 and L.a0 == rank * (NS // 2)
+        _shard_fill(L)
+        st = np.random.default_rng(5).choice(T - C, 2 * B, replace=False)
+        for s2 in (st, st[::-1].copy()):
+            L.train(starts=s2[rank * B:(rank + 1) * B])
+        A = L.actors
+        q.put((rank, _layers(L.critics, L.critics.data, 0, L.na), _layers(L.critics, L.critics.target, 0, L.na),
+               _layers(A, A.target, L.a0, L.a0 + L.na), _layers(A, A.data, 0, NS), L.losses.cpu().numpy(),
+               L.state_dict("critic", L.a0)["fc2.weight"].numpy()))
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put((rank, "error", traceback.format_exc() + repr(e)))
+
+
+def test_agent_sharded_critics_equal_union_batch(cuda):
+    """MADDPGLearner(agent_shard=True) on 2 ranks: each rank owns the critics and target actors of half the agents,
+    all-gathers both ranks' minibatches and the actor heads' actions, and updates only its agents. After two train()
+    calls each rank's critics, critic targets and target actors equal that slice of ONE process training every
+    agent on the union batch (same tolerance as the data-parallel test); the frozen actors stay bitwise whole."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in range(2)], key=lambda o: o[0])
+    for p in ps:
+        p.join(timeout=60)
+    for o in out:
+        assert not isinstance(o[1], str), o
+    ref = _shard_make(2 * B)
+    _shard_fill(ref)
+    st = np.random.default_rng(5).choice(T - C, 2 * B, replace=False)
+    for s2 in (st, st[::-1].copy()):
+        ref.train(starts=s2)
+    h = NS // 2
+    for rank, crit, ctgt, atgt, actors, losses, fc2 in out:
+        lo, hi = rank * h, (rank + 1) * h
+        for got, want in ((crit, _layers(ref.critics, ref.critics.data, lo, hi)),
+                          (ctgt, _layers(ref.critics, ref.critics.target, lo, hi)),
+                          (atgt, _layers(ref.actors, ref.actors.target, lo, hi))):
+            err = np.abs(got - want)
+            bad = err > 1e-6 + 1e-4 * np.abs(want)
+            assert bad.mean() < 0.01, (rank, int(bad.sum()), float(err.max()))
+        np.testing.assert_array_equal(actors, _layers(ref.actors, ref.actors.data, 0, NS))
+        np.testing.assert_allclose(losses, ref.losses.cpu().numpy(), rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(fc2, ref.state_dict("critic", lo)["fc2.weight"].numpy(), rtol=1e-4, atol=1e-5)
