@@ -115,10 +115,15 @@ typedef struct FlockScUpdate {
     float* critic_view; /* may be NULL. With do_adam: flock_sc_critic_update writes the critic's post-Adam
                            parameters here and, when this learn() soft-updates (update_rate above), the critic's
                            self soft update tau c + (1 - tau) c (the shared critic is its own target, :172-178)
-                           straight into `critic`; flock_sc_actor_update then reads the critic from critic_view.
+                           straight into `critic`. flock_sc_actor_update reads the critic from critic_view whenever
+                           it is given (with do_adam = 0 too: data-parallel gradient rounds).
                            Results are bitwise those of critic_view = NULL; what it buys is that the critic phase of
                            the NEXT learn() (which reads `critic`) may run while this actor phase still reads the
                            critic it was given (two views, alternated by the caller). */
+    float* actor_grad_out; /* may be NULL. The actor phase writes its gradient here (one actor, not agent-relative)
+                              instead of actors_grad + agent * actor_stride, and flock_sc_round_adam reads it
+                              there: data-parallel callers put it right behind critic_grad, so the two gradients
+                              of a round are ONE contiguous all-reduce bucket. */
 } FlockScUpdate;
 
 int64_t flock_sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2);
@@ -149,6 +154,14 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (a
  * no written state (actor_u must carry a critic_view, critic_u its own workspace and critic_view). The two updates
  * must have the same shapes. */
 int flock_sc_round(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u);
+/* The Adam half of a data-parallel round: after flock_sc_round with do_adam = 0 wrote the gradients and the caller
+ * all-reduced them (sums), one launch applies Adam to the whole critic (critic_u: with its critic_view and self
+ * soft update, as flock_sc_critic_update with do_adam) and / or to the actor of actor_u's agent (from
+ * actor_grad_out when set; its target soft update on soft learns), every gradient multiplied by *grad_scale
+ * (device scalar, e.g. 1 / world; NULL: 1) first; step counters advance as with do_adam. critic_u / actor_u must
+ * have do_adam = 1. */
+int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u,
+                        const float* grad_scale);
 
 /* learn() pipeline of a training loop that calls Agent.learn() once per env step (train_flock.py:120-121, one agent
  * per call): n_slots (2..8) staging slots, each with its own FlockScUpdate (do_adam, own critic_view, own workspace;

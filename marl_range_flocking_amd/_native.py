@@ -76,7 +76,7 @@ class FlockScUpdate(ctypes.Structure):
                 + [("actor_stride", ctypes.c_int64)]
                 + [(n, _c_void_p) for n in ("losses", "workspace", "counters")]
                 + [(n, _c_float) for n in ("alpha", "beta", "gamma", "beta1", "beta2", "eps", "tau")]
-                + [("update_rate", _c_int), ("critic_view", _c_void_p)])
+                + [("update_rate", _c_int), ("critic_view", _c_void_p), ("actor_grad_out", _c_void_p)])
 
 
 class FlockRingField(ctypes.Structure):
@@ -115,6 +115,7 @@ SIGNATURES.update({
     "flock_sc_critic_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_actor_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_round": [_c_void_p, ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScUpdate)],
+    "flock_sc_round_adam": [_c_void_p, ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScUpdate), _c_void_p],
     "flock_sc_pipeline_create": [_c_int, ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScRows),
                                  ctypes.POINTER(FlockScRows)],
     "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],

@@ -983,7 +983,8 @@ struct BwdJob {
     int nred, nblk, B;
     RedP red[kMaxRed];
     float* grad;
-    int64_t rel;  // grad / g1 are agent-relative: + rel * (*agent)
+    int64_t rel;       // g1 is agent-relative: + rel * (*agent)
+    int64_t grad_rel;  // grad is agent-relative: + grad_rel * (*agent) (0: FlockScUpdate.actor_grad_out)
     const int64_t* agent;
     float* loss;
 };
@@ -996,6 +997,7 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
     float* smem = reinterpret_cast<float*>(smem4);
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
     const int64_t base = j.rel ? j.rel * (*j.agent) : 0;
+    const int64_t gbase = j.grad_rel ? j.grad_rel * (*j.agent) : 0;
     if (bx < j.dh.tiles) {
         const GemmP& g = j.dh;
         const int tm = bx / g.tiles_n, tn = bx - tm * g.tiles_n;
@@ -1056,7 +1058,7 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int mm = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-            if (mm < g.M && nn < g.N) j.grad[base + j.w2_off + (int64_t)mm * g.ldc + nn] = out[q];
+            if (mm < g.M && nn < g.N) j.grad[gbase + j.w2_off + (int64_t)mm * g.ldc + nn] = out[q];
         }
     } else {
         const int b = bx - j.dh.tiles - j.dw.tiles;
@@ -1072,7 +1074,7 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
             if (rp.mode == 3)
                 *j.loss = gsum * (1.0f / (float)j.B);
             else
-                j.grad[base + rp.off + e] = gsum;
+                j.grad[gbase + rp.off + e] = gsum;
         }
     }
 }
@@ -1096,7 +1098,9 @@ struct GradAdam {
     int64_t adam_lo, adam_n;  // Adam-only region (gradients written by the bwd launch), relative to the agent base
     int adam_blocks;
     float *p, *grad, *m, *v;
-    int64_t rel;  // p/grad/m/v are agent-relative: + rel * (*agent)
+    int64_t rel;       // p/m/v (and target) are agent-relative: + rel * (*agent)
+    int64_t grad_rel;  // grad likewise: + grad_rel * (*agent) (0 with FlockScUpdate.actor_grad_out)
+    const float* grad_scale;  // Adam-only blocks: gradient *= *grad_scale first (data-parallel 1 / world), or NULL
     const int64_t* agent;
     int64_t* step;  // step[0], or step[*agent] when rel != 0
     unsigned* counter;
@@ -1151,7 +1155,7 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
     __shared__ int sh_soft;
     const int tid = threadIdx.x;
     const int64_t agent = ga.rel ? *ga.agent : 0;
-    const int64_t base = ga.rel * agent;
+    const int64_t base = ga.rel * agent, gbase = ga.grad_rel * agent;
     if (tid == 0) {
         const int64_t step0 = ga.do_adam ? ga.step[agent] : 0;
         const int64_t count = ga.soft_count ? ga.soft_count[*ga.agent] : step0;
@@ -1181,16 +1185,17 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
         const int64_t e0 = ga.adam_lo + (int64_t)(bx - adam0) * 1024, end = ga.adam_lo + ga.adam_n;
         AdamState st[4];
         float gi[4];
+        const float gs = ga.grad_scale ? *ga.grad_scale : 1.0f;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t e = e0 + q * 256 + tid;
             st[q] = e < end ? adam_load(ga, base + e) : AdamState{0.f, 0.f, 0.f, 0.f};
-            gi[q] = e < end ? ga.grad[base + e] : 0.0f;
+            gi[q] = e < end ? ga.grad[gbase + e] : 0.0f;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t e = e0 + q * 256 + tid;
-            if (e < end) adam_store(ga, base + e, st[q], gi[q], sh[0], sh[1], sh_soft != 0);
+            if (e < end) adam_store(ga, base + e, st[q], ga.grad_scale ? gi[q] * gs : gi[q], sh[0], sh[1], sh_soft != 0);
         }
     } else {
         const int b = bx;
@@ -1205,9 +1210,8 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
         bool wr;
         const float gsum = red_block(rp, b, ga.B, ga.dz, smem, smem + 256, e, wr);
         if (wr) {
-            const int64_t pe = base + rp.off + e;
-            ga.grad[pe] = gsum;
-            if (ga.do_adam) adam_store(ga, pe, st, gsum, sh[0], sh[1], sh_soft != 0);
+            ga.grad[gbase + rp.off + e] = gsum;
+            if (ga.do_adam) adam_store(ga, base + rp.off + e, st, gsum, sh[0], sh[1], sh_soft != 0);
         }
     }
     // the last block to arrive advances the step counter. No fence: every block's thread 0 consumed its load of
@@ -1438,7 +1442,7 @@ void bwd_common(Job& j, const float* W2, int64_t rel_w2, const int64_t* agent, c
     bw.F = H1n; bw.ntn = bw.dh.tiles_n;
     bw.w2_off = w2_off;
     bw.nred = 0; bw.nblk = 0; bw.B = B;
-    bw.grad = grad; bw.rel = rel; bw.agent = agent; bw.loss = loss;
+    bw.grad = grad; bw.rel = rel; bw.grad_rel = rel; bw.agent = agent; bw.loss = loss;
 }
 
 // the late launch's job: fc1 / LN1 reductions (+ Adam), Adam of [W2, total)
@@ -1460,6 +1464,7 @@ void late_common(Job& j, const FlockScUpdate* u, const float* DXH1, const float*
     ga.adam_n = total - W2;
     ga.adam_blocks = u->do_adam ? (int)((ga.adam_n + 1023) / 1024) : 0;
     ga.lr = 0.0f;
+    ga.grad_scale = nullptr;
     ga.b1 = u->beta1; ga.b2 = u->beta2; ga.eps = u->eps;
     ga.tau = u->tau;
     ga.one_minus_tau = (float)(1.0 - (double)u->tau);
@@ -1495,6 +1500,7 @@ void critic_job(const FlockScUpdate* u, Job& j) {
     GradAdam& ga = j.ga;
     ga.p = u->critic; ga.grad = u->critic_grad; ga.m = u->critic_exp_avg; ga.v = u->critic_exp_avg_sq;
     ga.rel = 0;
+    ga.grad_rel = 0;
     ga.agent = u->agent;
     ga.step = u->critic_step;
     ga.counter = u->counters;
@@ -1513,7 +1519,9 @@ void actor_job(const FlockScUpdate* u, Job& j) {
     const int B = j.B, in = j.in, na = j.na, H1 = j.H1, H2 = j.H2;
     const Ws& w = j.w;
     const bool view = u->do_adam && u->critic_view;
-    float* const critic = view ? u->critic_view : u->critic;  // the critic this actor step sees (post-Adam)
+    // the critic this actor step sees (post-Adam): the view whenever one is given (the data-parallel rounds compute
+    // gradients with do_adam = 0 after an earlier flock_sc_round_adam wrote the view)
+    float* const critic = u->critic_view ? u->critic_view : u->critic;
     j.a.critic = critic;
     const CriticOff co = critic_off(in, na, H1, H2);
     const ActorOff ao = actor_off(in, na, H1, H2);
@@ -1526,6 +1534,10 @@ void actor_job(const FlockScUpdate* u, Job& j) {
     BwdJob& bw = j.bw;
     bwd_common(j, u->actors + ao.W2, u->actor_stride, u->agent, w.AH1, w.AXH1, u->actors + ao.g1, w.ADY1, w.ADXH1,
                w.APS1, w.ADZ2, ao.W2, u->actors_grad, u->actor_stride, u->losses);
+    if (u->actor_grad_out) {  // this actor's gradient into the caller's bucket (not agent-relative)
+        bw.grad = u->actor_grad_out;
+        bw.grad_rel = 0;
+    }
     add_red(bw, w.ADZ2, H2, nullptr, 0, 0, 1, H2, ao.b2);
     add_red(bw, w.ADY2, H2, w.AXH2, H2, 1, 1, H2, ao.g2);
     add_red(bw, w.ADY2, H2, nullptr, 0, 0, 1, H2, ao.be2);
@@ -1536,6 +1548,11 @@ void actor_job(const FlockScUpdate* u, Job& j) {
     GradAdam& ga = j.ga;
     ga.p = u->actors; ga.grad = u->actors_grad; ga.m = u->actors_exp_avg; ga.v = u->actors_exp_avg_sq;
     ga.rel = u->actor_stride;
+    ga.grad_rel = u->actor_stride;
+    if (u->actor_grad_out) {
+        ga.grad = u->actor_grad_out;
+        ga.grad_rel = 0;
+    }
     ga.agent = u->agent;
     ga.step = u->actor_steps;
     ga.counter = u->counters + 1;
@@ -1762,6 +1779,51 @@ int64_t flock_sc_update_size(void) { return (int64_t)sizeof(FlockScUpdate); }
 int flock_sc_critic_update(void* stream, const FlockScUpdate* u) { return flock_sc_round(stream, u, nullptr); }
 
 int flock_sc_actor_update(void* stream, const FlockScUpdate* u) { return flock_sc_round(stream, nullptr, u); }
+
+int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u,
+                        const float* grad_scale) {
+    if (!critic_u && !actor_u) return fail(-3, "flock_sc_round_adam: NULL argument");
+    int rc = 0;
+    if (critic_u && (rc = check(critic_u))) return rc;
+    if (actor_u && (rc = check(actor_u))) return rc;
+    if ((critic_u && !critic_u->do_adam) || (actor_u && !actor_u->do_adam))
+        return fail(-5, "flock_sc_round_adam: the updates must have do_adam = 1");
+    Job jc, ja;
+    GradAdam* js[2] = {nullptr, nullptr};
+    int n = 0;
+    if (critic_u) {
+        critic_job(critic_u, jc);
+        js[n++] = &jc.ga;
+    }
+    if (actor_u) {
+        actor_job(actor_u, ja);
+        js[n++] = &ja.ga;
+    }
+    for (int i = 0; i < n; ++i) {  // Adam-only: no reductions, the whole parameter range from the gradient buffer
+        GradAdam& g = *js[i];
+        g.nred = 0;
+        g.nblk = 0;
+        g.adam_lo = 0;
+        g.grad_scale = grad_scale;
+    }
+    if (critic_u) {
+        const CriticOff co = critic_off(critic_u->in_dim, critic_u->n_actions, critic_u->fc1, critic_u->fc2);
+        jc.ga.adam_n = co.total;
+        jc.ga.adam_blocks = (int)((co.total + 1023) / 1024);
+    }
+    if (actor_u) {
+        const ActorOff ao = actor_off(actor_u->in_dim, actor_u->n_actions, actor_u->fc1, actor_u->fc2);
+        ja.ga.adam_n = ao.total;
+        ja.ga.adam_blocks = (int)((ao.total + 1023) / 1024);
+    }
+    GradAdam2 gg;
+    gg.j0 = *js[0];
+    gg.j1 = *js[n - 1];
+    gg.nb0 = late_blocks(gg.j0);
+    const int nb = gg.nb0 + (n == 2 ? late_blocks(gg.j1) : 0);
+    hipLaunchKernelGGL(sc_grad_adam, dim3(nb), dim3(256), 0, (hipStream_t)stream, gg);
+    return launched();
+}
 
 int flock_sc_round(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u) {
     if (!critic_u && !actor_u) return fail(-3, "flock_sc_round: NULL argument");

@@ -13,9 +13,11 @@ the replay ring is device-resident (HIP scatter/gather rows, no CPU round trip),
 actor in one batched GEMM chain, and the OU noise is a per-(env, agent) device process.
 
 learn() has two implementations with the same semantics:
-  * fused (default): flock_sc_critic_update + flock_sc_actor_update (csrc/flock_sc.hip) — 12 HIP launches reading
-    the replay ring, the agent's actor slice and the critic in place, Adam fused into the gradient kernels; the pair
-    is replayed as one HIP graph;
+  * fused (default): flock_sc_critic_update + flock_sc_actor_update (csrc/flock_sc.hip), five HIP launches each,
+    reading the replay rows, the agent's actor slice and the critic in place, Adam in the last launch. The bench
+    loop's native pipeline (pipeline_learn) runs the critic phase of learn t and the actor phase of learn t-1 as one
+    round of five launches (flock_sc_round); data-parallel replicas (dp_learn) run the round as gradients, ONE
+    all-reduce of the [critic | actor] bucket and one Adam launch (flock_sc_round_adam);
   * autograd (fused=False): the same update written with torch ops and the batched helpers of core.py.
 """
 import ctypes
@@ -172,6 +174,12 @@ class SharedCriticLearner:
             self.identity_idx = torch.arange(B, dtype=torch.int64, device=dev)
             names = ("state", "new_state", "action", "reward", "terminal")
             self._rows_ring = _native.FlockScRows(**{n: _p(rb[n]) for n in names})
+            if self.distributed:
+                # data-parallel rounds: the critic gradient and the round's actor gradient in ONE contiguous bucket
+                # (FlockScUpdate.critic_grad / actor_grad_out), all-reduced as one collective per env step
+                ct = C.numel
+                self.dp_actor_off = -(-ct // 64) * 64
+                self.dp_bucket = torch.zeros(self.dp_actor_off + A.per_agent, device=dev)
             for i in range(self.n_slots):
                 stg = {"state": torch.zeros(B, n_in, device=dev), "new_state": torch.zeros(B, n_in, device=dev),
                        "action": torch.zeros(B, na, device=dev), "reward": torch.zeros(B, device=dev),
@@ -183,6 +191,12 @@ class SharedCriticLearner:
                                         rows=_native.FlockScRows(**{n: _p(stg[n]) for n in names}),
                                         sc=_native.FlockScUpdate(**f, critic_view=_p(self.critic_views[i])),
                                         sc_grads=_native.FlockScUpdate(**dict(f, do_adam=0, update_rate=0))))
+                if self.distributed:
+                    bucket = dict(f, critic_grad=_p(self.dp_bucket), critic_view=_p(self.critic_views[i]),
+                                  actor_grad_out=_p(self.dp_bucket[self.dp_actor_off:]))
+                    self._slots[-1]["dp_grads"] = _native.FlockScUpdate(**dict(bucket, do_adam=0))
+                    self._slots[-1]["dp_adam"] = _native.FlockScUpdate(**bucket)
+            self._dp_pending = None
             self.staging = self._slots[0]["staging"]
 
     def _fused_update(self, u=None):
@@ -502,6 +516,47 @@ class SharedCriticLearner:
             except Exception:  # noqa: BLE001 - interpreter shutdown
                 pass
 
+    # ------------------------------------------------------------------ data-parallel rounds (bench, N > 1)
+    def _dp_round(self, c, a):
+        """One data-parallel round on the current stream: critic phase of slot c and / or actor phase of slot a
+        (None: absent) as gradients (flock_sc_round, do_adam = 0), ONE all-reduce (sum) of the bucket part they
+        wrote, then flock_sc_round_adam with grad_scale = 1 / world."""
+        lib = _native.lib()
+        st = _stream(self.device)
+        S = self._slots
+        byref = lambda i, k: ctypes.byref(S[i][k]) if i is not None else None  # noqa: E731
+        _native.check(lib.flock_sc_round(st, byref(c, "dp_grads"), byref(a, "dp_grads")), "flock_sc_round",
+                      learn=True)
+        lo = 0 if c is not None else self.dp_actor_off
+        hi = self.dp_bucket.numel() if a is not None else self.critic.numel
+        dist.allreduce_sum_(self.dp_bucket[lo:hi], self.group)
+        _native.check(lib.flock_sc_round_adam(st, byref(c, "dp_adam"), byref(a, "dp_adam"), _p(self.inv_world)),
+                      "flock_sc_round_adam", learn=True)
+
+    def dp_learn(self, slot, agent, slot_free):
+        """learn() of ``agent`` on the rows snapshot_into(slot, agent) copied, data-parallel, enqueued on the current
+        (learner) stream: its critic phase in one round with the previous learn's pending actor phase (the same
+        agent twice: one after the other). slot_free[i] is recorded once slot i's actor phase is enqueued."""
+        q = self._dp_pending
+        if q is not None and q[1] != agent:
+            self._dp_round(slot, q[0])
+            slot_free[q[0]].record()
+        else:
+            if q is not None:
+                self._dp_round(None, q[0])
+                slot_free[q[0]].record()
+            self._dp_round(slot, None)
+        self._dp_pending = (slot, agent)
+        return self._finish_learn(agent, soft_in_kernel=True)
+
+    def dp_flush(self, slot_free):
+        """Enqueue the pending actor phase of the last dp_learn (no-op when none)."""
+        q = self._dp_pending
+        if q is not None:
+            self._dp_round(None, q[0])
+            slot_free[q[0]].record()
+            self._dp_pending = None
+
     def update_slot(self, slot, agent):
         """The rest of learn() on the rows snapshot_into(slot, agent) copied, enqueued on the current stream."""
         self._run_fused(agent, slot)
@@ -561,9 +616,12 @@ class SharedCriticBench:
             self.actor_stream = torch.cuda.Stream(device=device, priority=prio) if self.pipelined else None
             self.critic_done = [torch.cuda.Event(), torch.cuda.Event()]
             self._handles = None
-            self.snap_done = [torch.cuda.Event(), torch.cuda.Event()]
+            ns = self.learner.n_slots
+            self.snap_done = [torch.cuda.Event() for _ in range(ns)]
             self.learn_done = [torch.cuda.Event(), torch.cuda.Event()]
-            self._used = [False, False]
+            self.slot_free = [torch.cuda.Event() for _ in range(ns)]
+            self._used = [False] * ns
+            self._dp_slot = 0
             self._prev_agent = None
         self.prev_obs = env.dnn.clone()
         self.prev_act = None
@@ -574,7 +632,8 @@ class SharedCriticBench:
                 f"agent = step mod "
                 f"{self.learner.n_agents}; all {self.env.E * self.env.N} transitions inserted into a 1e6-row "
                 f"device replay ring per step by the env kernel itself"
-                + ("; critic + actor gradient all-reduce over RCCL per learn)" if self.learner.distributed else ")"))
+                + ("; one [critic | actor] gradient all-reduce over RCCL per learn)" if self.learner.distributed
+                   else ")"))
 
     # bench.py hook interface: before(s) -> ring for the fused env step; after(s, a) -> learn(); prime()
     def before(self, s):
@@ -598,6 +657,21 @@ class SharedCriticBench:
             L.pipeline_learn(agent, *self._handles)
             return
         main = torch.cuda.current_stream(L.device)
+        if L.distributed:
+            # data-parallel: snapshot on the env stream, then one round of gradients, ONE all-reduce of the
+            # [critic | actor] bucket and the Adam launch on the learner stream (SharedCriticLearner.dp_learn)
+            slot = self._dp_slot
+            if self._used[slot]:
+                main.wait_event(self.slot_free[slot])
+            if not L.snapshot_into(slot, agent):
+                return
+            self.snap_done[slot].record(main)
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(self.snap_done[slot])
+                L.dp_learn(slot, agent, self.slot_free)
+            self._used[slot] = True
+            self._dp_slot = (slot + 1) % L.n_slots
+            return
         slot = s & 1
         if self._used[slot]:
             main.wait_event(self.learn_done[slot])
@@ -626,6 +700,9 @@ class SharedCriticBench:
         if self.overlap:
             if self._handles is not None:
                 self.learner.pipeline_flush(self._handles[1])
+            if self.learner.distributed:
+                with torch.cuda.stream(self.stream):
+                    self.learner.dp_flush(self.slot_free)
             cur = torch.cuda.current_stream(self.learner.device)
             cur.wait_stream(self.stream)
             if self.actor_stream is not None:
