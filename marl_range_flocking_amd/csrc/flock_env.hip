@@ -419,7 +419,7 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
     for (int u = 0; u < kRows; ++u) {
         const int q = qlo + u;
         P[u] = tot;
-        b[u] = 0;
+        b[u] = cmax;  // an unused (trailing) row: its slots land on the sentinel, never on entries scanned before
         if (q <= qhi) {
             const int yy = cy + q;
             const float ylo = (float)yy * cwy;
@@ -444,6 +444,10 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
         atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 22], 1ull);
     }
 #endif
+    // Slots past the lane's total are not masked. With a trailing unused row they land on the +inf sentinel at cmax
+    // (the entry count); after a lane's third row they read the entries that follow its last range (agents of the
+    // env outside its disk and never scanned before, whose computed d2 is at least their true periodic d2, so their
+    // keys lie above the (k+1)-th and its bucket: the top k+1 and the ambiguity test are unchanged).
     auto cand_index = [&](int tt, int& c0, int& c1) {
         c0 = tt + b[0];
         c1 = tt + 1 + b[0];
@@ -461,10 +465,8 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
         cand_index(t, c0, c1);
         const float4 q0 = ext[c0], q1 = ext[c1];
         const f32x2 d = cand_d2x2<PERIODIC>(xi, yi, box, q0, q1);
-        const uint32_t k0 = (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z);
-        const uint32_t k1 = (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z);
-        key_insert<L>(key, t < tot ? k0 : kEmpty);
-        key_insert<L>(key, t + 1 < tot ? k1 : kEmpty);
+        key_insert<L>(key, (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z));
+        key_insert<L>(key, (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z));
     }
 }
 
@@ -993,6 +995,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             if (PERIODIC && cx >= gx - kRg) ext[pr[cx - gx + kRg] + rank] = ghost;  // in front (gx >= 2 kRg)
             if (PERIODIC && cx < kRg) ext[pr[gx + kRg + cx] + rank] = ghost;        // behind
         }
+        // a sentinel behind the last entry (the seeded scan's clamp target): +inf position, d2 = +inf, a key above
+        // every real one
+        if (in_group && i == 0)
+            ext[pre[npre - 1]] = make_float4(__builtin_inff(), __builtin_inff(), __int_as_float(0), 0.0f);
         __syncthreads();
     }
 
@@ -1055,7 +1061,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #else
         scan_seeded<L, PERIODIC>(key, ext, pre, gx, gy, cy, use, r, p.ib, x, y, p.box, p.cwy, p.inv_cwx, p.inv_cwy,
-                                 cmax);
+                                 pre[npre - 1]);
 #endif
         ok = use;
         R = 1;  // rows of the exact rescan
