@@ -207,16 +207,15 @@ class VDNBench:
 
     def describe(self):
         return (f"VDN train() every {self.every} vectorized steps (update_iter 10, B 32, chunk 10); all "
-                f"{self.env.E} team transitions per step inserted into a 50k-row device replay ring"
-                + ("; gradient all-reduce over RCCL" if self.learner.distributed else ""))
+                f"{self.env.E} team transitions per step inserted into a 50k-row device replay ring by the env "
+                f"kernel itself" + ("; gradient all-reduce over RCCL" if self.learner.distributed else ""))
 
     def before(self, s):
-        self.prev = self.env.dnn
-        return None
+        # the env kernel writes every env's team transition itself (memory.put, train_flock.py:102: previous obs,
+        # action ids, rewards, new obs, any_done; FlockRing action_ids / env_done)
+        return self.learner.replay_slots(self.env.E)
 
     def after(self, s, a):
-        env = self.env
-        self.learner.put(self.prev, a, env.reward, env.dnn, env.any_done)
         if (s + 1) % self.every == 0 and self.learner.size() > self.learner.chunk:
             self.learner.train()
 

@@ -93,6 +93,8 @@ typedef struct FlockRing {
     float* actor_new_state;
     int64_t group;
     int store_done;
+    int action_ids; /* 1: action is the uw_discrete step's action id per agent, stored as f32 ([rows][group]) */
+    int env_done;   /* 1 (group = N): terminal is one flag per env row, the env's any_done (the VDN team done) */
 } FlockRing;
 int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
                         float dt, float v_min, float v_max, int periodic, int rigid_boundary,
@@ -101,7 +103,8 @@ int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sens
                         const FlockRing* ring);
 
 /* Optional extras of the *_ext entry points (each equals its plain entry point when ext is NULL or all-NULL):
- *  ring  (v2 only; may be NULL): the fused replay insert of flock_step_v2_store;
+ *  ring  (v2 and uw_discrete; may be NULL): the fused replay insert of flock_step_v2_store (uw_discrete: the VDN
+ *        team transition of learners/vdn/train_flock.py:102, with action_ids = 1 and env_done = 1);
  *  seeds (may be NULL): [E][N][k] u16 (rw), a compact side buffer of kNN search seeds. When set, the N >= 128
  *        cell-list kNN reads its seeds here instead of from nn_idx on entry (2 B instead of 8 B per seed) and
  *        writes this step's neighbour indices back for the next step. Any content is valid (out-of-range or repeated

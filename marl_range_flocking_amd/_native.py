@@ -91,7 +91,7 @@ class FlockRing(ctypes.Structure):
     _fields_ = ([(n, _c_void_p) for n in ("state", "action", "reward", "new_state", "terminal", "prev_obs")]
                 + [("capacity", ctypes.c_int64), ("start", ctypes.c_int64), ("skip", ctypes.c_int64)]
                 + [("actor_state", _c_void_p), ("actor_new_state", _c_void_p), ("group", ctypes.c_int64),
-                   ("store_done", _c_int)])
+                   ("store_done", _c_int), ("action_ids", _c_int), ("env_done", _c_int)])
 
 
 class FlockStepExt(ctypes.Structure):

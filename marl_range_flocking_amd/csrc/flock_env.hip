@@ -92,6 +92,7 @@ struct Params {
     const float* r_prev;
     int64_t r_cap, r_start, r_skip;
     int r_group, r_done;  // agents per ring row (1 or N); stored flag: 0 -> 1 - done, 1 -> done
+    int r_ids, r_env_done;  // action stored as the f32 action id; terminal one flag per env row (any_done)
     uint16_t* seeds;      // [E][N][k] compact kNN search seeds (rw), or NULL: nn_idx on entry is the hint
     // cell list (step variants, N >= 128)
     int cells, gx, gy, ecap;  // cells != 0: cell list on a gx x gy grid; extended-array capacity per env (2N + 2)
@@ -651,6 +652,15 @@ __device__ __forceinline__ void knn_scan(const float2* __restrict__ cand, int N,
     knn_finalize<L, PERIODIC>(key, cand, N, k, ib, xi, yi, box, bd, bj);
 }
 
+// fused replay insert with one terminal flag per env row (FlockRing.env_done): the env's any_done at its ring row
+__device__ __forceinline__ void env_done_row(const Params& p, int env, int flag) {
+    if (p.r_state && p.r_env_done && env >= p.r_skip) {
+        int64_t row = p.r_start + env - p.r_skip;
+        if (row >= p.r_cap) row -= p.r_cap;
+        p.r_term[row] = (flag != 0) == (p.r_done != 0) ? 1.0f : 0.0f;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // the fused step kernel
 
@@ -728,7 +738,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
-    float2 act_in = make_float2(0.0f, 0.0f);
+    float2 act_in = make_float2(0.0f, 0.0f);  // fused replay insert: the raw action (v2) or the f32 action id
     float prev_obs[L - 2];  // fused replay insert: the previous observation row, loaded early (latency hidden)
 #pragma unroll
     for (int s = 0; s < L - 2; ++s) prev_obs[s] = 0.0f;
@@ -851,6 +861,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             reinterpret_cast<float2*>(p.vel)[a] = make_float2(vx, vy);
         } else if (variant == FLOCK_VARIANT_UW_DISCRETE) {  // gym_flock_uw_discrete.py:324-366
             int64_t id = p.action_id[a];
+            act_in.x = (float)id;  // memory.put stores the action ids as floats (vdn/train_flock.py:99-102)
             if (id < 0 || id >= p.n_actions) {  // the reference raises KeyError (:329)
                 if (p.status) atomicOr(p.status, 1);
                 id = 0;
@@ -1219,9 +1230,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                             if (p.r_anew) p.r_anew[e * p.k + s] = dv[s];
                         }
                 }
-                stnt(reinterpret_cast<f32x2*>(p.r_action) + e, f32x2{act_in.x, act_in.y});
+                if (p.r_ids)
+                    stnt(p.r_action + e, act_in.x);
+                else
+                    stnt(reinterpret_cast<f32x2*>(p.r_action) + e, f32x2{act_in.x, act_in.y});
                 stnt(p.r_reward + e, r);
-                stnt(p.r_term + e, (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f);
+                if (!p.r_env_done) stnt(p.r_term + e, (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f);
             }
         }
     }
@@ -1236,14 +1250,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             if ((t & 63) == 0 && na) {
                 if (coll_w) __hip_atomic_fetch_or(&flags[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 const int old = __hip_atomic_fetch_add(&flags[1], na, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (old + na == p.N)
-                    p.any_done[env] =
-                        (uint8_t)__hip_atomic_load(&flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old + na == p.N) {
+                    const int f = __hip_atomic_load(&flags[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    p.any_done[env] = (uint8_t)f;
+                    env_done_row(p, env, f);
+                }
             }
         } else {
             if (active && coll) atomicOr(&flags[g], 1);
             __syncthreads();
-            if (active && i == 0) p.any_done[env] = (uint8_t)flags[g];
+            if (active && i == 0) {
+                p.any_done[env] = (uint8_t)flags[g];
+                env_done_row(p, env, flags[g]);
+            }
         }
     }
     PHASE(7);
@@ -1614,6 +1633,41 @@ const char* flock_last_error(void) { return g_err; }
 namespace {
 
 // ring (may be NULL): the fused replay insert; seeds (may be NULL): compact kNN search seeds
+// the fused replay insert's targets (FlockRing) into the launch parameters, checked
+int set_ring(Params& p, const FlockRing* ring, int E, int N, const char* who) {
+    if (!ring) return FLOCK_OK;
+    static thread_local char msg[160];
+    auto bad = [&](int code, const char* what) {
+        snprintf(msg, sizeof(msg), "%s: %s", who, what);
+        return fail(code, msg);
+    };
+    if (E && (!ring->state || !ring->action || !ring->reward || !ring->new_state || !ring->terminal ||
+              !ring->prev_obs))
+        return bad(FLOCK_E_NULL, "NULL ring pointer");
+    if (ring->group != 1 && ring->group != N)
+        return bad(FLOCK_E_ARG, "ring group must be 1 (a row per agent) or N (a row per env)");
+    if (ring->env_done && ring->group != N) return bad(FLOCK_E_ARG, "env_done needs group = N (a row per env)");
+    const int64_t units = ring->group == 1 ? (int64_t)E * N : (int64_t)E;
+    if (ring->skip < 0 || units - ring->skip > ring->capacity || ring->start < 0 || ring->start >= ring->capacity)
+        return bad(FLOCK_E_ARG, "need skip >= 0, rows - skip <= capacity, 0 <= start < capacity");
+    p.r_state = ring->state;
+    p.r_action = ring->action;
+    p.r_reward = ring->reward;
+    p.r_new = ring->new_state;
+    p.r_term = ring->terminal;
+    p.r_prev = ring->prev_obs;
+    p.r_cap = ring->capacity;
+    p.r_start = ring->start;
+    p.r_skip = ring->skip;
+    p.r_astate = ring->actor_state;
+    p.r_anew = ring->actor_new_state;
+    p.r_group = (int)ring->group;
+    p.r_done = ring->store_done;
+    p.r_ids = ring->action_ids != 0;
+    p.r_env_done = ring->env_done != 0;
+    return FLOCK_OK;
+}
+
 int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance, float dt,
                  float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
@@ -1623,32 +1677,7 @@ int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_rang
     if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done))
         return fail(FLOCK_E_NULL, "flock_step_v2: NULL pointer");
     Params p = base(E, N, k, box);
-    if (ring) {
-        if (E && (!ring->state || !ring->action || !ring->reward || !ring->new_state || !ring->terminal ||
-                  !ring->prev_obs))
-            return fail(FLOCK_E_NULL, "flock_step_v2_store: NULL ring pointer");
-        if (ring->group != 1 && ring->group != N)
-            return fail(FLOCK_E_ARG,
-                        "flock_step_v2_store: ring group must be 1 (a row per agent) or N (a row per env)");
-        const int64_t units = ring->group == 1 ? (int64_t)E * N : (int64_t)E;
-        if (ring->skip < 0 || units - ring->skip > ring->capacity || ring->start < 0 ||
-            ring->start >= ring->capacity)
-            return fail(FLOCK_E_ARG,
-                        "flock_step_v2_store: need skip >= 0, rows - skip <= capacity, 0 <= start < capacity");
-        p.r_state = ring->state;
-        p.r_action = ring->action;
-        p.r_reward = ring->reward;
-        p.r_new = ring->new_state;
-        p.r_term = ring->terminal;
-        p.r_prev = ring->prev_obs;
-        p.r_cap = ring->capacity;
-        p.r_start = ring->start;
-        p.r_skip = ring->skip;
-        p.r_astate = ring->actor_state;
-        p.r_anew = ring->actor_new_state;
-        p.r_group = (int)ring->group;
-        p.r_done = ring->store_done;
-    }
+    if ((rc = set_ring(p, ring, E, N, "flock_step_v2_store"))) return rc;
     p.variant = FLOCK_VARIANT_V2;
     p.periodic = periodic != 0;
     p.rigid = rigid_boundary != 0;
@@ -1750,7 +1779,6 @@ int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, flo
                                float noise_std, uint64_t seed, uint64_t rng_offset, const float* table,
                                int n_actions, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
                                uint8_t* any_done, int* status, const FlockStepExt* ext) {
-    if (ext && ext->ring) return fail(FLOCK_E_ARG, "flock_step_uw_discrete_ext: the fused replay insert is v2 only");
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !prev_heading || !action_id || !table || !vel || !dnn || !reward || !done ||
@@ -1758,6 +1786,9 @@ int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, flo
         return fail(FLOCK_E_NULL, "flock_step_uw_discrete: NULL pointer");
     if (n_actions < 1) return fail(FLOCK_E_ARG, "n_actions must be >= 1");
     Params p = base(E, N, k, box);
+    if ((rc = set_ring(p, ext ? ext->ring : nullptr, E, N, "flock_step_uw_discrete_ext"))) return rc;
+    if (p.r_state && !p.r_ids)
+        return fail(FLOCK_E_ARG, "flock_step_uw_discrete_ext: the ring stores action ids (action_ids = 1)");
     p.variant = FLOCK_VARIANT_UW_DISCRETE;
     p.rigid = rigid_boundary != 0;
     p.sensor_range = sensor_range;

@@ -403,14 +403,16 @@ class ReplayRing:
         self.counter += n
 
     def step_slots(self, n, state, action, reward, new_state, terminal, actor_state=None, actor_new_state=None,
-                   group=1, store_done=False):
+                   group=1, store_done=False, action_ids=False, env_done=False):
         """Reserve the next n rows for an env step that writes them itself (VecFlockEnv.step(ring=...) ->
         flock_step_v2_store) and return the kernel's FlockRing: same rows and counter as store() (when n exceeds
         the capacity only the last `capacity` rows are kept). Field names map the kernel's targets to this ring's
-        fields; group = agents per row (1, or N for one row per env); store_done: store done (else 1 - done)."""
+        fields; group = agents per row (1, or N for one row per env); store_done: store done (else 1 - done);
+        action_ids: the step's action ids stored as f32 (uw_discrete); env_done: one terminal flag per env row."""
         skip = max(0, n - self.capacity)
         # one FlockRing object per field mapping, updated in place: the env step's launch plan keeps a pointer to it
-        key = (state, action, reward, new_state, terminal, actor_state, actor_new_state, group, bool(store_done))
+        key = (state, action, reward, new_state, terminal, actor_state, actor_new_state, group, bool(store_done),
+               bool(action_ids), bool(env_done))
         rings = self.__dict__.setdefault("_rings", {})
         ring = rings.get(key)
         if ring is None:
@@ -420,7 +422,7 @@ class ReplayRing:
                 state=ptr(state), action=ptr(action), reward=ptr(reward), new_state=ptr(new_state),
                 terminal=ptr(terminal), prev_obs=None, capacity=self.capacity, start=0, skip=0,
                 actor_state=ptr(actor_state), actor_new_state=ptr(actor_new_state), group=group,
-                store_done=int(bool(store_done)))
+                store_done=int(bool(store_done)), action_ids=int(bool(action_ids)), env_done=int(bool(env_done)))
         ring.start = (self.counter + skip) % self.capacity
         ring.skip = skip
         self.counter += n

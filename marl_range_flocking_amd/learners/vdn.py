@@ -186,6 +186,13 @@ class VDNLearner:
                            "s_prime": torch.as_tensor(s_prime, device=self.device).float(),
                            "done": torch.as_tensor(done, device=self.device).reshape(n)})
 
+    def replay_slots(self, n_envs):
+        """Reserve the next n_envs rows for a uw_discrete env step that writes its team transitions itself
+        (VecFlockEnv.step(ring=...)): the row memory.put((s, a, r, s', [all_done])) of every env
+        (train_flock.py:102): previous obs, action ids as f32, rewards, new obs, the env's any_done."""
+        return self.replay.step_slots(n_envs, "s", "a", "r", "s_prime", "done", group=self.A, store_done=True,
+                                      action_ids=True, env_done=True)
+
     def size(self):
         return len(self.replay)
 

@@ -176,10 +176,14 @@ def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_id
 
 def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                      status=None, *, k, box, sensor_range, collision_distance, dt=0.1, v_max=2.5, rigid_boundary=False,
-                     noise_std=0.1, seed=0, rng_offset=0, seeds=None, plan=None):
+                     noise_std=0.1, seed=0, rng_offset=0, seeds=None, plan=None, ring=None):
     """gym_flock_uw_discrete.MultiAgentEnv.step (gym_flock_uw_discrete.py:110-122). noise=None → in-kernel
     Philox N(0, noise_std) draws; otherwise noise [E,N,2] is added to the action-table means (parity mode).
-    plan (StepPlan, optional; in-kernel noise only): record / replay the validated launch over the same buffers."""
+    plan (StepPlan, optional; in-kernel noise only): record / replay the validated launch over the same buffers.
+    ring (a _native.FlockRing with action_ids / env_done, VDNLearner.replay_slots): also write every env's team
+    transition into the VDN replay ring in the same launch (memory.put, learners/vdn/train_flock.py:102)."""
+    if plan is not None and plan.ring is not ring:
+        plan.fn = None  # recorded for another ring (or none): record again
     if noise is None and _planned(plan, pos, action_id, "action_id", torch.int64, tuple(pos.shape[:2]), dt,
                                   rng_offset):
         return
@@ -206,10 +210,12 @@ def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, d
             _ptr(noise), float(noise_std), int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(table),
             int(table.shape[0]), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done),
             _ptr(status))
-    ext = _ext(None, seeds, E, N, k, dev)
+    ext = _ext(ring, seeds, E, N, k, dev)
     L = _native.lib()
     _record(plan if noise is None else None, L.flock_step_uw_discrete if ext is None else L.flock_step_uw_discrete_ext,
             "flock_step_uw_discrete" if ext is None else "flock_step_uw_discrete_ext", args, ext, 13, 7, 17)
+    if plan is not None and noise is None:
+        plan.ring = ring  # a strong reference: the recorded ext points into it
 
 
 def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, *, k, box, collision_distance,

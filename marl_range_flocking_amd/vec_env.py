@@ -249,8 +249,8 @@ class VecFlockEnv:
         common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
                       rigid_boundary=c.rigid_boundary, plan=plan)
         if ring is not None:
-            if c.variant != "v2":
-                raise NotImplementedError("the fused replay insert is built for the v2 step")
+            if c.variant not in ("v2", "uw_discrete"):
+                raise NotImplementedError("the fused replay insert is built for the v2 and uw_discrete steps")
             ring.prev_obs = src["dnn"].data_ptr()
         T = self._torch_ops if ring is None else None
         if T is not None:
@@ -269,7 +269,7 @@ class VecFlockEnv:
             ops.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
                                  self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
                                  self.status, sensor_range=c.sensor_range, v_max=c.max_linear_velocity,
-                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, **common)
+                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, ring=ring, **common)
             self._rng_offset += 1
         else:
             ops.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],

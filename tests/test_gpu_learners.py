@@ -385,3 +385,39 @@ def test_fused_env_replay_insert_matches_store_transitions(cap, cuda):
     assert learners[0].replay.counter == learners[1].replay.counter == 3 * E * N
     for name in learners[0].replay.bufs:
         assert torch.equal(learners[0].replay.bufs[name], learners[1].replay.bufs[name]), name
+
+
+@pytest.mark.parametrize("N,cap", [(16, 100), (128, 40), (128, 25)], ids=["N16-wrap", "N128-wrap", "N128-larger"])
+def test_fused_vdn_team_insert_matches_put(N, cap, cuda):
+    """The VDN team transition (memory.put((s, a, r, s', [all_done])), learners/vdn/train_flock.py:102): a
+    uw_discrete VecFlockEnv.step(ids, ring=vdn.replay_slots(E)) writes previous obs, action ids as f32, rewards,
+    new obs and the env's any_done from the step kernel; every replay field and the counter equal step() followed by
+    put(prev, ids, reward, obs, any_done) bit for bit, across a ring wrap and with a step larger than the ring."""
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+    from marl_range_flocking_amd.learners.vdn import VDNLearner
+
+    E, k = 32, 4
+    box = float(round(np.sqrt(250.0 * N)))
+    envs, learners = [], []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant="uw_discrete", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0), device=cuda)
+        g = torch.Generator(device=cuda).manual_seed(5)
+        env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
+        env.headings.copy_(torch.rand(E, N, device=cuda, generator=g) * 2.6)
+        env.step(torch.zeros(E, N, dtype=torch.int64, device=cuda))
+        envs.append(env)
+        learners.append(VDNLearner(N, k, 10, batch_size=4, chunk_size=2, buffer_limit=cap, device=cuda,
+                                   use_graph=False))
+    g = torch.Generator(device=cuda).manual_seed(9)
+    for _ in range(3):
+        ids = torch.randint(0, 10, (E, N), device=cuda, generator=g)
+        fused_env, plain_env = envs
+        fused_env.step(ids, ring=learners[0].replay_slots(E))
+        prev = plain_env.dnn.clone()
+        plain_env.step(ids)
+        learners[1].put(prev, ids, plain_env.reward, plain_env.dnn, plain_env.any_done)
+        assert torch.equal(fused_env.dnn, plain_env.dnn) and torch.equal(fused_env.any_done, plain_env.any_done)
+    assert learners[0].replay.counter == learners[1].replay.counter == 3 * E
+    for name in learners[0].replay.bufs:
+        assert torch.equal(learners[0].replay.bufs[name], learners[1].replay.bufs[name]), name
