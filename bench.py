@@ -37,10 +37,11 @@ import torch
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 VALU_PEAK_LANEOPS = 39.3e12      # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz: non-packed f32 lane-ops/s (packed: 78.6e12)
 BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
-# fused replay insert (flock_step_v2_store), per agent-step: + previous obs read (k=4 floats) + the ring fields
-# written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG record: state,
-# next_state, actor_state, actor_next_state 16 each + action 8 + reward 4 + done 4
-RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80}
+# fused replay insert (flock_step_v2_store / the uw_discrete ring), per agent-step: + previous obs read (k=4 floats)
+# + the ring fields written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG
+# record: state, next_state, actor_state, actor_next_state 16 each + action 8 + reward 4 + done 4; VDN team
+# transition: s 16 + a (f32 id) 4 + r 4 + s' 16 (+ one done flag per env: 4 / N)
+RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80, "vdn": 16 + 40}
 EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 4))  # steps between HIP-event-timed env launches (timed region)
 
 

@@ -1456,12 +1456,14 @@ int check_common(int E, int N, int k) {
 struct Knobs {
     int env_launches;
     bool no_spec, no_split, no_cells;
+    int lds_pad;  // FLOCK_ENV_LDS_PAD: extra dynamic LDS bytes per step block (caps the blocks per CU; A/B only)
 };
 Knobs& knobs_mut() {
     static Knobs k = [] {
         const char* e = getenv("FLOCK_ENV_LAUNCHES");
+        const char* lp = getenv("FLOCK_ENV_LDS_PAD");
         return Knobs{e ? atoi(e) : 1, getenv("FLOCK_NO_SPEC") != nullptr, getenv("FLOCK_NO_SPLIT") != nullptr,
-                     getenv("FLOCK_NO_CELLS") != nullptr};
+                     getenv("FLOCK_NO_CELLS") != nullptr, lp ? atoi(lp) : 0};
     }();
     return k;
 }
@@ -1479,6 +1481,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
     if (knobs().no_spec) return false;  // A/B diagnostics: the generic instantiation
     Cfg c = c0;
+    c.lds += (size_t)knobs().lds_pad;
     if (SPL > 1) {  // one env per block of SPL * NC lanes; LDS: the G = 1 layout + the merge lists in place of ext
         if (knobs().no_split) return false;
         c = make_cfg(p.E, NC, false, 0, 0, 0, 1);

@@ -227,12 +227,21 @@ __device__ __forceinline__ void load_row(float (&v)[C], const float* p, int F, i
         v[c] = j < F ? p[j] : 0.0f;
     }
 }
+// stores of the kernels' per-row outputs (read by the next launch of the round); -DFLOCK_SC_NT (diagnostics A/B)
+// makes them non-temporal
+__device__ __forceinline__ void st_out(float* p, float v) {
+#ifdef FLOCK_SC_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 template <int C>
 __device__ __forceinline__ void store_row(float* p, const float (&v)[C], int F, int lane) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int j = lane + 64 * c;
-        if (j < F) p[j] = v[c];
+        if (j < F) st_out(p + j, v[c]);
     }
 }
 
@@ -877,7 +886,7 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-        if (m < g.M && n < g.N) g.C[(int64_t)m * g.ldc + n] = g.bias ? out[q] + bias : out[q];
+        if (m < g.M && n < g.N) st_out(g.C + (int64_t)m * g.ldc + n, g.bias ? out[q] + bias : out[q]);
     }
 }
 
@@ -1024,8 +1033,8 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
             const float dy = hv[q] > 0.0f ? out[q] : 0.0f;  // through the ReLU
             const float dxh = dy * gam;
             if (ok) {
-                j.DY1[(int64_t)m * j.F + n] = dy;
-                j.DXH1[(int64_t)m * j.F + n] = dxh;
+                st_out(j.DY1 + (int64_t)m * j.F + n, dy);
+                st_out(j.DXH1 + (int64_t)m * j.F + n, dxh);
             }
             s1[q] = ok ? dxh : 0.0f;
             s2[q] = ok ? dxh * xv[q] : 0.0f;

@@ -11,11 +11,13 @@ pass() {  # config tag alg
   done
   python tools/pmc_traffic.py $OUT/${tag}_FETCH_SIZE $OUT/${tag}_WRITE_SIZE --kernel step_kernel --algorithmic-bytes $alg --out $OUT/pmc_$tag.json
 }
-for c in ${CONFIGS:-2 4 5}; do
+# algorithmic bytes per launch: (SURVEY 8(d) bytes + the fused insert's bytes) x agents per launch
+for c in ${CONFIGS:-3 2 4 5}; do
   case $c in
-    2) pass 2 uw_N64_E1024 9764864 ;;
-    4) pass 4 uw_discrete_N512_E1024 36175872 ;;
-    5) pass 5 v2_ring_N1024_E2048 396361728 ;;
+    3) pass 3 v2_ring_N256_E4096 $(( (93 + 64) * 256 * 4096 )) ;;
+    2) pass 2 uw_N64_E1024 $(( 149 * 64 * 1024 )) ;;
+    4) pass 4 uw_discrete_ring_N512_E8192 $(( (69 + 56) * 512 * 8192 )) ;;
+    5) pass 5 v2_ring_N1024_E16384 $(( (93 + 96) * 1024 * 16384 )) ;;
   esac
 done
 echo ALLDONE
