@@ -27,7 +27,7 @@ if [[ $PHASES == *pmc* ]]; then
     step pmc_sq_$t.log 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM -d $OUT/pmc_sq_$t -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3
     python tools/pmc_sq_json.py $OUT/pmc_sq_$t --kernel step_kernel --out $OUT/pmc_sq_$t.json
   done
-  mkdir -p profiles_new; cp $OUT/pmc_*.json profiles_new/ 2>/dev/null
+  cp $OUT/pmc_*.json profiles/  # the bench lines below read them (copy them into the repo afterwards)
 fi
 if [[ $PHASES == *bench* ]]; then
   for c in ${CONFIGS:-3 2 4 5}; do
