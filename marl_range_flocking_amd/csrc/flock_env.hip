@@ -1595,6 +1595,8 @@ Params base(int E, int N, int k, float box) {
 // ---------------------------------------------------------------------------------------------------------------
 // C ABI
 
+void flock_sc_diag_no_spec(bool v);  // flock_sc.hip
+
 extern "C" {
 
 int flock_abi_version(void) { return FLOCK_ABI_VERSION; }
@@ -1610,6 +1612,8 @@ int flock_set_diag(const char* name, int value) {
         k.no_split = value != 0;
     else if (!strcmp(name, "no_cells"))
         k.no_cells = value != 0;
+    else if (!strcmp(name, "sc_no_spec"))
+        flock_sc_diag_no_spec(value != 0);
     else
         return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
     return FLOCK_OK;

@@ -311,8 +311,9 @@ __device__ __forceinline__ void ln_backward(const float (&dy)[C], const float (&
 
 // ---------------------------------------------------------------------------------------------------------------
 // c1 (grid.y = path): 0 target actor on s', 1 critic on s', 2 critic on s (+ the gathered minibatch rows)
-template <int C>
+template <int C, int HC>
 __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, int path) {
+    const int H1 = HC ? HC : a.H1;
     extern __shared__ float4 smem4[];
     float* xs = reinterpret_cast<float*>(smem4);  // [4 rows][kMaxIn] inputs, then the fc1 image
     float* sp = xs + kRowsPerBlock * kMaxIn;
@@ -336,29 +337,29 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
             }
         }
     }
-    stage(sp, net, a.H1 * (a.in + 3));
+    stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
     if (!live) return;
     float xh[C], h[C], rs;
-    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, a.H1, lane, xh, h, rs);
-    const int64_t ro = (int64_t)r * a.H1;
+    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
+    const int64_t ro = (int64_t)r * H1;
     if (path == 0) {
-        store_row<C>(w.TH1 + ro, h, a.H1, lane);
+        store_row<C>(w.TH1 + ro, h, H1, lane);
     } else if (path == 1) {
-        store_row<C>(w.NH1 + ro, h, a.H1, lane);
+        store_row<C>(w.NH1 + ro, h, H1, lane);
     } else {
-        store_row<C>(w.XH1 + ro, xh, a.H1, lane);
-        store_row<C>(w.H1 + ro, h, a.H1, lane);
+        store_row<C>(w.XH1 + ro, xh, H1, lane);
+        store_row<C>(w.H1 + ro, h, H1, lane);
         if (lane == 0) w.RS1[r] = rs;
     }
 }
 
 // c3: heads, TD target, MSE and the critic backward down to the fc2 pre-activation
-template <int C>
+template <int C, int HC, int NAC>
 __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);  // critic tail
-    const int H2 = a.H2, na = a.na;
+    const int H2 = HC ? HC : a.H2, na = NAC ? NAC : a.na;
     float* at = ct + round4(crit_tail_len(na, H2));  // target actor tail
     const int lane = threadIdx.x & 63;
     const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
@@ -468,8 +469,9 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
 
 // c5 / a5: ReLU + LN1 backward: dy = dh * [h > 0]; dz = LN backward(dy)
 // a1 (grid.y = path): 0 the agent's actor fc1/LN/ReLU on s (saved for backward), 1 the updated critic's on s
-template <int C>
+template <int C, int HC>
 __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, int path) {
+    const int H1 = HC ? HC : a.H1;
     extern __shared__ float4 smem4[];
     float* xs = reinterpret_cast<float*>(smem4);
     float* sp = xs + kRowsPerBlock * kMaxIn;
@@ -478,28 +480,28 @@ __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, i
     const bool live = r < a.B;
     const float* net = path == 0 ? a.actors + (*a.agent) * a.stride : a.critic;
     if (live && lane < a.in) xs[wv * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
-    stage(sp, net, a.H1 * (a.in + 3));
+    stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
     if (!live) return;
     float xh[C], h[C], rs;
-    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, a.H1, lane, xh, h, rs);
-    const int64_t ro = (int64_t)r * a.H1;
+    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
+    const int64_t ro = (int64_t)r * H1;
     if (path == 0) {
-        store_row<C>(w.AXH1 + ro, xh, a.H1, lane);
-        store_row<C>(w.AH1 + ro, h, a.H1, lane);
+        store_row<C>(w.AXH1 + ro, xh, H1, lane);
+        store_row<C>(w.AH1 + ro, h, H1, lane);
         if (lane == 0) w.ARS1[r] = rs;
     } else {
-        store_row<C>(w.CH1 + ro, h, a.H1, lane);
+        store_row<C>(w.CH1 + ro, h, H1, lane);
     }
 }
 
 // a3: actor LN2/ReLU/mu/tanh, Q(s, mu) with the updated critic, actor loss -mean Q, and the backward through the
 // critic's action branch (dQ/dmu) and the actor head down to the actor's fc2 pre-activation
-template <int C>
+template <int C, int HC, int NAC>
 __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);
-    const int H2 = a.H2, na = a.na;
+    const int H2 = HC ? HC : a.H2, na = NAC ? NAC : a.na;
     float* at = ct + round4(crit_tail_len(na, H2));
     const int lane = threadIdx.x & 63;
     const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
@@ -605,19 +607,19 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
 // blocks past them).
-template <int C>
+template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     if ((int)blockIdx.y < npc)
-        c1_body<C>(wc, ac, blockIdx.x, blockIdx.y);
+        c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
     else
-        a1_body<C>(wa, aa, blockIdx.x, blockIdx.y - npc);
+        a1_body<C, HC>(wa, aa, blockIdx.x, blockIdx.y - npc);
 }
-template <int C>
+template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
     if ((int)blockIdx.x < nbc)
-        c3_body<C>(wc, ac, blockIdx.x);
+        c3_body<C, HC, NAC>(wc, ac, blockIdx.x);
     else
-        a3_body<C>(wa, aa, blockIdx.x - nbc);
+        a3_body<C, HC, NAC>(wa, aa, blockIdx.x - nbc);
 }
 // ---------------------------------------------------------------------------------------------------------------
 // f32 GEMM tile on MFMA: C[m, n] = sum_k A(m, k) B(k, n) for one 32x32 output tile; A(m, k) = A[m*sam + k*sak],
@@ -1603,6 +1605,13 @@ void actor_job(const FlockScUpdate* u, Job& j) {
 
 size_t zmax(size_t a, size_t b) { return a > b ? a : b; }
 
+// The reference's production widths (fc1 400, fc2 300, 2 actions: agent_simple_shared_critic.py / train_flock.py
+// defaults) get row kernels with compile-time widths: every per-lane column mask and action loop folds away
+// (sc_k3 ~40 % fewer instructions per wave). flock_set_diag("sc_no_spec", 1) forces the generic instantiations
+// (the bitwise A/B of tests/test_gpu_learners.py).
+bool g_sc_no_spec = false;  // set by flock_sc_diag_no_spec (flock_set_diag)
+bool spec_shape(const Job& j) { return !g_sc_no_spec && j.H1 == 400 && j.H2 == 300 && j.na == 2; }
+
 // One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in five launches; either may be
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
 // computes exactly what the actor phase followed by the critic phase would.
@@ -1617,8 +1626,13 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
         const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
         const size_t lds = zmax(A.lds1, Z.lds1);
         const dim3 grid(rb, npc + npa);
-        SC_C_SWITCH(C, if ((rc = allow_lds(sc_k1<CC>, lds))) return rc;
-                    hipLaunchKernelGGL(sc_k1<CC>, grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a))
+        if (spec_shape(A)) {
+            if ((rc = allow_lds(sc_k1<7, 400>, lds))) return rc;
+            hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a);
+        } else {
+            SC_C_SWITCH(C, if ((rc = allow_lds(sc_k1<CC, 0>, lds))) return rc;
+                        hipLaunchKernelGGL((sc_k1<CC, 0>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a))
+        }
         if ((rc = launched())) return rc;
     }
     {  // 2: forward fc2 GEMMs
@@ -1634,8 +1648,13 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
         const int nbc = jc ? rb : 0;
         const size_t lds = zmax(A.lds3, Z.lds3);
         const dim3 grid(nbc + (ja ? rb : 0));
-        SC_C_SWITCH(C, if ((rc = allow_lds(sc_k3<CC>, lds))) return rc;
-                    hipLaunchKernelGGL(sc_k3<CC>, grid, dim3(256), lds, st, A.w, A.a, nbc, Z.w, Z.a))
+        if (spec_shape(A)) {
+            if ((rc = allow_lds(sc_k3<5, 300, 2>, lds))) return rc;
+            hipLaunchKernelGGL((sc_k3<5, 300, 2>), grid, dim3(256), lds, st, A.w, A.a, nbc, Z.w, Z.a);
+        } else {
+            SC_C_SWITCH(C, if ((rc = allow_lds(sc_k3<CC, 0, 0>, lds))) return rc;
+                        hipLaunchKernelGGL((sc_k3<CC, 0, 0>), grid, dim3(256), lds, st, A.w, A.a, nbc, Z.w, Z.a))
+        }
         if ((rc = launched())) return rc;
     }
     {  // 4: dH1 = dZ2 W2 with the LN1-backward epilogue, dW2, early reductions
@@ -1748,6 +1767,9 @@ __global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint
 }
 
 }  // namespace
+
+// the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
+void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
 
 extern "C" {
 

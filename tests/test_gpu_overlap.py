@@ -150,3 +150,39 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, cuda):
                  (ser.actor_steps, pip.actor_steps), (ser.critic.step_dev, pip.critic.step_dev),
                  (ser.losses, pip.losses)):
         assert torch.equal(x, y)
+
+
+def test_specialised_row_kernels_equal_generic(cuda):
+    """At the reference widths (fc1 400, fc2 300, 2 actions) the rounds run row kernels with compile-time widths;
+    flock_set_diag("sc_no_spec", 1) forces the generic ones. Merged rounds of both are bitwise equal."""
+    from marl_range_flocking_amd import _native
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    lib = _native.lib()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    n, d = 600, 20
+    rows = (torch.rand(n, d, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g) * 2 - 1,
+            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, d, device=cuda, generator=g),
+            torch.rand(n, device=cuda, generator=g) > 0.8)
+    ls = torch.cuda.Stream(device=cuda)
+    main = torch.cuda.current_stream(cuda)
+    out = []
+    for no_spec in (0, 1):
+        L = SharedCriticLearner(6, d, device=cuda, seed=3, batch_size=256, buffer_size=1000, snapshot=True,
+                                n_slots=3)
+        L.store_transitions(*rows)
+        assert lib.flock_set_diag(b"sc_no_spec", no_spec) == 0
+        try:
+            for a in (0, 3, 3, 1, 5, 2, 0):
+                assert L.pipeline_learn(a, main.cuda_stream, ls.cuda_stream)
+            L.pipeline_flush(ls.cuda_stream)
+            main.wait_stream(ls)
+            torch.cuda.synchronize()
+        finally:
+            lib.flock_set_diag(b"sc_no_spec", 0)
+        out.append(L)
+    a, b = out
+    for x, y in ((a.critic.data, b.critic.data), (a.critic.exp_avg_sq, b.critic.exp_avg_sq),
+                 (a.actors.data, b.actors.data), (a.actors.target, b.actors.target), (a.losses, b.losses)):
+        assert torch.equal(x, y)
+    assert torch.isfinite(a.critic.data).all() and a.losses.abs().sum() > 0
