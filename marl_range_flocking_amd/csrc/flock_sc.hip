@@ -604,11 +604,39 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     if (lane == 0) w.ARS2[r] = rs;
 }
 
+// -DFLOCK_SC_PROF (diagnostics build, tools/sc_block_prof.py): per-block start / end times (s_memrealtime, 100 MHz)
+// of the five round kernels (the start by thread 0, the end as the max over the block's waves), and phase marks of
+// the forward GEMM blocks
+#ifdef FLOCK_SC_PROF
+__device__ unsigned long long g_scprof[5][4096][2];
+struct ScProf {
+    int k;
+    unsigned long long t0;
+    __device__ explicit ScProf(int kk) : k(kk), t0(__builtin_amdgcn_s_memrealtime()) {}
+    __device__ ~ScProf() {
+        const int b = blockIdx.x + gridDim.x * blockIdx.y;
+        if (b < 4096 && (threadIdx.x & 63) == 0) {
+            if (threadIdx.x == 0) g_scprof[k][b][0] = t0;
+            atomicMax(&g_scprof[k][b][1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        }
+    }
+};
+#define SC_PROF(k) ScProf sc_prof_(k)
+__device__ unsigned long long g_scmark[4096][8];
+#define SC_MARK(MK, i)                                                                           \
+    if (MK && threadIdx.x == 0 && blockIdx.x + gridDim.x * blockIdx.y < 4096)                   \
+        g_scmark[blockIdx.x + gridDim.x * blockIdx.y][i] = __builtin_amdgcn_s_memrealtime();
+#else
+#define SC_PROF(k)
+#define SC_MARK(MK, i)
+#endif
+
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
 // blocks past them).
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
+    SC_PROF(0);
     if ((int)blockIdx.y < npc)
         c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
     else
@@ -616,6 +644,7 @@ __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, 
 }
 template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
+    SC_PROF(2);
     if ((int)blockIdx.x < nbc)
         c3_body<C, HC, NAC>(wc, ac, blockIdx.x);
     else
@@ -814,9 +843,10 @@ __device__ __forceinline__ f32x16 mfma_panel(f32x16 acc, const float* a, const f
 }
 
 // the 4 outputs of thread (wave w, lane l): rows 8w + 4(l >> 5) + q (q < 4), column l & 31
-template <int AV, int BV, int NF>
+template <int AV, int BV, int NF, int MK = 0>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
                                           float (&out)[4]) {
+    SC_MARK(MK, 0)
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
     const int kcmax = gemm_kc(g.K, g.kchunk);
     float* As = smem;
@@ -833,7 +863,9 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
         for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
             panel_store<AV, NF>(As, va, kc);
             panel_store<BV, NF>(Bs, vb, kc);
+            SC_MARK(MK, (k0 ? 4 : 1))
             __syncthreads();
+            SC_MARK(MK, (k0 ? 5 : 2))
             const int k1 = k0 + g.kchunk, kc1 = k1 < g.K ? gemm_kc(g.K - k1, g.kchunk) : 0;
             if (k1 < g.K) {  // the next chunk's loads fly during this chunk's MFMAs
                 panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
@@ -844,6 +876,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
             const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
             acc = mfma_panel(acc, a, b, kq);
             __syncthreads();
+            SC_MARK(MK, (k0 ? 6 : 3))
             kc = kc1;
         }
     } else {
@@ -862,6 +895,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
 #pragma unroll
     for (int v = 0; v < 16; ++v) red[(wv * 16 + v) * 64 + l] = acc[v];
     __syncthreads();
+    SC_MARK(MK, 7)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int v = 4 * wv + q;
@@ -873,6 +907,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
 // grid (max tiles, problems): block (x, y) computes tile x of problem y
 template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
+    SC_PROF(1);
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const GemmP& g = gb.p[blockIdx.y];
@@ -884,7 +919,7 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     const int n = tn * kT + (l & 31);
     const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
     float out[4];
-    gemm_tile<AV, BV, NF>(g, g.B + rel, tm, tn, smem, out);
+    gemm_tile<AV, BV, NF, 1>(g, g.B + rel, tm, tn, smem, out);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
@@ -1106,6 +1141,7 @@ struct Bwd2 {
 };
 template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
 __global__ __launch_bounds__(256) void sc_bwd(Bwd2 bb) {
+    SC_PROF(3);
     if ((int)blockIdx.x < bb.nb0)
         bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
     else
@@ -1253,6 +1289,7 @@ struct GradAdam2 {
     int nb0;
 };
 __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
+    SC_PROF(4);
     if ((int)blockIdx.x < gg.nb0)
         grad_adam_body(gg.j0, blockIdx.x, gg.nb0);
     else
@@ -2036,6 +2073,16 @@ int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream) {
     p->pending = -1;
     return 0;
 }
+
+#ifdef FLOCK_SC_PROF
+// diagnostics build only: copy out the per-block times of the last launch of each round kernel / the GEMM marks
+int flock_sc_prof_read(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_scprof), sizeof(g_scprof)) != hipSuccess;
+}
+int flock_sc_mark_read(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_scmark), sizeof(g_scmark)) != hipSuccess;
+}
+#endif
 
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;

@@ -23,10 +23,15 @@ def build():
     from marl_range_flocking_amd.build import CSRC, FILE_FLAGS, HIPCC_FLAGS, INCLUDE, hipcc
 
     os.makedirs(os.path.dirname(SO), exist_ok=True)
-    cmd = [hipcc()] + HIPCC_FLAGS + FILE_FLAGS["flock_env.hip"] + ["-DFLOCK_PHASE_PROF", "-shared", "-I", INCLUDE, "-o", SO,
-                                     os.path.join(CSRC, "flock_env.hip")]
+    b = os.path.dirname(SO)
+    obj = os.path.join(b, "flock_env_phase.o")
+    cmd = [hipcc()] + HIPCC_FLAGS + FILE_FLAGS["flock_env.hip"] + ["-DFLOCK_PHASE_PROF", "-c", "-I", INCLUDE, "-o", obj,
+                                                                 os.path.join(CSRC, "flock_env.hip")]
     print(" ".join(cmd))
     subprocess.check_call(cmd)
+    # linked with the product's learner objects (flock_env.hip calls into flock_sc.hip for the diagnostics knob)
+    subprocess.check_call([hipcc()] + HIPCC_FLAGS + ["-shared", "-o", SO, obj, os.path.join(b, "flock_learn.hip.o"),
+                                                     os.path.join(b, "flock_sc.hip.o")])
 
 
 def run(E, N, k, steps, variant="v2"):
