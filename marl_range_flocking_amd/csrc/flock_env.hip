@@ -110,6 +110,7 @@ struct Params {
 #ifdef FLOCK_PHASE_PROF
 // 64 slots x 32 counters (slot = blockIdx mod 64) so the end-of-kernel atomics do not pile onto one address
 __device__ unsigned long long g_phase[64 * 32];
+__device__ unsigned long long g_blk[4096][2];  // per block: start (thread 0) and end (max over waves), s_memrealtime
 #define PHASE(n)                                                             \
     do {                                                                     \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
@@ -122,6 +123,12 @@ __device__ unsigned long long g_phase[64 * 32];
     } while (0)
 #define PHASE_FLUSH()                                                                               \
     do {                                                                                            \
+        ph_acc[19] += __builtin_amdgcn_s_memtime() - st0_;                                          \
+        ph_acc[23] += __builtin_amdgcn_s_memrealtime() - rt0_;                                      \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                                         \
+            if (threadIdx.x == 0) g_blk[blockIdx.x][0] = rt0_;                                      \
+            atomicMax(&g_blk[blockIdx.x][1], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+        }                                                                                           \
         if ((threadIdx.x & 63) == 0)                                                                \
             _Pragma("unroll") for (int q_ = 0; q_ < 24; ++q_)                                       \
                 if (ph_acc[q_]) atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + q_], ph_acc[q_]);       \
@@ -723,6 +730,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #pragma unroll
     for (int q_ = 0; q_ < 24; ++q_) ph_acc[q_] = 0;
     unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+    const unsigned long long st0_ = t_prev, rt0_ = __builtin_amdgcn_s_memrealtime();  // in-kernel clock
     PHASE_COUNT(20, 1);
 #endif
 #ifdef FLOCK_STAGGER  // diagnostics: offset the phases of the first-round blocks sharing a CU (b, b + 256, ...)
@@ -1630,6 +1638,10 @@ int flock_phase_read(unsigned long long* host) {
     }
     memset(buf, 0, sizeof(buf));
     return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), buf, sizeof(buf)) != hipSuccess;
+}
+// diagnostics build only: per-block start / end (s_memrealtime) of the last launch (blocks < 4096)
+int flock_blk_read(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blk), sizeof(g_blk)) != hipSuccess;
 }
 #endif
 

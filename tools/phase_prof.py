@@ -105,6 +105,23 @@ def run(E, N, k, steps, variant="v2"):
     print(f"  waves taking 5x5: {buf[16] / waves:.4f}, full scan: {buf[17] / waves:.5f}, "
           f"ambiguous rescan: {buf[18] / waves:.5f}")
     print(f"  cell-scan pair iterations per wave: {buf[21] / waves:.1f} over {buf[22] / waves:.2f} row ranges")
+    bb = (ctypes.c_ulonglong * (4096 * 2))()
+    lib.flock_blk_read.argtypes = [ctypes.c_void_p]
+    if lib.flock_blk_read(bb) == 0:
+        t = np.frombuffer(bb, dtype=np.uint64).reshape(4096, 2).astype(np.int64)
+        nb = min(4096, (E * N + 255) // 256)
+        t = t[:nb]
+        t0 = t[:, 0].min()
+        st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0
+        span = en.max()
+        grid = np.linspace(0, span, 60)
+        conc = [int(((st <= g) & (en > g)).sum()) for g in grid]
+        print(f"  last launch, blocks 0..{nb - 1}: span {span:.1f} us, block lifetime p10/p50/p90 "
+              f"{np.percentile(en - st, 10):.1f}/{np.percentile(en - st, 50):.1f}/{np.percentile(en - st, 90):.1f} us; "
+              f"start p10/p50/p90 {np.percentile(st, 10):.1f}/{np.percentile(st, 50):.1f}/{np.percentile(st, 90):.1f}")
+        print("  resident blocks over the launch (60 samples): " + " ".join(str(c) for c in conc))
+    print(f"  in-kernel clock (shader cycles / s_memrealtime x 100 MHz over the waves' lifetimes): "
+          f"{buf[19] / max(buf[23], 1) * 0.1:.2f} GHz; mean wave lifetime {buf[23] / waves * 0.01:.2f} us")
 
 
 if __name__ == "__main__":
