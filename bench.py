@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")
+    ap.add_argument("--step-launches", type=int, default=None,
+                    help="env step as this many launches over env ranges (FlockConfig.step_launches; default: 2 "
+                         "with the overlapped shared-critic learner, whose rounds take the slots the first "
+                         "launch's tail frees; 1 otherwise)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
                          "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
@@ -271,10 +275,12 @@ def main():
     from marl_range_flocking_amd import FlockConfig, VecFlockEnv
 
     E, N, k = args.envs, args.agents, args.k
+    launches = args.step_launches or (2 if args.learner == "shared_critic" and args.overlap else 1)
     box = float(round(np.sqrt(250.0 * N)))  # main.py density: 10 agents in 50x50
     cfg = FlockConfig(variant=args.variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
                       range_start=(0, box), sensor_range=14.0, seed=1234 + rank,
-                      track_indices=args.variant == "v2")  # the reference returns neighbour indices for v2 only
+                      track_indices=args.variant == "v2",  # the reference returns neighbour indices for v2 only
+                      step_launches=launches)
     env = VecFlockEnv(cfg, device=dev)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     env.positions.copy_(torch.rand(E, N, 2, device=dev, generator=g) * box)
@@ -340,6 +346,20 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
+    # the env step alone (after the timed region, no learner beside it, as ONE launch): what the kernel does when it
+    # has the GPU to itself
+    alone_ms = None
+    if hook is not None:
+        env.set_param("step_launches", 1)
+        ev_alone = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for i, (a0, a1) in enumerate(ev_alone):
+            a = pool[i % len(pool)]
+            ring = hook.before(args.warmup + args.steps + i)
+            a0.record(stream)
+            env.step(a, ring=ring) if ring is not None else env.step(a)
+            a1.record(stream)
+        torch.cuda.synchronize(dev)
+        alone_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_alone[2:]]))
 
     total_agent_steps = world * E * N * args.steps
     value = total_agent_steps / el
@@ -405,7 +425,15 @@ def main():
                      "insert_bytes_per_agent_step": ins,
                      "achieved_incl_insert": (bpa + ins) * E * N / kern_s / 1e9,
                      "valu": valu,
-                     "binding": "valu" if valu and valu["frac"] > hbm_frac else "hbm"},
+                     "binding": "valu" if valu and valu["frac"] > hbm_frac else "hbm",
+                     "step_launches": launches,
+                     "kernel_alone_ms": alone_ms,
+                     "frac_alone": (bpa * E * N / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if alone_ms else None,
+                     "valu_frac_alone": (64.0 * sq["SQ_INSTS_VALU"] / (alone_ms * 1e-3) / VALU_PEAK_LANEOPS)
+                     if alone_ms and sq and "SQ_INSTS_VALU" in sq else None,
+                     "note": "kernel_ms / frac / valu: HIP events around every 4th env step of the timed region (the "
+                             "step's launches, with the learner's kernels beside them); *_alone: the same step as one "
+                             "launch with no learner, after the timed region"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, box, args.cpu_seconds)

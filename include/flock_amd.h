@@ -113,6 +113,10 @@ int flock_step_v2_store(void* stream, int E, int N, int k, float box, float sens
 typedef struct FlockStepExt {
     const FlockRing* ring;
     uint16_t* seeds;
+    /* > 1: the step as that many back-to-back launches over consecutive env ranges (identical results; envs are
+     * independent). While another stream's kernels run beside the step (the config-3 learner rounds), the boundary
+     * between two launches lets them take the block slots the first launch's tail frees. 0 or 1: one launch. */
+    int launches;
 } FlockStepExt;
 int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
                       float dt, float v_min, float v_max, int periodic, int rigid_boundary,

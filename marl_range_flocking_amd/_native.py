@@ -97,7 +97,7 @@ class FlockRing(ctypes.Structure):
 class FlockStepExt(ctypes.Structure):
     """Mirror of ``FlockStepExt`` (include/flock_amd.h): optional extras of the *_ext step entry points."""
 
-    _fields_ = [("ring", ctypes.POINTER(FlockRing)), ("seeds", _c_void_p)]
+    _fields_ = [("ring", ctypes.POINTER(FlockRing)), ("seeds", _c_void_p), ("launches", _c_int)]
 
 
 for _name in ("flock_step_v2_ext", "flock_step_uw_ext", "flock_step_uw_discrete_ext", "flock_step_flock_ext"):

@@ -67,6 +67,7 @@ int fail(int code, const char* msg) {
 struct Params {
     int E, N, k, G, S, P, ib;
     int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
+    int launches;  // FlockStepExt.launches: the step as this many launches over env ranges (0: the diagnostics knob)
     int variant, periodic, rigid, clamp;
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
     uint64_t seed, rng_offset;
@@ -1476,8 +1477,8 @@ Knobs& knobs_mut() {
     return k;
 }
 const Knobs& knobs() { return knobs_mut(); }
-int env_launches(int blocks) {
-    const int n = knobs().env_launches;
+int env_launches(int blocks, int requested) {
+    const int n = requested > 0 ? requested : knobs().env_launches;
     return n < 1 ? 1 : (n > blocks ? blocks : n);
 }
 
@@ -1496,7 +1497,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         c.T = SPL * NC;
         c.lds = ((c.lds + 15) & ~(size_t)15) + (size_t)(SPL - 1) * 6 * NC * sizeof(uint32_t);
     }
-    const int parts = env_launches(c.blocks);
+    const int parts = env_launches(c.blocks, p.launches);
     if (parts <= 1) {
         hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks), dim3(c.T), c.lds, s,
                            p);
@@ -1690,7 +1691,7 @@ int set_ring(Params& p, const FlockRing* ring, int E, int N, const char* who) {
 int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance, float dt,
                  float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
-                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds) {
+                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds, int launches = 0) {
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done))
@@ -1715,6 +1716,7 @@ int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_rang
     p.done = done;
     p.any_done = any_done;
     p.seeds = seeds;
+    p.launches = launches;
     return dispatch(p, (hipStream_t)stream, false);
 }
 
@@ -1747,7 +1749,7 @@ int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor
                       uint8_t* done, uint8_t* any_done, const FlockStepExt* ext) {
     return step_v2_impl(stream, E, N, k, box, sensor_range, collision_distance, dt, v_min, v_max, periodic,
                         rigid_boundary, pos, heading, action, vel, dnn, nn_idx, reward, done, any_done,
-                        ext ? ext->ring : nullptr, ext ? ext->seeds : nullptr);
+                        ext ? ext->ring : nullptr, ext ? ext->seeds : nullptr, ext ? ext->launches : 0);
 }
 
 int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
@@ -1767,6 +1769,7 @@ int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor
     p.cd = collision_distance;
     p.com_r = (float)((double)collision_distance * 4.0);  // collision_distance*4 (gym_flock_uw.py:197)
     p.seeds = ext ? ext->seeds : nullptr;
+    p.launches = ext ? ext->launches : 0;
     p.dt = dt;
     p.pos = pos;
     p.heading = const_cast<float*>(heading);
@@ -1832,6 +1835,7 @@ int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, flo
     p.any_done = any_done;
     p.status = status;
     p.seeds = ext ? ext->seeds : nullptr;
+    p.launches = ext ? ext->launches : 0;
     return dispatch(p, (hipStream_t)stream, false);
 }
 
@@ -1861,6 +1865,7 @@ int flock_step_flock_ext(void* stream, int E, int N, int k, float box, float col
     p.rigid = rigid_boundary != 0;
     p.clamp = 0;  // gym_flock.py:105: no clamp
     p.seeds = ext ? ext->seeds : nullptr;
+    p.launches = ext ? ext->launches : 0;
     p.cd = collision_distance;
     p.dt = dt;
     p.pos = pos;

@@ -40,6 +40,10 @@ class FlockConfig:
     # only their colliding agents for up to this many rounds (0: bounded rejection sampling alone, valid = False)
     reset_repair_rounds: int = 64
     track_indices: bool = True     # keep nearest_neighbors (the reference keeps them for v2 only)
+    # > 1: each step as that many launches over consecutive env ranges (FlockStepExt.launches; identical results).
+    # With learner kernels on another stream beside the step (bench config 3: 2), the launch boundary hands them the
+    # block slots the first launch's tail frees
+    step_launches: int = 1
     reset_check_distance: float = None  # uw_discrete resets with collision_distance = 4 (:145)
     extra: dict = field(default_factory=dict)
 
@@ -53,6 +57,8 @@ class FlockConfig:
             c.v_min = 0.005
         if c.reset_check_distance is None:
             c.reset_check_distance = 4.0 if c.variant == "uw_discrete" else c.collision_distance
+        if int(c.step_launches) < 1:
+            raise ValueError("step_launches must be >= 1")
         return c
 
 
@@ -111,11 +117,14 @@ class VecFlockEnv:
 
     def set_param(self, name, value):
         """Change a step / reset parameter (collision_distance, sensor_range, rigid_boundary, max_linear_velocity,
-        v_min, dt) between steps: the recorded launch plans hold the old scalars, so they are dropped. The reset
+        v_min, dt, step_launches) between steps: the recorded launch plans hold the old scalars, so they are dropped. The reset
         check distance follows collision_distance (gym_flock_v2.py:100-105) except for uw_discrete, whose reset
         checks with 4 (gym_flock_uw_discrete.py:145)."""
-        if name not in ("collision_distance", "sensor_range", "rigid_boundary", "max_linear_velocity", "v_min", "dt"):
+        if name not in ("collision_distance", "sensor_range", "rigid_boundary", "max_linear_velocity", "v_min", "dt",
+                        "step_launches"):
             raise AttributeError(f"{name} is not a runtime parameter")
+        if name == "step_launches" and int(value) < 1:
+            raise ValueError("step_launches must be >= 1")
         setattr(self.cfg, name, value)
         if name == "collision_distance" and self.cfg.variant != "uw_discrete":
             self.cfg.reset_check_distance = value
@@ -252,28 +261,31 @@ class VecFlockEnv:
             if c.variant not in ("v2", "uw_discrete"):
                 raise NotImplementedError("the fused replay insert is built for the v2 and uw_discrete steps")
             ring.prev_obs = src["dnn"].data_ptr()
-        T = self._torch_ops if ring is None else None
+        T = self._torch_ops if ring is None and c.step_launches <= 1 else None
         if T is not None:
             self._step_torch(T, a, noise, dt, src, dst)
         elif c.variant == "v2":
             ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
                         self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
-                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, seeds=self.seeds, **common)
+                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, seeds=self.seeds,
+                        launches=c.step_launches, **common)
         elif c.variant == "uw":
             ops.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
                         dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, sensor_range=c.sensor_range,
-                        seeds=self.seeds, **common)
+                        seeds=self.seeds, launches=c.step_launches, **common)
         elif c.variant == "uw_discrete":
             if noise is not None:
                 noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
             ops.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
                                  self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
                                  self.status, sensor_range=c.sensor_range, v_max=c.max_linear_velocity,
-                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, ring=ring, **common)
+                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, ring=ring,
+                                 launches=c.step_launches, **common)
             self._rng_offset += 1
         else:
             ops.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
-                           self.reward, self.done, self.any_done, seeds=self.seeds, **common)
+                           self.reward, self.done, self.any_done, seeds=self.seeds, launches=c.step_launches,
+                           **common)
         self._cur = nxt
         self.steps += 1
         info = {}

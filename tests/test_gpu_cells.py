@@ -319,3 +319,36 @@ def test_env_range_launches_are_bitwise_one_launch(cuda):
                          "seeds": env.seeds.clone() if env.seeds is not None else rew})
         for key in outs[0]:
             assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+
+
+@pytest.mark.parametrize("variant,periodic,N,kind", SPEC[:3], ids=[f"{v}-N{n}-{d}" for v, _, n, d in SPEC[:3]])
+def test_step_launches_are_bitwise_one_launch(variant, periodic, N, kind, cuda):
+    """FlockConfig.step_launches > 1 (FlockStepExt.launches): the step as several launches over consecutive env
+    ranges. Envs are independent, so three-step rollouts equal the one-launch step bit for bit."""
+    k, E = 4, 37
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(N + 11)
+    pos = _positions(kind, E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    envs = []
+    for launches in (1, 3):
+        env = VecFlockEnv(FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, periodic=periodic,
+                                      step_launches=launches), device=cuda)
+        env.set_state(positions=pos, headings=head)
+        envs.append(env)
+    for t in range(3):
+        if variant == "uw_discrete":
+            act = torch.from_numpy(rng.integers(0, 4, (E, N)).astype(np.int64))
+            kw = dict(noise=torch.from_numpy((0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)))
+        else:
+            act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
+            kw = {}
+        outs = []
+        for env in envs:
+            obs, rew, (done, anyd), _ = env.step(act, **kw)
+            torch.cuda.synchronize()
+            outs.append({"pos": env.positions.clone(), "head": env.headings.clone(), "dnn": env.dnn.clone(),
+                         "idx": env.nn_idx.clone(), "rew": rew.clone(), "done": done.clone(), "any": anyd.clone()})
+        for key in outs[0]:
+            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
