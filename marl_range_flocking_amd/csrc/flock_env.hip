@@ -885,9 +885,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 const U4 r = philox(p.seed, (uint32_t)a, (uint32_t)(a >> 32), (uint32_t)p.rng_offset,
                                     (uint32_t)(p.rng_offset >> 32) ^ 0x5EEDu);
                 const float u1 = fmaxf(u01(r.x), 1.0f / 16777216.0f), u2 = u01(r.y);
-                const float rad = sqrtf(-2.0f * logf(u1));
-                nl = rad * cosf(6.28318530718f * u2) * p.noise_std;
-                na = rad * sinf(6.28318530718f * u2) * p.noise_std;
+                // hardware transcendentals (v_log_f32 is log2; v_sin / v_cos_f32 take revolutions, u2 already is
+                // one): the draws must be N(0, std), not the bits of a particular libm (torch.normal's CPU stream
+                // cannot be reproduced on the device anyway); the ocml logf / sinf / cosf cost ~100 VALU per agent
+                const float rad = __builtin_sqrtf(-2.0f * 0.693147180560f * __builtin_amdgcn_logf(u1));
+                nl = rad * __builtin_amdgcn_cosf(u2) * p.noise_std;
+                na = rad * __builtin_amdgcn_sinf(u2) * p.noise_std;
             }
             float lin = __fadd_rn(mean.x, nl);
             const float ang = clamp_t(__fadd_rn(mean.y, na), -0.025f, 0.025f);  // :343

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round evidence in one GPU session (outputs under gpurun_out/ev2/; copy the summaries into profiles/r02/):
 #   GPU tests, smoke, every config's bench line + rocprofv3 kernel stats, and the env kernel's PMC passes
-#   (FETCH_SIZE, WRITE_SIZE: one pass each, MI355X_MICROARCH.md; SQ instruction mix) -> pmc_*.json.
+#   (FETCH_SIZE, WRITE_SIZE: one pass each, MI355X_MICROARCH.md; SQ instruction mix) -> pmc_*.json. The PMC passes
+#   run the step as one launch (--step-launches 1), so a dispatch's counters are one whole step's.
 # PHASES="tests bench pmc" selects parts. Every GPU step has its own time limit; the script stops at a failure.
 set -u
 OUT=gpurun_out/ev2; mkdir -p $OUT; export TMPDIR=/tmp
@@ -21,10 +22,10 @@ if [[ $PHASES == *pmc* ]]; then
   for c in ${CONFIGS:-3 2 4 5}; do
     t=$(tag_of $c)
     for ctr in FETCH_SIZE WRITE_SIZE; do
-      step pmc_${t}_$ctr.log 240 rocprofv3 --pmc $ctr -d $OUT/pmc_${t}_$ctr -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3
+      step pmc_${t}_$ctr.log 240 rocprofv3 --pmc $ctr -d $OUT/pmc_${t}_$ctr -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3 --step-launches 1
     done
     python tools/pmc_traffic.py $OUT/pmc_${t}_FETCH_SIZE $OUT/pmc_${t}_WRITE_SIZE --kernel step_kernel --algorithmic-bytes $(alg_of $c) --out $OUT/pmc_$t.json
-    step pmc_sq_$t.log 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM -d $OUT/pmc_sq_$t -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3
+    step pmc_sq_$t.log 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM -d $OUT/pmc_sq_$t -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3 --step-launches 1
     python tools/pmc_sq_json.py $OUT/pmc_sq_$t --kernel step_kernel --out $OUT/pmc_sq_$t.json
   done
   cp $OUT/pmc_*.json profiles/  # the bench lines below read them (copy them into the repo afterwards)
