@@ -972,6 +972,27 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
                                            int& e_out, bool& live_out) {
     const int tid = threadIdx.x;
     const bool dzm = rp.mode == 4 || rp.mode == 5;
+    const int el = tid & (kRedElems - 1), q = tid >> 4;
+    const int e = (b - rp.blk0) * kRedElems + el;
+    const bool live = e < rp.n;
+    const bool per_in = rp.mode == 2 || rp.mode == 4;
+    const int o = per_in ? e / rp.in : e;
+    const int i = per_in ? e - o * rp.in : e;
+    const bool prod = rp.mode == 1 || rp.mode == 2 || rp.mode == 4;
+    constexpr int kRB = 8;  // rows per batch of loads (row group q takes rows q, q + 16, ...)
+    float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
+    auto load = [&](int r0) {
+#pragma unroll
+        for (int k = 0; k < kRB; ++k) {
+            const int r = r0 + 16 * k;
+            const bool in = live && r < B;
+            dv[k] = in ? rp.D[(int64_t)r * rp.ldd + o] : 0.0f;
+            xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
+            xh[k] = (in && dzm) ? dz.XH[(int64_t)r * dz.F + o] : 0.0f;
+            rs[k] = (in && dzm) ? dz.RS[r] : 0.0f;
+        }
+    };
+    load(q);  // the first batch is in flight while the LN1 row statistics are formed
     if (dzm) {  // mean(dxh), mean(dxh xhat) of every row: its tiles' partial sums in a fixed order
         for (int r = tid; r < B; r += 256) {
             const float2* ps = reinterpret_cast<const float2*>(dz.PS + (int64_t)r * 2 * dz.ntn);
@@ -995,26 +1016,9 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
         }
         __syncthreads();
     }
-    const int el = tid & (kRedElems - 1), q = tid >> 4;
-    const int e = (b - rp.blk0) * kRedElems + el;
-    const bool live = e < rp.n;
-    const bool per_in = rp.mode == 2 || rp.mode == 4;
-    const int o = per_in ? e / rp.in : e;
-    const int i = per_in ? e - o * rp.in : e;
-    const bool prod = rp.mode == 1 || rp.mode == 2 || rp.mode == 4;
     float acc = 0.0f;
-    constexpr int kRB = 8;  // rows per batch of loads (row group q takes rows q, q + 16, ...)
     for (int r0 = q; r0 < B; r0 += 16 * kRB) {
-        float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
-#pragma unroll
-        for (int k = 0; k < kRB; ++k) {
-            const int r = r0 + 16 * k;
-            const bool in = live && r < B;
-            dv[k] = in ? rp.D[(int64_t)r * rp.ldd + o] : 0.0f;
-            xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
-            xh[k] = (in && dzm) ? dz.XH[(int64_t)r * dz.F + o] : 0.0f;
-            rs[k] = (in && dzm) ? dz.RS[r] : 0.0f;
-        }
+        if (r0 != q) load(r0);
         if (dzm) {
 #pragma unroll
             for (int k = 0; k < kRB; ++k) {
