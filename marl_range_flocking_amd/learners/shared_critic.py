@@ -609,7 +609,8 @@ class SharedCriticBench:
             # FLOCK_LEARN_PIPELINE=0 keeps one serial learn() per step on self.stream.
             self.pipelined = not self.learner.distributed and os.environ.get("FLOCK_LEARN_PIPELINE") != "0"
             # stream priority (FLOCK_LEARNER_PRIORITY=1): the one-stream learner ran at high priority; with the two
-            # pipelined streams high priority made steps 2-3x slower in fresh processes (tools/pipe_bench_probe.py)
+            # pipelined streams high priority made steps 2-3x slower in fresh processes; with the native pipeline's
+            # one learner stream it changes nothing (tools/cu_mask_probe.py)
             hi = os.environ.get("FLOCK_LEARNER_PRIORITY", "0" if self.pipelined else "1") == "1"
             prio = torch.cuda.Stream.priority_range()[1] if hi else 0
             self.stream = torch.cuda.Stream(device=device, priority=prio)
