@@ -112,11 +112,14 @@ struct Params {
 // 64 slots x 32 counters (slot = blockIdx mod 64) so the end-of-kernel atomics do not pile onto one address
 __device__ unsigned long long g_phase[64 * 32];
 __device__ unsigned long long g_blk[4096][2];  // per block: start (thread 0) and end (max over waves), s_memrealtime
+__device__ unsigned long long g_blkph[4096][8];  // per block: thread 0's s_memrealtime at each phase mark
 #define PHASE(n)                                                             \
     do {                                                                     \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
         ph_acc[n] += t_ - t_prev;                                            \
         t_prev = t_;                                                         \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                           \
+            g_blkph[blockIdx.x][n] = __builtin_amdgcn_s_memrealtime();       \
     } while (0)
 #define PHASE_COUNT(n, v) \
     do {                  \
@@ -1646,6 +1649,9 @@ int flock_phase_read(unsigned long long* host) {
 // diagnostics build only: per-block start / end (s_memrealtime) of the last launch (blocks < 4096)
 int flock_blk_read(unsigned long long* host) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blk), sizeof(g_blk)) != hipSuccess;
+}
+int flock_blkph_read(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blkph), sizeof(g_blkph)) != hipSuccess;
 }
 #endif
 

@@ -109,17 +109,30 @@ def run(E, N, k, steps, variant="v2"):
     lib.flock_blk_read.argtypes = [ctypes.c_void_p]
     if lib.flock_blk_read(bb) == 0:
         t = np.frombuffer(bb, dtype=np.uint64).reshape(4096, 2).astype(np.int64)
-        nb = min(4096, (E * N + 255) // 256)
-        t = t[:nb]
+        phb = (ctypes.c_ulonglong * (4096 * 8))()
+        lib.flock_blkph_read.argtypes = [ctypes.c_void_p]
+        lib.flock_blkph_read(phb)
+        ph = np.frombuffer(phb, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
+        keep = t[:, 0] > t[:, 0].max() - 100_000  # the last launch's blocks (started within 1 ms of its last one)
+        t, ph = t[keep], ph[keep]
+        nb = len(t)
         t0 = t[:, 0].min()
         st, en = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0
         span = en.max()
         grid = np.linspace(0, span, 60)
         conc = [int(((st <= g) & (en > g)).sum()) for g in grid]
-        print(f"  last launch, blocks 0..{nb - 1}: span {span:.1f} us, block lifetime p10/p50/p90 "
+        print(f"  last launch, {nb} blocks (of the first 4096): span {span:.1f} us, block lifetime p10/p50/p90 "
               f"{np.percentile(en - st, 10):.1f}/{np.percentile(en - st, 50):.1f}/{np.percentile(en - st, 90):.1f} us; "
               f"start p10/p50/p90 {np.percentile(st, 10):.1f}/{np.percentile(st, 50):.1f}/{np.percentile(st, 90):.1f}")
         print("  resident blocks over the launch (60 samples): " + " ".join(str(c) for c in conc))
+        late = np.argsort(en)[-3:]
+        ids = np.nonzero(keep)[0]
+        print("  last blocks to end: " + ", ".join(f"block {ids[j]} start {st[j]:.1f} end {en[j]:.1f} us" for j in late))
+        # thread 0's phase marks (us after its block's start): median block vs the three latest blocks
+        rel = (ph - t[:, :1]) / 100.0
+        print("  thread-0 phase marks, median block: " + " ".join(f"{np.median(rel[:, q]):.1f}" for q in range(8)))
+        for j in late:
+            print("  thread-0 phase marks, late block:   " + " ".join(f"{rel[j, q]:.1f}" for q in range(8)))
     print(f"  in-kernel clock (shader cycles / s_memrealtime x 100 MHz over the waves' lifetimes): "
           f"{buf[19] / max(buf[23], 1) * 0.1:.2f} GHz; mean wave lifetime {buf[23] / waves * 0.01:.2f} us")
 
