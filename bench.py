@@ -427,6 +427,7 @@ def main():
                      "valu": valu,
                      "binding": "valu" if valu and valu["frac"] > hbm_frac else "hbm",
                      "step_launches": launches,
+                     "kernel_ms_per_launch": kern_ms / launches,  # compare with rocprofv3's per-dispatch average
                      "kernel_alone_ms": alone_ms,
                      "frac_alone": (bpa * E * N / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if alone_ms else None,
                      "valu_frac_alone": (64.0 * sq["SQ_INSTS_VALU"] / (alone_ms * 1e-3) / VALU_PEAK_LANEOPS)
