@@ -117,6 +117,12 @@ typedef struct FlockStepExt {
      * independent). While another stream's kernels run beside the step (the config-3 learner rounds), the boundary
      * between two launches lets them take the block slots the first launch's tail frees. 0 or 1: one launch. */
     int launches;
+    /* != 0: normalize_distance=True of the reference constructors: the kNN (observation, collisions, rewards built
+     * on them) runs on positions / max_i |p_i| of each env (gym_flock_uw.py:125-133, gym_flock_uw_discrete.py:173-181,
+     * gym_flock.py:92-98, learners/maddpg_official_rnn/gym_flock_v2.py:134-141); state and centre-of-mass terms keep
+     * the raw positions. Ignored by the periodic v2 step (gym_flock_v2.py:135-151 never normalises). Such steps take
+     * the full-scan kernels (no cell list). */
+    int normalize_distance;
 } FlockStepExt;
 int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
                       float dt, float v_min, float v_max, int periodic, int rigid_boundary,
@@ -196,6 +202,15 @@ int flock_reset_ext(void* stream, int variant, int E, int N, int k, float range_
                     uint64_t seed, uint64_t rng_offset, const uint8_t* env_mask,
                     float* pos, float* heading, float* prev_heading, float* vel, float* dnn, int64_t* nn_idx,
                     float* mem, uint8_t* valid, int repair_rounds);
+
+/* flock_reset_ext plus normalize_distance (!= 0): the collision check and the reset observation use the kNN of
+ * positions / max_i |p_i| (the reference's reset() calls _computeDistances, gym_flock_v2.py:100 / :155-163 and
+ * siblings); the repair stage is off then (repair_rounds is ignored: it works on raw distances). */
+int flock_reset_ext2(void* stream, int variant, int E, int N, int k, float range_lo, float range_hi, float box,
+                     float sensor_range, float check_distance, int rigid_boundary, int max_attempts,
+                     uint64_t seed, uint64_t rng_offset, const uint8_t* env_mask,
+                     float* pos, float* heading, float* prev_heading, float* vel, float* dnn, int64_t* nn_idx,
+                     float* mem, uint8_t* valid, int repair_rounds, int normalize_distance);
 
 #ifdef __cplusplus
 }

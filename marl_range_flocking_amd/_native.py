@@ -39,6 +39,8 @@ SIGNATURES = {
                     _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9,
     "flock_reset_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float,
                         _c_float, _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9 + [_c_int],
+    "flock_reset_ext2": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float,
+                         _c_float, _c_int, _c_int, _c_u64, _c_u64] + [_c_void_p] * 9 + [_c_int, _c_int],
     # learner kernels (include/flock_learn.h)
     "flock_learn_last_error": [],
     "flock_adam_step": [_c_void_p, ctypes.c_int64] + [_c_void_p] * 5 + [_c_float] * 4 + [ctypes.c_int64, _c_void_p,
@@ -97,7 +99,8 @@ class FlockRing(ctypes.Structure):
 class FlockStepExt(ctypes.Structure):
     """Mirror of ``FlockStepExt`` (include/flock_amd.h): optional extras of the *_ext step entry points."""
 
-    _fields_ = [("ring", ctypes.POINTER(FlockRing)), ("seeds", _c_void_p), ("launches", _c_int)]
+    _fields_ = [("ring", ctypes.POINTER(FlockRing)), ("seeds", _c_void_p), ("launches", _c_int),
+                ("normalize_distance", _c_int)]
 
 
 for _name in ("flock_step_v2_ext", "flock_step_uw_ext", "flock_step_uw_discrete_ext", "flock_step_flock_ext"):

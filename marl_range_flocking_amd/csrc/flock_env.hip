@@ -69,6 +69,7 @@ struct Params {
     int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
     int launches;  // FlockStepExt.launches: the step as this many launches over env ranges (0: the diagnostics knob)
     int variant, periodic, rigid, clamp;
+    int normalize;  // normalize_distance: Euclidean kNN of positions / max_e |p| (full-scan path only, see dispatch)
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
     uint64_t seed, rng_offset;
     int n_actions;
@@ -960,6 +961,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     } else {
         __syncthreads();
     }
+    // normalize_distance (gym_flock_uw.py:127-133, gym_flock_uw_discrete.py:175-181, gym_flock.py:94-98, the RNN
+    // fork's gym_flock_v2.py:136-141): the kNN runs on positions / max_i torch.norm(p_i) of the env; the state, the
+    // centre-of-mass and alignment terms keep the raw positions. Runtime flag of the full-scan (!CELL, SPL = 1)
+    // Euclidean instantiations only: dispatch() routes normalize there.
+    float kx = x, ky = y;  // the kNN's coordinates of this agent
+    if (!CELL && !PERIODIC && SPL == 1 && p.normalize) {
+        float* r0 = red + (size_t)g * 2 * p.P;
+        __syncthreads();  // phase 2's sums have been read
+        if (in_group) {
+            r0[i] = active ? sqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y))) : 0.0f;  // norms >= 0: 0 pads
+            if (i < p.P - p.N) r0[p.N + i] = 0.0f;
+        }
+        __syncthreads();
+        for (int s = p.P >> 1; s >= 1; s >>= 1) {  // the max is exact in any order
+            if (in_group && i < s) r0[i] = fmaxf(r0[i], r0[i + s]);
+            __syncthreads();
+        }
+        if (active) {
+            const float m = r0[0];
+            kx = __fdiv_rn(x, m);
+            ky = __fdiv_rn(y, m);
+            lpos[g * p.S + i] = make_float2(kx, ky);
+        }
+        __syncthreads();
+    }
 
     PHASE(1);
     // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
@@ -1138,10 +1164,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
     if (active) {
         if (!ok) {
-            scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, x, y, p.box);
+            scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, kx, ky, p.box);
             R = 0;
         }
-        const bool amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj, R == 0);
+        const bool amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, R == 0);
 #ifdef FLOCK_PHASE_PROF
         if (__ballot(amb) != 0) PHASE_COUNT(18, 1);
 #endif
@@ -1293,6 +1319,7 @@ __global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
     float2* lpos = reinterpret_cast<float2*>(smem);
     int* flags = reinterpret_cast<int*>(lpos + p.G * p.S);  // [G] collision flag of the current attempt
     int* state = flags + p.G;                                // [G] 1 = still drawing
+    int* mx = state + p.G;  // [G] normalize_distance: max |p| of the draw (bits of a float >= 0, ordered as ints)
 
     const int t = threadIdx.x;
     const int g = t / p.N;
@@ -1322,9 +1349,23 @@ __global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
             y = boundary(y, p.box, p.rigid);
             lpos[g * p.S + i] = make_float2(x, y);
         }
+        if (in_group && i == 0) mx[g] = 0;
         __syncthreads();
+        float kx = x, ky = y;  // the kNN's coordinates: positions / max |p| under normalize_distance (:157-163)
+        if (p.normalize) {
+            if (active && drawing)
+                atomicMax(&mx[g], __float_as_int(sqrt_rn(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)))));
+            __syncthreads();
+            if (active && drawing) {
+                const float m = __int_as_float(mx[g]);
+                kx = __fdiv_rn(x, m);
+                ky = __fdiv_rn(y, m);
+                lpos[g * p.S + i] = make_float2(kx, ky);
+            }
+            __syncthreads();
+        }
         if (active && drawing) {
-            knn_scan<L, false>(lpos + g * p.S, p.N, p.k, p.ib, x, y, p.box, bd, bj);  // Euclidean (:100)
+            knn_scan<L, false>(lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj);  // Euclidean (:100)
             int coll = 0;
 #pragma unroll
             for (int s = 1; s < L - 1; ++s)
@@ -1349,7 +1390,7 @@ __global__ __launch_bounds__(1024) void reset_kernel(const Params p) {
     // check_distance to a LOWER-indexed agent re-draws its own position from a separate Philox stream, round after
     // round, until no pair is that close. The kNN + collision check of the reference then decides valid[] as for
     // a plain draw. Agent 0 never moves, so each round fixes at least the lowest conflicting index.
-    if (p.repair > 0 && __syncthreads_or(in_group && state[g])) {
+    if (p.repair > 0 && !p.normalize && __syncthreads_or(in_group && state[g])) {  // (host: repair 0 with normalize)
         const float2* lp = lpos + g * p.S;
         for (int round = 0; round < p.repair; ++round) {
             int bad = 0;
@@ -1447,7 +1488,7 @@ Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy, int G = 0) {
     c.T = ((c.G * N + 63) / 64) * 64;
     c.blocks = (E + c.G - 1) / c.G;
     if (reset)
-        c.lds = (size_t)c.G * c.S * sizeof(float2) + 2 * c.G * sizeof(int);
+        c.lds = (size_t)c.G * c.S * sizeof(float2) + 3 * c.G * sizeof(int);
     else
         c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + 2 * c.G * sizeof(int);
     if (!reset && cells) {  // ext (2N + 2 float4, 16-B aligned) + cnt + pre per env
@@ -1491,7 +1532,8 @@ int env_launches(int blocks, int requested) {
 // the specialised instantiations (step_kernel VAR / NC / SPL): the BASELINE configurations' per-GPU shapes
 template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1>
 bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
-    if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL)
+    if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL ||
+        p.normalize)
         return false;
     if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
     if (knobs().no_spec) return false;  // A/B diagnostics: the generic instantiation
@@ -1548,7 +1590,9 @@ void launch_reset_L(const Cfg& c, const Params& p, hipStream_t s) {
 
 int dispatch(Params& p, hipStream_t s, bool reset) {
     if (p.E == 0) return FLOCK_OK;
-    p.cells = (reset || knobs().no_cells) ? 0 : cell_grid(p.N, p.variant, &p.gx, &p.gy);
+    if (p.periodic) p.normalize = 0;  // the periodic kNN never normalises (gym_flock_v2.py:135-151)
+    // normalize_distance runs on the generic full-scan instantiations (a runtime flag there; launch_spec declines)
+    p.cells = (reset || knobs().no_cells || p.normalize) ? 0 : cell_grid(p.N, p.variant, &p.gx, &p.gy);
     if (p.cells) {
         p.ecap = 2 * p.N + 2;
         p.cwx = p.box / (float)p.gx;
@@ -1700,7 +1744,7 @@ int set_ring(Params& p, const FlockRing* ring, int E, int N, const char* who) {
 int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance, float dt,
                  float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
-                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds, int launches = 0) {
+                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds, int launches = 0, int normalize = 0) {
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done))
@@ -1726,6 +1770,7 @@ int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_rang
     p.any_done = any_done;
     p.seeds = seeds;
     p.launches = launches;
+    p.normalize = normalize != 0;  // Euclidean (periodic = 0, the RNN fork) only; dispatch clears it otherwise
     return dispatch(p, (hipStream_t)stream, false);
 }
 
@@ -1758,7 +1803,8 @@ int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor
                       uint8_t* done, uint8_t* any_done, const FlockStepExt* ext) {
     return step_v2_impl(stream, E, N, k, box, sensor_range, collision_distance, dt, v_min, v_max, periodic,
                         rigid_boundary, pos, heading, action, vel, dnn, nn_idx, reward, done, any_done,
-                        ext ? ext->ring : nullptr, ext ? ext->seeds : nullptr, ext ? ext->launches : 0);
+                        ext ? ext->ring : nullptr, ext ? ext->seeds : nullptr, ext ? ext->launches : 0,
+                        ext ? ext->normalize_distance : 0);
 }
 
 int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
@@ -1779,6 +1825,7 @@ int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor
     p.com_r = (float)((double)collision_distance * 4.0);  // collision_distance*4 (gym_flock_uw.py:197)
     p.seeds = ext ? ext->seeds : nullptr;
     p.launches = ext ? ext->launches : 0;
+    p.normalize = ext && ext->normalize_distance;
     p.dt = dt;
     p.pos = pos;
     p.heading = const_cast<float*>(heading);
@@ -1845,6 +1892,7 @@ int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, flo
     p.status = status;
     p.seeds = ext ? ext->seeds : nullptr;
     p.launches = ext ? ext->launches : 0;
+    p.normalize = ext && ext->normalize_distance;
     return dispatch(p, (hipStream_t)stream, false);
 }
 
@@ -1875,6 +1923,7 @@ int flock_step_flock_ext(void* stream, int E, int N, int k, float box, float col
     p.clamp = 0;  // gym_flock.py:105: no clamp
     p.seeds = ext ? ext->seeds : nullptr;
     p.launches = ext ? ext->launches : 0;
+    p.normalize = ext && ext->normalize_distance;
     p.cd = collision_distance;
     p.dt = dt;
     p.pos = pos;
@@ -1927,13 +1976,24 @@ int flock_reset_ext(void* stream, int variant, int E, int N, int k, float range_
                     float sensor_range, float check_distance, int rigid_boundary, int max_attempts, uint64_t seed,
                     uint64_t rng_offset, const uint8_t* env_mask, float* pos, float* heading, float* prev_heading,
                     float* vel, float* dnn, int64_t* nn_idx, float* mem, uint8_t* valid, int repair_rounds) {
+    return flock_reset_ext2(stream, variant, E, N, k, range_lo, range_hi, box, sensor_range, check_distance,
+                            rigid_boundary, max_attempts, seed, rng_offset, env_mask, pos, heading, prev_heading, vel,
+                            dnn, nn_idx, mem, valid, repair_rounds, 0);
+}
+
+int flock_reset_ext2(void* stream, int variant, int E, int N, int k, float range_lo, float range_hi, float box,
+                     float sensor_range, float check_distance, int rigid_boundary, int max_attempts, uint64_t seed,
+                     uint64_t rng_offset, const uint8_t* env_mask, float* pos, float* heading, float* prev_heading,
+                     float* vel, float* dnn, int64_t* nn_idx, float* mem, uint8_t* valid, int repair_rounds,
+                     int normalize_distance) {
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !dnn)) return fail(FLOCK_E_NULL, "flock_reset: NULL pointer");
     if (max_attempts < 1) return fail(FLOCK_E_ARG, "max_attempts must be >= 1");
     if (repair_rounds < 0) return fail(FLOCK_E_ARG, "repair_rounds must be >= 0");
     Params p = base(E, N, k, box);
-    p.repair = repair_rounds;
+    p.repair = normalize_distance ? 0 : repair_rounds;  // the repair stage works on raw distances
+    p.normalize = normalize_distance != 0;
     p.variant = variant;
     p.rigid = rigid_boundary != 0;
     p.sensor_range = sensor_range;

@@ -33,21 +33,19 @@ class SingleFlockEnv(_EnvBase):
     def __init__(self, agents, k, collision_distance, normalize_distance=False, rigid_boundary=False,
                  range_start=(0, 100), sensor_range=7, max_linear_velocity=2.5, desired_distance=15, *,
                  periodic=None, v_min=None, device=None, seed=0, max_reset_attempts=1024):
-        if normalize_distance:
-            # _computeDistances(normalize) (gym_flock_v2.py:157-163) is dead code in make_env (:424); not built.
-            raise NotImplementedError("normalize_distance=True is not supported by the HIP stepper")
         self.num_particles = agents
         self.k = k
         self.boundary = range_start[1]
         self.desired_distance = desired_distance
         self.range_start = range_start
-        self.normalize_distances = normalize_distance
         self._vec = VecFlockEnv(
             FlockConfig(variant=self.variant, num_envs=1, num_agents=agents, k=k,
                         collision_distance=collision_distance, range_start=tuple(range_start),
                         sensor_range=sensor_range, max_linear_velocity=max_linear_velocity,
                         rigid_boundary=rigid_boundary, periodic=periodic, v_min=v_min, seed=seed,
-                        max_reset_attempts=max_reset_attempts),
+                        max_reset_attempts=max_reset_attempts,
+                        # _computeDistances(normalize) (gym_flock_v2.py:157-163 and siblings)
+                        normalize_distance=bool(normalize_distance)),
             device=device or _default_device())
         self.device = self._vec.device
         # like the reference ctor (gym_flock_v2.py:54-57): random positions before the first reset
@@ -67,6 +65,9 @@ class SingleFlockEnv(_EnvBase):
     sensor_range = _param("sensor_range")
     rigid_boundary = _param("rigid_boundary")
     max_linear_velocity = _param("max_linear_velocity")
+    # the reference's attribute name (gym_flock_v2.py:52) over FlockConfig.normalize_distance
+    normalize_distances = property(lambda self: self._vec.cfg.normalize_distance,
+                                   lambda self, v: self._vec.set_param("normalize_distance", bool(v)))
 
     # ---- state views (shape as in the reference: (N, 2), (N,), (N, k)) --------------------------------------
     def _view(name):  # noqa: N805

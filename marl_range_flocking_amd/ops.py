@@ -54,17 +54,18 @@ def _check_k(N, k):
         raise RuntimeError("selected index k out of range")
 
 
-def _ext(ring=None, seeds=None, E=0, N=0, k=0, dev=None, launches=1):
+def _ext(ring=None, seeds=None, E=0, N=0, k=0, dev=None, launches=1, normalize=False):
     """FlockStepExt for the *_ext entry points, or None when there is nothing extra."""
     launches = int(launches)
     if launches < 1:
         raise ValueError("launches must be >= 1")
-    if ring is None and seeds is None and launches == 1:
+    if ring is None and seeds is None and launches == 1 and not normalize:
         return None
     if seeds is not None:
         _need(seeds, "seeds", torch.int16, (E, N, k), dev)
     return _native.FlockStepExt(ring=ctypes.pointer(ring) if ring is not None else None,
-                                seeds=_ptr(seeds) if seeds is not None else None, launches=launches)
+                                seeds=_ptr(seeds) if seeds is not None else None, launches=launches,
+                                normalize_distance=int(bool(normalize)))
 
 
 class StepPlan:
@@ -114,7 +115,7 @@ def _record(plan, lib_fn, name, args, ext, i_action, i_dt, i_rng=None):
 
 def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k, box, sensor_range,
             collision_distance, dt=0.1, v_min=0.005, v_max=2.5, periodic=True, rigid_boundary=False, ring=None,
-            seeds=None, plan=None, launches=1):
+            seeds=None, plan=None, launches=1, normalize=False):
     """gym_flock_v2.MultiAgentEnv.step (gym_flock_v2.py:71-83) for E envs; pos/heading updated in place.
     ring (a _native.FlockRing): also write every transition into a replay ring in the same launch
     (flock_step_v2_store; the store_transitions that follows each step in train_flock.py).
@@ -140,7 +141,7 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
     args = (_stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
             float(v_min), float(v_max), int(bool(periodic)), int(bool(rigid_boundary)), _ptr(pos), _ptr(heading),
             _ptr(action), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
-    ext = _ext(ring, seeds, E, N, k, dev, launches)
+    ext = _ext(ring, seeds, E, N, k, dev, launches, normalize)
     L = _native.lib()
     _record(plan, L.flock_step_v2 if ext is None else L.flock_step_v2_ext,
             "flock_step_v2" if ext is None else "flock_step_v2_ext", args, ext, 14, 7)
@@ -149,7 +150,8 @@ def step_v2(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, *, k
 
 
 def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done, *, k, box,
-            sensor_range, collision_distance, dt=0.1, rigid_boundary=False, seeds=None, plan=None, launches=1):
+            sensor_range, collision_distance, dt=0.1, rigid_boundary=False, seeds=None, plan=None, launches=1,
+            normalize=False):
     """gym_flock_uw.MultiAgentEnv.step (gym_flock_uw.py:69-81); mem_out = rolled 4-frame observation."""
     if _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
         return
@@ -171,7 +173,7 @@ def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_id
     args = (_stream(pos), E, N, k, float(box), float(sensor_range), float(collision_distance), float(dt),
             int(bool(rigid_boundary)), _ptr(pos), _ptr(heading), _ptr(prev_heading), _ptr(action), _ptr(mem_in),
             _ptr(mem_out), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done))
-    ext = _ext(None, seeds, E, N, k, dev, launches)
+    ext = _ext(None, seeds, E, N, k, dev, launches, normalize)
     L = _native.lib()
     _record(plan, L.flock_step_uw if ext is None else L.flock_step_uw_ext,
             "flock_step_uw" if ext is None else "flock_step_uw_ext", args, ext, 12, 7)
@@ -179,7 +181,8 @@ def step_uw(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_id
 
 def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                      status=None, *, k, box, sensor_range, collision_distance, dt=0.1, v_max=2.5, rigid_boundary=False,
-                     noise_std=0.1, seed=0, rng_offset=0, seeds=None, plan=None, launches=1, ring=None):
+                     noise_std=0.1, seed=0, rng_offset=0, seeds=None, plan=None, launches=1, ring=None,
+                     normalize=False):
     """gym_flock_uw_discrete.MultiAgentEnv.step (gym_flock_uw_discrete.py:110-122). noise=None → in-kernel
     Philox N(0, noise_std) draws; otherwise noise [E,N,2] is added to the action-table means (parity mode).
     plan (StepPlan, optional; in-kernel noise only): record / replay the validated launch over the same buffers.
@@ -213,7 +216,7 @@ def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, d
             _ptr(noise), float(noise_std), int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(table),
             int(table.shape[0]), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(reward), _ptr(done), _ptr(any_done),
             _ptr(status))
-    ext = _ext(ring, seeds, E, N, k, dev, launches)
+    ext = _ext(ring, seeds, E, N, k, dev, launches, normalize)
     L = _native.lib()
     _record(plan if noise is None else None, L.flock_step_uw_discrete if ext is None else L.flock_step_uw_discrete_ext,
             "flock_step_uw_discrete" if ext is None else "flock_step_uw_discrete_ext", args, ext, 13, 7, 17)
@@ -222,7 +225,7 @@ def step_uw_discrete(pos, heading, prev_heading, action_id, noise, table, vel, d
 
 
 def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, *, k, box, collision_distance,
-               dt=0.1, rigid_boundary=False, seeds=None, plan=None, launches=1):
+               dt=0.1, rigid_boundary=False, seeds=None, plan=None, launches=1, normalize=False):
     """gym_flock.MultiAgentEnv.step (gym_flock.py:48-60); vel is the unit-velocity state (rw)."""
     if _planned(plan, pos, action, "action", torch.float32, tuple(pos.shape), dt):
         return
@@ -242,7 +245,7 @@ def step_flock(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any
     args = (_stream(pos), E, N, k, float(box), float(collision_distance), float(dt), int(bool(rigid_boundary)),
             _ptr(pos), _ptr(vel), _ptr(action), _ptr(mem_in), _ptr(mem_out), _ptr(dnn), _ptr(nn_idx), _ptr(reward),
             _ptr(done), _ptr(any_done))
-    ext = _ext(None, seeds, E, N, k, dev, launches)
+    ext = _ext(None, seeds, E, N, k, dev, launches, normalize)
     L = _native.lib()
     _record(plan, L.flock_step_flock if ext is None else L.flock_step_flock_ext,
             "flock_step_flock" if ext is None else "flock_step_flock_ext", args, ext, 10, 6)
@@ -270,9 +273,10 @@ VARIANT_IDS = {"v2": 0, "uw": 1, "uw_discrete": 2, "flock": 3}
 
 def reset(variant, pos, dnn, *, k, range_start, box, sensor_range, check_distance, heading=None, prev_heading=None,
           vel=None, nn_idx=None, mem=None, valid=None, env_mask=None, rigid_boundary=False, max_attempts=64, seed=0,
-          rng_offset=0, repair_rounds=0):
+          rng_offset=0, repair_rounds=0, normalize=False):
     """Device-side reset with bounded rejection sampling (reference reset() recursion, e.g. gym_flock_v2.py:85-108);
-    repair_rounds > 0: envs whose every draw collided re-draw only their colliding agents (flock_reset_ext)."""
+    repair_rounds > 0: envs whose every draw collided re-draw only their colliding agents (flock_reset_ext).
+    normalize: normalize_distance=True (the collision check and observation on positions / max |p|; no repair)."""
     E, N, dev = _dims(pos)
     _check_k(N, k)
     f32 = torch.float32
@@ -285,9 +289,10 @@ def reset(variant, pos, dnn, *, k, range_start, box, sensor_range, check_distanc
     _opt(mem, "mem", f32, (E, N, 4, k), dev)
     _opt(valid, "valid", torch.bool, (E,), dev)
     _opt(env_mask, "env_mask", torch.bool, (E,), dev)
-    rc = _native.lib().flock_reset_ext(
+    rc = _native.lib().flock_reset_ext2(
         _stream(pos), VARIANT_IDS[variant], E, N, k, float(range_start[0]), float(range_start[1]), float(box),
         float(sensor_range), float(check_distance), int(bool(rigid_boundary)), int(max_attempts),
         int(seed) & (2**64 - 1), int(rng_offset) & (2**64 - 1), _ptr(env_mask), _ptr(pos), _ptr(heading),
-        _ptr(prev_heading), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(mem), _ptr(valid), int(repair_rounds))
-    _native.check(rc, "flock_reset_ext")
+        _ptr(prev_heading), _ptr(vel), _ptr(dnn), _ptr(nn_idx), _ptr(mem), _ptr(valid), int(repair_rounds),
+        int(bool(normalize)))
+    _native.check(rc, "flock_reset_ext2")

@@ -45,6 +45,9 @@ class FlockConfig:
     # block slots the first launch's tail frees
     step_launches: int = 1
     reset_check_distance: float = None  # uw_discrete resets with collision_distance = 4 (:145)
+    # normalize_distance=True of the reference constructors: the kNN on positions / max |p| per env (Euclidean steps
+    # and every reset; the periodic v2 step never normalises). Runs the full-scan kernels through the C ABI
+    normalize_distance: bool = False
     extra: dict = field(default_factory=dict)
 
     def resolved(self):
@@ -117,11 +120,11 @@ class VecFlockEnv:
 
     def set_param(self, name, value):
         """Change a step / reset parameter (collision_distance, sensor_range, rigid_boundary, max_linear_velocity,
-        v_min, dt, step_launches) between steps: the recorded launch plans hold the old scalars, so they are dropped. The reset
+        v_min, dt, step_launches, normalize_distance) between steps: the recorded launch plans hold the old scalars, so they are dropped. The reset
         check distance follows collision_distance (gym_flock_v2.py:100-105) except for uw_discrete, whose reset
         checks with 4 (gym_flock_uw_discrete.py:145)."""
         if name not in ("collision_distance", "sensor_range", "rigid_boundary", "max_linear_velocity", "v_min", "dt",
-                        "step_launches"):
+                        "step_launches", "normalize_distance"):
             raise AttributeError(f"{name} is not a runtime parameter")
         if name == "step_launches" and int(value) < 1:
             raise ValueError("step_launches must be >= 1")
@@ -164,7 +167,7 @@ class VecFlockEnv:
         if env_mask is not None:
             env_mask = env_mask.to(device=self.device, dtype=torch.bool).contiguous()
         heading = self.headings if c.variant != "flock" else None
-        if self._torch_ops is not None:
+        if self._torch_ops is not None and not c.normalize_distance:
             self._torch_ops.reset(self.positions, b["dnn"], heading, self.prev_headings, self.velocities, b["idx"],
                                   b["mem"], self.valid, env_mask, ops.VARIANT_IDS[c.variant], self.k,
                                   float(c.range_start[0]), float(c.range_start[1]), self.box, c.sensor_range,
@@ -176,7 +179,7 @@ class VecFlockEnv:
                       prev_heading=self.prev_headings, vel=self.velocities, nn_idx=b["idx"], mem=b["mem"],
                       valid=self.valid, env_mask=env_mask, rigid_boundary=c.rigid_boundary,
                       max_attempts=c.max_reset_attempts, seed=c.seed, rng_offset=self._rng_offset,
-                      repair_rounds=c.reset_repair_rounds)
+                      repair_rounds=c.reset_repair_rounds, normalize=c.normalize_distance)
         self._rng_offset += max(c.max_reset_attempts, c.reset_repair_rounds)
         if self.seeds is not None and b["idx"] is not None:  # the reset's neighbours seed the first step
             self.seeds.copy_(b["idx"])
@@ -256,12 +259,12 @@ class VecFlockEnv:
         if plan is None:
             plan = plans[pkey] = ops.StepPlan()
         common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
-                      rigid_boundary=c.rigid_boundary, plan=plan)
+                      rigid_boundary=c.rigid_boundary, plan=plan, normalize=c.normalize_distance)
         if ring is not None:
             if c.variant not in ("v2", "uw_discrete"):
                 raise NotImplementedError("the fused replay insert is built for the v2 and uw_discrete steps")
             ring.prev_obs = src["dnn"].data_ptr()
-        T = self._torch_ops if ring is None and c.step_launches <= 1 else None
+        T = self._torch_ops if ring is None and c.step_launches <= 1 and not c.normalize_distance else None
         if T is not None:
             self._step_torch(T, a, noise, dt, src, dst)
         elif c.variant == "v2":

@@ -89,14 +89,31 @@ static float pair_d2(float xi, float yi, float xj, float yj, float box, int peri
  * clamp != 0 → distances clamped to [0, sensor_range] (v2/uw/uw_discrete); 0 → unclamped (gym_flock.py:105).
  * Returns -1 if k+1 > N (the reference's topk raises "selected index k out of range").
  */
+/* normalize_distance=True of the reference constructors (test switch, set by oracle.py around a call): the
+ * Euclidean kNN runs on positions / max_i torch.norm(p_i) of each env (gym_flock_v2.py:157-163, gym_flock_uw.py:127-133,
+ * gym_flock_uw_discrete.py:175-181, gym_flock.py:94-98). The periodic kNN never normalises. */
+static int g_normalize = 0;
+void oracle_set_normalize(int on) { g_normalize = on != 0; }
+
 int oracle_knn(int E, int N, int k, float box, float sensor_range, int periodic, int clamp,
                const float* pos, float* dnn, int64_t* idx) {
     if (k + 1 > N || k < 1) return -1;
     int L = k + 1;
     float* bd = (float*)malloc(sizeof(float) * L);
     int* bj = (int*)malloc(sizeof(int) * L);
+    float* qn = (float*)malloc(sizeof(float) * 2 * (size_t)N);
     for (int e = 0; e < E; ++e) {
         const float* P = pos + (size_t)e * N * 2;
+        if (g_normalize && !periodic) {
+            float m = 0.0f;
+            for (int i = 0; i < N; ++i) {
+                float sx = P[2 * i] * P[2 * i], sy = P[2 * i + 1] * P[2 * i + 1];
+                float n = sqrtf(sx + sy); /* torch.norm(positions, dim=1) */
+                m = (n > m) ? n : m;       /* torch.max(magnitudes) */
+            }
+            for (int i = 0; i < 2 * N; ++i) qn[i] = P[i] / m; /* positions / max */
+            P = qn;
+        }
         for (int i = 0; i < N; ++i) {
             int cnt = 0;
             for (int j = 0; j < N; ++j) {
@@ -124,6 +141,7 @@ int oracle_knn(int E, int N, int k, float box, float sensor_range, int periodic,
     }
     free(bd);
     free(bj);
+    free(qn);
     return 0;
 }
 

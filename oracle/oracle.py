@@ -46,13 +46,27 @@ def _p(a):
 _I, _F = ctypes.c_int, ctypes.c_float
 
 
-def knn(pos, k, box, sensor_range=14.0, periodic=True, clamp=True):
+class _normalized:
+    """normalize_distance=True around one oracle call (oracle_set_normalize; the C switch is process-global)."""
+
+    def __init__(self, on):
+        self.on = bool(on)
+
+    def __enter__(self):
+        lib().oracle_set_normalize(_I(int(self.on)))
+
+    def __exit__(self, *exc):
+        lib().oracle_set_normalize(_I(0))
+
+
+def knn(pos, k, box, sensor_range=14.0, periodic=True, clamp=True, normalize=False):
     pos = _f(pos)
     E, N = pos.shape[:2]
     dnn = np.zeros((E, N, k), np.float32)
     idx = np.zeros((E, N, k), np.int64)
-    rc = lib().oracle_knn(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _I(int(periodic)), _I(int(clamp)),
-                          _p(pos), _p(dnn), _p(idx))
+    with _normalized(normalize):
+        rc = lib().oracle_knn(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _I(int(periodic)), _I(int(clamp)),
+                              _p(pos), _p(dnn), _p(idx))
     if rc != 0:
         raise RuntimeError("selected index k out of range")
     return dnn, idx
@@ -65,11 +79,12 @@ def _outs(E, N, k):
 
 
 def step_v2(pos, heading, action, *, k, box, sensor_range=14.0, cd=2.5, dt=0.1, v_min=0.005, v_max=2.5,
-            periodic=True, rigid=False):
+            periodic=True, rigid=False, normalize=False):
     pos, heading, action = _f(pos).copy(), _f(heading).copy(), _f(action)
     E, N = heading.shape
     o = _outs(E, N, k)
-    rc = lib().oracle_step_v2(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _F(cd), _F(dt), _F(v_min),
+    with _normalized(normalize):
+        rc = lib().oracle_step_v2(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _F(cd), _F(dt), _F(v_min),
                               _F(v_max), _I(int(periodic)), _I(int(rigid)), _p(pos), _p(heading), _p(action),
                               _p(o["vel"]), _p(o["dnn"]), _p(o["idx"]), _p(o["reward"]), _p(o["done"]),
                               _p(o["any_done"]))
@@ -79,13 +94,15 @@ def step_v2(pos, heading, action, *, k, box, sensor_range=14.0, cd=2.5, dt=0.1, 
     return o
 
 
-def step_uw(pos, heading, prev_heading, action, mem, *, k, box, sensor_range=14.0, cd=2.5, dt=0.1, rigid=False):
+def step_uw(pos, heading, prev_heading, action, mem, *, k, box, sensor_range=14.0, cd=2.5, dt=0.1, rigid=False,
+            normalize=False):
     pos, heading, prev = _f(pos).copy(), _f(heading).copy(), _f(prev_heading).copy()
     action, mem = _f(action), _f(mem)
     E, N = heading.shape
     o = _outs(E, N, k)
     mem_out = np.zeros((E, N, 4, k), np.float32)
-    rc = lib().oracle_step_uw(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _F(cd), _F(dt), _I(int(rigid)),
+    with _normalized(normalize):
+        rc = lib().oracle_step_uw(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _F(cd), _F(dt), _I(int(rigid)),
                               _p(pos), _p(heading), _p(prev), _p(action), _p(mem), _p(mem_out), _p(o["vel"]),
                               _p(o["dnn"]), _p(o["idx"]), _p(o["reward"]), _p(o["done"]), _p(o["any_done"]))
     if rc != 0:
@@ -95,13 +112,14 @@ def step_uw(pos, heading, prev_heading, action, mem, *, k, box, sensor_range=14.
 
 
 def step_uwd(pos, heading, prev_heading, action, noise, *, k, box, sensor_range=14.0, cd=3.0, dt=0.1, v_max=2.5,
-             rigid=False, table=UWD_TABLE):
+             rigid=False, table=UWD_TABLE, normalize=False):
     pos, heading, prev = _f(pos).copy(), _f(heading).copy(), _f(prev_heading).copy()
     action = np.ascontiguousarray(action, dtype=np.int64)
     noise, table = _f(noise), _f(table)
     E, N = heading.shape
     o = _outs(E, N, k)
-    rc = lib().oracle_step_uwd(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _F(cd), _F(dt), _F(v_max),
+    with _normalized(normalize):
+        rc = lib().oracle_step_uwd(_I(E), _I(N), _I(k), _F(box), _F(sensor_range), _F(cd), _F(dt), _F(v_max),
                                _I(int(rigid)), _p(pos), _p(heading), _p(prev), _p(action), _p(noise), _p(table),
                                _I(table.shape[0]), _p(o["vel"]), _p(o["dnn"]), _p(o["idx"]), _p(o["reward"]),
                                _p(o["done"]), _p(o["any_done"]))
@@ -113,12 +131,13 @@ def step_uwd(pos, heading, prev_heading, action, noise, *, k, box, sensor_range=
     return o
 
 
-def step_flock(pos, vel, action, mem, *, k, box, cd=2.5, dt=0.1, rigid=False):
+def step_flock(pos, vel, action, mem, *, k, box, cd=2.5, dt=0.1, rigid=False, normalize=False):
     pos, vel, action, mem = _f(pos).copy(), _f(vel).copy(), _f(action), _f(mem)
     E, N = pos.shape[:2]
     o = _outs(E, N, k)
     mem_out = np.zeros((E, N, 4, k), np.float32)
-    rc = lib().oracle_step_flock(_I(E), _I(N), _I(k), _F(box), _F(cd), _F(dt), _I(int(rigid)), _p(pos), _p(vel),
+    with _normalized(normalize):
+        rc = lib().oracle_step_flock(_I(E), _I(N), _I(k), _F(box), _F(cd), _F(dt), _I(int(rigid)), _p(pos), _p(vel),
                                  _p(action), _p(mem), _p(mem_out), _p(o["dnn"]), _p(o["idx"]), _p(o["reward"]),
                                  _p(o["done"]), _p(o["any_done"]))
     if rc != 0:

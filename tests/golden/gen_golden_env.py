@@ -65,7 +65,7 @@ def _boundary_rows(rng, pos, head, box, variant):
         head[3] = np.float32(-np.pi / 2)
 
 
-def gen_traj(mods, variant, N, k, E, T, box, cd=2.5, sr=14.0, seed=0, tag=""):
+def gen_traj(mods, variant, N, k, E, T, box, cd=2.5, sr=14.0, seed=0, tag="", normalize=False):
     import torch
 
     rng = np.random.default_rng(seed)
@@ -109,6 +109,8 @@ def gen_traj(mods, variant, N, k, E, T, box, cd=2.5, sr=14.0, seed=0, tag=""):
     orig_normal = torch.normal
     for e in range(E):
         env_kw = dict(agents=N, k=k, collision_distance=cd, range_start=(0, box))
+        if normalize:  # _computeDistances on positions / max |p| (gym_flock_uw.py:127-133 and siblings)
+            env_kw["normalize_distance"] = True
         if variant != "flock":
             env_kw["sensor_range"] = sr
         env = mod.MultiAgentEnv(**env_kw)
@@ -163,7 +165,7 @@ def gen_traj(mods, variant, N, k, E, T, box, cd=2.5, sr=14.0, seed=0, tag=""):
     np.savez_compressed(
         os.path.join(OUT, name),
         meta=np.array(_meta(variant=variant, N=N, k=k, E=E, T=T, box=box, collision_distance=cd,
-                            sensor_range=sr, dt=0.1, v_min=v_min, seed=seed)),
+                            sensor_range=sr, dt=0.1, v_min=v_min, seed=seed, normalize_distance=normalize)),
         pos0=pos0, head0=head0, prevh0=prevh0, mem0=mem0, vel0=vel0, actions=act, noise=noise,
         **out,
     )
@@ -217,11 +219,23 @@ def gen_errors(mods):
     print("errors:", msg)
 
 
+def gen_normalized(mods):
+    """normalize_distance=True (the Euclidean steps: uw, uw_discrete, gym_flock, the RNN fork of v2). Collision
+    distances are in normalised units (distances are <= 2 there)."""
+    gen_traj(mods, "uw", N=16, k=4, E=2, T=4, box=45, cd=0.05, seed=30, tag="_norm", normalize=True)
+    gen_traj(mods, "uwd", N=16, k=4, E=2, T=4, box=45, cd=0.05, seed=31, tag="_norm", normalize=True)
+    gen_traj(mods, "flock", N=16, k=4, E=2, T=4, box=45, cd=0.05, seed=32, tag="_norm", normalize=True)
+    gen_traj(mods, "v2fork", N=64, k=4, E=2, T=3, box=126, cd=0.02, seed=33, tag="_norm", normalize=True)
+
+
 def main():
     if not refshim.available():
         print("reference not present; nothing to do")
         return
     mods = _mods()
+    if "--normalized" in sys.argv:  # only the normalize_distance fixtures
+        gen_normalized(mods)
+        return
     # config-1-like plumbing + long trajectories
     gen_traj(mods, "flock", N=8, k=4, E=3, T=20, box=45, seed=1)
     gen_traj(mods, "v2", N=8, k=4, E=3, T=20, box=45, seed=2)
@@ -244,6 +258,7 @@ def main():
     gen_sense(mods, N=64, k=4, E=1, box=64, seed=21, lattice=True, tag="_lattice")
     gen_sense(mods, N=256, k=4, E=1, box=253, seed=22)
     gen_errors(mods)
+    gen_normalized(mods)
 
 
 if __name__ == "__main__":

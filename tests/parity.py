@@ -29,6 +29,15 @@ def d2_rows(pos, box, periodic):
     return (dx * dx).astype(np.float32) + (dy * dy).astype(np.float32)
 
 
+def knn_positions(pos, m):
+    """The positions the kNN ranks: pos / max |p| per env under normalize_distance (gym_flock_uw.py:127-133)."""
+    p = np.asarray(pos, np.float32)
+    if not m.get("normalize_distance", False):
+        return p
+    mag = np.sqrt((p[..., 0] * p[..., 0]).astype(np.float32) + (p[..., 1] * p[..., 1]).astype(np.float32))
+    return (p / mag.max(-1)[:, None, None]).astype(np.float32)
+
+
 def knn_mismatch(ref_idx, our_idx, D, tie_ulp=TIE_ULP):
     """Compare two [E,N,k] index arrays given distances D [E,N,N] (any monotone distance works).
 
@@ -59,10 +68,10 @@ def allclose_rel(a, b, rtol=RTOL, atol=0.0):
     return bool(ok.all()), (np.nanmax(np.abs(a - b) / np.maximum(np.abs(b), 1e-30)) if a.size else 0.0)
 
 
-def _knn_exact(pos, k, box, sr, periodic, clamp, gdnn, gidx):
+def _knn_exact(pos, k, box, sr, periodic, clamp, gdnn, gidx, normalize=False):
     """GPU kNN (distances and indices) bitwise equal to the C oracle's exact (d2, j) order on the same positions."""
     from oracle import oracle as O
 
-    dnn, idx = O.knn(pos, k, box, sr, periodic=periodic, clamp=clamp)
+    dnn, idx = O.knn(pos, k, box, sr, periodic=periodic, clamp=clamp, normalize=normalize)
     np.testing.assert_array_equal(gidx, idx)
     np.testing.assert_array_equal(gdnn, dnn)

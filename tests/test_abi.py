@@ -107,17 +107,18 @@ def test_shared_critic_round_and_pipeline_argument_checks(lib):
 
 
 def test_step_ext_layout_and_launches_option():
-    """FlockStepExt mirrors the header ({ring*, seeds*, int launches}: 24 bytes on x86-64); step_launches < 1 is
-    rejected by FlockConfig and by the ext builder before any launch."""
+    """FlockStepExt mirrors the header ({ring*, seeds*, int launches, int normalize_distance}: 24 bytes on x86-64);
+    step_launches < 1 is rejected by FlockConfig and by the ext builder before any launch."""
     from marl_range_flocking_amd import FlockConfig, _native, ops
 
     assert ctypes.sizeof(_native.FlockStepExt) == 24
-    assert [f[0] for f in _native.FlockStepExt._fields_] == ["ring", "seeds", "launches"]
+    assert [f[0] for f in _native.FlockStepExt._fields_] == ["ring", "seeds", "launches", "normalize_distance"]
     header = open(os.path.join(INCLUDE, "flock_amd.h")).read()
     body = header[header.index("typedef struct FlockStepExt"):header.index("} FlockStepExt;")]
-    assert "int launches;" in body
+    assert "int launches;" in body and body.index("int launches;") < body.index("int normalize_distance;")
     with pytest.raises(ValueError):
         FlockConfig(step_launches=0).resolved()
     with pytest.raises(ValueError):
         ops._ext(launches=0)
     assert ops._ext() is None and ops._ext(launches=2).launches == 2
+    assert ops._ext(normalize=True).normalize_distance == 1

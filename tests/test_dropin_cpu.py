@@ -49,7 +49,11 @@ def test_learner_shims_import_under_reference_paths(path, name, attr):
     assert hasattr(m, attr)
 
 
-def test_normalize_distance_rejected():
-    m = _imp(os.path.join(PKG, "environments"), "gym_flock_v2")
-    with pytest.raises(NotImplementedError):
-        m.MultiAgentEnv(10, 4, 2.5, normalize_distance=True)
+def test_normalize_distance_reaches_the_config():
+    """normalize_distance=True is accepted (gym_flock_v2.py:26) and becomes FlockConfig.normalize_distance; the
+    device step itself is covered by tests/test_gpu_env_parity.py (no GPU here: construction needs the device)."""
+    from marl_range_flocking_amd import FlockConfig
+
+    assert FlockConfig(normalize_distance=True).resolved().normalize_distance is True
+    src = open(os.path.join(PKG, "environments", "_base.py")).read()
+    assert "normalize_distance=bool(normalize_distance)" in src

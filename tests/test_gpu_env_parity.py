@@ -16,7 +16,7 @@ import torch
 
 from marl_range_flocking_amd import FlockConfig, VecFlockEnv, ops
 from oracle import oracle as O
-from parity import _knn_exact, allclose_rel, d2_rows, knn_mismatch, meta
+from parity import _knn_exact, allclose_rel, d2_rows, knn_mismatch, knn_positions, meta
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -28,7 +28,8 @@ def _env(m, E, device):
     return VecFlockEnv(FlockConfig(variant=VARIANT[v], num_envs=E, num_agents=m["N"], k=m["k"],
                                    collision_distance=m["collision_distance"], range_start=(0, m["box"]),
                                    sensor_range=m.get("sensor_range", 14.0), periodic=(v == "v2"),
-                                   v_min=m.get("v_min", 0.005)), device=device)
+                                   v_min=m.get("v_min", 0.005),
+                                   normalize_distance=m.get("normalize_distance", False)), device=device)
 
 
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "env_*.npz"))),
@@ -71,11 +72,11 @@ def test_step_matches_reference_and_oracle(path, cuda):
             assert ok, f"obs memory {err}"
         gidx = env.nn_idx.cpu().numpy()
         if v in ("v2", "v2fork"):
-            _, _, bad = knn_mismatch(z["nn_idx"][t], gidx, d2_rows(z["pos"][t], m["box"], periodic))
+            _, _, bad = knn_mismatch(z["nn_idx"][t], gidx, d2_rows(knn_positions(z["pos"][t], m), m["box"], periodic))
             assert not bad, f"t={t} indices vs reference beyond ties: {bad[:4]}"
         # bit-exact kNN against the oracle on the GPU's own positions
         _knn_exact(gpos, k, m["box"], m.get("sensor_range", 14.0), periodic, v != "flock", env.dnn.cpu().numpy(),
-                   gidx)
+                   gidx, normalize=m.get("normalize_distance", False))
 
 
 @pytest.mark.parametrize("N,k", [(2, 1), (5, 4), (8, 4), (64, 4), (100, 7), (256, 4), (257, 3), (512, 4),
@@ -280,3 +281,83 @@ def test_uw_discrete_bad_action_flags_status(cuda):
 def test_k_out_of_range_raises(cuda):
     with pytest.raises(RuntimeError, match="selected index k out of range"):
         ops.knn(torch.zeros(1, 4, 2, device=cuda), 4, 10.0)
+
+
+@pytest.mark.parametrize("variant", ["v2", "uw", "uw_discrete", "flock"])
+@pytest.mark.parametrize("N", [16, 300])
+def test_normalize_distance_step_and_reset_vs_oracle(variant, N, cuda):
+    """normalize_distance=True (gym_flock_uw.py:125-133 and siblings; the v2 RNN fork is v2 with periodic=False):
+    the step's kNN on positions / max |p| of each env, bit-exact against the oracle on the GPU's own positions, the
+    float state within rtol 1e-5; reset()'s collision check and observation on the same normalised kNN. N = 300
+    takes the one-env-per-block reduction over a non-power-of-two swarm (the cell list is off under normalize)."""
+    E, k, box = 3, 4, 60.0
+    rng = np.random.default_rng(N)
+    cfg = FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=0.01, range_start=(0, box),
+                      sensor_range=14.0, periodic=False, normalize_distance=True, reset_check_distance=1e-4)
+    env = VecFlockEnv(cfg, device=cuda)
+    pos = rng.uniform(0, box, (E, N, 2)).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    prev = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    vel = rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)
+    mem = rng.uniform(0, 1, (E, N, 4, k)).astype(np.float32)
+    has_mem = variant in ("uw", "flock")
+    env.set_state(positions=pos, headings=head, prev_headings=prev, velocities=vel, obs_memory=mem if has_mem else None)
+    kw = dict(k=k, box=box, cd=0.01, normalize=True)
+    if variant == "uw_discrete":
+        act = rng.integers(0, 10, (E, N)).astype(np.int64)
+        noise = (0.1 * rng.standard_normal((E, N, 2))).astype(np.float32)
+        env.step(torch.from_numpy(act), noise=torch.from_numpy(noise))
+        ref = O.step_uwd(pos, head, prev, act, noise, sensor_range=14.0, **kw)
+    else:
+        act = rng.uniform(-1, 1, (E, N, 2)).astype(np.float32)
+        env.step(torch.from_numpy(act))
+        if variant == "v2":
+            ref = O.step_v2(pos, head, act, sensor_range=14.0, periodic=False, **kw)
+        elif variant == "uw":
+            ref = O.step_uw(pos, head, prev, act, mem, sensor_range=14.0, **kw)
+        else:
+            ref = O.step_flock(pos, vel, act, mem, **kw)
+    torch.cuda.synchronize()
+    gpos = env.positions.cpu().numpy()
+    ok, err = allclose_rel(gpos, ref["pos"])
+    assert ok, f"positions rel err {err}"
+    gd, gi = env.dnn.cpu().numpy(), env.nn_idx.cpu().numpy()
+    assert float(gd.max()) <= 2.0 + 1e-6, "normalised distances are at most 2"
+    _knn_exact(gpos, k, box, 14.0, False, variant != "flock", gd, gi, normalize=True)
+    dn, _ = O.knn(gpos, k, box, 14.0, periodic=False, clamp=variant != "flock", normalize=True)
+    np.testing.assert_array_equal(env.done.cpu().numpy(), (dn < 0.01).any(-1))
+    np.testing.assert_array_equal(env.any_done.cpu().numpy(), (dn < 0.01).any(-1).any(-1))
+    if variant != "uw":  # uw's reward mixes in the centre-of-mass term: float state checked against the oracle
+        np.testing.assert_array_equal(env.reward.cpu().numpy(), ref["reward"])
+    else:
+        ok, err = allclose_rel(env.reward.cpu().numpy(), ref["reward"])
+        assert ok, f"uw reward {err}"
+    # reset: bounded draws judged on the normalised kNN; the observation is that kNN of the new positions
+    env.reset()
+    torch.cuda.synchronize()
+    rpos = env.positions.cpu().numpy()
+    dn, ix = O.knn(rpos, k, box, 14.0, periodic=False, clamp=variant != "flock", normalize=True)
+    np.testing.assert_array_equal(env.dnn.cpu().numpy(), dn)
+    np.testing.assert_array_equal(env.nn_idx.cpu().numpy(), ix)
+    np.testing.assert_array_equal(env.valid.cpu().numpy(), ~(dn < 1e-4).any(-1).any(-1))
+
+
+def test_dropin_normalize_distance(cuda):
+    """gym_flock_uw.MultiAgentEnv(normalize_distance=True) (gym_flock_uw.py:40-51): the constructor flag reaches the
+    device step; distances_to_nearest_neighbors are the normalised kNN of the env's positions."""
+    from marl_range_flocking_amd.environments import gym_flock_uw
+
+    env = gym_flock_uw.MultiAgentEnv(agents=12, k=4, collision_distance=0.001, normalize_distance=True,
+                                     range_start=(0, 50), sensor_range=7)
+    assert env.normalize_distances is True
+    env.reset()
+    env.step(torch.rand(12, 2, device=env.device) * 2 - 1)
+    torch.cuda.synchronize()
+    pos = env.positions.cpu().numpy()[None]
+    dn, ix = O.knn(pos, 4, 50.0, 7.0, periodic=False, clamp=True, normalize=True)
+    np.testing.assert_array_equal(env.distances_to_nearest_neighbors.cpu().numpy(), dn[0])
+    env.normalize_distances = False  # writes through: the next step senses raw distances
+    env.step(torch.rand(12, 2, device=env.device) * 2 - 1)
+    torch.cuda.synchronize()
+    dn, _ = O.knn(env.positions.cpu().numpy()[None], 4, 50.0, 7.0, periodic=False, clamp=True)
+    np.testing.assert_array_equal(env.distances_to_nearest_neighbors.cpu().numpy(), dn[0])

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from parity import RTOL, allclose_rel, d2_rows, knn_mismatch, meta
+from parity import RTOL, allclose_rel, d2_rows, knn_mismatch, knn_positions, meta
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 ENV_FIXTURES = sorted(glob.glob(os.path.join(GOLD, "env_*.npz")))
@@ -20,7 +20,7 @@ ENV_FIXTURES = sorted(glob.glob(os.path.join(GOLD, "env_*.npz")))
 
 def oracle_step(m, z, t, pos, head, prev, vel, mem):
     v, k = m["variant"], m["k"]
-    kw = dict(k=k, box=m["box"], cd=m["collision_distance"])
+    kw = dict(k=k, box=m["box"], cd=m["collision_distance"], normalize=m.get("normalize_distance", False))
     if v in ("v2", "v2fork"):
         return O.step_v2(pos, head, z["actions"][t], sensor_range=m["sensor_range"], v_min=m["v_min"],
                          periodic=(v == "v2"), **kw)
@@ -49,7 +49,7 @@ def test_oracle_matches_reference_teacher_forced(path):
         ok, err = allclose_rel(o["dnn"], z["dnn"][t], atol=1e-12)
         assert ok, f"t={t} dnn rel err {err}"
         if v in ("v2", "v2fork"):
-            D = d2_rows(z["pos"][t], m["box"], periodic=(v == "v2"))
+            D = d2_rows(knn_positions(z["pos"][t], m), m["box"], periodic=(v == "v2"))
             _, _, bad = knn_mismatch(z["nn_idx"][t], o["idx"], D)
             assert not bad, f"t={t} neighbour indices differ beyond ties at rows {bad[:5]}"
         np.testing.assert_array_equal(o["reward"], z["reward"][t])
