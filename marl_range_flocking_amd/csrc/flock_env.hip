@@ -69,7 +69,6 @@ struct Params {
     int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
     int launches;  // FlockStepExt.launches: the step as this many launches over env ranges (0: the diagnostics knob)
     int variant, periodic, rigid, clamp;
-    int normalize;  // normalize_distance: Euclidean kNN of positions / max_e |p| (full-scan path only, see dispatch)
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
     uint64_t seed, rng_offset;
     int n_actions;
@@ -104,6 +103,7 @@ struct Params {
     int max_attempts, repair;
     const uint8_t* env_mask;
     uint8_t* valid;
+    int normalize;  // normalize_distance: Euclidean kNN of positions / max_e |p| (full-scan path only, see dispatch)
 };
 
 // ---------------------------------------------------------------------------------------------------------------
