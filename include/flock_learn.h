@@ -63,6 +63,16 @@ int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs
                       const float* w_hh, const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb,
                       float* dgi, float* dw_hh, float* db_hh);
 
+/* VDN QNet feature chain of A agents, R rows each (learners/vdn/net.py:19-33; replaces the three per-agent Linear
+ * layers and two ReLUs before the GRUCell, train_flock.py:23-27 runs them per chunk step):
+ *   y1 = relu(x w1^T + b1) [64], y2 = relu(y1 w2^T + b2) [32], gi = y2 w_ih^T + b_ih [96]
+ * x element (a, c, b, f) at x[a*x_sa + c*x_sc + b*x_sb + f] with row r = c*B + b (R = C*B); w1 [A][64][n_in],
+ * b1 [A][64], w2 [A][32][64], b2 [A][32], w_ih [A][96][32], b_ih [A][96] contiguous. Out: gi [A][R][96];
+ * y1 [A][R][64] and y2 [A][R][32] (the post-ReLU activations the backward needs; each may be NULL). 1 <= n_in <= 16. */
+int flock_vdn_feat_fwd(void* stream, int A, int R, int B, int n_in, const float* x, int64_t x_sa, int64_t x_sc,
+                       int64_t x_sb, const float* w1, const float* b1, const float* w2, const float* b2,
+                       const float* w_ih, const float* b_ih, float* y1, float* y2, float* gi);
+
 /* gather: dst[r][:] = src[idx[r]][:]; scatter: dst[idx[r]][:] = src[r][:]; rows of `width` floats. */
 int flock_gather_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);
 int flock_scatter_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);

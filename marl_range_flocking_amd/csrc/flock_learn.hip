@@ -253,6 +253,135 @@ __global__ __launch_bounds__(kBlock) void gru_bwd_kernel(int64_t rows, int H, co
     }
 }
 
+// VDN QNet feature chain of A agents over R rows each, ONE launch (learners/vdn/net.py:19-33 agent_feature_i =
+// Linear(n_obs, 64)-ReLU-Linear(64, 32)-ReLU, then the GRUCell input side x W_ih^T + b_ih of every chunk step):
+//   y1 = relu(x W1^T + b1) [64], y2 = relu(y1 W2^T + b2) [32], gi = y2 Wih^T + bih [96]
+// replaces three batched GEMMs (K = n_obs, 64, 32) and two ReLU passes whose [A][R][64] / [A][R][32] intermediates
+// made the round trip through HBM. Block = 64 rows of one agent (grid R/64 x A): the agent's weights are staged
+// transposed in LDS (W^T[k][o]: the outputs of one k are contiguous, read as broadcast float4s), lane = row, the four
+// waves split the outputs of each layer; y1 / y2 stay in LDS (row stride 65 / 33: conflict-free); gi (and y1 / y2
+// when the backward needs them) leave through LDS as coalesced rows. x element (a, c, b, f) at
+// x[a*xa + c*xc + b*xb + f], row r = c*B + b (the replay gather's [B][C][A][n] layout is read in place).
+constexpr int kF1 = 64, kF2 = 32, kFG = 96, kFRows = 64, kFMaxIn = 16;
+__global__ __launch_bounds__(kBlock) void vdn_feat_fwd_kernel(int R, int B, int NI, const float* __restrict__ x,
+                                                              int64_t xa, int64_t xc, int64_t xb,
+                                                              const float* __restrict__ W1, const float* __restrict__ b1,
+                                                              const float* __restrict__ W2, const float* __restrict__ b2,
+                                                              const float* __restrict__ Wi, const float* __restrict__ bi,
+                                                              float* __restrict__ y1o, float* __restrict__ y2o,
+                                                              float* __restrict__ gi) {
+    // LDS (54.8 KB): [xs | w1t | w2t | y1s] are dead once layer 2 has run, and gs (layer 3's staging) reuses them
+    constexpr int kXs = kFRows * (kFMaxIn + 1), kW1 = kFMaxIn * kF1, kW2 = kF1 * kF2, kY1 = kFRows * (kF1 + 1);
+    static_assert(kFRows * (kFG + 1) <= kXs + kW1 + kW2 + kY1 && kXs % 4 == 0 && kW1 % 4 == 0 && kW2 % 4 == 0,
+                  "gs alias / float4 alignment");
+    __shared__ __attribute__((aligned(16))) float early[kXs + kW1 + kW2 + kY1];
+    __shared__ __attribute__((aligned(16))) float wit[kF2 * kFG];  // [k][o]
+    __shared__ float bs[kF1 + kF2 + kFG];
+    __shared__ float y2s[kFRows * (kF2 + 1)];
+    float* xs = early;
+    float* w1t = early + kXs;  // [k][o]
+    float* w2t = w1t + kW1;
+    float* y1s = w2t + kW2;
+    float* gs = early;
+    const int64_t a = blockIdx.y;
+    const int r0 = blockIdx.x * kFRows, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nr = min(kFRows, R - r0);
+    for (int e = tid; e < kF1 * NI; e += kBlock) {  // W1 [64][NI] -> [NI][64]
+        const int o = e / NI, k = e - o * NI;
+        w1t[k * kF1 + o] = W1[a * kF1 * NI + e];
+    }
+    for (int e = tid; e < kF2 * kF1; e += kBlock) {
+        const int o = e / kF1, k = e - o * kF1;
+        w2t[k * kF2 + o] = W2[a * kF2 * kF1 + e];
+    }
+    for (int e = tid; e < kFG * kF2; e += kBlock) {
+        const int o = e / kF2, k = e - o * kF2;
+        wit[k * kFG + o] = Wi[a * kFG * kF2 + e];
+    }
+    if (tid < kF1) bs[tid] = b1[a * kF1 + tid];
+    if (tid < kF2) bs[kF1 + tid] = b2[a * kF2 + tid];
+    if (tid < kFG) bs[kF1 + kF2 + tid] = bi[a * kFG + tid];
+    for (int e = tid; e < nr * NI; e += kBlock) {
+        const int rr = e / NI, f = e - rr * NI, r = r0 + rr, c = r / B, b = r - c * B;
+        xs[rr * (kFMaxIn + 1) + f] = x[a * xa + c * xc + b * xb + f];
+    }
+    __syncthreads();
+    const bool live = lane < nr;
+    // layer 1: wave wv computes outputs [16 wv, 16 wv + 16) of its lane's row
+    if (live) {
+        float acc[16];
+#pragma unroll
+        for (int o = 0; o < 16; ++o) acc[o] = 0.0f;
+        for (int k = 0; k < NI; ++k) {
+            const float xv = xs[lane * (kFMaxIn + 1) + k];
+            const float4* w = reinterpret_cast<const float4*>(w1t + k * kF1 + 16 * wv);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = w[q];
+                acc[4 * q] = fmaf(xv, v.x, acc[4 * q]);
+                acc[4 * q + 1] = fmaf(xv, v.y, acc[4 * q + 1]);
+                acc[4 * q + 2] = fmaf(xv, v.z, acc[4 * q + 2]);
+                acc[4 * q + 3] = fmaf(xv, v.w, acc[4 * q + 3]);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 16; ++o) y1s[lane * (kF1 + 1) + 16 * wv + o] = fmaxf(acc[o] + bs[16 * wv + o], 0.0f);
+    }
+    __syncthreads();
+    if (y1o)
+        for (int e = tid; e < nr * kF1; e += kBlock)
+            y1o[(a * R + r0) * kF1 + e] = y1s[(e / kF1) * (kF1 + 1) + (e % kF1)];
+    // layer 2: outputs [8 wv, 8 wv + 8)
+    if (live) {
+        float acc[8];
+#pragma unroll
+        for (int o = 0; o < 8; ++o) acc[o] = 0.0f;
+#pragma unroll 4
+        for (int k = 0; k < kF1; ++k) {
+            const float yv = y1s[lane * (kF1 + 1) + k];
+            const float4* w = reinterpret_cast<const float4*>(w2t + k * kF2 + 8 * wv);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float4 v = w[q];
+                acc[4 * q] = fmaf(yv, v.x, acc[4 * q]);
+                acc[4 * q + 1] = fmaf(yv, v.y, acc[4 * q + 1]);
+                acc[4 * q + 2] = fmaf(yv, v.z, acc[4 * q + 2]);
+                acc[4 * q + 3] = fmaf(yv, v.w, acc[4 * q + 3]);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+            y2s[lane * (kF2 + 1) + 8 * wv + o] = fmaxf(acc[o] + bs[kF1 + 8 * wv + o], 0.0f);
+    }
+    __syncthreads();
+    if (y2o)
+        for (int e = tid; e < nr * kF2; e += kBlock)
+            y2o[(a * R + r0) * kF2 + e] = y2s[(e / kF2) * (kF2 + 1) + (e % kF2)];
+    // GRU input side: outputs [24 wv, 24 wv + 24)
+    if (live) {
+        float acc[24];
+#pragma unroll
+        for (int o = 0; o < 24; ++o) acc[o] = 0.0f;
+#pragma unroll 4
+        for (int k = 0; k < kF2; ++k) {
+            const float yv = y2s[lane * (kF2 + 1) + k];
+            const float4* w = reinterpret_cast<const float4*>(wit + k * kFG + 24 * wv);
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const float4 v = w[q];
+                acc[4 * q] = fmaf(yv, v.x, acc[4 * q]);
+                acc[4 * q + 1] = fmaf(yv, v.y, acc[4 * q + 1]);
+                acc[4 * q + 2] = fmaf(yv, v.z, acc[4 * q + 2]);
+                acc[4 * q + 3] = fmaf(yv, v.w, acc[4 * q + 3]);
+            }
+        }
+#pragma unroll
+        for (int o = 0; o < 24; ++o) gs[lane * (kFG + 1) + 24 * wv + o] = acc[o] + bs[kF1 + kF2 + 24 * wv + o];
+    }
+    __syncthreads();
+    for (int e = tid; e < nr * kFG; e += kBlock) gi[(a * R + r0) * kFG + e] = gs[(e / kFG) * (kFG + 1) + (e % kFG)];
+}
+
 // dst[r, :] = src[idx[r], :]  (replay minibatch / chunk gather); one wave per row, 16-B vectors when aligned
 // GRUCell recurrence of A independent networks over a whole chunk of C steps, ONE block per network (replaces
 // C x (hidden GEMM + gate kernel + reset) launches per network: vdn/train_flock.py:23-36 and
@@ -613,6 +742,18 @@ int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs
         return fail(-4, "flock_gru_seq_bwd: cannot raise the LDS limit");
     hipLaunchKernelGGL(gru_seq_bwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dhs, hs, ws,
                        w_hh, keep, keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh);
+    return launched();
+}
+
+int flock_vdn_feat_fwd(void* stream, int A, int R, int B, int n_in, const float* x, int64_t x_sa, int64_t x_sc,
+                       int64_t x_sb, const float* w1, const float* b1, const float* w2, const float* b2,
+                       const float* w_ih, const float* b_ih, float* y1, float* y2, float* gi) {
+    if (A <= 0 || R <= 0) return 0;
+    if (!x || !w1 || !b1 || !w2 || !b2 || !w_ih || !b_ih || !gi) return fail(-3, "flock_vdn_feat_fwd: NULL pointer");
+    if (n_in < 1 || n_in > kFMaxIn) return fail(-2, "flock_vdn_feat_fwd: n_in must be in [1, 16]");
+    if (B < 1 || R % B != 0) return fail(-5, "flock_vdn_feat_fwd: R must be a multiple of B");
+    hipLaunchKernelGGL(vdn_feat_fwd_kernel, dim3((R + kFRows - 1) / kFRows, A), dim3(kBlock), 0, (hipStream_t)stream,
+                       R, B, n_in, x, x_sa, x_sc, x_sb, w1, b1, w2, b2, w_ih, b_ih, y1, y2, gi);
     return launched();
 }
 

@@ -338,6 +338,55 @@ def gru_seq(gi, W_hh, b_hh, keep):
     return _GRUSeqFn.apply(gi, W_hh, b_hh, keep, save)
 
 
+class _VdnFeatFn(torch.autograd.Function):
+    """The VDN QNet feature chain Linear(n_obs,64)-ReLU-Linear(64,32)-ReLU plus the GRUCell input side of every chunk
+    step, A agents in ONE launch (flock_vdn_feat_fwd; learners/vdn/net.py:19-33). The backward is the chain rule on
+    the saved post-ReLU activations as batched GEMMs (the weight gradients land in each parameter's own layout)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, Wi, bi, save):
+        A, C, B, n = x.shape
+        R = C * B
+        if x.stride(3) != 1:
+            x = x.contiguous()
+        W1, b1, W2, b2, Wi, bi = (t.contiguous() for t in (W1, b1, W2, b2, Wi, bi))
+        dev, f32 = x.device, x.dtype
+        gi = torch.empty((A, R, Wi.shape[1]), dtype=f32, device=dev)
+        y1 = torch.empty((A, R, W1.shape[1]), dtype=f32, device=dev) if save else None
+        y2 = torch.empty((A, R, W2.shape[1]), dtype=f32, device=dev) if save else None
+        sa, sc, sb, _ = x.stride()
+        rc = _native.lib().flock_vdn_feat_fwd(_stream(dev), A, R, B, n, _p(x), sa, sc, sb, _p(W1), _p(b1), _p(W2),
+                                              _p(b2), _p(Wi), _p(bi), _p(y1), _p(y2), _p(gi))
+        _native.check(rc, "flock_vdn_feat_fwd", learn=True)
+        if save:
+            ctx.save_for_backward(x, W2, Wi, y1, y2)
+        return gi
+
+    @staticmethod
+    def backward(ctx, dgi):
+        x, W2, Wi, y1, y2 = ctx.saved_tensors
+        A, C, B, n = x.shape
+        dWi = torch.bmm(dgi.transpose(1, 2), y2)
+        dbi = dgi.sum(1)
+        dz2 = torch.bmm(dgi, Wi).masked_fill_(y2 <= 0, 0.0)     # ReLU backward on the output (y > 0 iff z > 0)
+        dW2 = torch.bmm(dz2.transpose(1, 2), y1)
+        db2 = dz2.sum(1)
+        dz1 = torch.bmm(dz2, W2).masked_fill_(y1 <= 0, 0.0)
+        dW1 = torch.bmm(dz1.transpose(1, 2), x.reshape(A, C * B, n))
+        db1 = dz1.sum(1)
+        return None, dW1, db1, dW2, db2, dWi, dbi, None
+
+
+def vdn_feat(x, W1, b1, W2, b2, Wi, bi):
+    """x [A,C,B,n_obs] (any strides with a unit feature stride, e.g. the replay gather's permuted view) -> gi
+    [A, C*B, 96] = relu(relu(x W1^T + b1) W2^T + b2) Wi^T + bi per agent (hidden sizes 64 / 32, n_obs <= 16)."""
+    A, n = x.shape[0], x.shape[3]
+    if not (W1.shape == (A, 64, n) and W2.shape == (A, 32, 64) and Wi.shape == (A, 96, 32) and 1 <= n <= 16):
+        raise ValueError("vdn_feat: the QNet feature chain n_obs -> 64 -> 32 -> 3 x 32 (n_obs <= 16)")
+    save = torch.is_grad_enabled() and any(t.requires_grad for t in (W1, b1, W2, b2, Wi, bi))
+    return _VdnFeatFn.apply(x, W1, b1, W2, b2, Wi, bi, save)
+
+
 def gru_cell_gi(gi, h, W_hh, b_hh):
     """gru_cell from precomputed input-side gate pre-activations gi = x W_ih^T + b_ih [A,B,3H] (a recurrence can
     compute them for every step at once)."""

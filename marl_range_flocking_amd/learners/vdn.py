@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell, gru_seq
+from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell, gru_seq, vdn_feat
 
 HX = 32
 
@@ -44,6 +44,8 @@ class BatchedQNet:
     def __init__(self, n_agents, n_obs, n_actions, recurrent=True, device="cuda", generator=None):
         self.n_agents, self.n_obs, self.n_actions, self.recurrent = n_agents, n_obs, n_actions, recurrent
         self.hx_size = HX
+        # forward_seq's feature chain as one fused launch (False: batched GEMMs + ReLU passes, the A/B baseline)
+        self.fused_features = True
         self.device = torch.device(device)
         self.P = FlatParams(qnet_shapes(n_obs, n_actions, HX, recurrent), self.device, agents=n_agents)
         with torch.no_grad():  # nn.Linear / nn.GRUCell defaults: U(+-1/sqrt(fan_in)), GRU U(+-1/sqrt(hidden))
@@ -75,10 +77,16 @@ class BatchedQNet:
         launch. Same per-step math as forward_am."""
         P = self.P.params if P is None else P
         A, C, B, n = x.shape
-        y = F.relu(blinear(x.reshape(A, C * B, n), P["feat1.weight"], P["feat1.bias"]))
-        y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
+        if self.recurrent and n <= 16 and self.fused_features:
+            # feat1-ReLU-feat2-ReLU and the GRU input side of every step in one launch (flock_vdn_feat_fwd)
+            gi = vdn_feat(x, P["feat1.weight"], P["feat1.bias"], P["feat2.weight"], P["feat2.bias"],
+                          P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
+        else:
+            y = F.relu(blinear(x.reshape(A, C * B, n), P["feat1.weight"], P["feat1.bias"]))
+            y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
+            if self.recurrent:
+                gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
         if self.recurrent:  # the whole chunk's recurrence in one launch each way (flock_gru_seq_fwd / _bwd)
-            gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
             hs = gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep.unsqueeze(1).expand(C, A, B))
             y = hs.view(A, C * B, self.hx_size)
         return blinear(y, P["q.weight"], P["q.bias"]).view(A, C, B, -1)

@@ -151,3 +151,33 @@ def test_gru_seq_matches_per_step_grucell(A, C, B, per_agent, cuda):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5, msg=name)
     with torch.no_grad():  # no saved gates without grad
         torch.testing.assert_close(gru_seq(gi, W, b, keep), ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("A,C,B,n", [(3, 2, 5, 4), (8, 10, 32, 4), (512, 10, 32, 4), (4, 3, 70, 9)])
+def test_vdn_feat_matches_torch_linear_chain(A, C, B, n, cuda):
+    """flock_vdn_feat_fwd (one launch: Linear(n,64)-ReLU-Linear(64,32)-ReLU-(x W_ih^T + b_ih), learners/vdn/net.py:19-33)
+    against plain PyTorch fp32 nn.functional on the same per-agent weights, forward and every weight gradient, with
+    the input read in place through the replay gather's permuted layout. Tolerance: fp32 reassociation only
+    (rtol 1e-5 / atol 1e-5 of the output scale); rows = 70 and 320 cover partial 64-row blocks."""
+    from marl_range_flocking_amd.learners.core import vdn_feat
+
+    g = torch.Generator(device=cuda).manual_seed(A * 7 + B)
+    r = lambda *s: (torch.rand(*s, device=cuda, generator=g) * 2 - 1)  # noqa: E731
+    raw = r(B, C, A, n)                       # the replay gather's [B, C, A, n]
+    x = raw.permute(2, 1, 0, 3)               # [A, C, B, n] view (unit feature stride), as VDNLearner passes it
+    W = [r(A, 64, n) * 0.5, r(A, 64) * 0.5, r(A, 32, 64) * 0.2, r(A, 32) * 0.2, r(A, 96, 32) * 0.3, r(A, 96) * 0.3]
+    Wf = [w.clone().requires_grad_(True) for w in W]
+    Wt = [w.clone().requires_grad_(True) for w in W]
+    gi = vdn_feat(x, *Wf)
+    xr = x.reshape(A, C * B, n)
+    y = torch.relu(torch.baddbmm(Wt[1].unsqueeze(1), xr, Wt[0].transpose(1, 2)))
+    y = torch.relu(torch.baddbmm(Wt[3].unsqueeze(1), y, Wt[2].transpose(1, 2)))
+    ref = torch.baddbmm(Wt[5].unsqueeze(1), y, Wt[4].transpose(1, 2))
+    torch.testing.assert_close(gi, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+    up = r(A, C * B, 96)
+    (gi * up).sum().backward()
+    (ref * up).sum().backward()
+    for name, a_, b_ in zip(("W1", "b1", "W2", "b2", "Wi", "bi"), Wf, Wt):
+        torch.testing.assert_close(a_.grad, b_.grad, rtol=1e-4, atol=1e-5 * float(b_.grad.abs().max()), msg=name)
+    with torch.no_grad():  # the target network's path: gi only (no saved activations)
+        torch.testing.assert_close(vdn_feat(x, *W), ref.detach(), rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
