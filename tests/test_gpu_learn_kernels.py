@@ -122,7 +122,8 @@ def test_ring_store_fused_matches_row_copies(cap, n, steps, cuda):
     assert ring.counter == n * steps
 
 
-@pytest.mark.parametrize("A,C,B,per_agent", [(3, 10, 32, False), (5, 10, 128, True), (2, 1, 7, True), (4, 4, 200, False)])
+@pytest.mark.parametrize("A,C,B,per_agent", [(3, 10, 32, False), (5, 10, 128, True), (2, 1, 7, True), (4, 4, 200, False),
+                                             (2, 3, 16, True), (3, 5, 8, False), (512, 10, 32, False)])
 def test_gru_seq_matches_per_step_grucell(A, C, B, per_agent, cuda):
     """flock_gru_seq_fwd/_bwd (one launch per chunk) against the per-step loop the learners used before: gru_cell
     per step (hidden GEMM + gate kernel) with the done reset between steps, fp32 autograd, same inputs."""
