@@ -464,9 +464,7 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
 //   dW_hh += dgh^T h_prev, db_hh += sum_b dgh   (h_prev = keep[t-1] ? hs[t-1] : 0, zero at t = 0)
 // dW / db are written (this recurrence is their only use inside the chunk). LDS: dgh [B][3H], h_prev and carry
 // [B][H]. Thread (i, b) for dh_prev keeps column i of W_hh in registers; dW entries e = tid + 256 q are per thread.
-// RPT > 0 (B = RPT * 256 / H rows, RPT per thread): step t-1's global inputs (saved gates, dhs, h_prev, keep) are
-// loaded into registers while step t computes, so the ten dependent steps do not each wait on a memory round trip.
-template <int H, int RPT = 0>
+template <int H>
 __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const float* __restrict__ dhs,
                                                              const float* __restrict__ hs, const float* __restrict__ ws,
                                                              const float* __restrict__ W,
@@ -489,83 +487,6 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
     for (int q = 0; q < NW; ++q) accw[q] = 0.0f;
     float accb = 0.0f;
     for (int e = tid; e < B * H; e += kBlock) carry[e] = 0.0f;
-    if constexpr (RPT > 0) {
-        struct In {
-            float hp, r, z, nn, ghn, dh;
-            bool kp;
-        };
-        In cur[RPT], nxt[RPT];
-        auto load = [&](int t, In(&d)[RPT]) {
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) {
-                const int b = tid / H + bstep * q;
-                const int64_t row = (a * C + t) * B + b;
-                const bool kp = t > 0 && keep[(t - 1) * kt + a * ka + b * kb];
-                const float v = t > 0 ? hs[(row - B) * H + i] : 0.0f;  // independent of kp: no load chain
-                const float* w = ws + row * 4 * H;
-                d[q] = In{kp ? v : 0.0f, w[i], w[H + i], w[2 * H + i], w[3 * H + i], dhs[row * H + i], kp};
-            }
-        };
-        load(C - 1, cur);
-        for (int t = C - 1; t >= 0; --t) {
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) hprev[(tid / H + bstep * q) * H + i] = cur[q].hp;
-            __syncthreads();  // carry (previous iteration) and hprev visible
-            if (t > 0) load(t - 1, nxt);  // consumed by the next iteration
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) {
-                const int b = tid / H + bstep * q;
-                const int64_t row = (a * C + t) * B + b;
-                const In& c = cur[q];
-                const float go = c.dh + carry[b * H + i];
-                const float dn = go * (1.0f - c.z);
-                const float dz = go * (c.hp - c.nn);
-                const float dan = dn * (1.0f - c.nn * c.nn);
-                const float dr = dan * c.ghn;
-                const float dar = dr * (c.r * (1.0f - c.r));
-                const float daz = dz * (c.z * (1.0f - c.z));
-                float* gi_ = dgi + row * G;
-                gi_[i] = dar;
-                gi_[H + i] = daz;
-                gi_[2 * H + i] = dan;
-                dgh[b * G + i] = dar;
-                dgh[b * G + H + i] = daz;
-                dgh[b * G + 2 * H + i] = dan * c.r;
-                carry[b * H + i] = go * c.z;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < NW; ++q) {
-                const int e = tid + kBlock * q, g = e / H, ii = e - g * H;
-                float s = 0.0f;
-                for (int b = 0; b < B; ++b) s = fmaf(dgh[b * G + g], hprev[b * H + ii], s);
-                accw[q] += s;
-            }
-            if (tid < G) {
-                float s = 0.0f;
-                for (int b = 0; b < B; ++b) s += dgh[b * G + tid];
-                accb += s;
-            }
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) {
-                const int b = tid / H + bstep * q;
-                const float4* d4 = reinterpret_cast<const float4*>(dgh + b * G);
-                float s = 0.0f;
-#pragma unroll
-                for (int g4 = 0; g4 < G / 4; ++g4) {
-                    const float4 v = d4[g4];
-                    s = fmaf(v.x, wc[4 * g4], s);
-                    s = fmaf(v.y, wc[4 * g4 + 1], s);
-                    s = fmaf(v.z, wc[4 * g4 + 2], s);
-                    s = fmaf(v.w, wc[4 * g4 + 3], s);
-                }
-                carry[b * H + i] = cur[q].kp ? carry[b * H + i] + s : 0.0f;
-            }
-            __syncthreads();  // dgh / hprev reads done before the next step overwrites them
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) cur[q] = nxt[q];
-        }
-    } else
     for (int t = C - 1; t >= 0; --t) {
         // h_prev of step t (the reset previous output), and the gate gradients
         for (int e = tid; e < B * H; e += kBlock) {
@@ -824,26 +745,11 @@ int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs
     if (H != 32) return fail(-2, "flock_gru_seq_bwd: hidden size must be 32");
     const size_t lds = (size_t)B * (3 * H + 2 * H) * sizeof(float);
     if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_bwd: B too large for LDS");
-    constexpr int bstep = kBlock / 32;  // rows per pass of the block
-    const int rpt = (B % bstep == 0) ? B / bstep : 0;
-    auto launch = [&](auto kern) {
-        if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-            return fail(-4, "flock_gru_seq_bwd: cannot raise the LDS limit");
-        hipLaunchKernelGGL(kern, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dhs, hs, ws, w_hh, keep, keep_st,
-                           keep_sa, keep_sb, dgi, dw_hh, db_hh);
-        return 0;
-    };
-    int rc;
-    if (rpt == 4)  // VDN (B = 32): prefetching instantiation
-        rc = launch(gru_seq_bwd_kernel<32, 4>);
-    else if (rpt == 2)
-        rc = launch(gru_seq_bwd_kernel<32, 2>);
-    else if (rpt == 1)
-        rc = launch(gru_seq_bwd_kernel<32, 1>);
-    else
-        rc = launch(gru_seq_bwd_kernel<32, 0>);
-    if (rc) return rc;
+    if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(gru_seq_bwd_kernel<32>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(-4, "flock_gru_seq_bwd: cannot raise the LDS limit");
+    hipLaunchKernelGGL(gru_seq_bwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dhs, hs, ws,
+                       w_hh, keep, keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh);
     return launched();
 }
 
