@@ -257,30 +257,30 @@ __global__ __launch_bounds__(kBlock) void gru_bwd_kernel(int64_t rows, int H, co
 // Linear(n_obs, 64)-ReLU-Linear(64, 32)-ReLU, then the GRUCell input side x W_ih^T + b_ih of every chunk step):
 //   y1 = relu(x W1^T + b1) [64], y2 = relu(y1 W2^T + b2) [32], gi = y2 Wih^T + bih [96]
 // replaces three batched GEMMs (K = n_obs, 64, 32) and two ReLU passes whose [A][R][64] / [A][R][32] intermediates
-// made the round trip through HBM. Block = 64 rows of one agent (grid R/64 x A). The agent's weights are copied to
-// LDS in their own [o][k] layout (coalesced float4s); lane = row, the four waves split the outputs of each layer, and
-// every k-step of four reads the lane's activations as one float4 (rows padded to a 16-B multiple that keeps groups
-// of 8 lanes on distinct banks) and each output's weights as a broadcast float4. y1 / y2 stay in LDS; gi (and y1 /
-// y2 when the backward needs them) leave through LDS as coalesced rows. x element (a, c, b, f) at
+// made the round trip through HBM. One block per agent walks its rows 64 at a time; wave w owns rows [16 w, 16 w + 16)
+// of each group and runs each layer as f32 MFMA tiles (v_mfma_f32_16x16x4_f32: exact f32, a k-ordered fmaf chain per
+// output) over all of the layer's 16-column tiles: A operand = the wave's activation rows, B operand = the weight rows
+// ([o][k] layout), both read per lane from LDS rows padded to 2 mod 32 floats (16 rows x 2 k per half-wave on
+// distinct banks). y1 / y2 stay in LDS for the next layer; gi (and y1 / y2 when the backward needs them) are written
+// from the accumulators, 16 lanes to 64 contiguous bytes of a row. x element (a, c, b, f) at
 // x[a*xa + c*xc + b*xb + f], row r = c*B + b (the replay gather's [B][C][A][n] layout is read in place).
-// Measured (config 4, 512 agents x 320 rows): 77 us per launch, bound by the LDS return bandwidth of the broadcast
-// weight reads (~21 float4 reads per row); weights read with wave-uniform scalar loads instead measured 114 us.
+// Config 4 (512 agents x 320 rows), per launch: lane-per-row FMA with broadcast weight reads 77 us, MFMA tiles over
+// 64-row blocks 72 us (each block's serial load -> compute chain at two blocks per CU), this per-agent walk with
+// the next rows' x in flight 41 us.
 constexpr int kF1 = 64, kF2 = 32, kFG = 96, kFRows = 64, kFMaxIn = 16;
-constexpr int kSX = kFMaxIn + 4, kSY1 = kF1 + 4, kSY2 = kF2 + 4, kSG = kFG + 4;  // LDS row strides (floats)
+constexpr int kSW1 = kFMaxIn + 2, kSY1 = kF1 + 2, kSY2 = kF2 + 2;  // LDS row strides (floats)
+using f32x4_t = float __attribute__((ext_vector_type(4)));
 
-template <int K, int NO>  // acc[o] += sum_k y[k] w[o][k], k in fours (y: the lane's row, w: broadcast rows)
-__device__ __forceinline__ void dot_rows(float (&acc)[NO], const float* y, const float* w, int kmax) {
-    for (int k = 0; k < kmax; k += 4) {
-        const float4 yv = *reinterpret_cast<const float4*>(y + k);
+// NT column tiles of 16: acc[t] += A[16 rows][K] * W[16 t .. 16 t + 16][K]^T, k in steps of 4 (one MFMA each)
+template <int NT>
+__device__ __forceinline__ void mfma_rows(f32x4_t (&acc)[NT], const float* a, int sa, const float* w, int sw,
+                                          int K, int lane) {
+    const int i = lane & 15, kk = lane >> 4;
+    for (int k = 0; k < K; k += 4) {
+        const float av = a[i * sa + k + kk];
 #pragma unroll
-        for (int o = 0; o < NO; ++o) {
-            const float4 wv = *reinterpret_cast<const float4*>(w + o * K + k);
-            float s = acc[o];
-            s = fmaf(yv.x, wv.x, s);
-            s = fmaf(yv.y, wv.y, s);
-            s = fmaf(yv.z, wv.z, s);
-            acc[o] = fmaf(yv.w, wv.w, s);
-        }
+        for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w[(16 * t + i) * sw + k + kk], acc[t], 0, 0, 0);
     }
 }
 
@@ -291,103 +291,91 @@ __global__ __launch_bounds__(kBlock) void vdn_feat_fwd_kernel(int R, int B, int 
                                                               const float* __restrict__ Wi, const float* __restrict__ bi,
                                                               float* __restrict__ y1o, float* __restrict__ y2o,
                                                               float* __restrict__ gi) {
-    // LDS (57 KB): [xs | w1 | y1s] are dead once layer 2 has run, and gs (layer 3's staging) reuses them
-    constexpr int kXs = kFRows * kSX, kW1 = kF1 * kFMaxIn, kY1 = kFRows * kSY1;
-    static_assert(kFRows * kSG <= kXs + kW1 + kY1, "gs alias");
-    __shared__ __attribute__((aligned(16))) float early[kXs + kW1 + kY1];
-    __shared__ __attribute__((aligned(16))) float w2[kF2 * kF1];  // [o][k]
-    __shared__ __attribute__((aligned(16))) float wi[kFG * kF2];
-    __shared__ __attribute__((aligned(16))) float y2s[kFRows * kSY2];
+    // one block per agent (57 KB of LDS, two blocks per CU: the 512 agents of config 4 in one round); the weights
+    // are staged once and the block walks the agent's rows 64 at a time, loading the next 64 rows of x into
+    // registers while the current ones run through the three layers
+    __shared__ float w1[kF1 * kSW1];
+    __shared__ float w2[kF2 * kSY1];
+    __shared__ float wi[kFG * kSY2];
     __shared__ float bs[kF1 + kF2 + kFG];
-    float* xs = early;
-    float* w1 = early + kXs;  // [o][k], row stride K1 = NI rounded up to 4 (zero-padded)
-    float* y1s = w1 + kW1;
-    float* gs = early;
-    const int64_t a = blockIdx.y;
-    const int r0 = blockIdx.x * kFRows, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int nr = min(kFRows, R - r0), K1 = (NI + 3) & ~3;
+    __shared__ float xs[kFRows * kSW1];
+    __shared__ float y1s[kFRows * kSY1];
+    __shared__ float y2s[kFRows * kSY2];
+    const int64_t a = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int K1 = (NI + 3) & ~3;
+    const int sx = K1 + 2;  // xs / w1 row stride: 2 mod 4 (and so 2 (2j+1) mod 32: distinct banks for 16 rows)
     for (int e = tid; e < kF1 * K1; e += kBlock) {
         const int o = e / K1, k = e - o * K1;
-        w1[e] = k < NI ? W1[(a * kF1 + o) * NI + k] : 0.0f;
+        w1[o * sx + k] = k < NI ? W1[(a * kF1 + o) * NI + k] : 0.0f;
     }
-    {
-        const float4* s2 = reinterpret_cast<const float4*>(W2 + a * kF2 * kF1);
-        const float4* si = reinterpret_cast<const float4*>(Wi + a * kFG * kF2);
-        float4* d2 = reinterpret_cast<float4*>(w2);
-        float4* di = reinterpret_cast<float4*>(wi);
-        for (int e = tid; e < kF2 * kF1 / 4; e += kBlock) d2[e] = s2[e];
-        for (int e = tid; e < kFG * kF2 / 4; e += kBlock) di[e] = si[e];
-    }
+    for (int e = tid; e < kF2 * kF1; e += kBlock) w2[(e / kF1) * kSY1 + (e % kF1)] = W2[a * kF2 * kF1 + e];
+    for (int e = tid; e < kFG * kF2; e += kBlock) wi[(e / kF2) * kSY2 + (e % kF2)] = Wi[a * kFG * kF2 + e];
     if (tid < kF1) bs[tid] = b1[a * kF1 + tid];
     if (tid < kF2) bs[kF1 + tid] = b2[a * kF2 + tid];
     if (tid < kFG) bs[kF1 + kF2 + tid] = bi[a * kFG + tid];
-    for (int e = tid; e < kFRows * K1; e += kBlock) {
-        const int rr = e / K1, f = e - rr * K1, r = r0 + rr, c = r / B, b = r - c * B;
-        xs[rr * kSX + f] = (rr < nr && f < NI) ? x[a * xa + c * xc + b * xb + f] : 0.0f;
-    }
-    __syncthreads();
-    const bool live = lane < nr;
-    // layer 1: wave wv computes outputs [16 wv, 16 wv + 16) of its lane's row
-    if (live) {
-        float acc[16];
+    constexpr int kXPT = kFRows * kFMaxIn / kBlock;  // x elements per thread per 64 rows (at most)
+    float xr[kXPT];
+    auto load_x = [&](int r0) {
 #pragma unroll
-        for (int o = 0; o < 16; ++o) acc[o] = 0.0f;
-        for (int k = 0; k < K1; k += 4) {
-            const float4 xv = *reinterpret_cast<const float4*>(xs + lane * kSX + k);
-#pragma unroll
-            for (int o = 0; o < 16; ++o) {
-                const float4 w = *reinterpret_cast<const float4*>(w1 + (16 * wv + o) * K1 + k);
-                float s = acc[o];
-                s = fmaf(xv.x, w.x, s);
-                s = fmaf(xv.y, w.y, s);
-                s = fmaf(xv.z, w.z, s);
-                acc[o] = fmaf(xv.w, w.w, s);
+        for (int q = 0; q < kXPT; ++q) {
+            const int e = tid + kBlock * q, rr = e / K1, f = e - rr * K1, r = r0 + rr;
+            xr[q] = 0.0f;
+            if (e < kFRows * K1 && r < R && f < NI) {
+                const int c = r / B, b = r - c * B;
+                xr[q] = x[a * xa + c * xc + b * xb + f];
             }
         }
-        float4* yd = reinterpret_cast<float4*>(y1s + lane * kSY1 + 16 * wv);
+    };
+    load_x(0);
+    const int col = lane & 15, row4 = 16 * wv + 4 * (lane >> 4);  // C/D: col = lane & 15, row = 4 (lane >> 4) + v
+    for (int r0 = 0; r0 < R; r0 += kFRows) {
+        const int nr = min(kFRows, R - r0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float* bb = bs + 16 * wv + 4 * q;
-            yd[q] = make_float4(fmaxf(acc[4 * q] + bb[0], 0.0f), fmaxf(acc[4 * q + 1] + bb[1], 0.0f),
-                                fmaxf(acc[4 * q + 2] + bb[2], 0.0f), fmaxf(acc[4 * q + 3] + bb[3], 0.0f));
+        for (int q = 0; q < kXPT; ++q) {
+            const int e = tid + kBlock * q;
+            if (e < kFRows * K1) xs[(e / K1) * sx + (e % K1)] = xr[q];
+        }
+        __syncthreads();  // xs (and, first time round, the weights) visible; the previous rows' reads are done
+        if (r0 + kFRows < R) load_x(r0 + kFRows);  // in flight while these rows compute
+        const int64_t base = a * R + r0;
+        {  // layer 1: 4 column tiles
+            f32x4_t acc[4] = {};
+            mfma_rows<4>(acc, xs + 16 * wv * sx, sx, w1, sx, K1, lane);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float y = fmaxf(acc[t][v] + bs[16 * t + col], 0.0f);
+                    y1s[(row4 + v) * kSY1 + 16 * t + col] = y;
+                    if (y1o && row4 + v < nr) y1o[(base + row4 + v) * kF1 + 16 * t + col] = y;
+                }
+        }
+        __syncthreads();
+        {  // layer 2: 2 column tiles
+            f32x4_t acc[2] = {};
+            mfma_rows<2>(acc, y1s + 16 * wv * kSY1, kSY1, w2, kSY1, kF1, lane);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const float y = fmaxf(acc[t][v] + bs[kF1 + 16 * t + col], 0.0f);
+                    y2s[(row4 + v) * kSY2 + 16 * t + col] = y;
+                    if (y2o && row4 + v < nr) y2o[(base + row4 + v) * kF2 + 16 * t + col] = y;
+                }
+        }
+        __syncthreads();
+        {  // GRU input side: 6 column tiles, written from the accumulators (16 lanes = 64 contiguous bytes)
+            f32x4_t acc[6] = {};
+            mfma_rows<6>(acc, y2s + 16 * wv * kSY2, kSY2, wi, kSY2, kF2, lane);
+#pragma unroll
+            for (int t = 0; t < 6; ++t)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (row4 + v < nr)
+                        gi[(base + row4 + v) * kFG + 16 * t + col] = acc[t][v] + bs[kF1 + kF2 + 16 * t + col];
         }
     }
-    __syncthreads();
-    if (y1o)
-        for (int e = tid; e < nr * kF1; e += kBlock) y1o[(a * R + r0) * kF1 + e] = y1s[(e / kF1) * kSY1 + (e % kF1)];
-    // layer 2: outputs [8 wv, 8 wv + 8)
-    if (live) {
-        float acc[8];
-#pragma unroll
-        for (int o = 0; o < 8; ++o) acc[o] = 0.0f;
-        dot_rows<kF1, 8>(acc, y1s + lane * kSY1, w2 + 8 * wv * kF1, kF1);
-        float4* yd = reinterpret_cast<float4*>(y2s + lane * kSY2 + 8 * wv);
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const float* bb = bs + kF1 + 8 * wv + 4 * q;
-            yd[q] = make_float4(fmaxf(acc[4 * q] + bb[0], 0.0f), fmaxf(acc[4 * q + 1] + bb[1], 0.0f),
-                                fmaxf(acc[4 * q + 2] + bb[2], 0.0f), fmaxf(acc[4 * q + 3] + bb[3], 0.0f));
-        }
-    }
-    __syncthreads();
-    if (y2o)
-        for (int e = tid; e < nr * kF2; e += kBlock) y2o[(a * R + r0) * kF2 + e] = y2s[(e / kF2) * kSY2 + (e % kF2)];
-    // GRU input side: outputs [24 wv, 24 wv + 24)
-    if (live) {
-        float acc[24];
-#pragma unroll
-        for (int o = 0; o < 24; ++o) acc[o] = 0.0f;
-        dot_rows<kF2, 24>(acc, y2s + lane * kSY2, wi + 24 * wv * kF2, kF2);
-        float4* gd = reinterpret_cast<float4*>(gs + lane * kSG + 24 * wv);
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            const float* bb = bs + kF1 + kF2 + 24 * wv + 4 * q;
-            gd[q] = make_float4(acc[4 * q] + bb[0], acc[4 * q + 1] + bb[1], acc[4 * q + 2] + bb[2],
-                                acc[4 * q + 3] + bb[3]);
-        }
-    }
-    __syncthreads();
-    for (int e = tid; e < nr * kFG; e += kBlock) gi[(a * R + r0) * kFG + e] = gs[(e / kFG) * kSG + (e % kFG)];
 }
 
 // dst[r, :] = src[idx[r], :]  (replay minibatch / chunk gather); one wave per row, 16-B vectors when aligned
@@ -760,7 +748,7 @@ int flock_vdn_feat_fwd(void* stream, int A, int R, int B, int n_in, const float*
     if (!x || !w1 || !b1 || !w2 || !b2 || !w_ih || !b_ih || !gi) return fail(-3, "flock_vdn_feat_fwd: NULL pointer");
     if (n_in < 1 || n_in > kFMaxIn) return fail(-2, "flock_vdn_feat_fwd: n_in must be in [1, 16]");
     if (B < 1 || R % B != 0) return fail(-5, "flock_vdn_feat_fwd: R must be a multiple of B");
-    hipLaunchKernelGGL(vdn_feat_fwd_kernel, dim3((R + kFRows - 1) / kFRows, A), dim3(kBlock), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(vdn_feat_fwd_kernel, dim3(A), dim3(kBlock), 0, (hipStream_t)stream,
                        R, B, n_in, x, x_sa, x_sc, x_sb, w1, b1, w2, b2, w_ih, b_ih, y1, y2, gi);
     return launched();
 }
