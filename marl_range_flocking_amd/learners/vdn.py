@@ -230,9 +230,10 @@ class VDNLearner:
             target_q = target_q + self.gamma * max_q.sum(dim=0) * (1 - done)
         # loss += smooth_l1_loss(sum_q_t, target_q_t) over the chunk steps (:29): per-step means, summed in order
         per_step = F.smooth_l1_loss(sum_q, target_q, reduction="none").mean(dim=1)
-        loss = per_step[0]
+        steps = per_step.unbind(0)  # one backward node (a stack) instead of C select_backward zero-fill + copy pairs
+        loss = steps[0]
         for t in range(1, C):
-            loss = loss + per_step[t]
+            loss = loss + steps[t]
         self.q.P.grads_into(loss, Pq)
         with torch.no_grad():
             self.loss.copy_(loss.detach())
