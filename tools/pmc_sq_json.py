@@ -20,16 +20,17 @@ import statistics
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("dir")
+    ap.add_argument("dirs", nargs="+", help="one rocprofv3 -d directory per PMC pass")
     ap.add_argument("--kernel", default="step_kernel")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     per = collections.defaultdict(lambda: collections.defaultdict(float))  # counter -> dispatch -> value
-    for f in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
+    files = [f for d in a.dirs for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)]
+    for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if a.kernel in row.get("Kernel_Name", ""):
-                    per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+                    per[row["Counter_Name"]][(f, row["Dispatch_Id"])] += float(row["Counter_Value"])
     if not per:
         raise SystemExit("no counter rows found")
     out = {"kernel": a.kernel, "dispatches": max(len(v) for v in per.values())}
