@@ -18,9 +18,16 @@ Rank 0 prints ONE JSON line. Extra fields:
                 uw_discrete 69) x agent-steps per launch / kernel time, frac = achieved / 8 TB/s; the fused replay
                 insert's bytes are reported beside it (insert_bytes_per_agent_step), not in frac; traffic = measured
                 HBM bytes per launch (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, profiles/pmc_*.json).
-                VALU side: executed VALU lane-ops per launch (64 x SQ_INSTS_VALU, profiles/pmc_sq_*.json) / kernel
-                time / 39.3 T lane-ops/s (256 CU x 4 SIMD x 16 lanes x 2.4 GHz, non-packed). "binding" names the
-                larger of the two fractions.
+                VALU side (profiles/pmc_valu_*.json, profiles/ubench_valu.json): gfx950 co-issues the simple VALU ops
+                (f32 add/sub/mul/fma, v_mov_b32, v_add_u32, v_and_b32) of two waves in one quad-cycle (2 cycles per
+                wave64 instruction) and issues the rest in 4 (min/max/med3, compares, packed f32, 64-bit, 3-operand
+                integer ops) or 8 cycles (transcendental); SQ_ACTIVE_INST_VALU charges every instruction its
+                quad-cycles and SQ_ACTIVE_INST_VALU2 counts the co-issued pairs, so the step's VALU issue time per
+                SIMD is busy = 4 x (ACT - ACT2) / 1024 SIMDs cycles (a saturating ubench stream of any class reads
+                0.86-0.97 of its wall cycles on this measure). frac = busy / (kernel time x 2.4 GHz); peak = the
+                lane-op rate of this instruction mix with every SIMD issuing every cycle at 2.4 GHz
+                (64 x SQ_INSTS_VALU x 2.4e9 / busy); frac_full_rate = against 78.6 T lane-op/s (every instruction
+                co-issued). "binding" names the larger of the HBM and VALU fractions.
   cpu_baseline  the C oracle port on every host CPU this process may use (sched_getaffinity, capped by the
                 cgroup CPU quota) and on 1 thread, a bounded sample of the same workload; N=1 only.
 Configs 4 and 5 are 8-GPU configs: their GLOBAL env count (8192 / 16384) is split over the ranks (strong scaling);
@@ -35,7 +42,9 @@ import numpy as np
 import torch
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-VALU_PEAK_LANEOPS = 39.3e12      # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz: non-packed f32 lane-ops/s (packed: 78.6e12)
+CLOCK_HZ = 2.4e9                 # MI355X peak engine clock (MI355X_MICROARCH.md); the roofline's clock
+SIMDS = 1024                     # 256 CU x 4 SIMD
+VALU_PEAK_FULL_RATE = 64 * SIMDS * CLOCK_HZ / 2  # 78.6e12 lane-op/s: every wave64 instruction co-issued (2 cycles)
 BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
 # fused replay insert (flock_step_v2_store / the uw_discrete ring), per agent-step: + previous obs read (k=4 floats)
 # + the ring fields written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG
@@ -193,6 +202,22 @@ def cpu_baseline(args, box, seconds):
             "sample": f"oracle/flock_oracle.c {args.variant} step of {args.agents}-agent envs, sequential vectorized "
                       f"steps for {half:.0f} s: 1 thread x 8 envs ({s1 / t1:.3g} agent-steps/s), {threads} threads "
                       f"(the CPUs this process may use) x 32 envs ({steps / wall:.3g} agent-steps/s); {model}"}
+
+
+def valu_fields(vp, busy, lane_ops, kern_s, alone_ms, tag):
+    """The VALU roofline block: one step's counters (one launch, profiles/pmc_valu_<tag>.json) against the step's
+    HIP-event time in the timed region (kern_s) and alone (alone_ms)."""
+    peak = lane_ops * CLOCK_HZ / busy  # this instruction mix with every SIMD issuing every cycle
+    out = {"insts_per_launch": vp["SQ_INSTS_VALU"], "insts_per_wave": vp.get("valu_insts_per_wave"),
+           "issue_quadcycles": vp["SQ_ACTIVE_INST_VALU"], "coissue_quadcycles": vp["SQ_ACTIVE_INST_VALU2"],
+           "coissued_share": 2.0 * vp["SQ_ACTIVE_INST_VALU2"] / vp["SQ_INSTS_VALU"],
+           "busy_cycles_per_simd": busy, "clock_hz": CLOCK_HZ,
+           "lane_ops_per_s": lane_ops / kern_s, "peak": peak, "unit": "lane-op/s",
+           "frac": busy / (kern_s * CLOCK_HZ),
+           "frac_alone": busy / (alone_ms * 1e-3 * CLOCK_HZ) if alone_ms else None,
+           "peak_full_rate": VALU_PEAK_FULL_RATE, "frac_full_rate": lane_ops / kern_s / VALU_PEAK_FULL_RATE,
+           "source": f"profiles/pmc_valu_{tag}.json", "rates": "profiles/ubench_valu.json"}
+    return out
 
 
 class VDNBench:
@@ -380,13 +405,12 @@ def main():
 
     pt = pmc(os.path.basename(args.pmc)) if args.pmc else pmc(f"pmc_{tag}.json")
     traffic = pt.get("hbm_bytes_per_launch") if pt else None
-    sq = pmc(f"pmc_sq_{tag}.json")
+    vp = pmc(f"pmc_valu_{tag}.json")
     valu = None
-    if sq and "SQ_INSTS_VALU" in sq:
-        lane_ops = 64.0 * sq["SQ_INSTS_VALU"]
-        valu = {"insts_per_launch": sq["SQ_INSTS_VALU"], "insts_per_wave": sq.get("valu_insts_per_wave"),
-                "lane_ops_per_s": lane_ops / kern_s, "peak": VALU_PEAK_LANEOPS, "unit": "lane-op/s",
-                "frac": lane_ops / kern_s / VALU_PEAK_LANEOPS, "source": f"profiles/pmc_sq_{tag}.json"}
+    if vp and "SQ_ACTIVE_INST_VALU2" in vp:
+        busy = 4.0 * (vp["SQ_ACTIVE_INST_VALU"] - vp["SQ_ACTIVE_INST_VALU2"]) / SIMDS  # VALU issue cycles per SIMD
+        lane_ops = 64.0 * vp["SQ_INSTS_VALU"]
+        valu = valu_fields(vp, busy, lane_ops, kern_s, alone_ms, tag)
     hbm_frac = achieved / HBM_PEAK_GBS
     periodic = cfg.resolved().periodic
     c = CONFIGS[args.config]
@@ -430,8 +454,7 @@ def main():
                      "kernel_ms_per_launch": kern_ms / launches,  # compare with rocprofv3's per-dispatch average
                      "kernel_alone_ms": alone_ms,
                      "frac_alone": (bpa * E * N / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if alone_ms else None,
-                     "valu_frac_alone": (64.0 * sq["SQ_INSTS_VALU"] / (alone_ms * 1e-3) / VALU_PEAK_LANEOPS)
-                     if alone_ms and sq and "SQ_INSTS_VALU" in sq else None,
+                     "valu_frac_alone": valu["frac_alone"] if valu else None,
                      "note": "kernel_ms / frac / valu: HIP events around every 4th env step of the timed region (the "
                              "step's launches, with the learner's kernels beside them); *_alone: the same step as one "
                              "launch with no learner, after the timed region"},

@@ -22,6 +22,7 @@ if [[ $PHASES == *ubench* ]]; then
   [ -x tools/ubench_valu ] || hipcc --offload-arch=gfx950 -O3 -Wno-unused-value -o tools/ubench_valu tools/ubench_valu.hip
   step ubench_valu.json 120 tools/ubench_valu
   step ubench_pmc.log 120 rocprofv3 --pmc $PASS_B -d $OUT/ubench_pmc -o run --output-format csv -- tools/ubench_valu
+  python tools/ubench_summary.py $OUT/ubench_valu.json $OUT/ubench_pmc --out $OUT/ubench_valu_merged.json > /dev/null
 fi
 if [[ $PHASES == *bench* ]]; then
   step bench_config3.json 300 python bench.py --config 3

@@ -37,6 +37,35 @@
         for (int i = 0; i < 8; ++i) acc += __float_as_uint(f[i]);                                  \
         out[blockIdx.x * 256 + threadIdx.x] = acc;                                                 \
     }
+// v_cndmask_b32 with its lane mask in an SGPR pair (reading VCC right after the previous statement's VCC clobber
+// makes the compiler pad every instruction with hazard s_nops)
+#define SEL_OP(NAME, ASM)                                                                          \
+    __global__ __launch_bounds__(256) void k_##NAME(unsigned* out, unsigned seed) {                \
+        unsigned a[8];                                                                             \
+        for (int i = 0; i < 8; ++i) a[i] = seed * (threadIdx.x + i);                               \
+        const unsigned b = seed ^ 0x1234u;                                                         \
+        const uint64_t m = 0x5555aaaa3333ccccull ^ seed;                                           \
+        for (int it = 0; it < ITERS; ++it) {                                                       \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) asm volatile(ASM : "+v"(a[i]) : "v"(b), "s"(m)); \
+        }                                                                                          \
+        unsigned acc = 0;                                                                          \
+        for (int i = 0; i < 8; ++i) acc += a[i];                                                   \
+        out[blockIdx.x * 256 + threadIdx.x] = acc;                                                 \
+    }
+// compares writing an SGPR pair (the e64 form), one result register per chain
+#define CMP_OP(NAME, ASM)                                                                          \
+    __global__ __launch_bounds__(256) void k_##NAME(unsigned* out, unsigned seed) {                \
+        float f[8];                                                                                \
+        uint64_t r[8];                                                                             \
+        for (int i = 0; i < 8; ++i) f[i] = (float)(seed * (threadIdx.x + i)) * 1e-9f;              \
+        const float b = 0.999f;                                                                    \
+        for (int it = 0; it < ITERS; ++it) {                                                       \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) asm volatile(ASM : "=s"(r[i]) : "v"(f[i]), "v"(b)); \
+        }                                                                                          \
+        unsigned acc = 0;                                                                          \
+        for (int i = 0; i < 8; ++i) acc += (unsigned)r[i];                                         \
+        out[blockIdx.x * 256 + threadIdx.x] = acc;                                                 \
+    }
 #define U64_OP(NAME, ASM)                                                                          \
     __global__ __launch_bounds__(256) void k_##NAME(unsigned* out, unsigned seed) {                \
         uint64_t a[8];                                                                             \
@@ -67,7 +96,23 @@
     X(F32, v_sin_f32, "TRANS_F32", "v_sin_f32 %0, %0")                                             \
     X(F32, v_cmp_lt_f32, "other", "v_cmp_lt_f32 vcc, %0, %1")                                      \
     X(F32, v_cvt_i32_f32, "CVT", "v_cvt_i32_f32 %0, %0")                                           \
-    X(U32, v_cndmask_b32, "INT32", "v_cndmask_b32 %0, %0, %1, vcc")                                \
+    X(SEL, v_cndmask_b32, "INT32", "v_cndmask_b32 %0, %0, %1, %2")                                 \
+    X(CMP, v_cmp_lt_f32_e64, "other", "v_cmp_lt_f32_e64 %0, %1, %2")                               \
+    X(F32, v_max_f32, "other", "v_max_f32 %0, %0, %1")                                             \
+    X(F32, v_subrev_f32, "ADD_F32", "v_subrev_f32 %0, %0, %1")                                     \
+    X(F32, v_fmac_f32, "FMA_F32", "v_fmac_f32 %0, %1, %2")                                         \
+    X(U32, v_or_b32, "INT32", "v_or_b32 %0, %0, %1")                                               \
+    X(U32, v_xor_b32, "INT32", "v_xor_b32 %0, %0, %1")                                             \
+    X(U32, v_sub_u32, "INT32", "v_sub_u32 %0, %0, %1")                                             \
+    X(U32, v_lshlrev_b32, "INT32", "v_lshlrev_b32 %0, 1, %0")                                      \
+    X(U32, v_lshrrev_b32, "INT32", "v_lshrrev_b32 %0, 1, %0")                                      \
+    X(U32, v_max_u32, "INT32", "v_max_u32 %0, %0, %1")                                             \
+    X(U32, v_bfi_b32, "INT32", "v_bfi_b32 %0, %1, %0, %2")                                         \
+    X(U32, v_bfe_u32, "INT32", "v_bfe_u32 %0, %0, 3, 9")                                           \
+    X(U32, v_lshl_or_b32, "INT32", "v_lshl_or_b32 %0, %0, 1, %1")                                  \
+    X(U32, v_alignbit_b32, "INT32", "v_alignbit_b32 %0, %0, %1, 7")                                \
+    X(U32, v_mul_hi_u32, "INT32", "v_mul_hi_u32 %0, %0, %1")                                       \
+    X(U32, v_cvt_f32_u32, "CVT", "v_cvt_f32_u32 %0, %0")                                           \
     X(U32, v_mov_b32, "INT32", "v_mov_b32 %0, %1")                                                 \
     X(U32, v_med3_u32, "INT32", "v_med3_u32 %0, %0, %1, %2")                                       \
     X(U32, v_min_u32, "INT32", "v_min_u32 %0, %0, %1")                                             \
