@@ -28,8 +28,10 @@ Rank 0 prints ONE JSON line. Extra fields:
                 lane-op rate of this instruction mix with every SIMD issuing every cycle at 2.4 GHz
                 (64 x SQ_INSTS_VALU x 2.4e9 / busy); frac_full_rate = against 78.6 T lane-op/s (every instruction
                 co-issued). "binding" names the larger of the HBM and VALU fractions.
-  cpu_baseline  the C oracle port on every host CPU this process may use (sched_getaffinity, capped by the
-                cgroup CPU quota) and on 1 thread, a bounded sample of the same workload; N=1 only.
+  cpu_baseline  the reference's step on the host: v2 = environments/gym_flock_v2.py's torch-CPU op sequence
+                (oracle/torch_ref.py, calibrated against the reference, tests/golden/cpu_calibration.json) stepping
+                one env at a time on every host CPU this process may use (sched_getaffinity, capped by the cgroup
+                CPU quota) and on 1 thread; other variants the C oracle port; a bounded sample; N=1 only.
 Configs 4 and 5 are 8-GPU configs: their GLOBAL env count (8192 / 16384) is split over the ranks (strong scaling);
 config 3 (the headline) keeps 4096 envs per GPU (weak scaling).
 """
@@ -79,6 +81,10 @@ def parse():
                     help="env step as this many launches over env ranges (FlockConfig.step_launches; default: 2 "
                          "with the overlapped shared-critic learner, whose rounds take the slots the first "
                          "launch's tail frees; 1 otherwise)")
+    ap.add_argument("--loop", type=int, default=1, choices=[0, 1],
+                    help="config 3: enqueue the timed steps (env step + learn()) through torch.classes.flock."
+                         "ScTrainLoop, K steps per C++ call (bitwise the per-step path); 0: one Python call per step "
+                         "(flock::step_v2_store + the native learn() pipeline)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
                          "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
@@ -185,14 +191,60 @@ def host_cpus():
     return n, model
 
 
-def cpu_baseline(args, box, seconds):
-    """The C oracle (oracle/flock_oracle.c) on the host: 1 thread, then one thread per usable host CPU, each
-    stepping its own envs; a bounded sample of the same workload."""
-    from concurrent.futures import ThreadPoolExecutor
+def _torch_ref_run(args, box, seconds, threads, seed):
+    """The reference's v2 step as its torch-CPU op sequence (oracle/torch_ref.py), one env object stepped at a time
+    as the reference steps its single env, on `threads` torch threads for `seconds`: agent-steps/s."""
+    from oracle.torch_ref import V2Env
 
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        N, k = args.agents, args.k
+        g = torch.Generator().manual_seed(seed)
+        env = V2Env(torch.rand(N, 2, generator=g) * box, (1.0 - torch.rand(N, generator=g)) * 1.5 * np.pi, k=k,
+                    box=box, sensor_range=14.0, collision_distance=2.5)
+        acts = [torch.stack([torch.rand(N, generator=g), torch.rand(N, generator=g) * 3 - 1.5], -1) for _ in range(8)]
+        for a in acts[:2]:
+            env.step(a)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            env.step(acts[n % 8])
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                return N * n / el, n
+    finally:
+        torch.set_num_threads(prev)
+
+
+def cpu_baseline(args, box, seconds):
+    """The reference's CPU step on the box's host cores, a bounded sample of the same workload. v2 (the headline):
+    the torch-CPU restatement of environments/gym_flock_v2.py's step (oracle/torch_ref.py; pinned against the
+    reference's golden vectors by tests/test_cpu_baseline.py and timed against the reference itself, ratio ~1.0, in
+    tests/golden/cpu_calibration.json), one env at a time as the reference runs, on every usable host CPU and on one
+    thread. Other variants: the C oracle port (oracle/flock_oracle.c) on the same cores."""
     threads, model = host_cpus()
     half = seconds / 2
+    if args.variant == "v2":
+        v1, n1 = _torch_ref_run(args, box, half, 1, 0)
+        vt, nt = _torch_ref_run(args, box, half, threads, 1)
+        calib = None
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "cpu_calibration.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                calib = [r for r in json.load(f)["rows"] if r["N"] == args.agents] or None
+        best = max(v1, vt)
+        return {"value": best, "unit": "agent-steps/s", "cores": threads if vt >= v1 else 1, "kind": "port",
+                "value_1thread": v1, "value_all_threads": vt, "cpu_model": model, "host_cpus": os.cpu_count(),
+                "calibration_vs_reference": calib,
+                "sample": f"oracle/torch_ref.py: environments/gym_flock_v2.py's step as its torch-CPU op sequence "
+                          f"(meshgrid distances, topk, clamp, .item() sync), one {args.agents}-agent env stepped "
+                          f"sequentially as the reference does, {half:.0f} s on 1 torch thread ({n1} steps, "
+                          f"{v1:.3g} agent-steps/s) and {half:.0f} s on {threads} threads (the CPUs this process may "
+                          f"use; {nt} steps, {vt:.3g} agent-steps/s); value = the faster; {model}"}
     s1, t1 = _cpu_run(args, box, half, 0)
+    from concurrent.futures import ThreadPoolExecutor
+
     with ThreadPoolExecutor(threads) as ex:  # 32 envs per C call: the per-call Python work is negligible
         res = list(ex.map(lambda i: _cpu_run(args, box, half, 1 + i, E_s=32), range(threads)))
     steps = sum(r[0] for r in res)
@@ -345,8 +397,12 @@ def main():
             hook.after(s, a)
 
     stream = torch.cuda.current_stream(dev)
-    for s in range(args.warmup):
-        one_step(s)
+    use_loop = bool(args.loop) and hook is not None and getattr(hook, "can_loop", lambda: False)()
+    if use_loop:
+        hook.run_steps(0, args.warmup, pool)
+    else:
+        for s in range(args.warmup):
+            one_step(s)
     if hook is not None:
         hook.prime()  # graph capture / first update outside the timed region
     torch.cuda.synchronize(dev)
@@ -354,12 +410,18 @@ def main():
     # would add host and queue work of their own to a ~13-us launch-bound step)
     ev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for s in range(0, args.steps, EV_EVERY)}
+    evs = [e for s in sorted(ev) for e in ev[s]]
+    for e in evs:  # create the HIP events outside the timed region
+        e.record(stream)
 
     barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        one_step(args.warmup + s, ev.get(s))
+    if use_loop:
+        hook.run_steps(args.warmup, args.steps, pool, evs, EV_EVERY)
+    else:
+        for s in range(args.steps):
+            one_step(args.warmup + s, ev.get(s))
     if hook is not None and hasattr(hook, "finish"):
         hook.finish()  # the learner work still pending (the last learn's actor phase) runs inside the timed region
     host_el = time.perf_counter() - t0  # host enqueue time of the timed steps (no synchronisation inside)
@@ -430,6 +492,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
         "host_ms_per_step": host_el / args.steps * 1e3,
+        "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
+                      "one Python step per vectorized step (torch.ops.flock)"),
         "higher_is_better": True,
         "scaling": "strong" if args.global_split else "weak",
         "vs_baseline": None,

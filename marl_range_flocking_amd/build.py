@@ -19,7 +19,7 @@ ARCH = os.environ.get("FLOCK_OFFLOAD_ARCH", "gfx950")
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}"]
 
 
-TORCH_OPS_SRC = os.path.join(CSRC, "flock_torch.cpp")
+TORCH_OPS_SRCS = [os.path.join(CSRC, f) for f in ("flock_torch.cpp", "flock_torch_learn.cpp", "flock_torch_loop.cpp")]
 TORCH_OPS_LIB = os.path.join(BUILD_DIR, "libflock_torch.so")
 
 
@@ -48,9 +48,9 @@ FILE_FLAGS = {"flock_env.hip": ["-fno-slp-vectorize"]}
 
 
 def build_torch_ops(force=False, verbose=False):
-    """libflock_torch.so: the TORCH_LIBRARY(flock) custom ops (csrc/flock_torch.cpp), host C++ over libflock_amd.so,
+    """libflock_torch.so: the TORCH_LIBRARY(flock) custom ops (csrc/flock_torch*.cpp), host C++ over libflock_amd.so,
     compiled against this interpreter's torch headers and linked with rpath $ORIGIN."""
-    deps = [TORCH_OPS_SRC, LIB_PATH] + glob.glob(os.path.join(INCLUDE, "*.h"))
+    deps = TORCH_OPS_SRCS + [LIB_PATH] + glob.glob(os.path.join(INCLUDE, "*.h"))
     if not force and os.path.exists(TORCH_OPS_LIB) and all(os.path.getmtime(d) <= os.path.getmtime(TORCH_OPS_LIB)
                                                            for d in deps):
         return TORCH_OPS_LIB
@@ -62,9 +62,9 @@ def build_torch_ops(force=False, verbose=False):
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
            f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}", "-I", INCLUDE,
            "-I", os.path.join(rocm, "include"), "-I", os.path.join(tdir, "include"),
-           "-I", os.path.join(tdir, "include", "torch", "csrc", "api", "include"), TORCH_OPS_SRC, "-o", tmp,
+           "-I", os.path.join(tdir, "include", "torch", "csrc", "api", "include"), *TORCH_OPS_SRCS, "-o", tmp,
            "-L", BUILD_DIR, "-lflock_amd", "-L", os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch",
-           "-ltorch_cpu", "-Wl,-rpath,$ORIGIN"]
+           "-ltorch_cpu", "-L", os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

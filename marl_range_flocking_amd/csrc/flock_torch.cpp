@@ -10,9 +10,13 @@
 //   flock::step_uw           gym_flock_uw.py:69-81
 //   flock::step_uw_discrete  gym_flock_uw_discrete.py:110-122
 //   flock::step_flock        gym_flock.py:48-60
+//   flock::step_v2_store     step_v2 + the training loop's replay insert in the same launch (store_transitions,
+//                            maddpg_shared_critic/utils.py:47-54; add_record, maddpg_official_rnn/memory_rnn.py:53-67)
+//   flock::step_uw_discrete_store  step_uw_discrete + the VDN team transition (memory.put, vdn/train_flock.py:102)
 //   flock::knn               _computePeriodicDistances :135-151 / _computeDistances :155-175 (functional)
 //   flock::reset             reset() :85-108 and siblings (bounded draws + repair, flock_reset_ext)
 #include <ATen/ATen.h>
+#include <ATen/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -59,6 +63,12 @@ void rc_check(int rc, const char* fn) { TORCH_CHECK(rc == 0, fn, ": ", flock_las
 
 bool on_hip(const Tensor& t) { return t.device().is_cuda(); }
 
+// FlockStepExt.launches: the step as that many back-to-back launches over consecutive env ranges (same results)
+int launch_count(int64_t launches) {
+    TORCH_CHECK(launches >= 1 && launches <= 64, "launches must be in [1, 64], got ", launches);
+    return (int)launches;
+}
+
 // ----------------------------------------------------------------------------------------------------- step_v2
 void step_v2_checks(const Tensor& pos, const Tensor& heading, const Tensor& action, const Tensor& vel,
                     const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
@@ -81,10 +91,11 @@ void step_v2_hip(const Tensor& pos, const Tensor& heading, const Tensor& action,
                  const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
                  const Tensor& any_done, const optional<Tensor>& seeds, int64_t k, double box, double sensor_range,
                  double collision_distance, double dt, double v_min, double v_max, bool periodic,
-                 bool rigid_boundary) {
+                 bool rigid_boundary, int64_t launches) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds)};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_v2_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, (float)v_min,
                                (float)v_max, periodic, rigid_boundary, ptr<float>(pos), ptr<float>(heading),
@@ -96,7 +107,8 @@ void step_v2_hip(const Tensor& pos, const Tensor& heading, const Tensor& action,
 void step_v2_meta(const Tensor& pos, const Tensor& heading, const Tensor& action, const Tensor& vel,
                   const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
                   const Tensor& any_done, const optional<Tensor>& seeds, int64_t k, double, double, double, double,
-                  double, double, bool, bool) {
+                  double, double, bool, bool, int64_t launches) {
+    launch_count(launches);
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
 }
 
@@ -126,11 +138,12 @@ void step_uw_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_he
                  const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
                  const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
                  const optional<Tensor>& seeds, int64_t k, double box, double sensor_range,
-                 double collision_distance, double dt, bool rigid_boundary) {
+                 double collision_distance, double dt, bool rigid_boundary, int64_t launches) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
     step_uw_checks(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
                    seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds)};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_uw_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, rigid_boundary,
                                ptr<float>(pos), ptr<const float>(heading), ptr<float>(prev_heading),
@@ -143,7 +156,8 @@ void step_uw_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_he
 void step_uw_meta(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading, const Tensor& action,
                   const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
                   const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
-                  const optional<Tensor>& seeds, int64_t k, double, double, double, double, bool) {
+                  const optional<Tensor>& seeds, int64_t k, double, double, double, double, bool, int64_t launches) {
+    launch_count(launches);
     step_uw_checks(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
                    seeds, k);
 }
@@ -177,11 +191,12 @@ void step_uwd_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_h
                   const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
                   const Tensor& status, const optional<Tensor>& seeds, int64_t k, double box, double sensor_range,
                   double collision_distance, double dt, double v_max, bool rigid_boundary, double noise_std,
-                  int64_t seed, int64_t rng_offset) {
+                  int64_t seed, int64_t rng_offset, int64_t launches) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds)};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_uw_discrete_ext(
                  stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
                  (float)collision_distance, (float)dt, (float)v_max, rigid_boundary, ptr<float>(pos),
@@ -197,7 +212,8 @@ void step_uwd_meta(const Tensor& pos, const Tensor& heading, const Tensor& prev_
                    const optional<Tensor>& noise, const Tensor& table, const Tensor& vel, const Tensor& dnn,
                    const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
                    const Tensor& status, const optional<Tensor>& seeds, int64_t k, double, double, double, double,
-                   double, bool, double, int64_t, int64_t) {
+                   double, bool, double, int64_t, int64_t, int64_t launches) {
+    launch_count(launches);
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
 }
@@ -225,10 +241,11 @@ void step_flock_checks(const Tensor& pos, const Tensor& vel, const Tensor& actio
 void step_flock_hip(const Tensor& pos, const Tensor& vel, const Tensor& action, const Tensor& mem_in,
                     const Tensor& mem_out, const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward,
                     const Tensor& done, const Tensor& any_done, const optional<Tensor>& seeds, int64_t k,
-                    double box, double collision_distance, double dt, bool rigid_boundary) {
+                    double box, double collision_distance, double dt, bool rigid_boundary, int64_t launches) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
     step_flock_checks(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds)};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_flock_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                   (float)collision_distance, (float)dt, rigid_boundary, ptr<float>(pos),
                                   ptr<float>(vel), ptr<const float>(action), ptr<const float>(mem_in),
@@ -240,8 +257,131 @@ void step_flock_hip(const Tensor& pos, const Tensor& vel, const Tensor& action, 
 void step_flock_meta(const Tensor& pos, const Tensor& vel, const Tensor& action, const Tensor& mem_in,
                      const Tensor& mem_out, const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward,
                      const Tensor& done, const Tensor& any_done, const optional<Tensor>& seeds, int64_t k, double,
-                     double, double, bool) {
+                     double, double, bool, int64_t launches) {
+    launch_count(launches);
     step_flock_checks(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, seeds, k);
+}
+
+
+// ------------------------------------------------------------------------------------ fused replay insert (ring)
+// ring = [state, action, reward, new_state, terminal] device rings ([capacity, ...] f32), the optional record copies
+// actor_state / actor_new_state, prev_obs [E, N, k] (the observation before the step); meta = [start, skip, group,
+// store_done, action_ids, env_done] (FlockRing, include/flock_amd.h)
+FlockRing ring_of(const Tensor& pos, at::TensorList ring, const optional<Tensor>& actor_state,
+                  const optional<Tensor>& actor_new_state, const Tensor& prev_obs, at::IntArrayRef meta, int64_t k) {
+    auto [E, N] = dims(pos);
+    TORCH_CHECK(ring.size() == 5, "ring must be [state, action, reward, new_state, terminal]");
+    TORCH_CHECK(meta.size() == 6, "ring_meta must be [start, skip, group, store_done, action_ids, env_done]");
+    const int64_t start = meta[0], skip = meta[1], group = meta[2];
+    const bool ids = meta[4] != 0, env_done = meta[5] != 0;
+    TORCH_CHECK(group == 1 || group == N, "ring group must be 1 (a row per agent) or N (a row per env)");
+    TORCH_CHECK(!env_done || group == N, "env_done needs a row per env (group = N)");
+    TORCH_CHECK(ring[0].dim() >= 1, "ring fields must be [capacity, ...]");
+    const int64_t cap = ring[0].size(0), units = group == 1 ? E * N : E;
+    TORCH_CHECK(skip >= 0 && units - skip <= cap && start >= 0 && start < cap,
+                "ring: need 0 <= skip, rows - skip <= capacity and 0 <= start < capacity");
+    const char* names[5] = {"ring state", "ring action", "ring reward", "ring new_state", "ring terminal"};
+    const int64_t w[5] = {group * k, group * (ids ? 1 : 2), group, group * k, env_done ? 1 : group};
+    for (int i = 0; i < 5; ++i) {
+        TORCH_CHECK(ring[i].device() == pos.device() && ring[i].scalar_type() == at::kFloat &&
+                        ring[i].is_contiguous() && ring[i].dim() >= 1 && ring[i].size(0) == cap &&
+                        ring[i].numel() == cap * w[i],
+                    names[i], " must be a contiguous f32 [", cap, ", ", w[i], "] ring on ", pos.device());
+    }
+    const optional<Tensor>* extra[2] = {&actor_state, &actor_new_state};
+    for (const optional<Tensor>* t : extra)
+        if (t->has_value())
+            TORCH_CHECK((*t)->device() == pos.device() && (*t)->scalar_type() == at::kFloat &&
+                            (*t)->is_contiguous() && (*t)->numel() == cap * group * k,
+                        "ring actor_state / actor_new_state must be contiguous f32 [", cap, ", ", group * k, "]");
+    need(prev_obs, "prev_obs", at::kFloat, {E, N, k}, pos);
+    FlockRing r{};
+    r.state = ptr<float>(ring[0]);
+    r.action = ptr<float>(ring[1]);
+    r.reward = ptr<float>(ring[2]);
+    r.new_state = ptr<float>(ring[3]);
+    r.terminal = ptr<float>(ring[4]);
+    r.prev_obs = ptr<const float>(prev_obs);
+    r.capacity = cap;
+    r.start = start;
+    r.skip = skip;
+    r.actor_state = ptr<float>(actor_state);
+    r.actor_new_state = ptr<float>(actor_new_state);
+    r.group = group;
+    r.store_done = meta[3] != 0;
+    r.action_ids = ids;
+    r.env_done = env_done;
+    return r;
+}
+
+void step_v2_store_hip(const Tensor& pos, const Tensor& heading, const Tensor& action, const Tensor& vel,
+                       const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
+                       const Tensor& any_done, const optional<Tensor>& seeds, at::TensorList ring,
+                       const optional<Tensor>& actor_state, const optional<Tensor>& actor_new_state,
+                       const Tensor& prev_obs, at::IntArrayRef ring_meta, int64_t k, double box, double sensor_range,
+                       double collision_distance, double dt, double v_min, double v_max, bool periodic,
+                       bool rigid_boundary, int64_t launches) {
+    TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
+    step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
+    TORCH_CHECK(ring_meta.size() == 6 && ring_meta[4] == 0 && ring_meta[5] == 0,
+                "step_v2_store: action ids / env done flags are the uw_discrete ring's");
+    const FlockRing r = ring_of(pos, ring, actor_state, actor_new_state, prev_obs, ring_meta, k);
+    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    rc_check(flock_step_v2_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
+                               (float)sensor_range, (float)collision_distance, (float)dt, (float)v_min,
+                               (float)v_max, periodic, rigid_boundary, ptr<float>(pos), ptr<float>(heading),
+                               ptr<const float>(action), ptr<float>(vel), ptr<float>(dnn), ptr<int64_t>(nn_idx),
+                               ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(any_done), &ext),
+             "flock_step_v2_store");
+}
+
+void step_v2_store_meta(const Tensor& pos, const Tensor& heading, const Tensor& action, const Tensor& vel,
+                        const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
+                        const Tensor& any_done, const optional<Tensor>& seeds, at::TensorList ring,
+                        const optional<Tensor>& actor_state, const optional<Tensor>& actor_new_state,
+                        const Tensor& prev_obs, at::IntArrayRef ring_meta, int64_t k, double, double, double, double,
+                        double, double, bool, bool, int64_t launches) {
+    launch_count(launches);
+    step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
+    ring_of(pos, ring, actor_state, actor_new_state, prev_obs, ring_meta, k);
+}
+
+void step_uwd_store_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading, const Tensor& action_id,
+                        const optional<Tensor>& noise, const Tensor& table, const Tensor& vel, const Tensor& dnn,
+                        const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
+                        const Tensor& any_done, const Tensor& status, const optional<Tensor>& seeds,
+                        at::TensorList ring, const Tensor& prev_obs, at::IntArrayRef ring_meta, int64_t k, double box,
+                        double sensor_range, double collision_distance, double dt, double v_max, bool rigid_boundary,
+                        double noise_std, int64_t seed, int64_t rng_offset, int64_t launches) {
+    TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
+    step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
+                    status, seeds, k);
+    const FlockRing r = ring_of(pos, ring, c10::nullopt, c10::nullopt, prev_obs, ring_meta, k);
+    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    rc_check(flock_step_uw_discrete_ext(
+                 stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
+                 (float)collision_distance, (float)dt, (float)v_max, rigid_boundary, ptr<float>(pos),
+                 ptr<float>(heading), ptr<float>(prev_heading), ptr<const int64_t>(action_id),
+                 ptr<const float>(noise), (float)noise_std, (uint64_t)seed, (uint64_t)rng_offset,
+                 ptr<const float>(table), (int)table.size(0), ptr<float>(vel), ptr<float>(dnn),
+                 ptr<int64_t>(nn_idx), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(any_done),
+                 ptr<int>(status), &ext),
+             "flock_step_uw_discrete_store");
+}
+
+void step_uwd_store_meta(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading,
+                         const Tensor& action_id, const optional<Tensor>& noise, const Tensor& table,
+                         const Tensor& vel, const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward,
+                         const Tensor& done, const Tensor& any_done, const Tensor& status,
+                         const optional<Tensor>& seeds, at::TensorList ring, const Tensor& prev_obs,
+                         at::IntArrayRef ring_meta, int64_t k, double, double, double, double, double, bool, double,
+                         int64_t, int64_t, int64_t launches) {
+    launch_count(launches);
+    step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
+                    status, seeds, k);
+    ring_of(pos, ring, c10::nullopt, c10::nullopt, prev_obs, ring_meta, k);
 }
 
 // --------------------------------------------------------------------------------------------------------- knn
@@ -255,6 +395,7 @@ std::tuple<Tensor, Tensor> knn_alloc(const Tensor& pos, int64_t k) {
 std::tuple<Tensor, Tensor> knn_hip(const Tensor& pos_in, int64_t k, double box, double sensor_range, bool periodic,
                                    bool clamp) {
     TORCH_CHECK(on_hip(pos_in), "flock ops run on a HIP device only (no CPU fallback); got ", pos_in.device());
+    const at::OptionalDeviceGuard guard(pos_in.device());
     const Tensor pos = pos_in.contiguous();
     auto out = knn_alloc(pos, k);
     rc_check(flock_knn(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
@@ -294,6 +435,7 @@ void reset_hip(const Tensor& pos, const Tensor& dnn, const optional<Tensor>& hea
                double check_distance, bool rigid_boundary, int64_t max_attempts, int64_t seed, int64_t rng_offset,
                int64_t repair_rounds) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
     reset_checks(pos, dnn, heading, prev_heading, vel, nn_idx, mem, valid, env_mask, variant, k);
     rc_check(flock_reset_ext(stream_of(pos), (int)variant, (int)pos.size(0), (int)pos.size(1), (int)k,
                              (float)range_lo, (float)range_hi, (float)box, (float)sensor_range, (float)check_distance,
@@ -319,23 +461,36 @@ TORCH_LIBRARY(flock, m) {
         "step_v2(Tensor(a!) pos, Tensor(b!) heading, Tensor action, Tensor(c!) vel, Tensor(d!) dnn, "
         "Tensor(e!)? nn_idx, Tensor(f!) reward, Tensor(g!) done, Tensor(h!) any_done, Tensor(i!)? seeds, int k, "
         "float box, float sensor_range, float collision_distance, float dt=0.1, float v_min=0.005, "
-        "float v_max=2.5, bool periodic=True, bool rigid_boundary=False) -> ()");
+        "float v_max=2.5, bool periodic=True, bool rigid_boundary=False, int launches=1) -> ()");
     m.def(
         "step_uw(Tensor(a!) pos, Tensor heading, Tensor(b!) prev_heading, Tensor action, Tensor mem_in, "
         "Tensor(c!) mem_out, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
         "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!)? seeds, int k, float box, float sensor_range, "
-        "float collision_distance, float dt=0.1, bool rigid_boundary=False) -> ()");
+        "float collision_distance, float dt=0.1, bool rigid_boundary=False, int launches=1) -> ()");
     m.def(
         "step_uw_discrete(Tensor(a!) pos, Tensor(b!) heading, Tensor(c!) prev_heading, Tensor action_id, "
         "Tensor? noise, Tensor table, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
         "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!) status, Tensor(l!)? seeds, int k, float box, "
         "float sensor_range, float collision_distance, float dt=0.1, float v_max=2.5, bool rigid_boundary=False, "
-        "float noise_std=0.1, int seed=0, int rng_offset=0) -> ()");
+        "float noise_std=0.1, int seed=0, int rng_offset=0, int launches=1) -> ()");
     m.def(
         "step_flock(Tensor(a!) pos, Tensor(b!) vel, Tensor action, Tensor mem_in, Tensor(c!) mem_out, "
         "Tensor(d!) dnn, Tensor(e!)? nn_idx, Tensor(f!) reward, Tensor(g!) done, Tensor(h!) any_done, "
         "Tensor(i!)? seeds, int k, float box, float collision_distance, float dt=0.1, "
-        "bool rigid_boundary=False) -> ()");
+        "bool rigid_boundary=False, int launches=1) -> ()");
+    m.def(
+        "step_v2_store(Tensor(a!) pos, Tensor(b!) heading, Tensor action, Tensor(c!) vel, Tensor(d!) dnn, "
+        "Tensor(e!)? nn_idx, Tensor(f!) reward, Tensor(g!) done, Tensor(h!) any_done, Tensor(i!)? seeds, "
+        "Tensor(j!)[] ring, Tensor(k!)? ring_actor_state, Tensor(l!)? ring_actor_new_state, Tensor prev_obs, "
+        "int[] ring_meta, int k, float box, float sensor_range, float collision_distance, float dt=0.1, "
+        "float v_min=0.005, float v_max=2.5, bool periodic=True, bool rigid_boundary=False, int launches=1) -> ()");
+    m.def(
+        "step_uw_discrete_store(Tensor(a!) pos, Tensor(b!) heading, Tensor(c!) prev_heading, Tensor action_id, "
+        "Tensor? noise, Tensor table, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
+        "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!) status, Tensor(l!)? seeds, Tensor(m!)[] ring, "
+        "Tensor prev_obs, int[] ring_meta, int k, float box, float sensor_range, float collision_distance, "
+        "float dt=0.1, float v_max=2.5, bool rigid_boundary=False, float noise_std=0.1, int seed=0, "
+        "int rng_offset=0, int launches=1) -> ()");
     m.def(
         "knn(Tensor pos, int k, float box, float sensor_range=14.0, bool periodic=True, bool clamp=True) "
         "-> (Tensor dnn, Tensor nn_idx)");
@@ -351,6 +506,8 @@ TORCH_LIBRARY_IMPL(flock, CUDA, m) {  // ROCm builds of PyTorch dispatch HIP ten
     m.impl("step_uw", &step_uw_hip);
     m.impl("step_uw_discrete", &step_uwd_hip);
     m.impl("step_flock", &step_flock_hip);
+    m.impl("step_v2_store", &step_v2_store_hip);
+    m.impl("step_uw_discrete_store", &step_uwd_store_hip);
     m.impl("knn", &knn_hip);
     m.impl("reset", &reset_hip);
 }
@@ -360,6 +517,8 @@ TORCH_LIBRARY_IMPL(flock, Meta, m) {
     m.impl("step_uw", &step_uw_meta);
     m.impl("step_uw_discrete", &step_uwd_meta);
     m.impl("step_flock", &step_flock_meta);
+    m.impl("step_v2_store", &step_v2_store_meta);
+    m.impl("step_uw_discrete_store", &step_uwd_store_meta);
     m.impl("knn", &knn_meta);
     m.impl("reset", &reset_meta);
 }

@@ -30,6 +30,13 @@ def _stream(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
+def _ops():
+    """torch.ops.flock (csrc/flock_torch*.cpp): every learner kernel below launches through these custom ops."""
+    from .. import torch_ops
+
+    return torch_ops.load()
+
+
 def _require_cuda(t):
     if t.device.type != "cuda":
         raise RuntimeError("learner kernels run on a HIP device only (no CPU fallback)")
@@ -163,20 +170,20 @@ class FlatParams:
             self.agent_steps[agent] += 1
             (lo, hi), step = self.agent_range(agent), self.agent_steps[agent]
         sl = lambda t: None if t is None else t[lo:hi]  # noqa: E731
-        rc = _native.lib().flock_adam_step(
-            _stream(self.device), hi - lo, _p(sl(self.data)), _p(sl(self.grad)), _p(sl(self.exp_avg)),
-            _p(sl(self.exp_avg_sq)), _p(grad_scale), float(lr), float(betas[0]), float(betas[1]), float(eps), step,
-            _p(sl(self.target)) if tau is not None else None, float(tau or 0.0), int(target_mode))
-        _native.check(rc, "flock_adam_step", learn=True)
+        st = self.__dict__.get("_host_step")
+        if st is None:
+            st = self._host_step = torch.zeros(1, dtype=torch.int64, device=self.device)
+        st.fill_(step)
+        _ops().adam_step(sl(self.data), sl(self.grad), sl(self.exp_avg), sl(self.exp_avg_sq), st, grad_scale,
+                         sl(self.target) if tau is not None else None, float(lr), float(betas[0]), float(betas[1]),
+                         float(eps), float(tau or 0.0), int(target_mode))
 
     def adam_step_dev(self, lr, betas=(0.9, 0.999), eps=1e-8, grad_scale=None, tau=None, target_mode=0):
         """Adam step with the step count kept on the device (step_dev += 1 then the update): HIP-graph capturable."""
         self.step_dev.add_(1)
-        rc = _native.lib().flock_adam_step_dev(
-            _stream(self.device), self.numel, _p(self.data), _p(self.grad), _p(self.exp_avg), _p(self.exp_avg_sq),
-            _p(grad_scale), float(lr), float(betas[0]), float(betas[1]), float(eps), _p(self.step_dev),
-            _p(self.target) if tau is not None else None, float(tau or 0.0), int(target_mode))
-        _native.check(rc, "flock_adam_step_dev", learn=True)
+        _ops().adam_step(self.data, self.grad, self.exp_avg, self.exp_avg_sq, self.step_dev, grad_scale,
+                         self.target if tau is not None else None, float(lr), float(betas[0]), float(betas[1]),
+                         float(eps), float(tau or 0.0), int(target_mode))
 
     def state_tensors(self):
         return [t for t in (self.data, self.exp_avg, self.exp_avg_sq, self.target, self.step_dev) if t is not None]
@@ -186,9 +193,7 @@ class FlatParams:
         (the shared critic is its own target, agent_simple_shared_critic.py:63,76,172-178)."""
         lo, hi = (0, self.numel) if agent is None else self.agent_range(agent)
         dst = self.data if self_update else self.target
-        rc = _native.lib().flock_soft_update(_stream(self.device), hi - lo, _p(dst[lo:hi]), _p(self.data[lo:hi]),
-                                             float(tau), int(mode))
-        _native.check(rc, "flock_soft_update", learn=True)
+        _ops().soft_update(dst[lo:hi], self.data[lo:hi], float(tau), int(mode))
 
     def hard_update_target(self):
         self.target.copy_(self.data)
@@ -217,9 +222,7 @@ class GradNorm:
         self.max_parts = max_parts
 
     def __call__(self, grad, max_norm):
-        rc = _native.lib().flock_grad_norm(_stream(grad.device), grad.numel(), _p(grad), _p(self.partial),
-                                           self.max_parts, float(max_norm), _p(self.out))
-        _native.check(rc, "flock_grad_norm", learn=True)
+        _ops().grad_norm(grad, self.partial, self.out, float(max_norm))
         return self.out
 
 
@@ -269,8 +272,7 @@ class _GRUCellFn(torch.autograd.Function):
         rows = h.numel() // H
         hout = torch.empty_like(h)
         ws = torch.empty(rows * 4 * H, dtype=h.dtype, device=h.device)
-        rc = _native.lib().flock_gru_fwd(_stream(h.device), rows, H, _p(gi), _p(gh), _p(h), _p(hout), _p(ws))
-        _native.check(rc, "flock_gru_fwd", learn=True)
+        _ops().gru_cell_fwd(gi, gh, h, hout, ws)
         ctx.save_for_backward(h, ws)
         ctx.H = H
         return hout
@@ -284,9 +286,7 @@ class _GRUCellFn(torch.autograd.Function):
         dgi = torch.empty(*h.shape[:-1], 3 * H, dtype=h.dtype, device=h.device)
         dgh = torch.empty_like(dgi)
         dh = torch.empty_like(h)
-        rc = _native.lib().flock_gru_bwd(_stream(h.device), rows, H, _p(dhout), _p(h), _p(ws), _p(dgi), _p(dgh),
-                                         _p(dh))
-        _native.check(rc, "flock_gru_bwd", learn=True)
+        _ops().gru_cell_bwd(dhout, h, ws, dgi, dgh, dh)
         return dgi, dgh, dh
 
 
@@ -306,10 +306,7 @@ class _GRUSeqFn(torch.autograd.Function):
         k8 = keep.view(torch.uint8) if keep.dtype == torch.bool else keep
         hs = torch.empty((A, C, B, H), dtype=gi.dtype, device=gi.device)
         ws = torch.empty((A, C, B, 4 * H), dtype=gi.dtype, device=gi.device) if save else None
-        st = k8.stride()
-        rc = _native.lib().flock_gru_seq_fwd(_stream(gi.device), A, C, B, H, _p(gi), _p(W_hh), _p(b_hh), _p(k8),
-                                             st[0], st[1], st[2], _p(hs), _p(ws))
-        _native.check(rc, "flock_gru_seq_fwd", learn=True)
+        _ops().gru_seq_fwd(gi, W_hh, b_hh, k8, hs, ws)
         if save:
             ctx.save_for_backward(hs, ws, W_hh, k8)
         return hs
@@ -322,10 +319,7 @@ class _GRUSeqFn(torch.autograd.Function):
         dgi = torch.empty((A, C, B, 3 * H), dtype=hs.dtype, device=hs.device)
         dW = torch.empty_like(W_hh)
         db = torch.empty((A, 3 * H), dtype=hs.dtype, device=hs.device)
-        st = k8.stride()
-        rc = _native.lib().flock_gru_seq_bwd(_stream(hs.device), A, C, B, H, _p(dhs), _p(hs), _p(ws), _p(W_hh),
-                                             _p(k8), st[0], st[1], st[2], _p(dgi), _p(dW), _p(db))
-        _native.check(rc, "flock_gru_seq_bwd", learn=True)
+        _ops().gru_seq_bwd(dhs, hs, ws, W_hh, k8, dgi, dW, db)
         return dgi, dW, db, None, None
 
 
@@ -354,10 +348,7 @@ class _VdnFeatFn(torch.autograd.Function):
         gi = torch.empty((A, R, Wi.shape[1]), dtype=f32, device=dev)
         y1 = torch.empty((A, R, W1.shape[1]), dtype=f32, device=dev) if save else None
         y2 = torch.empty((A, R, W2.shape[1]), dtype=f32, device=dev) if save else None
-        sa, sc, sb, _ = x.stride()
-        rc = _native.lib().flock_vdn_feat_fwd(_stream(dev), A, R, B, n, _p(x), sa, sc, sb, _p(W1), _p(b1), _p(W2),
-                                              _p(b2), _p(Wi), _p(bi), _p(y1), _p(y2), _p(gi))
-        _native.check(rc, "flock_vdn_feat_fwd", learn=True)
+        _ops().vdn_feat_fwd(x, W1, b1, W2, b2, Wi, bi, y1, y2, gi)
         if save:
             ctx.save_for_backward(x, W2, Wi, y1, y2)
         return gi
@@ -394,6 +385,40 @@ def gru_cell_gi(gi, h, W_hh, b_hh):
     return _GRUCellFn.apply(gi, gh, h)
 
 
+class StepRing:
+    """The replay-ring targets of one env step that writes its transitions itself (flock::step_v2_store /
+    step_uw_discrete_store, include/flock_amd.h FlockRing): the ring field tensors [state, action, reward, new_state,
+    terminal] (+ the record's actor_state / actor_new_state copies) and meta = [start, skip, group, store_done,
+    action_ids, env_done]. ``ctypes()`` is the same ring as the C ABI's FlockRing (the launch-plan path)."""
+
+    def __init__(self, fields, actor_state, actor_new_state, group, store_done, action_ids, env_done):
+        self.fields, self.actor_state, self.actor_new_state = list(fields), actor_state, actor_new_state
+        self.meta = [0, 0, int(group), int(bool(store_done)), int(bool(action_ids)), int(bool(env_done))]
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        f = self.fields
+        self._c = _native.FlockRing(
+            state=ptr(f[0]), action=ptr(f[1]), reward=ptr(f[2]), new_state=ptr(f[3]), terminal=ptr(f[4]),
+            prev_obs=None, capacity=f[0].shape[0], start=0, skip=0, actor_state=ptr(actor_state),
+            actor_new_state=ptr(actor_new_state), group=int(group), store_done=self.meta[3],
+            action_ids=self.meta[4], env_done=self.meta[5])
+
+    def set_start(self, start, skip):
+        self.meta[0], self.meta[1] = int(start), int(skip)
+        self._c.start, self._c.skip = int(start), int(skip)
+
+    @property
+    def start(self):
+        return self.meta[0]
+
+    @property
+    def skip(self):
+        return self.meta[1]
+
+    def ctypes(self, prev_obs):
+        self._c.prev_obs = prev_obs.data_ptr()
+        return self._c
+
+
 class ReplayRing:
     """Device-resident ring buffer of named row tensors (``fields``: name -> row shape)."""
 
@@ -423,9 +448,8 @@ class ReplayRing:
             n = self.capacity
         if n == 0:
             return
-        fields = (_native.FlockRingField * len(rows))()
-        keep = []
-        for i, (name, val) in enumerate(rows.items()):
+        srcs, dsts, kinds = [], [], []
+        for name, val in rows.items():
             w = self._width(name)
             val = torch.as_tensor(val, device=self.device)
             kind = 0
@@ -443,12 +467,11 @@ class ReplayRing:
                     src, kind = src.contiguous(), 3
                 else:
                     src = src.float().contiguous()
-            keep.append(src)
-            fields[i] = _native.FlockRingField(src.data_ptr(), self.bufs[name].data_ptr(), w, kind)
+            srcs.append(src)
+            dsts.append(self.bufs[name])
+            kinds.append(kind)
         _require_cuda(self.bufs[next(iter(rows))])
-        rc = _native.lib().flock_ring_store(_stream(self.device), n, self.capacity, self.counter % self.capacity,
-                                            len(rows), fields)
-        _native.check(rc, "flock_ring_store", learn=True)
+        _ops().ring_store(srcs, dsts, kinds, self.counter % self.capacity)
         self.counter += n
 
     def step_slots(self, n, state, action, reward, new_state, terminal, actor_state=None, actor_new_state=None,
@@ -459,21 +482,19 @@ class ReplayRing:
         fields; group = agents per row (1, or N for one row per env); store_done: store done (else 1 - done);
         action_ids: the step's action ids stored as f32 (uw_discrete); env_done: one terminal flag per env row."""
         skip = max(0, n - self.capacity)
-        # one FlockRing object per field mapping, updated in place: the env step's launch plan keeps a pointer to it
+        # one StepRing per field mapping, updated in place (its ctypes FlockRing serves the launch-plan path, which
+        # keeps a pointer to it)
         key = (state, action, reward, new_state, terminal, actor_state, actor_new_state, group, bool(store_done),
                bool(action_ids), bool(env_done))
         rings = self.__dict__.setdefault("_rings", {})
         ring = rings.get(key)
         if ring is None:
             b = self.bufs
-            ptr = lambda name: None if name is None else b[name].data_ptr()  # noqa: E731
-            ring = rings[key] = _native.FlockRing(
-                state=ptr(state), action=ptr(action), reward=ptr(reward), new_state=ptr(new_state),
-                terminal=ptr(terminal), prev_obs=None, capacity=self.capacity, start=0, skip=0,
-                actor_state=ptr(actor_state), actor_new_state=ptr(actor_new_state), group=group,
-                store_done=int(bool(store_done)), action_ids=int(bool(action_ids)), env_done=int(bool(env_done)))
-        ring.start = (self.counter + skip) % self.capacity
-        ring.skip = skip
+            ring = rings[key] = StepRing([b[state], b[action], b[reward], b[new_state], b[terminal]],
+                                         None if actor_state is None else b[actor_state],
+                                         None if actor_new_state is None else b[actor_new_state], group,
+                                         store_done, action_ids, env_done)
+        ring.set_start((self.counter + skip) % self.capacity, skip)
         self.counter += n
         return ring
 
@@ -481,9 +502,7 @@ class ReplayRing:
         """Write rows at arbitrary positions idx (HIP row scatter)."""
         idx = idx.to(device=self.device, dtype=torch.int64).contiguous()
         src = rows.to(device=self.device, dtype=torch.float32).reshape(idx.numel(), -1).contiguous()
-        rc = _native.lib().flock_scatter_rows(_stream(self.device), idx.numel(), src.shape[1], _p(src), _p(idx),
-                                              _p(self.bufs[name]))
-        _native.check(rc, "flock_scatter_rows", learn=True)
+        _ops().scatter_rows(src, idx, self.bufs[name])
 
     def gather(self, name, idx, out=None):
         """rows idx (any shape of int64 indices) -> [*idx.shape, *row_shape]."""
@@ -491,9 +510,7 @@ class ReplayRing:
         w = self._width(name)
         if out is None:
             out = torch.empty((*idx.shape, *self.fields[name]), dtype=torch.float32, device=self.device)
-        rc = _native.lib().flock_gather_rows(_stream(self.device), idx.numel(), w, _p(self.bufs[name]), _p(idx),
-                                             _p(out))
-        _native.check(rc, "flock_gather_rows", learn=True)
+        _ops().gather_rows(self.bufs[name], idx, out)
         return out
 
 

@@ -15,6 +15,7 @@ import time
 import numpy as np
 import torch
 
+from ..vec_env import device_writes
 from .maddpg import MADDPGLearner
 from .shared_critic import SharedCriticLearner
 from .vdn import BatchedQNet, VDNLearner
@@ -131,17 +132,20 @@ class SuperAgent:
 
     def save(self):
         os.makedirs(self.save_dir, exist_ok=True)
-        for i in range(self.n_agents):
+        for i in range(self.n_agents):  # agent-sharded learners: each rank writes the networks it owns
             for net in ("actor", "critic"):
-                torch.save(self.learner.state_dict(net, i), self._ckpt(i, net))
-                torch.save(self.learner.state_dict(net, i, target=True), self._ckpt(i, "target_" + net))
+                for target in (False, True):
+                    if self.learner.owns(net, i, target):
+                        torch.save(self.learner.state_dict(net, i, target=target),
+                                   self._ckpt(i, ("target_" if target else "") + net))
         self.replay_buffer.save(f"{self.path_save}/save_agent_{time.strftime('%Y%m%d%H%M')}")
 
     def load(self):
         sds = {}
         for i in range(self.n_agents):
             for net in ("actor", "critic", "target_actor", "target_critic"):
-                sds[f"{net}{i}"] = torch.load(self._ckpt(i, net), weights_only=True)
+                if self.learner.owns(net.replace("target_", ""), i, net.startswith("target")):
+                    sds[f"{net}{i}"] = torch.load(self._ckpt(i, net), weights_only=True)
         self.learner.load_reference_state(sds)
 
     def load_replay_buffer(self):
@@ -308,10 +312,12 @@ class CriticNetwork:
         """Every agent's mu for one observation [N, in], computed once per observation: the reference driver calls
         choose_action agent after agent with the same tensor (train_flock.py:114-115), so agents 1..N-1 slice the
         batched result. The cache holds the observation tensor itself (its address cannot be reused while cached)
-        and keys on its storage, shape, strides and version counter (bumped by any in-place write); learn() and
-        load_models() drop it."""
+        and keys on its storage, shape, strides and version counter (bumped by any in-place write) and on the count of
+        VecFlockEnv steps / resets (kernel writes into an env's observation buffers bump no version counter);
+        learn() and load_models() drop it."""
         t = observation if torch.is_tensor(observation) else None
-        key = None if t is None else (t.data_ptr(), tuple(t.shape), t.stride(), t.dtype, t.device, t._version)
+        key = None if t is None else (t.data_ptr(), tuple(t.shape), t.stride(), t.dtype, t.device, t._version,
+                                      device_writes())
         c = self._act_cache
         if key is not None and c is not None and c[1] == key:
             return c[2]

@@ -32,8 +32,8 @@ import math
 import torch
 import torch.nn.functional as F
 
-from .. import _native, dist
-from .core import FlatParams, ReplayRing, _p, _stream, blinear, capture_graph, gru_cell, gru_seq, shared_linear
+from .. import dist
+from .core import FlatParams, ReplayRing, _ops, blinear, capture_graph, gru_cell, gru_seq, shared_linear
 
 HR = 32  # hidden_rnn (net.py:15,100)
 
@@ -403,15 +403,11 @@ class MADDPGLearner:
         idx = self.static_idx
         tidx = idx.t().contiguous()
         act = self.replay.gather("action", tidx)                                # [C, B, N, 2]
-        if self.reference_action_layout:  # actors_action [N,B,C,2].reshape(B,C,2N) (MADDPG.py:86), per rank
-            act = act.permute(2, 1, 0, 3).contiguous().reshape(B, C, 2 * N).transpose(0, 1)
-        else:
-            act = act.reshape(C, B, 2 * N)
         return {"S": self.replay.gather("state", tidx).reshape(C, B, N * k),
                 "S2": self.replay.gather("next_state", tidx).reshape(C, B, N * k),
                 "AS": self.replay.gather("actor_state", idx).permute(2, 1, 0, 3),   # [N, C, B, k]
                 "AS2": self.replay.gather("actor_next_state", idx).permute(2, 1, 0, 3),
-                "act": act.contiguous(),                                         # [C, B, 2N]
+                "act": act.contiguous(),                                         # [C, B, N, 2], raw
                 "R": self.replay.gather("reward", idx), "D": self.replay.gather("done", idx)}  # [B, C, N]
 
     # batch dimension of each field: the union batch is every rank's rows, rank after rank
@@ -428,6 +424,11 @@ class MADDPGLearner:
         U = {n: self._gather_cat(v, self._BATCH_DIM[n]) for n, v in self._local_batch().items()}
         C = self.C
         Bu = U["S"].shape[1]
+        # the action layout is applied to the UNION batch, as one process sampling all Bu rows would
+        if self.reference_action_layout:  # actors_action [N,Bu,C,2].reshape(Bu,C,2N) (MADDPG.py:86)
+            U["act"] = U["act"].permute(2, 1, 0, 3).contiguous().reshape(Bu, C, 2 * self.N).transpose(0, 1)
+        else:
+            U["act"] = U["act"].reshape(C, Bu, 2 * self.N)
         last = C - 1
         sl = lambda fp, buf: {n: fp.view(buf, n)[lo:hi] for n in fp.shapes}  # noqa: E731
         Pa, Pta = sl(self.actors, self.actors.data), sl(self.actors, self.actors.target)
@@ -459,8 +460,7 @@ class MADDPGLearner:
         self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
         for n in self.actors.shapes:  # the target actors of this rank's agents (mode 0, as _step)
             t, p_ = self.actors.view(self.actors.target, n)[lo:hi], self.actors.view(self.actors.data, n)[lo:hi]
-            _native.check(_native.lib().flock_soft_update(_stream(self.device), t.numel(), _p(t), _p(p_),
-                                                          float(self.tau), 0), "flock_soft_update", learn=True)
+            _ops().soft_update(t, p_, float(self.tau), 0)
         with torch.no_grad():
             sums = torch.stack([critic_loss.detach().sum(), actor_loss.detach().sum()])
             torch.distributed.all_reduce(sums, group=self.group)
@@ -505,9 +505,9 @@ class MADDPGLearner:
             i = int(key[len(key.rstrip("0123456789")):])
             fp = self.actors if net == "actor" else self.critics
             tgt = key.startswith("target")
-            if net == "critic" and self.shard:  # agent_shard: this rank's critics only
-                if not self.a0 <= i < self.a0 + self.na:
-                    continue
+            if not self.owns(net, i, tgt):  # agent_shard: another rank's critic or target actor
+                continue
+            if net == "critic" and self.shard:
                 i -= self.a0
             for n, v in sd.items():
                 if n in CRITIC_JOINED and net == "critic":
@@ -520,12 +520,21 @@ class MADDPGLearner:
                 else:
                     fp.load(n, v, agent=i, target=tgt)
 
+    def owns(self, net, i, target=False):
+        """Whether this rank holds agent i's network. agent_shard: the critics, critic targets and target actors of
+        agents [a0, a0 + na) only (the others' target actors are never soft-updated here); the frozen actors are
+        whole on every rank."""
+        if not self.shard or (net == "actor" and not target):
+            return True
+        return self.a0 <= i < self.a0 + self.na
+
     def state_dict(self, net, i, target=False):
-        """Reference state_dict of agent i's actor / critic (agent_shard: critics of this rank's agents only)."""
+        """Reference state_dict of agent i's actor / critic (agent_shard: only the networks this rank owns)."""
         fp = self.actors if net == "actor" else self.critics
+        if not self.owns(net, i, target):
+            what = ("target " if target else "") + net
+            raise KeyError(f"{what} {i} lives on another rank (this rank holds {self.a0}..{self.a0 + self.na - 1})")
         if net == "critic" and self.shard:
-            if not self.a0 <= i < self.a0 + self.na:
-                raise KeyError(f"critic {i} lives on another rank (this rank holds {self.a0}..{self.a0 + self.na - 1})")
             i -= self.a0
         out = {}
         for n in reference_names(fp):

@@ -29,7 +29,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import _native, dist
-from .core import FlatParams, ReplayRing, _p, _stream, blayer_norm, blinear, capture_graph
+from .core import FlatParams, ReplayRing, _ops, _p, blayer_norm, blinear, capture_graph
 
 
 def critic_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
@@ -166,6 +166,16 @@ class SharedCriticLearner:
                       workspace=_p(self.sc_workspace), counters=_p(self.sc_counters), alpha=self.alpha,
                       beta=self.beta, gamma=self.gamma, beta1=0.9, beta2=0.999, eps=1e-8, tau=self.tau,
                       update_rate=self.update_rate)
+        # the same update as torch.ops.flock.sc_round arguments (csrc/flock_torch_learn.cpp): the learner state, one
+        # job per phase ([idx, agent, 5 replay-row fields, workspace, critic_view(, actor_grad_out)]), sizes, rates
+        rows = lambda d: [d["state"], d["new_state"], d["action"], d["reward"], d["terminal"]]  # noqa: E731
+        self._sc_learner = [C.data, C.grad, C.exp_avg, C.exp_avg_sq, C.step_dev, A.data, A.grad, A.exp_avg,
+                            A.exp_avg_sq, A.target, self.actor_steps, self.losses, self.sc_counters]
+        self._sc_dims = [B, n_in, na, self.fc1, self.fc2, self.update_rate, 1]
+        self._sc_dims_grads = [B, n_in, na, self.fc1, self.fc2, 0, 0]
+        self._sc_hyper = [self.alpha, self.beta, self.gamma, 0.9, 0.999, 1e-8, self.tau]
+        self._sc_job = [self.static_idx, self.static_agent, *rows(rb), self.sc_workspace, self.critic_views[0]]
+        self._ring_rows = rows(rb)
         # single GPU: the soft updates run inside the gradient kernels (device-side count condition)
         self._sc = _native.FlockScUpdate(**fields, critic_view=_p(self.critic_views[0]))
         self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0, update_rate=0))  # data-parallel
@@ -188,23 +198,28 @@ class SharedCriticLearner:
                 f = dict(fields, idx=_p(self.identity_idx), agent=_p(agent_t), workspace=_p(self.sc_workspaces[i]),
                          **{"ring_" + n: _p(stg[n]) for n in names})
                 self._slots.append(dict(staging=stg, agent=agent_t, graph=None, graph_c=None, graph_a=None,
+                                        job=[self.identity_idx, agent_t, *rows(stg), self.sc_workspaces[i],
+                                             self.critic_views[i]],
                                         rows=_native.FlockScRows(**{n: _p(stg[n]) for n in names}),
                                         sc=_native.FlockScUpdate(**f, critic_view=_p(self.critic_views[i])),
                                         sc_grads=_native.FlockScUpdate(**dict(f, do_adam=0, update_rate=0))))
                 if self.distributed:
                     bucket = dict(f, critic_grad=_p(self.dp_bucket), critic_view=_p(self.critic_views[i]),
                                   actor_grad_out=_p(self.dp_bucket[self.dp_actor_off:]))
-                    self._slots[-1]["dp_grads"] = _native.FlockScUpdate(**dict(bucket, do_adam=0))
-                    self._slots[-1]["dp_adam"] = _native.FlockScUpdate(**bucket)
+                    self._slots[-1]["dp_job"] = self._slots[-1]["job"] + [self.dp_bucket[self.dp_actor_off:]]
+            if self.distributed:  # the learner state with the critic gradient in the bucket
+                self._sc_learner_dp = list(self._sc_learner)
+                self._sc_learner_dp[1] = self.dp_bucket[:C.numel]
             self._dp_pending = None
             self.staging = self._slots[0]["staging"]
 
-    def _fused_update(self, u=None):
-        lib = _native.lib()
-        u = ctypes.byref(self._sc if u is None else u)
-        st = _stream(self.device)
-        _native.check(lib.flock_sc_critic_update(st, u), "flock_sc_critic_update", learn=True)
-        _native.check(lib.flock_sc_actor_update(st, u), "flock_sc_actor_update", learn=True)
+    def _fused_update(self, job=None, dims=None):
+        """One learn() as two torch.ops.flock.sc_round launches sets: its critic phase, then its actor phase."""
+        T = _ops()
+        job = self._sc_job if job is None else job
+        dims = self._sc_dims if dims is None else dims
+        T.sc_round(self._sc_learner, job, [], dims, self._sc_hyper)
+        T.sc_round(self._sc_learner, [], job, dims, self._sc_hyper)
 
     def _fused_state(self):
         """Everything one fused update writes (graph-capture warm-ups are undone on these): the actor targets too,
@@ -215,13 +230,13 @@ class SharedCriticLearner:
 
     def _run_fused(self, agent, slot=None):
         S = self._slots[slot] if slot is not None else None
+        job = S["job"] if S is not None else self._sc_job
         if not self.distributed:
-            u = S["sc"] if S is not None else self._sc
             if not self.use_graph:
-                return self._fused_update(u)
+                return self._fused_update(job)
             g = S["graph"] if S is not None else self.graph
             if g is None:
-                g = capture_graph(lambda: self._fused_update(u), self.device, self._fused_state())
+                g = capture_graph(lambda: self._fused_update(job), self.device, self._fused_state())
                 if S is not None:
                     S["graph"] = g
                 else:
@@ -229,24 +244,19 @@ class SharedCriticLearner:
             return g.replay()
         # data-parallel: gradient-only kernels, RCCL all-reduce (sum) of each network's gradient, then the Adam
         # steps with grad_scale = 1 / world; the actor's target soft update (:180-185) rides in its Adam launch
-        lib = _native.lib()
-        st = _stream(self.device)
-        u = ctypes.byref(S["sc_grads"] if S is not None else self._sc_grads)
-        _native.check(lib.flock_sc_critic_update(st, u), "flock_sc_critic_update", learn=True)
+        T = _ops()
+        T.sc_round(self._sc_learner, job, [], self._sc_dims_grads, self._sc_hyper)
         dist.allreduce_sum_(self.critic.grad, self.group)
         self.critic.adam_step_dev(self.beta, grad_scale=self.inv_world)
-        _native.check(lib.flock_sc_actor_update(st, u), "flock_sc_actor_update", learn=True)
+        T.sc_round(self._sc_learner, [], job, self._sc_dims_grads, self._sc_hyper)
         A = self.actors
         lo, hi = A.agent_range(agent)
         dist.allreduce_sum_(A.grad[lo:hi], self.group)
         self.actor_steps[agent:agent + 1].add_(1)
         soft = self.count[agent] % self.update_rate == 0
-        rc = lib.flock_adam_step_dev(st, hi - lo, _p(A.data[lo:hi]), _p(A.grad[lo:hi]), _p(A.exp_avg[lo:hi]),
-                                     _p(A.exp_avg_sq[lo:hi]), _p(self.inv_world), float(self.alpha), 0.9, 0.999,
-                                     1e-8, _p(self.actor_steps[agent:agent + 1]),
-                                     _p(A.target[lo:hi]) if soft else None, float(self.tau) if soft else 0.0,
-                                     1 if soft else 0)
-        _native.check(rc, "flock_adam_step_dev", learn=True)
+        T.adam_step(A.data[lo:hi], A.grad[lo:hi], A.exp_avg[lo:hi], A.exp_avg_sq[lo:hi],
+                    self.actor_steps[agent:agent + 1], self.inv_world, A.target[lo:hi] if soft else None,
+                    float(self.alpha), 0.9, 0.999, 1e-8, float(self.tau) if soft else 0.0, 1 if soft else 0)
 
     # ------------------------------------------------------------------ acting
     def _stacked(self, fp, target=False):
@@ -390,10 +400,8 @@ class SharedCriticLearner:
                     self.snapshot_into(0, agent)
                 return self.update_slot(0, agent)
             else:
-                rc = _native.lib().flock_sc_prep(_stream(self.device), B, len(self.replay), self.seed,
-                                                 self._learn_calls, None if idx is not None else _p(self.static_idx),
-                                                 _p(self.static_agent), int(agent))
-                _native.check(rc, "flock_sc_prep", learn=True)
+                _ops().sc_prep(self.static_agent, None if idx is not None else self.static_idx, len(self.replay),
+                               self.seed, self._learn_calls, int(agent))
             self._run_fused(agent)
             return self._finish_learn(agent, soft_in_kernel=not self.distributed, actor_soft_done=self.distributed)
         if idx is None:                                                       # utils.py:65-76 (with replacement)
@@ -425,24 +433,24 @@ class SharedCriticLearner:
             return False
         self._learn_calls += 1
         S = self._slots[slot]
-        rc = _native.lib().flock_sc_prep_snapshot(
-            _stream(self.device), B, len(self.replay), self.seed, self._learn_calls, _p(self.static_idx),
-            _p(S["agent"]), int(agent), self.input_dim, self.n_actions, ctypes.byref(self._rows_ring),
-            ctypes.byref(S["rows"]))
-        _native.check(rc, "flock_sc_prep_snapshot", learn=True)
+        stg = S["staging"]
+        _ops().sc_prep_snapshot(self._ring_rows, [stg["state"], stg["new_state"], stg["action"], stg["reward"],
+                                                  stg["terminal"]], S["agent"], self.static_idx, len(self.replay),
+                                self.seed, self._learn_calls, int(agent))
         return True
 
     def _phase(self, slot, phase):
         """Enqueue the critic ("c": flock_sc_critic_update) or actor ("a": flock_sc_actor_update) phase of the
         update on staging slot ``slot`` on the current stream (one HIP graph replay per phase)."""
         S = self._slots[slot]
-        lib = _native.lib()
-        fn, name = ((lib.flock_sc_critic_update, "flock_sc_critic_update") if phase == "c"
-                    else (lib.flock_sc_actor_update, "flock_sc_actor_update"))
-        u = ctypes.byref(S["sc"])
+        T = _ops()
+        job = S["job"]
 
         def run():
-            _native.check(fn(_stream(self.device), u), name, learn=True)
+            if phase == "c":
+                T.sc_round(self._sc_learner, job, [], self._sc_dims, self._sc_hyper)
+            else:
+                T.sc_round(self._sc_learner, [], job, self._sc_dims, self._sc_hyper)
 
         if not self.use_graph:
             return run()
@@ -521,17 +529,15 @@ class SharedCriticLearner:
         """One data-parallel round on the current stream: critic phase of slot c and / or actor phase of slot a
         (None: absent) as gradients (flock_sc_round, do_adam = 0), ONE all-reduce (sum) of the bucket part they
         wrote, then flock_sc_round_adam with grad_scale = 1 / world."""
-        lib = _native.lib()
-        st = _stream(self.device)
+        T = _ops()
         S = self._slots
-        byref = lambda i, k: ctypes.byref(S[i][k]) if i is not None else None  # noqa: E731
-        _native.check(lib.flock_sc_round(st, byref(c, "dp_grads"), byref(a, "dp_grads")), "flock_sc_round",
-                      learn=True)
+        job = lambda i: S[i]["dp_job"] if i is not None else []  # noqa: E731
+        L = self._sc_learner_dp
+        T.sc_round(L, job(c), job(a), self._sc_dims_grads, self._sc_hyper)
         lo = 0 if c is not None else self.dp_actor_off
         hi = self.dp_bucket.numel() if a is not None else self.critic.numel
         dist.allreduce_sum_(self.dp_bucket[lo:hi], self.group)
-        _native.check(lib.flock_sc_round_adam(st, byref(c, "dp_adam"), byref(a, "dp_adam"), _p(self.inv_world)),
-                      "flock_sc_round_adam", learn=True)
+        T.sc_round_adam(L, job(c), job(a), self._sc_dims, self._sc_hyper, self.inv_world)
 
     def dp_learn(self, slot, agent, slot_free):
         """learn() of ``agent`` on the rows snapshot_into(slot, agent) copied, data-parallel, enqueued on the current
@@ -626,6 +632,65 @@ class SharedCriticBench:
             self._prev_agent = None
         self.prev_obs = env.dnn.clone()
         self.prev_act = None
+        self._loop = None
+        self._looped = False
+
+    # ---------------------------------------------------------------- K steps per call (torch.classes.flock)
+    def loop(self):
+        """torch.classes.flock.ScTrainLoop over this bench's env, replay ring and learner (csrc/flock_torch_loop.cpp):
+        K steps of [env step with the fused replay insert, learn()] enqueued by one C++ call, bitwise the per-step
+        path of before() / env.step(ring=...) / after(). Single GPU, overlapped native pipeline only."""
+        if self._loop is None:
+            env, L = self.env, self.learner
+            if not (self.overlap and self.pipelined and L.use_graph) or env.cfg.variant != "v2":
+                raise RuntimeError("ScTrainLoop is the single-GPU overlapped config-3 loop (v2, native pipeline)")
+            if self._handles is not None:
+                raise RuntimeError("ScTrainLoop must own the learn() pipeline from the first learn on")
+            from .. import torch_ops
+
+            torch_ops.load()
+            c = env.cfg
+            b0, b1 = env._bufs
+            none = torch.empty(0, device=env.device)
+            opt = lambda t: none if t is None else t  # noqa: E731
+            e = [env.positions, env.headings, env.velocities, b0["dnn"], b1["dnn"], opt(b0["idx"]), opt(b1["idx"]),
+                 env.reward, env.done, env.any_done, opt(env.seeds)]
+            ef = [env.box, c.sensor_range, c.collision_distance, c.dt, c.v_min, c.max_linear_velocity]
+            ei = [env.k, int(bool(c.periodic)), int(bool(c.rigid_boundary)), int(c.step_launches), env._cur]
+            rb = L.replay.bufs
+            ring = [rb["state"], rb["action"], rb["reward"], rb["new_state"], rb["terminal"]]
+            slots = [t for S in L._slots for t in S["job"]]
+            self._loop = torch.classes.flock.ScTrainLoop(e, ef, ei, ring, L.replay.counter, L._sc_learner, slots,
+                                                         L._sc_dims, L._sc_hyper, L.seed, L._learn_calls)
+        return self._loop
+
+    def can_loop(self):
+        return (self.overlap and self.pipelined and self.learner.use_graph and not self.learner.distributed
+                and self.env.cfg.variant == "v2" and self._handles is None)
+
+    def run_steps(self, first, K, actions, events=(), ev_every=1):
+        """Steps first .. first + K - 1 (actions[s % len(actions)] at step s) through the loop, then the Python
+        mirrors (env parity and step count, ring counter, learn counters) brought up to date."""
+        lp = self.loop()
+        env, L = self.env, self.learner
+        handles = []
+        for ev in events:
+            if not int(ev.cuda_event):  # torch creates the HIP event at its first record
+                ev.record()
+            handles.append(int(ev.cuda_event))
+        lp.run(int(first), int(K), list(actions), torch.cuda.current_stream(env.device).cuda_stream,
+               self.stream.cuda_stream, handles, int(ev_every))
+        parity, counter, calls = lp.state()
+        learns = calls - L._learn_calls
+        for s in range(first + K - learns, first + K):
+            L.count[s % L.n_agents] += 1
+        L._learn_calls, L.replay.counter = calls, counter
+        env._cur = parity
+        env.steps += K
+        from .. import vec_env
+
+        vec_env._DEVICE_WRITES[0] += K
+        self._looped = True
 
     def describe(self):
         return (f"maddpg_shared_critic learn() x1 per vectorized step ("
@@ -699,6 +764,8 @@ class SharedCriticBench:
         """Enqueue the pending actor phase (native pipeline) and join the learner stream(s) into the current one
         (end of a timed region)."""
         if self.overlap:
+            if self._looped:
+                self._loop.flush(self.stream.cuda_stream)
             if self._handles is not None:
                 self.learner.pipeline_flush(self._handles[1])
             if self.learner.distributed:

@@ -17,6 +17,21 @@ from . import ops
 
 VARIANTS = ("v2", "uw", "uw_discrete", "flock")
 
+# kernel writes into the env buffers do not bump the tensors' version counters: callers that cache results keyed on
+# an observation tensor (dropin.CriticNetwork.actions) also key on this count of steps and resets of every env
+_DEVICE_WRITES = [0]
+
+
+def device_writes():
+    return _DEVICE_WRITES[0]
+
+
+def _seed64(x):
+    """A uint64 seed / counter as the int64 with the same bits (the op schemas take int64; the C++ side casts back),
+    so launch="torch" and the ctypes plan path draw the same Philox stream for seeds >= 2**63."""
+    x = int(x) & (2**64 - 1)
+    return x - 2**64 if x >= 2**63 else x
+
 
 @dataclass
 class FlockConfig:
@@ -70,7 +85,7 @@ class VecFlockEnv:
     the PyTorch dispatcher, traceable by FakeTensor / torch.compile, and the cheaper host path (7.8-8.1 us per step
     against 10-11 us at configs 2 / 3, tools/host_cost_ops.py); "plan" launches through the C ABI with a recorded
     launch plan (ops.StepPlan: one ctypes call per step). Both run the same kernels with bitwise-equal results. A step
-    with a fused replay insert (ring=...) takes the C ABI path (the ring is a struct of device pointers)."""
+    with a fused replay insert (ring=...) goes through flock::step_v2_store / step_uw_discrete_store."""
 
     def __init__(self, config: FlockConfig = None, device="cuda", launch="torch", **kw):
         cfg = (config or FlockConfig(**kw)).resolved()
@@ -172,7 +187,7 @@ class VecFlockEnv:
                                   b["mem"], self.valid, env_mask, ops.VARIANT_IDS[c.variant], self.k,
                                   float(c.range_start[0]), float(c.range_start[1]), self.box, c.sensor_range,
                                   c.reset_check_distance, c.rigid_boundary, c.max_reset_attempts,
-                                  c.seed & (2**63 - 1), self._rng_offset, c.reset_repair_rounds)
+                                  _seed64(c.seed), _seed64(self._rng_offset), c.reset_repair_rounds)
         else:
             ops.reset(c.variant, self.positions, b["dnn"], k=self.k, range_start=c.range_start, box=self.box,
                       sensor_range=c.sensor_range, check_distance=c.reset_check_distance, heading=heading,
@@ -181,6 +196,7 @@ class VecFlockEnv:
                       max_attempts=c.max_reset_attempts, seed=c.seed, rng_offset=self._rng_offset,
                       repair_rounds=c.reset_repair_rounds, normalize=c.normalize_distance)
         self._rng_offset += max(c.max_reset_attempts, c.reset_repair_rounds)
+        _DEVICE_WRITES[0] += 1
         if self.seeds is not None and b["idx"] is not None:  # the reset's neighbours seed the first step
             self.seeds.copy_(b["idx"])
         if _keep_done:
@@ -203,37 +219,89 @@ class VecFlockEnv:
             self._bufs[self._cur]["mem"].copy_(torch.as_tensor(obs_memory).to(self.device))
 
     # ------------------------------------------------------------------ step
-    def _step_torch(self, T, a, noise, dt, src, dst):
-        """The step through torch.ops.flock (VecFlockEnv(launch="torch"))."""
+    def _step_torch(self, T, a, noise, dt, src, dst, ring=None):
+        """The step through torch.ops.flock (VecFlockEnv(launch="torch")); with a ring (a learner's StepRing), the
+        fused replay insert ops step_v2_store / step_uw_discrete_store."""
         c = self.cfg
         common = (self.k, self.box)
+        L = c.step_launches
         if c.variant == "v2":
-            T.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
-                      self.done, self.any_done, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
-                      c.v_min, c.max_linear_velocity, c.periodic, c.rigid_boundary)
+            if ring is None:
+                T.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
+                          self.done, self.any_done, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
+                          c.v_min, c.max_linear_velocity, c.periodic, c.rigid_boundary, L)
+            else:
+                T.step_v2_store(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"],
+                                self.reward, self.done, self.any_done, self.seeds, ring.fields, ring.actor_state,
+                                ring.actor_new_state, src["dnn"], ring.meta, *common, c.sensor_range,
+                                c.collision_distance, dt, c.v_min, c.max_linear_velocity, c.periodic,
+                                c.rigid_boundary, L)
         elif c.variant == "uw":
             T.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
                       dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, self.seeds, *common,
-                      c.sensor_range, c.collision_distance, dt, c.rigid_boundary)
+                      c.sensor_range, c.collision_distance, dt, c.rigid_boundary, L)
         elif c.variant == "uw_discrete":
             if noise is not None:
                 noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(
                     self.E, self.N, 2).contiguous()
-            T.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
-                               self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
-                               self.status, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
-                               c.max_linear_velocity, c.rigid_boundary, 0.1, c.seed & (2**63 - 1),
-                               self._rng_offset & (2**63 - 1))
+            if ring is None:
+                T.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
+                                   self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
+                                   self.status, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
+                                   c.max_linear_velocity, c.rigid_boundary, 0.1, _seed64(c.seed),
+                                   _seed64(self._rng_offset), L)
+            else:
+                T.step_uw_discrete_store(self.positions, self.headings, self.prev_headings, a, noise, self.table,
+                                         self.velocities, dst["dnn"], dst["idx"], self.reward, self.done,
+                                         self.any_done, self.status, self.seeds, ring.fields, src["dnn"], ring.meta,
+                                         *common, c.sensor_range, c.collision_distance, dt, c.max_linear_velocity,
+                                         c.rigid_boundary, 0.1, _seed64(c.seed), _seed64(self._rng_offset), L)
             self._rng_offset += 1
         else:
             T.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
                          self.reward, self.done, self.any_done, self.seeds, *common, c.collision_distance, dt,
-                         c.rigid_boundary)
+                         c.rigid_boundary, L)
+
+    def _step_plan(self, a, noise, dt, src, dst, nxt, ring):
+        """The step through the C ABI (ops.*): a launch plan per buffer parity (fixed buffers, so later steps skip
+        the tensor checks)."""
+        c = self.cfg
+        E, N, k = self.E, self.N, self.k
+        plans = self.__dict__.setdefault("_plans", {})
+        pkey = nxt if ring is None else (nxt, id(ring))  # ring steps: one plan per (parity, ring object)
+        plan = plans.get(pkey)
+        if plan is None:
+            plan = plans[pkey] = ops.StepPlan()
+        common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
+                      rigid_boundary=c.rigid_boundary, plan=plan, normalize=c.normalize_distance)
+        cring = ring.ctypes(src["dnn"]) if ring is not None else None
+        if c.variant == "v2":
+            ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
+                        self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
+                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=cring, seeds=self.seeds,
+                        launches=c.step_launches, **common)
+        elif c.variant == "uw":
+            ops.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
+                        dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, sensor_range=c.sensor_range,
+                        seeds=self.seeds, launches=c.step_launches, **common)
+        elif c.variant == "uw_discrete":
+            if noise is not None:
+                noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
+            ops.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
+                                 self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
+                                 self.status, sensor_range=c.sensor_range, v_max=c.max_linear_velocity,
+                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, ring=cring,
+                                 launches=c.step_launches, **common)
+            self._rng_offset += 1
+        else:
+            ops.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
+                           self.reward, self.done, self.any_done, seeds=self.seeds, launches=c.step_launches,
+                           **common)
 
     def step(self, action, noise=None, dt=None, copy=False, ring=None, auto_reset=False):
         """One vectorized step. action: [E,N,2] f32 (v2: [lin, ang]; uw/flock: velocity/acceleration) or
         [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info).
-        ring (v2): a _native.FlockRing from a learner's replay_slots(); the step also stores every transition
+        ring (v2, uw_discrete): a StepRing from a learner's replay_slots(); the step also stores every transition
         (previous obs, action, reward, new obs, 1 - done) into that replay ring in the same launch.
         auto_reset: every env whose step ended in a collision (any_done) is reset right behind the step, keyed on
         the device flag (no host sync) — what main.py:24-31 / train_flock.py do with env.reset() after done[1].
@@ -252,45 +320,18 @@ class VecFlockEnv:
             a = a.reshape(E, N).contiguous()
         else:
             a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
-        # launch plan of this buffer parity (ops.StepPlan): fixed buffers, so later steps skip the tensor checks
-        plans = self.__dict__.setdefault("_plans", {})
-        pkey = nxt if ring is None else (nxt, id(ring))  # ring steps: one plan per (parity, ring object)
-        plan = plans.get(pkey)
-        if plan is None:
-            plan = plans[pkey] = ops.StepPlan()
-        common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
-                      rigid_boundary=c.rigid_boundary, plan=plan, normalize=c.normalize_distance)
-        if ring is not None:
-            if c.variant not in ("v2", "uw_discrete"):
-                raise NotImplementedError("the fused replay insert is built for the v2 and uw_discrete steps")
-            ring.prev_obs = src["dnn"].data_ptr()
-        T = self._torch_ops if ring is None and c.step_launches <= 1 and not c.normalize_distance else None
+        if ring is not None and c.variant not in ("v2", "uw_discrete"):
+            raise NotImplementedError("the fused replay insert is built for the v2 and uw_discrete steps")
+        # the custom ops (default); launch="plan" and normalize_distance steps take the validated C-ABI launch plans
+        # (ops.StepPlan; FlockStepExt carries the normalize_distance flag)
+        T = self._torch_ops if not c.normalize_distance else None
         if T is not None:
-            self._step_torch(T, a, noise, dt, src, dst)
-        elif c.variant == "v2":
-            ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
-                        self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,
-                        v_max=c.max_linear_velocity, periodic=c.periodic, ring=ring, seeds=self.seeds,
-                        launches=c.step_launches, **common)
-        elif c.variant == "uw":
-            ops.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
-                        dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, sensor_range=c.sensor_range,
-                        seeds=self.seeds, launches=c.step_launches, **common)
-        elif c.variant == "uw_discrete":
-            if noise is not None:
-                noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
-            ops.step_uw_discrete(self.positions, self.headings, self.prev_headings, a, noise, self.table,
-                                 self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
-                                 self.status, sensor_range=c.sensor_range, v_max=c.max_linear_velocity,
-                                 seed=c.seed, rng_offset=self._rng_offset, seeds=self.seeds, ring=ring,
-                                 launches=c.step_launches, **common)
-            self._rng_offset += 1
+            self._step_torch(T, a, noise, dt, src, dst, ring)
         else:
-            ops.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
-                           self.reward, self.done, self.any_done, seeds=self.seeds, launches=c.step_launches,
-                           **common)
+            self._step_plan(a, noise, dt, src, dst, nxt, ring)
         self._cur = nxt
         self.steps += 1
+        _DEVICE_WRITES[0] += 1
         info = {}
         if auto_reset:
             final = self.__dict__.get("_final")

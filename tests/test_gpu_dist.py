@@ -180,12 +180,12 @@ def test_two_ranks_overlapped_bench_loop_equals_serial(cuda):
 NS = 4  # agents of the sharded test (divisible by the world size)
 
 
-def _shard_make(batch, group=None, shard=False):
+def _shard_make(batch, group=None, shard=False, layout=False):
     from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
 
     return MADDPGLearner(NS, K, recurrent=True, hidden1=32, hidden2=24, batch_size=batch, chunk_size=C,
                          buffer_capacity=128, min_size_buffer=batch, device="cuda:0", seed=0, dist_group=group,
-                         reference_action_layout=False, agent_shard=shard)
+                         reference_action_layout=layout, agent_shard=shard)
 
 
 def _shard_fill(L):
@@ -202,17 +202,25 @@ def _layers(fp, buf, lo, hi):
     return np.concatenate([fp.view(buf, n)[lo:hi].detach().cpu().numpy().ravel() for n in fp.shapes])
 
 
-def _shard_worker(rank, port, q):
+def _shard_worker(rank, port, q, layout):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", RANK=str(rank))
     try:
         torch.distributed.init_process_group("gloo")
-        L = _shard_make(B, torch.distributed.group.WORLD, shard=True)
+        L = _shard_make(B, torch.distributed.group.WORLD, shard=True, layout=layout)
         assert L.shard and L.na == NS // 2 and L.a0 == rank * (NS // 2)
         _shard_fill(L)
         st = np.random.default_rng(5).choice(T - C, 2 * B, replace=False)
         for s2 in (st, st[::-1].copy()):
             L.train(starts=s2[rank * B:(rank + 1) * B])
         A = L.actors
+        other = (L.a0 + L.na) % NS  # an agent of the other rank: its critic and target actor live there
+        for net, tgt in (("critic", False), ("critic", True), ("actor", True)):
+            try:
+                L.state_dict(net, other, target=tgt)
+                raise AssertionError(f"{net} target={tgt} of agent {other} exported by rank {rank}")
+            except KeyError:
+                pass
+        L.state_dict("actor", other)  # the frozen actors are whole on every rank
         q.put((rank, _layers(L.critics, L.critics.data, 0, L.na), _layers(L.critics, L.critics.target, 0, L.na),
                _layers(A, A.target, L.a0, L.a0 + L.na), _layers(A, A.data, 0, NS), L.losses.cpu().numpy(),
                L.state_dict("critic", L.a0)["fc2.weight"].numpy()))
@@ -224,17 +232,21 @@ def _shard_worker(rank, port, q):
         q.put((rank, "error", traceback.format_exc() + repr(e)))
 
 
-def test_agent_sharded_critics_equal_union_batch(cuda):
+@pytest.mark.parametrize("layout", [False, True], ids=["plain_actions", "reference_action_layout"])
+def test_agent_sharded_critics_equal_union_batch(layout, cuda):
     """MADDPGLearner(agent_shard=True) on 2 ranks: each rank owns the critics and target actors of half the agents,
     all-gathers both ranks' minibatches and the actor heads' actions, and updates only its agents. After two train()
     calls each rank's critics, critic targets and target actors equal that slice of ONE process training every
-    agent on the union batch (same tolerance as the data-parallel test); the frozen actors stay bitwise whole."""
+    agent on the union batch (same tolerance as the data-parallel test); the frozen actors stay bitwise whole. With
+    the reference's action layout (MADDPG.py:86's raw reshape, bench.py's config-5 default) the layout is applied to
+    the union batch, as the single process applies it to its batch. Another rank's critics and target actors are
+    not exported (KeyError)."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_shard_worker, args=(r, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_shard_worker, args=(r, port, q, layout)) for r in range(2)]
     for p in ps:
         p.start()
     out = sorted([q.get(timeout=300) for _ in range(2)], key=lambda o: o[0])
@@ -242,7 +254,7 @@ def test_agent_sharded_critics_equal_union_batch(cuda):
         p.join(timeout=60)
     for o in out:
         assert not isinstance(o[1], str), o
-    ref = _shard_make(2 * B)
+    ref = _shard_make(2 * B, layout=layout)
     _shard_fill(ref)
     st = np.random.default_rng(5).choice(T - C, 2 * B, replace=False)
     for s2 in (st, st[::-1].copy()):

@@ -1,0 +1,321 @@
+"""The learner kernels as torch.ops.flock custom ops (csrc/flock_torch_learn.cpp) on the GPU: torch.library.opcheck of
+every op (schema / mutation annotations, FakeTensor through the Meta kernels, AOT dispatch), each op bitwise equal to
+its C-ABI entry point called through ctypes on the same inputs, and the fused replay-insert steps (step_v2_store,
+step_uw_discrete_store) bitwise equal to the C-ABI launch-plan path, ring contents included."""
+import ctypes
+
+import pytest
+import torch
+
+from marl_range_flocking_amd import FlockConfig, VecFlockEnv, _native
+
+pytestmark = pytest.mark.gpu
+TESTS = ("test_schema", "test_faketensor", "test_aot_dispatch_dynamic")
+
+
+@pytest.fixture(scope="module")
+def flock():
+    from marl_range_flocking_amd import torch_ops
+
+    return torch_ops.load()
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _st(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _check(rc, name):
+    _native.check(rc, name, learn=True)
+
+
+def _clone(*ts):
+    return [t.clone() for t in ts]
+
+
+def test_adam_soft_update_grad_norm(flock, cuda):
+    g = torch.Generator(device=cuda).manual_seed(0)
+    n = 10_001
+    p, gr, m, v, tgt = (torch.randn(n, device=cuda, generator=g) for _ in range(5))
+    v = v.abs()
+    step = torch.full((1,), 3, dtype=torch.int64, device=cuda)
+    scale = torch.full((1,), 0.5, device=cuda)
+    args = (p, gr, m, v, step, scale, tgt, 3e-4, 0.9, 0.999, 1e-8, 0.01, 1)
+    torch.library.opcheck(flock.adam_step.default, _clone(*args[:7]) + list(args[7:]), test_utils=TESTS)
+    a = _clone(p, gr, m, v, tgt)
+    b = _clone(p, gr, m, v, tgt)
+    flock.adam_step(a[0], a[1], a[2], a[3], step, scale, a[4], 3e-4, 0.9, 0.999, 1e-8, 0.01, 1)
+    _check(_native.lib().flock_adam_step_dev(_st(cuda), n, _p(b[0]), _p(b[1]), _p(b[2]), _p(b[3]), _p(scale), 3e-4,
+                                             0.9, 0.999, 1e-8, _p(step), _p(b[4]), 0.01, 1), "flock_adam_step_dev")
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    # soft update, both modes
+    for mode in (0, 1):
+        torch.library.opcheck(flock.soft_update.default, (tgt.clone(), p, 0.01, mode), test_utils=TESTS)
+        a, b = tgt.clone(), tgt.clone()
+        flock.soft_update(a, p, 0.01, mode)
+        _check(_native.lib().flock_soft_update(_st(cuda), n, _p(b), _p(p), 0.01, mode), "flock_soft_update")
+        assert torch.equal(a, b)
+    # clip_grad_norm_ coefficient
+    part = torch.zeros(2048, dtype=torch.float64, device=cuda)
+    out_a, out_b = torch.zeros(2, device=cuda), torch.zeros(2, device=cuda)
+    torch.library.opcheck(flock.grad_norm.default, (gr, part.clone(), out_a.clone(), 5.0), test_utils=TESTS)
+    flock.grad_norm(gr, part, out_a, 5.0)
+    _check(_native.lib().flock_grad_norm(_st(cuda), n, _p(gr), _p(part), 2048, 5.0, _p(out_b)), "flock_grad_norm")
+    assert torch.equal(out_a, out_b)
+    torch.testing.assert_close(out_a[0].double(), torch.linalg.vector_norm(gr.double()), rtol=1e-5, atol=0)
+
+
+def test_gru_cell_and_sequence(flock, cuda):
+    g = torch.Generator(device=cuda).manual_seed(1)
+    A, C, B, H = 3, 10, 17, 32
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g)  # noqa: E731
+    gi, gh, h = rnd(A, B, 3 * H), rnd(A, B, 3 * H), rnd(A, B, H)
+    hout, ws = torch.zeros(A, B, H, device=cuda), torch.zeros(A, B, 4 * H, device=cuda)
+    torch.library.opcheck(flock.gru_cell_fwd.default, (gi, gh, h, hout.clone(), ws.clone()), test_utils=TESTS)
+    flock.gru_cell_fwd(gi, gh, h, hout, ws)
+    h2, ws2 = torch.zeros_like(hout), torch.zeros_like(ws)
+    rows = A * B
+    _check(_native.lib().flock_gru_fwd(_st(cuda), rows, H, _p(gi), _p(gh), _p(h), _p(h2), _p(ws2)), "flock_gru_fwd")
+    assert torch.equal(hout, h2) and torch.equal(ws, ws2)
+    dh_out = rnd(A, B, H)
+    outs = [torch.zeros(A, B, 3 * H, device=cuda), torch.zeros(A, B, 3 * H, device=cuda),
+            torch.zeros(A, B, H, device=cuda)]
+    torch.library.opcheck(flock.gru_cell_bwd.default, (dh_out, h, ws, *_clone(*outs)), test_utils=TESTS)
+    flock.gru_cell_bwd(dh_out, h, ws, *outs)
+    ref = _clone(*outs)
+    _check(_native.lib().flock_gru_bwd(_st(cuda), rows, H, _p(dh_out), _p(h), _p(ws), *map(_p, ref)),
+           "flock_gru_bwd")
+    for x, y in zip(outs, ref):
+        assert torch.equal(x, y)
+    # a chunk of steps; keep is an expanded [C, A, B] view (per batch row done flags, as VDN)
+    gis, whh, bhh = rnd(A, C, B, 3 * H), rnd(A, 3 * H, H) * 0.2, rnd(A, 3 * H)
+    keep = (torch.rand(C, 1, B, device=cuda, generator=g) > 0.2).expand(C, A, B)
+    hs, wss = torch.zeros(A, C, B, H, device=cuda), torch.zeros(A, C, B, 4 * H, device=cuda)
+    torch.library.opcheck(flock.gru_seq_fwd.default, (gis, whh, bhh, keep, hs.clone(), wss.clone()),
+                          test_utils=TESTS)
+    flock.gru_seq_fwd(gis, whh, bhh, keep, hs, wss)
+    hs2, wss2 = torch.zeros_like(hs), torch.zeros_like(wss)
+    k8 = keep.view(torch.uint8)
+    st = k8.stride()
+    _check(_native.lib().flock_gru_seq_fwd(_st(cuda), A, C, B, H, _p(gis), _p(whh), _p(bhh), _p(k8), st[0], st[1],
+                                           st[2], _p(hs2), _p(wss2)), "flock_gru_seq_fwd")
+    assert torch.equal(hs, hs2) and torch.equal(wss, wss2)
+    dhs = rnd(A, C, B, H)
+    outs = [torch.zeros(A, C, B, 3 * H, device=cuda), torch.zeros(A, 3 * H, H, device=cuda),
+            torch.zeros(A, 3 * H, device=cuda)]
+    torch.library.opcheck(flock.gru_seq_bwd.default, (dhs, hs, wss, whh, keep, *_clone(*outs)), test_utils=TESTS)
+    flock.gru_seq_bwd(dhs, hs, wss, whh, keep, *outs)
+    ref = _clone(*outs)
+    _check(_native.lib().flock_gru_seq_bwd(_st(cuda), A, C, B, H, _p(dhs), _p(hs), _p(wss), _p(whh), _p(k8), st[0],
+                                           st[1], st[2], *map(_p, ref)), "flock_gru_seq_bwd")
+    for x, y in zip(outs, ref):
+        assert torch.equal(x, y)
+
+
+def test_vdn_feat_fwd(flock, cuda):
+    g = torch.Generator(device=cuda).manual_seed(2)
+    A, C, B, n = 5, 10, 32, 4
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g) * 0.3  # noqa: E731
+    x = rnd(B, C, A, n).permute(2, 1, 0, 3)  # the replay gather's permuted view (unit feature stride)
+    W = [rnd(A, 64, n), rnd(A, 64), rnd(A, 32, 64), rnd(A, 32), rnd(A, 96, 32), rnd(A, 96)]
+    R = C * B
+    outs = [torch.zeros(A, R, 64, device=cuda), torch.zeros(A, R, 32, device=cuda), torch.zeros(A, R, 96, device=cuda)]
+    torch.library.opcheck(flock.vdn_feat_fwd.default, (x, *W, *_clone(*outs)), test_utils=TESTS)
+    flock.vdn_feat_fwd(x, *W, *outs)
+    ref = _clone(*outs)
+    sa, sc, sb, _ = x.stride()
+    _check(_native.lib().flock_vdn_feat_fwd(_st(cuda), A, R, B, n, _p(x), sa, sc, sb, *map(_p, W), *map(_p, ref)),
+           "flock_vdn_feat_fwd")
+    for a, b in zip(outs, ref):
+        assert torch.equal(a, b)
+
+
+def test_rows_and_ring_store(flock, cuda):
+    g = torch.Generator(device=cuda).manual_seed(3)
+    src = torch.randn(100, 7, device=cuda, generator=g)
+    idx = torch.randint(0, 100, (4, 9), device=cuda, generator=g)
+    dst = torch.zeros(4, 9, 7, device=cuda)
+    torch.library.opcheck(flock.gather_rows.default, (src, idx, dst.clone()), test_utils=TESTS)
+    flock.gather_rows(src, idx, dst)
+    assert torch.equal(dst, src[idx])
+    rows = torch.randn(36, 7, device=cuda, generator=g)
+    uidx = torch.randperm(100, device=cuda, generator=g)[:36]
+    tab = torch.zeros(100, 7, device=cuda)
+    torch.library.opcheck(flock.scatter_rows.default, (rows, uidx, tab.clone()), test_utils=TESTS)
+    flock.scatter_rows(rows, uidx, tab)
+    want = torch.zeros(100, 7, device=cuda)
+    want[uidx] = rows
+    assert torch.equal(tab, want)
+    # ring insert of four fields (f32, 1 - done, bool -> f32, int64 ids -> f32), wrapping around the end
+    cap, n = 50, 20
+    s = torch.randn(n, 4, device=cuda, generator=g)
+    d = torch.rand(n, device=cuda, generator=g) > 0.5
+    b = torch.rand(n, 3, device=cuda, generator=g) > 0.5
+    ids = torch.randint(0, 10, (n, 3), device=cuda, generator=g)
+    dsts = [torch.zeros(cap, 4, device=cuda), torch.zeros(cap, device=cuda), torch.zeros(cap, 3, device=cuda),
+            torch.zeros(cap, 3, device=cuda)]
+    torch.library.opcheck(flock.ring_store.default, ([s, d, b, ids], _clone(*dsts), [0, 1, 2, 3], 40),
+                          test_utils=TESTS)
+    flock.ring_store([s, d, b, ids], dsts, [0, 1, 2, 3], 40)
+    ref = _clone(*[torch.zeros_like(t) for t in dsts])
+    F = (_native.FlockRingField * 4)(*[_native.FlockRingField(x.data_ptr(), y.data_ptr(), y.numel() // cap, kd)
+                                       for x, y, kd in zip([s, d, b, ids], ref, [0, 1, 2, 3])])
+    _check(_native.lib().flock_ring_store(_st(cuda), n, cap, 40, 4, F), "flock_ring_store")
+    for x, y in zip(dsts, ref):
+        assert torch.equal(x, y)
+    rows_at = (40 + torch.arange(n, device=cuda)) % cap
+    assert torch.equal(dsts[0][rows_at], s) and torch.equal(dsts[1][rows_at], 1.0 - d.float())
+    assert torch.equal(dsts[3][rows_at], ids.float())
+
+
+def _sc_learner(cuda, seed=0, snapshot=True):
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    L = SharedCriticLearner(6, 4, fc1=64, fc2=48, batch_size=32, buffer_size=500, device=cuda, seed=seed,
+                            use_graph=False, snapshot=snapshot, n_slots=3)
+    g = torch.Generator(device=cuda).manual_seed(11)
+    n = 400
+    L.store_transitions(torch.rand(n, 4, device=cuda, generator=g) * 14, torch.rand(n, 2, device=cuda, generator=g),
+                        torch.where(torch.rand(n, device=cuda, generator=g) < 0.1, -5.0, 0.01),
+                        torch.rand(n, 4, device=cuda, generator=g) * 14, torch.rand(n, device=cuda, generator=g) < 0.1)
+    return L
+
+
+def _sc_state(L):
+    A, C = L.actors, L.critic
+    return [C.data, C.exp_avg, C.exp_avg_sq, C.step_dev, A.data, A.target, A.exp_avg, A.exp_avg_sq, L.actor_steps,
+            L.losses] + L.critic_views
+
+
+def test_shared_critic_ops_opcheck_and_bitwise_the_c_abi(flock, cuda):
+    """sc_prep / sc_prep_snapshot / sc_round through the ops equal the C ABI's flock_sc_prep_snapshot +
+    flock_sc_critic_update / flock_sc_actor_update (ctypes FlockScUpdate) on twin learners, over six learns."""
+    La, Lb = _sc_learner(cuda), _sc_learner(cuda)
+    lib = _native.lib()
+    for t in range(6):
+        agent = t % 6
+        # ops: snapshot into slot t % 3, then the two phases on that slot's rows
+        assert La.snapshot_into(t % 3, agent)
+        La._phase(t % 3, "c")
+        La._phase(t % 3, "a")
+        La._finish_learn(agent, soft_in_kernel=True)
+        # C ABI on the twin
+        Lb._learn_calls += 1
+        S = Lb._slots[t % 3]
+        _check(lib.flock_sc_prep_snapshot(_st(cuda), Lb.batch_size, len(Lb.replay), Lb.seed, Lb._learn_calls,
+                                          _p(Lb.static_idx), _p(S["agent"]), agent, Lb.input_dim, Lb.n_actions,
+                                          ctypes.byref(Lb._rows_ring), ctypes.byref(S["rows"])),
+               "flock_sc_prep_snapshot")
+        _check(lib.flock_sc_critic_update(_st(cuda), ctypes.byref(S["sc"])), "flock_sc_critic_update")
+        _check(lib.flock_sc_actor_update(_st(cuda), ctypes.byref(S["sc"])), "flock_sc_actor_update")
+        Lb._finish_learn(agent, soft_in_kernel=True)
+    for x, y in zip(_sc_state(La), _sc_state(Lb)):
+        assert torch.equal(x, y)
+    assert torch.equal(La.static_idx, Lb.static_idx)
+    # opcheck on clones of the learner state (the ops mutate them)
+    T = flock
+    learner = [t.clone() for t in La._sc_learner]
+    job = [t.clone() for t in La._slots[0]["job"]]
+    torch.library.opcheck(T.sc_round.default, (learner, job, [], La._sc_dims, La._sc_hyper), test_utils=TESTS)
+    torch.library.opcheck(T.sc_round.default, (learner, [], job, La._sc_dims, La._sc_hyper), test_utils=TESTS)
+    stg = [t.clone() for t in job[2:7]]
+    torch.library.opcheck(T.sc_prep_snapshot.default, (La._ring_rows, stg, job[1], La.static_idx.clone(),
+                                                        len(La.replay), 0, 1, 2), test_utils=TESTS)
+    torch.library.opcheck(T.sc_prep.default, (job[1], La.static_idx.clone(), len(La.replay), 0, 1, 2),
+                          test_utils=TESTS)
+    dp = lambda: [t.clone() for t in La._slots[1]["job"]] + [torch.zeros(La.actors.per_agent, device=cuda)]  # noqa
+    torch.library.opcheck(T.sc_round.default, (learner, dp(), dp(), La._sc_dims_grads, La._sc_hyper),
+                          test_utils=TESTS)
+    torch.library.opcheck(T.sc_round_adam.default, (learner, dp(), dp(), La._sc_dims, La._sc_hyper,
+                                                     torch.ones(1, device=cuda)), test_utils=TESTS)
+
+
+def test_shared_critic_sc_prep_path_bitwise_c_abi(flock, cuda):
+    """learn() without the snapshot (flock::sc_prep + two sc_round launch sets on the ring rows) against the C ABI."""
+    La, Lb = _sc_learner(cuda, snapshot=False), _sc_learner(cuda, snapshot=False)
+    lib = _native.lib()
+    for t in range(4):
+        La.learn(t % 6)
+        Lb._learn_calls += 1
+        _check(lib.flock_sc_prep(_st(cuda), Lb.batch_size, len(Lb.replay), Lb.seed, Lb._learn_calls,
+                                 _p(Lb.static_idx), _p(Lb.static_agent), t % 6), "flock_sc_prep")
+        _check(lib.flock_sc_critic_update(_st(cuda), ctypes.byref(Lb._sc)), "flock_sc_critic_update")
+        _check(lib.flock_sc_actor_update(_st(cuda), ctypes.byref(Lb._sc)), "flock_sc_actor_update")
+        Lb._finish_learn(t % 6, soft_in_kernel=True)
+    for x, y in zip(_sc_state(La)[:10], _sc_state(Lb)[:10]):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("kind", ["shared_critic", "maddpg_rnn", "vdn"])
+def test_fused_ring_step_ops_bitwise_the_plan_path(kind, flock, cuda):
+    """VecFlockEnv.step(ring=learner.replay_slots(...)) through step_v2_store / step_uw_discrete_store (launch
+    "torch") and through the C-ABI launch plan (launch "plan"): every env output and every ring field bitwise equal,
+    with two launches per step and a ring smaller than one step's rows (the skip path)."""
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+    from marl_range_flocking_amd.learners.vdn import VDNLearner
+
+    E, N, k = 24, 128, 4
+    variant = "uw_discrete" if kind == "vdn" else "v2"
+    box = float(round((250 * N) ** 0.5))
+    cfg = dict(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5, range_start=(0, box),
+               sensor_range=14.0, seed=5, step_launches=2, max_reset_attempts=8, reset_repair_rounds=8)
+    envs = [VecFlockEnv(FlockConfig(**cfg), device=cuda, launch=o) for o in ("plan", "torch")]
+    if kind == "shared_critic":
+        Ls = [SharedCriticLearner(N, k, fc1=32, fc2=24, batch_size=16, buffer_size=E * N - 100, device=cuda)
+              for _ in envs]
+        slots = lambda L: L.replay_slots(E * N)  # noqa: E731
+    elif kind == "maddpg_rnn":
+        Ls = [MADDPGLearner(N, k, recurrent=True, hidden1=32, hidden2=24, batch_size=8, chunk_size=10,
+                            buffer_capacity=E + 7, min_size_buffer=8, device=cuda) for _ in envs]
+        slots = lambda L: L.replay_slots(E)  # noqa: E731
+    else:
+        Ls = [VDNLearner(N, k, 10, buffer_limit=E + 7, device=cuda) for _ in envs]
+        slots = lambda L: L.replay_slots(E)  # noqa: E731
+    for e in envs:
+        e.reset()
+    g = torch.Generator(device=cuda).manual_seed(4)
+    for _ in range(3):
+        if variant == "uw_discrete":
+            a = torch.randint(0, 10, (E, N), device=cuda, generator=g)
+        else:
+            a = torch.stack([torch.rand(E, N, device=cuda, generator=g),
+                             torch.rand(E, N, device=cuda, generator=g) * 3 - 1.5], -1).contiguous()
+        for e, L in zip(envs, Ls):
+            e.step(a, ring=slots(L))
+        for name in ("positions", "headings", "velocities", "dnn", "reward", "done", "any_done"):
+            assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
+        for name in Ls[0].replay.bufs:
+            assert torch.equal(Ls[0].replay.bufs[name], Ls[1].replay.bufs[name]), name
+        assert Ls[0].replay.counter == Ls[1].replay.counter
+
+
+def test_step_store_opcheck(flock, cuda):
+    E, N, k, cap = 4, 32, 4, 100
+    g = torch.Generator(device=cuda).manual_seed(6)
+    f = dict(device=cuda)
+    pos = torch.rand(E, N, 2, generator=g, **f) * 60
+    st = [pos, torch.rand(E, N, generator=g, **f) * 4.7, torch.rand(E, N, 2, generator=g, **f),
+          torch.zeros(E, N, 2, **f), torch.zeros(E, N, k, **f), torch.zeros(E, N, k, dtype=torch.int64, **f),
+          torch.zeros(E, N, **f), torch.zeros(E, N, dtype=torch.bool, **f), torch.zeros(E, dtype=torch.bool, **f)]
+    ring = [torch.zeros(cap, k, **f), torch.zeros(cap, 2, **f), torch.zeros(cap, 1, **f), torch.zeros(cap, k, **f),
+            torch.zeros(cap, **f)]
+    prev = torch.rand(E, N, k, generator=g, **f)
+    args = (*st, None, ring, None, None, prev, [7, E * N - cap, 1, 0, 0, 0], k, 60.0, 14.0, 2.5)
+    torch.library.opcheck(flock.step_v2_store.default, args, test_utils=TESTS)
+    # uw_discrete with the VDN team transition (a row per env, action ids, env done flags)
+    from marl_range_flocking_amd.ops import UWD_TABLE
+
+    ids = torch.randint(0, 10, (E, N), device=cuda, generator=g)
+    vring = [torch.zeros(10, N, k, **f), torch.zeros(10, N, **f), torch.zeros(10, N, **f), torch.zeros(10, N, k, **f),
+             torch.zeros(10, 1, **f)]
+    args = (st[0], st[1], torch.zeros(E, N, **f), ids, None, torch.tensor(UWD_TABLE, **f), *st[3:5], None,
+            *st[6:9], torch.zeros(1, dtype=torch.int32, **f), None, vring, prev, [3, 0, N, 1, 1, 1], k, 60.0, 14.0,
+            3.0)
+    torch.library.opcheck(flock.step_uw_discrete_store.default, args, test_utils=TESTS)
+    with pytest.raises(RuntimeError, match="ring"):
+        flock.step_v2_store(*st, None, ring, None, None, prev, [cap, 0, 1, 0, 0, 0], k, 60.0, 14.0, 2.5)
