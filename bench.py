@@ -85,6 +85,11 @@ def parse():
                     help="config 3: enqueue the timed steps (env step + learn()) through torch.classes.flock."
                          "ScTrainLoop, K steps per C++ call (bitwise the per-step path); 0: one Python call per step "
                          "(flock::step_v2_store + the native learn() pipeline)")
+    ap.add_argument("--policy-steps", type=int, default=20,
+                    help="config 3, N=1: also time this many steps of the actor-driven loop of the reference's "
+                         "driver (choose_action of every agent + OU noise -> env.step + insert -> learn(), "
+                         "learners/maddpg_shared_critic/train_flock.py:114-121) after the headline, reported in the "
+                         "policy_in_loop field (0: skip)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
                          "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
@@ -346,6 +351,46 @@ class MADDPGBench:
             self.learner.train()
 
 
+def policy_loop(hook, env, first, steps):
+    """The actor-driven training loop of learners/maddpg_shared_critic/train_flock.py:114-121 at the bench's size:
+    choose_action of every agent on the current observation (mu + OU noise, agent_simple_shared_critic.py:92-107,
+    batched over all agents and envs), the env step with the fused replay insert, then one learn(). Each step's
+    actions come from the actors the previous learn() updated, so nothing of step s+1 overlaps learn(s) here."""
+    L = hook.learner
+    dev = env.device
+    stream = torch.cuda.current_stream(dev)
+    marks = []
+
+    def one(s, timed):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        if e:
+            e[0].record(stream)
+        a = L.choose_action(env.dnn, noise=True)
+        if e:
+            e[1].record(stream)
+        env.step(a, ring=hook.before(s))
+        if e:
+            e[2].record(stream)
+        L.learn(s % L.n_agents)
+        if e:
+            e[3].record(stream)
+            marks.append(e)
+
+    for i in range(3):  # graph capture of the serial learn() and the OU state outside the timed steps
+        one(first + i, False)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(first + 3 + i, True)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    part = lambda i: float(np.mean([m[i].elapsed_time(m[i + 1]) for m in marks]))  # noqa: E731
+    return {"ms_per_step": el / steps * 1e3, "value": env.E * env.N * steps / el, "unit": "agent-steps/s",
+            "steps": steps, "act_ms": part(0), "env_step_ms": part(1), "learn_ms": part(2),
+            "note": "choose_action (stacked actors, every env and agent, + OU noise) -> env step + replay insert -> "
+                    "learn(agent s mod 256), serial: the next step's actions need this learn()'s actor update"}
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
@@ -523,6 +568,10 @@ def main():
                              "step's launches, with the learner's kernels beside them); *_alone: the same step as one "
                              "launch with no learner, after the timed region"},
     }
+    if (hook is not None and args.learner == "shared_critic" and world == 1 and args.policy_steps > 0
+            and args.variant == "v2"):
+        hook.finish()
+        line["policy_in_loop"] = policy_loop(hook, env, args.warmup + args.steps + 100, args.policy_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, box, args.cpu_seconds)
     if rank == 0:

@@ -269,6 +269,12 @@ void step_flock_meta(const Tensor& pos, const Tensor& vel, const Tensor& action,
 // store_done, action_ids, env_done] (FlockRing, include/flock_amd.h)
 FlockRing ring_of(const Tensor& pos, at::TensorList ring, const optional<Tensor>& actor_state,
                   const optional<Tensor>& actor_new_state, const Tensor& prev_obs, at::IntArrayRef meta, int64_t k) {
+    // traced with symbolic sizes (AOT dispatch, dynamic shapes): no concrete sizes to check (the HIP wrapper does)
+    auto sym = [](const Tensor& t) { return t.defined() && t.unsafeGetTensorImpl()->has_symbolic_sizes_strides(); };
+    bool any = sym(pos) || sym(prev_obs) || (actor_state && sym(*actor_state)) ||
+               (actor_new_state && sym(*actor_new_state));
+    for (const Tensor& t : ring) any = any || sym(t);
+    if (any) return FlockRing{};
     auto [E, N] = dims(pos);
     TORCH_CHECK(ring.size() == 5, "ring must be [state, action, reward, new_state, terminal]");
     TORCH_CHECK(meta.size() == 6, "ring_meta must be [start, skip, group, store_done, action_ids, env_done]");

@@ -38,6 +38,19 @@ void hip_only(const Tensor& t, const char* op) {
     TORCH_CHECK(t.device().is_cuda(), op, ": flock ops run on a HIP device only (no CPU fallback); got ", t.device());
 }
 
+// A tensor traced with symbolic sizes (AOT dispatch with dynamic shapes) has no concrete sizes / numel to compare:
+// the Meta kernels skip their shape checks for it (the HIP wrappers always run them on the real tensors).
+bool symbolic(const Tensor& t) { return t.defined() && t.unsafeGetTensorImpl()->has_symbolic_sizes_strides(); }
+bool sym1(const Tensor& t) { return symbolic(t); }
+bool sym1(const optional<Tensor>& t) { return t.has_value() && symbolic(*t); }
+bool sym1(at::TensorList l) {
+    for (const Tensor& t : l)
+        if (symbolic(t)) return true;
+    return false;
+}
+template <typename... Ts>
+bool any_sym(const Ts&... ts) { return (sym1(ts) || ...); }
+
 // a dense f32 (or other dtype) buffer on `like`'s device
 void dense(const Tensor& t, const char* name, at::ScalarType dtype, const Tensor& like) {
     TORCH_CHECK(t.device() == like.device(), name, " must be on ", like.device(), ", got ", t.device());
@@ -59,6 +72,7 @@ T* ptr(const optional<Tensor>& t) { return t.has_value() ? static_cast<T*>(t->da
 // --------------------------------------------------------------------------------------------------- adam_step
 void adam_checks(const Tensor& param, const Tensor& grad, const Tensor& m, const Tensor& v, const Tensor& step,
                  const optional<Tensor>& grad_scale, const optional<Tensor>& target) {
+    if (any_sym(param, grad, m, v, step, grad_scale, target)) return;
     const int64_t n = param.numel();
     dense(param, "param", at::kFloat, param);
     dense(grad, "grad", at::kFloat, param);
@@ -100,6 +114,7 @@ void adam_step_meta(const Tensor& param, const Tensor& grad, const Tensor& m, co
 
 // ------------------------------------------------------------------------------------------------- soft_update
 void soft_checks(const Tensor& target, const Tensor& src, int64_t mode) {
+    if (any_sym(target, src)) return;
     dense(target, "target", at::kFloat, target);
     dense(src, "src", at::kFloat, target);
     numel_is(src, "src", target.numel());
@@ -117,6 +132,7 @@ void soft_update_meta(const Tensor& target, const Tensor& src, double, int64_t m
 
 // --------------------------------------------------------------------------------------------------- grad_norm
 void norm_checks(const Tensor& grad, const Tensor& partial, const Tensor& out) {
+    if (any_sym(grad, partial, out)) return;
     dense(grad, "grad", at::kFloat, grad);
     dense(partial, "partial", at::kDouble, grad);
     TORCH_CHECK(partial.dim() == 1 && partial.numel() >= 1, "partial must be a 1-D scratch buffer");
@@ -142,6 +158,7 @@ int64_t gru_rows(const Tensor& h) {
 }
 void gru_cell_fwd_checks(const Tensor& gi, const Tensor& gh, const Tensor& h, const Tensor& hout,
                          const optional<Tensor>& ws) {
+    if (any_sym(gi, gh, h, hout, ws)) return;
     const int64_t rows = gru_rows(h), H = h.size(-1);
     dense(h, "h", at::kFloat, h);
     dense(gi, "gi", at::kFloat, h);
@@ -170,6 +187,7 @@ void gru_cell_fwd_meta(const Tensor& gi, const Tensor& gh, const Tensor& h, cons
 }
 void gru_cell_bwd_checks(const Tensor& dhout, const Tensor& h, const Tensor& ws, const Tensor& dgi, const Tensor& dgh,
                          const Tensor& dh) {
+    if (any_sym(dhout, h, ws, dgi, dgh, dh)) return;
     const int64_t rows = gru_rows(h), H = h.size(-1);
     dense(h, "h", at::kFloat, h);
     dense(dhout, "dhout", at::kFloat, h);
@@ -207,6 +225,7 @@ void keep_check(const Tensor& keep, int64_t A, int64_t C, int64_t B, const Tenso
 }
 void gru_seq_fwd_checks(const Tensor& gi, const Tensor& w_hh, const Tensor& b_hh, const Tensor& keep, const Tensor& hs,
                         const optional<Tensor>& ws) {
+    if (any_sym(gi, w_hh, b_hh, keep, hs, ws)) return;
     TORCH_CHECK(gi.dim() == 4 && gi.size(3) % 3 == 0, "gi must be [A, C, B, 3H], got ", gi.sizes());
     const int64_t A = gi.size(0), C = gi.size(1), B = gi.size(2), H = gi.size(3) / 3;
     TORCH_CHECK(H == 32, "gru_seq: hidden size must be 32");
@@ -234,6 +253,7 @@ void gru_seq_fwd_meta(const Tensor& gi, const Tensor& w_hh, const Tensor& b_hh, 
 }
 void gru_seq_bwd_checks(const Tensor& dhs, const Tensor& hs, const Tensor& ws, const Tensor& w_hh, const Tensor& keep,
                         const Tensor& dgi, const Tensor& dw_hh, const Tensor& db_hh) {
+    if (any_sym(dhs, hs, ws, w_hh, keep, dgi, dw_hh, db_hh)) return;
     TORCH_CHECK(hs.dim() == 4, "hs must be [A, C, B, H], got ", hs.sizes());
     const int64_t A = hs.size(0), C = hs.size(1), B = hs.size(2), H = hs.size(3);
     TORCH_CHECK(H == 32, "gru_seq: hidden size must be 32");
@@ -268,6 +288,7 @@ void gru_seq_bwd_meta(const Tensor& dhs, const Tensor& hs, const Tensor& ws, con
 void vdn_feat_checks(const Tensor& x, const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2,
                      const Tensor& wi, const Tensor& bi, const optional<Tensor>& y1, const optional<Tensor>& y2,
                      const Tensor& gi) {
+    if (any_sym(x, w1, b1, w2, b2, wi, bi, y1, y2, gi)) return;
     TORCH_CHECK(x.dim() == 4, "x must be [A, C, B, n_obs], got ", x.sizes());
     const int64_t A = x.size(0), R = x.size(1) * x.size(2), n = x.size(3);
     TORCH_CHECK(n >= 1 && n <= 16, "vdn_feat_fwd: n_obs must be in [1, 16]");
@@ -305,6 +326,7 @@ void vdn_feat_fwd_meta(const Tensor& x, const Tensor& w1, const Tensor& b1, cons
 // src / dst: [rows_src, ...] f32 rows of `width` floats; idx: int64 of any shape; gather: dst [idx.numel(), width],
 // scatter: src [idx.numel(), width]
 void rows_checks(const Tensor& src, const Tensor& idx, const Tensor& dst, bool scatter) {
+    if (any_sym(src, idx, dst)) return;
     dense(src, "src", at::kFloat, src);
     dense(dst, "dst", at::kFloat, src);
     dense(idx, "idx", at::kLong, src);
@@ -336,6 +358,7 @@ void scatter_rows_meta(const Tensor& src, const Tensor& idx, const Tensor& dst) 
 // -------------------------------------------------------------------------------------------------- ring_store
 // src[i]: n rows of field i (f32 [n, w]; kind 1/2 u8|bool [n, w]; kind 3 int64 [n, w]); dst[i]: [capacity, w] f32
 void ring_checks(at::TensorList src, at::TensorList dst, at::IntArrayRef kind, int64_t start) {
+    if (dst.empty() || any_sym(src, dst)) return;
     TORCH_CHECK(src.size() >= 1 && src.size() <= 8 && dst.size() == src.size() && kind.size() == src.size(),
                 "ring_store: 1..8 fields with one dst and one kind each");
     const Tensor& like = dst[0];
@@ -387,6 +410,7 @@ void sc_rows_check(at::TensorList t, const char* what, int64_t in_dim, int64_t n
 }
 void snapshot_checks(at::TensorList ring, at::TensorList staging, const Tensor& agent_out,
                      const optional<Tensor>& idx_out, int64_t rows) {
+    if (ring.empty() || any_sym(ring, staging, agent_out, idx_out)) return;
     TORCH_CHECK(ring.size() == 5 && staging.size() == 5, "sc_prep_snapshot: 5 ring and 5 staging fields");
     const int64_t in_dim = ring[0].dim() == 2 ? ring[0].size(1) : 0;
     const int64_t na = ring[2].dim() == 2 ? ring[2].size(1) : 0;
@@ -418,7 +442,7 @@ void sc_prep_snapshot_meta(at::TensorList ring, at::TensorList staging, const Te
 //            actors_exp_avg, actors_exp_avg_sq, actors_target, actor_steps [n_agents] i64, losses [2],
 //            counters [2] i32]
 // job     = [] (no phase) or [idx [B] i64, agent [1] i64, state, new_state, action, reward, terminal (the rows the
-//            update reads: a staging slot or the ring), workspace, critic_view]
+//            update reads: a staging slot or the ring), workspace, critic_view (empty: none)(, actor_grad_out)]
 // dims    = [B, in_dim, n_actions, fc1, fc2, update_rate, do_adam]; hyper = [alpha, beta, gamma, beta1, beta2, eps, tau]
 struct ScArgs {
     FlockScUpdate u;
@@ -426,6 +450,7 @@ struct ScArgs {
 };
 void sc_round_checks(at::TensorList L, at::TensorList job, at::IntArrayRef dims, at::ArrayRef<double> hyper,
                      const char* what) {
+    if (L.empty() || any_sym(L, job)) return;
     TORCH_CHECK(L.size() == 13, "sc_round: learner must hold the 13 state tensors");
     TORCH_CHECK(dims.size() == 7 && hyper.size() == 7, "sc_round: dims [7] and hyper [7]");
     const Tensor& like = L[0];
@@ -451,8 +476,10 @@ void sc_round_checks(at::TensorList L, at::TensorList job, at::IntArrayRef dims,
     dense(job[7], "workspace", at::kFloat, like);
     numel_is(job[7], "workspace", flock_sc_workspace_floats((int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3],
                                                             (int)dims[4]));
-    dense(job[8], "critic_view", at::kFloat, like);
-    numel_is(job[8], "critic_view", L[0].numel());
+    if (job[8].numel() > 0) {  // an empty critic_view: none (FlockScUpdate.critic_view = NULL)
+        dense(job[8], "critic_view", at::kFloat, like);
+        numel_is(job[8], "critic_view", L[0].numel());
+    }
     if (job.size() == 10) {  // FlockScUpdate.actor_grad_out: one actor's gradient (data-parallel bucket)
         dense(job[9], "actor_grad_out", at::kFloat, like);
         numel_is(job[9], "actor_grad_out", L[5].numel() / L[10].numel());
@@ -496,7 +523,7 @@ FlockScUpdate sc_update(at::TensorList L, at::TensorList job, at::IntArrayRef di
     u.beta2 = (float)hyper[4];
     u.eps = (float)hyper[5];
     u.tau = (float)hyper[6];
-    u.critic_view = ptr<float>(job[8]);
+    u.critic_view = job[8].numel() > 0 ? ptr<float>(job[8]) : nullptr;
     u.actor_grad_out = job.size() == 10 ? ptr<float>(job[9]) : nullptr;
     return u;
 }
@@ -552,6 +579,7 @@ void sc_round_adam_meta(at::TensorList learner, at::TensorList critic_job, at::T
 
 // learn() prologue without a snapshot (flock_sc_prep): *agent_out = agent; idx[r] = Philox(seed, counter, r) mod rows
 void sc_prep_checks(const Tensor& agent_out, const optional<Tensor>& idx, int64_t rows) {
+    if (any_sym(agent_out, idx)) return;
     shaped(agent_out, "agent_out", at::kLong, {1}, agent_out);
     if (idx) {
         dense(*idx, "idx", at::kLong, agent_out);
@@ -578,7 +606,7 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         "adam_step(Tensor(a!) param, Tensor grad, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, Tensor step, "
         "Tensor? grad_scale, Tensor(d!)? target, float lr, float beta1=0.9, float beta2=0.999, float eps=1e-08, "
         "float tau=0.0, int target_mode=0) -> ()");
-    m.def("soft_update(Tensor(a!) target, Tensor src, float tau, int mode=0) -> ()");
+    m.def("soft_update(Tensor(a!) target, Tensor src, float tau, int form=0) -> ()");
     m.def("grad_norm(Tensor grad, Tensor(a!) partial, Tensor(b!) out, float max_norm) -> ()");
     m.def("gru_cell_fwd(Tensor gi, Tensor gh, Tensor h, Tensor(a!) hout, Tensor(b!)? ws) -> ()");
     m.def("gru_cell_bwd(Tensor dhout, Tensor h, Tensor ws, Tensor(a!) dgi, Tensor(b!) dgh, Tensor(c!) dh) -> ()");

@@ -175,6 +175,9 @@ class SharedCriticLearner:
         self._sc_dims_grads = [B, n_in, na, self.fc1, self.fc2, 0, 0]
         self._sc_hyper = [self.alpha, self.beta, self.gamma, 0.9, 0.999, 1e-8, self.tau]
         self._sc_job = [self.static_idx, self.static_agent, *rows(rb), self.sc_workspace, self.critic_views[0]]
+        # data-parallel gradient phases read the critic itself (no critic view: Adam runs between the phases)
+        self._no_view = torch.empty(0, device=dev)
+        self._sc_job_grads = self._sc_job[:8] + [self._no_view]
         self._ring_rows = rows(rb)
         # single GPU: the soft updates run inside the gradient kernels (device-side count condition)
         self._sc = _native.FlockScUpdate(**fields, critic_view=_p(self.critic_views[0]))
@@ -200,6 +203,8 @@ class SharedCriticLearner:
                 self._slots.append(dict(staging=stg, agent=agent_t, graph=None, graph_c=None, graph_a=None,
                                         job=[self.identity_idx, agent_t, *rows(stg), self.sc_workspaces[i],
                                              self.critic_views[i]],
+                                        job_grads=[self.identity_idx, agent_t, *rows(stg), self.sc_workspaces[i],
+                                                   self._no_view],
                                         rows=_native.FlockScRows(**{n: _p(stg[n]) for n in names}),
                                         sc=_native.FlockScUpdate(**f, critic_view=_p(self.critic_views[i])),
                                         sc_grads=_native.FlockScUpdate(**dict(f, do_adam=0, update_rate=0))))
@@ -231,6 +236,8 @@ class SharedCriticLearner:
     def _run_fused(self, agent, slot=None):
         S = self._slots[slot] if slot is not None else None
         job = S["job"] if S is not None else self._sc_job
+        if self.distributed:
+            job = S["job_grads"] if S is not None else self._sc_job_grads
         if not self.distributed:
             if not self.use_graph:
                 return self._fused_update(job)
