@@ -73,6 +73,14 @@ int flock_vdn_feat_fwd(void* stream, int A, int R, int B, int n_in, const float*
                        int64_t x_sb, const float* w1, const float* b1, const float* w2, const float* b2,
                        const float* w_ih, const float* b_ih, float* y1, float* y2, float* gi);
 
+/* Backward of flock_vdn_feat_fwd (the autograd chain of vdn/train_flock.py:40 through the feature layers), one
+ * launch for all agents: dgi [A][R][96] = dLoss/dgi, y1 [A][R][64] / y2 [A][R][32] the forward's post-ReLU outputs,
+ * x / w2 [A][32][64] / w_ih [A][96][32] as in the forward. Writes (not accumulates) dw1 [A][64][n_in], db1 [A][64],
+ * dw2 [A][32][64], db2 [A][32], dw_ih [A][96][32], db_ih [A][96]. */
+int flock_vdn_feat_bwd(void* stream, int A, int R, int B, int n_in, const float* x, int64_t x_sa, int64_t x_sc,
+                       int64_t x_sb, const float* w2, const float* w_ih, const float* y1, const float* y2,
+                       const float* dgi, float* dw1, float* db1, float* dw2, float* db2, float* dw_ih, float* db_ih);
+
 /* gather: dst[r][:] = src[idx[r]][:]; scatter: dst[idx[r]][:] = src[r][:]; rows of `width` floats. */
 int flock_gather_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);
 int flock_scatter_rows(void* stream, int64_t rows, int64_t width, const float* src, const int64_t* idx, float* dst);

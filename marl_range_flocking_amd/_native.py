@@ -53,6 +53,8 @@ SIGNATURES = {
     "flock_gru_bwd": [_c_void_p, ctypes.c_int64, _c_int] + [_c_void_p] * 6,
     "flock_vdn_feat_fwd": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p] + [ctypes.c_int64] * 3
                           + [_c_void_p] * 9,
+    "flock_vdn_feat_bwd": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p] + [ctypes.c_int64] * 3
+                          + [_c_void_p] * 11,
     "flock_gru_seq_fwd": [_c_void_p, _c_int, _c_int, _c_int, _c_int] + [_c_void_p] * 4 + [ctypes.c_int64] * 3
     + [_c_void_p] * 2,
     "flock_gru_seq_bwd": [_c_void_p, _c_int, _c_int, _c_int, _c_int] + [_c_void_p] * 5 + [ctypes.c_int64] * 3

@@ -271,6 +271,11 @@ constexpr int kF1 = 64, kF2 = 32, kFG = 96, kFRows = 64, kFMaxIn = 16;
 constexpr int kSW1 = kFMaxIn + 2, kSY1 = kF1 + 2, kSY2 = kF2 + 2;  // LDS row strides (floats)
 using f32x4_t = float __attribute__((ext_vector_type(4)));
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt), not for its global loads
+// (__syncthreads() waits for vmcnt(0) too, which would drain the next rows' prefetch at every barrier). The global
+// loads' own waits stay where their registers are first used.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // NT column tiles of 16: acc[t] += A[16 rows][K] * W[16 t .. 16 t + 16][K]^T, k in steps of 4 (one MFMA each)
 template <int NT>
 __device__ __forceinline__ void mfma_rows(f32x4_t (&acc)[NT], const float* a, int sa, const float* w, int sw,
@@ -336,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void vdn_feat_fwd_kernel(int R, int B, int 
             const int e = tid + kBlock * q;
             if (e < kFRows * K1) xs[(e / K1) * sx + (e % K1)] = xr[q];
         }
-        __syncthreads();  // xs (and, first time round, the weights) visible; the previous rows' reads are done
+        lds_barrier();  // xs (and, first time round, the weights) visible; the previous rows' reads are done
         if (r0 + kFRows < R) load_x(r0 + kFRows);  // in flight while these rows compute
         const int64_t base = a * R + r0;
         {  // layer 1: 4 column tiles
@@ -351,7 +356,7 @@ __global__ __launch_bounds__(kBlock) void vdn_feat_fwd_kernel(int R, int B, int 
                     if (y1o && row4 + v < nr) y1o[(base + row4 + v) * kF1 + 16 * t + col] = y;
                 }
         }
-        __syncthreads();
+        lds_barrier();
         {  // layer 2: 2 column tiles
             f32x4_t acc[2] = {};
             mfma_rows<2>(acc, y1s + 16 * wv * kSY1, kSY1, w2, kSY1, kF1, lane);
@@ -364,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void vdn_feat_fwd_kernel(int R, int B, int 
                     if (y2o && row4 + v < nr) y2o[(base + row4 + v) * kF2 + 16 * t + col] = y;
                 }
         }
-        __syncthreads();
+        lds_barrier();
         {  // GRU input side: 6 column tiles, written from the accumulators (16 lanes = 64 contiguous bytes)
             f32x4_t acc[6] = {};
             mfma_rows<6>(acc, y2s + 16 * wv * kSY2, kSY2, wi, kSY2, kF2, lane);
@@ -376,6 +381,196 @@ __global__ __launch_bounds__(kBlock) void vdn_feat_fwd_kernel(int R, int B, int 
                         gi[(base + row4 + v) * kFG + 16 * t + col] = acc[t][v] + bs[kF1 + kF2 + 16 * t + col];
         }
     }
+}
+
+// Backward of the same chain, ONE launch (the five batched GEMMs, two ReLU masks and three row sums of the autograd
+// backward, learners/core.py _VdnFeatFn): from dgi = dLoss/dgi [A][R][96] and the saved y1 / y2,
+//   dz2 = (dgi Wih) [y2 > 0]   dz1 = (dz2 W2) [y1 > 0]
+//   dWih = dgi^T y2, dbih = sum_r dgi, dW2 = dz2^T y1, db2 = sum_r dz2, dW1 = dz1^T x, db1 = sum_r dz1
+// One block of 8 waves (two per SIMD, so one wave's dependent MFMA chain hides behind the other's) per agent walks
+// its rows 64 at a time, the next 64 rows of dgi / y1 / y2 / x in registers while the current ones compute. Every
+// row chunk is staged FEATURE-major in LDS ([feature][row], stride 64 + 2), so the same arrays serve as the A
+// operand of the row GEMMs (dz2, dz1: A[row][k] read as T[k][row]) and as both operands of the weight-gradient
+// GEMMs, whose K dimension is the rows: the 24 tiles of dWih (6 x 2), dW2 (2 x 4) and dW1 (4 x 1) stay in MFMA
+// accumulators across all chunks (3 per wave) and are written once at the end; the bias sums run on VALU from the
+// same LDS rows. f32 MFMA (v_mfma_f32_16x16x4_f32): each output is a k-ordered fmaf chain.
+constexpr int kBS = kFRows + 2;  // feature-major row stride (floats): 2 mod 4
+constexpr int kBB = 512;         // threads per block of the backward
+__global__ __launch_bounds__(kBB) void vdn_feat_bwd_kernel(int R, int B, int NI, const float* __restrict__ x,
+                                                           int64_t xa, int64_t xc, int64_t xb,
+                                                           const float* __restrict__ W2, const float* __restrict__ Wi,
+                                                           const float* __restrict__ y1, const float* __restrict__ y2,
+                                                           const float* __restrict__ dgi,
+                                                           float* __restrict__ dW1, float* __restrict__ db1,
+                                                           float* __restrict__ dW2, float* __restrict__ db2,
+                                                           float* __restrict__ dWi, float* __restrict__ dbi) {
+    __shared__ float wiN[kFG * (kF2 + 2)];   // Wih [96][32] as stored: B[k][j] of dz2 = dgi Wih (k = 96 outputs)
+    __shared__ float w2N[kF2 * (kF1 + 2)];   // W2 [32][64] as stored: B[k][j] of dz1 = dz2 W2 (k = 32 outputs)
+    __shared__ float gT[kFG * kBS];          // dgi chunk, feature-major [96][64]
+    __shared__ float y2T[kF2 * kBS];         // [32][64]
+    __shared__ float y1T[kF1 * kBS];         // [64][64]
+    __shared__ float xT[kFMaxIn * kBS];      // [16][64] (features >= n_obs are zero)
+    __shared__ float z2T[kF2 * kBS];         // dz2 [32][64]
+    __shared__ float z1T[kF1 * kBS];         // dz1 [64][64]
+    const int64_t a = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;  // 8 waves
+    const int i16 = lane & 15, kk = lane >> 4;
+    for (int e = tid; e < kFG * kF2; e += kBB) wiN[(e / kF2) * (kF2 + 2) + e % kF2] = Wi[a * kFG * kF2 + e];
+    for (int e = tid; e < kF2 * kF1; e += kBB) w2N[(e / kF1) * (kF1 + 2) + e % kF1] = W2[a * kF2 * kF1 + e];
+    // per-thread register staging of the next chunk: dgi 64 x 96 (12 floats / thread), y1 64 x 64 (8), y2 64 x 32
+    // (4), x 64 x 16 (2), each read row-major with consecutive threads on consecutive floats
+    constexpr int kG = kFRows * kFG / kBB, kY1 = kFRows * kF1 / kBB, kY2 = kFRows * kF2 / kBB,
+                  kX = kFRows * kFMaxIn / kBB;
+    float rg[kG], r1[kY1], r2[kY2], rx[kX];
+    const int64_t base_a = a * (int64_t)R;
+    auto load = [&](int r0) {
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+            const int e = tid + kBB * q, rr = e / kFG;
+            rg[q] = r0 + rr < R ? dgi[(base_a + r0) * kFG + e] : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < kY1; ++q) {
+            const int e = tid + kBB * q, rr = e / kF1;
+            r1[q] = r0 + rr < R ? y1[(base_a + r0) * kF1 + e] : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < kY2; ++q) {
+            const int e = tid + kBB * q, rr = e / kF2;
+            r2[q] = r0 + rr < R ? y2[(base_a + r0) * kF2 + e] : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < kX; ++q) {
+            const int e = tid + kBB * q, rr = e / kFMaxIn, f = e - rr * kFMaxIn, r = r0 + rr;
+            rx[q] = 0.0f;
+            if (r < R && f < NI) {
+                const int c = r / B, b = r - c * B;
+                rx[q] = x[a * xa + c * xc + b * xb + f];
+            }
+        }
+    };
+    // persistent weight-gradient accumulators, three 16 x 16 tiles per wave: unit u = 3 wv + j of the 24 (dWih
+    // units 0..11 -> tile (m, n) = (u >> 1, u & 1); dW2 units 12..19 -> ((u - 12) >> 2, (u - 12) & 3); dW1 units
+    // 20..23 -> rows 16 (u - 20) of the 64 outputs x the 16 padded features)
+    f32x4_t acc3[3] = {};
+    float bsum = 0.0f;  // thread tid < 192: bias sum of feature tid (dbih 0..95, db2 96..127, db1 128..191)
+    load(0);
+    const int col = i16, row4 = 4 * kk;  // C/D layout: col = lane & 15, row = 4 (lane >> 4) + v
+    const int rg4 = wv & 3;              // the 16-row group of the row GEMMs this wave works on
+    for (int r0 = 0; r0 < R; r0 += kFRows) {
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+            const int e = tid + kBB * q, rr = e / kFG, f = e - rr * kFG;
+            gT[f * kBS + rr] = rg[q];
+        }
+#pragma unroll
+        for (int q = 0; q < kY1; ++q) {
+            const int e = tid + kBB * q, rr = e / kF1, f = e - rr * kF1;
+            y1T[f * kBS + rr] = r1[q];
+        }
+#pragma unroll
+        for (int q = 0; q < kY2; ++q) {
+            const int e = tid + kBB * q, rr = e / kF2, f = e - rr * kF2;
+            y2T[f * kBS + rr] = r2[q];
+        }
+#pragma unroll
+        for (int q = 0; q < kX; ++q) {
+            const int e = tid + kBB * q, rr = e / kFMaxIn, f = e - rr * kFMaxIn;
+            xT[f * kBS + rr] = rx[q];
+        }
+        lds_barrier();  // the chunk (and, first time round, the weights) visible; last chunk's reads are done
+        if (r0 + kFRows < R) load(r0 + kFRows);  // in flight while this chunk computes
+        {  // dz2 = (dgi Wih) [y2 > 0]: waves w and w + 4 share rows 16 (w & 3) .., one column tile each, K = 96
+            const int t = wv >> 2;
+            f32x4_t acc = {};
+#pragma unroll 4
+            for (int k = 0; k < kFG; k += 4)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(gT[(k + kk) * kBS + 16 * rg4 + i16],
+                                                           wiN[(k + kk) * (kF2 + 2) + 16 * t + i16], acc, 0, 0, 0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int r = 16 * rg4 + row4 + v, o = 16 * t + col;
+                z2T[o * kBS + r] = y2T[o * kBS + r] > 0.0f ? acc[v] : 0.0f;
+            }
+        }
+        lds_barrier();
+        {  // dz1 = (dz2 W2) [y1 > 0]: two column tiles per wave, K = 32
+            f32x4_t acc[2] = {};
+            const int t0 = 2 * (wv >> 2);
+#pragma unroll
+            for (int k = 0; k < kF2; k += 4) {
+                const float av = z2T[(k + kk) * kBS + 16 * rg4 + i16];
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, w2N[(k + kk) * (kF1 + 2) + 16 * (t0 + j) + i16],
+                                                                  acc[j], 0, 0, 0);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int r = 16 * rg4 + row4 + v, o = 16 * (t0 + j) + col;
+                    z1T[o * kBS + r] = y1T[o * kBS + r] > 0.0f ? acc[j][v] : 0.0f;
+                }
+        }
+        lds_barrier();
+        // weight gradients, K = this chunk's 64 rows: A[m][k] = T_a[m][row k], B[n][k] = T_b[n][row k]
+#pragma unroll 2
+        for (int k = 0; k < kFRows; k += 4) {
+            const int kr = k + kk;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int u = 3 * wv + j;
+                const float* Ta;
+                const float* Tb;
+                int m, n;
+                if (u < 12) {
+                    Ta = gT, Tb = y2T, m = u >> 1, n = u & 1;
+                } else if (u < 20) {
+                    Ta = z2T, Tb = y1T, m = (u - 12) >> 2, n = (u - 12) & 3;
+                } else {
+                    Ta = z1T, Tb = xT, m = u - 20, n = 0;
+                }
+                acc3[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ta[(16 * m + i16) * kBS + kr],
+                                                               Tb[(16 * n + i16) * kBS + kr], acc3[j], 0, 0, 0);
+            }
+        }
+        if (tid < kFG + kF2 + kF1) {  // bias sums: one feature per thread, rows in order
+            const float* src = tid < kFG ? gT + tid * kBS : tid < kFG + kF2 ? z2T + (tid - kFG) * kBS
+                                                                           : z1T + (tid - kFG - kF2) * kBS;
+            const int nr = min(kFRows, R - r0);
+            if (nr == kFRows) {
+#pragma unroll 16
+                for (int r = 0; r < kFRows; ++r) bsum += src[r];
+            } else {
+                for (int r = 0; r < nr; ++r) bsum += src[r];
+            }
+        }
+        lds_barrier();  // the next chunk's stores overwrite these arrays
+    }
+    // write the weight gradients from the accumulators (C/D: row = 4 kk + v within the tile, column = lane & 15)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int u = 3 * wv + j;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            if (u < 12) {
+                const int m = u >> 1, n = u & 1;
+                dWi[(a * kFG + 16 * m + row4 + v) * kF2 + 16 * n + col] = acc3[j][v];
+            } else if (u < 20) {
+                const int m = (u - 12) >> 2, n = (u - 12) & 3;
+                dW2[(a * kF2 + 16 * m + row4 + v) * kF1 + 16 * n + col] = acc3[j][v];
+            } else if (col < NI) {
+                dW1[(a * kF1 + 16 * (u - 20) + row4 + v) * NI + col] = acc3[j][v];
+            }
+        }
+    }
+    if (tid < kFG)
+        dbi[a * kFG + tid] = bsum;
+    else if (tid < kFG + kF2)
+        db2[a * kF2 + tid - kFG] = bsum;
+    else if (tid < kFG + kF2 + kF1)
+        db1[a * kF1 + tid - kFG - kF2] = bsum;
 }
 
 // dst[r, :] = src[idx[r], :]  (replay minibatch / chunk gather); one wave per row, 16-B vectors when aligned
@@ -750,6 +945,20 @@ int flock_vdn_feat_fwd(void* stream, int A, int R, int B, int n_in, const float*
     if (B < 1 || R % B != 0) return fail(-5, "flock_vdn_feat_fwd: R must be a multiple of B");
     hipLaunchKernelGGL(vdn_feat_fwd_kernel, dim3(A), dim3(kBlock), 0, (hipStream_t)stream,
                        R, B, n_in, x, x_sa, x_sc, x_sb, w1, b1, w2, b2, w_ih, b_ih, y1, y2, gi);
+    return launched();
+}
+
+int flock_vdn_feat_bwd(void* stream, int A, int R, int B, int n_in, const float* x, int64_t x_sa, int64_t x_sc,
+                       int64_t x_sb, const float* w2, const float* w_ih, const float* y1, const float* y2,
+                       const float* dgi, float* dw1, float* db1, float* dw2, float* db2, float* dw_ih,
+                       float* db_ih) {
+    if (A <= 0) return 0;
+    if (!x || !w2 || !w_ih || !y1 || !y2 || !dgi || !dw1 || !db1 || !dw2 || !db2 || !dw_ih || !db_ih)
+        return fail(-3, "flock_vdn_feat_bwd: NULL pointer");
+    if (n_in < 1 || n_in > kFMaxIn) return fail(-2, "flock_vdn_feat_bwd: n_in must be in [1, 16]");
+    if (R < 1 || B < 1 || R % B != 0) return fail(-5, "flock_vdn_feat_bwd: R must be a positive multiple of B");
+    hipLaunchKernelGGL(vdn_feat_bwd_kernel, dim3(A), dim3(kBB), 0, (hipStream_t)stream, R, B, n_in, x, x_sa, x_sc,
+                       x_sb, w2, w_ih, y1, y2, dgi, dw1, db1, dw2, db2, dw_ih, db_ih);
     return launched();
 }
 

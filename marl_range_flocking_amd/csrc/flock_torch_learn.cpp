@@ -12,7 +12,7 @@
 //   flock::grad_norm         clip_grad_norm_ (vdn/train_flock.py:42) without a host sync
 //   flock::gru_cell_fwd/_bwd nn.GRUCell elementwise part (maddpg_official_rnn/net.py:33,118; vdn/net.py:24)
 //   flock::gru_seq_fwd/_bwd  a whole chunk of GRUCell steps (vdn/train_flock.py:23-36, MADDPG.py:95-132)
-//   flock::vdn_feat_fwd      the VDN QNet feature chain + GRU input side (vdn/net.py:19-33)
+//   flock::vdn_feat_fwd/_bwd the VDN QNet feature chain + GRU input side (vdn/net.py:19-33) and its backward
 //   flock::gather_rows / scatter_rows / ring_store   replay gather / insert (memory_rnn.py:53-99, vdn/utils.py:18-60,
 //                            maddpg_shared_critic/utils.py:47-76)
 //   flock::sc_prep_snapshot  shared-critic learn() prologue: Philox row sample + minibatch copy (utils.py:65-76)
@@ -322,6 +322,47 @@ void vdn_feat_fwd_meta(const Tensor& x, const Tensor& w1, const Tensor& b1, cons
     vdn_feat_checks(x, w1, b1, w2, b2, wi, bi, y1, y2, gi);
 }
 
+// backward of the chain (flock_vdn_feat_bwd): dgi [A, C*B, 96], y1 / y2 the forward's outputs -> dw1 [A,64,n],
+// db1 [A,64], dw2 [A,32,64], db2 [A,32], dw_ih [A,96,32], db_ih [A,96]
+void vdn_feat_bwd_checks(const Tensor& x, const Tensor& w2, const Tensor& wi, const Tensor& y1, const Tensor& y2,
+                         const Tensor& dgi, const Tensor& dw1, const Tensor& db1, const Tensor& dw2, const Tensor& db2,
+                         const Tensor& dwi, const Tensor& dbi) {
+    if (any_sym(x, w2, wi, y1, y2, dgi, dw1, db1, dw2, db2, dwi, dbi)) return;
+    TORCH_CHECK(x.dim() == 4, "x must be [A, C, B, n_obs], got ", x.sizes());
+    const int64_t A = x.size(0), R = x.size(1) * x.size(2), n = x.size(3);
+    TORCH_CHECK(n >= 1 && n <= 16, "vdn_feat_bwd: n_obs must be in [1, 16]");
+    TORCH_CHECK(x.scalar_type() == at::kFloat && x.stride(3) == 1, "x must be f32 with a unit feature stride");
+    shaped(w2, "w2", at::kFloat, {A, 32, 64}, x);
+    shaped(wi, "w_ih", at::kFloat, {A, 96, 32}, x);
+    shaped(y1, "y1", at::kFloat, {A, R, 64}, x);
+    shaped(y2, "y2", at::kFloat, {A, R, 32}, x);
+    shaped(dgi, "dgi", at::kFloat, {A, R, 96}, x);
+    shaped(dw1, "dw1", at::kFloat, {A, 64, n}, x);
+    shaped(db1, "db1", at::kFloat, {A, 64}, x);
+    shaped(dw2, "dw2", at::kFloat, {A, 32, 64}, x);
+    shaped(db2, "db2", at::kFloat, {A, 32}, x);
+    shaped(dwi, "dw_ih", at::kFloat, {A, 96, 32}, x);
+    shaped(dbi, "db_ih", at::kFloat, {A, 96}, x);
+}
+void vdn_feat_bwd_hip(const Tensor& x, const Tensor& w2, const Tensor& wi, const Tensor& y1, const Tensor& y2,
+                      const Tensor& dgi, const Tensor& dw1, const Tensor& db1, const Tensor& dw2, const Tensor& db2,
+                      const Tensor& dwi, const Tensor& dbi) {
+    hip_only(x, "vdn_feat_bwd");
+    vdn_feat_bwd_checks(x, w2, wi, y1, y2, dgi, dw1, db1, dw2, db2, dwi, dbi);
+    const at::OptionalDeviceGuard g(x.device());
+    rc_check(flock_vdn_feat_bwd(stream_of(x), (int)x.size(0), (int)(x.size(1) * x.size(2)), (int)x.size(2),
+                                (int)x.size(3), ptr<const float>(x), x.stride(0), x.stride(1), x.stride(2),
+                                ptr<const float>(w2), ptr<const float>(wi), ptr<const float>(y1), ptr<const float>(y2),
+                                ptr<const float>(dgi), ptr<float>(dw1), ptr<float>(db1), ptr<float>(dw2),
+                                ptr<float>(db2), ptr<float>(dwi), ptr<float>(dbi)),
+             "flock_vdn_feat_bwd");
+}
+void vdn_feat_bwd_meta(const Tensor& x, const Tensor& w2, const Tensor& wi, const Tensor& y1, const Tensor& y2,
+                       const Tensor& dgi, const Tensor& dw1, const Tensor& db1, const Tensor& dw2, const Tensor& db2,
+                       const Tensor& dwi, const Tensor& dbi) {
+    vdn_feat_bwd_checks(x, w2, wi, y1, y2, dgi, dw1, db1, dw2, db2, dwi, dbi);
+}
+
 // --------------------------------------------------------------------------------- gather_rows / scatter_rows
 // src / dst: [rows_src, ...] f32 rows of `width` floats; idx: int64 of any shape; gather: dst [idx.numel(), width],
 // scatter: src [idx.numel(), width]
@@ -617,6 +658,9 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
     m.def(
         "vdn_feat_fwd(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w_ih, Tensor b_ih, "
         "Tensor(a!)? y1, Tensor(b!)? y2, Tensor(c!) gi) -> ()");
+    m.def(
+        "vdn_feat_bwd(Tensor x, Tensor w2, Tensor w_ih, Tensor y1, Tensor y2, Tensor dgi, Tensor(a!) dw1, "
+        "Tensor(b!) db1, Tensor(c!) dw2, Tensor(d!) db2, Tensor(e!) dw_ih, Tensor(f!) db_ih) -> ()");
     m.def("gather_rows(Tensor src, Tensor idx, Tensor(a!) dst) -> ()");
     m.def("scatter_rows(Tensor src, Tensor idx, Tensor(a!) dst) -> ()");
     m.def("ring_store(Tensor[] src, Tensor(a!)[] dst, int[] kind, int start) -> ()");
@@ -641,6 +685,7 @@ TORCH_LIBRARY_IMPL(flock, CUDA, m) {
     m.impl("gru_seq_fwd", &gru_seq_fwd_hip);
     m.impl("gru_seq_bwd", &gru_seq_bwd_hip);
     m.impl("vdn_feat_fwd", &vdn_feat_fwd_hip);
+    m.impl("vdn_feat_bwd", &vdn_feat_bwd_hip);
     m.impl("gather_rows", &gather_rows_hip);
     m.impl("scatter_rows", &scatter_rows_hip);
     m.impl("ring_store", &ring_store_hip);
@@ -659,6 +704,7 @@ TORCH_LIBRARY_IMPL(flock, Meta, m) {
     m.impl("gru_seq_fwd", &gru_seq_fwd_meta);
     m.impl("gru_seq_bwd", &gru_seq_bwd_meta);
     m.impl("vdn_feat_fwd", &vdn_feat_fwd_meta);
+    m.impl("vdn_feat_bwd", &vdn_feat_bwd_meta);
     m.impl("gather_rows", &gather_rows_meta);
     m.impl("scatter_rows", &scatter_rows_meta);
     m.impl("ring_store", &ring_store_meta);

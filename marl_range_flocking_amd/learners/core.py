@@ -338,7 +338,7 @@ class _VdnFeatFn(torch.autograd.Function):
     the saved post-ReLU activations as batched GEMMs (the weight gradients land in each parameter's own layout)."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, Wi, bi, save):
+    def forward(ctx, x, W1, b1, W2, b2, Wi, bi, save, fused_bwd=True):
         A, C, B, n = x.shape
         R = C * B
         if x.stride(3) != 1:
@@ -351,12 +351,20 @@ class _VdnFeatFn(torch.autograd.Function):
         _ops().vdn_feat_fwd(x, W1, b1, W2, b2, Wi, bi, y1, y2, gi)
         if save:
             ctx.save_for_backward(x, W2, Wi, y1, y2)
+            ctx.fused_bwd = bool(fused_bwd)
         return gi
 
     @staticmethod
     def backward(ctx, dgi):
         x, W2, Wi, y1, y2 = ctx.saved_tensors
         A, C, B, n = x.shape
+        if ctx.fused_bwd:  # one launch: flock::vdn_feat_bwd (MFMA, the weight gradients accumulated over all rows)
+            f = dict(dtype=x.dtype, device=x.device)
+            dW1, db1 = torch.empty(A, 64, n, **f), torch.empty(A, 64, **f)
+            dW2, db2 = torch.empty(A, 32, 64, **f), torch.empty(A, 32, **f)
+            dWi, dbi = torch.empty(A, 96, 32, **f), torch.empty(A, 96, **f)
+            _ops().vdn_feat_bwd(x, W2, Wi, y1, y2, dgi.contiguous(), dW1, db1, dW2, db2, dWi, dbi)
+            return None, dW1, db1, dW2, db2, dWi, dbi, None, None
         dWi = torch.bmm(dgi.transpose(1, 2), y2)
         dbi = dgi.sum(1)
         dz2 = torch.bmm(dgi, Wi).masked_fill_(y2 <= 0, 0.0)     # ReLU backward on the output (y > 0 iff z > 0)
@@ -365,17 +373,19 @@ class _VdnFeatFn(torch.autograd.Function):
         dz1 = torch.bmm(dz2, W2).masked_fill_(y1 <= 0, 0.0)
         dW1 = torch.bmm(dz1.transpose(1, 2), x.reshape(A, C * B, n))
         db1 = dz1.sum(1)
-        return None, dW1, db1, dW2, db2, dWi, dbi, None
+        return None, dW1, db1, dW2, db2, dWi, dbi, None, None
 
 
-def vdn_feat(x, W1, b1, W2, b2, Wi, bi):
+def vdn_feat(x, W1, b1, W2, b2, Wi, bi, fused_bwd=True):
     """x [A,C,B,n_obs] (any strides with a unit feature stride, e.g. the replay gather's permuted view) -> gi
-    [A, C*B, 96] = relu(relu(x W1^T + b1) W2^T + b2) Wi^T + bi per agent (hidden sizes 64 / 32, n_obs <= 16)."""
+    [A, C*B, 96] = relu(relu(x W1^T + b1) W2^T + b2) Wi^T + bi per agent (hidden sizes 64 / 32, n_obs <= 16).
+    fused_bwd: the backward as one flock::vdn_feat_bwd launch (False: batched GEMMs + masks + sums, the A/B
+    baseline)."""
     A, n = x.shape[0], x.shape[3]
     if not (W1.shape == (A, 64, n) and W2.shape == (A, 32, 64) and Wi.shape == (A, 96, 32) and 1 <= n <= 16):
         raise ValueError("vdn_feat: the QNet feature chain n_obs -> 64 -> 32 -> 3 x 32 (n_obs <= 16)")
     save = torch.is_grad_enabled() and any(t.requires_grad for t in (W1, b1, W2, b2, Wi, bi))
-    return _VdnFeatFn.apply(x, W1, b1, W2, b2, Wi, bi, save)
+    return _VdnFeatFn.apply(x, W1, b1, W2, b2, Wi, bi, save, fused_bwd)
 
 
 def gru_cell_gi(gi, h, W_hh, b_hh):

@@ -132,6 +132,19 @@ def test_vdn_feat_fwd(flock, cuda):
            "flock_vdn_feat_fwd")
     for a, b in zip(outs, ref):
         assert torch.equal(a, b)
+    # the backward (flock_vdn_feat_bwd) on the forward's saved activations
+    y1, y2 = outs[0], outs[1]
+    dgi = rnd(A, R, 96)
+    grads = [torch.zeros(A, 64, n, device=cuda), torch.zeros(A, 64, device=cuda), torch.zeros(A, 32, 64, device=cuda),
+             torch.zeros(A, 32, device=cuda), torch.zeros(A, 96, 32, device=cuda), torch.zeros(A, 96, device=cuda)]
+    torch.library.opcheck(flock.vdn_feat_bwd.default, (x, W[2], W[4], y1, y2, dgi, *_clone(*grads)),
+                          test_utils=TESTS)
+    flock.vdn_feat_bwd(x, W[2], W[4], y1, y2, dgi, *grads)
+    ref = _clone(*grads)
+    _check(_native.lib().flock_vdn_feat_bwd(_st(cuda), A, R, B, n, _p(x), sa, sc, sb, _p(W[2]), _p(W[4]), _p(y1),
+                                            _p(y2), _p(dgi), *map(_p, ref)), "flock_vdn_feat_bwd")
+    for a, b in zip(grads, ref):
+        assert torch.equal(a, b)
 
 
 def test_rows_and_ring_store(flock, cuda):
