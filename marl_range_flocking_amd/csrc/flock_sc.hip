@@ -1941,7 +1941,7 @@ struct FlockScPipeline {
     hipGraphExec_t merged[kMaxSlots], conly[kMaxSlots], aonly[kMaxSlots];
     Job jc[kMaxSlots], ja[kMaxSlots];  // direct launches (graphs == false): the rounds' arguments, built once
     bool graphs;
-    int diag;  // FLOCK_SC_PIPELINE_DIAG (timing diagnostics only; results are wrong): 1 no learner wait on the
+    int diag;  // -DFLOCK_SC_PIPELINE_DIAG=<bits> builds only (timing diagnostics; results are wrong): 1 no learner wait on the
                // snapshot, 2 no env wait on the slot, 3 neither
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
     bool used[kMaxSlots];
@@ -2012,8 +2012,11 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     // (FLOCK_SC_PIPELINE_GRAPHS=1, read here once): config-3 step 0.117 ms direct vs 0.125 ms with graphs
     const char* ge = getenv("FLOCK_SC_PIPELINE_GRAPHS");
     p->graphs = ge && ge[0] == '1';
-    const char* de = getenv("FLOCK_SC_PIPELINE_DIAG");
-    p->diag = de ? atoi(de) : 0;
+#ifdef FLOCK_SC_PIPELINE_DIAG
+    p->diag = FLOCK_SC_PIPELINE_DIAG;  // a diagnostics build (tools/build_variant.sh): drops stream dependencies
+#else
+    p->diag = 0;  // the shipped library never skips a dependency
+#endif
     int rc = 0;
     for (int i = 0; i < n_slots && !rc; ++i) {
         critic_job(&p->u[i], p->jc[i]);
