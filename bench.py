@@ -493,6 +493,20 @@ def main():
         torch.cuda.synchronize(dev)
         alone_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_alone[2:]]))
 
+    # the host cost of enqueueing a step, apart from the GPU: the GPU is held by a ~50 ms sleep kernel on the env
+    # stream while 32 steps are enqueued, so no full hardware queue throttles the enqueue (in the timed region the
+    # host runs ahead until the queue is full, and host_ms_per_step then follows the GPU)
+    host_us = None
+    if use_loop:
+        hook.finish()
+        torch.cuda.synchronize(dev)
+        torch.cuda._sleep(int(2.4e9 * 0.05))
+        t_h = time.perf_counter()
+        hook.run_steps(args.warmup + args.steps + 50, 32, pool)
+        host_us = (time.perf_counter() - t_h) / 32 * 1e6
+        hook.finish()
+        torch.cuda.synchronize(dev)
+
     total_agent_steps = world * E * N * args.steps
     value = total_agent_steps / el
     fused_ring = args.learner in RING_BYTES_PER_AGENT_STEP
@@ -537,6 +551,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
         "host_ms_per_step": host_el / args.steps * 1e3,
+        "host_enqueue_us_per_step": host_us,
         "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
                       "one Python step per vectorized step (torch.ops.flock)"),
         "higher_is_better": True,
