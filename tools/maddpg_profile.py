@@ -34,7 +34,10 @@ for use_graph in (True, False):
     print(f"use_graph={use_graph}: {1e3 * (time.perf_counter() - t0) / 5:.2f} ms per train()", flush=True)
 from torch.profiler import ProfilerActivity, profile
 
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
     L.train()
     torch.cuda.synchronize()
 print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_name_column_width=60))
+# the copies and GEMMs by input shape (where the time of aten::copy_ / mm / bmm goes)
+print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40,
+                                                         max_name_column_width=40, max_shapes_column_width=110))

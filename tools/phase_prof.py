@@ -34,7 +34,7 @@ def build():
                                                      os.path.join(b, "flock_sc.hip.o")])
 
 
-def run(E, N, k, steps, variant="v2"):
+def run(E, N, k, steps, variant="v2", seeds=False):
     import numpy as np
     import torch
 
@@ -57,6 +57,14 @@ def run(E, N, k, steps, variant="v2"):
     f.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 6 + [ctypes.c_int] * 2 + \
         [ctypes.c_void_p] * 9
     stream = torch.cuda.current_stream(dev).cuda_stream
+    ext = None
+    if seeds:  # the compact seed buffer (v2 only), as VecFlockEnv passes it
+        from marl_range_flocking_amd._native import FlockStepExt
+
+        sb = torch.zeros(E, N, k, dtype=torch.int16, device=dev)
+        ext = FlockStepExt(ring=None, seeds=sb.data_ptr(), launches=1, normalize_distance=0)
+        fe = lib.flock_step_v2_ext
+        fe.argtypes = f.argtypes + [ctypes.c_void_p]
     gd = lib.flock_step_uw_discrete
     gd.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 5 + [ctypes.c_int] + \
         [ctypes.c_void_p] * 5 + [ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int] + \
@@ -70,7 +78,11 @@ def run(E, N, k, steps, variant="v2"):
     prev = torch.zeros(E, N, device=dev)
 
     def step():
-        if variant == "v2":
+        if variant == "v2" and ext is not None:
+            rc = fe(stream, E, N, k, box, 14.0, 2.5, 0.1, 0.0, 2.5, 1, 0, pos.data_ptr(), head.data_ptr(),
+                    act.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(), rew.data_ptr(), done.data_ptr(),
+                    anyd.data_ptr(), ctypes.addressof(ext))
+        elif variant == "v2":
             rc = f(stream, E, N, k, box, 14.0, 2.5, 0.1, 0.0, 2.5, 1, 0, pos.data_ptr(), head.data_ptr(),
                    act.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(), rew.data_ptr(), done.data_ptr(),
                    anyd.data_ptr())
@@ -145,8 +157,9 @@ if __name__ == "__main__":
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uwd"])
+    ap.add_argument("--seeds", action="store_true", help="v2 through flock_step_v2_ext with a seed buffer")
     a = ap.parse_args()
     if a.build:
         build()
     else:
-        run(a.E, a.N, a.k, a.steps, a.variant)
+        run(a.E, a.N, a.k, a.steps, a.variant, a.seeds)
