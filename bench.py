@@ -27,7 +27,8 @@ Rank 0 prints ONE JSON line. Extra fields:
                 0.86-0.97 of its wall cycles on this measure). frac = busy / (kernel time x 2.4 GHz); peak = the
                 lane-op rate of this instruction mix with every SIMD issuing every cycle at 2.4 GHz
                 (64 x SQ_INSTS_VALU x 2.4e9 / busy); frac_full_rate = against 78.6 T lane-op/s (every instruction
-                co-issued). "binding" names the larger of the HBM and VALU fractions.
+                co-issued). "binding" names the larger of the HBM and VALU fractions (measured alone when the
+                line has an alone measurement), or "latency" when neither reaches half of its peak.
   cpu_baseline  the reference's step on the host: v2 = environments/gym_flock_v2.py's torch-CPU op sequence
                 (oracle/torch_ref.py, calibrated against the reference, tests/golden/cpu_calibration.json) stepping
                 one env at a time on every host CPU this process may use (sched_getaffinity, capped by the cgroup
@@ -54,6 +55,15 @@ BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  #
 # transition: s 16 + a (f32 id) 4 + r 4 + s' 16 (+ one done flag per env: 4 / N)
 RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80, "vdn": 16 + 40}
 EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 4))  # steps between HIP-event-timed env launches (timed region)
+
+
+def binding(valu, hbm_frac, alone_ms, alg_bytes):
+    """The roofline the env kernel is closest to (fractions of the kernel alone when measured, else in the loop);
+    "latency" when neither HBM nor VALU issue reaches half of its peak."""
+    h = alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if alone_ms else hbm_frac
+    v = (valu["frac_alone"] if alone_ms and valu.get("frac_alone") is not None else valu["frac"]) if valu else 0.0
+    name, f = ("valu", v) if v > h else ("hbm", h)
+    return name if f >= 0.5 else "latency"
 
 
 def parse():
@@ -573,7 +583,7 @@ def main():
                      "insert_bytes_per_agent_step": ins,
                      "achieved_incl_insert": (bpa + ins) * E * N / kern_s / 1e9,
                      "valu": valu,
-                     "binding": "valu" if valu and valu["frac"] > hbm_frac else "hbm",
+                     "binding": binding(valu, hbm_frac, alone_ms, bpa * E * N),
                      "step_launches": launches,
                      "kernel_ms_per_launch": kern_ms / launches,  # compare with rocprofv3's per-dispatch average
                      "kernel_alone_ms": alone_ms,

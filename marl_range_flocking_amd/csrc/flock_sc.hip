@@ -630,6 +630,13 @@ __device__ unsigned long long g_scmark[4096][8];
 #define SC_PROF(k)
 #define SC_MARK(MK, i)
 #endif
+// -DFLOCK_SC_PRIO=n (A/B builds): the round kernels' waves raise their issue priority (s_setprio n) over the env
+// kernel's waves they share SIMDs with
+#ifdef FLOCK_SC_PRIO
+#define SC_PRIO() __builtin_amdgcn_s_setprio(FLOCK_SC_PRIO)
+#else
+#define SC_PRIO()
+#endif
 
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
@@ -637,6 +644,7 @@ __device__ unsigned long long g_scmark[4096][8];
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     SC_PROF(0);
+    SC_PRIO();
     if ((int)blockIdx.y < npc)
         c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
     else
@@ -645,6 +653,7 @@ __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, 
 template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
     SC_PROF(2);
+    SC_PRIO();
     if ((int)blockIdx.x < nbc)
         c3_body<C, HC, NAC>(wc, ac, blockIdx.x);
     else
@@ -916,6 +925,7 @@ __device__ __forceinline__ int xcd_tile(int x, int tiles) {
 template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     SC_PROF(1);
+    SC_PRIO();
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const GemmP& g = gb.p[blockIdx.y];
@@ -1154,6 +1164,7 @@ struct Bwd2 {
 template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
 __global__ __launch_bounds__(256) void sc_bwd(Bwd2 bb) {
     SC_PROF(3);
+    SC_PRIO();
     if ((int)blockIdx.x < bb.nb0)
         bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
     else
@@ -1302,6 +1313,7 @@ struct GradAdam2 {
 };
 __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
     SC_PROF(4);
+    SC_PRIO();
     if ((int)blockIdx.x < gg.nb0)
         grad_adam_body(gg.j0, blockIdx.x, gg.nb0);
     else

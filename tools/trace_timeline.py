@@ -1,0 +1,95 @@
+"""Per-step timeline of the config-3 loop from a rocprofv3 --kernel-trace CSV (diagnostics).
+
+For every env step (the step_kernel launches) and every learner round (sc_k1 .. sc_grad_adam) prints the start / end
+relative to the first step, and summarises: the step period, the env launches' span, the round's span, the gap
+between the snapshot and the round's first kernel, the gaps between the round's kernels, and which stream set the
+period (did the env stream start its next step right after its previous one, or later).
+Usage: python tools/trace_timeline.py TRACE.csv [first_step=...]"""
+import csv
+import statistics as st
+import sys
+
+
+def load(path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
+    rows.sort()
+    return rows
+
+
+def short(name):
+    for key in ("step_kernel", "sc_prep_snapshot", "sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam"):
+        if key in name:
+            return key
+    return None
+
+
+def main():
+    rows = [(s, e, short(n)) for s, e, n in load(sys.argv[1])]
+    rows = [r for r in rows if r[2]]
+    # group: an env step = consecutive step_kernel launches followed by a snapshot; a round = k1..grad_adam
+    env_steps, cur = [], []
+    for s, e, k in rows:
+        if k == "step_kernel":
+            cur.append((s, e))
+        elif k == "sc_prep_snapshot" and cur:
+            env_steps.append((cur, (s, e)))
+            cur = []
+    rounds, rc = [], {}
+    for s, e, k in rows:
+        if k == "sc_k1":
+            rc = {"sc_k1": (s, e)}
+        elif k.startswith("sc_") and k != "sc_prep_snapshot" and rc:
+            rc[k] = (s, e)
+            if k == "sc_grad_adam":
+                rounds.append(rc)
+                rc = {}
+    n = min(len(env_steps), len(rounds))
+    skip = max(0, n - 60)  # the last 60 steps (the timed region sits at the end of a short bench)
+    t0 = env_steps[skip][0][0][0]
+    per, env_span, rnd_span, snap_gap, env_idle = [], [], [], [], []
+    kgaps = {k: [] for k in ("sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam")}
+    kdur = {k: [] for k in ("sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam")}
+    for i in range(skip, n - 1):
+        launches, snap = env_steps[i]
+        nxt = env_steps[i + 1][0][0][0]
+        per.append((nxt - launches[0][0]) / 1e3)
+        env_span.append((launches[-1][1] - launches[0][0]) / 1e3)
+        env_idle.append((nxt - snap[1]) / 1e3)
+        # the round that consumes this step's snapshot starts after it
+        r = next((rr for rr in rounds if rr["sc_k1"][0] >= snap[1]), None)
+        if r is None:
+            continue
+        snap_gap.append((r["sc_k1"][0] - snap[1]) / 1e3)
+        rnd_span.append((r["sc_grad_adam"][1] - r["sc_k1"][0]) / 1e3)
+        order = ["sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam"]
+        for a, b in zip(order, order[1:]):
+            kgaps[b].append((r[b][0] - r[a][1]) / 1e3)
+        for k in order:
+            kdur[k].append((r[k][1] - r[k][0]) / 1e3)
+        if i - skip < 12:
+            ls = " ".join("%7.1f-%7.1f" % ((s - t0) / 1e3, (e - t0) / 1e3) for s, e in launches)
+            print("step %3d env %s snap %7.1f-%7.1f | round %7.1f-%7.1f" % (
+                i - skip, ls, (snap[0] - t0) / 1e3, (snap[1] - t0) / 1e3, (r["sc_k1"][0] - t0) / 1e3,
+                (r["sc_grad_adam"][1] - t0) / 1e3))
+
+    def m(v):
+        return "%.1f (p10 %.1f p90 %.1f)" % (st.mean(v), sorted(v)[len(v) // 10], sorted(v)[9 * len(v) // 10])
+
+    print("steps analysed", len(per))
+    print("step period us            ", m(per))
+    print("env launches span us      ", m(env_span))
+    print("env stream idle after snap", m(env_idle))
+    print("snapshot end -> k1 start  ", m(snap_gap))
+    print("round span k1..grad us    ", m(rnd_span))
+    for k, v in kdur.items():
+        print("  %-13s dur %s" % (k, m(v)))
+    for k, v in kgaps.items():
+        print("  gap before %-13s %s" % (k, m(v)))
+
+
+if __name__ == "__main__":
+    main()
