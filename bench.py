@@ -47,6 +47,7 @@ import torch
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 CLOCK_HZ = 2.4e9                 # MI355X peak engine clock (MI355X_MICROARCH.md); the roofline's clock
 SIMDS = 1024                     # 256 CU x 4 SIMD
+MFMA_F32_PEAK = 157.3e12         # MI355X_MICROARCH.md: dense f32 matrix peak (v_mfma_f32_*)
 VALU_PEAK_FULL_RATE = 64 * SIMDS * CLOCK_HZ / 2  # 78.6e12 lane-op/s: every wave64 instruction co-issued (2 cycles)
 BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
 # fused replay insert (flock_step_v2_store / the uw_discrete ring), per agent-step: + previous obs read (k=4 floats)
@@ -395,8 +396,13 @@ def policy_loop(hook, env, first, steps):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     part = lambda i: float(np.mean([m[i].elapsed_time(m[i + 1]) for m in marks]))  # noqa: E731
+    # choose_action's algorithmic work: every actor's fc1, fc2 and mu head on every env row (f32 MFMA for fc2)
+    flops = 2.0 * env.E * env.N * (L.fc1 * L.input_dim + L.fc1 * L.fc2 + L.fc2 * L.n_actions)
+    act_ms = part(0)
     return {"ms_per_step": el / steps * 1e3, "value": env.E * env.N * steps / el, "unit": "agent-steps/s",
-            "steps": steps, "act_ms": part(0), "env_step_ms": part(1), "learn_ms": part(2),
+            "steps": steps, "act_ms": act_ms, "env_step_ms": part(1), "learn_ms": part(2),
+            "act_path": "flock_sc_act (one fused MFMA launch + the OU draws)" if L.fused_act_ok() else "torch bmm chain",
+            "act_tflops": flops / (act_ms * 1e-3) / 1e12, "act_mfma_frac": flops / (act_ms * 1e-3) / MFMA_F32_PEAK,
             "note": "choose_action (stacked actors, every env and agent, + OU noise) -> env step + replay insert -> "
                     "learn(agent s mod 256), serial: the next step's actions need this learn()'s actor update"}
 

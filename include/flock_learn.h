@@ -164,6 +164,16 @@ typedef struct FlockScRows {
 int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
                            int64_t* agent_out, int64_t agent, int in_dim, int n_actions, const FlockScRows* ring,
                            const FlockScRows* staging);
+/* Agent.choose_action of every agent on every env row in one launch (learners/maddpg_shared_critic/
+ * agent_simple_shared_critic.py:92-107; actor ddpg_network.py:132-141; OUActionNoiseGPU utils.py:15-18 with one
+ * process per (row, agent)). obs [rows][n_agents][in_dim] f32; actors: the agent-major actor buffer of
+ * FlockScUpdate (agent a at actors + a * actor_stride; 16-B aligned, actor_stride a multiple of 4); actions
+ * [rows][n_agents][2] = tanh(mu head) (+ the OU state after its step when ou_state is not NULL: ou <- ou +
+ * theta (0 - ou) dt + sigma_sqrt_dt noise, in that float op order, noise [rows][n_agents][2] N(0,1) draws).
+ * Limits: 1 <= in_dim <= 16, fc1 a multiple of 8 (<= 2000 at in_dim 4), fc2 <= 320, 2 actions. */
+int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim, int fc1, int fc2, const float* obs,
+                 const float* actors, int64_t actor_stride, float* actions, float* ou_state, const float* noise,
+                 float theta, float dt, float sigma_sqrt_dt);
 int flock_sc_critic_update(void* stream, const FlockScUpdate* u); /* :118-141 */
 int flock_sc_actor_update(void* stream, const FlockScUpdate* u);  /* :144-150 (after the critic update) */
 /* One round of six launches: the critic phase of critic_u and the actor phase of actor_u (either may be NULL; each

@@ -119,6 +119,8 @@ SIGNATURES.update({
     "flock_sc_prep_snapshot": [_c_void_p, _c_int, ctypes.c_int64, _c_u64, _c_u64, _c_void_p, _c_void_p,
                                ctypes.c_int64, _c_int, _c_int, _c_void_p, _c_void_p],
     "flock_sc_prep": [_c_void_p, _c_int, ctypes.c_int64, _c_u64, _c_u64, _c_void_p, _c_void_p, ctypes.c_int64],
+    "flock_sc_act": [_c_void_p, ctypes.c_int64, _c_int, _c_int, _c_int, _c_int, _c_void_p, _c_void_p, ctypes.c_int64,
+                     _c_void_p, _c_void_p, _c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float],
     "flock_sc_critic_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_actor_update": [_c_void_p, ctypes.POINTER(FlockScUpdate)],
     "flock_sc_round": [_c_void_p, ctypes.POINTER(FlockScUpdate), ctypes.POINTER(FlockScUpdate)],

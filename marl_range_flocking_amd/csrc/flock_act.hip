@@ -1,0 +1,410 @@
+// Batched shared-critic acting on MI355X (gfx950): choose_action of EVERY agent for EVERY env row in one launch.
+//
+// Reference: learners/maddpg_shared_critic/agent_simple_shared_critic.py:92-107 (Agent.choose_action: mu = actor(obs)
+// + noise()), the actor of ddpg_network.py:132-141 (fc1 -> LayerNorm -> ReLU -> fc2 -> LayerNorm -> ReLU -> mu ->
+// tanh) and OUActionNoiseGPU.__call__ (utils.py:15-18: x = x_prev + theta (mu - x_prev) dt + sigma sqrt(dt) N(0,1),
+// mu = 0, one process per (env, agent) here). The reference calls choose_action once per agent per env step on one
+// env; the training loop at the bench's size (4096 envs x 256 agents) needs 1M actor evaluations per step.
+//
+// One block = one agent x 64 env rows (4 waves). The work is fc2: [64 x fc1] x [fc1 x fc2] per block, on
+// v_mfma_f32_32x32x2_f32 (f32 in, f32 accumulate: no reduced precision anywhere). Nothing but the 16-B observation
+// rows and the 8-B actions touches HBM per (row, agent):
+//   * the A operand (the fc1 -> LayerNorm -> ReLU activations) is never stored: each lane recomputes its 4 values of
+//     a k-step from the row's observation (in registers), fc1's 4-float weight rows and LayerNorm affine (LDS
+//     broadcast reads) and the row's LayerNorm statistics (a prologue over all fc1 outputs of the block's rows);
+//   * the B operand (fc2.weight, [fc2][fc1] row-major = contiguous along k) is read straight from global memory as
+//     one float4 per lane per tile per k-step, one k-step ahead of the MFMAs; the lanes' k assignment (lane half h
+//     takes k0 + 4h .. k0 + 4h + 3, MFMA s of the step pairs k0 + s with k0 + 4 + s) makes both operands contiguous;
+//   * the fc2 outputs stay in the accumulators: LayerNorm (row sums by a 32-lane xor butterfly and one LDS
+//     exchange between the two waves covering a row), ReLU, the 2-wide mu head and tanh run in the epilogue;
+//   * XCD-aware work order: the blocks of one agent run on one XCD (block b -> work (b % 8) * W/8 + b / 8), so its
+//     fc2.weight (480 KB at 400 x 300) is fetched into that XCD's L2 once and read by its 64 row tiles from there.
+// The OU step and the noisy action are computed in the epilogue in the torch op order of choose_action
+// (learners/shared_critic.py), bit for bit: the noise z is drawn by the caller (torch.randn on its generator).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+
+#include "flock_learn.h"
+#include "learn_internal.h"
+
+using flock_learn_internal::fail;
+using flock_learn_internal::launched;
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kTM = 64;  // env rows per block (two 32-row bands)
+constexpr int kKC = 32;  // k depth of an LDS-staged fc2.weight chunk (STG)
+
+struct ActArgs {
+    const float* obs;     // [rows][A][in]
+    const float* actors;  // agent-major flat buffer, agent a at actors + a * stride
+    float* actions;       // [rows][A][2]
+    float* ou;            // [rows][A][2] or NULL (no noise)
+    const float* noise;   // [rows][A][2] N(0, 1) draws (with ou)
+    int64_t rows, stride;
+    int A, in, H1, H2, tiles;
+    float theta, dt, c;  // OU: theta, dt, sigma * sqrt(dt)
+};
+
+__device__ __forceinline__ float xor32(float v, int m) {  // lane l <- lane l ^ m within each 32-lane half
+    switch (m) {
+        case 1: return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (1 << 10) | 0x1F));
+        case 2: return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (2 << 10) | 0x1F));
+        case 4: return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (4 << 10) | 0x1F));
+        case 8: return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (8 << 10) | 0x1F));
+        default: return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (16 << 10) | 0x1F));
+    }
+}
+__device__ __forceinline__ float sum32(float v) {
+    v += xor32(v, 16);
+    v += xor32(v, 8);
+    v += xor32(v, 4);
+    v += xor32(v, 2);
+    v += xor32(v, 1);
+    return v;
+}
+
+// NT: 32-column tiles per wave (each wave covers half of the padded fc2 width: fc2 <= 64 NT); INC: compile-time
+// observation width (0: runtime, <= 16)
+template <int NT, int INC, bool STG>
+__global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
+    extern __shared__ float4 smem4[];
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    const int IN = INC ? INC : p.in, INP = (IN + 3) & ~3, H1 = p.H1, H2 = p.H2;
+    const int W = p.A * p.tiles, b = blockIdx.x;
+    const int work = (W & 7) == 0 ? (b & 7) * (W >> 3) + (b >> 3) : b;
+    const int agent = work / p.tiles, tile = work - agent * p.tiles;
+    const int64_t r0 = (int64_t)tile * kTM;
+    const float* P = p.actors + (int64_t)agent * p.stride;
+    const float* W1 = P;
+    const float* B1 = W1 + (int64_t)H1 * IN;
+    const float* G1 = B1 + H1;
+    const float* BE1 = G1 + H1;
+    const float* W2 = BE1 + H1;
+    const float* B2 = W2 + (int64_t)H2 * H1;
+    const float* G2 = B2 + H2;
+    const float* BE2 = G2 + H2;
+    const float* WMU = BE2 + H2;
+    const float* BMU = WMU + 2 * H2;
+
+    // LDS: fc1 rows [H1][INP], (b1, g1, be1, 0) [H1], observation rows [64][INP], row statistics, reductions
+    float* sW1 = reinterpret_cast<float*>(smem4);
+    float4* sQ = reinterpret_cast<float4*>(sW1 + H1 * INP);
+    float* sX = reinterpret_cast<float*>(sQ + H1);
+    float* sMean = sX + kTM * INP;
+    float* sRstd = sMean + kTM;
+    float* sRed = sRstd + kTM;      // [64][2]
+    float* sMu = sRed + 2 * kTM;    // [64][2 halves][2]
+
+    for (int e = tid; e < H1 * INP; e += 256) {
+        const int k = e / INP, i = e - k * INP;
+        sW1[e] = i < IN ? W1[k * IN + i] : 0.0f;
+    }
+    for (int k = tid; k < H1; k += 256) sQ[k] = make_float4(B1[k], G1[k], BE1[k], 0.0f);
+    for (int e = tid; e < kTM * INP; e += 256) {
+        const int r = e / INP, i = e - r * INP;
+        const int64_t gr = r0 + r;
+        sX[e] = (i < IN && gr < p.rows) ? p.obs[(gr * p.A + agent) * IN + i] : 0.0f;
+    }
+    __syncthreads();
+
+    // fc1 output of a row at k: the bias plus the dot product with the row's observation (an fma chain)
+    auto fc1 = [&](const float* x, int k) {
+        const float* wk = sW1 + k * INP;
+        float d = sQ[k].x;
+        if (INC == 4) {
+            const float4 w4 = *reinterpret_cast<const float4*>(wk);
+            d = fmaf(x[0], w4.x, d);
+            d = fmaf(x[1], w4.y, d);
+            d = fmaf(x[2], w4.z, d);
+            d = fmaf(x[3], w4.w, d);
+        } else {
+            for (int i = 0; i < IN; ++i) d = fmaf(x[i], wk[i], d);
+        }
+        return d;
+    };
+    {  // LayerNorm-1 statistics: 4 threads per row (k = q mod 4), two passes, unrolled so the LDS reads pipeline
+        const int r = tid >> 2, q = tid & 3;
+        float x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = i < IN ? sX[r * INP + i] : 0.0f;
+        float s = 0.0f;
+#pragma unroll 8
+        for (int k = q; k < H1; k += 4) s += fc1(x, k);
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        const float mean = s / (float)H1;
+        float v = 0.0f;
+#pragma unroll 8
+        for (int k = q; k < H1; k += 4) {
+            const float d = fc1(x, k) - mean;
+            v = fmaf(d, d, v);
+        }
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        if (q == 0) {
+            sMean[r] = mean;
+            sRstd[r] = 1.0f / sqrtf(v / (float)H1 + 1e-5f);
+        }
+    }
+    __syncthreads();
+
+    // main loop: wave w covers rows 32 (w >> 1) .. +31 and the column half w & 1 (NT tiles of 32)
+    const int band = w >> 1, half = w & 1, kh = 4 * (l >> 5);
+    const int ra = 32 * band + (l & 31);  // the row of this lane's A values
+    float xr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) xr[i] = i < IN ? sX[ra * INP + i] : 0.0f;
+    const float sr = sRstd[ra], nmr = -sMean[ra] * sr;  // (z - mean) rstd = fma(z, rstd, -mean rstd)
+    const float* bp[NT];
+    bool bv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = 32 * (NT * half + t) + (l & 31);
+        bv[t] = col < H2;
+        bp[t] = W2 + (int64_t)(bv[t] ? col : 0) * H1 + kh;
+    }
+    f32x16 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[t][v] = 0.0f;
+    // A values of the k-step at k0: rows' fc1 -> LayerNorm -> ReLU at k0 + kh .. k0 + kh + 3
+    auto a_vals = [&](int k0, float (&a)[4]) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = k0 + kh + s;
+            const float4 q = sQ[k];
+            const float y = fmaf(fc1(xr, k), sr, nmr);
+            a[s] = fmaxf(fmaf(y, q.y, q.z), 0.0f);
+        }
+    };
+    auto mfma_step = [&](const float (&a)[4], const float4 (&bq)[NT]) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], bq[t].x, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], bq[t].y, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], bq[t].z, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], bq[t].w, acc[t], 0, 0, 0);
+    };
+    if constexpr (!STG) {  // B fragments straight from global memory, one k-step ahead
+        float4 bq[NT], bn[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            bq[t] = bv[t] ? *reinterpret_cast<const float4*>(bp[t]) : make_float4(0, 0, 0, 0);
+        for (int k0 = 0; k0 < H1; k0 += 8) {
+            if (k0 + 8 < H1) {
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    bn[t] = bv[t] ? *reinterpret_cast<const float4*>(bp[t] + k0 + 8) : make_float4(0, 0, 0, 0);
+            }
+            float a[4];
+            a_vals(k0, a);
+            mfma_step(a, bq);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bq[t] = bn[t];
+        }
+    } else {  // B staged through LDS: kKC-deep chunks of every column, coalesced 128-B row segments, next chunk in
+              // registers during this chunk's MFMAs
+        float* sB = sMu + 4 * kTM;  // [64 NT][kKC + 4]
+        constexpr int kPer = (64 * NT * kKC / 4 + 255) / 256;  // float4 per thread per chunk
+        const int ncol = 64 * NT;
+        float4 pf[kPer];
+        auto fetch = [&](int k0) {
+#pragma unroll
+            for (int i = 0; i < kPer; ++i) {
+                const int f = tid + 256 * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+                pf[i] = (col < H2 && k0 + kq < H1)
+                            ? *reinterpret_cast<const float4*>(W2 + (int64_t)col * H1 + k0 + kq)
+                            : make_float4(0, 0, 0, 0);
+            }
+        };
+        fetch(0);
+        for (int k0 = 0; k0 < H1; k0 += kKC) {
+            __syncthreads();  // the previous chunk's fragments have been read
+#pragma unroll
+            for (int i = 0; i < kPer; ++i) {
+                const int f = tid + 256 * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+                if (col < ncol) *reinterpret_cast<float4*>(sB + col * (kKC + 4) + kq) = pf[i];
+            }
+            __syncthreads();
+            if (k0 + kKC < H1) fetch(k0 + kKC);
+            const int kc = H1 - k0 < kKC ? H1 - k0 : kKC;
+            for (int ks = 0; ks < kc; ks += 8) {
+                float a[4];
+                a_vals(k0 + ks, a);
+                float4 bq[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    bq[t] = *reinterpret_cast<const float4*>(sB + (32 * (NT * half + t) + (l & 31)) * (kKC + 4) + ks + kh);
+                mfma_step(a, bq);
+            }
+        }
+    }
+
+    // epilogue. acc[t][v] of lane l: row 8 (v >> 2) + 4 (l >> 5) + (v & 3) of the band, column 32 (NT half + t) +
+    // (l & 31). z = acc + fc2.bias, LayerNorm over the fc2 valid columns, ReLU, mu head, tanh.
+    float b2[NT], g2[NT], be2[NT], wm0[NT], wm1[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = 32 * (NT * half + t) + (l & 31);
+        b2[t] = bv[t] ? B2[col] : 0.0f;
+        g2[t] = bv[t] ? G2[col] : 0.0f;
+        be2[t] = bv[t] ? BE2[col] : 0.0f;
+        wm0[t] = bv[t] ? WMU[col] : 0.0f;
+        wm1[t] = bv[t] ? WMU[H2 + col] : 0.0f;
+    }
+    auto row_of = [&](int v) { return 32 * band + 8 * (v >> 2) + 4 * (l >> 5) + (v & 3); };
+    float red[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        float s = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            acc[t][v] = acc[t][v] + b2[t];
+            s += bv[t] ? acc[t][v] : 0.0f;
+        }
+        red[v] = sum32(s);
+    }
+    if ((l & 31) == 0)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
+    __syncthreads();
+    float mean[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int r = row_of(v);
+        mean[v] = (sRed[r * 2] + sRed[r * 2 + 1]) / (float)H2;
+    }
+    __syncthreads();  // sRed is reused
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        float s = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float d = acc[t][v] - mean[v];
+            s += bv[t] ? d * d : 0.0f;
+        }
+        red[v] = sum32(s);
+    }
+    if ((l & 31) == 0)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
+    __syncthreads();
+    float m0[16], m1[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int r = row_of(v);
+        const float rstd = 1.0f / sqrtf((sRed[r * 2] + sRed[r * 2 + 1]) / (float)H2 + 1e-5f);
+        float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float h = fmaxf((acc[t][v] - mean[v]) * rstd * g2[t] + be2[t], 0.0f);
+            s0 += h * wm0[t];
+            s1 += h * wm1[t];
+        }
+        m0[v] = sum32(s0);
+        m1[v] = sum32(s1);
+    }
+    if ((l & 31) == 0)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int r = row_of(v);
+            sMu[(r * 2 + half) * 2 + 0] = m0[v];
+            sMu[(r * 2 + half) * 2 + 1] = m1[v];
+        }
+    __syncthreads();
+    if (tid < 2 * kTM) {
+        const int r = tid >> 1, j = tid & 1;
+        const int64_t gr = r0 + r;
+        if (gr < p.rows) {
+            const float mu = tanhf((sMu[(r * 2) * 2 + j] + sMu[(r * 2 + 1) * 2 + j]) + BMU[j]);
+            const int64_t e = (gr * p.A + agent) * 2 + j;
+            if (p.ou) {  // shared_critic.py choose_action: ou + theta * (0 - ou) * dt + (sigma sqrt(dt)) * z
+                const float o = p.ou[e];
+                const float drift = __fmul_rn(__fmul_rn(p.theta, __fsub_rn(0.0f, o)), p.dt);
+                const float on = __fadd_rn(__fadd_rn(o, drift), __fmul_rn(p.c, p.noise[e]));
+                p.ou[e] = on;
+                p.actions[e] = __fadd_rn(mu, on);
+            } else {
+                p.actions[e] = mu;
+            }
+        }
+    }
+}
+
+template <int NT, int INC>
+int launch_act(hipStream_t st, const ActArgs& a, size_t lds, bool stage) {
+    if (stage && lds + sizeof(float) * 64 * NT * (kKC + 4) <= 64 * 1024) {
+        lds += sizeof(float) * 64 * NT * (kKC + 4);
+        hipLaunchKernelGGL((sc_act_kernel<NT, INC, true>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
+    } else {
+        hipLaunchKernelGGL((sc_act_kernel<NT, INC, false>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
+    }
+    return launched();
+}
+
+}  // namespace
+
+extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim, int fc1, int fc2, const float* obs,
+                            const float* actors, int64_t actor_stride, float* actions, float* ou_state,
+                            const float* noise, float theta, float dt, float sigma_sqrt_dt) {
+    if (!obs || !actors || !actions || (ou_state && !noise))
+        return fail(-3, "flock_sc_act: NULL argument");
+    if (rows < 0 || n_agents < 1 || in_dim < 1 || in_dim > 16 || fc1 < 8 || (fc1 & 7) || fc2 < 1 || fc2 > 320)
+        return fail(-5, "flock_sc_act: needs 1 <= in_dim <= 16, fc1 a multiple of 8, 1 <= fc2 <= 320");
+    if (((uintptr_t)actors & 15) || (actor_stride & 3))
+        return fail(-5, "flock_sc_act: actors must be 16-B aligned with a stride that is a multiple of 4");
+    const int64_t per = (int64_t)fc1 * (in_dim + 3) + (int64_t)fc2 * (fc1 + 5) + 2;
+    if (actor_stride < per) return fail(-5, "flock_sc_act: actor_stride smaller than one actor");
+    if (rows == 0) return 0;
+    const int64_t tiles = (rows + kTM - 1) / kTM;
+    if (tiles * n_agents > 0x7fffffff) return fail(-5, "flock_sc_act: too many rows x agents");
+    ActArgs a;
+    a.obs = obs;
+    a.actors = actors;
+    a.actions = actions;
+    a.ou = ou_state;
+    a.noise = noise;
+    a.rows = rows;
+    a.stride = actor_stride;
+    a.A = n_agents;
+    a.in = in_dim;
+    a.H1 = fc1;
+    a.H2 = fc2;
+    a.tiles = (int)tiles;
+    a.theta = theta;
+    a.dt = dt;
+    a.c = sigma_sqrt_dt;
+    const int inp = (in_dim + 3) & ~3;
+    const size_t lds = sizeof(float) * ((size_t)fc1 * inp + 4 * (size_t)fc1 + kTM * inp + 2 * kTM + 2 * kTM + 4 * kTM);
+    if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
+    hipStream_t st = (hipStream_t)stream;
+    const int nt = (fc2 + 63) / 64;
+    static const bool stage = [] {  // FLOCK_ACT_STAGE=0/1: fc2.weight straight from global memory / through LDS (A/B)
+        const char* e = getenv("FLOCK_ACT_STAGE");
+        return e ? e[0] == '1' : false;
+    }();
+    if (in_dim == 4) {
+        switch (nt) {
+            case 1: return launch_act<1, 4>(st, a, lds, stage);
+            case 2: return launch_act<2, 4>(st, a, lds, stage);
+            case 3: return launch_act<3, 4>(st, a, lds, stage);
+            case 4: return launch_act<4, 4>(st, a, lds, stage);
+            default: return launch_act<5, 4>(st, a, lds, stage);
+        }
+    }
+    switch (nt) {
+        case 1: return launch_act<1, 0>(st, a, lds, stage);
+        case 2: return launch_act<2, 0>(st, a, lds, stage);
+        case 3: return launch_act<3, 0>(st, a, lds, stage);
+        case 4: return launch_act<4, 0>(st, a, lds, stage);
+        default: return launch_act<5, 0>(st, a, lds, stage);
+    }
+}

@@ -20,6 +20,8 @@
 //   flock::sc_round          shared-critic learn(): critic phase (agent_simple_shared_critic.py:118-141) and / or the
 //                            actor phase (:144-155) of two learn() calls in one set of launches
 //   flock::sc_round_adam     the Adam half of a data-parallel round (after the gradient all-reduce)
+//   flock::sc_act            shared-critic choose_action of every agent on every env row (+ the OU step), one launch
+//                            (agent_simple_shared_critic.py:92-107, ddpg_network.py:132-141, utils.py:15-18)
 #include <ATen/ATen.h>
 #include <ATen/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -640,6 +642,43 @@ void sc_prep_meta(const Tensor& agent_out, const optional<Tensor>& idx, int64_t 
     sc_prep_checks(agent_out, idx, rows);
 }
 
+// ------------------------------------------------------------------------------------------------------- sc_act
+// obs [rows, A, in] f32 contiguous; actors: the agent-major actor buffer [A * stride] (stride = numel / A);
+// actions [rows, A, 2]; ou_state / noise [rows, A, 2] (both or neither)
+void sc_act_checks(const Tensor& obs, const Tensor& actors, const Tensor& actions, const optional<Tensor>& ou,
+                   const optional<Tensor>& noise, int64_t fc1, int64_t fc2) {
+    TORCH_CHECK(ou.has_value() == noise.has_value(), "sc_act: ou_state and noise go together");
+    if (any_sym(obs, actors, actions, ou, noise)) return;
+    TORCH_CHECK(obs.dim() == 3, "sc_act: obs must be [rows, n_agents, in_dim], got ", obs.sizes());
+    const int64_t R = obs.size(0), A = obs.size(1), n = obs.size(2);
+    dense(obs, "obs", at::kFloat, obs);
+    dense(actors, "actors", at::kFloat, obs);
+    TORCH_CHECK(A >= 1 && actors.numel() % A == 0, "sc_act: actors must hold n_agents equal blocks");
+    TORCH_CHECK(n >= 1 && n <= 16 && fc1 >= 8 && fc1 % 8 == 0 && fc2 >= 1 && fc2 <= 320,
+                "sc_act: needs 1 <= in_dim <= 16, fc1 a multiple of 8, 1 <= fc2 <= 320");
+    shaped(actions, "actions", at::kFloat, {R, A, 2}, obs);
+    if (ou) {
+        shaped(*ou, "ou_state", at::kFloat, {R, A, 2}, obs);
+        shaped(*noise, "noise", at::kFloat, {R, A, 2}, obs);
+    }
+}
+void sc_act_hip(const Tensor& obs, const Tensor& actors, const Tensor& actions, const optional<Tensor>& ou,
+                const optional<Tensor>& noise, int64_t fc1, int64_t fc2, double theta, double dt,
+                double sigma_sqrt_dt) {
+    hip_only(obs, "sc_act");
+    sc_act_checks(obs, actors, actions, ou, noise, fc1, fc2);
+    const at::OptionalDeviceGuard g(obs.device());
+    rc_check(flock_sc_act(stream_of(obs), obs.size(0), (int)obs.size(1), (int)obs.size(2), (int)fc1, (int)fc2,
+                          ptr<const float>(obs), ptr<const float>(actors), actors.numel() / obs.size(1),
+                          ptr<float>(actions), ptr<float>(ou), ptr<const float>(noise), (float)theta, (float)dt,
+                          (float)sigma_sqrt_dt),
+             "flock_sc_act");
+}
+void sc_act_meta(const Tensor& obs, const Tensor& actors, const Tensor& actions, const optional<Tensor>& ou,
+                 const optional<Tensor>& noise, int64_t fc1, int64_t fc2, double, double, double) {
+    sc_act_checks(obs, actors, actions, ou, noise, fc1, fc2);
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(flock, m) {
@@ -674,6 +713,9 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         "sc_round_adam(Tensor(a!)[] learner, Tensor(b!)[] critic_job, Tensor(c!)[] actor_job, int[] dims, "
         "float[] hyper, Tensor? grad_scale) -> ()");
     m.def("sc_prep(Tensor(a!) agent_out, Tensor(b!)? idx, int rows, int seed, int counter, int agent) -> ()");
+    m.def(
+        "sc_act(Tensor obs, Tensor actors, Tensor(a!) actions, Tensor(b!)? ou_state, Tensor? noise, int fc1, int fc2, "
+        "float theta, float dt, float sigma_sqrt_dt) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(flock, CUDA, m) {
@@ -693,6 +735,7 @@ TORCH_LIBRARY_IMPL(flock, CUDA, m) {
     m.impl("sc_round", &sc_round_hip);
     m.impl("sc_round_adam", &sc_round_adam_hip);
     m.impl("sc_prep", &sc_prep_hip);
+    m.impl("sc_act", &sc_act_hip);
 }
 
 TORCH_LIBRARY_IMPL(flock, Meta, m) {
@@ -712,4 +755,5 @@ TORCH_LIBRARY_IMPL(flock, Meta, m) {
     m.impl("sc_round", &sc_round_meta);
     m.impl("sc_round_adam", &sc_round_adam_meta);
     m.impl("sc_prep", &sc_prep_meta);
+    m.impl("sc_act", &sc_act_meta);
 }

@@ -269,11 +269,35 @@ class SharedCriticLearner:
     def _stacked(self, fp, target=False):
         return {n: fp.view(fp.target if target else fp.data, n) for n in fp.shapes}
 
+    def fused_act_ok(self):
+        """The widths flock_sc_act handles (the reference's 400 / 300 / 2 among them)."""
+        return (self.n_actions == 2 and 1 <= self.input_dim <= 16 and self.fc1 % 8 == 0 and self.fc1 >= 8
+                and 1 <= self.fc2 <= 320)
+
     @torch.no_grad()
-    def choose_action(self, obs, noise=True):
+    def choose_action(self, obs, noise=True, fused=None):
         """All agents at once: obs [..., n_agents, input_dim] -> actions [..., n_agents, n_actions] (mu + OU noise,
-        agent_simple_shared_critic.py:92-107; OUActionNoiseGPU utils.py:6-26 with one process per (env, agent))."""
+        agent_simple_shared_critic.py:92-107; OUActionNoiseGPU utils.py:6-26 with one process per (env, agent)).
+        fused (default: when the widths allow): ONE flock_sc_act launch computes every agent's actor on every row
+        and the OU step (csrc/flock_act.hip); else the batched torch GEMM chain below."""
         lead = obs.shape[:-2]
+        if fused is None:
+            fused = self.fused_act_ok()
+        if fused:
+            x = obs.reshape(-1, self.n_agents, self.input_dim)
+            x = x if x.dtype == torch.float32 and x.is_contiguous() else x.float().contiguous()
+            act = torch.empty((x.shape[0], self.n_agents, 2), dtype=torch.float32, device=self.device)
+            ou = z = None
+            if noise:
+                shape = (*lead, self.n_agents, 2)
+                if self.ou_state is None or tuple(self.ou_state.shape) != shape:
+                    self.ou_state = torch.zeros(shape, dtype=torch.float32, device=self.device)
+                z = torch.randn(shape, device=self.device, generator=self.gen).view(x.shape[0], self.n_agents, 2)
+                ou = self.ou_state.view(x.shape[0], self.n_agents, 2)
+            o = self.ou
+            _ops().sc_act(x, self.actors.data, act, ou, z, self.fc1, self.fc2, float(o["theta"]), float(o["dt"]),
+                          float(o["sigma"] * math.sqrt(o["dt"])))
+            return act.view(*lead, self.n_agents, 2)
         x = obs.reshape(-1, self.n_agents, self.input_dim).transpose(0, 1)  # [A, rows, in]
         mu = actor_forward(self._stacked(self.actors), x).transpose(0, 1).reshape(*lead, self.n_agents,
                                                                                   self.n_actions)

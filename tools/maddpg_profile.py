@@ -41,3 +41,10 @@ print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=45, max_nam
 # the copies and GEMMs by input shape (where the time of aten::copy_ / mm / bmm goes)
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=40,
                                                          max_name_column_width=40, max_shapes_column_width=110))
+# every copy-like op by input shape (the layout copies between the batched GEMMs)
+rows = [e for e in prof.key_averages(group_by_input_shape=True)
+        if any(k in e.key for k in ("copy", "add", "cat", "mul", "relu", "where", "sum", "Memcpy", "fill", "zero"))]
+rows.sort(key=lambda e: -e.device_time_total)
+print("copy-like ops by input shape (device us total, calls, shapes)")
+for e in rows[:40]:
+    print(f"{e.device_time_total:10.1f} {e.count:4d}  {e.key[:40]:40s} {str(e.input_shapes)[:150]}")
