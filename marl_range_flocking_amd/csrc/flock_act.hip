@@ -389,7 +389,7 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
     const int nt = (fc2 + 63) / 64;
     static const bool stage = [] {  // FLOCK_ACT_STAGE=0/1: fc2.weight straight from global memory / through LDS (A/B)
         const char* e = getenv("FLOCK_ACT_STAGE");
-        return e ? e[0] == '1' : false;
+        return e ? e[0] == '1' : true;
     }();
     if (in_dim == 4) {
         switch (nt) {

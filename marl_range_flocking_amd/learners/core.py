@@ -114,14 +114,18 @@ class FlatParams:
             d[name] = p
         return d
 
-    def grads_into(self, loss, leaves):
+    def grads_into(self, loss, leaves, direct=()):
         """Gradients of ``loss`` w.r.t. ``leaves`` written straight into the flat grad buffer with one multi-tensor
-        copy (instead of zero-fill + one AccumulateGrad add per parameter)."""
+        copy (instead of zero-fill + one AccumulateGrad add per parameter). ``direct``: names whose gradient the
+        backward itself writes into the grad view (linear_t with grad views): neither copied nor zeroed."""
         names = list(leaves)
         grads = torch.autograd.grad(loss, [leaves[n] for n in names], allow_unused=True)
         dst, src = [], []
         for n, g in zip(names, grads):
             view = leaves[n].grad
+            if n in direct:
+                assert g is None, f"{n}: written by its backward, yet autograd produced a gradient too"
+                continue
             if g is None:
                 view.zero_()
             else:
@@ -252,6 +256,52 @@ def shared_linear(x, W, b=None):
     lead = x.shape[:-1]
     y = y.view(*lead, A, out)
     return y.movedim(-2, 0)
+
+
+class _LinearTInto(torch.autograd.Function):
+    """linear_t with its weight / bias gradients written by the backward itself into given views of the flat grad
+    buffer (one GEMM + one row sum; no gradient tensor for autograd to return and no copy into the flat buffer
+    afterwards). The shared input gets no gradient (replay rows / detached actions). Each parameter must enter ONE
+    such call per update (the backward overwrites its view)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, gW, gb):
+        ctx.save_for_backward(x)
+        ctx.g = (gW, gb)
+        return _linear_t(x, W, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        gW, gb = ctx.g
+        A, out, n_in = gW.shape
+        d2 = dy.reshape(A * out, x.shape[0])
+        torch.mm(d2, x, out=gW.view(A * out, n_in))
+        if gb is not None:
+            torch.sum(d2, 1, out=gb.view(A * out))
+        return None, None, None, None, None
+
+
+def _linear_t(x, W, b):
+    A, out, n_in = W.shape
+    W2 = W.reshape(A * out, n_in)
+    y = torch.empty((A, out, x.shape[0]), dtype=x.dtype, device=x.device)  # a base tensor (in-place safe)
+    if b is None:
+        torch.mm(W2, x.t(), out=y.view(A * out, -1))
+    else:
+        torch.addmm(b.reshape(A * out, 1), W2, x.t(), out=y.view(A * out, -1))
+    return y
+
+
+def linear_t(x, W, b=None, gW=None, gb=None):
+    """Every agent's Linear on ONE input shared by all agents, TRANSPOSED: x [rows, in], W [A, out, in], b [A, out]
+    -> y^T [A, out, rows] (contiguous) = one GEMM [A*out, in] x [in, rows] against the agent-stacked weight, so a
+    per-agent consumer reads it without a layout copy (bmm takes the transposed operand) and its weight gradient
+    [A*out, rows] x [rows, in] lands in W's own layout. gW / gb (views of the flat grad buffer): the backward writes
+    the gradients there itself (grads_into(direct=...))."""
+    if gW is not None and torch.is_grad_enabled():
+        return _LinearTInto.apply(x, W, b, gW, gb)
+    return _linear_t(x, W, b)
 
 
 def blayer_norm(x, w, b, eps=1e-5):

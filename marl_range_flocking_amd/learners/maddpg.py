@@ -33,7 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, ReplayRing, _ops, blinear, capture_graph, gru_cell, gru_seq, shared_linear
+from .core import FlatParams, ReplayRing, _ops, blinear, capture_graph, gru_cell, gru_seq, linear_t, shared_linear
 
 HR = 32  # hidden_rnn (net.py:15,100)
 
@@ -136,15 +136,18 @@ def actor_seq(P, x, keep):
     return gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep)
 
 
-def critic_seq(P, x, keep):
+def critic_seq(P, x, keep, G=None):
     """The recurrent critics' GRU over a whole chunk: x [C,B,N*k] shared by every critic, keep [C,A,B] ->
-    (hidden outputs [A,C,B,32], fce outputs [A,C,B,32]). fce is one GEMM [C*B, N*k] x [N*k, A*32] for every agent
-    and step (its weight gradient one GEMM too), the GRU input GEMM one batched GEMM, the recurrence one gru_seq."""
+    (hidden outputs [A,C,B,32], fce outputs [A,C,B,32] (a transposed view)). fce is one GEMM [A*32, N*k] x
+    [N*k, C*B] for every agent and step (linear_t; its weight gradient one GEMM, written into G's views when given),
+    the GRU input GEMM one batched GEMM reading it transposed, the recurrence one gru_seq."""
     C, B, _ = x.shape
-    fx = shared_linear(x, P["fce.weight"], P["fce.bias"])               # [A, C, B, 32] (a permuted view)
-    A = fx.shape[0]
-    gi = blinear(fx.reshape(A, C * B, HR), P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, 3 * HR)
-    return gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep), fx
+    G = G or {}
+    fxT = linear_t(x.reshape(C * B, -1), P["fce.weight"], P["fce.bias"], G.get("fce.weight"), G.get("fce.bias"))
+    A = fxT.shape[0]
+    fx = fxT.transpose(1, 2)                                            # [A, C*B, 32], no copy
+    gi = blinear(fx, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, 3 * HR)
+    return gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep), fx.view(A, C, B, HR)
 
 
 def critic_gru(P, fx, h):
@@ -152,11 +155,16 @@ def critic_gru(P, fx, h):
     return gru_cell(fx, h, P["gru.weight_ih"], P["gru.weight_hh"], P["gru.bias_ih"], P["gru.bias_hh"])
 
 
-def critic_head(P, y, a):
+def critic_head(P, y, a, G=None):
     """fc2(cat([y, a])) -> ReLU -> fc3: y [A,B,h1] (post-ReLU fc1 output), a [B,2N] shared -> q [A,B,1].
-    fc2 runs as its two column blocks, y @ W_h^T + b + a @ W_a^T (same math, no [A,B,h1+2N] concat)."""
-    z = blinear(y, P["fc2.weight_h"], P["fc2.bias"]) + shared_linear(a, P["fc2.weight_a"])
-    return blinear(F.relu(z), P["fc3.weight"], P["fc3.bias"])
+    fc2 runs as its two column blocks (same math, no [A,B,h1+2N] concat), TRANSPOSED so that no GEMM output needs
+    a layout copy: z^T [A,h2,B] = W_a a^T + b (one GEMM over every agent, linear_t; gradients into G's views when
+    given) + W_h y^T (batched, in place), q^T [A,1,B] = W3 ReLU(z^T) + b3."""
+    G = G or {}
+    zT = linear_t(a, P["fc2.weight_a"], P["fc2.bias"], G.get("fc2.weight_a"), G.get("fc2.bias"))
+    zT = zT.baddbmm_(P["fc2.weight_h"], y.transpose(1, 2))
+    qT = torch.baddbmm(P["fc3.bias"].unsqueeze(-1), P["fc3.weight"], F.relu(zT))
+    return qT.transpose(1, 2)
 
 
 def critic_forward(P, x, a, h, recurrent):
@@ -329,6 +337,13 @@ class MADDPGLearner:
                                       store_done=True)
 
     # ---------------------------------------------------------------- update
+    @staticmethod
+    def _direct_grads(Pc, names=("fce.weight", "fce.bias", "fc2.weight_a", "fc2.bias")):
+        """The critic parameters whose shared-input GEMMs (linear_t) write their gradients straight into the flat
+        grad buffer: the two largest blocks (fce [A,32,N*k], fc2's action block [A,h2,2N]: ~85 % of the critic
+        parameters at config 5) and their biases. Each enters exactly one linear_t call per update."""
+        return {n: Pc[n].grad for n in names if n in Pc}
+
     def _update(self):
         self._fwd_bwd()
         self._step()
@@ -363,7 +378,8 @@ class MADDPGLearner:
                 y_ta = actor_seq(Pta, AS2, keep)[:, last]
                 y_tc = critic_seq(Ptc, S2, keep)[0][:, last]
                 y_a = actor_seq(Pa, AS, keep)[:, last]
-            hs_c, fx = critic_seq(Pc, S, keep)
+            G = self._direct_grads(Pc)
+            hs_c, fx = critic_seq(Pc, S, keep, G)
             y_c = hs_c[:, last]                                             # the heads see the pre-reset state
             h_c = torch.where(keep[last].unsqueeze(-1), y_c, 0.0)
             with torch.no_grad():
@@ -374,9 +390,10 @@ class MADDPGLearner:
             # the critic-loss head share one pass over a 2B batch
             h_aq = critic_gru(Pc, fx[:, last], h_c)
             y = F.relu(blinear(torch.cat([y_c, h_aq], 1), Pc["fc1.weight"], Pc["fc1.bias"]))
-            qq = critic_head(Pc, y, torch.cat([act[last], cpa], 0))
+            qq = critic_head(Pc, y, torch.cat([act[last], cpa], 0), G)
             q, aq = qq[:, :B], qq[:, B:]
         else:  # maddpg_official/MADDPG.py:67-108 (C == 1)
+            G = self._direct_grads(Pc, ("fc2.weight_a", "fc2.bias"))
             zero = torch.zeros((N, B, HR), device=self.device)
             with torch.no_grad():
                 ta, _ = actor_forward(Pta, AS2[:, 0], zero, False)
@@ -384,14 +401,14 @@ class MADDPGLearner:
                 pa, _ = actor_forward(Pa, AS[:, 0], zero, False)
                 cpa = pa.transpose(0, 1).reshape(B, 2 * N)
             y = F.relu(shared_linear(S[0], Pc["fc1.weight"], Pc["fc1.bias"]))
-            qq = critic_head(Pc, torch.cat([y, y], 1), torch.cat([act[0], cpa], 0))
+            qq = critic_head(Pc, torch.cat([y, y], 1), torch.cat([act[0], cpa], 0), G)
             q, aq = qq[:, :B], qq[:, B:]
         r = R[:, last].t().unsqueeze(-1)
         d = D[:, last].t().unsqueeze(-1)
         target = r + self.gamma * tq * (1 - d)                                  # MADDPG.py:135
         critic_loss = ((target - q) ** 2).mean(dim=(1, 2))                      # F.mse_loss per agent (:136)
         actor_loss = -aq.mean(dim=(1, 2))
-        self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc)
+        self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc, direct=G)
         with torch.no_grad():
             self.losses[0].copy_(critic_loss.detach().mean())
             self.losses[1].copy_(actor_loss.detach().mean())
@@ -444,19 +461,20 @@ class MADDPGLearner:
             cpa = heads[1].transpose(0, 1).reshape(Bu, 2 * self.N)
             y_tc = critic_seq(Ptc, U["S2"], keep)[0][:, last]
             tq = critic_head(Ptc, F.relu(blinear(y_tc, Ptc["fc1.weight"], Ptc["fc1.bias"])), cta)
-        hs_c, fx = critic_seq(Pc, U["S"], keep)
+        G = self._direct_grads(Pc)
+        hs_c, fx = critic_seq(Pc, U["S"], keep, G)
         y_c = hs_c[:, last]
         h_c = torch.where(keep[last].unsqueeze(-1), y_c, 0.0)
         h_aq = critic_gru(Pc, fx[:, last], h_c)
         y = F.relu(blinear(torch.cat([y_c, h_aq], 1), Pc["fc1.weight"], Pc["fc1.bias"]))
-        qq = critic_head(Pc, y, torch.cat([U["act"][last], cpa], 0))
+        qq = critic_head(Pc, y, torch.cat([U["act"][last], cpa], 0), G)
         q, aq = qq[:, :Bu], qq[:, Bu:]
         r = U["R"][:, last, lo:hi].t().unsqueeze(-1)
         d = U["D"][:, last, lo:hi].t().unsqueeze(-1)
         target = r + self.gamma * tq * (1 - d)                                  # MADDPG.py:135
         critic_loss = ((target - q) ** 2).mean(dim=(1, 2))
         actor_loss = -aq.mean(dim=(1, 2))
-        self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc)
+        self.critics.grads_into(critic_loss.sum() + actor_loss.sum(), Pc, direct=G)
         self.critics.adam_step_dev(self.critic_lr, tau=self.tau, target_mode=0)
         for n in self.actors.shapes:  # the target actors of this rank's agents (mode 0, as _step)
             t, p_ = self.actors.view(self.actors.target, n)[lo:hi], self.actors.view(self.actors.data, n)[lo:hi]
