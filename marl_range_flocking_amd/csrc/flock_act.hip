@@ -127,28 +127,28 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
         }
         return d;
     };
-    {  // LayerNorm-1 statistics: 4 threads per row (k = q mod 4), two passes, unrolled so the LDS reads pipeline
+    {  // LayerNorm-1 statistics: 4 threads per row (k = q mod 4), one pass over z - c with c = z(k = 0) of the row
+       // (a shift inside the row's spread: mean = c + S1 / n, var = S2 / n - (S1 / n)^2 without cancellation)
         const int r = tid >> 2, q = tid & 3;
         float x[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = i < IN ? sX[r * INP + i] : 0.0f;
-        float s = 0.0f;
-#pragma unroll 8
-        for (int k = q; k < H1; k += 4) s += fc1(x, k);
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        const float mean = s / (float)H1;
-        float v = 0.0f;
+        const float c = fc1(x, 0);
+        float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll 8
         for (int k = q; k < H1; k += 4) {
-            const float d = fc1(x, k) - mean;
-            v = fmaf(d, d, v);
+            const float d = fc1(x, k) - c;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
         }
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
         if (q == 0) {
-            sMean[r] = mean;
-            sRstd[r] = 1.0f / sqrtf(v / (float)H1 + 1e-5f);
+            const float dm = s1 / (float)H1;
+            sMean[r] = c + dm;
+            sRstd[r] = 1.0f / sqrtf(fmaxf(s2 / (float)H1 - dm * dm, 0.0f) + 1e-5f);
         }
     }
     __syncthreads();
@@ -276,13 +276,13 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
     __syncthreads();
+    // the LayerNorm-2 statistics once per row (64 threads), not per lane and accumulator row
+    float* sStat = sMean;  // [64] mean, then [64] rstd in sRstd (LayerNorm-1's are no longer read)
+    if (tid < kTM) sStat[tid] = (sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2;
+    __syncthreads();
     float mean[16];
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        const int r = row_of(v);
-        mean[v] = (sRed[r * 2] + sRed[r * 2 + 1]) / (float)H2;
-    }
-    __syncthreads();  // sRed is reused
+    for (int v = 0; v < 16; ++v) mean[v] = sStat[row_of(v)];
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
         float s = 0.0f;
@@ -297,11 +297,12 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
     __syncthreads();
+    if (tid < kTM) sRstd[tid] = 1.0f / sqrtf((sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2 + 1e-5f);
+    __syncthreads();
     float m0[16], m1[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
-        const int r = row_of(v);
-        const float rstd = 1.0f / sqrtf((sRed[r * 2] + sRed[r * 2 + 1]) / (float)H2 + 1e-5f);
+        const float rstd = sRstd[row_of(v)];
         float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
