@@ -673,19 +673,6 @@ constexpr int kFwdKC = 200;   // forward / input-gradient GEMM K chunk (FLOCK_GE
 constexpr int kGradKC = 128;  // the gradient kernels share one launch with ~400 LDS-free reduction blocks: a 34-KB
                               // panel keeps 4 blocks per CU resident so the whole grid runs in one round
 constexpr int kPitch = 33;
-// fc1 source of a forward GEMM whose A operand (fc1 -> LayerNorm -> ReLU of the input rows) is computed inside the
-// GEMM block itself: the round's first row launch (c1 / a1) folded into the forward GEMM (sc_gemm_fc1)
-struct Fc1Src {
-    const float* x;      // input rows x[row(r) * in + i]
-    const int64_t* idx;  // row(r) = idx[r], or r when NULL
-    const float* net;    // the network's fc1 block [W1 (H1 x in), b1, g1, be1] (+ relB * agent, as B)
-    int in;
-    float *XH, *H, *RS;  // LayerNorm-1 xhat / ReLU output / rstd rows for the backward (column-tile-0 blocks), or NULL
-    // the critic phase's minibatch rows (critic-on-s problem, column-tile-0 blocks): S, S2, A, R, T of ring rows idx[r]
-    float *S, *S2, *A, *R, *T;
-    const float *rs2, *ra, *rr, *rt;
-    int na;
-};
 struct GemmP {
     const float* A;
     const float* B;
@@ -696,7 +683,6 @@ struct GemmP {
     const int64_t* agent;
     int tiles_n, tiles;
     int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
-    Fc1Src f;    // f.net != NULL: A is computed from f (sc_gemm_fc1), not read
 };
 constexpr int kMaxBatch = 5;  // a round's forward GEMMs: 3 (critic phase) + 2 (actor phase)
 struct GemmBatch {
@@ -956,191 +942,6 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
         if (m < g.M && n < g.N) st_out(g.C + (int64_t)m * g.ldc + n, g.bias ? out[q] + bias : out[q]);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// Forward fc2 GEMM with the round's fc1 row launch folded in (sc_gemm_fc1). Per 32 x 32 output tile the block stages
-// the network's fc1 block (W1, b1, g1, be1: 11 KB at fc1 400, in 4) and its 32 input rows next to the first fc2.weight
-// panel fetch, forms the rows' LayerNorm-1 statistics (8 threads per row, two passes), and then computes every A
-// operand of its MFMAs in registers: a = ReLU(xhat g1 + be1), xhat = (z - mean) rstd, z = W1 x + b1 (the c1 / a1
-// formulas; only the statistics' summation order differs from the row kernels). Each block thus reads ~38 KB instead
-// of a 26-KB A panel per K chunk plus its own launch. The column-tile-0 blocks also write what the backward needs
-// (xhat, h, rstd rows) and, for the critic-on-s problem, the minibatch rows (S, S2, A, R, T).
-template <int INC>
-struct Fc1Row {  // one input row in registers (INC = 4) or in LDS (generic in)
-    float x[INC ? INC : 1];
-    const float* xs;
-    int in;
-    __device__ __forceinline__ void load(const float* row, int n) {
-        xs = row;
-        in = n;
-        if (INC)
-#pragma unroll
-            for (int i = 0; i < (INC ? INC : 1); ++i) x[i] = row[i];
-    }
-    // z = sum_i x_i W1[k][i] (an fmaf chain) + b1[k], as fc1_ln_relu
-    __device__ __forceinline__ float z(const float* img, int H1, int k) const {
-        float v = 0.0f;
-        if (INC) {
-            const float* w = img + k * (INC ? INC : 1);
-#pragma unroll
-            for (int i = 0; i < (INC ? INC : 1); ++i) v = fmaf(x[i], w[i], v);
-        } else {
-            const float* w = img + k * in;
-            for (int i = 0; i < in; ++i) v = fmaf(xs[i], w[i], v);
-        }
-        return v + img[H1 * (INC ? INC : in) + k];
-    }
-};
-
-template <int NF, int INC>
-__global__ __launch_bounds__(256) void sc_gemm_fc1(GemmBatch gb) {
-    SC_PROF(1);
-    SC_PRIO();
-    extern __shared__ float4 smem4[];
-    float* smem = reinterpret_cast<float*>(smem4);
-    const GemmP& g = gb.p[blockIdx.y];
-    if ((int)blockIdx.x >= g.tiles) return;
-    const int t = xcd_tile(blockIdx.x, g.tiles);
-    const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    const int64_t rel = g.relB ? g.relB * (*g.agent) : 0;
-    const Fc1Src& f = g.f;
-    const int in = INC ? INC : f.in, H1 = g.K;
-    const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-    const int kcmax = gemm_kc(g.K, g.kchunk);
-    // LDS: [B panel | the 4 partial tiles after the MFMAs] [fc1 image H1 (in + 3)] [x rows 32 x in] [mean, rstd 32 x 2]
-    const int pan = kcmax * kPitch > 4 * 16 * 64 ? kcmax * kPitch : 4 * 16 * 64;
-    float* Bs = smem;
-    float* red = smem;
-    float* img = smem + round4(pan);
-    float* xs = img + round4(H1 * (in + 3));
-    float* st = xs + round4(32 * in);
-    const float* Bp = g.B + rel;
-
-    int kc = gemm_kc(g.K, g.kchunk);
-    float4 vb[NF];
-    panel_fetch<0, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, 0, kc);
-    for (int e = tid; e < 32 * in; e += 256) {
-        const int r = e / in, i = e - r * in, row = tm * kT + r;
-        xs[e] = row < g.M ? f.x[(f.idx ? f.idx[row] : (int64_t)row) * in + i] : 0.0f;
-    }
-    stage(img, f.net + rel, H1 * (in + 3));
-    __syncthreads();
-    {  // LayerNorm-1 statistics of the tile's rows: 8 threads per row, k = q mod 8, two passes
-        const int r = tid >> 3, q = tid & 7;
-        Fc1Row<INC> xr;
-        xr.load(xs + r * in, in);
-        float s1 = 0.0f;
-        for (int k = q; k < H1; k += 8) s1 += xr.z(img, H1, k);
-        s1 += __shfl_xor(s1, 1);
-        s1 += __shfl_xor(s1, 2);
-        s1 += __shfl_xor(s1, 4);
-        const float mean = s1 / (float)H1;
-        float s2 = 0.0f;
-        for (int k = q; k < H1; k += 8) {
-            const float d = xr.z(img, H1, k) - mean;
-            s2 = fmaf(d, d, s2);
-        }
-        s2 += __shfl_xor(s2, 1);
-        s2 += __shfl_xor(s2, 2);
-        s2 += __shfl_xor(s2, 4);
-        if (q == 0) {
-            st[2 * r] = mean;
-            st[2 * r + 1] = rsqrt_rn(s2 / (float)H1 + kLnEps);
-        }
-    }
-    __syncthreads();
-    const float* g1 = img + H1 * (in + 1);
-    const float* be1 = g1 + H1;
-    const int ra = l & 31;
-    Fc1Row<INC> xa;
-    xa.load(xs + ra * in, in);
-    const float amean = st[2 * ra], arstd = st[2 * ra + 1];
-    auto aval = [&](int k) {  // the A operand (row ra, column k): ReLU(LN1(fc1(x))) as fc1_ln_relu
-        const float xh = (xa.z(img, H1, k) - amean) * arstd;
-        return relu(fmaf(xh, g1[k], be1[k]));
-    };
-    f32x16 acc;
-#pragma unroll
-    for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
-    for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
-        panel_store<0, NF>(Bs, vb, kc);
-        __syncthreads();
-        const int k1 = k0 + g.kchunk, kc1 = k1 < g.K ? gemm_kc(g.K - k1, g.kchunk) : 0;
-        if (k1 < g.K) panel_fetch<0, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k1, kc1);
-        const int kq = kc >> 2;  // multiple of 2; this wave's K slice of the chunk: [wv kq, (wv + 1) kq)
-        const int kb = k0 + wv * kq + (l >> 5);
-        const float* b = Bs + (wv * kq + (l >> 5)) * kPitch + (l & 31);
-        int kk = 0;
-        for (; kk + 16 <= kq; kk += 16) {
-            float av[8], bv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int k = kb + kk + 2 * u;
-                av[u] = k < g.K ? aval(k) : 0.0f;
-                bv[u] = b[(kk + 2 * u) * kPitch];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
-        }
-        for (; kk < kq; kk += 2) {
-            const int k = kb + kk;
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(k < g.K ? aval(k) : 0.0f, b[kk * kPitch], acc, 0, 0, 0);
-        }
-        __syncthreads();
-        kc = kc1;
-    }
-#pragma unroll
-    for (int v = 0; v < 16; ++v) red[(wv * 16 + v) * 64 + l] = acc[v];
-    __syncthreads();
-    const int n = tn * kT + (l & 31);
-    const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int v = 4 * wv + q;
-        const float o = ((red[(0 * 16 + v) * 64 + l] + red[(1 * 16 + v) * 64 + l]) + red[(2 * 16 + v) * 64 + l]) +
-                        red[(3 * 16 + v) * 64 + l];
-        const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-        if (m < g.M && n < g.N) st_out(g.C + (int64_t)m * g.ldc + n, g.bias ? o + bias : o);
-    }
-    if (tn != 0) return;
-    // column-tile-0 blocks: the LayerNorm-1 rows of the backward and the critic phase's minibatch rows
-    if (f.XH || f.H) {
-        const int r = tid >> 3, q = tid & 7, row = tm * kT + r;
-        if (row < g.M) {
-            Fc1Row<INC> xr;
-            xr.load(xs + r * in, in);
-            const float mean = st[2 * r], rstd = st[2 * r + 1];
-            for (int k = q; k < H1; k += 8) {
-                const float xh = (xr.z(img, H1, k) - mean) * rstd;
-                if (f.XH) st_out(f.XH + (int64_t)row * H1 + k, xh);
-                if (f.H) st_out(f.H + (int64_t)row * H1 + k, relu(fmaf(xh, g1[k], be1[k])));
-            }
-            if (f.RS && q == 0) f.RS[row] = rstd;
-        }
-    }
-    if (f.S) {
-        for (int e = tid; e < 32 * in; e += 256) {
-            const int r = e / in, i = e - r * in, row = tm * kT + r;
-            if (row < g.M) {
-                const int64_t ir = f.idx ? f.idx[row] : row;
-                f.S[(int64_t)row * in + i] = xs[e];
-                f.S2[(int64_t)row * in + i] = f.rs2[ir * in + i];
-            }
-        }
-        for (int e = tid; e < 32 * f.na; e += 256) {
-            const int r = e / f.na, o = e - r * f.na, row = tm * kT + r;
-            if (row < g.M) f.A[(int64_t)row * f.na + o] = f.ra[(f.idx ? f.idx[row] : (int64_t)row) * f.na + o];
-        }
-        if (tid < 32) {
-            const int row = tm * kT + tid;
-            if (row < g.M) {
-                const int64_t ir = f.idx ? f.idx[row] : row;
-                f.R[row] = f.rr[ir];
-                f.T[row] = f.rt[ir];
-            }
-        }
     }
 }
 
@@ -1554,26 +1355,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
     g.kchunk = balanced_kc(K, fwd_kc());
-    g.f = Fc1Src{};
     return g;
-}
-
-// fc1 folded into the forward GEMMs (sc_gemm_fc1, the default); FLOCK_SC_FC1_GEMM=0 (read once) keeps the separate
-// c1 / a1 row launch (A/B diagnostics)
-bool fc1_in_gemm() {
-    static const bool on = [] {
-        const char* e = getenv("FLOCK_SC_FC1_GEMM");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-Fc1Src fc1_src(const float* x, const int64_t* idx, const float* net, int in) {
-    Fc1Src f{};
-    f.x = x;
-    f.idx = idx;
-    f.net = net;
-    f.in = in;
-    return f;
 }
 
 // panel-loader variant for an operand X(r, k) = X[r*sr + k*sk] with R rows (see load_panel); rel: agent stride
@@ -1635,50 +1417,6 @@ int launch_gemm(hipStream_t st, const GemmBatch& gb) {
         case 1: return launch_gemm_nf<0, 1>(st, gb, grid, lds, nf);
         case 2: return launch_gemm_nf<1, 1>(st, gb, grid, lds, nf);
         default: return launch_gemm_v<2, 2, 16>(st, gb, grid, lds);
-    }
-}
-
-// the forward batch can run as sc_gemm_fc1: every problem has an fc1 source, B k-contiguous (panel variant 0)
-bool fc1_gemm_ok(const GemmBatch& gb) {
-    for (int i = 0; i < gb.n; ++i) {
-        const GemmP& g = gb.p[i];
-        if (!g.f.net || panel_variant(g.B, g.N, g.K, g.sbn, g.sbk, g.relB) != 0 || g.f.in > kMaxIn ||
-            g.K != gb.p[0].K || g.f.in != gb.p[0].f.in)
-            return false;
-    }
-    return gb.n > 0;
-}
-template <int NF, int INC>
-int launch_gemm_fc1_v(hipStream_t st, const GemmBatch& gb, dim3 grid, size_t lds) {
-    if (int rc = allow_lds(sc_gemm_fc1<NF, INC>, lds)) return rc;
-    hipLaunchKernelGGL((sc_gemm_fc1<NF, INC>), grid, dim3(256), lds, st, gb);
-    return launched();
-}
-int launch_gemm_fc1(hipStream_t st, const GemmBatch& gb) {
-    int kc = 8, tiles = 0;
-    for (int i = 0; i < gb.n; ++i) {
-        const int c = gemm_kc(gb.p[i].K, gb.p[i].kchunk);
-        kc = c > kc ? c : kc;
-        tiles = gb.p[i].tiles > tiles ? gb.p[i].tiles : tiles;
-    }
-    const int H1 = gb.p[0].K, in = gb.p[0].f.in;
-    const int pan = kc * kPitch > 4 * 16 * 64 ? kc * kPitch : 4 * 16 * 64;
-    const size_t lds = (size_t)(round4(pan) + round4(H1 * (in + 3)) + round4(32 * in) + 64) * sizeof(float);
-    const dim3 grid(tiles, gb.n);
-    const int nf = nf_of(kc);
-    if (in == 4) {
-        switch (nf) {
-            case 4: return launch_gemm_fc1_v<4, 4>(st, gb, grid, lds);
-            case 7: return launch_gemm_fc1_v<7, 4>(st, gb, grid, lds);
-            case 10: return launch_gemm_fc1_v<10, 4>(st, gb, grid, lds);
-            default: return launch_gemm_fc1_v<16, 4>(st, gb, grid, lds);
-        }
-    }
-    switch (nf) {
-        case 4: return launch_gemm_fc1_v<4, 0>(st, gb, grid, lds);
-        case 7: return launch_gemm_fc1_v<7, 0>(st, gb, grid, lds);
-        case 10: return launch_gemm_fc1_v<10, 0>(st, gb, grid, lds);
-        default: return launch_gemm_fc1_v<16, 0>(st, gb, grid, lds);
     }
 }
 
@@ -1829,16 +1567,6 @@ void critic_job(const FlockScUpdate* u, Job& j) {
     j.fwd[2] = gemm_p(w.H1, u->critic + co.W2, w.Z2 + 2 * (int64_t)B * H2, u->critic + co.b2, B, H2, H1, H1, 1, 1,
                       H1, H2, 0);
     j.nfwd = 3;
-    // fc1 of each path inside its GEMM (the c1 launch's work): s' rows for the target actor and critic(s'), s rows
-    // for critic(s), which also writes the LayerNorm-1 rows of the backward and the minibatch rows
-    j.fwd[0].f = fc1_src(u->ring_new_state, u->idx, u->actors_target, in);
-    j.fwd[1].f = fc1_src(u->ring_new_state, u->idx, u->critic, in);
-    Fc1Src& f2 = j.fwd[2].f;
-    f2 = fc1_src(u->ring_state, u->idx, u->critic, in);
-    f2.XH = w.XH1; f2.H = w.H1; f2.RS = w.RS1;
-    f2.S = w.S; f2.S2 = w.S2; f2.A = w.A; f2.R = w.R; f2.T = w.T;
-    f2.rs2 = u->ring_new_state; f2.ra = u->ring_action; f2.rr = u->ring_reward; f2.rt = u->ring_terminal;
-    f2.na = na;
     BwdJob& bw = j.bw;
     bwd_common(j, u->critic + co.W2, 0, u->agent, w.H1, w.XH1, u->critic + co.g1, w.DY1, w.DXH1, w.PS1, w.DZ2, co.W2,
                u->critic_grad, 0, u->losses + 1);
@@ -1885,12 +1613,6 @@ void actor_job(const FlockScUpdate* u, Job& j) {
     j.fwd[1] = gemm_p(w.CH1, critic + co.W2, w.Z2b + (int64_t)B * H2, critic + co.b2, B, H2, H1, H1, 1, 1, H1, H2,
                       0);
     j.nfwd = 2;
-    // fc1 inside the GEMMs (the a1 launch's work) on the critic phase's minibatch rows S: the actor path also writes
-    // its LayerNorm-1 rows for the backward
-    Fc1Src& f0 = j.fwd[0].f;
-    f0 = fc1_src(w.S, nullptr, u->actors, in);
-    f0.XH = w.AXH1; f0.H = w.AH1; f0.RS = w.ARS1;
-    j.fwd[1].f = fc1_src(w.S, nullptr, critic, in);
     BwdJob& bw = j.bw;
     bwd_common(j, u->actors + ao.W2, u->actor_stride, u->agent, w.AH1, w.AXH1, u->actors + ao.g1, w.ADY1, w.ADXH1,
                w.APS1, w.ADZ2, ao.W2, u->actors_grad, u->actor_stride, u->losses);
@@ -1971,16 +1693,7 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
         return fail(-5, "flock_sc_round: the two updates must have the same shapes");
     const int C = A.C, rb = A.rb;
     int rc = 0;
-    GemmBatch gb;
-    gb.n = 0;
-    if (jc)
-        for (int i = 0; i < jc->nfwd; ++i) gb.p[gb.n++] = jc->fwd[i];
-    if (ja)
-        for (int i = 0; i < ja->nfwd; ++i) gb.p[gb.n++] = ja->fwd[i];
-    const bool fused = fc1_in_gemm() && fc1_gemm_ok(gb);
-    if (fused) {  // 1 + 2: the forward GEMMs with fc1 computed inside (no row launch)
-        if ((rc = launch_gemm_fc1(st, gb))) return rc;
-    } else {  // 1: fc1 rows
+    {  // 1: fc1 rows
         const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
         const size_t lds = zmax(A.lds1, Z.lds1);
         const dim3 grid(rb, npc + npa);
@@ -1992,8 +1705,14 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
                         hipLaunchKernelGGL((sc_k1<CC, 0>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a))
         }
         if ((rc = launched())) return rc;
-        // 2: forward fc2 GEMMs (their A rows written by the row launch)
-        for (int i = 0; i < gb.n; ++i) gb.p[i].f = Fc1Src{};
+    }
+    {  // 2: forward fc2 GEMMs
+        GemmBatch gb;
+        gb.n = 0;
+        if (jc)
+            for (int i = 0; i < jc->nfwd; ++i) gb.p[gb.n++] = jc->fwd[i];
+        if (ja)
+            for (int i = 0; i < ja->nfwd; ++i) gb.p[gb.n++] = ja->fwd[i];
         if ((rc = launch_gemm(st, gb))) return rc;
     }
     {  // 3: heads, losses, backward to the fc2 pre-activation
