@@ -691,9 +691,8 @@ constexpr int clog2c(int n) {
 // candidates [q N / SPL, (q + 1) N / SPL) for agent (t mod N), and the agents' lanes merge the SPL partial top-L
 // key lists through LDS (the same key set, hence the same result, as the one-lane scan). At N = 64 this gives 4x the
 // waves of one lane per agent, where one wave per SIMD left every latency exposed.
-// step_body: the step of env block bx (the kernel below runs it for REP env blocks in turn)
 template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1>
-__device__ __forceinline__ void step_body(const Params& pin, const int bx) {
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params pin) {
     static_assert(SPL == 1 || (NC > 0 && !CELL && (NC % (2 * SPL)) == 0), "split scans: specialised N, no cells");
     Params p = pin;
     if (VAR >= 0) p.variant = VAR;
@@ -726,7 +725,7 @@ __device__ __forceinline__ void step_body(const Params& pin, const int bx) {
     const int t = threadIdx.x;
     const int g = t / p.N;
     const int i = t - g * p.N;
-    const int env = p.env0 + bx * p.G + g;
+    const int env = p.env0 + blockIdx.x * p.G + g;
     const bool in_group = g < p.G;
     const bool active = in_group && env < p.E;
     const size_t a = (size_t)env * p.N + i;
@@ -818,7 +817,7 @@ __device__ __forceinline__ void step_body(const Params& pin, const int bx) {
     if (active && variant == FLOCK_VARIANT_UW) prev_h = p.prev_heading[a];
     if constexpr (SPL > 1 && kMemEarly) {  // split instantiation: lane groups 1..3 roll memory frames 0..2 (k = 4)
         const int q = t / NC, ia = t - q * NC;
-        const int envb = p.env0 + bx;
+        const int envb = p.env0 + (int)blockIdx.x;
         if (q >= 1 && q < kMem && envb < p.E && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
             const size_t ab = (size_t)envb * NC + ia;
             reinterpret_cast<float4*>(p.mem_out + ab * kMem * 4)[q] =
@@ -1143,7 +1142,7 @@ __device__ __forceinline__ void step_body(const Params& pin, const int bx) {
     if constexpr (SPL > 1) {  // split scan: every lane group takes 1 / SPL of the candidates, then the merge
         constexpr int Q = NC / SPL;
         const int q = t / NC, ia = t - q * NC;
-        const bool live = p.env0 + bx < p.E;
+        const bool live = p.env0 + (int)blockIdx.x < p.E;
         uint32_t part[L];
         if (live) {
             const float2 me = lpos[ia];  // published by the phase-2 barrier
@@ -1309,19 +1308,6 @@ __device__ __forceinline__ void step_body(const Params& pin, const int bx) {
     }
     PHASE(7);
     PHASE_FLUSH();
-}
-
-// REP > 1: each block steps REP env blocks in turn (bx, bx + grid, ...), so one launch of blocks/REP workgroups keeps
-// every block slot busy to the end instead of refilling slots as blocks retire (a second generation of blocks and its
-// tail). The env steps are independent; the barrier orders the reuse of the LDS arrays.
-template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1, int REP = 1>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params pin) {
-    step_body<L, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>(pin, (int)blockIdx.x);
-#pragma unroll
-    for (int r = 1; r < REP; ++r) {
-        __syncthreads();
-        step_body<L, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>(pin, (int)blockIdx.x + r * (int)gridDim.x);
-    }
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1527,15 +1513,13 @@ struct Knobs {
     int env_launches;
     bool no_spec, no_split, no_cells;
     int lds_pad;  // FLOCK_ENV_LDS_PAD: extra dynamic LDS bytes per step block (caps the blocks per CU; A/B only)
-    int rep;      // FLOCK_ENV_REP: env blocks per workgroup of the config-3 instantiation (1 or 2)
 };
 Knobs& knobs_mut() {
     static Knobs k = [] {
         const char* e = getenv("FLOCK_ENV_LAUNCHES");
         const char* lp = getenv("FLOCK_ENV_LDS_PAD");
-        const char* rp = getenv("FLOCK_ENV_REP");
         return Knobs{e ? atoi(e) : 1, getenv("FLOCK_NO_SPEC") != nullptr, getenv("FLOCK_NO_SPLIT") != nullptr,
-                     getenv("FLOCK_NO_CELLS") != nullptr, lp ? atoi(lp) : 0, rp ? atoi(rp) : 1};
+                     getenv("FLOCK_NO_CELLS") != nullptr, lp ? atoi(lp) : 0};
     }();
     return k;
 }
@@ -1546,7 +1530,7 @@ int env_launches(int blocks, int requested) {
 }
 
 // the specialised instantiations (step_kernel VAR / NC / SPL): the BASELINE configurations' per-GPU shapes
-template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1, int REP = 1>
+template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1>
 bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL ||
         p.normalize)
@@ -1563,8 +1547,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     }
     const int parts = env_launches(c.blocks, p.launches);
     if (parts <= 1) {
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, REP>), dim3((c.blocks + REP - 1) / REP),
-                           dim3(c.T), c.lds, s, p);
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks), dim3(c.T), c.lds, s,
+                           p);
         return true;
     }
     // the step as `parts` back-to-back launches over consecutive env ranges (same results: envs are independent)
@@ -1572,9 +1556,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
-        q.E = min(p.E, (b0 + per) * c.G);  // the envs of this part only (a REP block's later env block stays inside)
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, REP>),
-                           dim3((min(per, c.blocks - b0) + REP - 1) / REP), dim3(c.T), c.lds, s, q);
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
+                           dim3(c.T), c.lds, s, q);
     }
     return true;
 }
@@ -1582,9 +1565,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
 template <int L>
 void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
     if constexpr (L == 6) {
-        if (knobs().rep == 2 ? launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6, 1, 2>(c, p, s)
-                             : launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6>(c, p, s))
-            return;  // config 3
+        if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6>(c, p, s)) return;         // config 3
         if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12>(c, p, s)) return;       // config 5
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
         if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
@@ -1690,8 +1671,6 @@ int flock_set_diag(const char* name, int value) {
         k.no_split = value != 0;
     else if (!strcmp(name, "no_cells"))
         k.no_cells = value != 0;
-    else if (!strcmp(name, "env_rep"))
-        k.rep = value;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
     else

@@ -321,37 +321,6 @@ def test_env_range_launches_are_bitwise_one_launch(cuda):
             assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
 
 
-@pytest.mark.parametrize("launches", [1, 3])
-def test_two_envs_per_block_are_bitwise_one_env_per_block(launches, cuda):
-    """flock_set_diag("env_rep", 2) / FLOCK_ENV_REP=2: the config-3 instantiation steps two env blocks per workgroup
-    (bx, bx + grid). Four-step rollouts (v2, N = 256, seeds, every output; E odd, so one workgroup's second env is
-    past the end; 3 launches: each launch's last workgroup must not step the next range's first env) equal the
-    one-env-per-workgroup rollout bit for bit."""
-    k, E, N = 4, 37, 256
-    box = float(round(np.sqrt(250 * N)))
-    rng = np.random.default_rng(23)
-    pos = rng.uniform(0, box, (E, N, 2)).astype(np.float32)
-    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
-    envs = []
-    for _ in range(2):
-        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
-                                      range_start=(0, box), sensor_range=14.0, step_launches=launches), device=cuda)
-        env.set_state(positions=pos, headings=head)
-        envs.append(env)
-    for t in range(4):
-        act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32))
-        outs = []
-        for i, env in enumerate(envs):
-            with diag("env_rep", 2 if i else 1, default=1):
-                obs, rew, (done, anyd), _ = env.step(act)
-                torch.cuda.synchronize()
-            outs.append({"pos": env.positions.clone(), "vel": env.velocities.clone(), "head": env.headings.clone(),
-                         "dnn": env.dnn.clone(), "idx": env.nn_idx.clone(), "rew": rew.clone(), "done": done.clone(),
-                         "any": anyd.clone(), "seeds": env.seeds.clone() if env.seeds is not None else rew})
-        for key in outs[0]:
-            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
-
-
 @pytest.mark.parametrize("variant,periodic,N,kind", SPEC[:3], ids=[f"{v}-N{n}-{d}" for v, _, n, d in SPEC[:3]])
 def test_step_launches_are_bitwise_one_launch(variant, periodic, N, kind, cuda):
     """FlockConfig.step_launches > 1 (FlockStepExt.launches): the step as several launches over consecutive env
