@@ -37,7 +37,10 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kTM = 64;  // env rows per block (two 32-row bands)
-constexpr int kKC = 32;  // k depth of an LDS-staged fc2.weight chunk (STG)
+#ifndef FLOCK_ACT_KC
+#define FLOCK_ACT_KC 40
+#endif
+constexpr int kKC = FLOCK_ACT_KC;  // k depth of an LDS-staged fc2.weight chunk (STG; a multiple of 8)
 
 struct ActArgs {
     const float* obs;     // [rows][A][in]
@@ -127,7 +130,15 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
         }
         return d;
     };
-    {  // LayerNorm-1 statistics: 4 threads per row (k = q mod 4), one pass over z - c with c = z(k = 0) of the row
+#ifndef FLOCK_ACT_DIAG
+#define FLOCK_ACT_DIAG 0  // timing-only builds (results wrong): 1 no LN1 statistics, 2 no epilogue, 4 no B fetch
+#endif
+    if (FLOCK_ACT_DIAG & 1) {
+        if (tid < kTM) {
+            sMean[tid] = 0.0f;
+            sRstd[tid] = 1.0f;
+        }
+    } else {  // LayerNorm-1 statistics: 4 threads per row (k = q mod 4), one pass over z - c with c = z(k = 0) of the row
        // (a shift inside the row's spread: mean = c + S1 / n, var = S2 / n - (S1 / n)^2 without cancellation)
         const int r = tid >> 2, q = tid & 3;
         float x[16];
@@ -217,6 +228,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
         const int ncol = 64 * NT;
         float4 pf[kPer];
         auto fetch = [&](int k0) {
+            if (FLOCK_ACT_DIAG & 4) return;
 #pragma unroll
             for (int i = 0; i < kPer; ++i) {
                 const int f = tid + 256 * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
@@ -226,6 +238,10 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
             }
         };
         fetch(0);
+        // software-pipelined: the A values of the NEXT k-step are computed between this step's B-fragment reads and
+        // its MFMAs (independent work the scheduler interleaves with the matrix instructions)
+        float a[4];
+        a_vals(0, a);
         for (int k0 = 0; k0 < H1; k0 += kKC) {
             __syncthreads();  // the previous chunk's fragments have been read
 #pragma unroll
@@ -237,17 +253,29 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
             if (k0 + kKC < H1) fetch(k0 + kKC);
             const int kc = H1 - k0 < kKC ? H1 - k0 : kKC;
             for (int ks = 0; ks < kc; ks += 8) {
-                float a[4];
-                a_vals(k0 + ks, a);
                 float4 bq[NT];
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
                     bq[t] = *reinterpret_cast<const float4*>(sB + (32 * (NT * half + t) + (l & 31)) * (kKC + 4) + ks + kh);
+                float an[4];
+                const int kn = k0 + ks + 8;
+                a_vals(kn < H1 ? kn : 0, an);
                 mfma_step(a, bq);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = an[q];
             }
         }
     }
 
+    if (FLOCK_ACT_DIAG & 2) {  // every accumulator stays live (one sum), no LayerNorm / head
+        float sum = 0.0f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) sum += acc[t][v];
+        if (tid < 2 * kTM && r0 + (tid >> 1) < p.rows) p.actions[((r0 + (tid >> 1)) * p.A + agent) * 2 + (tid & 1)] = sum;
+        return;
+    }
     // epilogue. acc[t][v] of lane l: row 8 (v >> 2) + 4 (l >> 5) + (v & 3) of the band, column 32 (NT half + t) +
     // (l & 31). z = acc + fc2.bias, LayerNorm over the fc2 valid columns, ReLU, mu head, tanh.
     float b2[NT], g2[NT], be2[NT], wm0[NT], wm1[NT];
