@@ -55,3 +55,25 @@ def test_meta_kernels(flock):
 def test_cpu_tensors_are_refused(flock):
     with pytest.raises(NotImplementedError):
         flock.knn(torch.zeros(2, 8, 2), 4, 10.0)
+
+
+def test_sc_act_schema_meta_and_refusal(flock):
+    """flock::sc_act (choose_action of every agent, csrc/flock_act.hip): mutation annotations, Meta shape checks with
+    the op's errors, and no CPU implementation."""
+    s = str(flock.sc_act.default._schema)
+    for arg in ("Tensor obs", "Tensor actors", "Tensor(a!) actions", "Tensor(b!)? ou_state", "Tensor? noise"):
+        assert arg in s, arg
+    m = dict(device="meta")
+    obs, actors = torch.empty(10, 3, 4, **m), torch.empty(3 * 320, **m)
+    act, ou, z = torch.empty(10, 3, 2, **m), torch.empty(10, 3, 2, **m), torch.empty(10, 3, 2, **m)
+    flock.sc_act(obs, actors, act, ou, z, 16, 8, 0.2, 0.01, 0.015)
+    flock.sc_act(obs, actors, act, None, None, 16, 8, 0.2, 0.01, 0.015)
+    with pytest.raises(RuntimeError, match="actions must have shape"):
+        flock.sc_act(obs, actors, torch.empty(10, 3, 3, **m), None, None, 16, 8, 0.2, 0.01, 0.015)
+    with pytest.raises(RuntimeError, match="fc1 a multiple of 8"):
+        flock.sc_act(obs, actors, act, None, None, 12, 8, 0.2, 0.01, 0.015)
+    with pytest.raises(RuntimeError, match="ou_state and noise"):
+        flock.sc_act(obs, actors, act, ou, None, 16, 8, 0.2, 0.01, 0.015)
+    with pytest.raises(NotImplementedError):
+        flock.sc_act(torch.zeros(10, 3, 4), torch.zeros(960), torch.zeros(10, 3, 2), None, None, 16, 8, 0.2, 0.01,
+                     0.015)
