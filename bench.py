@@ -89,9 +89,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=None, help="JSON with measured HBM bytes per launch (profiles/)")
     ap.add_argument("--step-launches", type=int, default=None,
-                    help="env step as this many launches over env ranges (FlockConfig.step_launches; default: 2 "
-                         "with the overlapped shared-critic learner, whose rounds take the slots the first "
-                         "launch's tail frees; 1 otherwise)")
+                    help="env step as this many launches over env ranges (FlockConfig.step_launches; default: 3 "
+                         "with the overlapped shared-critic learner, whose rounds take the slots each launch's "
+                         "tail frees; 1 otherwise)")
     ap.add_argument("--loop", type=int, default=1, choices=[0, 1],
                     help="config 3: enqueue the timed steps (env step + learn()) through torch.classes.flock."
                          "ScTrainLoop, K steps per C++ call (bitwise the per-step path); 0: one Python call per step "
@@ -413,7 +413,7 @@ def main():
     from marl_range_flocking_amd import FlockConfig, VecFlockEnv
 
     E, N, k = args.envs, args.agents, args.k
-    launches = args.step_launches or (2 if args.learner == "shared_critic" and args.overlap else 1)
+    launches = args.step_launches or (3 if args.learner == "shared_critic" and args.overlap else 1)
     box = float(round(np.sqrt(250.0 * N)))  # main.py density: 10 agents in 50x50
     cfg = FlockConfig(variant=args.variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5,
                       range_start=(0, box), sensor_range=14.0, seed=1234 + rank,

@@ -214,6 +214,21 @@ __device__ __forceinline__ int wave_max(int v) {
                                               max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48))));
 }
 
+// unsigned min over the 64 lanes (every lane active), wave-uniform: the same DPP pattern as wave_max
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_minu(uint32_t v) {
+    return min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = dpp_minu<0xB1>(v);
+    v = dpp_minu<0x4E>(v);
+    v = dpp_minu<0x141>(v);
+    v = dpp_minu<0x140>(v);
+    const uint32_t a = min((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16));
+    const uint32_t b = min((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)min(a, b));
+}
+
 // inclusive prefix sum over the 64 lanes (every lane active): DPP row_shr 1/2/4/8 within rows of 16, then
 // row_bcast 15 / 31 across rows (lanes without a source read the 0 of `old`)
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -573,6 +588,81 @@ __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)
         for (int c = pr[cx]; c < pr[cx + 2 * kRg + 1]; ++c) {
             const float4 q = ext[c];
             insert_exact<W>(bd, bj, pair_d2<PERIODIC>(xi, yi, q.x, q.y, box), __float_as_int(q.z));
+        }
+    }
+}
+
+// The same exact rescan with the whole wave (call with every lane of the wave active; `amb` marks the lanes that need
+// it). An ambiguous lane is rare (~5e-5 of the lanes at config 3), but its serial rescan (~50 dependent LDS reads and
+// branchy insertions over rows cy-1..cy+1, columns cx-kRg..cx+kRg) held its block ~2x as long and set the launch's
+// tail (timing build without rescans: 49 -> 43 us). Here the 64 lanes take one candidate each of the ambiguous
+// lane's neighbourhood per pass and the exact (d2, j) order comes from W rounds of wave-wide minima (d2 bits, then
+// j among the lanes holding that d2): the same (d2, j) set, hence the same result, as exact_rescan_cells.
+template <int L, bool PERIODIC>
+__device__ __forceinline__ void exact_rescan_wave(float (&bd)[L - 1], int (&bj)[L - 1], bool amb,
+                                                  const float4* __restrict__ ext_all, const int* __restrict__ pre_all,
+                                                  int ecap, int npre, int g, int gx, int gy, int cx, int cy, float xi,
+                                                  float yi, float box) {
+    constexpr int W = L - 1;
+    const int W2 = gx + 2 * kRg;
+    const int lane = __lane_id();
+    uint64_t todo = __ballot(amb);
+    while (todo) {
+        const int src = __ffsll((long long)todo) - 1;
+        todo &= todo - 1;
+        const float sx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), src));
+        const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yi), src));
+        const int scx = __builtin_amdgcn_readlane(cx, src), scy = __builtin_amdgcn_readlane(cy, src);
+        const int sg = __builtin_amdgcn_readlane(g, src);  // lanes past the env (G = 1, N < 256) carry g = 1
+        const float4* ext = ext_all + sg * ecap;
+        const int* pre = pre_all + sg * npre;
+        int rs[3], rn[3];  // the three row ranges of ext (wave-uniform)
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            int yr = scy + u - 1;
+            bool row = true;
+            if (PERIODIC)
+                yr = wrap_row(yr, gy);
+            else
+                row = yr >= 0 && yr < gy;
+            const int* pr = pre + (row ? yr : 0) * W2;
+            rs[u] = row ? pr[scx] : 0;
+            rn[u] = row ? pr[scx + 2 * kRg + 1] - rs[u] : 0;
+        }
+        const int n01 = rn[0] + rn[1], total = n01 + rn[2];
+        float ud[W];
+        int uj[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            ud[w] = __builtin_inff();
+            uj[w] = 0x7fffffff;
+        }
+        for (int base = 0; base < total; base += 64) {
+            const int tt = base + lane;
+            uint32_t kd = 0xFFFFFFFFu, kj = 0xFFFFFFFFu;  // d2 >= 0: its bits order like the floats (inf < ~0u)
+            if (tt < total) {
+                const int c = tt < rn[0] ? rs[0] + tt : (tt < n01 ? rs[1] + tt - rn[0] : rs[2] + tt - n01);
+                const float4 q = ext[c];
+                kd = __float_as_uint(pair_d2<PERIODIC>(sx, sy, q.x, q.y, box));
+                kj = (uint32_t)__float_as_int(q.z);
+            }
+#pragma unroll 1
+            for (int w = 0; w < W; ++w) {
+                const uint32_t md = wave_min_u32(kd);
+                if (md == 0xFFFFFFFFu) break;
+                const uint32_t mj = wave_min_u32(kd == md ? kj : 0xFFFFFFFFu);
+                const float d = __uint_as_float(md);
+                if (!(d < ud[W - 1] || (d == ud[W - 1] && (int)mj < uj[W - 1]))) break;  // the rest cannot enter
+                insert_exact<W>(ud, uj, d, (int)mj);
+                if (kd == md && kj == mj) kd = kj = 0xFFFFFFFFu;  // taken (one lane: (d2, j) pairs are distinct)
+            }
+        }
+        if (lane == src) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                bd[w] = ud[w];
+                bj[w] = uj[w];
+            }
         }
     }
 }
@@ -1162,18 +1252,30 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
         ok = true;
     }
+    bool amb = false;
     if (active) {
         if (!ok) {
             scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, kx, ky, p.box);
             R = 0;
         }
-        const bool amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, R == 0);
+        amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, R == 0);
 #ifdef FLOCK_PHASE_PROF
         if (__ballot(amb) != 0) PHASE_COUNT(18, 1);
 #endif
-        if (CELL && amb)
+    }
+#ifdef FLOCK_DIAG_NORESCAN  // diagnostics only: timing without the exact rescans (ambiguous lanes are wrong)
+    amb = false;
+#endif
+    // cell lanes (R = 1) with an ambiguous (k+1) / (k+2) bucket: exact rescan of rows cy-1..cy+1, columns
+    // cx-kRg..cx+kRg by the whole wave (envs are wave-aligned whenever CELL; every lane of the wave is here)
+    if (CELL && __ballot(amb) != 0) {
+#ifdef FLOCK_SERIAL_RESCAN  // A/B builds: the one-lane rescan
+        if (amb)
             exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, gx, gy, cx, cy, R, x, y,
                                             p.box);
+#else
+        exact_rescan_wave<L, PERIODIC>(bd, bj, amb, ext_all, pre_all, p.ecap, npre, g, gx, gy, cx, cy, x, y, p.box);
+#endif
     }
     PHASE(5);
 
