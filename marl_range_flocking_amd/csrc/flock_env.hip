@@ -598,8 +598,11 @@ __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)
 // tail (timing build without rescans: 49 -> 43 us). Here the 64 lanes take one candidate each of the ambiguous
 // lane's neighbourhood per pass and the exact (d2, j) order comes from W rounds of wave-wide minima (d2 bits, then
 // j among the lanes holding that d2): the same (d2, j) set, hence the same result, as exact_rescan_cells.
-template <int L, bool PERIODIC>
-__device__ __forceinline__ void exact_rescan_wave(float (&bd)[L - 1], int (&bj)[L - 1], bool amb,
+// R = 0 lanes (no cell list, or a cell lane that fell back to the full scan) rescan all N agents of their env from
+// lpos the same way (knn_finalize's serial full rescan: the config-2 kernel's straggler blocks).
+template <int L, bool PERIODIC, bool CELL>
+__device__ __forceinline__ void exact_rescan_wave(float (&bd)[L - 1], int (&bj)[L - 1], bool amb, int R,
+                                                  const float2* __restrict__ lpos, int S, int N,
                                                   const float4* __restrict__ ext_all, const int* __restrict__ pre_all,
                                                   int ecap, int npre, int g, int gx, int gy, int cx, int cy, float xi,
                                                   float yi, float box) {
@@ -612,22 +615,26 @@ __device__ __forceinline__ void exact_rescan_wave(float (&bd)[L - 1], int (&bj)[
         todo &= todo - 1;
         const float sx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), src));
         const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yi), src));
-        const int scx = __builtin_amdgcn_readlane(cx, src), scy = __builtin_amdgcn_readlane(cy, src);
         const int sg = __builtin_amdgcn_readlane(g, src);  // lanes past the env (G = 1, N < 256) carry g = 1
+        const bool cells = CELL && __builtin_amdgcn_readlane(R, src) == 1;
+        const float2* cand = lpos + sg * S;
         const float4* ext = ext_all + sg * ecap;
-        const int* pre = pre_all + sg * npre;
-        int rs[3], rn[3];  // the three row ranges of ext (wave-uniform)
+        int rs[3] = {0, 0, 0}, rn[3] = {N, 0, 0};  // ext row ranges (cell lanes), else all N of lpos
+        if (cells) {
+            const int scx = __builtin_amdgcn_readlane(cx, src), scy = __builtin_amdgcn_readlane(cy, src);
+            const int* pre = pre_all + sg * npre;
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            int yr = scy + u - 1;
-            bool row = true;
-            if (PERIODIC)
-                yr = wrap_row(yr, gy);
-            else
-                row = yr >= 0 && yr < gy;
-            const int* pr = pre + (row ? yr : 0) * W2;
-            rs[u] = row ? pr[scx] : 0;
-            rn[u] = row ? pr[scx + 2 * kRg + 1] - rs[u] : 0;
+            for (int u = 0; u < 3; ++u) {
+                int yr = scy + u - 1;
+                bool row = true;
+                if (PERIODIC)
+                    yr = wrap_row(yr, gy);
+                else
+                    row = yr >= 0 && yr < gy;
+                const int* pr = pre + (row ? yr : 0) * W2;
+                rs[u] = row ? pr[scx] : 0;
+                rn[u] = row ? pr[scx + 2 * kRg + 1] - rs[u] : 0;
+            }
         }
         const int n01 = rn[0] + rn[1], total = n01 + rn[2];
         float ud[W];
@@ -641,10 +648,16 @@ __device__ __forceinline__ void exact_rescan_wave(float (&bd)[L - 1], int (&bj)[
             const int tt = base + lane;
             uint32_t kd = 0xFFFFFFFFu, kj = 0xFFFFFFFFu;  // d2 >= 0: its bits order like the floats (inf < ~0u)
             if (tt < total) {
-                const int c = tt < rn[0] ? rs[0] + tt : (tt < n01 ? rs[1] + tt - rn[0] : rs[2] + tt - n01);
-                const float4 q = ext[c];
-                kd = __float_as_uint(pair_d2<PERIODIC>(sx, sy, q.x, q.y, box));
-                kj = (uint32_t)__float_as_int(q.z);
+                if (cells) {
+                    const int c = tt < rn[0] ? rs[0] + tt : (tt < n01 ? rs[1] + tt - rn[0] : rs[2] + tt - n01);
+                    const float4 q = ext[c];
+                    kd = __float_as_uint(pair_d2<PERIODIC>(sx, sy, q.x, q.y, box));
+                    kj = (uint32_t)__float_as_int(q.z);
+                } else {
+                    const float2 q = cand[tt];
+                    kd = __float_as_uint(pair_d2<PERIODIC>(sx, sy, q.x, q.y, box));
+                    kj = (uint32_t)tt;
+                }
             }
 #pragma unroll 1
             for (int w = 0; w < W; ++w) {
@@ -1258,7 +1271,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             scan_all<L, PERIODIC>(key, lpos + g * p.S, p.N, p.ib, kx, ky, p.box);
             R = 0;
         }
-        amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, R == 0);
+        amb = knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, false);
 #ifdef FLOCK_PHASE_PROF
         if (__ballot(amb) != 0) PHASE_COUNT(18, 1);
 #endif
@@ -1266,15 +1279,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #ifdef FLOCK_DIAG_NORESCAN  // diagnostics only: timing without the exact rescans (ambiguous lanes are wrong)
     amb = false;
 #endif
-    // cell lanes (R = 1) with an ambiguous (k+1) / (k+2) bucket: exact rescan of rows cy-1..cy+1, columns
-    // cx-kRg..cx+kRg by the whole wave (envs are wave-aligned whenever CELL; every lane of the wave is here)
-    if (CELL && __ballot(amb) != 0) {
-#ifdef FLOCK_SERIAL_RESCAN  // A/B builds: the one-lane rescan
-        if (amb)
+    // lanes with an ambiguous (k+1) / (k+2) bucket: exact rescan by the whole wave (every lane of the wave is here;
+    // with CELL, envs are wave-aligned) of rows cy-1..cy+1, columns cx-kRg..cx+kRg (cell lanes, R = 1) or of all N
+    // agents (R = 0)
+    if (__ballot(amb) != 0) {
+#ifdef FLOCK_SERIAL_RESCAN  // A/B builds: the one-lane rescans
+        if (amb && R == 0) knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, true);
+        if (CELL && amb && R == 1)
             exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, gx, gy, cx, cy, R, x, y,
                                             p.box);
 #else
-        exact_rescan_wave<L, PERIODIC>(bd, bj, amb, ext_all, pre_all, p.ecap, npre, g, gx, gy, cx, cy, x, y, p.box);
+        exact_rescan_wave<L, PERIODIC, CELL>(bd, bj, amb, R, lpos, p.S, p.N, ext_all, pre_all, p.ecap, npre, g, gx, gy,
+                                             cx, cy, kx, ky, p.box);
 #endif
     }
     PHASE(5);
