@@ -646,7 +646,8 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
 //   dh_prev = go z + dgh W_hh;  carry = keep[t-1] ? dh_prev : 0
 //   dW_hh += dgh^T h_prev, db_hh += sum_b dgh   (h_prev = keep[t-1] ? hs[t-1] : 0, zero at t = 0)
 // dW / db are written (this recurrence is their only use inside the chunk). LDS: dgh [B][3H], h_prev and carry
-// [B][H]. Thread (i, b) for dh_prev keeps column i of W_hh in registers; dW entries e = tid + 256 q are per thread.
+// [B][H]. Thread (i, b) for dh_prev keeps column i of W_hh in registers; thread tid owns the dW entries (g, tid % H)
+// of the gate quads tid / H + (256 / H) u.
 template <int H>
 __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const float* __restrict__ dhs,
                                                              const float* __restrict__ hs, const float* __restrict__ ws,
@@ -701,13 +702,31 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
             carry[b * H + i] = go * z;  // the direct term of dh_prev; the W_hh term is added below
         }
         __syncthreads();
-        // dW_hh / db_hh partial sums of this step
+        // dW_hh / db_hh partial sums of this step. Thread (ii = tid % H, m0 = tid / H) owns the NW entries
+        // (g, ii) with g in the gate quads m0 + (kBlock / H) u: per row b ONE hprev read and NW / 4 float4 reads of
+        // dgh (broadcast within the wave) instead of 2 NW scalar reads; each entry's sum runs over b in the same
+        // order as before (same bits)
+        {
+            constexpr int NQ = NW / 4, QS = kBlock / H;  // gate quads per thread, quad stride
+            static_assert(NW % 4 == 0 && G % 4 == 0 && (G / 4) == NQ * QS, "gru_seq_bwd: dW tiling");
+            const int ii = tid % H, m0 = tid / H;
+            float s[NW];
 #pragma unroll
-        for (int q = 0; q < NW; ++q) {
-            const int e = tid + kBlock * q, g = e / H, ii = e - g * H;
-            float s = 0.0f;
-            for (int b = 0; b < B; ++b) s = fmaf(dgh[b * G + g], hprev[b * H + ii], s);
-            accw[q] += s;
+            for (int q = 0; q < NW; ++q) s[q] = 0.0f;
+            for (int b = 0; b < B; ++b) {
+                const float hv = hprev[b * H + ii];
+                const float4* d4 = reinterpret_cast<const float4*>(dgh + b * G);
+#pragma unroll
+                for (int u = 0; u < NQ; ++u) {
+                    const float4 v = d4[m0 + QS * u];
+                    s[4 * u + 0] = fmaf(v.x, hv, s[4 * u + 0]);
+                    s[4 * u + 1] = fmaf(v.y, hv, s[4 * u + 1]);
+                    s[4 * u + 2] = fmaf(v.z, hv, s[4 * u + 2]);
+                    s[4 * u + 3] = fmaf(v.w, hv, s[4 * u + 3]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NW; ++q) accw[q] += s[q];
         }
         if (tid < G) {
             float s = 0.0f;
@@ -732,7 +751,10 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
         __syncthreads();  // dgh / hprev reads done before the next step overwrites them
     }
 #pragma unroll
-    for (int q = 0; q < NW; ++q) dW[a * G * H + tid + kBlock * q] = accw[q];
+    for (int q = 0; q < NW; ++q) {  // entry (g, ii) of thread tid: g = 4 (m0 + (kBlock / H) (q / 4)) + q % 4
+        const int g = 4 * (tid / H + (kBlock / H) * (q >> 2)) + (q & 3);
+        dW[a * G * H + g * H + tid % H] = accw[q];
+    }
     if (tid < G) db[a * G + tid] = accb;
 }
 
