@@ -349,7 +349,7 @@ class _GRUSeqFn(torch.autograd.Function):
     """A chunk of GRUCell steps for A networks in one launch each way (flock_gru_seq_fwd / _bwd)."""
 
     @staticmethod
-    def forward(ctx, gi, W_hh, b_hh, keep, save):
+    def forward(ctx, gi, W_hh, b_hh, keep, save, gW=None, gb=None):
         A, C, B, G = gi.shape
         H = G // 3
         gi, W_hh, b_hh = gi.contiguous(), W_hh.contiguous(), b_hh.contiguous()
@@ -359,6 +359,7 @@ class _GRUSeqFn(torch.autograd.Function):
         _ops().gru_seq_fwd(gi, W_hh, b_hh, k8, hs, ws)
         if save:
             ctx.save_for_backward(hs, ws, W_hh, k8)
+            ctx.g = (gW, gb)
         return hs
 
     @staticmethod
@@ -366,20 +367,29 @@ class _GRUSeqFn(torch.autograd.Function):
         hs, ws, W_hh, k8 = ctx.saved_tensors
         A, C, B, H = hs.shape
         dhs = dhs.contiguous()
+        gW, gb = ctx.g
+        direct = gW is not None
         dgi = torch.empty((A, C, B, 3 * H), dtype=hs.dtype, device=hs.device)
-        dW = torch.empty_like(W_hh)
-        db = torch.empty((A, 3 * H), dtype=hs.dtype, device=hs.device)
+        dW = gW if direct else torch.empty_like(W_hh)
+        db = gb if direct else torch.empty((A, 3 * H), dtype=hs.dtype, device=hs.device)
         _ops().gru_seq_bwd(dhs, hs, ws, W_hh, k8, dgi, dW, db)
-        return dgi, dW, db, None, None
+        if direct:  # written into the flat grad buffer's views (grads_into(direct=...))
+            return dgi, None, None, None, None, None, None
+        return dgi, dW, db, None, None, None, None
 
 
-def gru_seq(gi, W_hh, b_hh, keep):
+def gru_seq(gi, W_hh, b_hh, keep, gW=None, gb=None):
     """GRUCell recurrence of A networks over a chunk of C steps from a zero hidden state: gi [A,C,B,3H] (every
     step's x W_ih^T + b_ih), W_hh [A,3H,H], b_hh [A,3H], keep [C,A,B] bool (False: reset the hidden state after
-    that step; may be an expanded view) -> hs [A,C,B,H], each step's output before its reset."""
+    that step; may be an expanded view) -> hs [A,C,B,H], each step's output before its reset. gW / gb (contiguous
+    [A,3H,H] / [A,3H] views of a flat grad buffer, both or neither): the backward writes W_hh's and b_hh's gradients
+    there itself instead of returning them (each parameter in ONE such call per update: the backward overwrites)."""
     assert keep.dim() == 3 and keep.shape == (gi.shape[1], gi.shape[0], gi.shape[2])
     save = torch.is_grad_enabled() and any(t.requires_grad for t in (gi, W_hh, b_hh))
-    return _GRUSeqFn.apply(gi, W_hh, b_hh, keep, save)
+    if (gW is None) != (gb is None) or (gW is not None and not (gW.is_contiguous() and gb.is_contiguous() and
+                                                                 gW.shape == W_hh.shape and gb.shape == b_hh.shape)):
+        raise ValueError("gru_seq: gW / gb must both be given, contiguous and shaped like W_hh / b_hh")
+    return _GRUSeqFn.apply(gi, W_hh, b_hh, keep, save, gW, gb)
 
 
 class _VdnFeatFn(torch.autograd.Function):
@@ -388,7 +398,7 @@ class _VdnFeatFn(torch.autograd.Function):
     the saved post-ReLU activations as batched GEMMs (the weight gradients land in each parameter's own layout)."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, Wi, bi, save, fused_bwd=True):
+    def forward(ctx, x, W1, b1, W2, b2, Wi, bi, save, fused_bwd=True, grads=None):
         A, C, B, n = x.shape
         R = C * B
         if x.stride(3) != 1:
@@ -402,6 +412,7 @@ class _VdnFeatFn(torch.autograd.Function):
         if save:
             ctx.save_for_backward(x, W2, Wi, y1, y2)
             ctx.fused_bwd = bool(fused_bwd)
+            ctx.grads = grads
         return gi
 
     @staticmethod
@@ -409,12 +420,15 @@ class _VdnFeatFn(torch.autograd.Function):
         x, W2, Wi, y1, y2 = ctx.saved_tensors
         A, C, B, n = x.shape
         if ctx.fused_bwd:  # one launch: flock::vdn_feat_bwd (MFMA, the weight gradients accumulated over all rows)
+            if ctx.grads is not None:  # straight into the flat grad buffer's views (grads_into(direct=...))
+                _ops().vdn_feat_bwd(x, W2, Wi, y1, y2, dgi.contiguous(), *ctx.grads)
+                return (None,) * 10
             f = dict(dtype=x.dtype, device=x.device)
             dW1, db1 = torch.empty(A, 64, n, **f), torch.empty(A, 64, **f)
             dW2, db2 = torch.empty(A, 32, 64, **f), torch.empty(A, 32, **f)
             dWi, dbi = torch.empty(A, 96, 32, **f), torch.empty(A, 96, **f)
             _ops().vdn_feat_bwd(x, W2, Wi, y1, y2, dgi.contiguous(), dW1, db1, dW2, db2, dWi, dbi)
-            return None, dW1, db1, dW2, db2, dWi, dbi, None, None
+            return None, dW1, db1, dW2, db2, dWi, dbi, None, None, None
         dWi = torch.bmm(dgi.transpose(1, 2), y2)
         dbi = dgi.sum(1)
         dz2 = torch.bmm(dgi, Wi).masked_fill_(y2 <= 0, 0.0)     # ReLU backward on the output (y > 0 iff z > 0)
@@ -423,19 +437,29 @@ class _VdnFeatFn(torch.autograd.Function):
         dz1 = torch.bmm(dz2, W2).masked_fill_(y1 <= 0, 0.0)
         dW1 = torch.bmm(dz1.transpose(1, 2), x.reshape(A, C * B, n))
         db1 = dz1.sum(1)
-        return None, dW1, db1, dW2, db2, dWi, dbi, None, None
+        if ctx.grads is not None:
+            for g, v in zip(ctx.grads, (dW1, db1, dW2, db2, dWi, dbi)):
+                g.copy_(v)
+            return (None,) * 10
+        return None, dW1, db1, dW2, db2, dWi, dbi, None, None, None
 
 
-def vdn_feat(x, W1, b1, W2, b2, Wi, bi, fused_bwd=True):
+def vdn_feat(x, W1, b1, W2, b2, Wi, bi, fused_bwd=True, grads=None):
     """x [A,C,B,n_obs] (any strides with a unit feature stride, e.g. the replay gather's permuted view) -> gi
     [A, C*B, 96] = relu(relu(x W1^T + b1) W2^T + b2) Wi^T + bi per agent (hidden sizes 64 / 32, n_obs <= 16).
     fused_bwd: the backward as one flock::vdn_feat_bwd launch (False: batched GEMMs + masks + sums, the A/B
-    baseline)."""
+    baseline). grads: (gW1, gb1, gW2, gb2, gWi, gbi), contiguous views of a flat grad buffer shaped like the
+    parameters: the backward writes the six gradients there itself instead of returning them."""
     A, n = x.shape[0], x.shape[3]
     if not (W1.shape == (A, 64, n) and W2.shape == (A, 32, 64) and Wi.shape == (A, 96, 32) and 1 <= n <= 16):
         raise ValueError("vdn_feat: the QNet feature chain n_obs -> 64 -> 32 -> 3 x 32 (n_obs <= 16)")
+    if grads is not None:
+        grads = tuple(grads)
+        if len(grads) != 6 or any(not g.is_contiguous() or g.shape != p.shape
+                                  for g, p in zip(grads, (W1, b1, W2, b2, Wi, bi))):
+            raise ValueError("vdn_feat: grads must be six contiguous views shaped like W1, b1, W2, b2, Wi, bi")
     save = torch.is_grad_enabled() and any(t.requires_grad for t in (W1, b1, W2, b2, Wi, bi))
-    return _VdnFeatFn.apply(x, W1, b1, W2, b2, Wi, bi, save, fused_bwd)
+    return _VdnFeatFn.apply(x, W1, b1, W2, b2, Wi, bi, save, fused_bwd, grads)
 
 
 def gru_cell_gi(gi, h, W_hh, b_hh):

@@ -69,27 +69,38 @@ class BatchedQNet:
             h = y
         return blinear(y, P["q.weight"], P["q.bias"]), h
 
-    def forward_seq(self, x, keep, P=None):
+    # parameters whose gradients forward_seq(..., direct_grads=True)'s backward writes into the flat grad buffer
+    DIRECT = ("feat1.weight", "feat1.bias", "feat2.weight", "feat2.bias", "gru.weight_ih", "gru.bias_ih",
+              "gru.weight_hh", "gru.bias_hh")
+
+    def forward_seq(self, x, keep, P=None, direct_grads=False):
         """A whole chunk, agent-major: x [A,C,B,n_obs], keep [C,B] (False: the hidden state is reset after that
         step, train_flock.py:34-36) -> q [A,C,B,n_actions] from zero initial hidden states. The feature layers, the
         GRU input GEMM and the q head do not depend on the recurrence, so each runs ONCE over all C steps (one
         batched GEMM of C*B rows per agent); the recurrence itself (hidden GEMM, gates, resets) is one gru_seq
-        launch. Same per-step math as forward_am."""
+        launch. Same per-step math as forward_am. direct_grads (the fused path only; returns whether it applied):
+        the backward writes the gradients of DIRECT into self.P.grad's views itself (grads_into(direct=DIRECT))
+        instead of handing them to autograd for a copy."""
         P = self.P.params if P is None else P
         A, C, B, n = x.shape
-        if self.recurrent and n <= 16 and self.fused_features:
+        fused = self.recurrent and n <= 16 and self.fused_features
+        G = {k: self.P.view(self.P.grad, k) for k in self.DIRECT} if (direct_grads and fused) else None
+        if fused:
             # feat1-ReLU-feat2-ReLU and the GRU input side of every step in one launch (flock_vdn_feat_fwd)
             gi = vdn_feat(x, P["feat1.weight"], P["feat1.bias"], P["feat2.weight"], P["feat2.bias"],
-                          P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
+                          P["gru.weight_ih"], P["gru.bias_ih"],
+                          grads=None if G is None else [G[k] for k in self.DIRECT[:6]]).view(A, C, B, -1)
         else:
             y = F.relu(blinear(x.reshape(A, C * B, n), P["feat1.weight"], P["feat1.bias"]))
             y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
             if self.recurrent:
                 gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
         if self.recurrent:  # the whole chunk's recurrence in one launch each way (flock_gru_seq_fwd / _bwd)
-            hs = gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep.unsqueeze(1).expand(C, A, B))
+            hs = gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep.unsqueeze(1).expand(C, A, B),
+                         gW=None if G is None else G["gru.weight_hh"], gb=None if G is None else G["gru.bias_hh"])
             y = hs.view(A, C * B, self.hx_size)
-        return blinear(y, P["q.weight"], P["q.bias"]).view(A, C, B, -1)
+        q = blinear(y, P["q.weight"], P["q.bias"]).view(A, C, B, -1)
+        return (q, G is not None) if direct_grads else q
 
     def __call__(self, obs, hidden):
         """Reference layout: obs [B,A,n_obs], hidden [B,A,H] -> (q [B,A,n_actions], hidden [B,A,H])."""
@@ -220,7 +231,7 @@ class VDNLearner:
         Pq, Pt = self.train_leaves, self.target_params()
         keep = done == 0                                                # hidden[done_mask] = 0 (:34-36)
         # agent-major whole-chunk tensors [A, C, B, ...] (one GEMM per layer for all steps, BatchedQNet.forward_seq)
-        q_out = self.q.forward_seq(s.permute(1, 0, 2, 3), keep, Pq)      # [A, C, B, n_act]
+        q_out, direct = self.q.forward_seq(s.permute(1, 0, 2, 3), keep, Pq, direct_grads=True)  # [A, C, B, n_act]
         q_a = q_out.gather(3, a.permute(1, 0, 2).unsqueeze(-1)).squeeze(-1)
         sum_q = q_a.sum(dim=0)                                          # [C, B]
         with torch.no_grad():
@@ -234,7 +245,7 @@ class VDNLearner:
         loss = steps[0]
         for t in range(1, C):
             loss = loss + steps[t]
-        self.q.P.grads_into(loss, Pq)
+        self.q.P.grads_into(loss, Pq, direct=self.q.DIRECT if direct else ())
         with torch.no_grad():
             self.loss.copy_(loss.detach())
 

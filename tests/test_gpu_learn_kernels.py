@@ -184,3 +184,38 @@ def test_vdn_feat_matches_torch_linear_chain(A, C, B, n, fused_bwd, cuda):
         torch.testing.assert_close(a_.grad, b_.grad, rtol=1e-4, atol=1e-5 * float(b_.grad.abs().max()), msg=name)
     with torch.no_grad():  # the target network's path: gi only (no saved activations)
         torch.testing.assert_close(vdn_feat(x, *W), ref.detach(), rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("fused_bwd", [True, False], ids=["vdn_feat_bwd", "autograd_bwd"])
+def test_direct_grad_views_equal_returned_grads(fused_bwd, cuda):
+    """vdn_feat(grads=...) and gru_seq(gW=, gb=) write their weight gradients into given views of a flat buffer in
+    the backward (VDNLearner: grads_into(direct=...), no autograd copy into the flat grad buffer): bitwise the
+    gradients the same launches return to autograd, and autograd sees no gradient for those leaves."""
+    from marl_range_flocking_amd.learners.core import gru_seq, vdn_feat
+
+    A, C, B, n, H = 16, 10, 32, 4, 32
+    g = torch.Generator(device=cuda).manual_seed(5)
+    r = lambda *s: (torch.rand(*s, device=cuda, generator=g) * 2 - 1)  # noqa: E731
+    x = r(B, C, A, n).permute(2, 1, 0, 3)
+    W = [r(A, 64, n) * 0.5, r(A, 64) * 0.5, r(A, 32, 64) * 0.2, r(A, 32) * 0.2, r(A, 96, 32) * 0.3, r(A, 96) * 0.3,
+         r(A, 3 * H, H) * 0.3, r(A, 3 * H) * 0.3]
+    keep = torch.rand(C, A, B, device=cuda, generator=g) > 0.1
+    up = r(A, C, B, H)
+
+    def run(direct):
+        P = [w.clone().requires_grad_(True) for w in W]
+        flat = torch.full((sum(w.numel() for w in W),), float("nan"), device=cuda)
+        views, off = [], 0
+        for w in W:
+            views.append(flat[off:off + w.numel()].view(w.shape))
+            off += w.numel()
+        gi = vdn_feat(x, *P[:6], fused_bwd=fused_bwd, grads=views[:6] if direct else None).view(A, C, B, 3 * H)
+        hs = gru_seq(gi, P[6], P[7], keep, gW=views[6] if direct else None, gb=views[7] if direct else None)
+        grads = torch.autograd.grad((hs * up).sum(), P, allow_unused=True)
+        if direct:
+            assert all(gr is None for gr in grads)
+            return views
+        return grads
+
+    for name, a_, b_ in zip(("W1", "b1", "W2", "b2", "Wi", "bi", "W_hh", "b_hh"), run(True), run(False)):
+        assert torch.equal(a_, b_), name
