@@ -62,6 +62,18 @@ int flock_gru_seq_fwd(void* stream, int A, int C, int B, int H, const float* gi,
 int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs, const float* hs, const float* ws,
                       const float* w_hh, const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb,
                       float* dgi, float* dw_hh, float* db_hh);
+/* The same recurrence with VDN's q head fused (learners/vdn/net.py:34-37, QNet.q = Linear(32, n_actions) on every
+ * step's GRU output): q_fwd also writes q [A][C][B][NA] = hs W_q^T + b_q (w_q [A][NA][H], b_q [A][NA], NA <= 16);
+ * hs and ws may be NULL together (no backward). q_bwd takes dq = dLoss/dq [A][C][B][NA] in place of dhs and also
+ * writes dw_q [A][NA][H], db_q [A][NA]. Replaces the q head's batched GEMMs (forward, both backward GEMMs and the
+ * bias sum) of vdn/train_flock.py:23-28's q(s) for every agent and step. */
+int flock_gru_seq_q_fwd(void* stream, int A, int C, int B, int H, int NA, const float* gi, const float* w_hh,
+                        const float* b_hh, const float* w_q, const float* b_q, const uint8_t* keep, int64_t keep_st,
+                        int64_t keep_sa, int64_t keep_sb, float* hs, float* ws, float* q);
+int flock_gru_seq_q_bwd(void* stream, int A, int C, int B, int H, int NA, const float* dq, const float* hs,
+                        const float* ws, const float* w_hh, const float* w_q, const uint8_t* keep, int64_t keep_st,
+                        int64_t keep_sa, int64_t keep_sb, float* dgi, float* dw_hh, float* db_hh, float* dw_q,
+                        float* db_q);
 
 /* VDN QNet feature chain of A agents, R rows each (learners/vdn/net.py:19-33; replaces the three per-agent Linear
  * layers and two ReLUs before the GRUCell, train_flock.py:23-27 runs them per chunk step):

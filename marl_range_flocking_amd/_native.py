@@ -59,6 +59,8 @@ SIGNATURES = {
     + [_c_void_p] * 2,
     "flock_gru_seq_bwd": [_c_void_p, _c_int, _c_int, _c_int, _c_int] + [_c_void_p] * 5 + [ctypes.c_int64] * 3
     + [_c_void_p] * 3,
+    "flock_gru_seq_q_fwd": [_c_void_p] + [_c_int] * 5 + [_c_void_p] * 6 + [ctypes.c_int64] * 3 + [_c_void_p] * 3,
+    "flock_gru_seq_q_bwd": [_c_void_p] + [_c_int] * 5 + [_c_void_p] * 6 + [ctypes.c_int64] * 3 + [_c_void_p] * 5,
     "flock_gather_rows": [_c_void_p, ctypes.c_int64, ctypes.c_int64, _c_void_p, _c_void_p, _c_void_p],
     "flock_scatter_rows": [_c_void_p, ctypes.c_int64, ctypes.c_int64, _c_void_p, _c_void_p, _c_void_p],
 }

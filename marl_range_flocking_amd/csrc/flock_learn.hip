@@ -582,16 +582,32 @@ __global__ __launch_bounds__(kBB) void vdn_feat_bwd_kernel(int R, int B, int NI,
 // keep: uint8 at keep[t*kt + a*ka + b*kb]; the initial hidden state is zero (every reference chunk starts from
 // init_hidden). Thread (j, b): hidden unit j = tid % H of rows b = tid / H + (256 / H) * q; its three W_hh rows
 // live in registers, the hidden states in LDS (ping-pong). ws [A][C][B][4H] = (r, z, n, gh_n) for the backward.
-template <int H>
+// The q head fused (QH, VDN's QNet.q: q = h' W_q^T + b_q of every step's output, learners/vdn/net.py:36-37): W_q /
+// b_q staged in LDS, each step's outputs h' kept in a ping-pong LDS buffer, and after the step's barrier the
+// B x NA q values of the step computed from it (float4 reads, k-ordered fmaf from b_q) into q [A][C][B][NA]; hs may
+// then be NULL (no backward).
+struct QHead {
+    const float* W;  // [A][NA][H]
+    const float* b;  // [A][NA]
+    float* q;        // [A][C][B][NA]
+    int NA;
+};
+template <int H, bool QH = false>
 __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const float* __restrict__ gi,
                                                              const float* __restrict__ W, const float* __restrict__ bias,
                                                              const uint8_t* __restrict__ keep, int64_t kt, int64_t ka,
                                                              int64_t kb, float* __restrict__ hs,
-                                                             float* __restrict__ ws) {
+                                                             float* __restrict__ ws, QHead qh = QHead{}) {
     extern __shared__ float4 seq_smem[];
     float* hcur = reinterpret_cast<float*>(seq_smem);
     float* hnxt = hcur + B * H;
+    float* hq = hnxt + B * H;      // QH: [2][B][H] step outputs (ping-pong)
+    float* wq = hq + 2 * B * H;    // QH: [NA][H] W_q, then [NA] b_q
     const int64_t a = blockIdx.x;
+    if (QH) {
+        for (int e = threadIdx.x; e < qh.NA * (H + 1); e += kBlock)
+            wq[e] = e < qh.NA * H ? qh.W[a * qh.NA * H + e] : qh.b[a * qh.NA + e - qh.NA * H];
+    }
     const int tid = threadIdx.x, j = tid % H, bstep = kBlock / H;
     const float* Wa = W + a * 3 * H * H;
     float wr[H], wz[H], wn[H];
@@ -624,7 +640,8 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
             const float nn = tanhf(g[2 * H + j] + ghn * r);
             const float hv = hcur[b * H + j];
             const float ho = (hv - nn) * z + nn;
-            hs[row * H + j] = ho;
+            if (!QH || hs) hs[row * H + j] = ho;
+            if (QH) hq[(t & 1) * B * H + b * H + j] = ho;
             if (ws) {
                 float* w = ws + row * 4 * H;
                 w[j] = r;
@@ -635,6 +652,24 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
             hnxt[b * H + j] = keep[t * kt + a * ka + b * kb] ? ho : 0.0f;
         }
         __syncthreads();
+        if (QH) {  // q of step t (its h' stay in hq[t & 1] until after the next step's barrier)
+            const float* hb = hq + (t & 1) * B * H;
+            for (int e = threadIdx.x; e < B * qh.NA; e += kBlock) {
+                const int b = e / qh.NA, o = e - b * qh.NA;
+                const float4* w4 = reinterpret_cast<const float4*>(wq + o * H);
+                const float4* h4 = reinterpret_cast<const float4*>(hb + b * H);
+                float acc = wq[qh.NA * H + o];
+#pragma unroll
+                for (int k4 = 0; k4 < H / 4; ++k4) {
+                    const float4 w = w4[k4], h = h4[k4];
+                    acc = fmaf(w.x, h.x, acc);
+                    acc = fmaf(w.y, h.y, acc);
+                    acc = fmaf(w.z, h.z, acc);
+                    acc = fmaf(w.w, h.w, acc);
+                }
+                qh.q[((a * C + t) * B + b) * qh.NA + o] = acc;
+            }
+        }
         float* tmp = hcur;
         hcur = hnxt;
         hnxt = tmp;
@@ -648,13 +683,26 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
 // dW / db are written (this recurrence is their only use inside the chunk). LDS: dgh [B][3H], h_prev and carry
 // [B][H]. Thread (i, b) for dh_prev keeps column i of W_hh in registers; thread tid owns the dW entries (g, tid % H)
 // of the gate quads tid / H + (256 / H) u.
-template <int H>
-__global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const float* __restrict__ dhs,
+// QH (the fused q head's backward): dhs is dq [A][C][B][NA] (the gradient of the q values); the step's dL/dh' is
+// dq W_q (column i of W_q in registers), and dW_q = sum_(t,b) dq^T h', db_q = sum_(t,b) dq accumulate per thread over
+// its rows and steps, then over the kBlock / H row groups in a fixed order (LDS) -> dWq [A][NA][H], dbq [A][NA].
+struct QHeadBwd {
+    const float* W;  // [A][NA][H]
+    float* dW;       // [A][NA][H]
+    float* db;       // [A][NA]
+    int NA;
+};
+constexpr int kMaxQ = 16;
+template <int H, int NQ = 0>  // NQ > 0: the q head fused, at most NQ actions (registers sized for NQ)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) void gru_seq_bwd_kernel(int C, int B, const float* __restrict__ dhs,
                                                              const float* __restrict__ hs, const float* __restrict__ ws,
                                                              const float* __restrict__ W,
                                                              const uint8_t* __restrict__ keep, int64_t kt, int64_t ka,
                                                              int64_t kb, float* __restrict__ dgi,
-                                                             float* __restrict__ dW, float* __restrict__ db) {
+                                                             float* __restrict__ dW, float* __restrict__ db,
+                                                             QHeadBwd qh = QHeadBwd{}) {
+    constexpr bool QH = NQ > 0;
+    constexpr int NQA = QH ? NQ : 1;
     constexpr int G = 3 * H, NW = G * H / kBlock;  // dW entries per thread
     extern __shared__ float4 seq_smem[];
     float* dgh = reinterpret_cast<float*>(seq_smem);  // [B][G]
@@ -662,6 +710,13 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
     float* carry = hprev + B * H;                      // [B][H]
     const int64_t a = blockIdx.x;
     const int tid = threadIdx.x, i = tid % H, bstep = kBlock / H;
+    // QH: W_q in LDS behind carry ([NA][H]); dW_q[:, i] partials in registers; lanes i < NA also sum db_q[i]
+    float* wq = carry + B * H;
+    float aqw[NQA], aqb = 0.0f;
+#pragma unroll
+    for (int o = 0; o < NQA; ++o) aqw[o] = 0.0f;
+    if (QH)
+        for (int e = tid; e < qh.NA * H; e += kBlock) wq[e] = qh.W[a * qh.NA * H + e];
     const float* Wa = W + a * G * H;
     float wc[G];  // column i of W_hh
 #pragma unroll
@@ -684,7 +739,23 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
             const int64_t row = (a * C + t) * B + b;
             const float* w = ws + row * 4 * H;
             const float r = w[i], z = w[H + i], nn = w[2 * H + i], ghn = w[3 * H + i];
-            const float go = dhs[row * H + i] + carry[b * H + i];
+            float dho;
+            if (QH) {  // dL/dh' of the q head: dq W_q, k-ordered; and its dW_q / db_q partials
+                const float* dq = dhs + row * qh.NA;
+                const float ho = hs[row * H + i];
+                dho = 0.0f;
+#pragma unroll
+                for (int o = 0; o < NQA; ++o)
+                    if (o < qh.NA) {
+                        const float d = dq[o];
+                        dho = fmaf(d, wq[o * H + i], dho);
+                        aqw[o] = fmaf(d, ho, aqw[o]);
+                    }
+                if (i < qh.NA) aqb += dq[i];
+            } else {
+                dho = dhs[row * H + i];
+            }
+            const float go = dho + carry[b * H + i];
             const float hv = hprev[b * H + i];
             const float dn = go * (1.0f - z);
             const float dz = go * (hv - nn);
@@ -707,8 +778,8 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
         // dgh (broadcast within the wave) instead of 2 NW scalar reads; each entry's sum runs over b in the same
         // order as before (same bits)
         {
-            constexpr int NQ = NW / 4, QS = kBlock / H;  // gate quads per thread, quad stride
-            static_assert(NW % 4 == 0 && G % 4 == 0 && (G / 4) == NQ * QS, "gru_seq_bwd: dW tiling");
+            constexpr int NGQ = NW / 4, QS = kBlock / H;  // gate quads per thread, quad stride
+            static_assert(NW % 4 == 0 && G % 4 == 0 && (G / 4) == NGQ * QS, "gru_seq_bwd: dW tiling");
             const int ii = tid % H, m0 = tid / H;
             float s[NW];
 #pragma unroll
@@ -717,7 +788,7 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
                 const float hv = hprev[b * H + ii];
                 const float4* d4 = reinterpret_cast<const float4*>(dgh + b * G);
 #pragma unroll
-                for (int u = 0; u < NQ; ++u) {
+                for (int u = 0; u < NGQ; ++u) {
                     const float4 v = d4[m0 + QS * u];
                     s[4 * u + 0] = fmaf(v.x, hv, s[4 * u + 0]);
                     s[4 * u + 1] = fmaf(v.y, hv, s[4 * u + 1]);
@@ -756,6 +827,25 @@ __global__ __launch_bounds__(kBlock) void gru_seq_bwd_kernel(int C, int B, const
         dW[a * G * H + g * H + tid % H] = accw[q];
     }
     if (tid < G) db[a * G + tid] = accb;
+    if (QH) {  // the q head's gradients: the bstep row groups' partials summed in group order
+        float* red = dgh;  // [bstep][NA][H] + [bstep][NA] over dgh.. (the loop is done with them: its last barrier)
+        const int grp = tid / H;
+#pragma unroll
+        for (int o = 0; o < NQA; ++o)
+            if (o < qh.NA) red[(grp * qh.NA + o) * H + i] = aqw[o];
+        if (i < qh.NA) red[bstep * qh.NA * H + grp * qh.NA + i] = aqb;
+        __syncthreads();
+        for (int e = tid; e < qh.NA * H; e += kBlock) {
+            float s = 0.0f;
+            for (int q = 0; q < bstep; ++q) s += red[q * qh.NA * H + e];
+            qh.dW[a * qh.NA * H + e] = s;
+        }
+        if (tid < qh.NA) {
+            float s = 0.0f;
+            for (int q = 0; q < bstep; ++q) s += red[bstep * qh.NA * H + q * qh.NA + tid];
+            qh.db[a * qh.NA + tid] = s;
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(int64_t rows, int64_t width, const float* __restrict__ src,
@@ -939,6 +1029,56 @@ int flock_gru_seq_fwd(void* stream, int A, int C, int B, int H, const float* gi,
     hipLaunchKernelGGL(gru_seq_fwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, gi, w_hh, b_hh,
                        keep, keep_st, keep_sa, keep_sb, hs, ws);
     return launched();
+}
+
+int flock_gru_seq_q_fwd(void* stream, int A, int C, int B, int H, int NA, const float* gi, const float* w_hh,
+                        const float* b_hh, const float* w_q, const float* b_q, const uint8_t* keep, int64_t keep_st,
+                        int64_t keep_sa, int64_t keep_sb, float* hs, float* ws, float* q) {
+    if (A <= 0 || C <= 0 || B <= 0) return 0;
+    if (!gi || !w_hh || !b_hh || !w_q || !b_q || !keep || !q) return fail(-3, "flock_gru_seq_q_fwd: NULL pointer");
+    if (H != 32) return fail(-2, "flock_gru_seq_q_fwd: hidden size must be 32");
+    if (NA < 1 || NA > kMaxQ) return fail(-2, "flock_gru_seq_q_fwd: 1 <= n_actions <= 16");
+    if (ws && !hs) return fail(-3, "flock_gru_seq_q_fwd: ws needs hs (the backward reads both)");
+    const size_t lds = ((size_t)4 * B * H + (size_t)NA * (H + 1)) * sizeof(float);
+    if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_q_fwd: B too large for LDS");
+    if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(gru_seq_fwd_kernel<32, true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return fail(-4, "flock_gru_seq_q_fwd: cannot raise the LDS limit");
+    hipLaunchKernelGGL((gru_seq_fwd_kernel<32, true>), dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, gi, w_hh,
+                       b_hh, keep, keep_st, keep_sa, keep_sb, hs, ws, QHead{w_q, b_q, q, NA});
+    return launched();
+}
+
+int flock_gru_seq_q_bwd(void* stream, int A, int C, int B, int H, int NA, const float* dq, const float* hs,
+                        const float* ws, const float* w_hh, const float* w_q, const uint8_t* keep, int64_t keep_st,
+                        int64_t keep_sa, int64_t keep_sb, float* dgi, float* dw_hh, float* db_hh, float* dw_q,
+                        float* db_q) {
+    if (A <= 0 || C <= 0 || B <= 0) return 0;
+    if (!dq || !hs || !ws || !w_hh || !w_q || !keep || !dgi || !dw_hh || !db_hh || !dw_q || !db_q)
+        return fail(-3, "flock_gru_seq_q_bwd: NULL pointer");
+    if (H != 32) return fail(-2, "flock_gru_seq_q_bwd: hidden size must be 32");
+    if (NA < 1 || NA > kMaxQ) return fail(-2, "flock_gru_seq_q_bwd: 1 <= n_actions <= 16");
+    // dgh, h_prev, carry, W_q; the q head's final reduction ((kBlock / H) (NA H + NA) floats) reuses the same space
+    // from its start once the recurrence is done
+    const size_t body = (size_t)B * (3 * H + 2 * H) + (size_t)NA * H, red = (size_t)(kBlock / H) * NA * (H + 1);
+    const size_t lds = (body > red ? body : red) * sizeof(float);
+    if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_q_bwd: B too large for LDS");
+    const QHeadBwd qh{w_q, dw_q, db_q, NA};
+    auto go = [&](auto kern) {
+        if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return fail(-4, "flock_gru_seq_q_bwd: cannot raise the LDS limit");
+        hipLaunchKernelGGL(kern, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dq, hs, ws, w_hh, keep,
+                           keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh, qh);
+        return launched();
+    };
+    // registers sized for the head: the smallest instantiation that holds NA
+    if (NA <= 2) return go(gru_seq_bwd_kernel<32, 2>);
+    if (NA <= 4) return go(gru_seq_bwd_kernel<32, 4>);
+    if (NA <= 6) return go(gru_seq_bwd_kernel<32, 6>);
+    if (NA <= 8) return go(gru_seq_bwd_kernel<32, 8>);
+    if (NA <= 10) return go(gru_seq_bwd_kernel<32, 10>);
+    return go(gru_seq_bwd_kernel<32, 16>);
 }
 
 int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs, const float* hs, const float* ws,

@@ -12,6 +12,7 @@
 //   flock::grad_norm         clip_grad_norm_ (vdn/train_flock.py:42) without a host sync
 //   flock::gru_cell_fwd/_bwd nn.GRUCell elementwise part (maddpg_official_rnn/net.py:33,118; vdn/net.py:24)
 //   flock::gru_seq_fwd/_bwd  a whole chunk of GRUCell steps (vdn/train_flock.py:23-36, MADDPG.py:95-132)
+//   flock::gru_seq_q_fwd/_bwd  the same with VDN's q head fused (learners/vdn/net.py:34-37)
 //   flock::vdn_feat_fwd/_bwd the VDN QNet feature chain + GRU input side (vdn/net.py:19-33) and its backward
 //   flock::gather_rows / scatter_rows / ring_store   replay gather / insert (memory_rnn.py:53-99, vdn/utils.py:18-60,
 //                            maddpg_shared_critic/utils.py:47-76)
@@ -282,6 +283,86 @@ void gru_seq_bwd_hip(const Tensor& dhs, const Tensor& hs, const Tensor& ws, cons
 void gru_seq_bwd_meta(const Tensor& dhs, const Tensor& hs, const Tensor& ws, const Tensor& w_hh, const Tensor& keep,
                       const Tensor& dgi, const Tensor& dw_hh, const Tensor& db_hh) {
     gru_seq_bwd_checks(dhs, hs, ws, w_hh, keep, dgi, dw_hh, db_hh);
+}
+
+// ---------------------------------------------------------------------------------- gru_seq_q_fwd / gru_seq_q_bwd
+// the recurrence with VDN's q head fused: w_q [A, NA, H], b_q [A, NA], q [A, C, B, NA]; hs / ws optional together
+void gru_seq_q_fwd_checks(const Tensor& gi, const Tensor& w_hh, const Tensor& b_hh, const Tensor& w_q,
+                          const Tensor& b_q, const Tensor& keep, const optional<Tensor>& hs,
+                          const optional<Tensor>& ws, const Tensor& q) {
+    if (any_sym(gi, w_hh, b_hh, w_q, b_q, keep, hs, ws, q)) return;
+    TORCH_CHECK(gi.dim() == 4 && gi.size(3) % 3 == 0, "gi must be [A, C, B, 3H], got ", gi.sizes());
+    const int64_t A = gi.size(0), C = gi.size(1), B = gi.size(2), H = gi.size(3) / 3;
+    TORCH_CHECK(H == 32, "gru_seq_q: hidden size must be 32");
+    TORCH_CHECK(w_q.dim() == 3 && w_q.size(1) >= 1 && w_q.size(1) <= 16, "w_q must be [A, NA <= 16, H]");
+    const int64_t NA = w_q.size(1);
+    shaped(gi, "gi", at::kFloat, {A, C, B, 3 * H}, gi);
+    shaped(w_hh, "w_hh", at::kFloat, {A, 3 * H, H}, gi);
+    shaped(b_hh, "b_hh", at::kFloat, {A, 3 * H}, gi);
+    shaped(w_q, "w_q", at::kFloat, {A, NA, H}, gi);
+    shaped(b_q, "b_q", at::kFloat, {A, NA}, gi);
+    keep_check(keep, A, C, B, gi);
+    TORCH_CHECK(hs.has_value() == ws.has_value(), "gru_seq_q_fwd: hs and ws are given together (the backward's)");
+    if (hs) shaped(*hs, "hs", at::kFloat, {A, C, B, H}, gi);
+    if (ws) shaped(*ws, "ws", at::kFloat, {A, C, B, 4 * H}, gi);
+    shaped(q, "q", at::kFloat, {A, C, B, NA}, gi);
+}
+void gru_seq_q_fwd_hip(const Tensor& gi, const Tensor& w_hh, const Tensor& b_hh, const Tensor& w_q, const Tensor& b_q,
+                       const Tensor& keep, const optional<Tensor>& hs, const optional<Tensor>& ws, const Tensor& q) {
+    hip_only(gi, "gru_seq_q_fwd");
+    gru_seq_q_fwd_checks(gi, w_hh, b_hh, w_q, b_q, keep, hs, ws, q);
+    const at::OptionalDeviceGuard g(gi.device());
+    rc_check(flock_gru_seq_q_fwd(stream_of(gi), (int)gi.size(0), (int)gi.size(1), (int)gi.size(2),
+                                 (int)gi.size(3) / 3, (int)w_q.size(1), ptr<const float>(gi), ptr<const float>(w_hh),
+                                 ptr<const float>(b_hh), ptr<const float>(w_q), ptr<const float>(b_q),
+                                 static_cast<const uint8_t*>(keep.data_ptr()), keep.stride(0), keep.stride(1),
+                                 keep.stride(2), ptr<float>(hs), ptr<float>(ws), ptr<float>(q)),
+             "flock_gru_seq_q_fwd");
+}
+void gru_seq_q_fwd_meta(const Tensor& gi, const Tensor& w_hh, const Tensor& b_hh, const Tensor& w_q,
+                        const Tensor& b_q, const Tensor& keep, const optional<Tensor>& hs, const optional<Tensor>& ws,
+                        const Tensor& q) {
+    gru_seq_q_fwd_checks(gi, w_hh, b_hh, w_q, b_q, keep, hs, ws, q);
+}
+void gru_seq_q_bwd_checks(const Tensor& dq, const Tensor& hs, const Tensor& ws, const Tensor& w_hh, const Tensor& w_q,
+                          const Tensor& keep, const Tensor& dgi, const Tensor& dw_hh, const Tensor& db_hh,
+                          const Tensor& dw_q, const Tensor& db_q) {
+    if (any_sym(dq, hs, ws, w_hh, w_q, keep, dgi, dw_hh, db_hh, dw_q, db_q)) return;
+    TORCH_CHECK(hs.dim() == 4, "hs must be [A, C, B, H], got ", hs.sizes());
+    const int64_t A = hs.size(0), C = hs.size(1), B = hs.size(2), H = hs.size(3);
+    TORCH_CHECK(H == 32, "gru_seq_q: hidden size must be 32");
+    TORCH_CHECK(w_q.dim() == 3 && w_q.size(1) >= 1 && w_q.size(1) <= 16, "w_q must be [A, NA <= 16, H]");
+    const int64_t NA = w_q.size(1);
+    shaped(hs, "hs", at::kFloat, {A, C, B, H}, hs);
+    shaped(dq, "dq", at::kFloat, {A, C, B, NA}, hs);
+    shaped(ws, "ws", at::kFloat, {A, C, B, 4 * H}, hs);
+    shaped(w_hh, "w_hh", at::kFloat, {A, 3 * H, H}, hs);
+    shaped(w_q, "w_q", at::kFloat, {A, NA, H}, hs);
+    keep_check(keep, A, C, B, hs);
+    shaped(dgi, "dgi", at::kFloat, {A, C, B, 3 * H}, hs);
+    shaped(dw_hh, "dw_hh", at::kFloat, {A, 3 * H, H}, hs);
+    shaped(db_hh, "db_hh", at::kFloat, {A, 3 * H}, hs);
+    shaped(dw_q, "dw_q", at::kFloat, {A, NA, H}, hs);
+    shaped(db_q, "db_q", at::kFloat, {A, NA}, hs);
+}
+void gru_seq_q_bwd_hip(const Tensor& dq, const Tensor& hs, const Tensor& ws, const Tensor& w_hh, const Tensor& w_q,
+                       const Tensor& keep, const Tensor& dgi, const Tensor& dw_hh, const Tensor& db_hh,
+                       const Tensor& dw_q, const Tensor& db_q) {
+    hip_only(hs, "gru_seq_q_bwd");
+    gru_seq_q_bwd_checks(dq, hs, ws, w_hh, w_q, keep, dgi, dw_hh, db_hh, dw_q, db_q);
+    const at::OptionalDeviceGuard g(hs.device());
+    rc_check(flock_gru_seq_q_bwd(stream_of(hs), (int)hs.size(0), (int)hs.size(1), (int)hs.size(2), (int)hs.size(3),
+                                 (int)w_q.size(1), ptr<const float>(dq), ptr<const float>(hs), ptr<const float>(ws),
+                                 ptr<const float>(w_hh), ptr<const float>(w_q),
+                                 static_cast<const uint8_t*>(keep.data_ptr()), keep.stride(0), keep.stride(1),
+                                 keep.stride(2), ptr<float>(dgi), ptr<float>(dw_hh), ptr<float>(db_hh),
+                                 ptr<float>(dw_q), ptr<float>(db_q)),
+             "flock_gru_seq_q_bwd");
+}
+void gru_seq_q_bwd_meta(const Tensor& dq, const Tensor& hs, const Tensor& ws, const Tensor& w_hh, const Tensor& w_q,
+                        const Tensor& keep, const Tensor& dgi, const Tensor& dw_hh, const Tensor& db_hh,
+                        const Tensor& dw_q, const Tensor& db_q) {
+    gru_seq_q_bwd_checks(dq, hs, ws, w_hh, w_q, keep, dgi, dw_hh, db_hh, dw_q, db_q);
 }
 
 // ------------------------------------------------------------------------------------------------ vdn_feat_fwd
@@ -695,6 +776,12 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         "gru_seq_bwd(Tensor dhs, Tensor hs, Tensor ws, Tensor w_hh, Tensor keep, Tensor(a!) dgi, Tensor(b!) dw_hh, "
         "Tensor(c!) db_hh) -> ()");
     m.def(
+        "gru_seq_q_fwd(Tensor gi, Tensor w_hh, Tensor b_hh, Tensor w_q, Tensor b_q, Tensor keep, Tensor(a!)? hs, "
+        "Tensor(b!)? ws, Tensor(c!) q) -> ()");
+    m.def(
+        "gru_seq_q_bwd(Tensor dq, Tensor hs, Tensor ws, Tensor w_hh, Tensor w_q, Tensor keep, Tensor(a!) dgi, "
+        "Tensor(b!) dw_hh, Tensor(c!) db_hh, Tensor(d!) dw_q, Tensor(e!) db_q) -> ()");
+    m.def(
         "vdn_feat_fwd(Tensor x, Tensor w1, Tensor b1, Tensor w2, Tensor b2, Tensor w_ih, Tensor b_ih, "
         "Tensor(a!)? y1, Tensor(b!)? y2, Tensor(c!) gi) -> ()");
     m.def(
@@ -726,6 +813,8 @@ TORCH_LIBRARY_IMPL(flock, CUDA, m) {
     m.impl("gru_cell_bwd", &gru_cell_bwd_hip);
     m.impl("gru_seq_fwd", &gru_seq_fwd_hip);
     m.impl("gru_seq_bwd", &gru_seq_bwd_hip);
+    m.impl("gru_seq_q_fwd", &gru_seq_q_fwd_hip);
+    m.impl("gru_seq_q_bwd", &gru_seq_q_bwd_hip);
     m.impl("vdn_feat_fwd", &vdn_feat_fwd_hip);
     m.impl("vdn_feat_bwd", &vdn_feat_bwd_hip);
     m.impl("gather_rows", &gather_rows_hip);
@@ -746,6 +835,8 @@ TORCH_LIBRARY_IMPL(flock, Meta, m) {
     m.impl("gru_cell_bwd", &gru_cell_bwd_meta);
     m.impl("gru_seq_fwd", &gru_seq_fwd_meta);
     m.impl("gru_seq_bwd", &gru_seq_bwd_meta);
+    m.impl("gru_seq_q_fwd", &gru_seq_q_fwd_meta);
+    m.impl("gru_seq_q_bwd", &gru_seq_q_bwd_meta);
     m.impl("vdn_feat_fwd", &vdn_feat_fwd_meta);
     m.impl("vdn_feat_bwd", &vdn_feat_bwd_meta);
     m.impl("gather_rows", &gather_rows_meta);

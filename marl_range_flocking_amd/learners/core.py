@@ -392,6 +392,60 @@ def gru_seq(gi, W_hh, b_hh, keep, gW=None, gb=None):
     return _GRUSeqFn.apply(gi, W_hh, b_hh, keep, save, gW, gb)
 
 
+class _GRUSeqQFn(torch.autograd.Function):
+    """gru_seq with VDN's q head fused (flock_gru_seq_q_fwd / _bwd): returns q [A,C,B,NA] = hs W_q^T + b_q of every
+    step's GRU output; the backward takes dq in place of dhs and also yields dW_q, db_q. g: optional grad views of
+    (W_hh, b_hh, W_q, b_q) that the backward writes itself (grads_into(direct=...))."""
+
+    @staticmethod
+    def forward(ctx, gi, W_hh, b_hh, Wq, bq, keep, save, g=None):
+        A, C, B, G = gi.shape
+        H, NA = G // 3, Wq.shape[1]
+        gi, W_hh, b_hh, Wq, bq = (t.contiguous() for t in (gi, W_hh, b_hh, Wq, bq))
+        k8 = keep.view(torch.uint8) if keep.dtype == torch.bool else keep
+        f = dict(dtype=gi.dtype, device=gi.device)
+        hs = torch.empty((A, C, B, H), **f) if save else None
+        ws = torch.empty((A, C, B, 4 * H), **f) if save else None
+        q = torch.empty((A, C, B, NA), **f)
+        _ops().gru_seq_q_fwd(gi, W_hh, b_hh, Wq, bq, k8, hs, ws, q)
+        if save:
+            ctx.save_for_backward(hs, ws, W_hh, Wq, k8)
+            ctx.g = g
+        return q
+
+    @staticmethod
+    def backward(ctx, dq):
+        hs, ws, W_hh, Wq, k8 = ctx.saved_tensors
+        A, C, B, H = hs.shape
+        f = dict(dtype=hs.dtype, device=hs.device)
+        dgi = torch.empty((A, C, B, 3 * H), **f)
+        if ctx.g is not None:
+            gW, gb, gWq, gbq = ctx.g
+            _ops().gru_seq_q_bwd(dq.contiguous(), hs, ws, W_hh, Wq, k8, dgi, gW, gb, gWq, gbq)
+            return dgi, None, None, None, None, None, None, None
+        dW, db = torch.empty_like(W_hh), torch.empty((A, 3 * H), **f)
+        dWq, dbq = torch.empty_like(Wq), torch.empty((A, Wq.shape[1]), **f)
+        _ops().gru_seq_q_bwd(dq.contiguous(), hs, ws, W_hh, Wq, k8, dgi, dW, db, dWq, dbq)
+        return dgi, dW, db, dWq, dbq, None, None, None
+
+
+def gru_seq_q(gi, W_hh, b_hh, Wq, bq, keep, grads=None):
+    """gru_seq followed by every agent's q head Linear(H, NA) on every step's output, in one launch each way: gi
+    [A,C,B,3H], W_hh [A,3H,H], b_hh [A,3H], Wq [A,NA,H] (NA <= 16), bq [A,NA], keep [C,A,B] -> q [A,C,B,NA] (the
+    GRU outputs are not returned). grads: optional contiguous views (gW_hh, gb_hh, gW_q, gb_q) shaped like the
+    parameters that the backward writes itself."""
+    assert keep.dim() == 3 and keep.shape == (gi.shape[1], gi.shape[0], gi.shape[2])
+    if not (Wq.dim() == 3 and 1 <= Wq.shape[1] <= 16 and Wq.shape[2] == W_hh.shape[2]):
+        raise ValueError("gru_seq_q: W_q must be [A, NA <= 16, H]")
+    if grads is not None:
+        grads = tuple(grads)
+        if len(grads) != 4 or any(not g.is_contiguous() or g.shape != p.shape
+                                  for g, p in zip(grads, (W_hh, b_hh, Wq, bq))):
+            raise ValueError("gru_seq_q: grads must be four contiguous views shaped like W_hh, b_hh, W_q, b_q")
+    save = torch.is_grad_enabled() and any(t.requires_grad for t in (gi, W_hh, b_hh, Wq, bq))
+    return _GRUSeqQFn.apply(gi, W_hh, b_hh, Wq, bq, keep, save, grads)
+
+
 class _VdnFeatFn(torch.autograd.Function):
     """The VDN QNet feature chain Linear(n_obs,64)-ReLU-Linear(64,32)-ReLU plus the GRUCell input side of every chunk
     step, A agents in ONE launch (flock_vdn_feat_fwd; learners/vdn/net.py:19-33). The backward is the chain rule on

@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell, gru_seq, vdn_feat
+from .core import gru_seq_q, FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell, gru_seq, vdn_feat
 
 HX = 32
 
@@ -46,6 +46,9 @@ class BatchedQNet:
         self.hx_size = HX
         # forward_seq's feature chain as one fused launch (False: batched GEMMs + ReLU passes, the A/B baseline)
         self.fused_features = True
+        # with fused_features: the GRU recurrence and the q head as one launch each way (False: gru_seq + batched
+        # GEMM q head, the A/B baseline)
+        self.fused_qhead = n_actions <= 16
         self.device = torch.device(device)
         self.P = FlatParams(qnet_shapes(n_obs, n_actions, HX, recurrent), self.device, agents=n_agents)
         with torch.no_grad():  # nn.Linear / nn.GRUCell defaults: U(+-1/sqrt(fan_in)), GRU U(+-1/sqrt(hidden))
@@ -71,16 +74,16 @@ class BatchedQNet:
 
     # parameters whose gradients forward_seq(..., direct_grads=True)'s backward writes into the flat grad buffer
     DIRECT = ("feat1.weight", "feat1.bias", "feat2.weight", "feat2.bias", "gru.weight_ih", "gru.bias_ih",
-              "gru.weight_hh", "gru.bias_hh")
+              "gru.weight_hh", "gru.bias_hh", "q.weight", "q.bias")
 
     def forward_seq(self, x, keep, P=None, direct_grads=False):
         """A whole chunk, agent-major: x [A,C,B,n_obs], keep [C,B] (False: the hidden state is reset after that
         step, train_flock.py:34-36) -> q [A,C,B,n_actions] from zero initial hidden states. The feature layers, the
         GRU input GEMM and the q head do not depend on the recurrence, so each runs ONCE over all C steps (one
         batched GEMM of C*B rows per agent); the recurrence itself (hidden GEMM, gates, resets) is one gru_seq
-        launch. Same per-step math as forward_am. direct_grads (the fused path only; returns whether it applied):
-        the backward writes the gradients of DIRECT into self.P.grad's views itself (grads_into(direct=DIRECT))
-        instead of handing them to autograd for a copy."""
+        launch. Same per-step math as forward_am. direct_grads (fused feature chain only): the backward writes the
+        gradients of DIRECT (without the q head's unless fused_qhead) into self.P.grad's views itself; returns
+        (q, the names it writes) for grads_into(direct=...)."""
         P = self.P.params if P is None else P
         A, C, B, n = x.shape
         fused = self.recurrent and n <= 16 and self.fused_features
@@ -95,12 +98,17 @@ class BatchedQNet:
             y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
             if self.recurrent:
                 gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
+        if fused and self.fused_qhead:  # recurrence + q head in one launch each way (flock_gru_seq_q_fwd / _bwd)
+            q = gru_seq_q(gi, P["gru.weight_hh"], P["gru.bias_hh"], P["q.weight"], P["q.bias"],
+                          keep.unsqueeze(1).expand(C, A, B),
+                          grads=None if G is None else [G[k] for k in self.DIRECT[6:]])
+            return (q, self.DIRECT if G is not None else ()) if direct_grads else q
         if self.recurrent:  # the whole chunk's recurrence in one launch each way (flock_gru_seq_fwd / _bwd)
             hs = gru_seq(gi, P["gru.weight_hh"], P["gru.bias_hh"], keep.unsqueeze(1).expand(C, A, B),
                          gW=None if G is None else G["gru.weight_hh"], gb=None if G is None else G["gru.bias_hh"])
             y = hs.view(A, C * B, self.hx_size)
-        q = blinear(y, P["q.weight"], P["q.bias"]).view(A, C, B, -1)
-        return (q, G is not None) if direct_grads else q
+        q = blinear(y, P["q.weight"], P["q.bias"]).view(A, C, B, -1)  # (its gradients go through autograd)
+        return (q, self.DIRECT[:8] if G is not None else ()) if direct_grads else q
 
     def __call__(self, obs, hidden):
         """Reference layout: obs [B,A,n_obs], hidden [B,A,H] -> (q [B,A,n_actions], hidden [B,A,H])."""
@@ -245,7 +253,7 @@ class VDNLearner:
         loss = steps[0]
         for t in range(1, C):
             loss = loss + steps[t]
-        self.q.P.grads_into(loss, Pq, direct=self.q.DIRECT if direct else ())
+        self.q.P.grads_into(loss, Pq, direct=direct)
         with torch.no_grad():
             self.loss.copy_(loss.detach())
 

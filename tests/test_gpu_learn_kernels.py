@@ -219,3 +219,30 @@ def test_direct_grad_views_equal_returned_grads(fused_bwd, cuda):
 
     for name, a_, b_ in zip(("W1", "b1", "W2", "b2", "Wi", "bi", "W_hh", "b_hh"), run(True), run(False)):
         assert torch.equal(a_, b_), name
+
+
+@pytest.mark.parametrize("A,C,B,NA", [(3, 10, 32, 10), (512, 10, 32, 10), (4, 3, 8, 2), (2, 5, 32, 16)])
+def test_gru_seq_q_matches_gru_seq_and_linear(A, C, B, NA, cuda):
+    """flock_gru_seq_q_fwd / _bwd (recurrence + VDN's q head Linear(32, NA) in one launch each way) against gru_seq
+    followed by the batched torch Linear of the same weights: q, and the gradients of gi, W_hh, b_hh, W_q, b_q.
+    Tolerance: fp32 reassociation of the q dot products / weight-gradient sums (rtol 1e-5 forward, 1e-4 grads)."""
+    from marl_range_flocking_amd.learners.core import gru_seq, gru_seq_q
+
+    g = torch.Generator(device=cuda).manual_seed(A + NA)
+    H = 32
+    r = lambda *s: torch.randn(*s, device=cuda, generator=g)  # noqa: E731
+    W = [r(A, C, B, 3 * H), 0.3 * r(A, 3 * H, H), 0.3 * r(A, 3 * H), 0.3 * r(A, NA, H), 0.3 * r(A, NA)]
+    keep = torch.rand(C, A, B, device=cuda, generator=g) > 0.15
+    P1 = [w.clone().requires_grad_(True) for w in W]
+    P2 = [w.clone().requires_grad_(True) for w in W]
+    q1 = gru_seq_q(P1[0], P1[1], P1[2], P1[3], P1[4], keep)
+    hs = gru_seq(P2[0], P2[1], P2[2], keep)
+    q2 = torch.baddbmm(P2[4].unsqueeze(1), hs.reshape(A, C * B, H), P2[3].transpose(1, 2)).view(A, C, B, NA)
+    torch.testing.assert_close(q1, q2, rtol=1e-5, atol=1e-5)
+    up = r(A, C, B, NA)
+    d1 = torch.autograd.grad((q1 * up).sum(), P1)
+    d2 = torch.autograd.grad((q2 * up).sum(), P2)
+    for name, a_, b_ in zip(("gi", "W_hh", "b_hh", "W_q", "b_q"), d1, d2):
+        torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-5 * float(b_.abs().max()), msg=name)
+    with torch.no_grad():  # the target network's call (no saved states)
+        torch.testing.assert_close(gru_seq_q(*W, keep), q2.detach(), rtol=1e-5, atol=1e-5)

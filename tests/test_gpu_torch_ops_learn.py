@@ -332,3 +332,39 @@ def test_step_store_opcheck(flock, cuda):
     torch.library.opcheck(flock.step_uw_discrete_store.default, args, test_utils=TESTS)
     with pytest.raises(RuntimeError, match="ring"):
         flock.step_v2_store(*st, None, ring, None, None, prev, [cap, 0, 1, 0, 0, 0], k, 60.0, 14.0, 2.5)
+
+
+def test_gru_seq_q_ops(flock, cuda):
+    """flock::gru_seq_q_fwd / _bwd (the recurrence with VDN's q head fused): opcheck (schema, Meta, fake tensors)
+    and bitwise equal to the C ABI entry points; the forward without hs / ws (the target network's call)."""
+    g = torch.Generator(device=cuda).manual_seed(9)
+    A, C, B, H, NA = 3, 10, 32, 32, 10
+    rnd = lambda *s: torch.randn(*s, device=cuda, generator=g) * 0.3  # noqa: E731
+    gis, whh, bhh, wq, bq = rnd(A, C, B, 3 * H), rnd(A, 3 * H, H) * 0.2, rnd(A, 3 * H), rnd(A, NA, H), rnd(A, NA)
+    keep = (torch.rand(C, 1, B, device=cuda, generator=g) > 0.2).expand(C, A, B)
+    hs, wss, q = (torch.zeros(A, C, B, H, device=cuda), torch.zeros(A, C, B, 4 * H, device=cuda),
+                  torch.zeros(A, C, B, NA, device=cuda))
+    torch.library.opcheck(flock.gru_seq_q_fwd.default, (gis, whh, bhh, wq, bq, keep, hs.clone(), wss.clone(),
+                                                        q.clone()), test_utils=TESTS)
+    flock.gru_seq_q_fwd(gis, whh, bhh, wq, bq, keep, hs, wss, q)
+    q_nohs = torch.zeros_like(q)
+    flock.gru_seq_q_fwd(gis, whh, bhh, wq, bq, keep, None, None, q_nohs)
+    assert torch.equal(q, q_nohs)
+    hs2, wss2, q2 = torch.zeros_like(hs), torch.zeros_like(wss), torch.zeros_like(q)
+    k8 = keep.view(torch.uint8)
+    st = k8.stride()
+    _check(_native.lib().flock_gru_seq_q_fwd(_st(cuda), A, C, B, H, NA, _p(gis), _p(whh), _p(bhh), _p(wq), _p(bq),
+                                             _p(k8), st[0], st[1], st[2], _p(hs2), _p(wss2), _p(q2)),
+           "flock_gru_seq_q_fwd")
+    assert torch.equal(hs, hs2) and torch.equal(wss, wss2) and torch.equal(q, q2)
+    dq = rnd(A, C, B, NA)
+    outs = [torch.zeros(A, C, B, 3 * H, device=cuda), torch.zeros(A, 3 * H, H, device=cuda),
+            torch.zeros(A, 3 * H, device=cuda), torch.zeros(A, NA, H, device=cuda), torch.zeros(A, NA, device=cuda)]
+    torch.library.opcheck(flock.gru_seq_q_bwd.default, (dq, hs, wss, whh, wq, keep, *_clone(*outs)),
+                          test_utils=TESTS)
+    flock.gru_seq_q_bwd(dq, hs, wss, whh, wq, keep, *outs)
+    ref = _clone(*outs)
+    _check(_native.lib().flock_gru_seq_q_bwd(_st(cuda), A, C, B, H, NA, _p(dq), _p(hs), _p(wss), _p(whh), _p(wq),
+                                             _p(k8), st[0], st[1], st[2], *map(_p, ref)), "flock_gru_seq_q_bwd")
+    for x, y in zip(outs, ref):
+        assert torch.equal(x, y)
