@@ -2104,14 +2104,9 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->seq = 0;
     // the learner stream waits for each snapshot on the device (the round's row launch spins on gate[0]) instead of a
     // cross-queue barrier packet; FLOCK_SC_GATE=0 (read here) keeps the event waits. Graph replays keep the events
-    // (their captured arguments cannot carry a new sequence number). The spin needs the two streams' kernels to run
-    // concurrently: under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION, which serialises dispatches) a
-    // round launched ahead of its snapshot would wait out its bound, so the event waits are the default there
-    // (FLOCK_SC_GATE=1 forces the gate)
+    // (their captured arguments cannot carry a new sequence number)
     const char* gte = getenv("FLOCK_SC_GATE");
-    const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
-    const bool gate_on = gte ? gte[0] != '0' : !(pmc && pmc[0] && pmc[0] != '0');
-    if (!rc && !p->graphs && p->diag == 0 && gate_on) {
+    if (!rc && !p->graphs && p->diag == 0 && !(gte && gte[0] == '0')) {
         if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
             hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
             rc = fail(-4, "flock_sc_pipeline_create: gate");
