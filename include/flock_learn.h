@@ -222,10 +222,6 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
-/* Waits for learner_stream and reports whether any round of the pipeline gave up waiting for its snapshot: the
- * critic phase's first launch waits for the snapshot on the device (a sequence number the snapshot kernel publishes,
- * instead of a cross-queue event; bounded at 0.5 s, after which it proceeds and sets the flag this returns as -6). */
-int flock_sc_pipeline_check(FlockScPipeline* p, void* learner_stream);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);
 
 #ifdef __cplusplus

@@ -131,7 +131,6 @@ SIGNATURES.update({
                                  ctypes.POINTER(FlockScRows)],
     "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],
     "flock_sc_pipeline_flush": [_c_void_p, _c_void_p],
-    "flock_sc_pipeline_check": [_c_void_p, _c_void_p],
     "flock_sc_pipeline_destroy": [_c_void_p],
 })
 RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,

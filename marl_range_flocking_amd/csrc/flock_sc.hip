@@ -139,10 +139,6 @@ struct RowArgs {
     const float* actors_target;
     int64_t stride;
     float gamma, invB;
-    // device-side snapshot gate (flock_sc_pipeline): the critic phase's row launch waits until gate[0] >= gate_seq
-    // (published by the snapshot kernel) instead of a cross-queue event wait; NULL: no wait
-    unsigned long long* gate;
-    unsigned long long gate_seq;
 };
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -645,28 +641,10 @@ __device__ unsigned long long g_scmark[4096][8];
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
 // blocks past them).
-// gate[0]: the last published snapshot sequence number, gate[1]: the snapshot blocks' arrival counter, gate[2]: set
-// when a waiter gave up (flock_sc_pipeline_check reports it)
-constexpr unsigned long long kGateTimeoutTicks = 50000000ull;  // 0.5 s of s_memrealtime (100 MHz)
-__device__ __forceinline__ void gate_wait(unsigned long long* gate, unsigned long long seq) {
-    if (threadIdx.x == 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while ((long long)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - seq) < 0) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
-                __hip_atomic_fetch_or(gate + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(4);
-        }
-    }
-    __syncthreads();
-}
-
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     SC_PROF(0);
     SC_PRIO();
-    if (ac.gate && (int)blockIdx.y < npc) gate_wait(ac.gate, ac.gate_seq);  // the critic phase reads the snapshot
     if ((int)blockIdx.y < npc)
         c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
     else
@@ -1499,8 +1477,6 @@ RowArgs row_args(const FlockScUpdate* u) {
     a.critic = u->critic; a.actors = u->actors; a.actors_target = u->actors_target; a.stride = u->actor_stride;
     a.gamma = u->gamma;
     a.invB = 1.0f / (float)u->B;
-    a.gate = nullptr;  // only flock_sc_pipeline_learn gates a critic phase on its snapshot
-    a.gate_seq = 0;
     return a;
 }
 
@@ -1825,9 +1801,13 @@ __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t see
 
 // learn() prologue with a minibatch snapshot: the sampled rows of every replay field are copied to staging rows
 // 0..B-1, so the update can read the staging copy (with the identity index) while the next env step rewrites the ring
-__device__ __forceinline__ void snapshot_row(int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
-                                             int in_dim, int n_actions, const FlockScRows& src,
-                                             const FlockScRows& dst, int vec, int r) {
+__global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
+                                                        int64_t* idx_out, int64_t* agent_out, int64_t agent,
+                                                        int in_dim, int n_actions, FlockScRows src,
+                                                        FlockScRows dst, int vec) {
+    const int r = blockIdx.x * 64 + threadIdx.x;
+    if (r == 0) *agent_out = agent;
+    if (r >= B) return;
     const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
     const uint64_t u = ((uint64_t)q.x << 32) | q.y;
     const int64_t row = (int64_t)(u % (uint64_t)rows);  // the row sc_prep samples for r
@@ -1856,39 +1836,11 @@ __device__ __forceinline__ void snapshot_row(int B, int64_t rows, uint64_t seed,
     dst.reward[r] = rw;
     dst.terminal[r] = te;
 }
-__global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
-                                                        int64_t* idx_out, int64_t* agent_out, int64_t agent,
-                                                        int in_dim, int n_actions, FlockScRows src,
-                                                        FlockScRows dst, int vec, unsigned long long* gate,
-                                                        unsigned long long seq) {
-    const int r = blockIdx.x * 64 + threadIdx.x;
-    if (r == 0) *agent_out = agent;
-    if (r < B) snapshot_row(B, rows, seed, counter, idx_out, in_dim, n_actions, src, dst, vec, r);
-    if (gate) {  // publish seq once every block's rows are written back to memory (agent-scope release per block)
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned long long prev =
-                __hip_atomic_fetch_add(gate + 1, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-            if (prev == gridDim.x - 1ull) {
-                __hip_atomic_store(gate + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(gate, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-}
 
 }  // namespace
 
 // the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
 void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
-
-namespace {
-// the snapshot gate of the pipeline call in progress (flock_sc_pipeline_learn sets them around its snapshot launch;
-// NULL / 0 for every other caller of flock_sc_prep_snapshot)
-thread_local unsigned long long* g_snap_gate = nullptr;
-thread_local unsigned long long g_snap_seq = 0;
-}  // namespace
 
 extern "C" {
 
@@ -1906,8 +1858,7 @@ int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uin
     for (const FlockScRows* x : rs)
         vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
     hipLaunchKernelGGL(sc_prep_snapshot, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, B, rows, seed,
-                       counter, idx_out, agent_out, agent, in_dim, n_actions, *ring, *staging, vec, g_snap_gate,
-                       g_snap_seq);
+                       counter, idx_out, agent_out, agent, in_dim, n_actions, *ring, *staging, vec);
     return launched();
 }
 
@@ -2005,10 +1956,6 @@ struct FlockScPipeline {
     int diag;  // -DFLOCK_SC_PIPELINE_DIAG=<bits> builds only (timing diagnostics; results are wrong): 1 no learner wait on the
                // snapshot, 2 no env wait on the slot, 3 neither
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
-    // device-side snapshot gate (direct launches): gate[0] published sequence, gate[1] snapshot arrivals, gate[2]
-    // timeout flag; seq counts the snapshots this pipeline published. NULL: cross-queue event waits
-    unsigned long long* gate;
-    unsigned long long seq;
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
@@ -2100,21 +2047,6 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->slot = 0;
     p->pending = -1;
     p->pending_agent = -1;
-    p->gate = nullptr;
-    p->seq = 0;
-    // the learner stream waits for each snapshot on the device (the round's row launch spins on gate[0]) instead of a
-    // cross-queue barrier packet; FLOCK_SC_GATE=0 (read here) keeps the event waits. Graph replays keep the events
-    // (their captured arguments cannot carry a new sequence number)
-    const char* gte = getenv("FLOCK_SC_GATE");
-    if (!rc && !p->graphs && p->diag == 0 && !(gte && gte[0] == '0')) {
-        if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
-            hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
-            rc = fail(-4, "flock_sc_pipeline_create: gate");
-    }
-    for (int i = 0; i < n_slots; ++i) {
-        p->jc[i].a.gate = nullptr;
-        p->ja[i].a.gate = nullptr;
-    }
     if (rc) {
         flock_sc_pipeline_destroy(p);
         return nullptr;
@@ -2130,21 +2062,11 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const FlockScUpdate& u = p->u[s];
     if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
-    if (p->gate) {
-        g_snap_gate = p->gate;
-        g_snap_seq = ++p->seq;
-        p->jc[s].a.gate = p->gate;  // this learn's critic phase waits for seq on the device
-        p->jc[s].a.gate_seq = p->seq;
-    }
     int rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                     u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
-    g_snap_gate = nullptr;
-    g_snap_seq = 0;
     if (rc) return rc;
-    bool ok = true;
-    if (!p->gate)
-        ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
-             ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
+    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
+              ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
     if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     const int q = p->pending;
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
@@ -2189,19 +2111,8 @@ int flock_sc_mark_read(unsigned long long* host) {
 }
 #endif
 
-int flock_sc_pipeline_check(FlockScPipeline* p, void* learner_stream) {
-    if (!p) return fail(-3, "flock_sc_pipeline_check: NULL pipeline");
-    if (!p->gate) return 0;
-    unsigned long long flag = 0;
-    if (hipStreamSynchronize((hipStream_t)learner_stream) != hipSuccess ||
-        hipMemcpy(&flag, p->gate + 2, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_check: copy failed");
-    return flag ? fail(-6, "flock_sc_pipeline: a round gave up waiting for its snapshot (device gate timeout)") : 0;
-}
-
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;
-    if (p->gate) (void)hipFree(p->gate);
     for (int i = 0; i < p->n; ++i) {
         hipGraphExec_t* gs[3] = {&p->merged[i], &p->conly[i], &p->aonly[i]};
         for (hipGraphExec_t* g : gs)

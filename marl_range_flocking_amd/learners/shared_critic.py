@@ -542,14 +542,10 @@ class SharedCriticLearner:
         return True
 
     def pipeline_flush(self, learner_stream):
-        """Enqueue the pending actor phase of the last pipeline_learn (no-op when none), then wait for learner_stream
-        and check the pipeline's device snapshot gate (flock_sc_pipeline_check)."""
+        """Enqueue the pending actor phase of the last pipeline_learn (no-op when none)."""
         if self.__dict__.get("_pipe") is not None:
             _native.check(_native.lib().flock_sc_pipeline_flush(self._pipe, learner_stream),
                           "flock_sc_pipeline_flush", learn=True)
-            # waits for learner_stream: raises if a round gave up waiting for its snapshot (device gate timeout)
-            _native.check(_native.lib().flock_sc_pipeline_check(self._pipe, learner_stream),
-                          "flock_sc_pipeline_check", learn=True)
 
     def __del__(self):
         h = self.__dict__.get("_pipe")
