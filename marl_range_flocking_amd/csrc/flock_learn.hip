@@ -712,9 +712,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     const int tid = threadIdx.x, i = tid % H, bstep = kBlock / H;
     // QH: W_q in LDS behind carry ([NA][H]); dW_q[:, i] partials in registers; lanes i < NA also sum db_q[i]
     float* wq = carry + B * H;
-    float aqw[NQA], aqb = 0.0f;
-#pragma unroll
-    for (int o = 0; o < NQA; ++o) aqw[o] = 0.0f;
+    float* dqs = wq + (QH ? qh.NA * H : 0);  // QH: [B][NA] dq of the step
+    float aqb = 0.0f;
+    // dW_q partials: thread-private LDS slots [kBlock / H][NA][H] (no sharing: no barrier; keeps the 256-VGPR
+    // budget of two waves per SIMD without spills)
+    float* aqs = dqs + (QH ? B * qh.NA : 0);
+    const int grp0 = tid / H;
+    if (QH)
+        for (int o = 0; o < qh.NA; ++o) aqs[(grp0 * qh.NA + o) * H + i] = 0.0f;
     if (QH)
         for (int e = tid; e < qh.NA * H; e += kBlock) wq[e] = qh.W[a * qh.NA * H + e];
     const float* Wa = W + a * G * H;
@@ -734,22 +739,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
             if (t > 0 && keep[(t - 1) * kt + a * ka + b * kb]) v = hs[((a * C + t - 1) * B + b) * H + (e - b * H)];
             hprev[e] = v;
         }
-        __syncthreads();  // carry (previous iteration) and hprev visible
+        if (QH)  // this step's dq rows (contiguous [B][NA]) into LDS: one coalesced round trip, broadcast reads below
+            for (int e = tid; e < B * qh.NA; e += kBlock) dqs[e] = dhs[(a * C + t) * B * qh.NA + e];
+        __syncthreads();  // carry (previous iteration), hprev and dq visible
         for (int b = tid / H; b < B; b += bstep) {
             const int64_t row = (a * C + t) * B + b;
             const float* w = ws + row * 4 * H;
             const float r = w[i], z = w[H + i], nn = w[2 * H + i], ghn = w[3 * H + i];
             float dho;
             if (QH) {  // dL/dh' of the q head: dq W_q, k-ordered; and its dW_q / db_q partials
-                const float* dq = dhs + row * qh.NA;
+                const float* dq = dqs + b * qh.NA;
                 const float ho = hs[row * H + i];
                 dho = 0.0f;
-#pragma unroll
+#pragma unroll 2
                 for (int o = 0; o < NQA; ++o)
                     if (o < qh.NA) {
                         const float d = dq[o];
                         dho = fmaf(d, wq[o * H + i], dho);
-                        aqw[o] = fmaf(d, ho, aqw[o]);
+                        float* slot = aqs + (grp0 * qh.NA + o) * H + i;
+                        *slot = fmaf(d, ho, *slot);
                     }
                 if (i < qh.NA) aqb += dq[i];
             } else {
@@ -828,21 +836,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
     }
     if (tid < G) db[a * G + tid] = accb;
     if (QH) {  // the q head's gradients: the bstep row groups' partials summed in group order
-        float* red = dgh;  // [bstep][NA][H] + [bstep][NA] over dgh.. (the loop is done with them: its last barrier)
+        float* redb = dgh;  // [bstep][NA] db_q partials (the loop is done with dgh: its last barrier)
         const int grp = tid / H;
-#pragma unroll
-        for (int o = 0; o < NQA; ++o)
-            if (o < qh.NA) red[(grp * qh.NA + o) * H + i] = aqw[o];
-        if (i < qh.NA) red[bstep * qh.NA * H + grp * qh.NA + i] = aqb;
+        if (i < qh.NA) redb[grp * qh.NA + i] = aqb;
         __syncthreads();
         for (int e = tid; e < qh.NA * H; e += kBlock) {
             float s = 0.0f;
-            for (int q = 0; q < bstep; ++q) s += red[q * qh.NA * H + e];
+            for (int q = 0; q < bstep; ++q) s += aqs[q * qh.NA * H + e];
             qh.dW[a * qh.NA * H + e] = s;
         }
         if (tid < qh.NA) {
             float s = 0.0f;
-            for (int q = 0; q < bstep; ++q) s += red[bstep * qh.NA * H + q * qh.NA + tid];
+            for (int q = 0; q < bstep; ++q) s += redb[q * qh.NA + tid];
             qh.db[a * qh.NA + tid] = s;
         }
     }
@@ -1060,7 +1065,8 @@ int flock_gru_seq_q_bwd(void* stream, int A, int C, int B, int H, int NA, const 
     if (NA < 1 || NA > kMaxQ) return fail(-2, "flock_gru_seq_q_bwd: 1 <= n_actions <= 16");
     // dgh, h_prev, carry, W_q; the q head's final reduction ((kBlock / H) (NA H + NA) floats) reuses the same space
     // from its start once the recurrence is done
-    const size_t body = (size_t)B * (3 * H + 2 * H) + (size_t)NA * H, red = (size_t)(kBlock / H) * NA * (H + 1);
+    const size_t body = (size_t)B * (3 * H + 2 * H + NA) + (size_t)NA * H + (size_t)(kBlock / H) * NA * H;
+    const size_t red = (size_t)(kBlock / H) * NA;  // the db_q partials over dgh at the end
     const size_t lds = (body > red ? body : red) * sizeof(float);
     if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_q_bwd: B too large for LDS");
     const QHeadBwd qh{w_q, dw_q, db_q, NA};
@@ -1073,7 +1079,6 @@ int flock_gru_seq_q_bwd(void* stream, int A, int C, int B, int H, int NA, const 
         return launched();
     };
     // registers sized for the head: the smallest instantiation that holds NA
-    if (NA <= 2) return go(gru_seq_bwd_kernel<32, 2>);
     if (NA <= 4) return go(gru_seq_bwd_kernel<32, 4>);
     if (NA <= 6) return go(gru_seq_bwd_kernel<32, 6>);
     if (NA <= 8) return go(gru_seq_bwd_kernel<32, 8>);
