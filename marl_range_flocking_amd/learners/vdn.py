@@ -98,7 +98,10 @@ class BatchedQNet:
             y = F.relu(blinear(y, P["feat2.weight"], P["feat2.bias"]))
             if self.recurrent:
                 gi = blinear(y, P["gru.weight_ih"], P["gru.bias_ih"]).view(A, C, B, -1)
-        if fused and self.fused_qhead:  # recurrence + q head in one launch each way (flock_gru_seq_q_fwd / _bwd)
+        NA = self.n_actions
+        # the fused backward's LDS: B (5 H + NA) + 9 NA H floats of 160 KB (B <= 224 at NA = 10); else gru_seq + GEMMs
+        qfits = B * (5 * self.hx_size + NA) + 9 * NA * self.hx_size <= 40960
+        if fused and self.fused_qhead and qfits:  # recurrence + q head in one launch each way (flock_gru_seq_q_*)
             q = gru_seq_q(gi, P["gru.weight_hh"], P["gru.bias_hh"], P["q.weight"], P["q.bias"],
                           keep.unsqueeze(1).expand(C, A, B),
                           grads=None if G is None else [G[k] for k in self.DIRECT[6:]])

@@ -246,3 +246,20 @@ def test_gru_seq_q_matches_gru_seq_and_linear(A, C, B, NA, cuda):
         torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-5 * float(b_.abs().max()), msg=name)
     with torch.no_grad():  # the target network's call (no saved states)
         torch.testing.assert_close(gru_seq_q(*W, keep), q2.detach(), rtol=1e-5, atol=1e-5)
+
+
+def test_vdn_forward_seq_large_batch_falls_back(cuda):
+    """forward_seq at a batch the fused q-head backward's LDS cannot hold (B = 256, NA = 10) takes gru_seq + the
+    batched q GEMMs instead of failing; same q as the fused path at a small batch slice (tolerance: fp32
+    reassociation of the q head)."""
+    from marl_range_flocking_amd.learners.vdn import BatchedQNet
+
+    g = torch.Generator(device=cuda).manual_seed(3)
+    net = BatchedQNet(4, 4, 10, device=cuda, generator=g)
+    x = torch.rand(4, 10, 256, 4, device=cuda, generator=g)
+    keep = torch.rand(10, 256, device=cuda, generator=g) > 0.1
+    P = net.P.new_leaves()
+    q, names = net.forward_seq(x, keep, P, direct_grads=True)
+    assert names == net.DIRECT[:8]  # fused feature chain, unfused q head
+    q_small = net.forward_seq(x[:, :, :32].contiguous(), keep[:, :32], P)
+    torch.testing.assert_close(q[:, :, :32], q_small, rtol=1e-5, atol=1e-5)
