@@ -989,7 +989,10 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
     const int o = per_in ? e / rp.in : e;
     const int i = per_in ? e - o * rp.in : e;
     const bool prod = rp.mode == 1 || rp.mode == 2 || rp.mode == 4;
-    constexpr int kRB = 8;  // rows per batch of loads (row group q takes rows q, q + 16, ...)
+#ifndef FLOCK_RED_RB
+#define FLOCK_RED_RB 8
+#endif
+    constexpr int kRB = FLOCK_RED_RB;  // rows per batch of loads (row group q takes rows q, q + 16, ...)
     float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
     auto load = [&](int r0) {
 #pragma unroll

@@ -8,4 +8,4 @@ B=marl_range_flocking_amd/_build
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 "$@" -c -I include \
     -o $B/flock_sc_$name.o marl_range_flocking_amd/csrc/flock_sc.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -shared -o $B/libflock_amd_$name.so \
-    $B/flock_env.hip.o $B/flock_learn.hip.o $B/flock_sc_$name.o
+    $B/flock_env.hip.o $B/flock_act.hip.o $B/flock_learn.hip.o $B/flock_sc_$name.o
