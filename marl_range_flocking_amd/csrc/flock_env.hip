@@ -241,6 +241,19 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
+// replay-ring stores of the fused insert: non-temporal (the rows are read back only by the learner's minibatch
+// gathers, long after the XCD's L2 has turned over). Same-box A/B at config 3 (`profiles/r03/ntring/`): env kernel
+// alone 42.5-43.8 -> 39.2-42.1 us; non-temporal stores for the other output streams too were slower (44.9-45.2 us).
+// -DFLOCK_PLAIN_RING: plain stores (A/B builds)
+template <typename T>
+__device__ __forceinline__ void st_ring(T* p, T v) {
+#ifdef FLOCK_PLAIN_RING
+    *p = v;
+#else
+    __builtin_nontemporal_store(v, p);
+#endif
+}
+
 // pair_d2 of two candidates at once: the squares and sums as packed f32 ops (v_pk_mul / v_pk_add, one candidate
 // per half; each half rounds exactly like the scalar mul, mul, add), so both packed issue slots do useful work.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -266,7 +279,11 @@ __device__ __forceinline__ T ldnt(const T* p) {
 }
 template <typename T>
 __device__ __forceinline__ void stnt(T* p, T v) {
+#ifdef FLOCK_NT_STORES  // A/B builds: the per-agent output streams non-temporal, the loads plain
+    __builtin_nontemporal_store(v, p);
+#else
     *p = v;
+#endif
 }
 #endif
 template <bool PERIODIC>
@@ -1375,9 +1392,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 if (row >= p.r_cap) row -= p.r_cap;
                 const int64_t e = row * p.r_group + r_slot;  // this agent's element of the row
                 if (L - 2 == 4 && p.k == 4 && !p.r_astate && !p.r_anew) {  // 16-B stores
-                    stnt(reinterpret_cast<f32x4*>(p.r_state + e * p.k),
+                    st_ring(reinterpret_cast<f32x4*>(p.r_state + e * p.k),
                          f32x4{prev_obs[0], prev_obs[1 % (L - 2)], prev_obs[2 % (L - 2)], prev_obs[3 % (L - 2)]});
-                    stnt(reinterpret_cast<f32x4*>(p.r_new + e * p.k),
+                    st_ring(reinterpret_cast<f32x4*>(p.r_new + e * p.k),
                          f32x4{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]});
                 } else {
 #pragma unroll
@@ -1390,11 +1407,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                         }
                 }
                 if (p.r_ids)
-                    stnt(p.r_action + e, act_in.x);
+                    st_ring(p.r_action + e, act_in.x);
                 else
-                    stnt(reinterpret_cast<f32x2*>(p.r_action) + e, f32x2{act_in.x, act_in.y});
-                stnt(p.r_reward + e, r);
-                if (!p.r_env_done) stnt(p.r_term + e, (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f);
+                    st_ring(reinterpret_cast<f32x2*>(p.r_action) + e, f32x2{act_in.x, act_in.y});
+                st_ring(p.r_reward + e, r);
+                if (!p.r_env_done) st_ring(p.r_term + e, (coll != 0) == (p.r_done != 0) ? 1.0f : 0.0f);
             }
         }
     }
