@@ -275,7 +275,11 @@ __device__ __forceinline__ void stnt(T* p, T v) {
 #else
 template <typename T>
 __device__ __forceinline__ T ldnt(const T* p) {
+#ifdef FLOCK_NT_LOADS  // A/B builds: the per-agent input streams non-temporal
+    return __builtin_nontemporal_load(p);
+#else
     return *p;
+#endif
 }
 template <typename T>
 __device__ __forceinline__ void stnt(T* p, T v) {
@@ -286,6 +290,18 @@ __device__ __forceinline__ void stnt(T* p, T v) {
 #endif
 }
 #endif
+
+// inputs read once and never written back by the step (the action, the previous observation row of the fused
+// insert); -DFLOCK_NT_ONCE (A/B builds): non-temporal
+template <typename T>
+__device__ __forceinline__ T ld_once(const T* p) {
+#ifdef FLOCK_NT_ONCE
+    return __builtin_nontemporal_load(p);
+#else
+    return ldnt(p);
+#endif
+}
+
 template <bool PERIODIC>
 __device__ __forceinline__ f32x2 pair_d2x2(float xi, float yi, float x0, float y0, float x1, float y1, float box) {
     float dx0 = __fsub_rn(xi, x0), dx1 = __fsub_rn(xi, x1);
@@ -908,7 +924,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (active && p.r_state && r_unit >= p.r_skip) {
             const float* po = p.r_prev + a * p.k;
             if (L - 2 == 4 && p.k == 4) {  // one 16-B load (rows of 4 floats are 16-B aligned)
-                const f32x4 v = ldnt(reinterpret_cast<const f32x4*>(po));
+                const f32x4 v = ld_once(reinterpret_cast<const f32x4*>(po));
                 prev_obs[0] = v.x;
                 prev_obs[1 % (L - 2)] = v.y;
                 prev_obs[2 % (L - 2)] = v.z;
@@ -968,7 +984,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         x = pp.x;
         y = pp.y;
         if (variant == FLOCK_VARIANT_V2) {  // gym_flock_v2.py:317-350 (heading=True)
-            const f32x2 ac = ldnt(reinterpret_cast<const f32x2*>(p.action) + a);
+            const f32x2 ac = ld_once(reinterpret_cast<const f32x2*>(p.action) + a);
             act_in = make_float2(ac.x, ac.y);
             const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
             h = __fadd_rn(ldnt(p.heading + a), __fmul_rn(ang, p.dt));        // :329
