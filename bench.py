@@ -489,6 +489,12 @@ def main():
     torch.cuda.synchronize(dev)
     barrier(world)
     el = time.perf_counter() - t0
+    handoff = None
+    if hook is not None and hasattr(hook, "learner") and hasattr(hook.learner, "pipeline_check"):
+        hook.learner.pipeline_check()  # raises if a round gave up waiting for its snapshot (device-side gate)
+        if hook.learner.__dict__.get("_pipe") is not None:
+            handoff = ("device gate (sc1 snapshot + polled sequence number)" if hook.learner.pipeline().gated()
+                       else "cross-queue event wait")
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -570,6 +576,7 @@ def main():
         "host_enqueue_us_per_step": host_us,
         "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
                       "one Python step per vectorized step (torch.ops.flock)"),
+        "snapshot_handoff": handoff,
         "higher_is_better": True,
         "scaling": "strong" if args.global_split else "weak",
         "vs_baseline": None,

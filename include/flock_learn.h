@@ -223,6 +223,25 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
                             uint64_t counter, int64_t agent);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);
+/* Data-parallel rounds (one replica per GPU, the same learn() sequence on every rank): after this call every round
+ * of the pipeline runs as gradients only (do_adam = 0, critic_grad = bucket, actor_grad_out = bucket + actor_off),
+ * then `allreduce(ctx, bucket + lo, hi - lo, learner_stream)` over the part the round wrote (the critic gradient
+ * [0, critic_floats) with a critic phase, the actor gradient [actor_off, bucket_floats) with an actor phase), which
+ * must enqueue a SUM all-reduce of those floats on learner_stream (e.g. RCCL) and return 0, then
+ * flock_sc_round_adam with grad_scale (device scalar, 1 / world: the mean). Bitwise one process learning on the
+ * union of the ranks' minibatches when the sums are exact in any order (SharedCriticLearner.dp_learn). Call before
+ * the first flock_sc_pipeline_learn. */
+/* The device-side snapshot gate (single GPU, the default; FLOCK_SC_GATE=0 or rocprofv3 counter collection, which
+ * serialises dispatches: cross-queue event waits instead): the snapshot kernel writes the staging rows `sc1` and
+ * publishes a sequence number after all its stores completed, and the round's critic row blocks poll it (bounded,
+ * 0.2 s) instead of the learner stream waiting for an event. A waiter that gives up sets an error word and computes
+ * nothing; flock_sc_pipeline_check (synchronous: call after synchronising the learner stream) returns -6 then.
+ * flock_sc_pipeline_gated: 1 when the gate is in use. */
+int flock_sc_pipeline_check(FlockScPipeline* p);
+int flock_sc_pipeline_gated(const FlockScPipeline* p);
+typedef int (*FlockAllreduceFn)(void* ctx, float* data, int64_t n, void* learner_stream);
+int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_off,
+                             int64_t bucket_floats, const float* grad_scale, FlockAllreduceFn allreduce, void* ctx);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,30 @@ class FlockScUpdate(ctypes.Structure):
                 + [("update_rate", _c_int), ("critic_view", _c_void_p), ("actor_grad_out", _c_void_p)])
 
 
+def sc_update(learner, job, dims, hyper):
+    """The FlockScUpdate of a torch.ops.flock.sc_round argument list (learner state [13], job [9 or 10], dims [7],
+    hyper [7]; csrc/flock_torch_sc.h), for callers of the C ABI (the op-vs-C-ABI tests)."""
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else None  # noqa: E731
+    L = learner
+    B, n_in, na, fc1, fc2, rate, do_adam = dims
+    u = FlockScUpdate(B=B, in_dim=n_in, n_actions=na, fc1=fc1, fc2=fc2, do_adam=do_adam, idx=p(job[0]),
+                      agent=p(job[1]), ring_state=p(job[2]), ring_new_state=p(job[3]), ring_action=p(job[4]),
+                      ring_reward=p(job[5]), ring_terminal=p(job[6]), critic=p(L[0]), critic_grad=p(L[1]),
+                      critic_exp_avg=p(L[2]), critic_exp_avg_sq=p(L[3]), critic_step=p(L[4]), actors=p(L[5]),
+                      actors_grad=p(L[6]), actors_exp_avg=p(L[7]), actors_exp_avg_sq=p(L[8]), actors_target=p(L[9]),
+                      actor_steps=p(L[10]), actor_stride=L[5].numel() // L[10].numel(), losses=p(L[11]),
+                      workspace=p(job[7]), counters=p(L[12]), update_rate=rate, critic_view=p(job[8]),
+                      actor_grad_out=p(job[9]) if len(job) > 9 else None)
+    for n, v in zip(("alpha", "beta", "gamma", "beta1", "beta2", "eps", "tau"), hyper):
+        setattr(u, n, v)
+    return u
+
+
+def sc_rows(rows):
+    """FlockScRows of [state, new_state, action, reward, terminal] tensors."""
+    return FlockScRows(*[ctypes.c_void_p(t.data_ptr()) for t in rows])
+
+
 class FlockRingField(ctypes.Structure):
     """Mirror of ``FlockRingField`` (include/flock_learn.h)."""
 
@@ -131,6 +155,10 @@ SIGNATURES.update({
                                  ctypes.POINTER(FlockScRows)],
     "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],
     "flock_sc_pipeline_flush": [_c_void_p, _c_void_p],
+    "flock_sc_pipeline_check": [_c_void_p],
+    "flock_sc_pipeline_gated": [_c_void_p],
+    "flock_sc_pipeline_set_dp": [_c_void_p, _c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_void_p,
+                                 _c_void_p, _c_void_p],
     "flock_sc_pipeline_destroy": [_c_void_p],
 })
 RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,

@@ -47,6 +47,7 @@
 #include <string.h>
 
 #include "flock_amd.h"
+#include "flock_mem.h"
 
 #pragma clang fp contract(off)
 
@@ -241,14 +242,18 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
+using flock_mem::st_sc1;  // write-through stores (csrc/flock_mem.h): A/B builds below
+
 // replay-ring stores of the fused insert: non-temporal (the rows are read back only by the learner's minibatch
 // gathers, long after the XCD's L2 has turned over). Same-box A/B at config 3 (`profiles/r03/ntring/`): env kernel
 // alone 42.5-43.8 -> 39.2-42.1 us; non-temporal stores for the other output streams too were slower (44.9-45.2 us).
-// -DFLOCK_PLAIN_RING: plain stores (A/B builds)
+// -DFLOCK_PLAIN_RING: plain stores, -DFLOCK_SC1_RING: write-through stores (A/B builds)
 template <typename T>
 __device__ __forceinline__ void st_ring(T* p, T v) {
-#ifdef FLOCK_PLAIN_RING
+#if defined(FLOCK_PLAIN_RING)
     *p = v;
+#elif defined(FLOCK_SC1_RING)
+    st_sc1(p, v);
 #else
     __builtin_nontemporal_store(v, p);
 #endif
@@ -283,8 +288,10 @@ __device__ __forceinline__ T ldnt(const T* p) {
 }
 template <typename T>
 __device__ __forceinline__ void stnt(T* p, T v) {
-#ifdef FLOCK_NT_STORES  // A/B builds: the per-agent output streams non-temporal, the loads plain
+#if defined(FLOCK_NT_STORES)  // A/B builds: the per-agent output streams non-temporal, the loads plain
     __builtin_nontemporal_store(v, p);
+#elif defined(FLOCK_SC1_OUT)  // A/B builds: the per-agent output streams write-through
+    st_sc1(p, v);
 #else
     *p = v;
 #endif

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include "flock_learn.h"
+#include "flock_mem.h"
 #include "learn_internal.h"
 
 namespace {
@@ -139,6 +140,10 @@ struct RowArgs {
     const float* actors_target;
     int64_t stride;
     float gamma, invB;
+    // device-side snapshot gate (flock_sc_pipeline): the critic phase's row blocks wait until gate[0] >= gate_seq
+    // (published by the snapshot kernel) instead of a cross-queue event wait; NULL: no wait
+    unsigned long long* gate;
+    unsigned long long gate_seq;
 };
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -319,21 +324,25 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = bx * kRowsPerBlock + wv;
-    const float* net = path == 0 ? a.actors_target + (*a.agent) * a.stride : a.critic;  // fc1 block at offset 0
+    // the replay rows and the agent index are read `sc1`: with the device-side gate (sc_k1) they are a snapshot
+    // another queue's kernel has just written through (csrc/flock_mem.h)
+    using flock_mem::ld_sc1;
+    const float* net = path == 0 ? a.actors_target + ld_sc1(a.agent) * a.stride : a.critic;  // fc1 block at offset 0
     const bool live = r < a.B;
     if (live) {
         const int64_t ir = a.idx[r];
         const float* x = (path == 2 ? a.rs : a.rs2) + ir * a.in;
-        if (lane < a.in) xs[wv * kMaxIn + lane] = x[lane];
+        const float xv = lane < a.in ? ld_sc1(x + lane) : 0.0f;
+        if (lane < a.in) xs[wv * kMaxIn + lane] = xv;
         if (path == 2) {
             if (lane < a.in) {
-                w.S[(int64_t)r * a.in + lane] = x[lane];
-                w.S2[(int64_t)r * a.in + lane] = a.rs2[ir * a.in + lane];
+                w.S[(int64_t)r * a.in + lane] = xv;
+                w.S2[(int64_t)r * a.in + lane] = ld_sc1(a.rs2 + ir * a.in + lane);
             }
-            if (lane < a.na) w.A[(int64_t)r * a.na + lane] = a.ra[ir * a.na + lane];
+            if (lane < a.na) w.A[(int64_t)r * a.na + lane] = ld_sc1(a.ra + ir * a.na + lane);
             if (lane == 0) {
-                w.R[r] = a.rr[ir];
-                w.T[r] = a.rt[ir];
+                w.R[r] = ld_sc1(a.rr + ir);
+                w.T[r] = ld_sc1(a.rt + ir);
             }
         }
     }
@@ -641,10 +650,38 @@ __device__ unsigned long long g_scmark[4096][8];
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
 // blocks past them).
+// The device-side snapshot gate: gate[0] = the sequence number of the last published snapshot, gate[1] = error word
+// (set by a waiter that gave up; flock_sc_pipeline_check reports it). One lane polls gate[0] with `sc1` loads until it
+// reaches seq; the block's waves then read the snapshot rows with `sc1` loads after the barrier (the producer wrote
+// them `sc1`, waited for every store, and set the flag after a workgroup barrier: csrc/flock_mem.h). A wait longer
+// than kGateTimeoutTicks sets the error word and the block computes nothing (the host raises; no silent result).
+constexpr unsigned long long kGateTimeoutTicks = 20000000ull;  // 0.2 s of s_memrealtime (100 MHz)
+__device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned long long seq) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        int good = 1;
+        if ((long long)(flock_mem::ld_sc1(gate) - seq) < 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((long long)(flock_mem::ld_sc1(gate) - seq) < 0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+                    __hip_atomic_store(gate + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    good = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     SC_PROF(0);
     SC_PRIO();
+    if (ac.gate && (int)blockIdx.y < npc && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
     if ((int)blockIdx.y < npc)
         c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
     else
@@ -1480,6 +1517,8 @@ RowArgs row_args(const FlockScUpdate* u) {
     a.critic = u->critic; a.actors = u->actors; a.actors_target = u->actors_target; a.stride = u->actor_stride;
     a.gamma = u->gamma;
     a.invB = 1.0f / (float)u->B;
+    a.gate = nullptr;  // only flock_sc_pipeline_learn gates a critic phase on its snapshot
+    a.gate_seq = 0;
     return a;
 }
 
@@ -1803,41 +1842,68 @@ __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t see
 }
 
 // learn() prologue with a minibatch snapshot: the sampled rows of every replay field are copied to staging rows
-// 0..B-1, so the update can read the staging copy (with the identity index) while the next env step rewrites the ring
+// 0..B-1, so the update can read the staging copy (with the identity index) while the next env step rewrites the ring.
+// SC1: every staging store write-through (the device-side gate's producer, csrc/flock_mem.h)
+template <bool SC1>
+__device__ __forceinline__ void snapshot_row(int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
+                                             int in_dim, int n_actions, const FlockScRows& src,
+                                             const FlockScRows& dst, int vec, int r) {
+    const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
+    const uint64_t u = ((uint64_t)q.x << 32) | q.y;
+    const int64_t row = (int64_t)(u % (uint64_t)rows);  // the row sc_prep samples for r
+    if (idx_out) idx_out[r] = row;
+    auto st = [](auto* p, auto v) {
+        if constexpr (SC1)
+            flock_mem::st_sc1(p, v);
+        else
+            *p = v;
+    };
+    // every load of the row first, then the stores (src and dst may alias as far as the compiler knows: interleaved,
+    // each store would wait for its load, one memory round trip per field)
+    if (vec) {  // the v2 shapes (in_dim 4, n_actions 2) with aligned fields: 16-B / 8-B rows
+        const float4 s0 = *reinterpret_cast<const float4*>(src.state + row * 4);
+        const float4 ns = *reinterpret_cast<const float4*>(src.new_state + row * 4);
+        const float2 ac = *reinterpret_cast<const float2*>(src.action + row * 2);
+        const float rw = src.reward[row], te = src.terminal[row];
+        st(reinterpret_cast<float4*>(dst.state + (int64_t)r * 4), s0);
+        st(reinterpret_cast<float4*>(dst.new_state + (int64_t)r * 4), ns);
+        st(reinterpret_cast<float2*>(dst.action + (int64_t)r * 2), ac);
+        st(dst.reward + r, rw);
+        st(dst.terminal + r, te);
+        return;
+    }
+    for (int c = 0; c < in_dim; ++c) {
+        const float a = src.state[row * in_dim + c], b = src.new_state[row * in_dim + c];
+        st(dst.state + (int64_t)r * in_dim + c, a);
+        st(dst.new_state + (int64_t)r * in_dim + c, b);
+    }
+    for (int c = 0; c < n_actions; ++c) st(dst.action + (int64_t)r * n_actions + c, src.action[row * n_actions + c]);
+    const float rw = src.reward[row], te = src.terminal[row];
+    st(dst.reward + r, rw);
+    st(dst.terminal + r, te);
+}
+
 __global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
                                                         int64_t* idx_out, int64_t* agent_out, int64_t agent,
                                                         int in_dim, int n_actions, FlockScRows src,
                                                         FlockScRows dst, int vec) {
     const int r = blockIdx.x * 64 + threadIdx.x;
     if (r == 0) *agent_out = agent;
-    if (r >= B) return;
-    const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
-    const uint64_t u = ((uint64_t)q.x << 32) | q.y;
-    const int64_t row = (int64_t)(u % (uint64_t)rows);  // the row sc_prep samples for r
-    if (idx_out) idx_out[r] = row;
-    // every load of the row first, then the stores (src and dst may alias as far as the compiler knows: interleaved,
-    // each store would wait for its load, one memory round trip per field)
-    if (vec) {  // the v2 shapes (in_dim 4, n_actions 2) with aligned fields: 16-B / 8-B rows
-        const float4 st = *reinterpret_cast<const float4*>(src.state + row * 4);
-        const float4 ns = *reinterpret_cast<const float4*>(src.new_state + row * 4);
-        const float2 ac = *reinterpret_cast<const float2*>(src.action + row * 2);
-        const float rw = src.reward[row], te = src.terminal[row];
-        *reinterpret_cast<float4*>(dst.state + (int64_t)r * 4) = st;
-        *reinterpret_cast<float4*>(dst.new_state + (int64_t)r * 4) = ns;
-        *reinterpret_cast<float2*>(dst.action + (int64_t)r * 2) = ac;
-        dst.reward[r] = rw;
-        dst.terminal[r] = te;
-        return;
-    }
-    for (int c = 0; c < in_dim; ++c) {
-        const float a = src.state[row * in_dim + c], b = src.new_state[row * in_dim + c];
-        dst.state[(int64_t)r * in_dim + c] = a;
-        dst.new_state[(int64_t)r * in_dim + c] = b;
-    }
-    for (int c = 0; c < n_actions; ++c) dst.action[(int64_t)r * n_actions + c] = src.action[row * n_actions + c];
-    const float rw = src.reward[row], te = src.terminal[row];
-    dst.reward[r] = rw;
-    dst.terminal[r] = te;
+    if (r < B) snapshot_row<false>(rows, seed, counter, idx_out, in_dim, n_actions, src, dst, vec, r);
+}
+
+// the same snapshot as ONE block that publishes it through the device-side gate: rows and agent stored `sc1`, every
+// wave's stores waited for, a workgroup barrier, then one lane's `sc1` store of gate[0] = seq (csrc/flock_mem.h)
+__global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows, uint64_t seed, uint64_t counter,
+                                                             int64_t* agent_out, int64_t agent, int in_dim,
+                                                             int n_actions, FlockScRows src, FlockScRows dst, int vec,
+                                                             unsigned long long* gate, unsigned long long seq) {
+    if (threadIdx.x == 0) flock_mem::st_sc1(agent_out, agent);
+    for (int r = threadIdx.x; r < B; r += 256)
+        snapshot_row<true>(rows, seed, counter, nullptr, in_dim, n_actions, src, dst, vec, r);
+    flock_mem::wait_vmem();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(gate, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
@@ -1959,10 +2025,23 @@ struct FlockScPipeline {
     int diag;  // -DFLOCK_SC_PIPELINE_DIAG=<bits> builds only (timing diagnostics; results are wrong): 1 no learner wait on the
                // snapshot, 2 no env wait on the slot, 3 neither
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
+    // device-side snapshot gate (direct launches, single GPU): gate[0] the published sequence number, gate[1] the
+    // error word of a waiter that gave up; seq counts this pipeline's snapshots. NULL: cross-queue event waits
+    unsigned long long* gate;
+    unsigned long long seq;
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
     int64_t pending_agent;
+    // data-parallel rounds (flock_sc_pipeline_set_dp): gradients into the [critic | actor] bucket, the caller's
+    // all-reduce of the part a round wrote, then the Adam launch with grad_scale
+    bool dp;
+    FlockScUpdate ug[kMaxSlots], uadam[kMaxSlots];
+    float* bucket;
+    int64_t actor_off, bucket_floats, critic_floats;
+    const float* grad_scale;
+    FlockAllreduceFn allreduce;
+    void* allreduce_ctx;
 };
 
 namespace {
@@ -1986,6 +2065,17 @@ int capture_round(const FlockScUpdate* uc, const FlockScUpdate* ua, hipGraphExec
 }
 // one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none)
 int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a) {
+    if (p->dp) {
+        // gradients only (do_adam = 0) into the bucket, ONE all-reduce (sum) of the part they wrote, then the Adam
+        // launch (gradients scaled by *grad_scale): SharedCriticLearner._dp_round
+        int rc = flock_sc_round(ls, c >= 0 ? &p->ug[c] : nullptr, a >= 0 ? &p->ug[a] : nullptr);
+        if (rc) return rc;
+        const int64_t lo = c >= 0 ? 0 : p->actor_off, hi = a >= 0 ? p->bucket_floats : p->critic_floats;
+        if ((rc = p->allreduce(p->allreduce_ctx, p->bucket + lo, hi - lo, ls)))
+            return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
+        return flock_sc_round_adam(ls, c >= 0 ? &p->uadam[c] : nullptr, a >= 0 ? &p->uadam[a] : nullptr,
+                                   p->grad_scale);
+    }
     if (!p->graphs) return launch_round(ls, c >= 0 ? &p->jc[c] : nullptr, a >= 0 ? &p->ja[a] : nullptr);
     hipGraphExec_t g = c >= 0 && a >= 0 ? p->merged[c] : (c >= 0 ? p->conly[c] : p->aonly[a]);
     return hipGraphLaunch(g, ls) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: graph launch failed");
@@ -2050,6 +2140,23 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->slot = 0;
     p->pending = -1;
     p->pending_agent = -1;
+    p->dp = false;
+    p->gate = nullptr;
+    p->seq = 0;
+    // the learner stream waits for each snapshot on the device (the critic phase's row blocks poll gate[0]) instead of
+    // a cross-queue barrier packet; FLOCK_SC_GATE=0 / 1 (read here) forces either. The spin needs the two queues'
+    // kernels to run concurrently: under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION, which serialises
+    // dispatches) a round dispatched ahead of its snapshot would wait out its bound, so the event waits are the
+    // default there. Graph replays and data-parallel rounds keep the events.
+    const char* gte = getenv("FLOCK_SC_GATE");
+    const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
+    const bool gate_on = gte ? gte[0] != '0' : !(pmc && pmc[0] && pmc[0] != '0');
+    if (!rc && !p->graphs && p->diag == 0 && gate_on) {
+        if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess)
+            rc = fail(-4, "flock_sc_pipeline_create: gate");
+    }
     if (rc) {
         flock_sc_pipeline_destroy(p);
         return nullptr;
@@ -2065,11 +2172,29 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const FlockScUpdate& u = p->u[s];
     if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
-    int rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
+    int rc = 0;
+    bool ok = true;
+    if (p->gate && !p->dp) {
+        // the snapshot publishes gate[0] = seq; this learn's critic row blocks wait for it on the device
+        if (u.B < 1 || rows < 1) return fail(-5, "flock_sc_pipeline_learn: need B, rows >= 1");
+        const FlockScRows& src = p->ring;
+        const FlockScRows& dst = p->staging[s];
+        int vec = u.in_dim == 4 && u.n_actions == 2;
+        for (const FlockScRows* x : {&src, &dst})
+            vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
+        const unsigned long long seq = ++p->seq;
+        hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
+                           const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq);
+        if ((rc = launched())) return rc;
+        p->jc[s].a.gate = p->gate;
+        p->jc[s].a.gate_seq = seq;
+    } else {
+        rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                     u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
-    if (rc) return rc;
-    bool ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
-              ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
+        if (rc) return rc;
+        ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
+             ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
+    }
     if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     const int q = p->pending;
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
@@ -2089,6 +2214,37 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     p->pending_agent = agent;
     p->used[s] = true;
     p->slot = (s + 1) % n;
+    return 0;
+}
+
+int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_offset,
+                             int64_t bucket_floats, const float* grad_scale, FlockAllreduceFn allreduce, void* ctx) {
+    if (!p || !bucket || !allreduce) return fail(-3, "flock_sc_pipeline_set_dp: NULL argument");
+    if (p->used[0] || p->pending >= 0) return fail(-5, "flock_sc_pipeline_set_dp: the pipeline has already learned");
+    const FlockScUpdate& u0 = p->u[0];
+    const int64_t ct = critic_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).total;
+    const int64_t at = actor_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).total;
+    if (critic_floats < ct || actor_offset < critic_floats || bucket_floats < actor_offset + at)
+        return fail(-5, "flock_sc_pipeline_set_dp: the bucket must hold [critic gradient | actor gradient]");
+    if (((uintptr_t)(bucket + actor_offset) & 15) != 0)
+        return fail(-5, "flock_sc_pipeline_set_dp: the actor part of the bucket must be 16-B aligned");
+    p->dp = true;
+    p->bucket = bucket;
+    p->critic_floats = critic_floats;
+    p->actor_off = actor_offset;
+    p->bucket_floats = bucket_floats;
+    p->grad_scale = grad_scale;
+    p->allreduce = allreduce;
+    p->allreduce_ctx = ctx;
+    for (int i = 0; i < p->n; ++i) {
+        FlockScUpdate a = p->u[i];
+        a.critic_grad = bucket;
+        a.actor_grad_out = bucket + actor_offset;
+        p->uadam[i] = a;  // do_adam = 1, the slot's update_rate: flock_sc_round_adam
+        a.do_adam = 0;
+        a.update_rate = 0;
+        p->ug[i] = a;  // the gradient round
+    }
     return 0;
 }
 
@@ -2114,8 +2270,22 @@ int flock_sc_mark_read(unsigned long long* host) {
 }
 #endif
 
+int flock_sc_pipeline_check(FlockScPipeline* p) {
+    if (!p) return fail(-3, "flock_sc_pipeline_check: NULL pipeline");
+    if (!p->gate) return 0;
+    unsigned long long flag = 0;
+    if (hipMemcpy(&flag, p->gate + 1, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_check: copy failed");
+    return flag ? fail(-6, "flock_sc_pipeline: a learn() round gave up waiting for its minibatch snapshot (device gate "
+                           "timeout); its results are invalid")
+                : 0;
+}
+
+int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate && !p->dp ? 1 : 0; }
+
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;
+    if (p->gate) (void)hipFree(p->gate);
     for (int i = 0; i < p->n; ++i) {
         hipGraphExec_t* gs[3] = {&p->merged[i], &p->conly[i], &p->aonly[i]};
         for (hipGraphExec_t* g : gs)

@@ -29,6 +29,7 @@
 #include <torch/library.h>
 
 #include "flock_learn.h"
+#include "flock_torch_sc.h"
 
 namespace {
 
@@ -568,10 +569,10 @@ void sc_prep_snapshot_meta(at::TensorList ring, at::TensorList staging, const Te
 // job     = [] (no phase) or [idx [B] i64, agent [1] i64, state, new_state, action, reward, terminal (the rows the
 //            update reads: a staging slot or the ring), workspace, critic_view (empty: none)(, actor_grad_out)]
 // dims    = [B, in_dim, n_actions, fc1, fc2, update_rate, do_adam]; hyper = [alpha, beta, gamma, beta1, beta2, eps, tau]
-struct ScArgs {
-    FlockScUpdate u;
-    bool set = false;
-};
+}  // namespace
+
+namespace flock_torch {
+
 void sc_round_checks(at::TensorList L, at::TensorList job, at::IntArrayRef dims, at::ArrayRef<double> hyper,
                      const char* what) {
     if (L.empty() || any_sym(L, job)) return;
@@ -651,6 +652,13 @@ FlockScUpdate sc_update(at::TensorList L, at::TensorList job, at::IntArrayRef di
     u.actor_grad_out = job.size() == 10 ? ptr<float>(job[9]) : nullptr;
     return u;
 }
+}  // namespace flock_torch
+
+namespace {
+
+using flock_torch::sc_round_checks;
+using flock_torch::sc_update;
+
 void sc_round_hip(at::TensorList learner, at::TensorList critic_job, at::TensorList actor_job, at::IntArrayRef dims,
                   at::ArrayRef<double> hyper) {
     TORCH_CHECK(!learner.empty(), "sc_round: empty learner state");
@@ -800,6 +808,12 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         "sc_round_adam(Tensor(a!)[] learner, Tensor(b!)[] critic_job, Tensor(c!)[] actor_job, int[] dims, "
         "float[] hyper, Tensor? grad_scale) -> ()");
     m.def("sc_prep(Tensor(a!) agent_out, Tensor(b!)? idx, int rows, int seed, int counter, int agent) -> ()");
+    // the workspace floats one shared-critic job needs (flock_sc_workspace_floats; no tensors: a CatchAll kernel)
+    m.def("sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2) -> int",
+          [](int64_t B, int64_t in_dim, int64_t na, int64_t fc1, int64_t fc2) -> int64_t {
+              TORCH_CHECK(B >= 1 && in_dim >= 1 && na >= 1 && fc1 >= 1 && fc2 >= 1, "sc_workspace_floats: sizes >= 1");
+              return flock_sc_workspace_floats((int)B, (int)in_dim, (int)na, (int)fc1, (int)fc2);
+          });
     m.def(
         "sc_act(Tensor obs, Tensor actors, Tensor(a!) actions, Tensor(b!)? ou_state, Tensor? noise, int fc1, int fc2, "
         "float theta, float dt, float sigma_sqrt_dt) -> ()");

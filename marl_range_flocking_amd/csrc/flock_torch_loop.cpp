@@ -1,29 +1,41 @@
-// flock_torch_loop.cpp — torch.classes.flock.ScTrainLoop: the config-3 training loop (BASELINE config 3, the
-// reference's learners/maddpg_shared_critic/train_flock.py:112-123 cadence: env.step, store_transitions, one learn()
-// per step) enqueued K steps per call from C++, so the host cost of a vectorized step is a few launch calls instead
-// of a Python round trip through the step op and the learner (the per-step path: VecFlockEnv.step(ring=...) through
-// flock::step_v2_store + SharedCriticLearner.pipeline_learn).
+// flock_torch_loop.cpp — the shared-critic learn() pipeline and the config-3 training loop as torch custom classes.
+//
+// torch.classes.flock.ScPipeline: the native learn() pipeline of one SharedCriticLearner (flock_sc_pipeline_*,
+//   include/flock_learn.h): its staging slots, events and the pending actor phase. learn() enqueues Agent.learn() of
+//   one agent (agent_simple_shared_critic.py:115-185): the minibatch snapshot on the env stream, one merged round on
+//   the learner stream. ONE object per learner: the per-step Python path (SharedCriticLearner.pipeline_learn) and the
+//   C++ loop below drive the same object, so the pending actor phase and the slot rotation carry over between them.
+//   set_dp() turns every round into the data-parallel form (gradients into the [critic | actor] bucket, a SUM
+//   all-reduce over the c10d ProcessGroup enqueued on the learner stream, the Adam launch with grad_scale = 1 / world;
+//   SharedCriticLearner.dp_learn).
+// torch.classes.flock.ScTrainLoop: the config-3 training loop (BASELINE config 3, the reference's
+//   learners/maddpg_shared_critic/train_flock.py:112-123 cadence: env.step, store_transitions, one learn() per step)
+//   enqueued K steps per call from C++, so the host cost of a vectorized step is a few launch calls instead of a
+//   Python round trip through the step op and the learner (the per-step path: VecFlockEnv.step(ring=...) through
+//   flock::step_v2_store + SharedCriticLearner.pipeline_learn).
 //
 // Per step s (global index first + s), exactly what that per-step path enqueues:
 //   env stream      flock_step_v2_ext with the fused replay insert (FlockRing rows (counter + skip) mod capacity,
 //                   prev_obs = the current observation buffer), the env's double-buffered dnn / nn_idx flipped;
-//   env + learner   learn() of agent (first + s) mod n_agents through the native pipeline (flock_sc_pipeline_learn:
-//                   minibatch snapshot on the env stream, one merged round on the learner stream), once the ring
-//                   holds a batch.
-// The loop owns the pipeline (built from the learner's tensors, as SharedCriticLearner.pipeline() builds it) and the
-// host mirrors of the env parity, the ring counter and the learn counter; state() returns them so the Python
-// objects can be brought up to date. Results are bitwise those of the per-step path
-// (tests/test_gpu_train_loop.py).
+//   env + learner   learn() of agent (first + s) mod n_agents through the pipeline, once the ring holds a batch.
+// The loop keeps host mirrors of the env parity, the ring counter and the learn counter; set_state() loads the Python
+// objects' values before a call (per-step Python steps may have run in between) and state() returns them after it.
+// Results are bitwise those of the per-step path (tests/test_gpu_train_loop.py, tests/test_gpu_dist.py).
 #include <ATen/ATen.h>
 #include <ATen/DeviceGuard.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
+#include <string>
 #include <vector>
 
 #include "flock_amd.h"
 #include "flock_learn.h"
+#include "flock_torch_sc.h"
 
 namespace {
 
@@ -40,6 +52,131 @@ void f32(const Tensor& t, const char* name, int64_t numel, const Tensor& like) {
                 "ScTrainLoop: ", name, " must be a contiguous f32 tensor of ", numel, " elements on ", like.device());
 }
 
+struct ScPipeline : torch::CustomClassHolder {
+    std::vector<Tensor> keep;  // every tensor the pipeline's FlockScUpdates point into (kept alive)
+    FlockScPipeline* pipe = nullptr;
+    at::Device device = at::Device(at::kCPU);
+    int64_t batch = 0, in_dim = 0, n_actions = 0, n_agents = 0, n_slots = 0;
+    // data-parallel rounds
+    c10::intrusive_ptr<c10d::ProcessGroup> pg;
+    Tensor bucket, grad_scale;
+    std::string cb_error;
+
+    // learner: the 13 state tensors; slots: n_slots jobs of 9 tensors (SharedCriticLearner._slots[i]["job"]: the
+    // slot's staging rows, workspace and critic view); ring: the replay ring's [state, new_state, action, reward,
+    // terminal]; dims / hyper: as flock::sc_round takes them (do_adam = 1)
+    ScPipeline(std::vector<Tensor> learner, std::vector<Tensor> slots, std::vector<Tensor> ring,
+               std::vector<int64_t> dims, std::vector<double> hyper) {
+        TORCH_CHECK(learner.size() == 13 && dims.size() == 7 && hyper.size() == 7 && dims[6] == 1,
+                    "ScPipeline: learner state [13], dims [7] with do_adam = 1, hyper [7]");
+        TORCH_CHECK(slots.size() % 9 == 0 && slots.size() / 9 >= 2 && slots.size() / 9 <= 8,
+                    "ScPipeline: 2..8 slots of 9 tensors");
+        TORCH_CHECK(ring.size() == 5, "ScPipeline: ring = [state, new_state, action, reward, terminal]");
+        TORCH_CHECK(learner[0].device().is_cuda(), "ScPipeline: the learner lives on a HIP device (no CPU fallback)");
+        device = learner[0].device();
+        n_slots = (int64_t)(slots.size() / 9);
+        batch = dims[0], in_dim = dims[1], n_actions = dims[2];
+        n_agents = learner[10].numel();
+        const at::TensorList L(learner);
+        std::vector<FlockScUpdate> us(n_slots);
+        std::vector<FlockScRows> staging(n_slots);
+        for (int64_t s = 0; s < n_slots; ++s) {
+            const at::TensorList job = at::TensorList(slots).slice(9 * s, 9);
+            flock_torch::sc_round_checks(L, job, dims, hyper, "slot");
+            TORCH_CHECK(job[8].numel() > 0, "ScPipeline: every slot needs its own critic view");
+            us[s] = flock_torch::sc_update(L, job, dims, hyper);
+            staging[s] = FlockScRows{static_cast<float*>(job[2].data_ptr()), static_cast<float*>(job[3].data_ptr()),
+                                     static_cast<float*>(job[4].data_ptr()), static_cast<float*>(job[5].data_ptr()),
+                                     static_cast<float*>(job[6].data_ptr())};
+        }
+        for (const Tensor& t : ring)
+            TORCH_CHECK(t.device() == device && t.scalar_type() == at::kFloat && t.is_contiguous(),
+                        "ScPipeline: ring fields are contiguous f32 tensors on ", device);
+        const FlockScRows rr{static_cast<float*>(ring[0].data_ptr()), static_cast<float*>(ring[1].data_ptr()),
+                             static_cast<float*>(ring[2].data_ptr()), static_cast<float*>(ring[3].data_ptr()),
+                             static_cast<float*>(ring[4].data_ptr())};
+        keep = learner;
+        keep.insert(keep.end(), slots.begin(), slots.end());
+        keep.insert(keep.end(), ring.begin(), ring.end());
+        const at::OptionalDeviceGuard g(device);
+        pipe = flock_sc_pipeline_create((int)n_slots, us.data(), &rr, staging.data());
+        TORCH_CHECK(pipe, "flock_sc_pipeline_create: ", flock_learn_last_error());
+    }
+
+    ~ScPipeline() override {
+        if (pipe) flock_sc_pipeline_destroy(pipe);
+    }
+
+    // the all-reduce between a data-parallel round's gradient and Adam launches: a SUM over the process group,
+    // enqueued on the learner stream (RCCL: the collective's stream waits for the learner stream and the learner
+    // stream for the collective; no host wait)
+    static int allreduce_cb(void* ctx, float* data, int64_t n, void* stream) {
+        auto* self = static_cast<ScPipeline*>(ctx);
+        try {
+            const c10::hip::HIPStream hs =
+                c10::hip::getStreamFromExternal(static_cast<hipStream_t>(stream), self->device.index());
+            const c10::hip::HIPStreamGuard guard(hs);
+            std::vector<Tensor> ts{at::from_blob(data, {n}, at::TensorOptions().dtype(at::kFloat).device(self->device))};
+            c10d::AllreduceOptions opts;
+            opts.reduceOp = c10d::ReduceOp::SUM;
+            self->pg->allreduce(ts, opts)->wait();
+            return 0;
+        } catch (const std::exception& e) {
+            self->cb_error = e.what();
+            return -4;
+        }
+    }
+
+    // data-parallel rounds over pg: bucket [critic gradient | pad | actor gradient] (bucket[:critic_floats] must be the
+    // learner state's critic_grad view), grad_scale [1] = 1 / world
+    void set_dp(c10::intrusive_ptr<c10d::ProcessGroup> group, Tensor bucket_, int64_t critic_floats, int64_t actor_off,
+                Tensor grad_scale_) {
+        TORCH_CHECK(group, "ScPipeline.set_dp: a process group");
+        TORCH_CHECK(bucket_.device() == device && bucket_.scalar_type() == at::kFloat && bucket_.is_contiguous(),
+                    "ScPipeline.set_dp: the bucket is a contiguous f32 tensor on ", device);
+        TORCH_CHECK(grad_scale_.device() == device && grad_scale_.scalar_type() == at::kFloat &&
+                        grad_scale_.numel() == 1,
+                    "ScPipeline.set_dp: grad_scale is one f32 on ", device);
+        pg = std::move(group);
+        bucket = bucket_;
+        grad_scale = grad_scale_;
+        const int rc = flock_sc_pipeline_set_dp(pipe, static_cast<float*>(bucket.data_ptr()), critic_floats, actor_off,
+                                                bucket.numel(), static_cast<const float*>(grad_scale.data_ptr()),
+                                                &ScPipeline::allreduce_cb, this);
+        TORCH_CHECK(rc == 0, "flock_sc_pipeline_set_dp: ", flock_learn_last_error());
+    }
+
+    void check(int rc, const char* fn) {
+        if (rc == 0) return;
+        std::string msg = flock_learn_last_error();
+        if (!cb_error.empty()) msg += " (" + cb_error + ")", cb_error.clear();
+        TORCH_CHECK(false, fn, ": ", msg);
+    }
+
+    // learn() of `agent` on `rows` ring rows (min(counter, capacity)), the learn counter `counter` (Philox)
+    void learn(int64_t rows, int64_t seed, int64_t counter, int64_t agent, int64_t env_stream, int64_t learner_stream) {
+        TORCH_CHECK(agent >= 0 && agent < n_agents, "ScPipeline.learn: agent out of range");
+        const at::OptionalDeviceGuard g(device);
+        check(flock_sc_pipeline_learn(pipe, reinterpret_cast<void*>(env_stream), reinterpret_cast<void*>(learner_stream),
+                                      rows, (uint64_t)seed, (uint64_t)counter, agent),
+              "flock_sc_pipeline_learn");
+    }
+
+    void flush(int64_t learner_stream) {
+        const at::OptionalDeviceGuard g(device);
+        check(flock_sc_pipeline_flush(pipe, reinterpret_cast<void*>(learner_stream)), "flock_sc_pipeline_flush");
+    }
+
+    // raises if a round gave up waiting for its snapshot (device-side gate timeout; its results are invalid).
+    // Synchronous: call once the learner stream has been synchronised
+    void verify() {
+        const at::OptionalDeviceGuard g(device);
+        check(flock_sc_pipeline_check(pipe), "flock_sc_pipeline_check");
+    }
+
+    bool gated() const { return flock_sc_pipeline_gated(pipe) != 0; }
+};
+
 struct ScTrainLoop : torch::CustomClassHolder {
     // env: [pos, heading, vel, dnn0, dnn1, idx0, idx1, reward, done, any_done, seeds] (idx / seeds may be empty)
     std::vector<Tensor> env;
@@ -51,27 +188,32 @@ struct ScTrainLoop : torch::CustomClassHolder {
     std::vector<Tensor> ring;
     int64_t capacity, counter;
     // learner
-    std::vector<Tensor> keep;  // every tensor the pipeline's FlockScUpdates point into (kept alive)
-    FlockScPipeline* pipe = nullptr;
-    int64_t batch, n_agents, seed, learn_calls;
+    c10::intrusive_ptr<ScPipeline> pipe;
+    int64_t seed, learn_calls;
 
     ScTrainLoop(std::vector<Tensor> env_, std::vector<double> env_f, std::vector<int64_t> env_i,
-                std::vector<Tensor> ring_, int64_t counter_, std::vector<Tensor> learner, std::vector<Tensor> slots,
-                std::vector<int64_t> dims, std::vector<double> hyper, int64_t seed_, int64_t learn_calls_)
-        : env(std::move(env_)), ring(std::move(ring_)), counter(counter_), seed(seed_), learn_calls(learn_calls_) {
+                std::vector<Tensor> ring_, int64_t counter_, c10::intrusive_ptr<ScPipeline> pipe_, int64_t seed_,
+                int64_t learn_calls_)
+        : env(std::move(env_)), ring(std::move(ring_)), counter(counter_), pipe(std::move(pipe_)), seed(seed_),
+          learn_calls(learn_calls_) {
         TORCH_CHECK(env.size() == 11, "ScTrainLoop: env = [pos, heading, vel, dnn0, dnn1, idx0, idx1, reward, done, "
                     "any_done, seeds]");
         TORCH_CHECK(env_f.size() == 6 && env_i.size() == 5,
                     "ScTrainLoop: env_f = [box, sensor_range, collision_distance, dt, v_min, v_max], env_i = [k, "
                     "periodic, rigid_boundary, launches, parity]");
+        TORCH_CHECK(pipe, "ScTrainLoop: a learn() pipeline (torch.classes.flock.ScPipeline)");
         const Tensor& pos = env[0];
         TORCH_CHECK(pos.device().is_cuda() && pos.dim() == 3 && pos.size(2) == 2, "ScTrainLoop: pos [E, N, 2] on HIP");
+        TORCH_CHECK(pos.device() == pipe->device, "ScTrainLoop: the env and the learner must share a device");
         E = pos.size(0);
         N = pos.size(1);
         box = env_f[0], sensor_range = env_f[1], cd = env_f[2], dt = env_f[3], v_min = env_f[4], v_max = env_f[5];
         k = env_i[0], periodic = env_i[1] != 0, rigid = env_i[2] != 0, launches = env_i[3], parity = env_i[4] & 1;
         TORCH_CHECK(k >= 1 && k + 1 <= N, "selected index k out of range");
         TORCH_CHECK(launches >= 1 && launches <= 64, "ScTrainLoop: launches in [1, 64]");
+        TORCH_CHECK(pipe->in_dim == k && pipe->n_actions == 2, "ScTrainLoop: the learner's input is the k-wide "
+                    "observation and its action the 2 controls");
+        TORCH_CHECK(pipe->n_agents == N, "ScTrainLoop: one actor per agent");
         f32(env[0], "pos", E * N * 2, pos);
         f32(env[1], "heading", E * N, pos);
         f32(env[2], "vel", E * N * 2, pos);
@@ -94,63 +236,15 @@ struct ScTrainLoop : torch::CustomClassHolder {
         const int64_t w[5] = {k, 2, 1, k, 1};
         const char* rn[5] = {"ring state", "ring action", "ring reward", "ring new_state", "ring terminal"};
         for (int i = 0; i < 5; ++i) f32(ring[i], rn[i], capacity * w[i], pos);
-        // learner: the pipeline's slots (SharedCriticLearner._slots[i]["job"]), as flock::sc_round takes them
-        TORCH_CHECK(learner.size() == 13 && dims.size() == 7 && hyper.size() == 7 && dims[6] == 1,
-                    "ScTrainLoop: learner state [13], dims [7] with do_adam, hyper [7]");
-        TORCH_CHECK(slots.size() % 9 == 0 && slots.size() / 9 >= 2 && slots.size() / 9 <= 8,
-                    "ScTrainLoop: 2..8 slots of 9 tensors");
-        const int ns = (int)(slots.size() / 9);
-        batch = dims[0];
-        n_agents = learner[10].numel();
-        TORCH_CHECK(dims[1] == k && dims[2] == 2, "ScTrainLoop: the learner's input is the k-wide observation");
-        std::vector<FlockScUpdate> us(ns);
-        std::vector<FlockScRows> staging(ns);
-        for (int s = 0; s < ns; ++s) {
-            const Tensor* j = &slots[9 * s];
-            FlockScUpdate& u = us[s];
-            u = FlockScUpdate{};
-            u.B = (int)dims[0], u.in_dim = (int)dims[1], u.n_actions = (int)dims[2], u.fc1 = (int)dims[3],
-            u.fc2 = (int)dims[4], u.update_rate = (int)dims[5], u.do_adam = 1;
-            u.idx = static_cast<const int64_t*>(j[0].data_ptr());
-            u.agent = static_cast<const int64_t*>(j[1].data_ptr());
-            u.ring_state = static_cast<const float*>(j[2].data_ptr());
-            u.ring_new_state = static_cast<const float*>(j[3].data_ptr());
-            u.ring_action = static_cast<const float*>(j[4].data_ptr());
-            u.ring_reward = static_cast<const float*>(j[5].data_ptr());
-            u.ring_terminal = static_cast<const float*>(j[6].data_ptr());
-            u.workspace = static_cast<float*>(j[7].data_ptr());
-            u.critic_view = static_cast<float*>(j[8].data_ptr());
-            u.critic = static_cast<float*>(learner[0].data_ptr());
-            u.critic_grad = static_cast<float*>(learner[1].data_ptr());
-            u.critic_exp_avg = static_cast<float*>(learner[2].data_ptr());
-            u.critic_exp_avg_sq = static_cast<float*>(learner[3].data_ptr());
-            u.critic_step = static_cast<int64_t*>(learner[4].data_ptr());
-            u.actors = static_cast<float*>(learner[5].data_ptr());
-            u.actors_grad = static_cast<float*>(learner[6].data_ptr());
-            u.actors_exp_avg = static_cast<float*>(learner[7].data_ptr());
-            u.actors_exp_avg_sq = static_cast<float*>(learner[8].data_ptr());
-            u.actors_target = static_cast<float*>(learner[9].data_ptr());
-            u.actor_steps = static_cast<int64_t*>(learner[10].data_ptr());
-            u.actor_stride = learner[5].numel() / n_agents;
-            u.losses = static_cast<float*>(learner[11].data_ptr());
-            u.counters = static_cast<unsigned*>(learner[12].data_ptr());
-            u.alpha = (float)hyper[0], u.beta = (float)hyper[1], u.gamma = (float)hyper[2], u.beta1 = (float)hyper[3],
-            u.beta2 = (float)hyper[4], u.eps = (float)hyper[5], u.tau = (float)hyper[6];
-            staging[s] = FlockScRows{const_cast<float*>(u.ring_state), const_cast<float*>(u.ring_new_state),
-                                     const_cast<float*>(u.ring_action), const_cast<float*>(u.ring_reward),
-                                     const_cast<float*>(u.ring_terminal)};
-        }
-        const FlockScRows rr{static_cast<float*>(ring[0].data_ptr()), static_cast<float*>(ring[3].data_ptr()),
-                             static_cast<float*>(ring[1].data_ptr()), static_cast<float*>(ring[2].data_ptr()),
-                             static_cast<float*>(ring[4].data_ptr())};
-        keep = learner;
-        keep.insert(keep.end(), slots.begin(), slots.end());
-        pipe = flock_sc_pipeline_create(ns, us.data(), &rr, staging.data());
-        TORCH_CHECK(pipe, "flock_sc_pipeline_create: ", flock_learn_last_error());
     }
 
-    ~ScTrainLoop() override {
-        if (pipe) flock_sc_pipeline_destroy(pipe);
+    // the Python objects' current values (VecFlockEnv._cur, ReplayRing.counter, SharedCriticLearner._learn_calls):
+    // per-step Python steps may have advanced them since the last call
+    void set_state(int64_t parity_, int64_t counter_, int64_t learn_calls_) {
+        TORCH_CHECK(counter_ >= 0 && learn_calls_ >= 0, "ScTrainLoop.set_state: counters are >= 0");
+        parity = parity_ & 1;
+        counter = counter_;
+        learn_calls = learn_calls_;
     }
 
     // K vectorized steps from global step `first`; actions: a pool of [E, N, 2] f32 tensors (step s uses
@@ -163,7 +257,6 @@ struct ScTrainLoop : torch::CustomClassHolder {
         TORCH_CHECK(ev_every >= 1 && events.size() % 2 == 0, "ScTrainLoop.run: event pairs and ev_every >= 1");
         const at::OptionalDeviceGuard g(env[0].device());
         void* es = reinterpret_cast<void*>(env_stream);
-        void* ls = reinterpret_cast<void*>(learner_stream);
         const int64_t n = E * N;
         size_t ev = 0;
         for (int64_t s = 0; s < K; ++s) {
@@ -200,20 +293,15 @@ struct ScTrainLoop : torch::CustomClassHolder {
             }
             parity = nxt;
             counter += n;
-            if (counter >= batch) {  // SharedCriticLearner.pipeline_learn: learn() once the ring holds a batch
+            if (counter >= pipe->batch) {  // SharedCriticLearner.pipeline_learn: learn() once the ring holds a batch
                 ++learn_calls;
-                const int64_t rows = counter < capacity ? counter : capacity;
-                const int rl = flock_sc_pipeline_learn(pipe, es, ls, rows, (uint64_t)seed, (uint64_t)learn_calls,
-                                                       step % n_agents);
-                TORCH_CHECK(rl == 0, "flock_sc_pipeline_learn: ", flock_learn_last_error());
+                pipe->learn(counter < capacity ? counter : capacity, seed, learn_calls, step % pipe->n_agents,
+                            env_stream, learner_stream);
             }
         }
     }
 
-    void flush(int64_t learner_stream) {
-        TORCH_CHECK(flock_sc_pipeline_flush(pipe, reinterpret_cast<void*>(learner_stream)) == 0,
-                    "flock_sc_pipeline_flush: ", flock_learn_last_error());
-    }
+    void flush(int64_t learner_stream) { pipe->flush(learner_stream); }
 
     std::vector<int64_t> state() const { return {parity, counter, learn_calls}; }
 };
@@ -221,10 +309,18 @@ struct ScTrainLoop : torch::CustomClassHolder {
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(flock, m) {
+    m.class_<ScPipeline>("ScPipeline")
+        .def(torch::init<std::vector<Tensor>, std::vector<Tensor>, std::vector<Tensor>, std::vector<int64_t>,
+                         std::vector<double>>())
+        .def("set_dp", &ScPipeline::set_dp)
+        .def("learn", &ScPipeline::learn)
+        .def("flush", &ScPipeline::flush)
+        .def("verify", &ScPipeline::verify)
+        .def("gated", &ScPipeline::gated);
     m.class_<ScTrainLoop>("ScTrainLoop")
         .def(torch::init<std::vector<Tensor>, std::vector<double>, std::vector<int64_t>, std::vector<Tensor>, int64_t,
-                         std::vector<Tensor>, std::vector<Tensor>, std::vector<int64_t>, std::vector<double>, int64_t,
-                         int64_t>())
+                         c10::intrusive_ptr<ScPipeline>, int64_t, int64_t>())
+        .def("set_state", &ScTrainLoop::set_state)
         .def("run", &ScTrainLoop::run)
         .def("flush", &ScTrainLoop::flush)
         .def("state", &ScTrainLoop::state);

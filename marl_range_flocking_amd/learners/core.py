@@ -8,7 +8,6 @@
 * ``gru_cell``: nn.GRUCell with the gate GEMMs batched and the elementwise part in flock_gru_fwd/bwd.
 * ``ReplayRing``: device-resident ring of named row tensors with HIP row scatter (insert) / gather (sample).
 """
-import ctypes
 import math
 from collections import OrderedDict
 
@@ -16,18 +15,8 @@ import warnings
 
 import torch
 
-from .. import _native
-
 # agent-major stacked views are strided; their grads alias the same strides on purpose
 warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")
-
-
-def _p(t):
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
-
-
-def _stream(dev):
-    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
 def _ops():
@@ -527,22 +516,14 @@ class StepRing:
     """The replay-ring targets of one env step that writes its transitions itself (flock::step_v2_store /
     step_uw_discrete_store, include/flock_amd.h FlockRing): the ring field tensors [state, action, reward, new_state,
     terminal] (+ the record's actor_state / actor_new_state copies) and meta = [start, skip, group, store_done,
-    action_ids, env_done]. ``ctypes()`` is the same ring as the C ABI's FlockRing (the launch-plan path)."""
+    action_ids, env_done]. The launch-plan path builds the C ABI's FlockRing from it (ops.flock_ring)."""
 
     def __init__(self, fields, actor_state, actor_new_state, group, store_done, action_ids, env_done):
         self.fields, self.actor_state, self.actor_new_state = list(fields), actor_state, actor_new_state
         self.meta = [0, 0, int(group), int(bool(store_done)), int(bool(action_ids)), int(bool(env_done))]
-        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-        f = self.fields
-        self._c = _native.FlockRing(
-            state=ptr(f[0]), action=ptr(f[1]), reward=ptr(f[2]), new_state=ptr(f[3]), terminal=ptr(f[4]),
-            prev_obs=None, capacity=f[0].shape[0], start=0, skip=0, actor_state=ptr(actor_state),
-            actor_new_state=ptr(actor_new_state), group=int(group), store_done=self.meta[3],
-            action_ids=self.meta[4], env_done=self.meta[5])
 
     def set_start(self, start, skip):
         self.meta[0], self.meta[1] = int(start), int(skip)
-        self._c.start, self._c.skip = int(start), int(skip)
 
     @property
     def start(self):
@@ -551,10 +532,6 @@ class StepRing:
     @property
     def skip(self):
         return self.meta[1]
-
-    def ctypes(self, prev_obs):
-        self._c.prev_obs = prev_obs.data_ptr()
-        return self._c
 
 
 class ReplayRing:
@@ -620,8 +597,8 @@ class ReplayRing:
         fields; group = agents per row (1, or N for one row per env); store_done: store done (else 1 - done);
         action_ids: the step's action ids stored as f32 (uw_discrete); env_done: one terminal flag per env row."""
         skip = max(0, n - self.capacity)
-        # one StepRing per field mapping, updated in place (its ctypes FlockRing serves the launch-plan path, which
-        # keeps a pointer to it)
+        # one StepRing per field mapping, updated in place (ops.flock_ring builds its FlockRing for the launch-plan
+        # path, which keeps a pointer to it)
         key = (state, action, reward, new_state, terminal, actor_state, actor_new_state, group, bool(store_done),
                bool(action_ids), bool(env_done))
         rings = self.__dict__.setdefault("_rings", {})

@@ -20,16 +20,14 @@ learn() has two implementations with the same semantics:
     all-reduce of the [critic | actor] bucket and one Adam launch (flock_sc_round_adam);
   * autograd (fused=False): the same update written with torch ops and the batched helpers of core.py.
 """
-import ctypes
 import math
-
 import os
 
 import torch
 import torch.nn.functional as F
 
-from .. import _native, dist
-from .core import FlatParams, ReplayRing, _ops, _p, blayer_norm, blinear, capture_graph
+from .. import dist
+from .core import FlatParams, ReplayRing, _ops, blayer_norm, blinear, capture_graph
 
 
 def critic_shapes(input_dim, fc1=400, fc2=300, n_actions=2):
@@ -140,11 +138,10 @@ class SharedCriticLearner:
 
     # ------------------------------------------------------------------ fused HIP update (csrc/flock_sc.hip)
     def _init_fused(self):
-        lib = _native.lib()
         dev = self.device
         B, n_in, na = self.batch_size, self.input_dim, self.n_actions
         self.static_agent = torch.zeros(1, dtype=torch.int64, device=dev)
-        n_ws = lib.flock_sc_workspace_floats(B, n_in, na, self.fc1, self.fc2)
+        n_ws = _ops().sc_workspace_floats(B, n_in, na, self.fc1, self.fc2)
         self.sc_workspace = torch.zeros(int(n_ws), dtype=torch.float32, device=dev)
         self.sc_counters = torch.zeros(2, dtype=torch.int32, device=dev)
         # critic views (FlockScUpdate.critic_view): the critic phase writes the post-Adam critic into a view and the
@@ -155,19 +152,8 @@ class SharedCriticLearner:
         self.sc_workspaces = [self.sc_workspace] + [torch.zeros_like(self.sc_workspace) for _ in range(ns - 1)]
         rb = self.replay.bufs
         C, A = self.critic, self.actors
-        fields = dict(B=B, in_dim=n_in, n_actions=na, fc1=self.fc1, fc2=self.fc2, do_adam=1,
-                      idx=_p(self.static_idx), agent=_p(self.static_agent), ring_state=_p(rb["state"]),
-                      ring_new_state=_p(rb["new_state"]), ring_action=_p(rb["action"]), ring_reward=_p(rb["reward"]),
-                      ring_terminal=_p(rb["terminal"]), critic=_p(C.data), critic_grad=_p(C.grad),
-                      critic_exp_avg=_p(C.exp_avg), critic_exp_avg_sq=_p(C.exp_avg_sq), critic_step=_p(C.step_dev),
-                      actors=_p(A.data), actors_grad=_p(A.grad), actors_exp_avg=_p(A.exp_avg),
-                      actors_exp_avg_sq=_p(A.exp_avg_sq), actors_target=_p(A.target),
-                      actor_steps=_p(self.actor_steps), actor_stride=A.per_agent, losses=_p(self.losses),
-                      workspace=_p(self.sc_workspace), counters=_p(self.sc_counters), alpha=self.alpha,
-                      beta=self.beta, gamma=self.gamma, beta1=0.9, beta2=0.999, eps=1e-8, tau=self.tau,
-                      update_rate=self.update_rate)
-        # the same update as torch.ops.flock.sc_round arguments (csrc/flock_torch_learn.cpp): the learner state, one
-        # job per phase ([idx, agent, 5 replay-row fields, workspace, critic_view(, actor_grad_out)]), sizes, rates
+        # the update as torch.ops.flock.sc_round arguments (csrc/flock_torch_learn.cpp): the learner state, one job per
+        # phase ([idx, agent, 5 replay-row fields, workspace, critic_view(, actor_grad_out)]), sizes, rates
         rows = lambda d: [d["state"], d["new_state"], d["action"], d["reward"], d["terminal"]]  # noqa: E731
         self._sc_learner = [C.data, C.grad, C.exp_avg, C.exp_avg_sq, C.step_dev, A.data, A.grad, A.exp_avg,
                             A.exp_avg_sq, A.target, self.actor_steps, self.losses, self.sc_counters]
@@ -179,14 +165,10 @@ class SharedCriticLearner:
         self._no_view = torch.empty(0, device=dev)
         self._sc_job_grads = self._sc_job[:8] + [self._no_view]
         self._ring_rows = rows(rb)
-        # single GPU: the soft updates run inside the gradient kernels (device-side count condition)
-        self._sc = _native.FlockScUpdate(**fields, critic_view=_p(self.critic_views[0]))
-        self._sc_grads = _native.FlockScUpdate(**dict(fields, do_adam=0, update_rate=0))  # data-parallel
         self._slots = []
+        self._pipe = None
         if self.snapshot:
             self.identity_idx = torch.arange(B, dtype=torch.int64, device=dev)
-            names = ("state", "new_state", "action", "reward", "terminal")
-            self._rows_ring = _native.FlockScRows(**{n: _p(rb[n]) for n in names})
             if self.distributed:
                 # data-parallel rounds: the critic gradient and the round's actor gradient in ONE contiguous bucket
                 # (FlockScUpdate.critic_grad / actor_grad_out), all-reduced as one collective per env step
@@ -198,19 +180,12 @@ class SharedCriticLearner:
                        "action": torch.zeros(B, na, device=dev), "reward": torch.zeros(B, device=dev),
                        "terminal": torch.zeros(B, device=dev)}
                 agent_t = torch.zeros(1, dtype=torch.int64, device=dev)
-                f = dict(fields, idx=_p(self.identity_idx), agent=_p(agent_t), workspace=_p(self.sc_workspaces[i]),
-                         **{"ring_" + n: _p(stg[n]) for n in names})
                 self._slots.append(dict(staging=stg, agent=agent_t, graph=None, graph_c=None, graph_a=None,
                                         job=[self.identity_idx, agent_t, *rows(stg), self.sc_workspaces[i],
                                              self.critic_views[i]],
                                         job_grads=[self.identity_idx, agent_t, *rows(stg), self.sc_workspaces[i],
-                                                   self._no_view],
-                                        rows=_native.FlockScRows(**{n: _p(stg[n]) for n in names}),
-                                        sc=_native.FlockScUpdate(**f, critic_view=_p(self.critic_views[i])),
-                                        sc_grads=_native.FlockScUpdate(**dict(f, do_adam=0, update_rate=0))))
+                                                   self._no_view]))
                 if self.distributed:
-                    bucket = dict(f, critic_grad=_p(self.dp_bucket), critic_view=_p(self.critic_views[i]),
-                                  actor_grad_out=_p(self.dp_bucket[self.dp_actor_off:]))
                     self._slots[-1]["dp_job"] = self._slots[-1]["job"] + [self.dp_bucket[self.dp_actor_off:]]
             if self.distributed:  # the learner state with the critic gradient in the bucket
                 self._sc_learner_dp = list(self._sc_learner)
@@ -512,20 +487,26 @@ class SharedCriticLearner:
         return self._finish_learn(agent, soft_in_kernel=True)
 
     def pipeline(self):
-        """The native learn() pipeline (flock_sc_pipeline_*, include/flock_learn.h) over the n_slots staging slots:
-        snapshot plus ONE six-launch round (this learn's critic phase with the previous learn's actor phase,
-        flock_sc_round) enqueued by one C call, no cross-stream wait between the phases."""
-        if self.__dict__.get("_pipe") is None:
-            if not (self.snapshot and self.fused) or self.distributed:
-                raise RuntimeError("the native pipeline needs a single-GPU fused learner with snapshot=True")
-            lib = _native.lib()
-            n = len(self._slots)
-            us = (_native.FlockScUpdate * n)(*[S["sc"] for S in self._slots])
-            rows = (_native.FlockScRows * n)(*[S["rows"] for S in self._slots])
-            h = lib.flock_sc_pipeline_create(n, us, ctypes.byref(self._rows_ring), rows)
-            if not h:
-                raise RuntimeError("flock_sc_pipeline_create: " + lib.flock_learn_last_error().decode())
-            self._pipe = h
+        """The native learn() pipeline (torch.classes.flock.ScPipeline over flock_sc_pipeline_*, include/flock_learn.h)
+        over the n_slots staging slots: per learn() the minibatch snapshot on the env stream and ONE round (this
+        learn's critic phase with the previous learn's actor phase, flock_sc_round) on the learner stream, enqueued by
+        one call. ONE object per learner: the per-step path (pipeline_learn) and the C++ training loop
+        (ScTrainLoop) share its slots and its pending actor phase. Data-parallel learners (dist_group) run every
+        round as gradients, one RCCL all-reduce of the [critic | actor] bucket over the group and the Adam launch
+        (set_dp; dp_learn's rounds, enqueued from C++)."""
+        if self._pipe is None:
+            if not (self.snapshot and self.fused):
+                raise RuntimeError("the native pipeline needs a fused learner with snapshot=True")
+            from .. import torch_ops
+
+            torch_ops.load()
+            slots = [t for S in self._slots for t in S["job"]]
+            p = torch.classes.flock.ScPipeline(self._sc_learner, slots, self._ring_rows, self._sc_dims,
+                                               self._sc_hyper)
+            if self.distributed:
+                p.set_dp(self.group if self.group is not None else torch.distributed.group.WORLD, self.dp_bucket,
+                         self.critic.numel, self.dp_actor_off, self.inv_world)
+            self._pipe = p
         return self._pipe
 
     def pipeline_learn(self, agent, env_stream, learner_stream):
@@ -535,25 +516,21 @@ class SharedCriticLearner:
         if self.replay.counter < self.batch_size:
             return False
         self._learn_calls += 1
-        rc = _native.lib().flock_sc_pipeline_learn(self.pipeline(), env_stream, learner_stream, len(self.replay),
-                                                   self.seed, self._learn_calls, int(agent))
-        _native.check(rc, "flock_sc_pipeline_learn", learn=True)
+        self.pipeline().learn(len(self.replay), self.seed, self._learn_calls, int(agent), int(env_stream),
+                              int(learner_stream))
         self._finish_learn(agent, soft_in_kernel=True)
         return True
 
     def pipeline_flush(self, learner_stream):
         """Enqueue the pending actor phase of the last pipeline_learn (no-op when none)."""
-        if self.__dict__.get("_pipe") is not None:
-            _native.check(_native.lib().flock_sc_pipeline_flush(self._pipe, learner_stream),
-                          "flock_sc_pipeline_flush", learn=True)
+        if self._pipe is not None:
+            self._pipe.flush(int(learner_stream))
 
-    def __del__(self):
-        h = self.__dict__.get("_pipe")
-        if h:
-            try:
-                _native.lib().flock_sc_pipeline_destroy(h)
-            except Exception:  # noqa: BLE001 - interpreter shutdown
-                pass
+    def pipeline_check(self):
+        """Raise if a pipelined round gave up waiting for its minibatch snapshot (the device-side gate's bounded
+        wait, flock_sc_pipeline_check): its update is invalid. Synchronous; call after synchronising."""
+        if self._pipe is not None:
+            self._pipe.verify()
 
     # ------------------------------------------------------------------ data-parallel rounds (bench, N > 1)
     def _dp_round(self, c, a):
@@ -643,8 +620,10 @@ class SharedCriticBench:
             # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
             # with graphs, the native pipeline (one merged six-launch round per step on self.stream,
             # SharedCriticLearner.pipeline_learn); without, two streams (update_slot_pipelined).
-            # FLOCK_LEARN_PIPELINE=0 keeps one serial learn() per step on self.stream.
-            self.pipelined = not self.learner.distributed and os.environ.get("FLOCK_LEARN_PIPELINE") != "0"
+            # FLOCK_LEARN_PIPELINE=0 keeps one serial learn() per step on self.stream (data-parallel: the Python
+            # dp_learn rounds). Data-parallel learners run the same native pipeline, every round as gradients + one
+            # RCCL all-reduce + the Adam launch (SharedCriticLearner.pipeline, set_dp).
+            self.pipelined = os.environ.get("FLOCK_LEARN_PIPELINE") != "0"
             # stream priority (FLOCK_LEARNER_PRIORITY=1): the one-stream learner ran at high priority; with the two
             # pipelined streams high priority made steps 2-3x slower in fresh processes; with the native pipeline's
             # one learner stream it changes nothing (tools/cu_mask_probe.py)
@@ -668,15 +647,14 @@ class SharedCriticBench:
 
     # ---------------------------------------------------------------- K steps per call (torch.classes.flock)
     def loop(self):
-        """torch.classes.flock.ScTrainLoop over this bench's env, replay ring and learner (csrc/flock_torch_loop.cpp):
-        K steps of [env step with the fused replay insert, learn()] enqueued by one C++ call, bitwise the per-step
-        path of before() / env.step(ring=...) / after(). Single GPU, overlapped native pipeline only."""
+        """torch.classes.flock.ScTrainLoop over this bench's env, replay ring and the learner's pipeline
+        (csrc/flock_torch_loop.cpp): K steps of [env step with the fused replay insert, learn()] enqueued by one C++
+        call, bitwise the per-step path of before() / env.step(ring=...) / after(). Overlapped native pipeline only;
+        data-parallel learners included (the pipeline's rounds then carry the RCCL all-reduce)."""
         if self._loop is None:
             env, L = self.env, self.learner
-            if not (self.overlap and self.pipelined and L.use_graph) or env.cfg.variant != "v2":
-                raise RuntimeError("ScTrainLoop is the single-GPU overlapped config-3 loop (v2, native pipeline)")
-            if self._handles is not None:
-                raise RuntimeError("ScTrainLoop must own the learn() pipeline from the first learn on")
+            if not self.can_loop():
+                raise RuntimeError("ScTrainLoop is the overlapped config-3 loop (v2, native learn() pipeline)")
             from .. import torch_ops
 
             torch_ops.load()
@@ -690,18 +668,18 @@ class SharedCriticBench:
             ei = [env.k, int(bool(c.periodic)), int(bool(c.rigid_boundary)), int(c.step_launches), env._cur]
             rb = L.replay.bufs
             ring = [rb["state"], rb["action"], rb["reward"], rb["new_state"], rb["terminal"]]
-            slots = [t for S in L._slots for t in S["job"]]
-            self._loop = torch.classes.flock.ScTrainLoop(e, ef, ei, ring, L.replay.counter, L._sc_learner, slots,
-                                                         L._sc_dims, L._sc_hyper, L.seed, L._learn_calls)
+            self._loop = torch.classes.flock.ScTrainLoop(e, ef, ei, ring, L.replay.counter, L.pipeline(), L.seed,
+                                                         L._learn_calls)
         return self._loop
 
     def can_loop(self):
-        return (self.overlap and self.pipelined and self.learner.use_graph and not self.learner.distributed
-                and self.env.cfg.variant == "v2" and self._handles is None)
+        return (self.overlap and self.pipelined and self.learner.use_graph and self.env.cfg.variant == "v2")
 
     def run_steps(self, first, K, actions, events=(), ev_every=1):
         """Steps first .. first + K - 1 (actions[s % len(actions)] at step s) through the loop, then the Python
-        mirrors (env parity and step count, ring counter, learn counters) brought up to date."""
+        mirrors (env parity and step count, ring counter, learn counters) brought up to date. The loop first takes
+        the Python objects' current values (set_state): per-step steps (step(), env.step(ring=before(s))) may have
+        run since its last call."""
         lp = self.loop()
         env, L = self.env, self.learner
         handles = []
@@ -709,6 +687,7 @@ class SharedCriticBench:
             if not int(ev.cuda_event):  # torch creates the HIP event at its first record
                 ev.record()
             handles.append(int(ev.cuda_event))
+        lp.set_state(env._cur, L.replay.counter, L._learn_calls)
         lp.run(int(first), int(K), list(actions), torch.cuda.current_stream(env.device).cuda_stream,
                self.stream.cuda_stream, handles, int(ev_every))
         parity, counter, calls = lp.state()
@@ -746,9 +725,10 @@ class SharedCriticBench:
         # the update runs on the learner stream; staging slots alternate, and a slot is refilled only after the
         # update that read it two steps ago has finished
         if self.pipelined and L.use_graph:
-            # the native pipeline: snapshot on the env stream, then one round (this critic phase + the previous
-            # learn's actor phase) on self.stream, enqueued by one C call (stream handles cached at the first call:
-            # the env stream is the stream current then)
+            # the native pipeline (the same ScPipeline object the C++ loop drives): snapshot on the env stream, then
+            # one round (this critic phase + the previous learn's actor phase; data-parallel: as gradients, one RCCL
+            # all-reduce and the Adam launch) on self.stream (stream handles cached at the first call: the env stream
+            # is the stream current then)
             if self._handles is None:
                 self._handles = (torch.cuda.current_stream(L.device).cuda_stream, self.stream.cuda_stream)
             L.pipeline_learn(agent, *self._handles)
@@ -795,11 +775,9 @@ class SharedCriticBench:
         """Enqueue the pending actor phase (native pipeline) and join the learner stream(s) into the current one
         (end of a timed region)."""
         if self.overlap:
-            if self._looped:
-                self._loop.flush(self.stream.cuda_stream)
-            if self._handles is not None:
-                self.learner.pipeline_flush(self._handles[1])
-            if self.learner.distributed:
+            if self._looped or self._handles is not None:  # one pipeline object: the loop's and the per-step path's
+                self.learner.pipeline_flush(self.stream.cuda_stream)
+            if self.learner.distributed and self.learner.__dict__.get("_dp_pending") is not None:
                 with torch.cuda.stream(self.stream):
                     self.learner.dp_flush(self.slot_free)
             cur = torch.cuda.current_stream(self.learner.device)

@@ -54,6 +54,23 @@ def _check_k(N, k):
         raise RuntimeError("selected index k out of range")
 
 
+def flock_ring(ring, prev_obs):
+    """The C ABI's FlockRing of a learner's StepRing (learners/core.py) for the launch-plan path: one ctypes struct
+    per StepRing, updated in place (start / skip of the step, the previous observation buffer), so a StepPlan that
+    recorded a pointer to it sees every step's values."""
+    c = ring.__dict__.get("_flock_ring")
+    if c is None:
+        f, m = ring.fields, ring.meta
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        c = ring._flock_ring = _native.FlockRing(
+            state=ptr(f[0]), action=ptr(f[1]), reward=ptr(f[2]), new_state=ptr(f[3]), terminal=ptr(f[4]),
+            prev_obs=None, capacity=f[0].shape[0], start=0, skip=0, actor_state=ptr(ring.actor_state),
+            actor_new_state=ptr(ring.actor_new_state), group=m[2], store_done=m[3], action_ids=m[4], env_done=m[5])
+    c.start, c.skip = ring.meta[0], ring.meta[1]
+    c.prev_obs = prev_obs.data_ptr()
+    return c
+
+
 def _ext(ring=None, seeds=None, E=0, N=0, k=0, dev=None, launches=1, normalize=False):
     """FlockStepExt for the *_ext entry points, or None when there is nothing extra."""
     launches = int(launches)

@@ -274,7 +274,7 @@ class VecFlockEnv:
             plan = plans[pkey] = ops.StepPlan()
         common = dict(k=k, box=self.box, collision_distance=c.collision_distance, dt=dt,
                       rigid_boundary=c.rigid_boundary, plan=plan, normalize=c.normalize_distance)
-        cring = ring.ctypes(src["dnn"]) if ring is not None else None
+        cring = ops.flock_ring(ring, src["dnn"]) if ring is not None else None
         if c.variant == "v2":
             ops.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
                         self.done, self.any_done, sensor_range=c.sensor_range, v_min=c.v_min,

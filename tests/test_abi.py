@@ -104,6 +104,7 @@ def test_shared_critic_round_and_pipeline_argument_checks(lib):
     assert "n_slots" in lib.flock_learn_last_error().decode()
     assert lib.flock_sc_pipeline_flush(None, None) == -3
     assert lib.flock_sc_pipeline_learn(None, None, None, 1, 0, 0, 0) == -3
+    assert lib.flock_sc_pipeline_set_dp(None, None, 0, 0, 0, None, None, None) == -3
 
 
 def test_step_ext_layout_and_launches_option():

@@ -1,6 +1,8 @@
 """Overlapped env step / learner (bench.py config 3 hook): learn(s) on its own stream after its minibatch snapshot,
 env step s+1 concurrently on the main stream. Every kernel must still see the same data, so after several steps
 every parameter, Adam moment, replay field and loss equals the serial loop's bit for bit."""
+import os
+
 import pytest
 import torch
 
@@ -144,6 +146,8 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, cuda):
     pip.pipeline_flush(ls.cuda_stream)  # nothing pending: a no-op
     main.wait_stream(ls)
     torch.cuda.synchronize()
+    pip.pipeline_check()  # no round gave up waiting for its snapshot (device-side gate)
+    assert pip.pipeline().gated() == (os.environ.get("FLOCK_SC_GATE", "1") != "0")
     for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg, pip.critic.exp_avg),
                  (ser.critic.exp_avg_sq, pip.critic.exp_avg_sq), (ser.actors.data, pip.actors.data),
                  (ser.actors.exp_avg, pip.actors.exp_avg), (ser.actors.target, pip.actors.target),
@@ -186,3 +190,41 @@ def test_specialised_row_kernels_equal_generic(cuda):
                  (a.actors.data, b.actors.data), (a.actors.target, b.actors.target), (a.losses, b.losses)):
         assert torch.equal(x, y)
     assert torch.isfinite(a.critic.data).all() and a.losses.abs().sum() > 0
+
+
+@pytest.mark.parametrize("n_slots", [2, 3])
+def test_device_gate_is_bitwise_the_event_wait(n_slots, cuda):
+    """The device-side snapshot gate (the critic row blocks poll a sequence number the `sc1` snapshot publishes)
+    against the cross-queue event wait (FLOCK_SC_GATE=0): the overlapped config-3 loop with env kernels co-running on
+    the env stream (uneven load, L1-warm consumers) ends with every learner tensor bitwise equal, and no round gave
+    up waiting."""
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
+
+    E, Na, steps = 512, 256, 24
+    g = torch.Generator(device=cuda).manual_seed(2)
+    pool = [torch.stack([torch.rand(E, Na, device=cuda, generator=g),
+                         torch.rand(E, Na, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
+    out = []
+    for gate in ("0", "1"):
+        os.environ["FLOCK_SC_GATE"] = gate
+        try:
+            env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
+                                          range_start=(0, 253.0), sensor_range=14.0, step_launches=3), device=cuda)
+            gp = torch.Generator(device=cuda).manual_seed(5)
+            env.positions.copy_(torch.rand(E, Na, 2, device=cuda, generator=gp) * 253.0)
+            env.headings.copy_(torch.rand(E, Na, device=cuda, generator=gp) * 4.7)
+            hook = SharedCriticBench(env, device=cuda, seed=7, n_slots=n_slots)
+            hook.run_steps(0, steps, pool)
+            hook.finish()
+            torch.cuda.synchronize()
+            L = hook.learner
+            L.pipeline_check()
+            assert L.pipeline().gated() == (gate == "1")
+            C, A = L.critic, L.actors
+            out.append([C.data.clone(), C.exp_avg.clone(), C.exp_avg_sq.clone(), A.data.clone(), A.target.clone(),
+                        A.exp_avg.clone(), A.exp_avg_sq.clone(), L.actor_steps.clone(), L.losses.clone()])
+        finally:
+            os.environ.pop("FLOCK_SC_GATE", None)
+    for x, y in zip(*out):
+        assert torch.equal(x, y)

@@ -219,12 +219,14 @@ def test_shared_critic_ops_opcheck_and_bitwise_the_c_abi(flock, cuda):
         # C ABI on the twin
         Lb._learn_calls += 1
         S = Lb._slots[t % 3]
+        ring, stg = _native.sc_rows(Lb._ring_rows), _native.sc_rows(S["job"][2:7])
+        u = _native.sc_update(Lb._sc_learner, S["job"], Lb._sc_dims, Lb._sc_hyper)
         _check(lib.flock_sc_prep_snapshot(_st(cuda), Lb.batch_size, len(Lb.replay), Lb.seed, Lb._learn_calls,
                                           _p(Lb.static_idx), _p(S["agent"]), agent, Lb.input_dim, Lb.n_actions,
-                                          ctypes.byref(Lb._rows_ring), ctypes.byref(S["rows"])),
+                                          ctypes.byref(ring), ctypes.byref(stg)),
                "flock_sc_prep_snapshot")
-        _check(lib.flock_sc_critic_update(_st(cuda), ctypes.byref(S["sc"])), "flock_sc_critic_update")
-        _check(lib.flock_sc_actor_update(_st(cuda), ctypes.byref(S["sc"])), "flock_sc_actor_update")
+        _check(lib.flock_sc_critic_update(_st(cuda), ctypes.byref(u)), "flock_sc_critic_update")
+        _check(lib.flock_sc_actor_update(_st(cuda), ctypes.byref(u)), "flock_sc_actor_update")
         Lb._finish_learn(agent, soft_in_kernel=True)
     for x, y in zip(_sc_state(La), _sc_state(Lb)):
         assert torch.equal(x, y)
@@ -256,8 +258,9 @@ def test_shared_critic_sc_prep_path_bitwise_c_abi(flock, cuda):
         Lb._learn_calls += 1
         _check(lib.flock_sc_prep(_st(cuda), Lb.batch_size, len(Lb.replay), Lb.seed, Lb._learn_calls,
                                  _p(Lb.static_idx), _p(Lb.static_agent), t % 6), "flock_sc_prep")
-        _check(lib.flock_sc_critic_update(_st(cuda), ctypes.byref(Lb._sc)), "flock_sc_critic_update")
-        _check(lib.flock_sc_actor_update(_st(cuda), ctypes.byref(Lb._sc)), "flock_sc_actor_update")
+        u = _native.sc_update(Lb._sc_learner, Lb._sc_job, Lb._sc_dims, Lb._sc_hyper)
+        _check(lib.flock_sc_critic_update(_st(cuda), ctypes.byref(u)), "flock_sc_critic_update")
+        _check(lib.flock_sc_actor_update(_st(cuda), ctypes.byref(u)), "flock_sc_actor_update")
         Lb._finish_learn(t % 6, soft_in_kernel=True)
     for x, y in zip(_sc_state(La)[:10], _sc_state(Lb)[:10]):
         assert torch.equal(x, y)

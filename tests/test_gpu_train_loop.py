@@ -17,7 +17,7 @@ def _bench(cuda):
 
     box = float(round((250 * N) ** 0.5))
     env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=K, collision_distance=2.5,
-                                  range_start=(0, box), sensor_range=14.0, seed=1, step_launches=2), device=cuda)
+                                  range_start=(0, box), sensor_range=14.0, seed=1, step_launches=3), device=cuda)
     g = torch.Generator(device=cuda).manual_seed(0)
     env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
     env.headings.copy_((1.0 - torch.rand(E, N, device=cuda, generator=g)) * 4.712389)
@@ -81,7 +81,8 @@ def test_train_loop_records_timing_events(cuda):
 
 
 def test_config3_bench_step_full_size(cuda):
-    """The exact timed step of bench.py at BASELINE config 3 (4096 envs x 256 agents, v2 periodic, two launches,
+    """The exact timed step of bench.py at BASELINE config 3 (4096 envs x 256 agents, v2 periodic, three launches
+    (bench.py's default: an uneven 1365 / 1365 / 1366 env split),
     compact search seeds, the specialised cell-list instantiation, the replay insert fused into the step, one learn()
     per step through ScTrainLoop), checked on a sample of envs: the step against the C oracle from the same pre-step
     state (state rtol 1e-5; kNN bit-exact on the GPU's own post-step positions), reward / done of every row, and the
@@ -92,7 +93,7 @@ def test_config3_bench_step_full_size(cuda):
 
     E, N, k, box = 4096, 256, 4, 253.0
     env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
-                                  range_start=(0, box), sensor_range=14.0, seed=1234, step_launches=2), device=cuda)
+                                  range_start=(0, box), sensor_range=14.0, seed=1234, step_launches=3), device=cuda)
     g = torch.Generator(device=cuda).manual_seed(1234)
     env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
     env.headings.copy_((1.0 - torch.rand(E, N, device=cuda, generator=g)) * 1.5 * 3.141592653589793)
@@ -102,7 +103,9 @@ def test_config3_bench_step_full_size(cuda):
     hook.run_steps(0, 3, pool)
     hook.finish()
     torch.cuda.synchronize()
-    sample = torch.arange(5, E, 211, device=cuda)
+    # every 211th env plus the envs on each side of the three launches' range boundaries (1365 / 2730)
+    edges = torch.tensor([0, 1364, 1365, 2729, 2730, E - 1], device=cuda)
+    sample = torch.unique(torch.cat([torch.arange(5, E, 211, device=cuda), edges]))
     pre_pos, pre_head = env.positions[sample].cpu().numpy(), env.headings[sample].cpu().numpy()
     prev_obs = env.dnn.clone()
     L = hook.learner
@@ -133,3 +136,30 @@ def test_config3_bench_step_full_size(cuda):
     assert torch.equal(rb["reward"][rows].reshape(-1), env.reward[ei, ii])
     assert torch.equal(rb["new_state"][rows], d[ei, ii])
     assert torch.equal(rb["terminal"][rows].reshape(-1), 1.0 - env.done[ei, ii].float())
+
+
+def test_per_step_calls_between_loop_calls_stay_bitwise(cuda):
+    """Per-step Python steps (SharedCriticBench.step: the step op + pipeline_learn) interleaved with ScTrainLoop
+    calls: the loop takes the Python mirrors' parity / ring counter / learn counter before every call (set_state)
+    and both paths drive the learner's ONE ScPipeline, so the pending actor phase carries over between them. The
+    result is bitwise 12 per-step steps."""
+    pool = _pool(cuda)
+    env_a, hook_a = _bench(cuda)
+    for s in range(12):
+        hook_a.step(s, pool[s % len(pool)])
+    hook_a.finish()
+    env_b, hook_b = _bench(cuda)
+    for s in range(3):
+        hook_b.step(s, pool[s % len(pool)])
+    hook_b.run_steps(3, 4, pool)  # an odd number of per-step steps before: the loop must read the other dnn buffer
+    hook_b.step(7, pool[7 % len(pool)])
+    hook_b.run_steps(8, 3, pool)
+    hook_b.step(11, pool[11 % len(pool)])
+    hook_b.finish()
+    torch.cuda.synchronize()
+    sa, sb = _state(env_a, hook_a), _state(env_b, hook_b)
+    for name in sa:
+        assert torch.equal(sa[name], sb[name]), name
+    La, Lb = hook_a.learner, hook_b.learner
+    assert (La.replay.counter, La._learn_calls, La.count) == (Lb.replay.counter, Lb._learn_calls, Lb.count)
+    assert (env_a._cur, env_a.steps) == (env_b._cur, env_b.steps)
