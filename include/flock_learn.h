@@ -238,6 +238,10 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p);
  * nothing; flock_sc_pipeline_check (synchronous: call after synchronising the learner stream) returns -6 then.
  * flock_sc_pipeline_gated: 1 when the gate is in use. */
 int flock_sc_pipeline_check(FlockScPipeline* p);
+/* The fused three-launch rounds (the reference widths; FLOCK_SC_FUSE=0 keeps five launches) hand rows between the
+ * workgroups of one launch through counters in the update's workspace; a wait that gives up (bounded, 0.2 s) sets an
+ * error word there. Synchronous check of it (flock_sc_pipeline_check checks every slot's workspace too): -6. */
+int flock_sc_workspace_check(const FlockScUpdate* u);
 int flock_sc_pipeline_gated(const FlockScPipeline* p);
 typedef int (*FlockAllreduceFn)(void* ctx, float* data, int64_t n, void* learner_stream);
 int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_off,

@@ -1813,6 +1813,7 @@ Params base(int E, int N, int k, float box) {
 // C ABI
 
 void flock_sc_diag_no_spec(bool v);  // flock_sc.hip
+void flock_sc_diag_no_fuse(bool v);  // flock_sc.hip
 
 extern "C" {
 
@@ -1831,6 +1832,8 @@ int flock_set_diag(const char* name, int value) {
         k.no_cells = value != 0;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
+    else if (!strcmp(name, "sc_no_fuse"))
+        flock_sc_diag_no_fuse(value != 0);
     else
         return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
     return FLOCK_OK;

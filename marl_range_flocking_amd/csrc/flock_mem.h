@@ -44,6 +44,10 @@ __device__ __forceinline__ int64_t ld_sc1(const int64_t* p) {
 __device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ float2 ld_sc1_f2(const float2* p) {
+    return __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT));
+}
 // 16-B `sc1` load
 __device__ __forceinline__ float4 ld_sc1_x4(const float4* p) {
     float4 v;

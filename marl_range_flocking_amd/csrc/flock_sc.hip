@@ -102,7 +102,12 @@ struct Ws {
     float* Z2b;                            // [2][B][H2] actor fc2, critic fc2
     float *AXH2, *ARS2, *AH2, *DM, *ADY2, *ADZ2, *ALOSS;
     float *ADY1, *ADXH1, *APS1;
+    // fused rounds (launch_round_fused): [0, 16) arrivals of the forward GEMM tiles per 32-row tile, [16] arrivals of
+    // the bwd blocks, [17] the launch's finished blocks (the last one resets the counters it used), [18] error word.
+    // Zero between launches (workspaces are allocated zeroed).
+    unsigned* SYNC;
 };
+constexpr int kSyncTiles = 16, kSyncBwd = 16, kSyncDone = 17, kSyncErr = 18, kSyncWords = 64;
 
 int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
     int64_t off = 0;
@@ -125,6 +130,8 @@ int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
     x.AXH2 = take(H2); x.ARS2 = take(1); x.AH2 = take(H2); x.DM = take(na); x.ADY2 = take(H2); x.ADZ2 = take(H2);
     x.ALOSS = take(1);
     x.ADY1 = take(H1); x.ADXH1 = take(H1); x.APS1 = take(ps);
+    x.SYNC = base ? reinterpret_cast<unsigned*>(base + off) : nullptr;
+    off += kSyncWords;
     if (w) *w = x;
     return off;
 }
@@ -224,22 +231,34 @@ __device__ __forceinline__ void ln_stats(const float (&z)[C], int F, int lane, f
     rstd = rsqrt_rn(wave_sum(q) / (float)F + kLnEps);
 }
 
-template <int C>
-__device__ __forceinline__ void load_row(float (&v)[C], const float* p, int F, int lane) {
+// F (fused rounds, launch_round_fused): the row was written by another workgroup of the SAME launch and handed off
+// through an arrival counter, so it is read `sc1` (csrc/flock_mem.h); otherwise by an earlier launch: plain loads
+template <int C, bool F = false>
+__device__ __forceinline__ void load_row(float (&v)[C], const float* p, int Fw, int lane) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int j = lane + 64 * c;
-        v[c] = j < F ? p[j] : 0.0f;
+        v[c] = j < Fw ? (F ? flock_mem::ld_sc1(p + j) : p[j]) : 0.0f;
     }
 }
+// reads of data another workgroup of the same launch produced (fused rounds): `sc1`
+template <bool F>
+__device__ __forceinline__ float ld_in(const float* p) {
+    return F ? flock_mem::ld_sc1(p) : *p;
+}
 // stores of the kernels' per-row outputs (read by the next launch of the round); -DFLOCK_SC_NT (diagnostics A/B)
-// makes them non-temporal
+// makes them non-temporal. F: read by a later workgroup of the same launch (fused rounds): write-through `sc1`
+template <bool F = false>
 __device__ __forceinline__ void st_out(float* p, float v) {
+    if constexpr (F) {
+        flock_mem::st_sc1(p, v);
+    } else {
 #ifdef FLOCK_SC_NT
-    __builtin_nontemporal_store(v, p);
+        __builtin_nontemporal_store(v, p);
 #else
-    *p = v;
+        *p = v;
 #endif
+    }
 }
 template <int C>
 __device__ __forceinline__ void store_row(float* p, const float (&v)[C], int F, int lane) {
@@ -364,7 +383,7 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
 }
 
 // c3: heads, TD target, MSE and the critic backward down to the fc2 pre-activation
-template <int C, int HC, int NAC>
+template <int C, int HC, int NAC, bool F = false>
 __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);  // critic tail
@@ -378,9 +397,9 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     float zt[C], zn[C], zs[C];
     float rwd = 0.0f, term = 0.0f, act[kMaxAct];
     if (live) {
-        load_row<C>(zt, w.Z2 + (int64_t)r * H2, H2, lane);
-        load_row<C>(zn, w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
-        load_row<C>(zs, w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
+        load_row<C, F>(zt, w.Z2 + (int64_t)r * H2, H2, lane);
+        load_row<C, F>(zn, w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
+        load_row<C, F>(zs, w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
         rwd = w.R[r];
         term = w.T[r];
 #pragma unroll
@@ -506,7 +525,7 @@ __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, i
 
 // a3: actor LN2/ReLU/mu/tanh, Q(s, mu) with the updated critic, actor loss -mean Q, and the backward through the
 // critic's action branch (dQ/dmu) and the actor head down to the actor's fc2 pre-activation
-template <int C, int HC, int NAC>
+template <int C, int HC, int NAC, bool F = false>
 __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);
@@ -520,8 +539,8 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     const int64_t ro = (int64_t)r * H2;
     float za2[C], zc2[C];
     if (live) {
-        load_row<C>(za2, w.Z2b + ro, H2, lane);
-        load_row<C>(zc2, w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
+        load_row<C, F>(za2, w.Z2b + ro, H2, lane);
+        load_row<C, F>(zc2, w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
     stage(at, a.actors + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
@@ -720,6 +739,7 @@ struct GemmP {
     const int64_t* agent;
     int tiles_n, tiles;
     int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
+    unsigned* sig;  // fused rounds: one arrival per finished tile at sig[tile row] (the k3 rows' hand-off); NULL: none
 };
 constexpr int kMaxBatch = 5;  // a round's forward GEMMs: 3 (critic phase) + 2 (actor phase)
 struct GemmBatch {
@@ -958,16 +978,15 @@ __device__ __forceinline__ int xcd_tile(int x, int tiles) {
     return (tiles & 7) == 0 && (int)gridDim.x == tiles ? (x & 7) * (tiles >> 3) + (x >> 3) : x;
 }
 
-// grid (max tiles, problems): block (x, y) computes tile xcd_tile(x) of problem y
-template <int AV, int BV, int NF>
-__global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
-    SC_PROF(1);
-    SC_PRIO();
+// one forward GEMM tile: block x of problem y computes tile xcd_tile(x). F (fused rounds): the tile is stored
+// write-through and its arrival counted at g.sig[tile row] once every wave's stores have completed (csrc/flock_mem.h)
+template <int AV, int BV, int NF, bool F>
+__device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
-    const GemmP& g = gb.p[blockIdx.y];
-    if ((int)blockIdx.x >= g.tiles) return;
-    const int t = xcd_tile(blockIdx.x, g.tiles);
+    const GemmP& g = gb.p[y];
+    if (x >= g.tiles) return;
+    const int t = xcd_tile(x, g.tiles);
     const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
     const int64_t rel = g.relB ? g.relB * (*g.agent) : 0;
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -978,8 +997,21 @@ __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-        if (m < g.M && n < g.N) st_out(g.C + (int64_t)m * g.ldc + n, g.bias ? out[q] + bias : out[q]);
+        if (m < g.M && n < g.N) st_out<F>(g.C + (int64_t)m * g.ldc + n, g.bias ? out[q] + bias : out[q]);
     }
+    if (F) {
+        flock_mem::wait_vmem();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(g.sig + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// grid (max tiles, problems): block (x, y) computes tile xcd_tile(x) of problem y
+template <int AV, int BV, int NF>
+__global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
+    SC_PROF(1);
+    SC_PRIO();
+    gemm_block<AV, BV, NF, false>(gb, blockIdx.y, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1015,6 +1047,8 @@ struct DzArgs {
 
 // One block's reduction: the 16-element slice of rp for block b (thread el = tid & 15, row group q = tid >> 4);
 // returns the sum in threads q == 0 (0 elsewhere). part: 256 floats of LDS; mst: [B][2] LDS (modes 4 / 5)
+// F (fused rounds): D and the row sums PS were written by the bwd blocks of the same launch: `sc1` loads
+template <bool F = false>
 __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const DzArgs& dz, float* part, float* mst,
                                            int& e_out, bool& live_out) {
     const int tid = threadIdx.x;
@@ -1036,7 +1070,7 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
         for (int k = 0; k < kRB; ++k) {
             const int r = r0 + 16 * k;
             const bool in = live && r < B;
-            dv[k] = in ? rp.D[(int64_t)r * rp.ldd + o] : 0.0f;
+            dv[k] = in ? ld_in<F>(rp.D + (int64_t)r * rp.ldd + o) : 0.0f;
             xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
             xh[k] = (in && dzm) ? dz.XH[(int64_t)r * dz.F + o] : 0.0f;
             rs[k] = (in && dzm) ? dz.RS[r] : 0.0f;
@@ -1053,7 +1087,8 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
             for (int t0 = 0; t0 < dz.ntn; t0 += kPB) {
                 float2 v[kPB];
 #pragma unroll
-                for (int u = 0; u < kPB; ++u) v[u] = t0 + u < dz.ntn ? ps[t0 + u] : make_float2(0.0f, 0.0f);
+                for (int u = 0; u < kPB; ++u)
+                    v[u] = t0 + u < dz.ntn ? (F ? flock_mem::ld_sc1_f2(ps + t0 + u) : ps[t0 + u]) : make_float2(0.0f, 0.0f);
 #pragma unroll
                 for (int u = 0; u < kPB; ++u)
                     if (t0 + u < dz.ntn) {
@@ -1109,7 +1144,8 @@ struct BwdJob {
 __host__ __device__ inline int bwd_blocks(const BwdJob& j) { return j.dh.tiles + j.dw.tiles + j.nblk; }
 
 // the 4 rows of thread (wave w, lane l) in a 32 x 32 tile: 8w + 4(l >> 5) + q; its column: l & 31
-template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
+// F (fused rounds): every output is read by the grad blocks of the same launch: write-through `sc1` stores
+template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW, bool F = false>
 __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
@@ -1142,8 +1178,8 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
             const float dy = hv[q] > 0.0f ? out[q] : 0.0f;  // through the ReLU
             const float dxh = dy * gam;
             if (ok) {
-                st_out(j.DY1 + (int64_t)m * j.F + n, dy);
-                st_out(j.DXH1 + (int64_t)m * j.F + n, dxh);
+                st_out<F>(j.DY1 + (int64_t)m * j.F + n, dy);
+                st_out<F>(j.DXH1 + (int64_t)m * j.F + n, dxh);
             }
             s1[q] = ok ? dxh : 0.0f;
             s2[q] = ok ? dxh * xv[q] : 0.0f;
@@ -1161,8 +1197,8 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
             for (int q = 0; q < 4; ++q) {
                 const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
                 if (m < g.M) {
-                    j.PS1[((int64_t)m * j.ntn + tn) * 2] = s1[q];
-                    j.PS1[((int64_t)m * j.ntn + tn) * 2 + 1] = s2[q];
+                    st_out<F>(j.PS1 + ((int64_t)m * j.ntn + tn) * 2, s1[q]);
+                    st_out<F>(j.PS1 + ((int64_t)m * j.ntn + tn) * 2 + 1, s2[q]);
                 }
             }
         }
@@ -1176,7 +1212,7 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int mm = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-            if (mm < g.M && nn < g.N) j.grad[gbase + j.w2_off + (int64_t)mm * g.ldc + nn] = out[q];
+            if (mm < g.M && nn < g.N) st_out<F>(j.grad + gbase + j.w2_off + (int64_t)mm * g.ldc + nn, out[q]);
         }
     } else {
         const int b = bx - j.dh.tiles - j.dw.tiles;
@@ -1190,9 +1226,9 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
         const float gsum = red_block(rp, b, j.B, none, smem, nullptr, e, wr);
         if (wr) {
             if (rp.mode == 3)
-                *j.loss = gsum * (1.0f / (float)j.B);
+                st_out<F>(j.loss, gsum * (1.0f / (float)j.B));
             else
-                j.grad[gbase + rp.off + e] = gsum;
+                st_out<F>(j.grad + gbase + rp.off + e, gsum);
         }
     }
 }
@@ -1268,6 +1304,8 @@ __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamSt
 
 // one job's blocks of the late launch: [0, nblk) reductions, [nblk, + adam_blocks) Adam of the bwd launch's
 // gradients, then soft_blocks self soft update blocks
+// F (fused rounds): the gradients and LN1 row sums the bwd blocks of the same launch wrote are read `sc1`
+template <bool F = false>
 __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int nb) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
@@ -1310,7 +1348,7 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
         for (int q = 0; q < 4; ++q) {
             const int64_t e = e0 + q * 256 + tid;
             st[q] = e < end ? adam_load(ga, base + e) : AdamState{0.f, 0.f, 0.f, 0.f};
-            gi[q] = e < end ? ga.grad[gbase + e] : 0.0f;
+            gi[q] = e < end ? ld_in<F>(ga.grad + gbase + e) : 0.0f;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1328,7 +1366,7 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
         const AdamState st = ad ? adam_load(ga, base + rp.off + e1) : AdamState{0.f, 0.f, 0.f, 0.f};
         int e;
         bool wr;
-        const float gsum = red_block(rp, b, ga.B, ga.dz, smem, smem + 256, e, wr);
+        const float gsum = red_block<F>(rp, b, ga.B, ga.dz, smem, smem + 256, e, wr);
         if (wr) {
             ga.grad[gbase + rp.off + e] = gsum;
             if (ga.do_adam) adam_store(ga, base + rp.off + e, st, gsum, sh[0], sh[1], sh_soft != 0);
@@ -1358,6 +1396,112 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
         grad_adam_body(gg.j0, blockIdx.x, gg.nb0);
     else
         grad_adam_body(gg.j1, blockIdx.x - gg.nb0, gridDim.x - gg.nb0);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Fused rounds: three launches instead of five. [k1] rows, then ONE launch of the forward GEMM tiles and the k3 rows
+// (each k3 block waits for the tiles of its 32-row tile), then ONE launch of the bwd blocks and the gradient / Adam
+// blocks (each waits for every bwd block of its job). Hand-offs inside a launch follow MI355X_MICROARCH.md's row 1
+// (csrc/flock_mem.h): the producer's outputs are stored `sc1`, every wave waits for its stores, a workgroup barrier,
+// one lane's agent-scope counter add; the consumer's lane 0 polls the counter with `sc1` loads, a workgroup barrier,
+// then `sc1` loads of the handed-off rows. Consumers have higher block indices than every producer they wait for, so
+// they are dispatched after them and the wait always ends; a wait beyond kGateTimeoutTicks sets the workspace's error
+// word and the block computes nothing (flock_sc_pipeline_check / flock_sc_workspace_check report it). The counters
+// are zero between launches: the launch's last finishing block resets the ones it used. The math of every block is
+// the unfused kernels' (results bitwise equal: tests/test_gpu_overlap.py).
+__device__ __forceinline__ bool wait_count(const unsigned* ctr, unsigned need, unsigned* err) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        int good = 1;
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    good = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+// every block of a fused launch ends here: the last one to finish resets the counters the launch used
+struct SyncReset {
+    unsigned* done;
+    unsigned total;  // blocks of the launch
+    unsigned* r[2];  // counter ranges to zero
+    int n[2];
+};
+__device__ __forceinline__ void launch_done(const SyncReset& sr) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(sr.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == sr.total - 1u) {
+            for (int k = 0; k < 2; ++k)
+                for (int i = 0; i < sr.n[k]; ++i) __hip_atomic_store(sr.r[k] + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sr.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+struct K3Side {
+    Ws w;
+    RowArgs a;
+    int nb;         // k3 blocks of this job (0: absent)
+    unsigned need;  // tile arrivals per 32-row tile (paths x column tiles)
+};
+// forward launch: grid (max tiles, problems + k3 rows): y < gb.n GEMM tiles (signalling), then the k3 blocks of the
+// critic job (kc) and of the actor job (ka), linear index over the trailing rows
+template <int AV, int BV, int NF, int C, int HC, int NAC>
+__global__ __launch_bounds__(256) void sc_fwd(GemmBatch gb, K3Side kc, K3Side ka, SyncReset sr) {
+    SC_PRIO();
+    const int y = blockIdx.y;
+    if (y < gb.n) {
+        gemm_block<AV, BV, NF, true>(gb, y, blockIdx.x);
+    } else {
+        const int kb = (y - gb.n) * (int)gridDim.x + (int)blockIdx.x;
+        if (kb < kc.nb) {
+            if (wait_count(kc.w.SYNC + (kb * kRowsPerBlock) / kT, kc.need, kc.w.SYNC + kSyncErr))
+                c3_body<C, HC, NAC, true>(kc.w, kc.a, kb);
+        } else if (kb < kc.nb + ka.nb) {
+            const int b = kb - kc.nb;
+            if (wait_count(ka.w.SYNC + (b * kRowsPerBlock) / kT, ka.need, ka.w.SYNC + kSyncErr))
+                a3_body<C, HC, NAC, true>(ka.w, ka.a, b);
+        }
+    }
+    launch_done(sr);
+}
+// backward launch: [bwd blocks of j0 | of j1 | gradient / Adam blocks of j0 | of j1]
+struct BwdSync {
+    unsigned* arr[2];  // bwd arrivals of each job
+    unsigned* err[2];
+    int nbw[2];        // bwd blocks of each job (0: absent)
+};
+template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
+__global__ __launch_bounds__(256) void sc_bwdg(Bwd2 bb, GradAdam2 gg, BwdSync bs, SyncReset sr) {
+    SC_PRIO();
+    const int bx = blockIdx.x;
+    const int nbw = bs.nbw[0] + bs.nbw[1];
+    if (bx < nbw) {
+        const int j = bx < bs.nbw[0] ? 0 : 1;
+        bwd_body<AVH, BVH, AVW, BVW, NFH, NFW, true>(j == 0 ? bb.j0 : bb.j1, j == 0 ? bx : bx - bs.nbw[0]);
+        flock_mem::wait_vmem();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(bs.arr[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        const int g = bx - nbw;
+        const int j = g < gg.nb0 ? 0 : 1;
+        if (wait_count(bs.arr[j], (unsigned)bs.nbw[j], bs.err[j])) {
+            if (j == 0)
+                grad_adam_body<true>(gg.j0, g, gg.nb0);
+            else
+                grad_adam_body<true>(gg.j1, g - gg.nb0, (int)gridDim.x - nbw - gg.nb0);
+        }
+    }
+    launch_done(sr);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1395,6 +1539,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
     g.kchunk = balanced_kc(K, fwd_kc());
+    g.sig = nullptr;
     return g;
 }
 
@@ -1728,11 +1873,14 @@ bool spec_shape(const Job& j) { return !g_sc_no_spec && j.H1 == 400 && j.H2 == 3
 // One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in five launches; either may be
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
 // computes exactly what the actor phase followed by the critic phase would.
+int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja);
+
 int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
     const Job& A = jc ? *jc : *ja;  // the first job (placeholder arguments for an absent one)
     const Job& Z = ja ? *ja : *jc;
     if (jc && ja && (jc->B != ja->B || jc->in != ja->in || jc->na != ja->na || jc->H1 != ja->H1 || jc->H2 != ja->H2))
         return fail(-5, "flock_sc_round: the two updates must have the same shapes");
+    if (const int fr = launch_round_fused(st, jc, ja); fr != 1) return fr;  // the three-launch round (or its error)
     const int C = A.C, rb = A.rb;
     int rc = 0;
     {  // 1: fc1 rows
@@ -1809,6 +1957,97 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
     const size_t lds = red_lds(A.B);
     if ((rc = allow_lds(sc_grad_adam, lds))) return rc;
     hipLaunchKernelGGL(sc_grad_adam, dim3(nb), dim3(256), lds, st, gg);
+    return launched();
+}
+
+// FLOCK_SC_FUSE=0 (read once) or flock_set_diag("sc_no_fuse", 1): the five-launch rounds everywhere (A/B and the
+// bitwise tests of the fused rounds)
+bool g_sc_no_fuse = false;
+bool fuse_rounds() {
+    static const bool on = [] {
+        const char* e = getenv("FLOCK_SC_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    return on && !g_sc_no_fuse;
+}
+
+// The fused three-launch round (see sc_fwd / sc_bwdg) where its instantiation covers the shapes: the reference's
+// widths (fc1 400, fc2 300, 2 actions: the specialised row kernels), the forward GEMMs on the (k-contiguous,
+// k-contiguous) panel loaders at 7 float4 per operand (balanced K chunks of 200), the bwd launch's fast variant and
+// B <= 512 (16 row tiles). Returns 1 when the shapes are not covered (the caller runs the five launches).
+int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja) {
+    const Job& A = jc ? *jc : *ja;
+    const Job& Z = ja ? *ja : *jc;
+    const bool both = jc && ja;
+    if (!fuse_rounds() || !spec_shape(A) || A.B > kSyncTiles * kT || A.rb > 65535) return 1;
+    GemmBatch gb;
+    gb.n = 0;
+    if (jc)
+        for (int i = 0; i < jc->nfwd; ++i) {
+            gb.p[gb.n] = jc->fwd[i];
+            gb.p[gb.n++].sig = jc->w.SYNC;
+        }
+    if (ja)
+        for (int i = 0; i < ja->nfwd; ++i) {
+            gb.p[gb.n] = ja->fwd[i];
+            gb.p[gb.n++].sig = ja->w.SYNC;
+        }
+    int kc = 8, tiles = 0;
+    for (int i = 0; i < gb.n; ++i) {
+        if (gemm_variant(gb.p[i]) != 0) return 1;
+        const int c = gemm_kc(gb.p[i].K, gb.p[i].kchunk);
+        kc = c > kc ? c : kc;
+        tiles = gb.p[i].tiles > tiles ? gb.p[i].tiles : tiles;
+    }
+    if (nf_of(kc) != 7) return 1;
+    int kh = 8, kw = 8;
+    for (const BwdJob* b : {&A.bw, &Z.bw}) {
+        if (gemm_variant(b->dh) != 1 || gemm_variant(b->dw) != 2) return 1;
+        const int ch = gemm_kc(b->dh.K, b->dh.kchunk), cw = gemm_kc(b->dw.K, b->dw.kchunk);
+        kh = ch > kh ? ch : kh;
+        kw = cw > kw ? cw : kw;
+    }
+    if (nf_of(kh) != 7 || nf_of(kw) != 4) return 1;
+    if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks || A.bw.nblk > kMaxRedBlocks) return 1;
+    int rc = 0;
+    const int C = A.C, rb = A.rb, tile_rows = (A.B + kT - 1) / kT;
+    {  // 1: fc1 rows (the unfused row launch)
+        const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
+        const size_t lds = zmax(A.lds1, Z.lds1);
+        const dim3 grid(rb, npc + npa);
+        (void)C;
+        if ((rc = allow_lds(sc_k1<7, 400>, lds))) return rc;
+        hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a);
+        if ((rc = launched())) return rc;
+    }
+    {  // 2: forward GEMM tiles + the k3 rows
+        K3Side kcs{jc ? jc->w : A.w, jc ? jc->a : A.a, jc ? rb : 0, (unsigned)(3 * gb.p[0].tiles_n)};
+        K3Side kas{ja ? ja->w : A.w, ja ? ja->a : A.a, ja ? rb : 0, (unsigned)(2 * gb.p[0].tiles_n)};
+        const int nk3 = kcs.nb + kas.nb;
+        const dim3 grid(tiles, gb.n + (nk3 + tiles - 1) / tiles);
+        const size_t lds = zmax(gemm_lds_bytes(kc, kc), zmax(A.lds3, Z.lds3));
+        SyncReset sr{A.w.SYNC + kSyncDone, grid.x * grid.y, {jc ? jc->w.SYNC : nullptr, ja ? ja->w.SYNC : nullptr},
+                     {jc ? tile_rows : 0, ja ? tile_rows : 0}};
+        if ((rc = allow_lds(sc_fwd<0, 0, 7, 5, 300, 2>, lds))) return rc;
+        hipLaunchKernelGGL((sc_fwd<0, 0, 7, 5, 300, 2>), grid, dim3(256), lds, st, gb, kcs, kas, sr);
+        if ((rc = launched())) return rc;
+    }
+    // 3: bwd blocks + gradient / Adam blocks
+    Bwd2 bb;
+    bb.j0 = A.bw;
+    bb.j1 = Z.bw;
+    bb.nb0 = bwd_blocks(A.bw);
+    GradAdam2 gg;
+    gg.j0 = A.ga;
+    gg.j1 = Z.ga;
+    gg.nb0 = late_blocks(A.ga);
+    BwdSync bs{{A.w.SYNC + kSyncBwd, Z.w.SYNC + kSyncBwd}, {A.w.SYNC + kSyncErr, Z.w.SYNC + kSyncErr},
+               {bb.nb0, both ? bwd_blocks(Z.bw) : 0}};
+    const int nb = bs.nbw[0] + bs.nbw[1] + gg.nb0 + (both ? late_blocks(Z.ga) : 0);
+    const size_t lds = zmax(zmax(bwd_lds(A.bw), bwd_lds(Z.bw)), red_lds(A.B));
+    SyncReset sr{A.w.SYNC + kSyncDone, (unsigned)nb, {A.w.SYNC + kSyncBwd, Z.w.SYNC + kSyncBwd}, {1, both ? 1 : 0}};
+    if ((rc = allow_lds(sc_bwdg<0, 1, 1, 1, 7, 4>, lds))) return rc;
+    hipLaunchKernelGGL((sc_bwdg<0, 1, 1, 1, 7, 4>), dim3(nb), dim3(256), lds, st, bb, gg, bs, sr);
     return launched();
 }
 
@@ -1910,6 +2149,7 @@ __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows
 
 // the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
 void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
+void flock_sc_diag_no_fuse(bool v) { g_sc_no_fuse = v; }
 
 extern "C" {
 
@@ -2272,12 +2512,26 @@ int flock_sc_mark_read(unsigned long long* host) {
 
 int flock_sc_pipeline_check(FlockScPipeline* p) {
     if (!p) return fail(-3, "flock_sc_pipeline_check: NULL pipeline");
+    for (int i = 0; i < p->n; ++i)
+        if (int rc = flock_sc_workspace_check(&p->u[i])) return rc;
     if (!p->gate) return 0;
     unsigned long long flag = 0;
     if (hipMemcpy(&flag, p->gate + 1, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_check: copy failed");
     return flag ? fail(-6, "flock_sc_pipeline: a learn() round gave up waiting for its minibatch snapshot (device gate "
                            "timeout); its results are invalid")
+                : 0;
+}
+
+int flock_sc_workspace_check(const FlockScUpdate* u) {
+    if (!u || !u->workspace) return fail(-3, "flock_sc_workspace_check: NULL argument");
+    Ws w;
+    ws_layout(u->B, u->in_dim, u->n_actions, u->fc1, u->fc2, u->workspace, &w);
+    unsigned flag = 0;
+    if (hipMemcpy(&flag, w.SYNC + kSyncErr, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(-4, "flock_sc_workspace_check: copy failed");
+    return flag ? fail(-6, "flock_sc: a fused round's block gave up waiting for its inputs (hand-off timeout); the "
+                           "update's results are invalid")
                 : 0;
 }
 

@@ -527,10 +527,14 @@ class SharedCriticLearner:
             self._pipe.flush(int(learner_stream))
 
     def pipeline_check(self):
-        """Raise if a pipelined round gave up waiting for its minibatch snapshot (the device-side gate's bounded
-        wait, flock_sc_pipeline_check): its update is invalid. Synchronous; call after synchronising."""
+        """Raise if a round gave up waiting for its inputs: the device-side snapshot gate or a fused round's in-launch
+        hand-off (bounded waits; flock_sc_pipeline_check / flock_sc_workspace_check): its update is invalid.
+        Synchronous; call after synchronising."""
         if self._pipe is not None:
             self._pipe.verify()
+        if self.fused:
+            for ws in self.sc_workspaces:
+                _ops().sc_check(ws, self._sc_dims)
 
     # ------------------------------------------------------------------ data-parallel rounds (bench, N > 1)
     def _dp_round(self, c, a):
