@@ -504,8 +504,9 @@ class SharedCriticLearner:
             p = torch.classes.flock.ScPipeline(self._sc_learner, slots, self._ring_rows, self._sc_dims,
                                                self._sc_hyper)
             if self.distributed:
-                p.set_dp(self.group if self.group is not None else torch.distributed.group.WORLD, self.dp_bucket,
-                         self.critic.numel, self.dp_actor_off, self.inv_world)
+                group = self.group if self.group is not None else torch.distributed.group.WORLD
+                # the c10d ProcessGroup as the TorchScript object the C++ class takes (ProcessGroup.boxed())
+                p.set_dp(group.boxed(), self.dp_bucket, self.critic.numel, self.dp_actor_off, self.inv_world)
             self._pipe = p
         return self._pipe
 

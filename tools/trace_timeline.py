@@ -21,7 +21,9 @@ def load(path):
 
 
 def short(name):
-    for key in ("step_kernel", "sc_prep_snapshot", "sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam"):
+    # the fused rounds' kernels (sc_fwd, sc_bwdg) are checked before the prefixes they contain
+    for key in ("step_kernel", "sc_prep_snapshot", "sc_k1", "sc_fwd", "sc_bwdg", "sc_gemm", "sc_k3", "sc_bwd",
+                "sc_grad_adam"):
         if key in name:
             return key
     return None
@@ -39,20 +41,24 @@ def main():
             env_steps.append((cur, (s, e)))
             cur = []
     rounds, rc = [], {}
+    last = "sc_grad_adam"
     for s, e, k in rows:
         if k == "sc_k1":
             rc = {"sc_k1": (s, e)}
         elif k.startswith("sc_") and k != "sc_prep_snapshot" and rc:
             rc[k] = (s, e)
-            if k == "sc_grad_adam":
+            if k in ("sc_grad_adam", "sc_bwdg"):
+                last = k
                 rounds.append(rc)
                 rc = {}
+    fused = last == "sc_bwdg"
+    order = ["sc_k1", "sc_fwd", "sc_bwdg"] if fused else ["sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam"]
     n = min(len(env_steps), len(rounds))
     skip = max(0, n - 60)  # the last 60 steps (the timed region sits at the end of a short bench)
     t0 = env_steps[skip][0][0][0]
     per, env_span, rnd_span, snap_gap, env_idle = [], [], [], [], []
-    kgaps = {k: [] for k in ("sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam")}
-    kdur = {k: [] for k in ("sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam")}
+    kgaps = {k: [] for k in order[1:]}
+    kdur = {k: [] for k in order}
     for i in range(skip, n - 1):
         launches, snap = env_steps[i]
         nxt = env_steps[i + 1][0][0][0]
@@ -63,9 +69,10 @@ def main():
         r = next((rr for rr in rounds if rr["sc_k1"][0] >= snap[1]), None)
         if r is None:
             continue
+        if any(k not in r for k in order):
+            continue
         snap_gap.append((r["sc_k1"][0] - snap[1]) / 1e3)
-        rnd_span.append((r["sc_grad_adam"][1] - r["sc_k1"][0]) / 1e3)
-        order = ["sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam"]
+        rnd_span.append((r[order[-1]][1] - r["sc_k1"][0]) / 1e3)
         for a, b in zip(order, order[1:]):
             kgaps[b].append((r[b][0] - r[a][1]) / 1e3)
         for k in order:
@@ -74,7 +81,7 @@ def main():
             ls = " ".join("%7.1f-%7.1f" % ((s - t0) / 1e3, (e - t0) / 1e3) for s, e in launches)
             print("step %3d env %s snap %7.1f-%7.1f | round %7.1f-%7.1f" % (
                 i - skip, ls, (snap[0] - t0) / 1e3, (snap[1] - t0) / 1e3, (r["sc_k1"][0] - t0) / 1e3,
-                (r["sc_grad_adam"][1] - t0) / 1e3))
+                (r[order[-1]][1] - t0) / 1e3))
 
     def m(v):
         return "%.1f (p10 %.1f p90 %.1f)" % (st.mean(v), sorted(v)[len(v) // 10], sorted(v)[9 * len(v) // 10])
