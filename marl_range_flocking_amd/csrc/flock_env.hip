@@ -1814,6 +1814,7 @@ Params base(int E, int N, int k, float box) {
 
 void flock_sc_diag_no_spec(bool v);  // flock_sc.hip
 void flock_sc_diag_no_fuse(bool v);  // flock_sc.hip
+void flock_sc_diag_fuse_k1(int v);   // flock_sc.hip
 
 extern "C" {
 
@@ -1834,6 +1835,8 @@ int flock_set_diag(const char* name, int value) {
         flock_sc_diag_no_spec(value != 0);
     else if (!strcmp(name, "sc_no_fuse"))
         flock_sc_diag_no_fuse(value != 0);
+    else if (!strcmp(name, "sc_fuse_k1"))  // 0 / 1; -1: back to FLOCK_SC_FUSE
+        flock_sc_diag_fuse_k1(value);
     else
         return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
     return FLOCK_OK;

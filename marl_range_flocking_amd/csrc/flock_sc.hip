@@ -107,7 +107,8 @@ struct Ws {
     // Zero between launches (workspaces are allocated zeroed).
     unsigned* SYNC;
 };
-constexpr int kSyncTiles = 16, kSyncBwd = 16, kSyncDone = 17, kSyncErr = 18, kSyncWords = 64;
+// [20 + 16 path + tile): arrivals of the k1 row blocks per path and 32-row tile (the k1-fused forward launch)
+constexpr int kSyncTiles = 16, kSyncBwd = 16, kSyncDone = 17, kSyncErr = 18, kSyncK1 = 20, kSyncWords = 128;
 
 int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
     int64_t off = 0;
@@ -260,12 +261,12 @@ __device__ __forceinline__ void st_out(float* p, float v) {
 #endif
     }
 }
-template <int C>
+template <int C, bool FU = false>
 __device__ __forceinline__ void store_row(float* p, const float (&v)[C], int F, int lane) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int j = lane + 64 * c;
-        if (j < F) st_out(p + j, v[c]);
+        if (j < F) st_out<FU>(p + j, v[c]);
     }
 }
 
@@ -335,7 +336,9 @@ __device__ __forceinline__ void ln_backward(const float (&dy)[C], const float (&
 
 // ---------------------------------------------------------------------------------------------------------------
 // c1 (grid.y = path): 0 target actor on s', 1 critic on s', 2 critic on s (+ the gathered minibatch rows)
-template <int C, int HC>
+// F (the k1-fused forward launch): every output row is read by later workgroups of the same launch (the GEMM tiles,
+// the k3 rows): stored write-through `sc1`
+template <int C, int HC, bool F = false>
 __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, int path) {
     const int H1 = HC ? HC : a.H1;
     extern __shared__ float4 smem4[];
@@ -355,13 +358,13 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
         if (lane < a.in) xs[wv * kMaxIn + lane] = xv;
         if (path == 2) {
             if (lane < a.in) {
-                w.S[(int64_t)r * a.in + lane] = xv;
-                w.S2[(int64_t)r * a.in + lane] = ld_sc1(a.rs2 + ir * a.in + lane);
+                st_out<F>(w.S + (int64_t)r * a.in + lane, xv);
+                st_out<F>(w.S2 + (int64_t)r * a.in + lane, ld_sc1(a.rs2 + ir * a.in + lane));
             }
-            if (lane < a.na) w.A[(int64_t)r * a.na + lane] = ld_sc1(a.ra + ir * a.na + lane);
+            if (lane < a.na) st_out<F>(w.A + (int64_t)r * a.na + lane, ld_sc1(a.ra + ir * a.na + lane));
             if (lane == 0) {
-                w.R[r] = ld_sc1(a.rr + ir);
-                w.T[r] = ld_sc1(a.rt + ir);
+                st_out<F>(w.R + r, ld_sc1(a.rr + ir));
+                st_out<F>(w.T + r, ld_sc1(a.rt + ir));
             }
         }
     }
@@ -372,13 +375,13 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
     fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
     const int64_t ro = (int64_t)r * H1;
     if (path == 0) {
-        store_row<C>(w.TH1 + ro, h, H1, lane);
+        store_row<C, F>(w.TH1 + ro, h, H1, lane);
     } else if (path == 1) {
-        store_row<C>(w.NH1 + ro, h, H1, lane);
+        store_row<C, F>(w.NH1 + ro, h, H1, lane);
     } else {
-        store_row<C>(w.XH1 + ro, xh, H1, lane);
-        store_row<C>(w.H1 + ro, h, H1, lane);
-        if (lane == 0) w.RS1[r] = rs;
+        store_row<C, F>(w.XH1 + ro, xh, H1, lane);
+        store_row<C, F>(w.H1 + ro, h, H1, lane);
+        if (lane == 0) st_out<F>(w.RS1 + r, rs);
     }
 }
 
@@ -400,10 +403,10 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
         load_row<C, F>(zt, w.Z2 + (int64_t)r * H2, H2, lane);
         load_row<C, F>(zn, w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
         load_row<C, F>(zs, w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
-        rwd = w.R[r];
-        term = w.T[r];
+        rwd = ld_in<F>(w.R + r);
+        term = ld_in<F>(w.T + r);
 #pragma unroll
-        for (int o = 0; o < kMaxAct; ++o) act[o] = o < na ? w.A[(int64_t)r * na + o] : 0.0f;
+        for (int o = 0; o < kMaxAct; ++o) act[o] = o < na ? ld_in<F>(w.A + (int64_t)r * na + o) : 0.0f;
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
     stage(at, a.actors_target + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
@@ -497,7 +500,7 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
 
 // c5 / a5: ReLU + LN1 backward: dy = dh * [h > 0]; dz = LN backward(dy)
 // a1 (grid.y = path): 0 the agent's actor fc1/LN/ReLU on s (saved for backward), 1 the updated critic's on s
-template <int C, int HC>
+template <int C, int HC, bool F = false>
 __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, int path) {
     const int H1 = HC ? HC : a.H1;
     extern __shared__ float4 smem4[];
@@ -515,11 +518,11 @@ __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, i
     fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
     const int64_t ro = (int64_t)r * H1;
     if (path == 0) {
-        store_row<C>(w.AXH1 + ro, xh, H1, lane);
-        store_row<C>(w.AH1 + ro, h, H1, lane);
-        if (lane == 0) w.ARS1[r] = rs;
+        store_row<C, F>(w.AXH1 + ro, xh, H1, lane);
+        store_row<C, F>(w.AH1 + ro, h, H1, lane);
+        if (lane == 0) st_out<F>(w.ARS1 + r, rs);
     } else {
-        store_row<C>(w.CH1 + ro, h, H1, lane);
+        store_row<C, F>(w.CH1 + ro, h, H1, lane);
     }
 }
 
@@ -696,6 +699,27 @@ __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned lon
     return ok != 0;
 }
 
+// a fused launch's wait for n arrivals on a counter (same hand-off form as gate_wait)
+__device__ __forceinline__ bool wait_count(const unsigned* ctr, unsigned need, unsigned* err) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        int good = 1;
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    good = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     SC_PROF(0);
@@ -740,6 +764,7 @@ struct GemmP {
     int tiles_n, tiles;
     int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
     unsigned* sig;  // fused rounds: one arrival per finished tile at sig[tile row] (the k3 rows' hand-off); NULL: none
+    const unsigned* wait;  // k1-fused forward launch: the k1 row blocks' arrivals per tile row of A
 };
 constexpr int kMaxBatch = 5;  // a round's forward GEMMs: 3 (critic phase) + 2 (actor phase)
 struct GemmBatch {
@@ -832,18 +857,27 @@ __device__ __forceinline__ void load_panel(float* __restrict__ P, const float* _
 // panel_fetch issues the global loads into registers, panel_store writes them to LDS. gemm_tile fetches the A and
 // B panels of a chunk together (one memory round trip instead of two) and the next chunk's panels before the
 // current chunk's MFMAs.
-template <int V, int NF>
+// SC (V = 0 only; the k1-fused forward launch): the panel was written by other workgroups of the same launch and is
+// read with `sc1` 16-B buffer loads (X uniform: one buffer resource; csrc/flock_mem.h)
+template <int V, int NF, bool SC = false>
 __device__ __forceinline__ void panel_fetch(float4 (&v)[NF], const float* __restrict__ X, int R, int Kd, int sr,
                                             int sk, int r0, int k0, int kc) {
     const int tid = threadIdx.x;
     if (V == 0) {
         const int q = kc >> 2, items = 32 * q;
+        __amdgpu_buffer_rsrc_t rsrc;
+        if constexpr (SC) rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
             const int t = tid + 256 * i;
             const int rr = t / q, k = k0 + 4 * (t - rr * q), rw = r0 + rr;
-            v[i] = (t < items && rw < R && k < Kd) ? *reinterpret_cast<const float4*>(X + (int64_t)rw * sr + k)
-                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+            const bool in = t < items && rw < R && k < Kd;
+            if constexpr (SC) {
+                const auto u = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? (rw * sr + k) * 4 : 0, 0, 16);
+                v[i] = in ? __builtin_bit_cast(float4, u) : make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                v[i] = in ? *reinterpret_cast<const float4*>(X + (int64_t)rw * sr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
     } else {
         const int items = 8 * kc;
@@ -909,7 +943,8 @@ __device__ __forceinline__ f32x16 mfma_panel(f32x16 acc, const float* a, const f
 }
 
 // the 4 outputs of thread (wave w, lane l): rows 8w + 4(l >> 5) + q (q < 4), column l & 31
-template <int AV, int BV, int NF, int MK = 0>
+// ASC: the A panels are read `sc1` (panel_fetch SC; the k1-fused forward launch)
+template <int AV, int BV, int NF, int MK = 0, bool ASC = false>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
                                           float (&out)[4]) {
     SC_MARK(MK, 0)
@@ -924,7 +959,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
     if constexpr (AV != 2 && BV != 2) {
         float4 va[NF], vb[NF];
         int kc = gemm_kc(g.K, g.kchunk);
-        panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
+        panel_fetch<AV, NF, ASC>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
         panel_fetch<BV, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, 0, kc);
         for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
             panel_store<AV, NF>(As, va, kc);
@@ -934,7 +969,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
             SC_MARK(MK, (k0 ? 5 : 2))
             const int k1 = k0 + g.kchunk, kc1 = k1 < g.K ? gemm_kc(g.K - k1, g.kchunk) : 0;
             if (k1 < g.K) {  // the next chunk's loads fly during this chunk's MFMAs
-                panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
+                panel_fetch<AV, NF, ASC>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
                 panel_fetch<BV, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k1, kc1);
             }
             const int kq = kc >> 2;  // multiple of 2
@@ -980,8 +1015,10 @@ __device__ __forceinline__ int xcd_tile(int x, int tiles) {
 
 // one forward GEMM tile: block x of problem y computes tile xcd_tile(x). F (fused rounds): the tile is stored
 // write-through and its arrival counted at g.sig[tile row] once every wave's stores have completed (csrc/flock_mem.h)
-template <int AV, int BV, int NF, bool F>
-__device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
+// K1 (the k1-fused forward launch): the tile first waits for the k1 row blocks of its 32 rows (g.wait[tm]) and reads
+// its A panels `sc1`
+template <int AV, int BV, int NF, bool F, bool K1 = false>
+__device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x, unsigned* err = nullptr) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const GemmP& g = gb.p[y];
@@ -992,8 +1029,12 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int n = tn * kT + (l & 31);
     const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
+    if (K1) {
+        const int rows = min(g.M - tm * kT, kT);
+        if (!wait_count(g.wait + tm, (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock), err)) return;
+    }
     float out[4];
-    gemm_tile<AV, BV, NF, 1>(g, g.B + rel, tm, tn, smem, out);
+    gemm_tile<AV, BV, NF, 1, K1>(g, g.B + rel, tm, tn, smem, out);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
@@ -1409,39 +1450,19 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
 // word and the block computes nothing (flock_sc_pipeline_check / flock_sc_workspace_check report it). The counters
 // are zero between launches: the launch's last finishing block resets the ones it used. The math of every block is
 // the unfused kernels' (results bitwise equal: tests/test_gpu_overlap.py).
-__device__ __forceinline__ bool wait_count(const unsigned* ctr, unsigned need, unsigned* err) {
-    __shared__ int ok;
-    if (threadIdx.x == 0) {
-        int good = 1;
-        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
-                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    good = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        ok = good;
-    }
-    __syncthreads();
-    return ok != 0;
-}
 // every block of a fused launch ends here: the last one to finish resets the counters the launch used
 struct SyncReset {
     unsigned* done;
     unsigned total;  // blocks of the launch
-    unsigned* r[2];  // counter ranges to zero
-    int n[2];
+    unsigned* r[4];  // counter ranges to zero
+    int n[4];
 };
 __device__ __forceinline__ void launch_done(const SyncReset& sr) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned prev = __hip_atomic_fetch_add(sr.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (prev == sr.total - 1u) {
-            for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < 4; ++k)
                 for (int i = 0; i < sr.n[k]; ++i) __hip_atomic_store(sr.r[k] + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(sr.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1453,14 +1474,39 @@ struct K3Side {
     int nb;         // k3 blocks of this job (0: absent)
     unsigned need;  // tile arrivals per 32-row tile (paths x column tiles)
 };
-// forward launch: grid (max tiles, problems + k3 rows): y < gb.n GEMM tiles (signalling), then the k3 blocks of the
+// forward launch: grid (max tiles, [k1 rows +] problems + k3 rows): with K1 the first ny1 rows of the grid are the k1
+// row blocks (critic job: 3 paths x rb, actor job: 2 paths x rb; linear index), each signalling its path's 32-row
+// tile; then y - ny1 < gb.n GEMM tiles (waiting for their A rows with K1, signalling), then the k3 blocks of the
 // critic job (kc) and of the actor job (ka), linear index over the trailing rows
-template <int AV, int BV, int NF, int C, int HC, int NAC>
-__global__ __launch_bounds__(256) void sc_fwd(GemmBatch gb, K3Side kc, K3Side ka, SyncReset sr) {
+template <int AV, int BV, int NF, int C, int HC, int NAC, bool K1>
+__global__ __launch_bounds__(256) void sc_fwd(GemmBatch gb, K3Side kc, K3Side ka, SyncReset sr, int ny1) {
     SC_PRIO();
-    const int y = blockIdx.y;
-    if (y < gb.n) {
-        gemm_block<AV, BV, NF, true>(gb, y, blockIdx.x);
+    const int y = (int)blockIdx.y - (K1 ? ny1 : 0);
+    if (K1 && y < 0) {
+        const int kb = (int)blockIdx.y * (int)gridDim.x + (int)blockIdx.x;
+        const int rb = (kc.nb > 0 ? kc : ka).nb;  // row blocks per path (the jobs share B)
+        const int nc = kc.nb > 0 ? 3 * rb : 0, na = ka.nb > 0 ? 2 * rb : 0;
+        if (kb < nc + na) {
+            const bool crit = kb < nc;
+            const K3Side& j = crit ? kc : ka;
+            const int path = (crit ? kb : kb - nc) / rb, bx = (crit ? kb : kb - nc) - path * rb;
+            if (crit) {
+                if (j.a.gate && !gate_wait(j.a.gate, j.a.gate_seq)) {  // this learn's snapshot
+                    launch_done(sr);
+                    return;
+                }
+                c1_body<7, 400, true>(j.w, j.a, bx, path);
+            } else {
+                a1_body<7, 400, true>(j.w, j.a, bx, path);
+            }
+            flock_mem::wait_vmem();
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_fetch_add(j.w.SYNC + kSyncK1 + 16 * path + (bx * kRowsPerBlock) / kT, 1u,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (y < gb.n) {
+        gemm_block<AV, BV, NF, true, K1>(gb, y, blockIdx.x, kc.w.SYNC + kSyncErr);
     } else {
         const int kb = (y - gb.n) * (int)gridDim.x + (int)blockIdx.x;
         if (kb < kc.nb) {
@@ -1540,6 +1586,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
     g.kchunk = balanced_kc(K, fwd_kc());
     g.sig = nullptr;
+    g.wait = nullptr;
     return g;
 }
 
@@ -1963,13 +2010,17 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
 // FLOCK_SC_FUSE=0 (read once) or flock_set_diag("sc_no_fuse", 1): the five-launch rounds everywhere (A/B and the
 // bitwise tests of the fused rounds)
 bool g_sc_no_fuse = false;
-bool fuse_rounds() {
-    static const bool on = [] {
+int g_sc_fuse_k1 = -1;  // flock_set_diag("sc_fuse_k1", 0 / 1); -1: FLOCK_SC_FUSE
+int fuse_env() {
+    static const int v = [] {
         const char* e = getenv("FLOCK_SC_FUSE");
-        return !(e && e[0] == '0');
+        return e ? atoi(e) : 1;
     }();
-    return on && !g_sc_no_fuse;
+    return v;
 }
+bool fuse_rounds() { return fuse_env() != 0 && !g_sc_no_fuse; }
+// FLOCK_SC_FUSE=2: the k1 row blocks join the forward launch too (two launches per round)
+bool fuse_k1() { return g_sc_fuse_k1 >= 0 ? g_sc_fuse_k1 != 0 : fuse_env() == 2; }
 
 // The fused three-launch round (see sc_fwd / sc_bwdg) where its instantiation covers the shapes: the reference's
 // widths (fc1 400, fc2 300, 2 actions: the specialised row kernels), the forward GEMMs on the (k-contiguous,
@@ -2010,26 +2061,41 @@ int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja) {
     if (nf_of(kh) != 7 || nf_of(kw) != 4) return 1;
     if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks || A.bw.nblk > kMaxRedBlocks) return 1;
     int rc = 0;
-    const int C = A.C, rb = A.rb, tile_rows = (A.B + kT - 1) / kT;
-    {  // 1: fc1 rows (the unfused row launch)
+    const int rb = A.rb, tile_rows = (A.B + kT - 1) / kT;
+    const bool k1f = fuse_k1();
+    if (!k1f) {  // 1: fc1 rows (the unfused row launch)
         const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
         const size_t lds = zmax(A.lds1, Z.lds1);
         const dim3 grid(rb, npc + npa);
-        (void)C;
         if ((rc = allow_lds(sc_k1<7, 400>, lds))) return rc;
         hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a);
         if ((rc = launched())) return rc;
     }
-    {  // 2: forward GEMM tiles + the k3 rows
+    {  // 2: [fc1 rows +] forward GEMM tiles + the k3 rows
         K3Side kcs{jc ? jc->w : A.w, jc ? jc->a : A.a, jc ? rb : 0, (unsigned)(3 * gb.p[0].tiles_n)};
         K3Side kas{ja ? ja->w : A.w, ja ? ja->a : A.a, ja ? rb : 0, (unsigned)(2 * gb.p[0].tiles_n)};
-        const int nk3 = kcs.nb + kas.nb;
-        const dim3 grid(tiles, gb.n + (nk3 + tiles - 1) / tiles);
-        const size_t lds = zmax(gemm_lds_bytes(kc, kc), zmax(A.lds3, Z.lds3));
-        SyncReset sr{A.w.SYNC + kSyncDone, grid.x * grid.y, {jc ? jc->w.SYNC : nullptr, ja ? ja->w.SYNC : nullptr},
-                     {jc ? tile_rows : 0, ja ? tile_rows : 0}};
-        if ((rc = allow_lds(sc_fwd<0, 0, 7, 5, 300, 2>, lds))) return rc;
-        hipLaunchKernelGGL((sc_fwd<0, 0, 7, 5, 300, 2>), grid, dim3(256), lds, st, gb, kcs, kas, sr);
+        if (k1f)  // each problem's A rows come from one k1 path of its job: critic 0, 1, 2 then actor 0, 1
+            for (int i = 0; i < gb.n; ++i) {
+                const bool crit = jc && i < jc->nfwd;
+                const int path = crit ? i : i - (jc ? jc->nfwd : 0);
+                gb.p[i].wait = (crit ? jc->w.SYNC : ja->w.SYNC) + kSyncK1 + 16 * path;
+            }
+        const int nk3 = kcs.nb + kas.nb, nk1 = k1f ? (jc ? 3 * rb : 0) + (ja ? 2 * rb : 0) : 0;
+        const int ny1 = (nk1 + tiles - 1) / tiles;
+        const dim3 grid(tiles, ny1 + gb.n + (nk3 + tiles - 1) / tiles);
+        size_t lds = zmax(gemm_lds_bytes(kc, kc), zmax(A.lds3, Z.lds3));
+        if (k1f) lds = zmax(lds, zmax(A.lds1, Z.lds1));
+        SyncReset sr{A.w.SYNC + kSyncDone, grid.x * grid.y,
+                     {jc ? jc->w.SYNC : nullptr, ja ? ja->w.SYNC : nullptr,
+                      jc ? jc->w.SYNC + kSyncK1 : nullptr, ja ? ja->w.SYNC + kSyncK1 : nullptr},
+                     {jc ? tile_rows : 0, ja ? tile_rows : 0, jc && k1f ? 16 * 3 : 0, ja && k1f ? 16 * 2 : 0}};
+        if (k1f) {
+            if ((rc = allow_lds(sc_fwd<0, 0, 7, 5, 300, 2, true>, lds))) return rc;
+            hipLaunchKernelGGL((sc_fwd<0, 0, 7, 5, 300, 2, true>), grid, dim3(256), lds, st, gb, kcs, kas, sr, ny1);
+        } else {
+            if ((rc = allow_lds(sc_fwd<0, 0, 7, 5, 300, 2, false>, lds))) return rc;
+            hipLaunchKernelGGL((sc_fwd<0, 0, 7, 5, 300, 2, false>), grid, dim3(256), lds, st, gb, kcs, kas, sr, 0);
+        }
         if ((rc = launched())) return rc;
     }
     // 3: bwd blocks + gradient / Adam blocks
@@ -2045,7 +2111,8 @@ int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja) {
                {bb.nb0, both ? bwd_blocks(Z.bw) : 0}};
     const int nb = bs.nbw[0] + bs.nbw[1] + gg.nb0 + (both ? late_blocks(Z.ga) : 0);
     const size_t lds = zmax(zmax(bwd_lds(A.bw), bwd_lds(Z.bw)), red_lds(A.B));
-    SyncReset sr{A.w.SYNC + kSyncDone, (unsigned)nb, {A.w.SYNC + kSyncBwd, Z.w.SYNC + kSyncBwd}, {1, both ? 1 : 0}};
+    SyncReset sr{A.w.SYNC + kSyncDone, (unsigned)nb, {A.w.SYNC + kSyncBwd, Z.w.SYNC + kSyncBwd, nullptr, nullptr},
+                 {1, both ? 1 : 0, 0, 0}};
     if ((rc = allow_lds(sc_bwdg<0, 1, 1, 1, 7, 4>, lds))) return rc;
     hipLaunchKernelGGL((sc_bwdg<0, 1, 1, 1, 7, 4>), dim3(nb), dim3(256), lds, st, bb, gg, bs, sr);
     return launched();
@@ -2150,6 +2217,7 @@ __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows
 // the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
 void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
 void flock_sc_diag_no_fuse(bool v) { g_sc_no_fuse = v; }
+void flock_sc_diag_fuse_k1(int v) { g_sc_fuse_k1 = v; }
 
 extern "C" {
 

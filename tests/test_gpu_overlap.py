@@ -197,7 +197,8 @@ def test_device_gate_and_fused_rounds_are_bitwise_the_plain_pipeline(n_slots, cu
     """The device-side snapshot gate (the critic row blocks poll a sequence number the `sc1` snapshot publishes;
     FLOCK_SC_GATE=0: the cross-queue event wait) and the fused three-launch rounds (forward GEMM tiles + k3 rows in one
     launch, bwd + gradient / Adam blocks in one launch, hand-offs through workspace counters; flock_set_diag
-    "sc_no_fuse": five launches), in all four combinations: the overlapped config-3 loop at the reference widths with
+    "sc_no_fuse": five launches; "sc_fuse_k1": the fc1 rows in the forward launch too, two launches), in all six
+    combinations: the overlapped config-3 loop at the reference widths with
     env kernels co-running on the env stream (uneven load, L1-warm consumers) ends with every learner tensor bitwise
     equal, and no wait gave up."""
     from marl_range_flocking_amd import FlockConfig, VecFlockEnv, _native
@@ -209,9 +210,10 @@ def test_device_gate_and_fused_rounds_are_bitwise_the_plain_pipeline(n_slots, cu
     pool = [torch.stack([torch.rand(E, Na, device=cuda, generator=g),
                          torch.rand(E, Na, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
     out = []
-    for gate, fuse in (("0", 0), ("1", 0), ("0", 1), ("1", 1)):
+    for gate, fuse in (("0", 0), ("1", 0), ("0", 1), ("1", 1), ("0", 2), ("1", 2)):
         os.environ["FLOCK_SC_GATE"] = gate
-        assert lib.flock_set_diag(b"sc_no_fuse", 1 - fuse) == 0
+        assert lib.flock_set_diag(b"sc_no_fuse", int(fuse == 0)) == 0
+        assert lib.flock_set_diag(b"sc_fuse_k1", int(fuse == 2)) == 0
         try:
             env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
                                           range_start=(0, 253.0), sensor_range=14.0, step_launches=3), device=cuda)
@@ -232,14 +234,15 @@ def test_device_gate_and_fused_rounds_are_bitwise_the_plain_pipeline(n_slots, cu
         finally:
             os.environ.pop("FLOCK_SC_GATE", None)
             lib.flock_set_diag(b"sc_no_fuse", 0)
+            lib.flock_set_diag(b"sc_fuse_k1", -1)
     for mode in out[1:]:
         for i, (x, y) in enumerate(zip(out[0], mode)):
             assert torch.equal(x, y), i
 
 
 def test_fused_rounds_bitwise_serial_learns(cuda):
-    """The fused rounds through the plain learn() path (one critic-only and one actor-only round per learn, the
-    reference widths, B = 256) against the five-launch rounds: bitwise equal after a sequence with a repeated agent;
+    """The fused rounds (three launches; two with the fc1 rows fused too) through the plain learn() path (one
+    critic-only and one actor-only round per learn, the reference widths, B = 256) against the five-launch rounds: bitwise equal after a sequence with a repeated agent;
     the workspace error word stays clear."""
     from marl_range_flocking_amd import _native
     from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
@@ -251,8 +254,9 @@ def test_fused_rounds_bitwise_serial_learns(cuda):
             torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, d, device=cuda, generator=g) * 14,
             torch.rand(n, device=cuda, generator=g) > 0.9)
     out = []
-    for fuse in (0, 1):
-        assert lib.flock_set_diag(b"sc_no_fuse", 1 - fuse) == 0
+    for fuse in (0, 1, 2):
+        assert lib.flock_set_diag(b"sc_no_fuse", int(fuse == 0)) == 0
+        assert lib.flock_set_diag(b"sc_fuse_k1", int(fuse == 2)) == 0
         try:
             L = SharedCriticLearner(5, d, device=cuda, seed=3, batch_size=256, buffer_size=3000, use_graph=False)
             L.store_transitions(*rows)
@@ -262,10 +266,12 @@ def test_fused_rounds_bitwise_serial_learns(cuda):
             L.pipeline_check()
         finally:
             lib.flock_set_diag(b"sc_no_fuse", 0)
+            lib.flock_set_diag(b"sc_fuse_k1", -1)
         out.append(L)
-    a, b = out
-    for x, y in ((a.critic.data, b.critic.data), (a.critic.exp_avg_sq, b.critic.exp_avg_sq),
-                 (a.actors.data, b.actors.data), (a.actors.target, b.actors.target), (a.losses, b.losses),
-                 (a.actor_steps, b.actor_steps)):
-        assert torch.equal(x, y)
+    a = out[0]
+    for b in out[1:]:
+        for x, y in ((a.critic.data, b.critic.data), (a.critic.exp_avg_sq, b.critic.exp_avg_sq),
+                     (a.actors.data, b.actors.data), (a.actors.target, b.actors.target), (a.losses, b.losses),
+                     (a.actor_steps, b.actor_steps)):
+            assert torch.equal(x, y)
     assert torch.isfinite(a.critic.data).all() and a.losses.abs().sum() > 0
