@@ -132,13 +132,14 @@ class SuperAgent:
 
     def save(self):
         os.makedirs(self.save_dir, exist_ok=True)
-        for i in range(self.n_agents):  # agent-sharded learners: each rank writes the networks it owns
+        for i in range(self.n_agents):  # one writer per file: the owner of a sharded network, one rank otherwise
             for net in ("actor", "critic"):
                 for target in (False, True):
-                    if self.learner.owns(net, i, target):
+                    if self.learner.writes(net, i, target):
                         torch.save(self.learner.state_dict(net, i, target=target),
                                    self._ckpt(i, ("target_" if target else "") + net))
-        self.replay_buffer.save(f"{self.path_save}/save_agent_{time.strftime('%Y%m%d%H%M')}")
+        # the replay ring is rank-local (each rank's envs): one file per rank
+        self.replay_buffer.save(f"{self.path_save}/save_agent_{time.strftime('%Y%m%d%H%M')}{self.learner.rank_suffix()}")
 
     def load(self):
         sds = {}

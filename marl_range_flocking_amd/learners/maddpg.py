@@ -546,6 +546,21 @@ class MADDPGLearner:
             return True
         return self.a0 <= i < self.a0 + self.na
 
+    def writes(self, net, i, target=False):
+        """Whether this rank writes agent i's checkpoint file (one writer per file into a shared save_dir): the owner
+        of a sharded network; for networks held whole on every rank (the frozen actors under agent_shard, everything
+        of data-parallel replicas) rank i % world, or rank 0 for replicas."""
+        if not self.distributed:
+            return True
+        W, r = torch.distributed.get_world_size(self.group), torch.distributed.get_rank(self.group)
+        if self.shard and not (net == "actor" and not target):
+            return self.owns(net, i, target)
+        return r == (i % W if self.shard else 0)
+
+    def rank_suffix(self):
+        """'' on one process; '_rank<r>' for rank-local state (each rank's replay ring holds its own envs)."""
+        return f"_rank{torch.distributed.get_rank(self.group)}" if self.distributed else ""
+
     def state_dict(self, net, i, target=False):
         """Reference state_dict of agent i's actor / critic (agent_shard: only the networks this rank owns)."""
         fp = self.actors if net == "actor" else self.critics

@@ -297,9 +297,13 @@ def _shard_worker(rank, port, q, layout):
             except KeyError:
                 pass
         L.state_dict("actor", other)  # the frozen actors are whole on every rank
+        # checkpoint writers (SuperAgent.save): exactly one rank writes each file
+        writes = {(net, i, tg) for net in ("actor", "critic") for i in range(NS) for tg in (False, True)
+                  if L.writes(net, i, tg)}
+        assert all(L.owns(net, i, tg) for net, i, tg in writes)
         q.put((rank, _layers(L.critics, L.critics.data, 0, L.na), _layers(L.critics, L.critics.target, 0, L.na),
                _layers(A, A.target, L.a0, L.a0 + L.na), _layers(A, A.data, 0, NS), L.losses.cpu().numpy(),
-               L.state_dict("critic", L.a0)["fc2.weight"].numpy()))
+               L.state_dict("critic", L.a0)["fc2.weight"].numpy(), writes))
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
     except Exception as e:  # noqa: BLE001
@@ -336,7 +340,9 @@ def test_agent_sharded_critics_equal_union_batch(layout, cuda):
     for s2 in (st, st[::-1].copy()):
         ref.train(starts=s2)
     h = NS // 2
-    for rank, crit, ctgt, atgt, actors, losses, fc2 in out:
+    w0, w1 = out[0][7], out[1][7]
+    assert not (w0 & w1) and len(w0 | w1) == 2 * 2 * NS  # every (net, agent, target) file has exactly one writer
+    for rank, crit, ctgt, atgt, actors, losses, fc2, _ in out:
         lo, hi = rank * h, (rank + 1) * h
         for got, want in ((crit, _layers(ref.critics, ref.critics.data, lo, hi)),
                           (ctgt, _layers(ref.critics, ref.critics.target, lo, hi)),
