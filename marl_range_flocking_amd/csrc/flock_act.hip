@@ -36,7 +36,8 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kTM = 64;  // env rows per block (two 32-row bands)
+// env rows per block: TM = 64 (two 32-row bands, 4 waves) or 128 (four bands, 8 waves: every fc2.weight chunk staged in
+// LDS is read by twice the rows, so the L2 -> LDS traffic per FLOP halves); FLOCK_ACT_TM picks it (default 128)
 #ifndef FLOCK_ACT_KC
 #define FLOCK_ACT_KC 40
 #endif
@@ -73,15 +74,16 @@ __device__ __forceinline__ float sum32(float v) {
 
 // NT: 32-column tiles per wave (each wave covers half of the padded fc2 width: fc2 <= 64 NT); INC: compile-time
 // observation width (0: runtime, <= 16)
-template <int NT, int INC, bool STG>
-__global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
+template <int NT, int INC, bool STG, int TM>
+__global__ __launch_bounds__(4 * TM, 2) void sc_act_kernel(ActArgs p) {
+    constexpr int NTH = 4 * TM;  // threads: 2 waves per 32-row band (the two column halves)
     extern __shared__ float4 smem4[];
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
     const int IN = INC ? INC : p.in, INP = (IN + 3) & ~3, H1 = p.H1, H2 = p.H2;
     const int W = p.A * p.tiles, b = blockIdx.x;
     const int work = (W & 7) == 0 ? (b & 7) * (W >> 3) + (b >> 3) : b;
     const int agent = work / p.tiles, tile = work - agent * p.tiles;
-    const int64_t r0 = (int64_t)tile * kTM;
+    const int64_t r0 = (int64_t)tile * TM;
     const float* P = p.actors + (int64_t)agent * p.stride;
     const float* W1 = P;
     const float* B1 = W1 + (int64_t)H1 * IN;
@@ -98,17 +100,17 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
     float* sW1 = reinterpret_cast<float*>(smem4);
     float4* sQ = reinterpret_cast<float4*>(sW1 + H1 * INP);
     float* sX = reinterpret_cast<float*>(sQ + H1);
-    float* sMean = sX + kTM * INP;
-    float* sRstd = sMean + kTM;
-    float* sRed = sRstd + kTM;      // [64][2]
-    float* sMu = sRed + 2 * kTM;    // [64][2 halves][2]
+    float* sMean = sX + TM * INP;
+    float* sRstd = sMean + TM;
+    float* sRed = sRstd + TM;      // [64][2]
+    float* sMu = sRed + 2 * TM;    // [64][2 halves][2]
 
-    for (int e = tid; e < H1 * INP; e += 256) {
+    for (int e = tid; e < H1 * INP; e += NTH) {
         const int k = e / INP, i = e - k * INP;
         sW1[e] = i < IN ? W1[k * IN + i] : 0.0f;
     }
-    for (int k = tid; k < H1; k += 256) sQ[k] = make_float4(B1[k], G1[k], BE1[k], 0.0f);
-    for (int e = tid; e < kTM * INP; e += 256) {
+    for (int k = tid; k < H1; k += NTH) sQ[k] = make_float4(B1[k], G1[k], BE1[k], 0.0f);
+    for (int e = tid; e < TM * INP; e += NTH) {
         const int r = e / INP, i = e - r * INP;
         const int64_t gr = r0 + r;
         sX[e] = (i < IN && gr < p.rows) ? p.obs[(gr * p.A + agent) * IN + i] : 0.0f;
@@ -134,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
 #define FLOCK_ACT_DIAG 0  // timing-only builds (results wrong): 1 no LN1 statistics, 2 no epilogue, 4 no B fetch
 #endif
     if (FLOCK_ACT_DIAG & 1) {
-        if (tid < kTM) {
+        if (tid < TM) {
             sMean[tid] = 0.0f;
             sRstd[tid] = 1.0f;
         }
@@ -223,15 +225,15 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
         }
     } else {  // B staged through LDS: kKC-deep chunks of every column, coalesced 128-B row segments, next chunk in
               // registers during this chunk's MFMAs
-        float* sB = sMu + 4 * kTM;  // [64 NT][kKC + 4]
-        constexpr int kPer = (64 * NT * kKC / 4 + 255) / 256;  // float4 per thread per chunk
+        float* sB = sMu + 4 * TM;  // [64 NT][kKC + 4]
+        constexpr int kPer = (64 * NT * kKC / 4 + NTH - 1) / NTH;  // float4 per thread per chunk
         const int ncol = 64 * NT;
         float4 pf[kPer];
         auto fetch = [&](int k0) {
             if (FLOCK_ACT_DIAG & 4) return;
 #pragma unroll
             for (int i = 0; i < kPer; ++i) {
-                const int f = tid + 256 * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+                const int f = tid + NTH * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
                 pf[i] = (col < H2 && k0 + kq < H1)
                             ? *reinterpret_cast<const float4*>(W2 + (int64_t)col * H1 + k0 + kq)
                             : make_float4(0, 0, 0, 0);
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
             __syncthreads();  // the previous chunk's fragments have been read
 #pragma unroll
             for (int i = 0; i < kPer; ++i) {
-                const int f = tid + 256 * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+                const int f = tid + NTH * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
                 if (col < ncol) *reinterpret_cast<float4*>(sB + col * (kKC + 4) + kq) = pf[i];
             }
             __syncthreads();
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int v = 0; v < 16; ++v) sum += acc[t][v];
-        if (tid < 2 * kTM && r0 + (tid >> 1) < p.rows) p.actions[((r0 + (tid >> 1)) * p.A + agent) * 2 + (tid & 1)] = sum;
+        if (tid < 2 * TM && r0 + (tid >> 1) < p.rows) p.actions[((r0 + (tid >> 1)) * p.A + agent) * 2 + (tid & 1)] = sum;
         return;
     }
     // epilogue. acc[t][v] of lane l: row 8 (v >> 2) + 4 (l >> 5) + (v & 3) of the band, column 32 (NT half + t) +
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
     __syncthreads();
     // the LayerNorm-2 statistics once per row (64 threads), not per lane and accumulator row
     float* sStat = sMean;  // [64] mean, then [64] rstd in sRstd (LayerNorm-1's are no longer read)
-    if (tid < kTM) sStat[tid] = (sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2;
+    if (tid < TM) sStat[tid] = (sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2;
     __syncthreads();
     float mean[16];
 #pragma unroll
@@ -325,7 +327,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
     __syncthreads();
-    if (tid < kTM) sRstd[tid] = 1.0f / sqrtf((sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2 + 1e-5f);
+    if (tid < TM) sRstd[tid] = 1.0f / sqrtf((sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2 + 1e-5f);
     __syncthreads();
     float m0[16], m1[16];
 #pragma unroll
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
             sMu[(r * 2 + half) * 2 + 1] = m1[v];
         }
     __syncthreads();
-    if (tid < 2 * kTM) {
+    if (tid < 2 * TM) {
         const int r = tid >> 1, j = tid & 1;
         const int64_t gr = r0 + r;
         if (gr < p.rows) {
@@ -368,15 +370,23 @@ __global__ __launch_bounds__(256, 2) void sc_act_kernel(ActArgs p) {
     }
 }
 
-template <int NT, int INC>
+template <int NT, int INC, int TM>
 int launch_act(hipStream_t st, const ActArgs& a, size_t lds, bool stage) {
     if (stage && lds + sizeof(float) * 64 * NT * (kKC + 4) <= 64 * 1024) {
         lds += sizeof(float) * 64 * NT * (kKC + 4);
-        hipLaunchKernelGGL((sc_act_kernel<NT, INC, true>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
+        hipLaunchKernelGGL((sc_act_kernel<NT, INC, true, TM>), dim3(a.A * a.tiles), dim3(4 * TM), lds, st, a);
     } else {
-        hipLaunchKernelGGL((sc_act_kernel<NT, INC, false>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
+        hipLaunchKernelGGL((sc_act_kernel<NT, INC, false, TM>), dim3(a.A * a.tiles), dim3(4 * TM), lds, st, a);
     }
     return launched();
+}
+
+template <int NT, int INC>
+int launch_act_tm(hipStream_t st, ActArgs a, int inp, bool stage, int tm) {
+    a.tiles = (int)((a.rows + tm - 1) / tm);
+    const size_t lds = sizeof(float) * ((size_t)a.H1 * inp + 4 * (size_t)a.H1 + (size_t)tm * inp + 8 * (size_t)tm);
+    if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
+    return tm == 128 ? launch_act<NT, INC, 128>(st, a, lds, stage) : launch_act<NT, INC, 64>(st, a, lds, stage);
 }
 
 }  // namespace
@@ -393,8 +403,11 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
     const int64_t per = (int64_t)fc1 * (in_dim + 3) + (int64_t)fc2 * (fc1 + 5) + 2;
     if (actor_stride < per) return fail(-5, "flock_sc_act: actor_stride smaller than one actor");
     if (rows == 0) return 0;
-    const int64_t tiles = (rows + kTM - 1) / kTM;
-    if (tiles * n_agents > 0x7fffffff) return fail(-5, "flock_sc_act: too many rows x agents");
+    static const int tm = [] {  // FLOCK_ACT_TM=64 / 128: env rows per block (A/B)
+        const char* e = getenv("FLOCK_ACT_TM");
+        return e && atoi(e) == 64 ? 64 : 128;
+    }();
+    if ((rows + 63) / 64 * n_agents > 0x7fffffff) return fail(-5, "flock_sc_act: too many rows x agents");
     ActArgs a;
     a.obs = obs;
     a.actors = actors;
@@ -407,13 +420,11 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
     a.in = in_dim;
     a.H1 = fc1;
     a.H2 = fc2;
-    a.tiles = (int)tiles;
+    a.tiles = 0;
     a.theta = theta;
     a.dt = dt;
     a.c = sigma_sqrt_dt;
     const int inp = (in_dim + 3) & ~3;
-    const size_t lds = sizeof(float) * ((size_t)fc1 * inp + 4 * (size_t)fc1 + kTM * inp + 2 * kTM + 2 * kTM + 4 * kTM);
-    if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
     hipStream_t st = (hipStream_t)stream;
     const int nt = (fc2 + 63) / 64;
     static const bool stage = [] {  // FLOCK_ACT_STAGE=0/1: fc2.weight straight from global memory / through LDS (A/B)
@@ -422,18 +433,18 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
     }();
     if (in_dim == 4) {
         switch (nt) {
-            case 1: return launch_act<1, 4>(st, a, lds, stage);
-            case 2: return launch_act<2, 4>(st, a, lds, stage);
-            case 3: return launch_act<3, 4>(st, a, lds, stage);
-            case 4: return launch_act<4, 4>(st, a, lds, stage);
-            default: return launch_act<5, 4>(st, a, lds, stage);
+            case 1: return launch_act_tm<1, 4>(st, a, inp, stage, tm);
+            case 2: return launch_act_tm<2, 4>(st, a, inp, stage, tm);
+            case 3: return launch_act_tm<3, 4>(st, a, inp, stage, tm);
+            case 4: return launch_act_tm<4, 4>(st, a, inp, stage, tm);
+            default: return launch_act_tm<5, 4>(st, a, inp, stage, tm);
         }
     }
     switch (nt) {
-        case 1: return launch_act<1, 0>(st, a, lds, stage);
-        case 2: return launch_act<2, 0>(st, a, lds, stage);
-        case 3: return launch_act<3, 0>(st, a, lds, stage);
-        case 4: return launch_act<4, 0>(st, a, lds, stage);
-        default: return launch_act<5, 0>(st, a, lds, stage);
+        case 1: return launch_act_tm<1, 0>(st, a, inp, stage, tm);
+        case 2: return launch_act_tm<2, 0>(st, a, inp, stage, tm);
+        case 3: return launch_act_tm<3, 0>(st, a, inp, stage, tm);
+        case 4: return launch_act_tm<4, 0>(st, a, inp, stage, tm);
+        default: return launch_act_tm<5, 0>(st, a, inp, stage, tm);
     }
 }

@@ -37,6 +37,14 @@ if [ -n "${TIMELINES:-}" ]; then
     python3 tools/trace_timeline.py "$f" > $d/timeline.txt 2>&1; tail -12 $d/timeline.txt
   done
 fi
+if [ "${ACT:-0}" = "1" ]; then  # the acting kernel: 64 vs 128 env rows per block, interleaved
+  for r in 1 2; do
+    for tm in 64 128; do
+      step act_${tm}_$r.txt 200 env FLOCK_ACT_TM=$tm python3 tools/act_bench.py
+      echo "TM=$tm r$r: $(tail -1 $OUT/act_${tm}_$r.txt)"
+    done
+  done
+fi
 if [ "${DRIVER:-0}" = "1" ]; then
   step driver_1.json 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
   step driver_2.json 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
