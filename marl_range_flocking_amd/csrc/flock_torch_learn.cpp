@@ -815,6 +815,10 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
     m.def(
         "sc_prep_snapshot(Tensor[] ring, Tensor(a!)[] staging, Tensor(b!) agent_out, Tensor(c!)? idx_out, int rows, "
         "int seed, int counter, int agent) -> ()");
+    // sc_round / sc_round_adam mark every tensor of each list mutable (read-only replay rows and staging included)
+    // and give each list one alias set; the data-parallel bucket is viewed from two lists (learner[1] and job[9]).
+    // They are eager / HIP-graph ops: not for functionalization or torch.compile (which would need exact per-tensor
+    // write sets and one alias annotation for the shared bucket).
     m.def(
         "sc_round(Tensor(a!)[] learner, Tensor(b!)[] critic_job, Tensor(c!)[] actor_job, int[] dims, "
         "float[] hyper) -> ()");

@@ -274,6 +274,10 @@ class _LinearTInto(torch.autograd.Function):
 def _linear_t(x, W, b):
     A, out, n_in = W.shape
     W2 = W.reshape(A * out, n_in)
+    if torch.is_grad_enabled() and (x.requires_grad or W.requires_grad or (b is not None and b.requires_grad)):
+        # under autograd without gradient views: the functional forms (out= ops are not differentiable)
+        y = W2 @ x.t() if b is None else torch.addmm(b.reshape(A * out, 1), W2, x.t())
+        return y.view(A, out, x.shape[0])
     y = torch.empty((A, out, x.shape[0]), dtype=x.dtype, device=x.device)  # a base tensor (in-place safe)
     if b is None:
         torch.mm(W2, x.t(), out=y.view(A * out, -1))
