@@ -409,7 +409,8 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
         for (int o = 0; o < kMaxAct; ++o) act[o] = o < na ? ld_in<F>(w.A + (int64_t)r * na + o) : 0.0f;
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
-    stage(at, a.actors_target + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    // F: the agent index as the snapshot wrote it (the k1-fused launch may have started before the snapshot ran)
+    stage(at, a.actors_target + (F ? flock_mem::ld_sc1(a.agent) : *a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
     if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
@@ -1025,14 +1026,15 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x, un
     if (x >= g.tiles) return;
     const int t = xcd_tile(x, g.tiles);
     const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    const int64_t rel = g.relB ? g.relB * (*g.agent) : 0;
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int n = tn * kT + (l & 31);
-    const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
-    if (K1) {
+    if (K1) {  // first the k1 rows of this tile: they follow the snapshot (gate), which also wrote *g.agent
         const int rows = min(g.M - tm * kT, kT);
         if (!wait_count(g.wait + tm, (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock), err)) return;
     }
+    // K1: this launch may have started before the snapshot wrote the agent index: read it `sc1` after the wait
+    const int64_t rel = g.relB ? g.relB * (K1 ? flock_mem::ld_sc1(g.agent) : *g.agent) : 0;
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int n = tn * kT + (l & 31);
+    const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
     float out[4];
     gemm_tile<AV, BV, NF, 1, K1>(g, g.B + rel, tm, tn, smem, out);
 #pragma unroll
