@@ -233,12 +233,14 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p);
  * the first flock_sc_pipeline_learn. */
 /* The device-side snapshot gate (single GPU, the default; FLOCK_SC_GATE=0 or rocprofv3 counter collection, which
  * serialises dispatches: cross-queue event waits instead): the snapshot kernel writes the staging rows `sc1` and
- * publishes a sequence number after all its stores completed, and the round's critic row blocks poll it (bounded,
- * 0.2 s) instead of the learner stream waiting for an event. A waiter that gives up sets an error word and computes
+ * publishes a sequence number after all its stores completed, and the learner stream waits for it on the device
+ * instead of for an event: FLOCK_SC_GATE=2 (default) one wave launched before the round polls it (bounded, 0.2 s),
+ * FLOCK_SC_GATE=1 the round's critic row blocks poll it. A waiter that gives up sets an error word and computes
  * nothing; flock_sc_pipeline_check (synchronous: call after synchronising the learner stream) returns -6 then.
- * flock_sc_pipeline_gated: 1 when the gate is in use. */
+ * flock_sc_pipeline_gated: the gate mode in use (0 = event waits). */
 int flock_sc_pipeline_check(FlockScPipeline* p);
-/* The fused three-launch rounds (the reference widths; FLOCK_SC_FUSE=0 keeps five launches) hand rows between the
+/* The fused rounds (the reference widths; FLOCK_SC_FUSE=1: three launches, 2: two; default 0, five launches: the
+ * fused launches measured slower beside the env kernels, whose slots their waiting blocks hold) hand rows between the
  * workgroups of one launch through counters in the update's workspace; a wait that gives up (bounded, 0.2 s) sets an
  * error word there. Synchronous check of it (flock_sc_pipeline_check checks every slot's workspace too): -6. */
 int flock_sc_workspace_check(const FlockScUpdate* u);

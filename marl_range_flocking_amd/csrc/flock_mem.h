@@ -48,12 +48,6 @@ __device__ __forceinline__ float2 ld_sc1_f2(const float2* p) {
     return __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT));
 }
-// 16-B `sc1` load
-__device__ __forceinline__ float4 ld_sc1_x4(const float4* p) {
-    float4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
 
 // every vector-memory operation of this wave has completed (stores acknowledged): the producer side of a hand-off
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }

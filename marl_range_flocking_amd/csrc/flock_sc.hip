@@ -410,7 +410,7 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
     // F: the agent index as the snapshot wrote it (the k1-fused launch may have started before the snapshot ran)
-    stage(at, a.actors_target + (F ? flock_mem::ld_sc1(a.agent) : *a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    stage(at, a.actors_target + flock_mem::ld_sc1(a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
     if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
@@ -510,7 +510,7 @@ __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, i
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = bx * kRowsPerBlock + wv;
     const bool live = r < a.B;
-    const float* net = path == 0 ? a.actors + (*a.agent) * a.stride : a.critic;
+    const float* net = path == 0 ? a.actors + flock_mem::ld_sc1(a.agent) * a.stride : a.critic;
     if (live && lane < a.in) xs[wv * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
     stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
@@ -547,7 +547,7 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
         load_row<C, F>(zc2, w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
-    stage(at, a.actors + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    stage(at, a.actors + flock_mem::ld_sc1(a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
     if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
@@ -1031,7 +1031,7 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x, un
         if (!wait_count(g.wait + tm, (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock), err)) return;
     }
     // K1: this launch may have started before the snapshot wrote the agent index: read it `sc1` after the wait
-    const int64_t rel = g.relB ? g.relB * (K1 ? flock_mem::ld_sc1(g.agent) : *g.agent) : 0;
+    const int64_t rel = g.relB ? g.relB * flock_mem::ld_sc1(g.agent) : 0;
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int n = tn * kT + (l & 31);
     const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
@@ -1193,12 +1193,12 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-    const int64_t base = j.rel ? j.rel * (*j.agent) : 0;
-    const int64_t gbase = j.grad_rel ? j.grad_rel * (*j.agent) : 0;
+    const int64_t base = j.rel ? j.rel * flock_mem::ld_sc1(j.agent) : 0;
+    const int64_t gbase = j.grad_rel ? j.grad_rel * flock_mem::ld_sc1(j.agent) : 0;
     if (bx < j.dh.tiles) {
         const GemmP& g = j.dh;
         const int tm = bx / g.tiles_n, tn = bx - tm * g.tiles_n;
-        const int64_t relB = g.relB ? g.relB * (*g.agent) : 0;
+        const int64_t relB = g.relB ? g.relB * flock_mem::ld_sc1(g.agent) : 0;
         const int n = tn * kT + (l & 31);
         const bool nok = n < g.N;
         // the epilogue's inputs, loaded before the GEMM
@@ -1355,11 +1355,11 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
     __shared__ float sh[2];
     __shared__ int sh_soft;
     const int tid = threadIdx.x;
-    const int64_t agent = ga.rel ? *ga.agent : 0;
+    const int64_t agent = ga.rel ? flock_mem::ld_sc1(ga.agent) : 0;
     const int64_t base = ga.rel * agent, gbase = ga.grad_rel * agent;
     if (tid == 0) {
         const int64_t step0 = ga.do_adam ? ga.step[agent] : 0;
-        const int64_t count = ga.soft_count ? ga.soft_count[*ga.agent] : step0;
+        const int64_t count = ga.soft_count ? ga.soft_count[flock_mem::ld_sc1(ga.agent)] : step0;
         sh_soft = ga.do_adam && ga.soft_rate > 0 && (count % ga.soft_rate) == 0;  // this learn's count
         if (ga.do_adam) {
             const double st = (double)(step0 + 1);
@@ -2016,7 +2016,7 @@ int g_sc_fuse_k1 = -1;  // flock_set_diag("sc_fuse_k1", 0 / 1); -1: FLOCK_SC_FUS
 int fuse_env() {
     static const int v = [] {
         const char* e = getenv("FLOCK_SC_FUSE");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 0;
     }();
     return v;
 }
@@ -2214,6 +2214,14 @@ __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows
     if (threadIdx.x == 0) __hip_atomic_store(gate, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// gate mode 2: ONE wave on the learner stream waits for gate[0] >= seq (gate_wait's bounded poll); the round's launches
+// follow it on the same stream, so no round block ever spins and only this wave holds a slot while the env runs. The
+// round reads the staged rows and the agent index `sc1` (c1_body, ld_sc1 of every *agent), so the hand-off holds
+// whatever the kernel boundary does to the other XCDs' L2.
+__global__ __launch_bounds__(64) void sc_gate_kernel(unsigned long long* gate, unsigned long long seq) {
+    (void)gate_wait(gate, seq);
+}
+
 }  // namespace
 
 // the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
@@ -2336,9 +2344,11 @@ struct FlockScPipeline {
                // snapshot, 2 no env wait on the slot, 3 neither
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
     // device-side snapshot gate (direct launches, single GPU): gate[0] the published sequence number, gate[1] the
-    // error word of a waiter that gave up; seq counts this pipeline's snapshots. NULL: cross-queue event waits
+    // error word of a waiter that gave up; seq counts this pipeline's snapshots. NULL: cross-queue event waits.
+    // gate_mode 1: the critic phase's k1 row blocks poll; 2: one wave on the learner stream (sc_gate_kernel) polls
     unsigned long long* gate;
     unsigned long long seq;
+    int gate_mode;
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
@@ -2460,8 +2470,9 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     // default there. Graph replays and data-parallel rounds keep the events.
     const char* gte = getenv("FLOCK_SC_GATE");
     const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
-    const bool gate_on = gte ? gte[0] != '0' : !(pmc && pmc[0] && pmc[0] != '0');
-    if (!rc && !p->graphs && p->diag == 0 && gate_on) {
+    p->gate_mode = gte ? atoi(gte) : (pmc && pmc[0] && pmc[0] != '0') ? 0 : 2;
+    if (p->gate_mode < 0 || p->gate_mode > 2) p->gate_mode = 0;
+    if (!rc && !p->graphs && p->diag == 0 && p->gate_mode) {
         if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
             hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess)
@@ -2473,6 +2484,15 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     }
     return p;
 }
+
+namespace {
+// gate mode 2: the learner stream's wait for this learn's snapshot (the seq just published by pipeline_learn)
+int gate_kernel(FlockScPipeline* p, hipStream_t ls) {
+    if (!p->gate || p->dp || p->gate_mode != 2) return 0;
+    hipLaunchKernelGGL(sc_gate_kernel, dim3(1), dim3(64), 0, ls, p->gate, p->seq);
+    return launched();
+}
+}  // namespace
 
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent) {
@@ -2496,7 +2516,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
                            const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq);
         if ((rc = launched())) return rc;
-        p->jc[s].a.gate = p->gate;
+        p->jc[s].a.gate = p->gate_mode == 1 ? p->gate : nullptr;
         p->jc[s].a.gate_seq = seq;
     } else {
         rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
@@ -2509,6 +2529,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const int q = p->pending;
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
         // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
+        if ((rc = gate_kernel(p, ls))) return rc;
         if ((rc = pipeline_round(p, ls, s, q))) return rc;
         ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
     } else {
@@ -2517,6 +2538,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
             if ((rc = pipeline_round(p, ls, -1, q))) return rc;
             ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
         }
+        if (ok && (rc = gate_kernel(p, ls))) return rc;
         if (ok && (rc = pipeline_round(p, ls, s, -1))) return rc;
     }
     if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
@@ -2605,7 +2627,7 @@ int flock_sc_workspace_check(const FlockScUpdate* u) {
                 : 0;
 }
 
-int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate && !p->dp ? 1 : 0; }
+int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate && !p->dp ? p->gate_mode : 0; }
 
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;

@@ -174,7 +174,7 @@ struct ScPipeline : torch::CustomClassHolder {
         check(flock_sc_pipeline_check(pipe), "flock_sc_pipeline_check");
     }
 
-    bool gated() const { return flock_sc_pipeline_gated(pipe) != 0; }
+    int64_t gated() const { return flock_sc_pipeline_gated(pipe); }
 };
 
 struct ScTrainLoop : torch::CustomClassHolder {

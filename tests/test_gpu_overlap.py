@@ -147,7 +147,7 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, cuda):
     main.wait_stream(ls)
     torch.cuda.synchronize()
     pip.pipeline_check()  # no round gave up waiting for its snapshot (device-side gate)
-    assert pip.pipeline().gated() == (os.environ.get("FLOCK_SC_GATE", "1") != "0")
+    assert pip.pipeline().gated() == int(os.environ.get("FLOCK_SC_GATE", "2"))
     for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg, pip.critic.exp_avg),
                  (ser.critic.exp_avg_sq, pip.critic.exp_avg_sq), (ser.actors.data, pip.actors.data),
                  (ser.actors.exp_avg, pip.actors.exp_avg), (ser.actors.target, pip.actors.target),
@@ -210,7 +210,7 @@ def test_device_gate_and_fused_rounds_are_bitwise_the_plain_pipeline(n_slots, cu
     pool = [torch.stack([torch.rand(E, Na, device=cuda, generator=g),
                          torch.rand(E, Na, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
     out = []
-    modes = (("0", 0), ("0", 0), ("1", 0), ("0", 1), ("1", 1), ("0", 2), ("1", 2))  # the plain pipeline twice
+    modes = (("0", 0), ("0", 0), ("1", 0), ("2", 0), ("0", 1), ("1", 1), ("2", 1), ("1", 2), ("2", 2))  # plain twice
     for gate, fuse in modes:
         os.environ["FLOCK_SC_GATE"] = gate
         assert lib.flock_set_diag(b"sc_no_fuse", int(fuse == 0)) == 0
@@ -227,7 +227,7 @@ def test_device_gate_and_fused_rounds_are_bitwise_the_plain_pipeline(n_slots, cu
             torch.cuda.synchronize()
             L = hook.learner
             L.pipeline_check()
-            assert L.pipeline().gated() == (gate == "1")
+            assert L.pipeline().gated() == int(gate)
             C, A = L.critic, L.actors
             out.append([C.data.clone(), C.exp_avg.clone(), C.exp_avg_sq.clone(), A.data.clone(), A.target.clone(),
                         A.exp_avg.clone(), A.exp_avg_sq.clone(), L.actor_steps.clone(), L.losses.clone(),

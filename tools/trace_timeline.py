@@ -1,6 +1,7 @@
 """Per-step timeline of the config-3 loop from a rocprofv3 --kernel-trace CSV (diagnostics).
 
-For every env step (the step_kernel launches) and every learner round (sc_k1 .. sc_grad_adam) prints the start / end
+For every env step (the step_kernel launches) and every learner round (its first kernel: sc_gate_kernel, sc_k1 or
+sc_fwd, .. its last: sc_grad_adam or sc_bwdg) prints the start / end
 relative to the first step, and summarises: the step period, the env launches' span, the round's span, the gap
 between the snapshot and the round's first kernel, the gaps between the round's kernels, and which stream set the
 period (did the env stream start its next step right after its previous one, or later).
@@ -22,8 +23,8 @@ def load(path):
 
 def short(name):
     # the fused rounds' kernels (sc_fwd, sc_bwdg) are checked before the prefixes they contain
-    for key in ("step_kernel", "sc_prep_snapshot", "sc_k1", "sc_fwd", "sc_bwdg", "sc_gemm", "sc_k3", "sc_bwd",
-                "sc_grad_adam"):
+    for key in ("step_kernel", "sc_prep_snapshot", "sc_gate_kernel", "sc_k1", "sc_fwd", "sc_bwdg", "sc_gemm", "sc_k3",
+                "sc_bwd", "sc_grad_adam"):
         if key in name:
             return key
     return None
@@ -40,19 +41,16 @@ def main():
         elif k == "sc_prep_snapshot" and cur:
             env_steps.append((cur, (s, e)))
             cur = []
-    rounds, rc = [], {}
-    last = "sc_grad_adam"
+    rounds, rc, order = [], {}, None
     for s, e, k in rows:
-        if k == "sc_k1":
-            rc = {"sc_k1": (s, e)}
-        elif k.startswith("sc_") and k != "sc_prep_snapshot" and rc:
+        if k.startswith("sc_") and k != "sc_prep_snapshot":
+            rc.setdefault("_order", []).append(k)
             rc[k] = (s, e)
             if k in ("sc_grad_adam", "sc_bwdg"):
-                last = k
+                order = order or rc["_order"]
+                rc["_first"] = rc[rc["_order"][0]]
                 rounds.append(rc)
                 rc = {}
-    fused = last == "sc_bwdg"
-    order = ["sc_k1", "sc_fwd", "sc_bwdg"] if fused else ["sc_k1", "sc_gemm", "sc_k3", "sc_bwd", "sc_grad_adam"]
     n = min(len(env_steps), len(rounds))
     skip = max(0, n - 60)  # the last 60 steps (the timed region sits at the end of a short bench)
     t0 = env_steps[skip][0][0][0]
@@ -66,13 +64,13 @@ def main():
         env_span.append((launches[-1][1] - launches[0][0]) / 1e3)
         env_idle.append((nxt - snap[1]) / 1e3)
         # the round that consumes this step's snapshot starts after it
-        r = next((rr for rr in rounds if rr["sc_k1"][0] >= snap[1]), None)
+        r = next((rr for rr in rounds if rr["_first"][1] >= snap[1]), None)
         if r is None:
             continue
         if any(k not in r for k in order):
             continue
-        snap_gap.append((r["sc_k1"][0] - snap[1]) / 1e3)
-        rnd_span.append((r[order[-1]][1] - r["sc_k1"][0]) / 1e3)
+        snap_gap.append((r["_first"][1] - snap[1]) / 1e3)
+        rnd_span.append((r[order[-1]][1] - r["_first"][0]) / 1e3)
         for a, b in zip(order, order[1:]):
             kgaps[b].append((r[b][0] - r[a][1]) / 1e3)
         for k in order:
@@ -80,7 +78,7 @@ def main():
         if i - skip < 12:
             ls = " ".join("%7.1f-%7.1f" % ((s - t0) / 1e3, (e - t0) / 1e3) for s, e in launches)
             print("step %3d env %s snap %7.1f-%7.1f | round %7.1f-%7.1f" % (
-                i - skip, ls, (snap[0] - t0) / 1e3, (snap[1] - t0) / 1e3, (r["sc_k1"][0] - t0) / 1e3,
+                i - skip, ls, (snap[0] - t0) / 1e3, (snap[1] - t0) / 1e3, (r["_first"][0] - t0) / 1e3,
                 (r[order[-1]][1] - t0) / 1e3))
 
     def m(v):
@@ -90,8 +88,9 @@ def main():
     print("step period us            ", m(per))
     print("env launches span us      ", m(env_span))
     print("env stream idle after snap", m(env_idle))
-    print("snapshot end -> k1 start  ", m(snap_gap))
-    print("round span k1..grad us    ", m(rnd_span))
+    print("round order               ", " ".join(order))
+    print("snapshot end -> 1st k end ", m(snap_gap))
+    print("round span us             ", m(rnd_span))
     for k, v in kdur.items():
         print("  %-13s dur %s" % (k, m(v)))
     for k, v in kgaps.items():
