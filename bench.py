@@ -498,9 +498,13 @@ def main():
     for e in evs:  # create the HIP events outside the timed region
         e.record(stream)
 
+    span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for e in span:
+        e.record(stream)
     barrier(world)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    span[0].record(stream)  # the GPU-side span of the timed region (its first to its last enqueued command)
     if use_loop:
         hook.run_steps(args.warmup, args.steps, pool, evs, EV_EVERY)
     else:
@@ -508,6 +512,7 @@ def main():
             one_step(args.warmup + s, ev.get(s))
     if hook is not None and hasattr(hook, "finish"):
         hook.finish()  # the learner work still pending (the last learn's actor phase) runs inside the timed region
+    span[1].record(stream)
     host_el = time.perf_counter() - t0  # host enqueue time of the timed steps (no synchronisation inside)
     torch.cuda.synchronize(dev)
     barrier(world)
@@ -596,6 +601,9 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3,
         "host_ms_per_step": host_el / args.steps * 1e3,
+        # HIP events at the start and the end of the timed region on the launch stream: the GPU-side span, i.e.
+        # ms_per_step without the launch latency of the first command and the final synchronisation
+        "gpu_span_ms_per_step": span[0].elapsed_time(span[1]) / args.steps,
         "host_enqueue_us_per_step": host_us,
         "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
                       "one Python step per vectorized step (torch.ops.flock)"),

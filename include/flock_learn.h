@@ -231,10 +231,11 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p);
  * flock_sc_round_adam with grad_scale (device scalar, 1 / world: the mean). Bitwise one process learning on the
  * union of the ranks' minibatches when the sums are exact in any order (SharedCriticLearner.dp_learn). Call before
  * the first flock_sc_pipeline_learn. */
-/* The device-side snapshot gate (single GPU, the default; FLOCK_SC_GATE=0 or rocprofv3 counter collection, which
- * serialises dispatches: cross-queue event waits instead): the snapshot kernel writes the staging rows `sc1` and
- * publishes a sequence number after all its stores completed, and the learner stream waits for it on the device
- * instead of for an event: FLOCK_SC_GATE=2 (default) one wave launched before the round polls it (bounded, 0.2 s),
+/* The device-side snapshot gate (single GPU, opt-in: FLOCK_SC_GATE=1 / 2; the default 0, and always under rocprofv3
+ * counter collection, which serialises dispatches, is the cross-queue event wait, measured faster in round 4): the
+ * snapshot kernel writes the staging rows `sc1` and publishes a sequence number after all its stores completed, and
+ * the learner stream waits for it on the device instead of for an event: FLOCK_SC_GATE=2 one wave launched before
+ * the round polls it (bounded, 0.2 s),
  * FLOCK_SC_GATE=1 the round's critic row blocks poll it. A waiter that gives up sets an error word and computes
  * nothing; flock_sc_pipeline_check (synchronous: call after synchronising the learner stream) returns -6 then.
  * flock_sc_pipeline_gated: the gate mode in use (0 = event waits). */

@@ -1133,10 +1133,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     PHASE(1);
     // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
     int cx = 0, cy = 0;
+#ifdef FLOCK_DIAG_BINREP  // diagnostics: the binning phase run FLOCK_DIAG_BINREP times (its marginal cost; same results)
+    for (int rep_ = 0; rep_ < FLOCK_DIAG_BINREP; ++rep_)
+#endif
     if (CELL) {
         int* cnt = cnt_all + g * ncell;
         int* pre = pre_all + g * npre;
         float4* ext = ext_all + g * p.ecap;
+#ifdef FLOCK_DIAG_BINREP
+        if (rep_ > 0) {
+            if (in_group)
+                for (int c = i; c < ncell; c += p.N) cnt[c] = 0;
+            __syncthreads();
+        }
+#endif
         int rank = 0;
         if (active) {
             cx = min((int)(x * p.inv_cwx), gx - 1);  // x, y in [0, box] after check_boundary

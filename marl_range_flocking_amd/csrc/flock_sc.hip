@@ -2463,14 +2463,15 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->dp = false;
     p->gate = nullptr;
     p->seq = 0;
-    // the learner stream waits for each snapshot on the device (the critic phase's row blocks poll gate[0]) instead of
-    // a cross-queue barrier packet; FLOCK_SC_GATE=0 / 1 (read here) forces either. The spin needs the two queues'
-    // kernels to run concurrently: under rocprofv3 counter collection (ROCPROF_COUNTER_COLLECTION, which serialises
-    // dispatches) a round dispatched ahead of its snapshot would wait out its bound, so the event waits are the
-    // default there. Graph replays and data-parallel rounds keep the events.
+    // the learner stream's wait for each snapshot: a cross-queue event wait (0, the default), or on the device
+    // (FLOCK_SC_GATE=1: the critic phase's row blocks poll gate[0]; 2: one wave launched before the round polls it).
+    // Round 4, same-box interleaved A/B at config 3 (profiles/r04/eval1): event 0.0819-0.0825 ms per step, gate 2
+    // 0.0826-0.0839. The spin needs the two queues' kernels to run concurrently: under rocprofv3 counter collection
+    // (ROCPROF_COUNTER_COLLECTION, which serialises dispatches) a round dispatched ahead of its snapshot would wait out
+    // its bound, so the event waits are forced there. Graph replays and data-parallel rounds keep the events.
     const char* gte = getenv("FLOCK_SC_GATE");
     const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
-    p->gate_mode = gte ? atoi(gte) : (pmc && pmc[0] && pmc[0] != '0') ? 0 : 2;
+    p->gate_mode = (pmc && pmc[0] && pmc[0] != '0') ? 0 : gte ? atoi(gte) : 0;
     if (p->gate_mode < 0 || p->gate_mode > 2) p->gate_mode = 0;
     if (!rc && !p->graphs && p->diag == 0 && p->gate_mode) {
         if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
