@@ -221,6 +221,30 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
                                           const FlockScRows* staging);
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent);
+/* Direct learns (no snapshot), for a loop whose every env step rewrites the WHOLE replay ring (E N >= capacity, so the
+ * ring's content after step t is a function of step t alone) and that keeps one physical copy of the ring per slot:
+ *   flock_sc_pipeline_acquire(p, env_stream) -> slot s: enqueues, on env_stream, the wait until slot s's previous
+ *     learn() has finished with its rows; the caller then steps the env into ring copy s (the fused insert);
+ *   flock_sc_pipeline_learn_direct(..., &copy_s): event on env_stream -> the learner stream waits for it -> the same
+ *     rounds as flock_sc_pipeline_learn, whose critic phase draws its minibatch rows itself (the same Philox rows the
+ *     snapshot copies) straight from copy s and takes `agent` by value.
+ * Bitwise the snapshot learns (the rows, the agent and every round are the same); what it removes is the snapshot
+ * kernel between the env steps on env_stream. Not with data-parallel rounds or graph replays (-5). The copy a loop
+ * wrote last holds the logical ring (ScTrainLoop: the caller copies it back into the ring). */
+int flock_sc_pipeline_acquire(FlockScPipeline* p, void* env_stream);
+/* Copy learns: the same ring copies (any number, 2..8, used in turn; copy c's env step waits until the snapshot that
+ * last read copy c has run: flock_sc_pipeline_copy_acquire), but the minibatch snapshot runs on a stream of the
+ * pipeline's own, behind an event wait for the env step that wrote the copy, and publishes a sequence number through
+ * the device gate (`sc1` rows, csrc/flock_mem.h); the learner stream polls it with one wave and runs the rounds. So
+ * neither the env stream (no snapshot between its steps) nor the learner stream (no cross-queue wait) carries the
+ * snapshot's latency. Bitwise the snapshot learns. Needs the gate (flock_sc_pipeline_copy_ok: not data-parallel, not
+ * graph replays, not under rocprofv3 counter collection, which serialises dispatches). */
+int flock_sc_pipeline_copy_ok(const FlockScPipeline* p);
+int flock_sc_pipeline_copy_acquire(FlockScPipeline* p, void* env_stream, int copy);
+int flock_sc_pipeline_learn_copy(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
+                                 uint64_t seed, uint64_t counter, int64_t agent, int copy, const FlockScRows* ring);
+int flock_sc_pipeline_learn_direct(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
+                                   uint64_t seed, uint64_t counter, int64_t agent, const FlockScRows* ring);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);
 /* Data-parallel rounds (one replica per GPU, the same learn() sequence on every rank): after this call every round

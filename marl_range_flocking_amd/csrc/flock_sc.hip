@@ -37,7 +37,13 @@ namespace {
 using flock_learn_internal::fail;
 using flock_learn_internal::launched;
 
-constexpr int kRowsPerBlock = 4;
+// replay rows per row-kernel block: 4 waves x kRW rows each (-DFLOCK_SC_RW=2 / 4: fewer, longer row blocks beside the
+// env kernel; A/B builds)
+#ifndef FLOCK_SC_RW
+#define FLOCK_SC_RW 1
+#endif
+constexpr int kRW = FLOCK_SC_RW;
+constexpr int kRowsPerBlock = 4 * kRW;
 constexpr int kMaxAct = 4;
 constexpr int kMaxIn = 64;
 constexpr int kMaxFeat = 1024;
@@ -152,6 +158,12 @@ struct RowArgs {
     // (published by the snapshot kernel) instead of a cross-queue event wait; NULL: no wait
     unsigned long long* gate;
     unsigned long long gate_seq;
+    // direct rounds (flock_sc_pipeline_learn_direct): rows > 0 makes the critic phase's k1 draw its minibatch rows
+    // itself (sample_row(seed, counter, rows, r); idx unused) from the ring copy the env step just wrote, and take the
+    // agent index by value (agent_val >= 0; its path-0 blocks also store it to *agent for the round's later launches)
+    uint64_t seed, counter;
+    int64_t rows;
+    int64_t agent_val;
 };
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -175,6 +187,32 @@ __device__ __forceinline__ float wave_sum(float v) {
     return (r0 + r1) + (r2 + r3);
 }
 __device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
+
+// learn() prologue: the agent index and the minibatch rows (Philox4x32-10, counter = (learn counter, row))
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+// the replay row that minibatch row r of learn `counter` samples: Philox4x32-10(seed, (r, 0x5C5C5C5C, counter)) mod rows
+// (uniform with replacement, ReplayBuffer.sample_buffer utils.py:65-76; sc_prep, the snapshot and the direct rounds'
+// k1 rows all draw it this way)
+__device__ __forceinline__ int64_t sample_row(uint64_t seed, uint64_t counter, int64_t rows, int r) {
+    const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
+    const uint64_t u = ((uint64_t)q.x << 32) | q.y;
+    return (int64_t)(u % (uint64_t)rows);
+}
 __device__ __forceinline__ float rsqrt_rn(float x) { return 1.0f / __builtin_sqrtf(x); }
 
 // copy n floats global -> LDS (dst 16-B aligned) with every load of a round issued before any LDS store
@@ -345,17 +383,29 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
     float* xs = reinterpret_cast<float*>(smem4);  // [4 rows][kMaxIn] inputs, then the fc1 image
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int r = bx * kRowsPerBlock + wv;
     // the replay rows and the agent index are read `sc1`: with the device-side gate (sc_k1) they are a snapshot
     // another queue's kernel has just written through (csrc/flock_mem.h)
     using flock_mem::ld_sc1;
-    const float* net = path == 0 ? a.actors_target + ld_sc1(a.agent) * a.stride : a.critic;  // fc1 block at offset 0
-    const bool live = r < a.B;
-    if (live) {
-        const int64_t ir = a.idx[r];
+    const float* net = path == 0 ? a.actors_target + (a.agent_val >= 0 ? a.agent_val : ld_sc1(a.agent)) * a.stride
+                                 : a.critic;  // fc1 block at offset 0
+    // direct rounds: this learn's agent index for the round's later readers (F: the fused forward launch's GEMM tiles
+    // and k3 rows read it `sc1` after this block's arrival, which follows every wave's vmcnt(0) wait)
+    if (path == 0 && a.agent_val >= 0 && threadIdx.x == 0) {
+        int64_t* ag = const_cast<int64_t*>(a.agent);
+        if constexpr (F)
+            flock_mem::st_sc1(ag, a.agent_val);
+        else
+            *ag = a.agent_val;
+    }
+    // wave wv takes rows bx kRowsPerBlock + 4 q + wv, q < kRW
+#pragma unroll
+    for (int q = 0; q < kRW; ++q) {
+        const int r = bx * kRowsPerBlock + 4 * q + wv;
+        if (r >= a.B) continue;
+        const int64_t ir = a.rows > 0 ? sample_row(a.seed, a.counter, a.rows, r) : a.idx[r];
         const float* x = (path == 2 ? a.rs : a.rs2) + ir * a.in;
         const float xv = lane < a.in ? ld_sc1(x + lane) : 0.0f;
-        if (lane < a.in) xs[wv * kMaxIn + lane] = xv;
+        if (lane < a.in) xs[(4 * q + wv) * kMaxIn + lane] = xv;
         if (path == 2) {
             if (lane < a.in) {
                 st_out<F>(w.S + (int64_t)r * a.in + lane, xv);
@@ -370,18 +420,22 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
     }
     stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
-    if (!live) return;
-    float xh[C], h[C], rs;
-    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
-    const int64_t ro = (int64_t)r * H1;
-    if (path == 0) {
-        store_row<C, F>(w.TH1 + ro, h, H1, lane);
-    } else if (path == 1) {
-        store_row<C, F>(w.NH1 + ro, h, H1, lane);
-    } else {
-        store_row<C, F>(w.XH1 + ro, xh, H1, lane);
-        store_row<C, F>(w.H1 + ro, h, H1, lane);
-        if (lane == 0) st_out<F>(w.RS1 + r, rs);
+#pragma unroll
+    for (int q = 0; q < kRW; ++q) {
+        const int r = bx * kRowsPerBlock + 4 * q + wv;
+        if (r >= a.B) continue;
+        float xh[C], h[C], rs;
+        fc1_ln_relu<C>(xs + (4 * q + wv) * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
+        const int64_t ro = (int64_t)r * H1;
+        if (path == 0) {
+            store_row<C, F>(w.TH1 + ro, h, H1, lane);
+        } else if (path == 1) {
+            store_row<C, F>(w.NH1 + ro, h, H1, lane);
+        } else {
+            store_row<C, F>(w.XH1 + ro, xh, H1, lane);
+            store_row<C, F>(w.H1 + ro, h, H1, lane);
+            if (lane == 0) st_out<F>(w.RS1 + r, rs);
+        }
     }
 }
 
@@ -393,29 +447,44 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     const int H2 = HC ? HC : a.H2, na = NAC ? NAC : a.na;
     float* at = ct + round4(crit_tail_len(na, H2));  // target actor tail
     const int lane = threadIdx.x & 63;
-    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
-    const bool live = r < a.B;
     const CriticOff co = critic_off(a.in, na, a.H1, H2);
     const ActorOff ao = actor_off(a.in, na, a.H1, H2);
-    float zt[C], zn[C], zs[C];
-    float rwd = 0.0f, term = 0.0f, act[kMaxAct];
-    if (live) {
-        load_row<C, F>(zt, w.Z2 + (int64_t)r * H2, H2, lane);
-        load_row<C, F>(zn, w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
-        load_row<C, F>(zs, w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
-        rwd = ld_in<F>(w.R + r);
-        term = ld_in<F>(w.T + r);
+    // every row of this wave (bx kRowsPerBlock + 4 q + wave, q < kRW) loaded before the tails' staging barrier
+    float ztq[kRW][C], znq[kRW][C], zsq[kRW][C];
+    float rwdq[kRW], termq[kRW], actq[kRW][kMaxAct];
 #pragma unroll
-        for (int o = 0; o < kMaxAct; ++o) act[o] = o < na ? ld_in<F>(w.A + (int64_t)r * na + o) : 0.0f;
+    for (int rq = 0; rq < kRW; ++rq) {
+        const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
+        rwdq[rq] = 0.0f;
+        termq[rq] = 0.0f;
+#pragma unroll
+        for (int o = 0; o < kMaxAct; ++o) actq[rq][o] = 0.0f;
+        if (r < a.B) {
+            load_row<C, F>(ztq[rq], w.Z2 + (int64_t)r * H2, H2, lane);
+            load_row<C, F>(znq[rq], w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
+            load_row<C, F>(zsq[rq], w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
+            rwdq[rq] = ld_in<F>(w.R + r);
+            termq[rq] = ld_in<F>(w.T + r);
+#pragma unroll
+            for (int o = 0; o < kMaxAct; ++o) actq[rq][o] = o < na ? ld_in<F>(w.A + (int64_t)r * na + o) : 0.0f;
+        }
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
     // F: the agent index as the snapshot wrote it (the k1-fused launch may have started before the snapshot ran)
     stage(at, a.actors_target + flock_mem::ld_sc1(a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
-    if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
     const float cbq = cWq[H2];
     const float *tg2 = at, *tbe2 = at + H2, *tWmu = at + 2 * H2, *tbmu = tWmu + na * H2;
+#pragma unroll
+    for (int rq = 0; rq < kRW; ++rq) {
+    const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
+    if (r >= a.B) continue;
+    const float(&zt)[C] = ztq[rq];
+    const float(&zn)[C] = znq[rq];
+    const float(&zs)[C] = zsq[rq];
+    const float rwd = rwdq[rq], term = termq[rq];
+    const float(&act)[kMaxAct] = actq[rq];
     float xh[C], y[C], rs;
 
     // target actor on s': mu' = tanh(Wmu ReLU(LN2(z)) + bmu)                    (:126, ddpg_network.py:134-140)
@@ -497,6 +566,7 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     store_row<C>(w.XH2 + ro, xh, H2, lane);
     store_row<C>(w.DZ2 + ro, dz2, H2, lane);
     if (lane == 0) w.RS2[r] = rs;
+    }
 }
 
 // c5 / a5: ReLU + LN1 backward: dy = dh * [h > 0]; dz = LN backward(dy)
@@ -508,22 +578,28 @@ __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, i
     float* xs = reinterpret_cast<float*>(smem4);
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int r = bx * kRowsPerBlock + wv;
-    const bool live = r < a.B;
     const float* net = path == 0 ? a.actors + flock_mem::ld_sc1(a.agent) * a.stride : a.critic;
-    if (live && lane < a.in) xs[wv * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
+#pragma unroll
+    for (int q = 0; q < kRW; ++q) {
+        const int r = bx * kRowsPerBlock + 4 * q + wv;
+        if (r < a.B && lane < a.in) xs[(4 * q + wv) * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
+    }
     stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
-    if (!live) return;
-    float xh[C], h[C], rs;
-    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
-    const int64_t ro = (int64_t)r * H1;
-    if (path == 0) {
-        store_row<C, F>(w.AXH1 + ro, xh, H1, lane);
-        store_row<C, F>(w.AH1 + ro, h, H1, lane);
-        if (lane == 0) st_out<F>(w.ARS1 + r, rs);
-    } else {
-        store_row<C, F>(w.CH1 + ro, h, H1, lane);
+#pragma unroll
+    for (int q = 0; q < kRW; ++q) {
+        const int r = bx * kRowsPerBlock + 4 * q + wv;
+        if (r >= a.B) continue;
+        float xh[C], h[C], rs;
+        fc1_ln_relu<C>(xs + (4 * q + wv) * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
+        const int64_t ro = (int64_t)r * H1;
+        if (path == 0) {
+            store_row<C, F>(w.AXH1 + ro, xh, H1, lane);
+            store_row<C, F>(w.AH1 + ro, h, H1, lane);
+            if (lane == 0) st_out<F>(w.ARS1 + r, rs);
+        } else {
+            store_row<C, F>(w.CH1 + ro, h, H1, lane);
+        }
     }
 }
 
@@ -536,23 +612,31 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     const int H2 = HC ? HC : a.H2, na = NAC ? NAC : a.na;
     float* at = ct + round4(crit_tail_len(na, H2));
     const int lane = threadIdx.x & 63;
-    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
-    const bool live = r < a.B;
     const CriticOff co = critic_off(a.in, na, a.H1, H2);
     const ActorOff ao = actor_off(a.in, na, a.H1, H2);
-    const int64_t ro = (int64_t)r * H2;
-    float za2[C], zc2[C];
-    if (live) {
-        load_row<C, F>(za2, w.Z2b + ro, H2, lane);
-        load_row<C, F>(zc2, w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
+    // every row of this wave (bx kRowsPerBlock + 4 q + wave, q < kRW) loaded before the tails' staging barrier
+    float za2q[kRW][C], zc2q[kRW][C];
+#pragma unroll
+    for (int rq = 0; rq < kRW; ++rq) {
+        const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
+        if (r < a.B) {
+            load_row<C, F>(za2q[rq], w.Z2b + (int64_t)r * H2, H2, lane);
+            load_row<C, F>(zc2q[rq], w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
+        }
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
     stage(at, a.actors + flock_mem::ld_sc1(a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
-    if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
     const float cbq = cWq[H2];
     const float *ag2 = at, *abe2 = at + H2, *aWmu = at + 2 * H2, *abmu = aWmu + na * H2;
+#pragma unroll
+    for (int rq = 0; rq < kRW; ++rq) {
+    const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
+    if (r >= a.B) continue;
+    const int64_t ro = (int64_t)r * H2;
+    const float(&za2)[C] = za2q[rq];
+    const float(&zc2)[C] = zc2q[rq];
 
     float xh[C], y[C], h2[C], rs;
     ln_affine<C>(za2, ag2, abe2, H2, lane, xh, y, rs);
@@ -634,6 +718,7 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     store_row<C>(w.ADY2 + ro, dy2, H2, lane);
     store_row<C>(w.ADZ2 + ro, dz2, H2, lane);
     if (lane == 0) w.ARS2[r] = rs;
+    }
 }
 
 // -DFLOCK_SC_PROF (diagnostics build, tools/sc_block_prof.py): per-block start / end times (s_memrealtime, 100 MHz)
@@ -1713,6 +1798,10 @@ RowArgs row_args(const FlockScUpdate* u) {
     a.invB = 1.0f / (float)u->B;
     a.gate = nullptr;  // only flock_sc_pipeline_learn gates a critic phase on its snapshot
     a.gate_seq = 0;
+    a.seed = 0;
+    a.counter = 0;
+    a.rows = 0;  // the rows come through idx (only flock_sc_pipeline_learn_direct samples in k1)
+    a.agent_val = -1;
     return a;
 }
 
@@ -2120,33 +2209,12 @@ int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja) {
     return launched();
 }
 
-// learn() prologue: the agent index and the minibatch rows (Philox4x32-10, counter = (learn counter, row))
-__device__ __forceinline__ uint4 philox4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
-    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0;
-        c1 = lo1;
-        c2 = n2;
-        c3 = lo0;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-    return make_uint4(c0, c1, c2, c3);
-}
 
 __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
                                                int64_t* agent_out, int64_t agent) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r == 0) *agent_out = agent;
-    if (idx && r < B) {
-        const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
-        const uint64_t u = ((uint64_t)q.x << 32) | q.y;
-        idx[r] = (int64_t)(u % (uint64_t)rows);
-    }
+    if (idx && r < B) idx[r] = sample_row(seed, counter, rows, r);
 }
 
 // learn() prologue with a minibatch snapshot: the sampled rows of every replay field are copied to staging rows
@@ -2156,9 +2224,7 @@ template <bool SC1>
 __device__ __forceinline__ void snapshot_row(int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
                                              int in_dim, int n_actions, const FlockScRows& src,
                                              const FlockScRows& dst, int vec, int r) {
-    const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
-    const uint64_t u = ((uint64_t)q.x << 32) | q.y;
-    const int64_t row = (int64_t)(u % (uint64_t)rows);  // the row sc_prep samples for r
+    const int64_t row = sample_row(seed, counter, rows, r);  // the row sc_prep samples for r
     if (idx_out) idx_out[r] = row;
     auto st = [](auto* p, auto v) {
         if constexpr (SC1)
@@ -2351,6 +2417,13 @@ struct FlockScPipeline {
     int gate_mode;
     bool used[kMaxSlots];
     int slot;
+    int acquired;  // flock_sc_pipeline_acquire's slot (its ring copy may be written), -1 otherwise
+    // copy learns (flock_sc_pipeline_learn_copy): the snapshots run on a stream of their own (created at the first
+    // copy learn); copy_written[c]: env step into ring copy c done (env stream), copy_read[c]: the snapshot that read
+    // copy c done (snapshot stream)
+    hipStream_t snap_stream;
+    hipEvent_t copy_written[kMaxSlots], copy_read[kMaxSlots];
+    bool copy_used[kMaxSlots];
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
     int64_t pending_agent;
     // data-parallel rounds (flock_sc_pipeline_set_dp): gradients into the [critic | actor] bucket, the caller's
@@ -2458,6 +2531,12 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
         p->used[i] = false;
     }
     p->slot = 0;
+    p->acquired = -1;
+    p->snap_stream = nullptr;
+    for (int i = 0; i < kMaxSlots; ++i) {
+        p->copy_written[i] = p->copy_read[i] = nullptr;
+        p->copy_used[i] = false;
+    }
     p->pending = -1;
     p->pending_agent = -1;
     p->dp = false;
@@ -2471,9 +2550,12 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     // its bound, so the event waits are forced there. Graph replays and data-parallel rounds keep the events.
     const char* gte = getenv("FLOCK_SC_GATE");
     const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
-    p->gate_mode = (pmc && pmc[0] && pmc[0] != '0') ? 0 : gte ? atoi(gte) : 0;
+    const bool pmc_on = pmc && pmc[0] && pmc[0] != '0';
+    p->gate_mode = pmc_on ? 0 : gte ? atoi(gte) : 0;
     if (p->gate_mode < 0 || p->gate_mode > 2) p->gate_mode = 0;
-    if (!rc && !p->graphs && p->diag == 0 && p->gate_mode) {
+    // the gate words exist whenever a device-side wait may be used: the snapshot learns' gate modes and the copy
+    // learns (flock_sc_pipeline_learn_copy), not under counter collection
+    if (!rc && !p->graphs && p->diag == 0 && !pmc_on) {
         if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
             hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess)
@@ -2488,10 +2570,42 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
 
 namespace {
 // gate mode 2: the learner stream's wait for this learn's snapshot (the seq just published by pipeline_learn)
-int gate_kernel(FlockScPipeline* p, hipStream_t ls) {
-    if (!p->gate || p->dp || p->gate_mode != 2) return 0;
+int gate_kernel(FlockScPipeline* p, hipStream_t ls, bool always = false) {
+    if (!p->gate || p->dp || (!always && p->gate_mode != 2)) return 0;
     hipLaunchKernelGGL(sc_gate_kernel, dim3(1), dim3(64), 0, ls, p->gate, p->seq);
     return launched();
+}
+}  // namespace
+
+namespace {
+// the rounds of a learn() whose critic phase (slot s) reads inputs the learner stream already waits for: the critic
+// phase of s beside the actor phase of the previous learn, or one after the other (same agent). gated: gate mode 2's
+// polling wave goes in front of the critic phase (snapshot learns only)
+int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent, bool gated, bool poll = false) {
+    const int n = p->n;
+    int rc = 0;
+    bool ok = true;
+    const int q = p->pending;
+    if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
+        // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
+        if (gated && (rc = gate_kernel(p, ls, poll))) return rc;
+        if ((rc = pipeline_round(p, ls, s, q))) return rc;
+        ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
+    } else {
+        // same agent (this critic phase reads the target actor that actor phase soft-updates): one after the other
+        if (q >= 0) {
+            if ((rc = pipeline_round(p, ls, -1, q))) return rc;
+            ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
+        }
+        if (ok && gated && (rc = gate_kernel(p, ls, poll))) return rc;
+        if (ok && (rc = pipeline_round(p, ls, s, -1))) return rc;
+    }
+    if (!ok) return fail(-4, "flock_sc_pipeline: stream operation failed");
+    p->pending = s;
+    p->pending_agent = agent;
+    p->used[s] = true;
+    p->slot = (s + 1) % n;
+    return 0;
 }
 }  // namespace
 
@@ -2499,13 +2613,27 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
                             uint64_t counter, int64_t agent) {
     if (!p) return fail(-3, "flock_sc_pipeline_learn: NULL pipeline");
     hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
-    const int s = p->slot, n = p->n;
+    const int s = p->slot;
     const FlockScUpdate& u = p->u[s];
+    p->acquired = -1;
     if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
+    {  // the critic phase reads the slot's staging rows through the identity index (a direct learn may have run)
+        RowArgs& a = p->jc[s].a;
+        a.idx = u.idx;
+        a.rs = u.ring_state;
+        a.rs2 = u.ring_new_state;
+        a.ra = u.ring_action;
+        a.rr = u.ring_reward;
+        a.rt = u.ring_terminal;
+        a.rows = 0;
+        a.agent_val = -1;
+        a.gate = nullptr;
+    }
     int rc = 0;
     bool ok = true;
-    if (p->gate && !p->dp) {
+    const bool gated = p->gate && p->gate_mode && !p->dp;
+    if (gated) {
         // the snapshot publishes gate[0] = seq; this learn's critic row blocks wait for it on the device
         if (u.B < 1 || rows < 1) return fail(-5, "flock_sc_pipeline_learn: need B, rows >= 1");
         const FlockScRows& src = p->ring;
@@ -2520,34 +2648,119 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         p->jc[s].a.gate = p->gate_mode == 1 ? p->gate : nullptr;
         p->jc[s].a.gate_seq = seq;
     } else {
+#ifndef FLOCK_SC_DIAG_NOSNAP  // timing-only builds (results wrong): no snapshot kernel on the env stream
         rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                     u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
+#endif
         if (rc) return rc;
         ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
              ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
     }
     if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
-    const int q = p->pending;
-    if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
-        // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
-        if ((rc = gate_kernel(p, ls))) return rc;
-        if ((rc = pipeline_round(p, ls, s, q))) return rc;
-        ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
-    } else {
-        // same agent (this critic phase reads the target actor that actor phase soft-updates): one after the other
-        if (q >= 0) {
-            if ((rc = pipeline_round(p, ls, -1, q))) return rc;
-            ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
-        }
-        if (ok && (rc = gate_kernel(p, ls))) return rc;
-        if (ok && (rc = pipeline_round(p, ls, s, -1))) return rc;
-    }
-    if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
-    p->pending = s;
-    p->pending_agent = agent;
-    p->used[s] = true;
-    p->slot = (s + 1) % n;
+    return enqueue_rounds(p, ls, s, agent, gated);
+}
+
+int flock_sc_pipeline_acquire(FlockScPipeline* p, void* env_stream) {
+    if (!p) return fail(-3, "flock_sc_pipeline_acquire: NULL pipeline");
+    const int s = p->slot;
+    if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent((hipStream_t)env_stream, p->slot_free[s], 0) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_acquire: wait");
+    p->acquired = s;
+    return s;
+}
+
+int flock_sc_pipeline_learn_direct(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
+                                   uint64_t seed, uint64_t counter, int64_t agent, const FlockScRows* ring) {
+    if (!p || !ring) return fail(-3, "flock_sc_pipeline_learn_direct: NULL argument");
+    if (p->dp || p->graphs)
+        return fail(-5, "flock_sc_pipeline_learn_direct: not with data-parallel rounds or graph replays");
+    if (!ring->state || !ring->new_state || !ring->action || !ring->reward || !ring->terminal)
+        return fail(-3, "flock_sc_pipeline_learn_direct: NULL field pointer");
+    if (rows < 1 || agent < 0) return fail(-5, "flock_sc_pipeline_learn_direct: need rows >= 1 and an agent");
+    const int s = p->slot;
+    if (p->acquired != s)
+        return fail(-5, "flock_sc_pipeline_learn_direct: flock_sc_pipeline_acquire must precede the env step that "
+                        "writes the ring copy");
+    p->acquired = -1;
+    hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
+    RowArgs& a = p->jc[s].a;
+    a.idx = nullptr;
+    a.rs = ring->state;
+    a.rs2 = ring->new_state;
+    a.ra = ring->action;
+    a.rr = ring->reward;
+    a.rt = ring->terminal;
+    a.seed = seed;
+    a.counter = counter;
+    a.rows = rows;
+    a.agent_val = agent;
+    a.gate = nullptr;
+    if (hipEventRecord(p->snap_done[s], es) != hipSuccess ||
+        (!(p->diag & 1) && hipStreamWaitEvent(ls, p->snap_done[s], 0) != hipSuccess))
+        return fail(-4, "flock_sc_pipeline_learn_direct: stream operation failed");
+    return enqueue_rounds(p, ls, s, agent, false);
+}
+
+int flock_sc_pipeline_copy_acquire(FlockScPipeline* p, void* env_stream, int copy) {
+    if (!p) return fail(-3, "flock_sc_pipeline_copy_acquire: NULL pipeline");
+    if (copy < 0 || copy >= kMaxSlots) return fail(-5, "flock_sc_pipeline_copy_acquire: copy out of range");
+    if (p->copy_used[copy] && hipStreamWaitEvent((hipStream_t)env_stream, p->copy_read[copy], 0) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_copy_acquire: wait");
     return 0;
+}
+
+int flock_sc_pipeline_learn_copy(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
+                                 uint64_t seed, uint64_t counter, int64_t agent, int copy, const FlockScRows* ring) {
+    if (!p || !ring) return fail(-3, "flock_sc_pipeline_learn_copy: NULL argument");
+    if (!flock_sc_pipeline_copy_ok(p))
+        return fail(-5, "flock_sc_pipeline_learn_copy: needs the device gate (not with data-parallel rounds, graph "
+                        "replays or under counter collection)");
+    if (copy < 0 || copy >= kMaxSlots) return fail(-5, "flock_sc_pipeline_learn_copy: copy out of range");
+    if (!ring->state || !ring->new_state || !ring->action || !ring->reward || !ring->terminal)
+        return fail(-3, "flock_sc_pipeline_learn_copy: NULL field pointer");
+    const int s = p->slot;
+    const FlockScUpdate& u = p->u[s];
+    if (u.B < 1 || rows < 1) return fail(-5, "flock_sc_pipeline_learn_copy: need B, rows >= 1");
+    hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
+    p->acquired = -1;
+    if (!p->snap_stream && hipStreamCreateWithFlags(&p->snap_stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_learn_copy: stream");
+    for (hipEvent_t* e : {&p->copy_written[copy], &p->copy_read[copy]})
+        if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
+            return fail(-4, "flock_sc_pipeline_learn_copy: event");
+    hipStream_t ss = p->snap_stream;
+    // snapshot stream: after the env step that wrote the copy, and once the slot's previous learn() is done with its
+    // staging rows, the minibatch snapshot (copy -> staging, published through the gate); the copy is free again
+    // after it
+    if (hipEventRecord(p->copy_written[copy], es) != hipSuccess || hipStreamWaitEvent(ss, p->copy_written[copy], 0) ||
+        (p->used[s] && hipStreamWaitEvent(ss, p->slot_free[s], 0) != hipSuccess))
+        return fail(-4, "flock_sc_pipeline_learn_copy: stream operation failed");
+    {  // the critic phase reads the slot's staging rows (identity index), the agent index from *u.agent
+        RowArgs& a = p->jc[s].a;
+        a.idx = u.idx;
+        a.rs = u.ring_state;
+        a.rs2 = u.ring_new_state;
+        a.ra = u.ring_action;
+        a.rr = u.ring_reward;
+        a.rt = u.ring_terminal;
+        a.rows = 0;
+        a.agent_val = -1;
+        a.gate = nullptr;
+    }
+    const FlockScRows& dst = p->staging[s];
+    int vec = u.in_dim == 4 && u.n_actions == 2;
+    for (const FlockScRows* x : {ring, &dst})
+        vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
+    const unsigned long long seq = ++p->seq;
+    hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, ss, u.B, rows, seed, counter,
+                       const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, *ring, dst, vec, p->gate, seq);
+    int rc = launched();
+    if (rc) return rc;
+    if (hipEventRecord(p->copy_read[copy], ss) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline_learn_copy: stream operation failed");
+    p->copy_used[copy] = true;
+    // learner stream: one polling wave for this snapshot's sequence number, then the rounds
+    return enqueue_rounds(p, ls, s, agent, true, true);
 }
 
 int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_offset,
@@ -2630,9 +2843,16 @@ int flock_sc_workspace_check(const FlockScUpdate* u) {
 
 int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate && !p->dp ? p->gate_mode : 0; }
 
+int flock_sc_pipeline_copy_ok(const FlockScPipeline* p) { return p && p->gate && !p->dp && !p->graphs ? 1 : 0; }
+
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;
     if (p->gate) (void)hipFree(p->gate);
+    if (p->snap_stream) (void)hipStreamDestroy(p->snap_stream);
+    for (int i = 0; i < kMaxSlots; ++i) {
+        if (p->copy_written[i]) (void)hipEventDestroy(p->copy_written[i]);
+        if (p->copy_read[i]) (void)hipEventDestroy(p->copy_read[i]);
+    }
     for (int i = 0; i < p->n; ++i) {
         hipGraphExec_t* gs[3] = {&p->merged[i], &p->conly[i], &p->aonly[i]};
         for (hipGraphExec_t* g : gs)

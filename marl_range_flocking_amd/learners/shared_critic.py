@@ -388,6 +388,7 @@ class SharedCriticLearner:
         """Agent.learn() of agent ``agent`` (agent_simple_shared_critic.py:115-155). Returns (actor_loss,
         critic_loss, True) as device tensors (no host sync), or (0, 0, False) before the buffer holds a batch."""
         B = self.batch_size
+        self.replay.bufs  # noqa: B018 (a loop with direct learns may have left the newest rows in a ring copy)
         if self.replay.counter < B:
             return 0, 0, False
         self._learn_calls += 1
@@ -435,6 +436,7 @@ class SharedCriticLearner:
         B = self.batch_size
         if not self.snapshot:
             raise RuntimeError("snapshot_into needs SharedCriticLearner(snapshot=True)")
+        self.replay.bufs  # noqa: B018 (see learn)
         if self.replay.counter < B:
             return False
         self._learn_calls += 1
@@ -514,6 +516,9 @@ class SharedCriticLearner:
         """Enqueue learn(agent) through the native pipeline (raw stream handles): the snapshot on env_stream, the
         round on learner_stream. The actor phase stays pending until the next call or pipeline_flush. Returns False
         (nothing enqueued) before the buffer holds a batch, like snapshot_into."""
+        if self.replay._pending is not None:  # (see learn) the copy-back runs on env_stream, before the snapshot
+            with torch.cuda.stream(torch.cuda.ExternalStream(int(env_stream), device=self.device)):
+                self.replay.bufs  # noqa: B018
         if self.replay.counter < self.batch_size:
             return False
         self._learn_calls += 1
@@ -610,7 +615,7 @@ class SharedCriticBench:
     """bench.py hook for BASELINE config 3: after each vectorized env step, insert every agent's transition into the
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
-    def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=3):
+    def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=None, buffer_size=1_000_000):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
@@ -618,8 +623,10 @@ class SharedCriticBench:
         # exploration), so step s+1 does not depend on learn(s) and every kernel still sees the same data
         # (with data-parallel replicas the update's two all-reduces run on the learner stream too)
         self.overlap = bool(overlap and fused)
+        if n_slots is None:  # staging slots (and ring copies of direct learns); FLOCK_SC_SLOTS: A/B
+            n_slots = int(os.environ.get("FLOCK_SC_SLOTS", "3"))
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
-                                           buffer_size=1_000_000, dist_group=group, fused=fused,
+                                           buffer_size=buffer_size, dist_group=group, fused=fused,
                                            snapshot=self.overlap, n_slots=n_slots)
         if self.overlap:
             # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
@@ -675,7 +682,32 @@ class SharedCriticBench:
             ring = [rb["state"], rb["action"], rb["reward"], rb["new_state"], rb["terminal"]]
             self._loop = torch.classes.flock.ScTrainLoop(e, ef, ei, ring, L.replay.counter, L.pipeline(), L.seed,
                                                          L._learn_calls)
+            self._copies = None
+            mode = self.ring_copy_mode()
+            if mode:
+                # physical copies of the ring, one written per env step (every step rewrites the whole ring):
+                # mode 2 (copy learns): 3 copies in turn, each learn's snapshot on the pipeline's own stream and the
+                # learner polling the device gate (flock_sc_pipeline_learn_copy); mode 1 (direct learns): one copy
+                # per pipeline slot, the critic phase samples its rows there (flock_sc_pipeline_learn_direct).
+                # Both bitwise the snapshot learns
+                n = L.n_slots if mode == 1 else 3
+                self._copies = [[torch.zeros_like(t) for t in ring] for _ in range(n)]
+                self._loop.set_copies([t for c in self._copies for t in c], mode)
         return self._loop
+
+    def ring_copy_mode(self):
+        """How the loop's learns get their minibatch: 0 the snapshot on the env stream (flock_sc_pipeline_learn),
+        1 direct learns, 2 copy learns (see loop()). 1 and 2 need every env step to rewrite the whole ring (E N >=
+        capacity, as at config 3: 1,048,576 transitions into a 1e6-row ring) and a single-GPU pipeline launching its
+        rounds directly; 2 also the device gate (not under counter collection). FLOCK_SC_RING_COPIES=0/1/2 (A/B)."""
+        L = self.learner
+        want = int(os.environ.get("FLOCK_SC_RING_COPIES", "0"))
+        if (want == 0 or L.distributed or os.environ.get("FLOCK_SC_PIPELINE_GRAPHS", "0") == "1"
+                or self.env.E * self.env.N < L.replay.capacity):
+            return 0
+        if want == 2 and not L.pipeline().copy_ok():
+            return 0
+        return want
 
     def can_loop(self):
         return (self.overlap and self.pipelined and self.learner.use_graph and self.env.cfg.variant == "v2")
@@ -695,7 +727,11 @@ class SharedCriticBench:
         lp.set_state(env._cur, L.replay.counter, L._learn_calls)
         lp.run(int(first), int(K), list(actions), torch.cuda.current_stream(env.device).cuda_stream,
                self.stream.cuda_stream, handles, int(ev_every))
-        parity, counter, calls = lp.state()
+        parity, counter, calls, last_copy = lp.state()
+        if last_copy >= 0:  # direct learns: the newest rows are in that ring copy (ReplayRing.bufs copies them back)
+            c = self._copies[last_copy]
+            L.replay.set_pending_copy({"state": c[0], "action": c[1], "reward": c[2], "new_state": c[3],
+                                       "terminal": c[4]})
         learns = calls - L._learn_calls
         for s in range(first + K - learns, first + K):
             L.count[s % L.n_agents] += 1
