@@ -38,10 +38,17 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // env rows per block: TM = 64 (two 32-row bands, 4 waves) or 128 (four bands, 8 waves: every fc2.weight chunk staged in
 // LDS is read by twice the rows, so the L2 -> LDS traffic per FLOP halves); FLOCK_ACT_TM picks it (default 64: the 128-row blocks measured 8% slower, 2.755 vs 2.553 ms)
+// k depth of an LDS-staged fc2.weight chunk (STG; a multiple of 8) and the waves per SIMD the register allocation must
+// allow (launch bounds). Round 4: 16-deep chunks (a 25.6-KB chunk buffer, 8 float4 of prefetch per thread) fit the block
+// in 168 VGPRs and ~41 KB of LDS, so THREE blocks share a CU (was 40-deep chunks, 245 VGPRs, two blocks): 2.49-2.51
+// against 2.55-2.56 ms per call (profiles/r04/act); 24-deep chunks at three waves spill (2.85 ms)
 #ifndef FLOCK_ACT_KC
-#define FLOCK_ACT_KC 40
+#define FLOCK_ACT_KC 16
 #endif
-constexpr int kKC = FLOCK_ACT_KC;  // k depth of an LDS-staged fc2.weight chunk (STG; a multiple of 8)
+constexpr int kKC = FLOCK_ACT_KC;
+#ifndef FLOCK_ACT_WAVES
+#define FLOCK_ACT_WAVES 3
+#endif
 
 struct ActArgs {
     const float* obs;     // [rows][A][in]
@@ -75,7 +82,7 @@ __device__ __forceinline__ float sum32(float v) {
 // NT: 32-column tiles per wave (each wave covers half of the padded fc2 width: fc2 <= 64 NT); INC: compile-time
 // observation width (0: runtime, <= 16)
 template <int NT, int INC, bool STG, int TM>
-__global__ __launch_bounds__(4 * TM, 2) void sc_act_kernel(ActArgs p) {
+__global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs p) {
     constexpr int NTH = 4 * TM;  // threads: 2 waves per 32-row band (the two column halves)
     extern __shared__ float4 smem4[];
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
