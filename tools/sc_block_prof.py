@@ -27,12 +27,16 @@ def build():
     subprocess.check_call([hipcc()] + HIPCC_FLAGS + ["-DFLOCK_SC_PROF", "-c", "-I", INCLUDE, "-o", obj,
                                                      os.path.join(CSRC, "flock_sc.hip")])
     subprocess.check_call([hipcc()] + HIPCC_FLAGS + ["-shared", "-o", SO, os.path.join(BUILD, "flock_env.hip.o"),
-                                                     os.path.join(BUILD, "flock_learn.hip.o"), obj])
+                                                     os.path.join(BUILD, "flock_learn.hip.o"),
+                                                     os.path.join(BUILD, "flock_act.hip.o"), obj])
     print(SO)
 
 
 def run(corun, learns):
-    os.environ["FLOCK_LIB"] = SO
+    # the learner launches through libflock_torch.so, which links _build/libflock_amd.so: run with the profiling
+    # build copied over it (SWAPPED=1; tools/gpu_scprof.sh), else through FLOCK_LIB (the ctypes paths only)
+    if os.environ.get("SWAPPED") != "1":
+        os.environ["FLOCK_LIB"] = SO
     sys.path.insert(0, ROOT)
     import numpy as np
     import torch
@@ -41,7 +45,7 @@ def run(corun, learns):
     from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
     lib = _native.lib()
-    assert lib._name == SO, lib._name
+    assert hasattr(lib, "flock_sc_prof_read"), "not the -DFLOCK_SC_PROF build: " + lib._name
     dev = torch.device("cuda", 0)
     E, N = 4096, 256
     env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=4, range_start=(0, 253),
