@@ -1164,7 +1164,13 @@ struct RedP {
     int64_t off;
 };
 constexpr int kMaxRed = 12;
-constexpr int kRedElems = 16;
+// output elements per reduction block; the block's 256 threads are kRedElems elements x kRedGroups row groups (group q
+// takes rows q, q + kRedGroups, ...). -DFLOCK_RED_ELEMS=8 / 4: more row groups, fewer rows per thread (A/B builds)
+#ifndef FLOCK_RED_ELEMS
+#define FLOCK_RED_ELEMS 16
+#endif
+constexpr int kRedElems = FLOCK_RED_ELEMS;
+constexpr int kRedGroups = 256 / kRedElems;
 constexpr int kMaxRedBlocks = 4096;
 
 // LN1 row statistics for modes 4 / 5, from the bwd launch's per-tile row sums
@@ -1173,7 +1179,8 @@ struct DzArgs {
     int F, ntn;
 };
 
-// One block's reduction: the 16-element slice of rp for block b (thread el = tid & 15, row group q = tid >> 4);
+// One block's reduction: the kRedElems-element slice of rp for block b (thread el = tid % kRedElems, row group
+// q = tid / kRedElems);
 // returns the sum in threads q == 0 (0 elsewhere). part: 256 floats of LDS; mst: [B][2] LDS (modes 4 / 5)
 // F (fused rounds): D and the row sums PS were written by the bwd blocks of the same launch: `sc1` loads
 template <bool F = false>
@@ -1181,7 +1188,7 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
                                            int& e_out, bool& live_out) {
     const int tid = threadIdx.x;
     const bool dzm = rp.mode == 4 || rp.mode == 5;
-    const int el = tid & (kRedElems - 1), q = tid >> 4;
+    const int el = tid & (kRedElems - 1), q = tid / kRedElems;
     const int e = (b - rp.blk0) * kRedElems + el;
     const bool live = e < rp.n;
     const bool per_in = rp.mode == 2 || rp.mode == 4;
@@ -1191,12 +1198,12 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
 #ifndef FLOCK_RED_RB
 #define FLOCK_RED_RB 8
 #endif
-    constexpr int kRB = FLOCK_RED_RB;  // rows per batch of loads (row group q takes rows q, q + 16, ...)
+    constexpr int kRB = FLOCK_RED_RB;  // rows per batch of loads (row group q takes rows q, q + kRedGroups, ...)
     float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
     auto load = [&](int r0) {
 #pragma unroll
         for (int k = 0; k < kRB; ++k) {
-            const int r = r0 + 16 * k;
+            const int r = r0 + kRedGroups * k;
             const bool in = live && r < B;
             dv[k] = in ? ld_in<F>(rp.D + (int64_t)r * rp.ldd + o) : 0.0f;
             xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
@@ -1230,12 +1237,12 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
         __syncthreads();
     }
     float acc = 0.0f;
-    for (int r0 = q; r0 < B; r0 += 16 * kRB) {
+    for (int r0 = q; r0 < B; r0 += kRedGroups * kRB) {
         if (r0 != q) load(r0);
         if (dzm) {
 #pragma unroll
             for (int k = 0; k < kRB; ++k) {
-                const int r = min(r0 + 16 * k, B - 1);
+                const int r = min(r0 + kRedGroups * k, B - 1);
                 dv[k] = rs[k] * (dv[k] - mst[2 * r] - xh[k] * mst[2 * r + 1]);  // ln_backward's dz
             }
         }
@@ -1247,7 +1254,7 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
     float gsum = 0.0f;
     if (q == 0 && live) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) gsum += part[k * kRedElems + el];
+        for (int k = 0; k < kRedGroups; ++k) gsum += part[k * kRedElems + el];
     }
     e_out = e;
     live_out = live && q == 0;
@@ -1490,7 +1497,7 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
             if (b >= ga.red[q].blk0) q0 = q;
         const RedP& rp = ga.red[q0];
         const int e1 = (b - rp.blk0) * kRedElems + (tid & (kRedElems - 1));
-        const bool ad = (tid >> 4) == 0 && e1 < rp.n && rp.mode != 3 && ga.do_adam;
+        const bool ad = tid / kRedElems == 0 && e1 < rp.n && rp.mode != 3 && ga.do_adam;
         const AdamState st = ad ? adam_load(ga, base + rp.off + e1) : AdamState{0.f, 0.f, 0.f, 0.f};
         int e;
         bool wr;
@@ -1748,10 +1755,10 @@ void add_red(J& ga, const float* D, int ldd, const float* X, int ldx, int mode, 
     r.blk0 = ga.nblk;
     ga.nblk += (n + kRedElems - 1) / kRedElems;
 }
-size_t red_lds(int B) { return (size_t)(16 * kRedElems + 2 * B) * sizeof(float); }  // part + LN1 row statistics
+size_t red_lds(int B) { return (size_t)(256 + 2 * B) * sizeof(float); }  // part + LN1 row statistics
 size_t bwd_lds(const BwdJob& j) {
     const size_t a = gemm_lds_bytes(j.dh.K, j.dh.kchunk), b = gemm_lds_bytes(j.dw.K, j.dw.kchunk);
-    const size_t r = 16 * kRedElems * sizeof(float);
+    const size_t r = 256 * sizeof(float);
     return a > b ? (a > r ? a : r) : (b > r ? b : r);
 }
 
