@@ -70,6 +70,35 @@ __device__ __forceinline__ float xor32(float v, int m) {  // lane l <- lane l ^ 
         default: return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (16 << 10) | 0x1F));
     }
 }
+// one step of a transposed reduction across the 32-lane half: v[0, 2H) -> v[0, H), lane l keeping the upper half
+// when (l & m) != 0 and adding its xor-m partner's copy of the half it keeps (H swizzles for 2H values)
+template <int H>
+__device__ __forceinline__ void tstep(float* v, int l, int m) {
+    const bool hi = (l & m) != 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        const float keep = hi ? v[i + H] : v[i];
+        const float send = hi ? v[i] : v[i + H];
+        v[i] = keep + xor32(send, m);
+    }
+}
+// the 32-lane sums of 16 values in 16 swizzles (16 separate butterflies take 80): afterwards v[0] of lane l holds the
+// sum of value (l >> 1) & 15 (lanes 2j and 2j + 1 alike)
+__device__ __forceinline__ void tsum32_16(float (&v)[16], int l) {
+    tstep<8>(v, l, 16);
+    tstep<4>(v, l, 8);
+    tstep<2>(v, l, 4);
+    tstep<1>(v, l, 2);
+    v[0] += xor32(v[0], 1);
+}
+// the same for 32 values in 31 swizzles: v[0] of lane l holds the sum of value l & 31
+__device__ __forceinline__ void tsum32_32(float (&v)[32], int l) {
+    tstep<16>(v, l, 16);
+    tstep<8>(v, l, 8);
+    tstep<4>(v, l, 4);
+    tstep<2>(v, l, 2);
+    tstep<1>(v, l, 1);
+}
 __device__ __forceinline__ float sum32(float v) {
     v += xor32(v, 16);
     v += xor32(v, 8);
@@ -298,6 +327,8 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
         wm1[t] = bv[t] ? WMU[H2 + col] : 0.0f;
     }
     auto row_of = [&](int v) { return 32 * band + 8 * (v >> 2) + 4 * (l >> 5) + (v & 3); };
+    // row sums over the lanes' 32 columns by transposed reductions (tsum32_*): lane l ends with the sum of one row
+    const int jr = (l >> 1) & 15;  // the accumulator row (v index) whose sum lane l holds after tsum32_16
     float red[16];
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
@@ -307,11 +338,10 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
             acc[t][v] = acc[t][v] + b2[t];
             s += bv[t] ? acc[t][v] : 0.0f;
         }
-        red[v] = sum32(s);
+        red[v] = s;
     }
-    if ((l & 31) == 0)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
+    tsum32_16(red, l);
+    if ((l & 1) == 0) sRed[row_of(jr) * 2 + half] = red[0];
     __syncthreads();
     // the LayerNorm-2 statistics once per row (64 threads), not per lane and accumulator row
     float* sStat = sMean;  // [64] mean, then [64] rstd in sRstd (LayerNorm-1's are no longer read)
@@ -328,15 +358,14 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
             const float d = acc[t][v] - mean[v];
             s += bv[t] ? d * d : 0.0f;
         }
-        red[v] = sum32(s);
+        red[v] = s;
     }
-    if ((l & 31) == 0)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) sRed[row_of(v) * 2 + half] = red[v];
+    tsum32_16(red, l);
+    if ((l & 1) == 0) sRed[row_of(jr) * 2 + half] = red[0];
     __syncthreads();
     if (tid < TM) sRstd[tid] = 1.0f / sqrtf((sRed[tid * 2] + sRed[tid * 2 + 1]) / (float)H2 + 1e-5f);
     __syncthreads();
-    float m0[16], m1[16];
+    float mm[32];  // [0, 16) the mu head's output 0 per accumulator row, [16, 32) output 1
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
         const float rstd = sRstd[row_of(v)];
@@ -347,16 +376,14 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
             s0 += h * wm0[t];
             s1 += h * wm1[t];
         }
-        m0[v] = sum32(s0);
-        m1[v] = sum32(s1);
+        mm[v] = s0;
+        mm[16 + v] = s1;
     }
-    if ((l & 31) == 0)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int r = row_of(v);
-            sMu[(r * 2 + half) * 2 + 0] = m0[v];
-            sMu[(r * 2 + half) * 2 + 1] = m1[v];
-        }
+    tsum32_32(mm, l);
+    {  // lane l holds value l & 31: output (l & 31) >> 4 of accumulator row l & 15
+        const int jv = l & 15, jo = (l >> 4) & 1;
+        sMu[(row_of(jv) * 2 + half) * 2 + jo] = mm[0];
+    }
     __syncthreads();
     if (tid < 2 * TM) {
         const int r = tid >> 1, j = tid & 1;
