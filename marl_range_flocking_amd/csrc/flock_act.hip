@@ -404,6 +404,238 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
     }
 }
 
+// The 16 x 16 variant (FLOCK_ACT_MFMA=16): one wave = 16 env rows x EVERY fc2 column, on v_mfma_f32_16x16x4_f32 (the
+// same f32 rate as 32x32x2). NT 16-column tiles cover fc2 <= 16 NT: 304 columns computed for the reference's 300
+// (1.3 % padding, against 6.7 % for the 32-column tiles). Lane l = (group g = l >> 4, row rl = l & 15) supplies the A
+// values of its row at k = k0 + 2g + s (s = 0, 1: the two MFMAs of an 8-deep k-step; 2 fc1 values per lane per step,
+// half the 32 x 32 kernel's) and reads each tile's B pair (k0 + 2g, k0 + 2g + 1) as one 8-B LDS read (conflict-free:
+// 20-float column pitch). The accumulators hold rows 4g + i (i < 4) of column 16t + rl, so a row's LayerNorm-2 sums
+// and its mu head stay inside one 16-lane group: xor butterflies / a transposed reduction, no LDS exchange and no
+// barrier in the epilogue. fc2's bias, LayerNorm-2 affine and mu rows are staged in LDS with the fc1 rows.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <int NT, int INC>
+__global__ __launch_bounds__(256, FLOCK_ACT_WAVES) void sc_act16_kernel(ActArgs p) {
+    constexpr int TM = 64, NTH = 256, NC = 16 * NT;
+    extern __shared__ float4 smem4[];
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+    const int IN = INC ? INC : p.in, INP = (IN + 3) & ~3, H1 = p.H1, H2 = p.H2;
+    const int W = p.A * p.tiles, b = blockIdx.x;
+    const int work = (W & 7) == 0 ? (b & 7) * (W >> 3) + (b >> 3) : b;
+    const int agent = work / p.tiles, tile = work - agent * p.tiles;
+    const int64_t r0 = (int64_t)tile * TM;
+    const float* P = p.actors + (int64_t)agent * p.stride;
+    const float* W1 = P;
+    const float* B1 = W1 + (int64_t)H1 * IN;
+    const float* G1 = B1 + H1;
+    const float* BE1 = G1 + H1;
+    const float* W2 = BE1 + H1;
+    const float* B2 = W2 + (int64_t)H2 * H1;
+    const float* G2 = B2 + H2;
+    const float* BE2 = G2 + H2;
+    const float* WMU = BE2 + H2;
+    const float* BMU = WMU + 2 * H2;
+
+    // LDS: fc1 rows [H1][INP], (b1, g1, be1, 0) [H1], observation rows [64][INP], LayerNorm-1 statistics [64] x 2,
+    // fc2 bias / LayerNorm-2 gamma, beta / mu rows 0, 1 [5][NC], the staged fc2.weight chunk [NC][kKC + 4]
+    float* sW1 = reinterpret_cast<float*>(smem4);
+    float4* sQ = reinterpret_cast<float4*>(sW1 + H1 * INP);
+    float* sX = reinterpret_cast<float*>(sQ + H1);
+    float* sMean = sX + TM * INP;
+    float* sRstd = sMean + TM;
+    float* sP2 = sRstd + TM;
+    float* sB = sP2 + 5 * NC;
+
+    for (int e = tid; e < H1 * INP; e += NTH) {
+        const int k = e / INP, i = e - k * INP;
+        sW1[e] = i < IN ? W1[k * IN + i] : 0.0f;
+    }
+    for (int k = tid; k < H1; k += NTH) sQ[k] = make_float4(B1[k], G1[k], BE1[k], 0.0f);
+    for (int e = tid; e < TM * INP; e += NTH) {
+        const int r = e / INP, i = e - r * INP;
+        const int64_t gr = r0 + r;
+        sX[e] = (i < IN && gr < p.rows) ? p.obs[(gr * p.A + agent) * IN + i] : 0.0f;
+    }
+    for (int c = tid; c < NC; c += NTH) {  // zero past fc2: padded columns add nothing anywhere
+        const bool v = c < H2;
+        sP2[c] = v ? B2[c] : 0.0f;
+        sP2[NC + c] = v ? G2[c] : 0.0f;
+        sP2[2 * NC + c] = v ? BE2[c] : 0.0f;
+        sP2[3 * NC + c] = v ? WMU[c] : 0.0f;
+        sP2[4 * NC + c] = v ? WMU[H2 + c] : 0.0f;
+    }
+    __syncthreads();
+    auto fc1 = [&](const float* x, int k) {
+        const float* wk = sW1 + k * INP;
+        float d = sQ[k].x;
+        if (INC == 4) {
+            const float4 w4 = *reinterpret_cast<const float4*>(wk);
+            d = fmaf(x[0], w4.x, d);
+            d = fmaf(x[1], w4.y, d);
+            d = fmaf(x[2], w4.z, d);
+            d = fmaf(x[3], w4.w, d);
+        } else {
+            for (int i = 0; i < IN; ++i) d = fmaf(x[i], wk[i], d);
+        }
+        return d;
+    };
+    const int g = l >> 4, rl = l & 15, ra = 16 * w + rl;
+    {  // LayerNorm-1 statistics: 4 threads per row, one shifted pass (as sc_act_kernel; computing fc1 on the MFMA
+       // here instead, two passes over the 16-column tiles, measured slower: 2.53-2.54 against 2.42-2.44 ms)
+        const int r = tid >> 2, q = tid & 3;
+        float x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = i < IN ? sX[r * INP + i] : 0.0f;
+        const float c = fc1(x, 0);
+        float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 8
+        for (int k = q; k < H1; k += 4) {
+            const float d = fc1(x, k) - c;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+        }
+        s1 += __shfl_xor(s1, 1);
+        s1 += __shfl_xor(s1, 2);
+        s2 += __shfl_xor(s2, 1);
+        s2 += __shfl_xor(s2, 2);
+        if (q == 0) {
+            const float dm = s1 / (float)H1;
+            sMean[r] = c + dm;
+            sRstd[r] = 1.0f / sqrtf(fmaxf(s2 / (float)H1 - dm * dm, 0.0f) + 1e-5f);
+        }
+    }
+    __syncthreads();
+
+    float xr[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) xr[i] = i < IN ? sX[ra * INP + i] : 0.0f;
+    const float sr = sRstd[ra], nmr = -sMean[ra] * sr;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[t][i] = 0.0f;
+    auto a_vals = [&](int k0, float (&a)[2]) {  // this lane's row at k0 + 2g + s
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int k = k0 + 2 * g + s;
+            const float4 q = sQ[k];
+            const float y = fmaf(fc1(xr, k), sr, nmr);
+            a[s] = fmaxf(fmaf(y, q.y, q.z), 0.0f);
+        }
+    };
+    constexpr int kPer = (NC * kKC / 4 + NTH - 1) / NTH;  // float4 per thread per chunk
+    float4 pf[kPer];
+    auto fetch = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int f = tid + NTH * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+            pf[i] = (col < H2 && k0 + kq < H1) ? *reinterpret_cast<const float4*>(W2 + (int64_t)col * H1 + k0 + kq)
+                                               : make_float4(0, 0, 0, 0);
+        }
+    };
+    fetch(0);
+    float a[2];
+    a_vals(0, a);
+    for (int k0 = 0; k0 < H1; k0 += kKC) {
+        __syncthreads();  // the previous chunk's pairs have been read
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            const int f = tid + NTH * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+            if (col < NC) *reinterpret_cast<float4*>(sB + col * (kKC + 4) + kq) = pf[i];
+        }
+        __syncthreads();
+        if (k0 + kKC < H1) fetch(k0 + kKC);
+        const int kc = H1 - k0 < kKC ? H1 - k0 : kKC;
+        for (int ks = 0; ks < kc; ks += 8) {
+            float an[2];
+            const int kn = k0 + ks + 8;
+            a_vals(kn < H1 ? kn : 0, an);
+            const float* bcol = sB + rl * (kKC + 4) + ks + 2 * g;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * (kKC + 4));
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb.x, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb.y, acc[t], 0, 0, 0);
+            }
+            a[0] = an[0];
+            a[1] = an[1];
+        }
+    }
+
+    // epilogue: acc[t][i] = fc2 output of row 16 w + 4 g + i, column 16 t + rl (before the bias)
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = 16 * t + rl;
+        const bool v = col < H2;
+        const float b2 = sP2[col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc[t][i] = acc[t][i] + b2;
+            s[i] += v ? acc[t][i] : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[i] += xor32(s[i], m);  // the 16-lane sums, in every lane of the group
+    float mean[4], var[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mean[i] = s[i] / (float)H2;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const bool v = 16 * t + rl < H2;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float d = acc[t][i] - mean[i];
+            var[i] += v ? d * d : 0.0f;
+        }
+    }
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) var[i] += xor32(var[i], m);
+    float rstd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rstd[i] = 1.0f / sqrtf(var[i] / (float)H2 + 1e-5f);
+    float mm[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // [i] mu output 0 of row i, [4 + i] output 1
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int col = 16 * t + rl;
+        const float g2 = sP2[NC + col], be2 = sP2[2 * NC + col], w0 = sP2[3 * NC + col], w1 = sP2[4 * NC + col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float h = fmaxf((acc[t][i] - mean[i]) * rstd[i] * g2 + be2, 0.0f);
+            mm[i] += h * w0;
+            mm[4 + i] += h * w1;
+        }
+    }
+    // transposed reduction over the 16-lane group: lanes 2j, 2j + 1 end with value j = ((rl >> 3) & 1) 4 +
+    // ((rl >> 2) & 1) 2 + ((rl >> 1) & 1)
+    tstep<4>(mm, l, 8);
+    tstep<2>(mm, l, 4);
+    tstep<1>(mm, l, 2);
+    mm[0] += xor32(mm[0], 1);
+    if ((l & 1) == 0) {
+        const int jv = (((rl >> 3) & 1) << 2) | (((rl >> 2) & 1) << 1) | ((rl >> 1) & 1);
+        const int j = jv >> 2, row = 16 * w + 4 * g + (jv & 3);
+        const int64_t gr = r0 + row;
+        if (gr < p.rows) {
+            const float mu = tanhf(mm[0] + BMU[j]);
+            const int64_t e = (gr * p.A + agent) * 2 + j;
+            if (p.ou) {  // shared_critic.py choose_action: ou + theta * (0 - ou) * dt + (sigma sqrt(dt)) * z
+                const float o = p.ou[e];
+                const float drift = __fmul_rn(__fmul_rn(p.theta, __fsub_rn(0.0f, o)), p.dt);
+                const float on = __fadd_rn(__fadd_rn(o, drift), __fmul_rn(p.c, p.noise[e]));
+                p.ou[e] = on;
+                p.actions[e] = __fadd_rn(mu, on);
+            } else {
+                p.actions[e] = mu;
+            }
+        }
+    }
+}
+
 template <int NT, int INC, int TM>
 int launch_act(hipStream_t st, const ActArgs& a, size_t lds, bool stage) {
     if (stage && lds + sizeof(float) * 64 * NT * (kKC + 4) <= 64 * 1024) {
@@ -412,6 +644,17 @@ int launch_act(hipStream_t st, const ActArgs& a, size_t lds, bool stage) {
     } else {
         hipLaunchKernelGGL((sc_act_kernel<NT, INC, false, TM>), dim3(a.A * a.tiles), dim3(4 * TM), lds, st, a);
     }
+    return launched();
+}
+
+// the 16 x 16 kernel (NT 16-column tiles; in_dim 4, the LDS staging path, 64-row blocks)
+template <int NT>
+int launch_act16(hipStream_t st, ActArgs a) {
+    a.tiles = (int)((a.rows + 63) / 64);
+    const size_t lds = sizeof(float) * ((size_t)a.H1 * 4 + 4 * (size_t)a.H1 + 64 * 4 + 2 * 64 + 5 * 16 * NT +
+                                        (size_t)16 * NT * (kKC + 4));
+    if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
+    hipLaunchKernelGGL((sc_act16_kernel<NT, 4>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
     return launched();
 }
 
@@ -465,6 +708,18 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
         const char* e = getenv("FLOCK_ACT_STAGE");
         return e ? e[0] == '1' : true;
     }();
+    static const int mfma = [] {  // FLOCK_ACT_MFMA=16 / 32: the 16 x 16 kernel (default) or the 32 x 32 one (A/B)
+        const char* e = getenv("FLOCK_ACT_MFMA");
+        return e && atoi(e) == 32 ? 32 : 16;
+    }();
+    if (in_dim == 4 && mfma == 16 && stage && tm == 64) {
+        switch ((fc2 + 15) / 16) {  // the widths with an instantiation; others take the 32 x 32 kernel
+            case 7: return launch_act16<7>(st, a);
+            case 19: return launch_act16<19>(st, a);
+            case 20: return launch_act16<20>(st, a);
+            default: break;
+        }
+    }
     if (in_dim == 4) {
         switch (nt) {
             case 1: return launch_act_tm<1, 4>(st, a, inp, stage, tm);

@@ -15,6 +15,7 @@ WIDTHS = [  # (n_agents, rows, in_dim, fc1, fc2)
     (5, 7, 4, 16, 8),
     (3, 65, 3, 64, 100),     # runtime observation width, fc2 not a multiple of 32
     (9, 64, 6, 48, 257),
+    (4, 130, 4, 64, 100),    # in_dim 4, fc2 100: the 16 x 16 kernel's seven-tile instantiation
 ]
 
 
