@@ -101,6 +101,12 @@ def parse():
                          "driver (choose_action of every agent + OU noise -> env.step + insert -> learn(), "
                          "learners/maddpg_shared_critic/train_flock.py:114-121) after the headline, reported in the "
                          "policy_in_loop field (0: skip)")
+    ap.add_argument("--diag-presleep-us", type=float, default=0.0,
+                    help="diagnostics only (never a bench line): a sleep kernel of this length opens the timed region "
+                         "so the host enqueues ahead of the GPU; the line then reports it in diag_presleep_ms")
+    ap.add_argument("--diag-prewarm-ms", type=float, default=0.0,
+                    help="diagnostics only (never a bench line): keep the GPU busy with matmuls for this long before "
+                         "the warmup steps (clock / power-state probe)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
                          "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
@@ -481,6 +487,15 @@ def main():
             hook.after(s, a)
 
     stream = torch.cuda.current_stream(dev)
+    if args.diag_prewarm_ms > 0:
+        xw = torch.rand(4096, 4096, device=dev)
+        torch.cuda.synchronize(dev)
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < args.diag_prewarm_ms * 1e-3:
+            for _ in range(4):
+                xw = torch.tanh(xw @ xw * 1e-3)
+            torch.cuda.synchronize(dev)
+        del xw
     use_loop = bool(args.loop) and hook is not None and getattr(hook, "can_loop", lambda: False)()
     if use_loop:
         hook.run_steps(0, args.warmup, pool)
@@ -505,6 +520,8 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     span[0].record(stream)  # the GPU-side span of the timed region (its first to its last enqueued command)
+    if args.diag_presleep_us > 0:
+        torch.cuda._sleep(int(args.diag_presleep_us * 1e-6 * 2.1e9))  # ~2.1 GHz shader clock under load
     if use_loop:
         hook.run_steps(args.warmup, args.steps, pool, evs, EV_EVERY)
     else:
@@ -604,6 +621,8 @@ def main():
         # HIP events at the start and the end of the timed region on the launch stream: the GPU-side span, i.e.
         # ms_per_step without the launch latency of the first command and the final synchronisation
         "gpu_span_ms_per_step": span[0].elapsed_time(span[1]) / args.steps,
+        **({"diag_presleep_us": args.diag_presleep_us} if args.diag_presleep_us > 0 else {}),
+        **({"diag_prewarm_ms": args.diag_prewarm_ms} if args.diag_prewarm_ms > 0 else {}),
         "host_enqueue_us_per_step": host_us,
         "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
                       "one Python step per vectorized step (torch.ops.flock)"),
