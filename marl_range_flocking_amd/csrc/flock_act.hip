@@ -49,6 +49,16 @@ constexpr int kKC = FLOCK_ACT_KC;
 #ifndef FLOCK_ACT_WAVES
 #define FLOCK_ACT_WAVES 3
 #endif
+// the same two knobs for the 16 x 16 kernel (sc_act16_kernel): 8-deep chunks (one k-step per staged chunk, a 14.6-KB
+// chunk buffer, ~35 KB of LDS per block) let FOUR blocks share a CU: 2.33-2.35 against 2.41-2.44 ms per call for 16-deep
+// chunks at three (0.69-0.70 of the f32 MFMA peak; profiles/r04/act16_kc/); 24-deep chunks at two: 2.70-2.72 ms
+#ifndef FLOCK_ACT16_KC
+#define FLOCK_ACT16_KC 8
+#endif
+constexpr int kKC16 = FLOCK_ACT16_KC;
+#ifndef FLOCK_ACT16_WAVES
+#define FLOCK_ACT16_WAVES 4
+#endif
 
 struct ActArgs {
     const float* obs;     // [rows][A][in]
@@ -408,13 +418,13 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
 // same f32 rate as 32x32x2). NT 16-column tiles cover fc2 <= 16 NT: 304 columns computed for the reference's 300
 // (1.3 % padding, against 6.7 % for the 32-column tiles). Lane l = (group g = l >> 4, row rl = l & 15) supplies the A
 // values of its row at k = k0 + 2g + s (s = 0, 1: the two MFMAs of an 8-deep k-step; 2 fc1 values per lane per step,
-// half the 32 x 32 kernel's) and reads each tile's B pair (k0 + 2g, k0 + 2g + 1) as one 8-B LDS read (conflict-free:
-// 20-float column pitch). The accumulators hold rows 4g + i (i < 4) of column 16t + rl, so a row's LayerNorm-2 sums
+// half the 32 x 32 kernel's) and reads each tile's B pair (k0 + 2g, k0 + 2g + 1) as one 8-B LDS read (column pitch
+// kKC16 + 4 floats). The accumulators hold rows 4g + i (i < 4) of column 16t + rl, so a row's LayerNorm-2 sums
 // and its mu head stay inside one 16-lane group: xor butterflies / a transposed reduction, no LDS exchange and no
 // barrier in the epilogue. fc2's bias, LayerNorm-2 affine and mu rows are staged in LDS with the fc1 rows.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <int NT, int INC>
-__global__ __launch_bounds__(256, FLOCK_ACT_WAVES) void sc_act16_kernel(ActArgs p) {
+__global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArgs p) {
     constexpr int TM = 64, NTH = 256, NC = 16 * NT;
     extern __shared__ float4 smem4[];
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(256, FLOCK_ACT_WAVES) void sc_act16_kernel(ActArgs 
     const float* BMU = WMU + 2 * H2;
 
     // LDS: fc1 rows [H1][INP], (b1, g1, be1, 0) [H1], observation rows [64][INP], LayerNorm-1 statistics [64] x 2,
-    // fc2 bias / LayerNorm-2 gamma, beta / mu rows 0, 1 [5][NC], the staged fc2.weight chunk [NC][kKC + 4]
+    // fc2 bias / LayerNorm-2 gamma, beta / mu rows 0, 1 [5][NC], the staged fc2.weight chunk [NC][kKC16 + 4]
     float* sW1 = reinterpret_cast<float*>(smem4);
     float4* sQ = reinterpret_cast<float4*>(sW1 + H1 * INP);
     float* sX = reinterpret_cast<float*>(sQ + H1);
@@ -523,12 +533,12 @@ __global__ __launch_bounds__(256, FLOCK_ACT_WAVES) void sc_act16_kernel(ActArgs 
             a[s] = fmaxf(fmaf(y, q.y, q.z), 0.0f);
         }
     };
-    constexpr int kPer = (NC * kKC / 4 + NTH - 1) / NTH;  // float4 per thread per chunk
+    constexpr int kPer = (NC * kKC16 / 4 + NTH - 1) / NTH;  // float4 per thread per chunk
     float4 pf[kPer];
     auto fetch = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
-            const int f = tid + NTH * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
+            const int f = tid + NTH * i, col = f / (kKC16 / 4), kq = 4 * (f % (kKC16 / 4));
             pf[i] = (col < H2 && k0 + kq < H1) ? *reinterpret_cast<const float4*>(W2 + (int64_t)col * H1 + k0 + kq)
                                                : make_float4(0, 0, 0, 0);
         }
@@ -536,24 +546,24 @@ __global__ __launch_bounds__(256, FLOCK_ACT_WAVES) void sc_act16_kernel(ActArgs 
     fetch(0);
     float a[2];
     a_vals(0, a);
-    for (int k0 = 0; k0 < H1; k0 += kKC) {
+    for (int k0 = 0; k0 < H1; k0 += kKC16) {
         __syncthreads();  // the previous chunk's pairs have been read
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
-            const int f = tid + NTH * i, col = f / (kKC / 4), kq = 4 * (f % (kKC / 4));
-            if (col < NC) *reinterpret_cast<float4*>(sB + col * (kKC + 4) + kq) = pf[i];
+            const int f = tid + NTH * i, col = f / (kKC16 / 4), kq = 4 * (f % (kKC16 / 4));
+            if (col < NC) *reinterpret_cast<float4*>(sB + col * (kKC16 + 4) + kq) = pf[i];
         }
         __syncthreads();
-        if (k0 + kKC < H1) fetch(k0 + kKC);
-        const int kc = H1 - k0 < kKC ? H1 - k0 : kKC;
+        if (k0 + kKC16 < H1) fetch(k0 + kKC16);
+        const int kc = H1 - k0 < kKC16 ? H1 - k0 : kKC16;
         for (int ks = 0; ks < kc; ks += 8) {
             float an[2];
             const int kn = k0 + ks + 8;
             a_vals(kn < H1 ? kn : 0, an);
-            const float* bcol = sB + rl * (kKC + 4) + ks + 2 * g;
+            const float* bcol = sB + rl * (kKC16 + 4) + ks + 2 * g;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * (kKC + 4));
+                const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * (kKC16 + 4));
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb.x, acc[t], 0, 0, 0);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb.y, acc[t], 0, 0, 0);
             }
@@ -652,7 +662,7 @@ template <int NT>
 int launch_act16(hipStream_t st, ActArgs a) {
     a.tiles = (int)((a.rows + 63) / 64);
     const size_t lds = sizeof(float) * ((size_t)a.H1 * 4 + 4 * (size_t)a.H1 + 64 * 4 + 2 * 64 + 5 * 16 * NT +
-                                        (size_t)16 * NT * (kKC + 4));
+                                        (size_t)16 * NT * (kKC16 + 4));
     if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
     hipLaunchKernelGGL((sc_act16_kernel<NT, 4>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
     return launched();

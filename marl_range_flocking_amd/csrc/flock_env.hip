@@ -68,6 +68,7 @@ int fail(int code, const char* msg) {
 struct Params {
     int E, N, k, G, S, P, ib;
     int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
+    int pf_ahead;  // > 0: each block pulls the kinematics inputs of block blockIdx.x + pf_ahead into L2 (see step_kernel)
     int launches;  // FlockStepExt.launches: the step as this many launches over env ranges (0: the diagnostics knob)
     int variant, periodic, rigid, clamp;
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
@@ -865,13 +866,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     int* pre_all = cnt_all + (CELL ? p.G * ncell : 0);
     int* wtot_all = pre_all + (CELL ? p.G * npre : 0);  // [G][16] per-wave totals of the binning scan
 
-    const int t = threadIdx.x;
-    const int g = t / p.N;
-    const int i = t - g * p.N;
-    const int env = p.env0 + blockIdx.x * p.G + g;
-    const bool in_group = g < p.G;
-    const bool active = in_group && env < p.E;
-    const size_t a = (size_t)env * p.N + i;
     const int variant = p.variant;
 #ifdef FLOCK_PHASE_PROF
     unsigned long long ph_acc[24];
@@ -879,8 +873,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     for (int q_ = 0; q_ < 24; ++q_) ph_acc[q_] = 0;
     unsigned long long t_prev = __builtin_amdgcn_s_memtime();
     const unsigned long long st0_ = t_prev, rt0_ = __builtin_amdgcn_s_memrealtime();  // in-kernel clock
-    PHASE_COUNT(20, 1);
 #endif
+    const int t = threadIdx.x;
+    const int g = t / p.N;
+    const int i = t - g * p.N;
+    const bool in_group = g < p.G;
+    PHASE_COUNT(20, 1);
+    const int env = p.env0 + blockIdx.x * p.G + g;
+    const bool active = in_group && env < p.E;
+    const size_t a = (size_t)env * p.N + i;
 #ifdef FLOCK_STAGGER  // diagnostics: offset the phases of the first-round blocks sharing a CU (b, b + 256, ...)
     if (blockIdx.x < 2048) {
         const int m = (blockIdx.x >> 8) & 7;
@@ -1074,6 +1075,34 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         lpos[g * p.S + i] = make_float2(x, y);
     }
     if (kLateAfter) load_late();
+    // L2 pull-ahead (pf_ahead > 0: more env blocks than are resident, launch_spec): the block that will take this
+    // one's place on the CU is pf_ahead blocks later; one lane per 128 B pulls its positions, headings and actions
+    // into the caches (one dword each, kept in a register that is only consumed at the end), issued after this
+    // block's own loads so that no wait for them waits for the pull. Config 5: 0.807 -> 0.760 ms per launch; config 3
+    // as one launch (4096 blocks, 2048 resident): 39.0-39.2 -> 37.2-37.8 µs (profiles/r04/pf/)
+    int pf_sink = 0;
+    const bool pf_on = p.pf_ahead > 0;
+    if (pf_on) {
+        const int eb = p.env0 + (int)(blockIdx.x + p.pf_ahead) * p.G;
+        const int ne = min(p.G, p.E - eb);
+        if (ne > 0) {
+            const int nb = ne * p.N;             // agents of that block
+            const int l8 = (nb * 8 + 127) >> 7;  // lines of the 8-B fields, of the heading
+            const int l4 = (nb * 4 + 127) >> 7;
+            const char* base = nullptr;
+            int q = t;
+            if (q < l8) {
+                base = reinterpret_cast<const char*>(p.pos) + (size_t)eb * p.N * 8;
+            } else if ((q -= l8) < l4) {
+                base = reinterpret_cast<const char*>(p.heading) + (size_t)eb * p.N * 4;
+            } else if ((q -= l4) < l8) {
+                base = variant == FLOCK_VARIANT_UW_DISCRETE ? reinterpret_cast<const char*>(p.action_id)
+                                                             : reinterpret_cast<const char*>(p.action);
+                if (base) base += (size_t)eb * p.N * 8;
+            }
+            if (base) pf_sink = *reinterpret_cast<const int*>(base + (size_t)q * 128);
+        }
+    }
 
     PHASE(0);
     // ---- phase 2: per-env sums in a fixed tree order (same order as oracle tree_sum) -------------------------
@@ -1424,11 +1453,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 int64_t row = p.r_start + r_unit - p.r_skip;
                 if (row >= p.r_cap) row -= p.r_cap;
                 const int64_t e = row * p.r_group + r_slot;  // this agent's element of the row
-                if (L - 2 == 4 && p.k == 4 && !p.r_astate && !p.r_anew) {  // 16-B stores
-                    st_ring(reinterpret_cast<f32x4*>(p.r_state + e * p.k),
-                         f32x4{prev_obs[0], prev_obs[1 % (L - 2)], prev_obs[2 % (L - 2)], prev_obs[3 % (L - 2)]});
-                    st_ring(reinterpret_cast<f32x4*>(p.r_new + e * p.k),
-                         f32x4{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]});
+                if (L - 2 == 4 && p.k == 4) {  // 16-B stores (the RNN-MADDPG ring's actor copies too)
+                    const f32x4 so{prev_obs[0], prev_obs[1 % (L - 2)], prev_obs[2 % (L - 2)], prev_obs[3 % (L - 2)]};
+                    const f32x4 sn{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]};
+                    st_ring(reinterpret_cast<f32x4*>(p.r_state + e * p.k), so);
+                    st_ring(reinterpret_cast<f32x4*>(p.r_new + e * p.k), sn);
+                    if (p.r_astate) st_ring(reinterpret_cast<f32x4*>(p.r_astate + e * p.k), so);
+                    if (p.r_anew) st_ring(reinterpret_cast<f32x4*>(p.r_anew + e * p.k), sn);
                 } else {
 #pragma unroll
                     for (int s = 0; s < L - 2; ++s)
@@ -1475,6 +1506,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
     }
     PHASE(7);
+    if (pf_on) asm volatile("" ::"v"(pf_sink));  // the L2 pull completes before the wave ends
     PHASE_FLUSH();
 }
 
@@ -1680,6 +1712,8 @@ int check_common(int E, int N, int k) {
 struct Knobs {
     int env_launches;
     bool no_spec, no_split, no_cells;
+    int pf;  // FLOCK_ENV_PF: the env blocks' L2 pull-ahead (step_kernel): -1 (default) where launch_spec enables it,
+             // 0 off, 1 on for every specialised one-launch step, 2 also across the launches of a multi-launch step
     int lds_pad;  // FLOCK_ENV_LDS_PAD: extra dynamic LDS bytes per step block (caps the blocks per CU; A/B only)
 };
 Knobs& knobs_mut() {
@@ -1687,7 +1721,8 @@ Knobs& knobs_mut() {
         const char* e = getenv("FLOCK_ENV_LAUNCHES");
         const char* lp = getenv("FLOCK_ENV_LDS_PAD");
         return Knobs{e ? atoi(e) : 1, getenv("FLOCK_NO_SPEC") != nullptr, getenv("FLOCK_NO_SPLIT") != nullptr,
-                     getenv("FLOCK_NO_CELLS") != nullptr, lp ? atoi(lp) : 0};
+                     getenv("FLOCK_NO_CELLS") != nullptr,
+                     getenv("FLOCK_ENV_PF") ? atoi(getenv("FLOCK_ENV_PF")) : -1, lp ? atoi(lp) : 0};
     }();
     return k;
 }
@@ -1698,7 +1733,17 @@ int env_launches(int blocks, int requested) {
 }
 
 // the specialised instantiations (step_kernel VAR / NC / SPL): the BASELINE configurations' per-GPU shapes
-template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1>
+// resident blocks of a kernel on the current device (occupancy at T threads and lds bytes per block); 0 on error
+int resident_blocks(const void* kernel, int T, size_t lds) {
+    int dev = 0, per_cu = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, T, lds) != hipSuccess)
+        return 0;
+    return per_cu * cus;
+}
+
+template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1, bool PF = false>
 bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL ||
         p.normalize)
@@ -1714,6 +1759,19 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         c.lds = ((c.lds + 15) & ~(size_t)15) + (size_t)(SPL - 1) * 6 * NC * sizeof(uint32_t);
     }
     const int parts = env_launches(c.blocks, p.launches);
+    const int pfk = knobs().pf;
+    if (parts <= 1 && (pfk > 0 || (pfk < 0 && PF))) {  // each block pulls a later block's inputs into L2
+        auto* kern = step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>;
+        static int pf_lds = -1, pf_res = 0;  // per instantiation (the LDS size is fixed by NC, GXC, GYC)
+        if (pf_lds != (int)c.lds) {
+            pf_res = resident_blocks(reinterpret_cast<const void*>(kern), c.T, c.lds);
+            pf_lds = (int)c.lds;
+        }
+        Params q = p;
+        q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? pf_res : 0;
+        hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(c.T), c.lds, s, q);
+        return true;
+    }
     if (parts <= 1) {
         hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks), dim3(c.T), c.lds, s,
                            p);
@@ -1724,6 +1782,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
+        q.pf_ahead = (pfk == 2 && b0 + per < c.blocks) ? per : 0;  // A/B: pull the next launch's inputs
         hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
                            dim3(c.T), c.lds, s, q);
     }
@@ -1733,8 +1792,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
 template <int L>
 void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
     if constexpr (L == 6) {
-        if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6>(c, p, s)) return;         // config 3
-        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12>(c, p, s)) return;       // config 5
+        if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6, 1, true>(c, p, s)) return;  // config 3 (+ L2 pull)
+        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12, 1, true>(c, p, s)) return;  // config 5 (+ L2 pull)
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
         if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
     }
@@ -1841,6 +1900,8 @@ int flock_set_diag(const char* name, int value) {
         k.no_split = value != 0;
     else if (!strcmp(name, "no_cells"))
         k.no_cells = value != 0;
+    else if (!strcmp(name, "pf"))
+        k.pf = value;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
     else if (!strcmp(name, "sc_no_fuse"))
@@ -1897,6 +1958,10 @@ int set_ring(Params& p, const FlockRing* ring, int E, int N, const char* who) {
     const int64_t units = ring->group == 1 ? (int64_t)E * N : (int64_t)E;
     if (ring->skip < 0 || units - ring->skip > ring->capacity || ring->start < 0 || ring->start >= ring->capacity)
         return bad(FLOCK_E_ARG, "need skip >= 0, rows - skip <= capacity, 0 <= start < capacity");
+    auto a16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };  // k = 4: the observation rows move as 16 B
+    if (E && p.k == 4 && !(a16(ring->state) && a16(ring->new_state) && a16(ring->prev_obs) &&
+                           a16(ring->actor_state) && a16(ring->actor_new_state)))
+        return bad(FLOCK_E_ARG, "k = 4 ring observation fields must be 16-B aligned");
     p.r_state = ring->state;
     p.r_action = ring->action;
     p.r_reward = ring->reward;

@@ -352,3 +352,41 @@ def test_step_launches_are_bitwise_one_launch(variant, periodic, N, kind, cuda):
                          "idx": env.nn_idx.clone(), "rew": rew.clone(), "done": done.clone(), "any": anyd.clone()})
         for key in outs[0]:
             assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+
+
+@pytest.mark.parametrize("N,E", [(1024, 1100), (256, 2600)], ids=["config5-shape", "config3-shape"])
+@pytest.mark.parametrize("kind", ["uniform", "clustered"])
+def test_l2_pull_ahead_is_bitwise_the_plain_launch(kind, N, E, cuda):
+    """Config 5's and config 3's shapes (v2, N = 1024 / 256, periodic) as one launch of more env blocks than fit on
+    the device at once: each block then pulls the kinematics inputs of the block pf_ahead places later into the
+    caches (pf = -1, the default there); pf = 0 launches the plain blocks. E above the resident blocks (512 / 2048;
+    the last blocks pull nothing) with the RNN-MADDPG record insert (one ring row per env, the actor copies as 16-B
+    stores): three steps agree bit for bit on every output, the seed buffer and every replay field."""
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+    k = 4
+    box = float(round(np.sqrt(250 * N)))
+    rng = np.random.default_rng(11)
+    pos = _positions(kind, E, N, box, rng).astype(np.float32)
+    head = rng.uniform(0, 2 * np.pi, (E, N)).astype(np.float32)
+    envs, learners = [], []
+    for _ in range(2):
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, periodic=True), device=cuda)
+        env.set_state(positions=pos, headings=head)
+        envs.append(env)
+        learners.append(MADDPGLearner(N, k, recurrent=True, hidden1=8, hidden2=8, batch_size=8, chunk_size=4,
+                                      buffer_capacity=1500, min_size_buffer=8, device=cuda, use_graph=False))
+    for t in range(3):
+        act = torch.from_numpy(rng.uniform(-1.0, 2.5, (E, N, 2)).astype(np.float32)).to(cuda)
+        outs = []
+        for i, (env, L) in enumerate(zip(envs, learners)):
+            with diag("pf", -1 if i == 0 else 0, default=-1):
+                obs, rew, (done, anyd), _ = env.step(act, ring=L.replay_slots(E))
+                torch.cuda.synchronize()
+            outs.append({"pos": env.positions, "vel": env.velocities, "head": env.headings, "dnn": env.dnn,
+                         "idx": env.nn_idx, "rew": rew, "done": done, "any": anyd, "seeds": env.seeds.clone()})
+        for key in outs[0]:
+            assert torch.equal(outs[0][key], outs[1][key]), f"step {t}: {key}"
+    for name in learners[0].replay.bufs:
+        assert torch.equal(learners[0].replay.bufs[name], learners[1].replay.bufs[name]), name
