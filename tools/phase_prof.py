@@ -34,7 +34,7 @@ def build():
                                                      os.path.join(b, "flock_sc.hip.o")])
 
 
-def run(E, N, k, steps, variant="v2", seeds=False):
+def run(E, N, k, steps, variant="v2", seeds=False, windows=0):
     import numpy as np
     import torch
 
@@ -101,6 +101,19 @@ def run(E, N, k, steps, variant="v2", seeds=False):
     torch.cuda.synchronize()
     buf = (ctypes.c_ulonglong * 32)()
     lib.flock_phase_read(buf)
+    for w in range(windows):  # drift probe: kernel time and in-kernel clock per window of `steps` steps
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        lib.flock_phase_read(buf)
+        waves = buf[20]
+        print(f"window {w:3d}: {e0.elapsed_time(e1) / steps * 1e3:6.1f} us/launch, clock "
+              f"{buf[19] / max(buf[23], 1) * 0.1:.2f} GHz, wave lifetime {buf[23] / waves * 0.01:.2f} us, "
+              f"kinematics {buf[0] / waves:.0f} scan {buf[3] / waves:.0f} binning {buf[2] / waves:.0f} cycles/wave, "
+              f"rescan {buf[18] / waves:.5f}", flush=True)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(steps):
@@ -158,8 +171,9 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uwd"])
     ap.add_argument("--seeds", action="store_true", help="v2 through flock_step_v2_ext with a seed buffer")
+    ap.add_argument("--windows", type=int, default=0, help="first time this many windows of --steps steps (drift)")
     a = ap.parse_args()
     if a.build:
         build()
     else:
-        run(a.E, a.N, a.k, a.steps, a.variant, a.seeds)
+        run(a.E, a.N, a.k, a.steps, a.variant, a.seeds, a.windows)
