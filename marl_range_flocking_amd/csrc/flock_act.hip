@@ -56,6 +56,20 @@ constexpr int kKC = FLOCK_ACT_KC;
 #define FLOCK_ACT16_KC 8
 #endif
 constexpr int kKC16 = FLOCK_ACT16_KC;
+// column pitch of the staged chunk, 2 mod 4 floats: the compiler pairs two tiles' 8-B B reads into ds_read2_b64, whose
+// 16-lane groups bank on 32 dwords; rl * pitch then puts the 16 rows' pairs on 32 distinct banks (a pitch of KC + 4
+// put rows rl and rl + 8 on one bank pair: 2-way conflicts on every B read)
+#ifndef FLOCK_ACT16_PITCH
+#define FLOCK_ACT16_PITCH (FLOCK_ACT16_KC + 2)
+#endif
+constexpr int kBP16 = FLOCK_ACT16_PITCH;
+// FLOCK_ACT16_DB=1: two chunk buffers, one barrier per chunk (the next chunk is stored into the other buffer after
+// this chunk's MFMAs); fc2's bias / LayerNorm-2 / mu rows are then read from global memory in the epilogue instead of
+// LDS, so four blocks still share a CU
+#ifndef FLOCK_ACT16_DB
+#define FLOCK_ACT16_DB 0
+#endif
+constexpr bool kDB16 = FLOCK_ACT16_DB != 0;
 #ifndef FLOCK_ACT16_WAVES
 #define FLOCK_ACT16_WAVES 4
 #endif
@@ -419,7 +433,7 @@ __global__ __launch_bounds__(4 * TM, FLOCK_ACT_WAVES) void sc_act_kernel(ActArgs
 // (1.3 % padding, against 6.7 % for the 32-column tiles). Lane l = (group g = l >> 4, row rl = l & 15) supplies the A
 // values of its row at k = k0 + 2g + s (s = 0, 1: the two MFMAs of an 8-deep k-step; 2 fc1 values per lane per step,
 // half the 32 x 32 kernel's) and reads each tile's B pair (k0 + 2g, k0 + 2g + 1) as one 8-B LDS read (column pitch
-// kKC16 + 4 floats). The accumulators hold rows 4g + i (i < 4) of column 16t + rl, so a row's LayerNorm-2 sums
+// kBP16 floats, 2 mod 4: conflict-free when two tiles' reads pair into ds_read2_b64). The accumulators hold rows 4g + i (i < 4) of column 16t + rl, so a row's LayerNorm-2 sums
 // and its mu head stay inside one 16-lane group: xor butterflies / a transposed reduction, no LDS exchange and no
 // barrier in the epilogue. fc2's bias, LayerNorm-2 affine and mu rows are staged in LDS with the fc1 rows.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -446,14 +460,20 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
     const float* BMU = WMU + 2 * H2;
 
     // LDS: fc1 rows [H1][INP], (b1, g1, be1, 0) [H1], observation rows [64][INP], LayerNorm-1 statistics [64] x 2,
-    // fc2 bias / LayerNorm-2 gamma, beta / mu rows 0, 1 [5][NC], the staged fc2.weight chunk [NC][kKC16 + 4]
+    // fc2 bias / LayerNorm-2 gamma, beta / mu rows 0, 1 [5][NC], the staged fc2.weight chunk [NC][kBP16]
     float* sW1 = reinterpret_cast<float*>(smem4);
     float4* sQ = reinterpret_cast<float4*>(sW1 + H1 * INP);
     float* sX = reinterpret_cast<float*>(sQ + H1);
     float* sMean = sX + TM * INP;
     float* sRstd = sMean + TM;
     float* sP2 = sRstd + TM;
-    float* sB = sP2 + 5 * NC;
+    float* sB = kDB16 ? sP2 : sP2 + 5 * NC;  // kDB16: [2][NC][kBP16], no sP2
+    // fc2 bias, LayerNorm-2 gamma / beta, mu rows 0 / 1 at column col (zero past fc2: padded columns add nothing)
+    auto p2 = [&](int j, int col) {
+        if (!kDB16) return sP2[j * NC + col];
+        const float* src = j == 0 ? B2 : j == 1 ? G2 : j == 2 ? BE2 : j == 3 ? WMU : WMU + H2;
+        return col < H2 ? src[col] : 0.0f;
+    };
 
     for (int e = tid; e < H1 * INP; e += NTH) {
         const int k = e / INP, i = e - k * INP;
@@ -465,7 +485,7 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
         const int64_t gr = r0 + r;
         sX[e] = (i < IN && gr < p.rows) ? p.obs[(gr * p.A + agent) * IN + i] : 0.0f;
     }
-    for (int c = tid; c < NC; c += NTH) {  // zero past fc2: padded columns add nothing anywhere
+    for (int c = tid; c < (kDB16 ? 0 : NC); c += NTH) {  // zero past fc2: padded columns add nothing anywhere
         const bool v = c < H2;
         sP2[c] = v ? B2[c] : 0.0f;
         sP2[NC + c] = v ? G2[c] : 0.0f;
@@ -543,32 +563,56 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
                                                : make_float4(0, 0, 0, 0);
         }
     };
-    fetch(0);
-    float a[2];
-    a_vals(0, a);
-    for (int k0 = 0; k0 < H1; k0 += kKC16) {
-        __syncthreads();  // the previous chunk's pairs have been read
+    auto stage = [&](float* buf) {
 #pragma unroll
         for (int i = 0; i < kPer; ++i) {
             const int f = tid + NTH * i, col = f / (kKC16 / 4), kq = 4 * (f % (kKC16 / 4));
-            if (col < NC) *reinterpret_cast<float4*>(sB + col * (kKC16 + 4) + kq) = pf[i];
+            if (col < NC) {  // two 8-B stores (the pitch keeps rows 8-B, not 16-B, aligned)
+                float2* dst = reinterpret_cast<float2*>(buf + col * kBP16 + kq);
+                dst[0] = make_float2(pf[i].x, pf[i].y);
+                dst[1] = make_float2(pf[i].z, pf[i].w);
+            }
         }
+    };
+    fetch(0);
+    float a[2];
+    a_vals(0, a);
+    if (kDB16) {
+        stage(sB);
+        if (kKC16 < H1) fetch(kKC16);
         __syncthreads();
-        if (k0 + kKC16 < H1) fetch(k0 + kKC16);
+    }
+    int cur = 0;
+    for (int k0 = 0; k0 < H1; k0 += kKC16) {
+        if (!kDB16) {
+            __syncthreads();  // the previous chunk's pairs have been read
+            stage(sB);
+            __syncthreads();
+            if (k0 + kKC16 < H1) fetch(k0 + kKC16);
+        }
+        const float* bufc = sB + cur * NC * kBP16;
         const int kc = H1 - k0 < kKC16 ? H1 - k0 : kKC16;
         for (int ks = 0; ks < kc; ks += 8) {
             float an[2];
             const int kn = k0 + ks + 8;
             a_vals(kn < H1 ? kn : 0, an);
-            const float* bcol = sB + rl * (kKC16 + 4) + ks + 2 * g;
+            const float* bcol = bufc + rl * kBP16 + ks + 2 * g;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * (kKC16 + 4));
+                const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * kBP16);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb.x, acc[t], 0, 0, 0);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb.y, acc[t], 0, 0, 0);
             }
             a[0] = an[0];
             a[1] = an[1];
+        }
+        if (kDB16) {  // the next chunk into the other buffer (read by every wave before the previous barrier)
+            if (k0 + kKC16 < H1) {
+                stage(sB + (cur ^ 1) * NC * kBP16);
+                if (k0 + 2 * kKC16 < H1) fetch(k0 + 2 * kKC16);
+            }
+            __syncthreads();
+            cur ^= 1;
         }
     }
 
@@ -578,7 +622,7 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
     for (int t = 0; t < NT; ++t) {
         const int col = 16 * t + rl;
         const bool v = col < H2;
-        const float b2 = sP2[col];
+        const float b2 = p2(0, col);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             acc[t][i] = acc[t][i] + b2;
@@ -612,7 +656,7 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const int col = 16 * t + rl;
-        const float g2 = sP2[NC + col], be2 = sP2[2 * NC + col], w0 = sP2[3 * NC + col], w1 = sP2[4 * NC + col];
+        const float g2 = p2(1, col), be2 = p2(2, col), w0 = p2(3, col), w1 = p2(4, col);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const float h = fmaxf((acc[t][i] - mean[i]) * rstd[i] * g2 + be2, 0.0f);
@@ -661,8 +705,8 @@ int launch_act(hipStream_t st, const ActArgs& a, size_t lds, bool stage) {
 template <int NT>
 int launch_act16(hipStream_t st, ActArgs a) {
     a.tiles = (int)((a.rows + 63) / 64);
-    const size_t lds = sizeof(float) * ((size_t)a.H1 * 4 + 4 * (size_t)a.H1 + 64 * 4 + 2 * 64 + 5 * 16 * NT +
-                                        (size_t)16 * NT * (kKC16 + 4));
+    const size_t lds = sizeof(float) * ((size_t)a.H1 * 4 + 4 * (size_t)a.H1 + 64 * 4 + 2 * 64 +
+                                        (kDB16 ? (size_t)2 * 16 * NT * kBP16 : 5 * 16 * NT + (size_t)16 * NT * kBP16));
     if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
     hipLaunchKernelGGL((sc_act16_kernel<NT, 4>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
     return launched();
