@@ -63,13 +63,6 @@ constexpr int kKC16 = FLOCK_ACT16_KC;
 #define FLOCK_ACT16_PITCH (FLOCK_ACT16_KC + 2)
 #endif
 constexpr int kBP16 = FLOCK_ACT16_PITCH;
-// FLOCK_ACT16_DB=1: two chunk buffers, one barrier per chunk (the next chunk is stored into the other buffer after
-// this chunk's MFMAs); fc2's bias / LayerNorm-2 / mu rows are then read from global memory in the epilogue instead of
-// LDS, so four blocks still share a CU
-#ifndef FLOCK_ACT16_DB
-#define FLOCK_ACT16_DB 0
-#endif
-constexpr bool kDB16 = FLOCK_ACT16_DB != 0;
 #ifndef FLOCK_ACT16_WAVES
 #define FLOCK_ACT16_WAVES 4
 #endif
@@ -467,13 +460,8 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
     float* sMean = sX + TM * INP;
     float* sRstd = sMean + TM;
     float* sP2 = sRstd + TM;
-    float* sB = kDB16 ? sP2 : sP2 + 5 * NC;  // kDB16: [2][NC][kBP16], no sP2
-    // fc2 bias, LayerNorm-2 gamma / beta, mu rows 0 / 1 at column col (zero past fc2: padded columns add nothing)
-    auto p2 = [&](int j, int col) {
-        if (!kDB16) return sP2[j * NC + col];
-        const float* src = j == 0 ? B2 : j == 1 ? G2 : j == 2 ? BE2 : j == 3 ? WMU : WMU + H2;
-        return col < H2 ? src[col] : 0.0f;
-    };
+    float* sB = sP2 + 5 * NC;
+    auto p2 = [&](int j, int col) { return sP2[j * NC + col]; };  // bias, LN-2 gamma / beta, mu rows 0 / 1
 
     for (int e = tid; e < H1 * INP; e += NTH) {
         const int k = e / INP, i = e - k * INP;
@@ -485,7 +473,7 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
         const int64_t gr = r0 + r;
         sX[e] = (i < IN && gr < p.rows) ? p.obs[(gr * p.A + agent) * IN + i] : 0.0f;
     }
-    for (int c = tid; c < (kDB16 ? 0 : NC); c += NTH) {  // zero past fc2: padded columns add nothing anywhere
+    for (int c = tid; c < NC; c += NTH) {  // zero past fc2: padded columns add nothing anywhere
         const bool v = c < H2;
         sP2[c] = v ? B2[c] : 0.0f;
         sP2[NC + c] = v ? G2[c] : 0.0f;
@@ -577,26 +565,19 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
     fetch(0);
     float a[2];
     a_vals(0, a);
-    if (kDB16) {
-        stage(sB);
-        if (kKC16 < H1) fetch(kKC16);
-        __syncthreads();
-    }
-    int cur = 0;
+    // (two chunk buffers with one barrier per chunk, fc2's row parameters then read from global memory to keep four
+    // blocks per CU, measured slower: 2.36-2.38 against 2.30-2.31 ms, profiles/r04/act16_kc/db_ab.txt)
     for (int k0 = 0; k0 < H1; k0 += kKC16) {
-        if (!kDB16) {
-            __syncthreads();  // the previous chunk's pairs have been read
-            stage(sB);
-            __syncthreads();
-            if (k0 + kKC16 < H1) fetch(k0 + kKC16);
-        }
-        const float* bufc = sB + cur * NC * kBP16;
+        __syncthreads();  // the previous chunk's pairs have been read
+        stage(sB);
+        __syncthreads();
+        if (k0 + kKC16 < H1) fetch(k0 + kKC16);
         const int kc = H1 - k0 < kKC16 ? H1 - k0 : kKC16;
         for (int ks = 0; ks < kc; ks += 8) {
             float an[2];
             const int kn = k0 + ks + 8;
             a_vals(kn < H1 ? kn : 0, an);
-            const float* bcol = bufc + rl * kBP16 + ks + 2 * g;
+            const float* bcol = sB + rl * kBP16 + ks + 2 * g;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * kBP16);
@@ -605,14 +586,6 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
             }
             a[0] = an[0];
             a[1] = an[1];
-        }
-        if (kDB16) {  // the next chunk into the other buffer (read by every wave before the previous barrier)
-            if (k0 + kKC16 < H1) {
-                stage(sB + (cur ^ 1) * NC * kBP16);
-                if (k0 + 2 * kKC16 < H1) fetch(k0 + 2 * kKC16);
-            }
-            __syncthreads();
-            cur ^= 1;
         }
     }
 
@@ -706,7 +679,7 @@ template <int NT>
 int launch_act16(hipStream_t st, ActArgs a) {
     a.tiles = (int)((a.rows + 63) / 64);
     const size_t lds = sizeof(float) * ((size_t)a.H1 * 4 + 4 * (size_t)a.H1 + 64 * 4 + 2 * 64 +
-                                        (kDB16 ? (size_t)2 * 16 * NT * kBP16 : 5 * 16 * NT + (size_t)16 * NT * kBP16));
+                                        5 * 16 * NT + (size_t)16 * NT * kBP16);
     if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
     hipLaunchKernelGGL((sc_act16_kernel<NT, 4>), dim3(a.A * a.tiles), dim3(256), lds, st, a);
     return launched();
