@@ -69,6 +69,7 @@ struct Params {
     int E, N, k, G, S, P, ib;
     int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
     int pf_ahead;  // > 0: each block pulls the kinematics inputs of block blockIdx.x + pf_ahead into L2 (see step_kernel)
+    int pf_late;   // with pf_ahead: also that block's late inputs (compact seeds, the fused insert's previous observation)
     int launches;  // FlockStepExt.launches: the step as this many launches over env ranges (0: the diagnostics knob)
     int variant, periodic, rigid, clamp;
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
@@ -1078,8 +1079,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     // L2 pull-ahead (pf_ahead > 0: more env blocks than are resident, launch_spec): the block that will take this
     // one's place on the CU is pf_ahead blocks later; one lane per 128 B pulls its positions, headings and actions
     // into the caches (one dword each, kept in a register that is only consumed at the end), issued after this
-    // block's own loads so that no wait for them waits for the pull. Config 5: 0.807 -> 0.760 ms per launch; config 3
-    // as one launch (4096 blocks, 2048 resident): 39.0-39.2 -> 37.2-37.8 µs (profiles/r04/pf/)
+    // block's own loads so that no wait for them waits for the pull. Config 5: 0.807 -> 0.760 ms per launch, 0.687 with
+    // the late inputs too (pf_late); config 3 as one launch (4096 blocks, 2048 resident): 39.0-39.2 -> 37.2-37.8 µs
+    // (the late inputs there: 38.7-39.7 µs, not pulled) (profiles/r04/pf/)
     int pf_sink = 0;
     const bool pf_on = p.pf_ahead > 0;
     if (pf_on) {
@@ -1099,6 +1101,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 base = variant == FLOCK_VARIANT_UW_DISCRETE ? reinterpret_cast<const char*>(p.action_id)
                                                              : reinterpret_cast<const char*>(p.action);
                 if (base) base += (size_t)eb * p.N * 8;
+            } else if ((q -= l8) < (p.pf_late && p.seeds && p.k == 4 ? l8 : 0)) {  // pf_late: the compact seeds,
+                base = reinterpret_cast<const char*>(p.seeds) + (size_t)eb * p.N * 8;
+            } else if ((q -= (p.pf_late && p.seeds && p.k == 4 ? l8 : 0)) <
+                       (p.pf_late && p.r_state && p.k == 4 ? 2 * l8 : 0)) {  // the previous observation rows
+                base = reinterpret_cast<const char*>(p.r_prev) + (size_t)eb * p.N * 16;
             }
             if (base) pf_sink = *reinterpret_cast<const int*>(base + (size_t)q * 128);
         }
@@ -1712,8 +1719,8 @@ int check_common(int E, int N, int k) {
 struct Knobs {
     int env_launches;
     bool no_spec, no_split, no_cells;
-    int pf;  // FLOCK_ENV_PF: the env blocks' L2 pull-ahead (step_kernel): -1 (default) where launch_spec enables it,
-             // 0 off, 1 on for every specialised one-launch step, 2 also across the launches of a multi-launch step
+    int pf;  // FLOCK_ENV_PF: the env blocks' L2 pull-ahead (step_kernel), bits: 1 the kinematics inputs, 2 also the
+             // late inputs, 4 across the launches of a multi-launch step (A/B); -1 (default): launch_spec's PF
     int lds_pad;  // FLOCK_ENV_LDS_PAD: extra dynamic LDS bytes per step block (caps the blocks per CU; A/B only)
 };
 Knobs& knobs_mut() {
@@ -1743,7 +1750,7 @@ int resident_blocks(const void* kernel, int T, size_t lds) {
     return per_cu * cus;
 }
 
-template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1, bool PF = false>
+template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1, int PF = 0>
 bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL ||
         p.normalize)
@@ -1759,8 +1766,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         c.lds = ((c.lds + 15) & ~(size_t)15) + (size_t)(SPL - 1) * 6 * NC * sizeof(uint32_t);
     }
     const int parts = env_launches(c.blocks, p.launches);
-    const int pfk = knobs().pf;
-    if (parts <= 1 && (pfk > 0 || (pfk < 0 && PF))) {  // each block pulls a later block's inputs into L2
+    const int pfk = knobs().pf >= 0 ? knobs().pf : PF;
+    if (parts <= 1 && (pfk & 1)) {  // each block pulls a later block's inputs into L2
         auto* kern = step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>;
         static int pf_lds = -1, pf_res = 0;  // per instantiation (the LDS size is fixed by NC, GXC, GYC)
         if (pf_lds != (int)c.lds) {
@@ -1769,6 +1776,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         }
         Params q = p;
         q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? pf_res : 0;
+        q.pf_late = (pfk & 2) != 0;
         hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(c.T), c.lds, s, q);
         return true;
     }
@@ -1782,7 +1790,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
-        q.pf_ahead = (pfk == 2 && b0 + per < c.blocks) ? per : 0;  // A/B: pull the next launch's inputs
+        q.pf_ahead = ((pfk & 4) && b0 + per < c.blocks) ? per : 0;  // A/B: pull the next launch's inputs
+        q.pf_late = (pfk & 2) != 0;
         hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
                            dim3(c.T), c.lds, s, q);
     }
@@ -1792,8 +1801,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
 template <int L>
 void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
     if constexpr (L == 6) {
-        if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6, 1, true>(c, p, s)) return;  // config 3 (+ L2 pull)
-        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12, 1, true>(c, p, s)) return;  // config 5 (+ L2 pull)
+        if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6, 1, 1>(c, p, s)) return;  // config 3 (+ L2 pull)
+        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12, 1, 3>(c, p, s)) return;  // config 5 (+ L2 pull, late)
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
         if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
     }
