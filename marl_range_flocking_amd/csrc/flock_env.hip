@@ -997,6 +997,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             act_in = make_float2(ac.x, ac.y);
             const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
             h = __fadd_rn(ldnt(p.heading + a), __fmul_rn(ang, p.dt));        // :329
+#ifdef FLOCK_PHASE_PROF  // diagnostics: the kinematics inputs' arrival (phase 9) apart from the rest of phase 0
+            asm volatile("s_waitcnt vmcnt(0)" ::"v"(h), "v"(x) : "memory");
+            PHASE(9);
+#endif
             const float lin = clamp_t(ac.x, p.v_min, p.v_max);               // :331
             float sn, cs;
             sincosf(h, &sn, &cs);                                            // ocml: the sinf / cosf bits
