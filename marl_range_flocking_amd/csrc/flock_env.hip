@@ -896,6 +896,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
+#ifdef FLOCK_LATE_KIN_STORES  // A/B: v2's position / heading / velocity stores with the other outputs (phase 5)
+    constexpr bool kLateKinStores = VAR == FLOCK_VARIANT_V2;
+#else
+    constexpr bool kLateKinStores = false;
+#endif
+    float kin_vx = 0.0f, kin_vy = 0.0f;
     float2 act_in = make_float2(0.0f, 0.0f);  // fused replay insert: the raw action (v2) or the f32 action id
     float prev_obs[L - 2];  // fused replay insert: the previous observation row, loaded early (latency hidden)
 #pragma unroll
@@ -1010,8 +1016,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             vy = __fmul_rn(nan_to_num(vy), p.dt);
             x = __fadd_rn(x, vx);                                            // :350
             y = __fadd_rn(y, vy);
-            stnt(p.heading + a, h);
-            stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
+            if (!kLateKinStores) {
+                stnt(p.heading + a, h);
+                stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
+            } else {
+                kin_vx = vx;
+                kin_vy = vy;
+            }
         } else if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:269-302 (heading=False)
             const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
             const float n = sqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
@@ -1075,11 +1086,17 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (variant != kSense) {
             x = boundary(x, p.box, p.rigid);  // check_boundary :271-304
             y = boundary(y, p.box, p.rigid);
-            stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
+            if (!(kLateKinStores && variant == FLOCK_VARIANT_V2)) stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
         }
         lpos[g * p.S + i] = make_float2(x, y);
     }
+#ifdef FLOCK_PHASE_PROF
+    PHASE(10);  // kinematics arithmetic and stores issued
+#endif
     if (kLateAfter) load_late();
+#ifdef FLOCK_PHASE_PROF
+    PHASE(11);  // late loads issued
+#endif
     // L2 pull-ahead (pf_ahead > 0: more env blocks than are resident, launch_spec): the block that will take this
     // one's place on the CU is pf_ahead blocks later; one lane per 128 B pulls its positions, headings and actions
     // into the caches (one dword each, kept in a register that is only consumed at the end), issued after this
@@ -1387,6 +1404,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
     int coll = 0;
+    if (kLateKinStores && active) {
+        stnt(p.heading + a, h);
+        stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{kin_vx, kin_vy});
+        stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
+    }
     if (active) {
         float dv[L - 1];
 #pragma unroll

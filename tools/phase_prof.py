@@ -122,14 +122,14 @@ def run(E, N, k, steps, variant="v2", seeds=False, windows=0):
     torch.cuda.synchronize()
     lib.flock_phase_read(buf)
     waves = buf[20]
-    tot = sum(buf[i] for i in range(8)) + buf[9]
+    tot = sum(buf[i] for i in range(8)) + buf[9] + buf[10] + buf[11]
     print(f"E={E} N={N} k={k}: kernel {e0.elapsed_time(e1) / steps * 1e3:.1f} us/launch, waves/launch "
           f"{waves / steps:.0f}")
     for i, n in enumerate(NAMES):
         print(f"  {n:20s} {buf[i] / waves:9.0f} cycles/wave  {100.0 * buf[i] / tot:5.1f} %")
-    if buf[9]:  # v2: phase 0 split at the kinematics inputs' arrival
-        print(f"    (of the kinematics: inputs arrived after {buf[9] / waves:.0f} cycles/wave, "
-              f"the rest {buf[0] / waves:.0f})")
+    if buf[9]:  # v2: phase 0 split at the kinematics inputs' arrival, the stores, the late loads
+        print(f"    (of the kinematics: inputs arrived after {buf[9] / waves:.0f} cycles/wave, arithmetic + stores "
+              f"{buf[10] / waves:.0f}, late loads issued {buf[11] / waves:.0f}, pull issued {buf[0] / waves:.0f})")
     print(f"  waves taking 5x5: {buf[16] / waves:.4f}, full scan: {buf[17] / waves:.5f}, "
           f"ambiguous rescan: {buf[18] / waves:.5f}")
     print(f"  cell-scan pair iterations per wave: {buf[21] / waves:.1f} over {buf[22] / waves:.2f} row ranges")
