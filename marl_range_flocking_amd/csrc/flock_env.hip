@@ -68,8 +68,7 @@ int fail(int code, const char* msg) {
 struct Params {
     int E, N, k, G, S, P, ib;
     int env0;  // first env of this launch (a step split into several launches; 0 otherwise)
-    int pf_ahead;  // > 0: each block pulls the kinematics inputs of block blockIdx.x + pf_ahead into L2 (see step_kernel)
-    int pf_late;   // with pf_ahead: also that block's late inputs (compact seeds, the fused insert's previous observation)
+    int pf_ahead;  // > 0: each block pulls the inputs of block blockIdx.x + pf_ahead into L2 (step_kernel's PFM)
     int launches;  // FlockStepExt.launches: the step as this many launches over env ranges (0: the diagnostics knob)
     int variant, periodic, rigid, clamp;
     float box, sensor_range, cd, dt, v_min, v_max, noise_std, com_r;
@@ -836,7 +835,7 @@ constexpr int clog2c(int n) {
 // candidates [q N / SPL, (q + 1) N / SPL) for agent (t mod N), and the agents' lanes merge the SPL partial top-L
 // key lists through LDS (the same key set, hence the same result, as the one-lane scan). At N = 64 this gives 4x the
 // waves of one lane per agent, where one wave per SIMD left every latency exposed.
-template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1>
+template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1, int PFM = 0>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params pin) {
     static_assert(SPL == 1 || (NC > 0 && !CELL && (NC % (2 * SPL)) == 0), "split scans: specialised N, no cells");
     Params p = pin;
@@ -1101,10 +1100,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     // one's place on the CU is pf_ahead blocks later; one lane per 128 B pulls its positions, headings and actions
     // into the caches (one dword each, kept in a register that is only consumed at the end), issued after this
     // block's own loads so that no wait for them waits for the pull. Config 5: 0.807 -> 0.760 ms per launch, 0.687 with
-    // the late inputs too (pf_late); config 3 as one launch (4096 blocks, 2048 resident): 39.0-39.2 -> 37.2-37.8 µs
+    // the late inputs too (PFM 3); config 3 as one launch (4096 blocks, 2048 resident): 39.0-39.2 -> 37.2-37.8 µs
     // (the late inputs there: 38.7-39.7 µs, not pulled) (profiles/r04/pf/)
     int pf_sink = 0;
-    const bool pf_on = p.pf_ahead > 0;
+    const bool pf_on = PFM != 0 && p.pf_ahead > 0;  // PFM: 1 the kinematics inputs, 3 also the late inputs
     if (pf_on) {
         const int eb = p.env0 + (int)(blockIdx.x + p.pf_ahead) * p.G;
         const int ne = min(p.G, p.E - eb);
@@ -1122,10 +1121,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 base = variant == FLOCK_VARIANT_UW_DISCRETE ? reinterpret_cast<const char*>(p.action_id)
                                                              : reinterpret_cast<const char*>(p.action);
                 if (base) base += (size_t)eb * p.N * 8;
-            } else if ((q -= l8) < (p.pf_late && p.seeds && p.k == 4 ? l8 : 0)) {  // pf_late: the compact seeds,
+            } else if ((q -= l8) < ((PFM & 2) && p.seeds && p.k == 4 ? l8 : 0)) {  // PFM & 2: the compact seeds,
                 base = reinterpret_cast<const char*>(p.seeds) + (size_t)eb * p.N * 8;
-            } else if ((q -= (p.pf_late && p.seeds && p.k == 4 ? l8 : 0)) <
-                       (p.pf_late && p.r_state && p.k == 4 ? 2 * l8 : 0)) {  // the previous observation rows
+            } else if ((q -= ((PFM & 2) && p.seeds && p.k == 4 ? l8 : 0)) <
+                       ((PFM & 2) && p.r_state && p.k == 4 ? 2 * l8 : 0)) {  // the previous observation rows
                 base = reinterpret_cast<const char*>(p.r_prev) + (size_t)eb * p.N * 16;
             }
             if (base) pf_sink = *reinterpret_cast<const int*>(base + (size_t)q * 128);
@@ -1745,8 +1744,8 @@ int check_common(int E, int N, int k) {
 struct Knobs {
     int env_launches;
     bool no_spec, no_split, no_cells;
-    int pf;  // FLOCK_ENV_PF: the env blocks' L2 pull-ahead (step_kernel), bits: 1 the kinematics inputs, 2 also the
-             // late inputs, 4 across the launches of a multi-launch step (A/B); -1 (default): launch_spec's PF
+    int pf;  // FLOCK_ENV_PF: the env blocks' L2 pull-ahead (step_kernel's PFM) where launch_spec has one: -1 (default)
+             // on, 0 off (A/B; the pull is compiled only into the shapes that use it)
     int lds_pad;  // FLOCK_ENV_LDS_PAD: extra dynamic LDS bytes per step block (caps the blocks per CU; A/B only)
 };
 Knobs& knobs_mut() {
@@ -1792,9 +1791,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         c.lds = ((c.lds + 15) & ~(size_t)15) + (size_t)(SPL - 1) * 6 * NC * sizeof(uint32_t);
     }
     const int parts = env_launches(c.blocks, p.launches);
-    const int pfk = knobs().pf >= 0 ? knobs().pf : PF;
-    if (parts <= 1 && (pfk & 1)) {  // each block pulls a later block's inputs into L2
-        auto* kern = step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>;
+    if (PF != 0 && parts <= 1 && knobs().pf != 0) {  // each block pulls a later block's inputs into L2
+        auto* kern = step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, PF>;
         static int pf_lds = -1, pf_res = 0;  // per instantiation (the LDS size is fixed by NC, GXC, GYC)
         if (pf_lds != (int)c.lds) {
             pf_res = resident_blocks(reinterpret_cast<const void*>(kern), c.T, c.lds);
@@ -1802,7 +1800,6 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         }
         Params q = p;
         q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? pf_res : 0;
-        q.pf_late = (pfk & 2) != 0;
         hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(c.T), c.lds, s, q);
         return true;
     }
@@ -1816,8 +1813,6 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
-        q.pf_ahead = ((pfk & 4) && b0 + per < c.blocks) ? per : 0;  // A/B: pull the next launch's inputs
-        q.pf_late = (pfk & 2) != 0;
         hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
                            dim3(c.T), c.lds, s, q);
     }
