@@ -55,9 +55,10 @@ int flock_abi_version(void);
 const char* flock_last_error(void);
 /* Diagnostics (A/B tests and tools only; the defaults are the product paths): "env_launches" (n launches over env
  * ranges per step), "no_spec" (generic step instantiations), "no_split" (one lane per agent in the split-scan
- * instantiations), "no_cells" (full scans instead of the cell list), "sc_no_spec" (generic shared-critic row kernels
- * at fc 400/300). The env knobs are initialised once from FLOCK_ENV_LAUNCHES, FLOCK_NO_SPEC, FLOCK_NO_SPLIT,
- * FLOCK_NO_CELLS; not thread-safe against concurrent launches. */
+ * instantiations), "no_cells" (full scans instead of the cell list), "pf" (-1 default / 0 off: the env blocks' L2
+ * pull-ahead of a later block's inputs in the shapes compiled with it), "sc_no_spec" (generic shared-critic row
+ * kernels at fc 400/300). The env knobs are initialised once from FLOCK_ENV_LAUNCHES, FLOCK_NO_SPEC, FLOCK_NO_SPLIT,
+ * FLOCK_NO_CELLS, FLOCK_ENV_PF; not thread-safe against concurrent launches. */
 int flock_set_diag(const char* name, int value);
 
 /* gym_flock_v2 step: pos (rw), heading (rw), action [lin, ang] → vel, dnn, nn_idx, reward, done, any_done. */
