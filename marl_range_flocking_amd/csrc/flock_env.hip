@@ -1799,7 +1799,11 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
             pf_lds = (int)c.lds;
         }
         Params q = p;
-        q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? pf_res : 0;
+        static const int gen = [] {  // FLOCK_ENV_PF_GEN (A/B): pull that many block generations ahead (default 1)
+            const char* e = getenv("FLOCK_ENV_PF_GEN");
+            return e && atoi(e) > 0 ? atoi(e) : 1;
+        }();
+        q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? gen * pf_res : 0;
         hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(c.T), c.lds, s, q);
         return true;
     }
