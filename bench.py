@@ -538,8 +538,10 @@ def main():
     if hook is not None and hasattr(hook, "learner") and hasattr(hook.learner, "pipeline_check"):
         hook.learner.pipeline_check()  # raises if a round gave up waiting for its snapshot (device-side gate)
         if hook.learner.__dict__.get("_pipe") is not None:
-            handoff = {0: "cross-queue event wait", 1: "device gate polled by the critic row blocks",
-                       2: "device gate polled by one wave on the learner stream"}[hook.learner.pipeline().gated()]
+            handoff = {0: "cross-queue event wait", 1: "device gate polled by the critic row blocks"}[
+                hook.learner.pipeline().gated()]
+            if getattr(hook.learner, "dp_split", False):
+                handoff += "; data-parallel actor all-reduce + Adam on a second group and stream
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

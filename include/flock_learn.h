@@ -204,47 +204,31 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
                         const float* grad_scale);
 
 /* learn() pipeline of a training loop that calls Agent.learn() once per env step (train_flock.py:120-121, one agent
- * per call): n_slots (2..8) staging slots, each with its own FlockScUpdate (do_adam, own critic_view, own workspace;
- * ring fields = that slot's staging rows, idx = 0..B-1). Rounds (flock_sc_round) are captured once as HIP graphs.
- * flock_sc_pipeline_learn enqueues learn() t of `agent` with no host synchronisation:
- *   env_stream:     [wait until the slot's previous learn() has finished] minibatch snapshot (flock_sc_prep_snapshot,
- *                   rows sampled with Philox(seed, counter)) -> event
- *   learner_stream: wait for the snapshot -> ONE round: the critic phase of learn t with the actor phase of learn t-1
- *                   (if learn t-1 had the same agent: its actor phase, then this critic phase)
- * so the learner runs one six-launch round per env step beside the next env step (which may rewrite the ring once
- * the snapshot ran), with no cross-stream wait between the two phases. The actor phase of the last learn() stays
- * pending until the next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise
- * those of the serial learn() sequence. Returns NULL (create) or a negative code; flock_learn_last_error() has the
- * message. */
+ * per call; replaces agent_simple_shared_critic.py:115-185 called in that cadence): n_slots (2..8) staging slots, each
+ * with its own FlockScUpdate (do_adam, own critic_view, own workspace; ring fields = that slot's staging rows, idx =
+ * 0..B-1). flock_sc_pipeline_learn enqueues learn() t of `agent` with no host synchronisation:
+ *   env_stream:     [wait until the slot's previous learn() has finished] minibatch snapshot (rows sampled with
+ *                   Philox(seed, counter), as flock_sc_prep_snapshot)
+ *   learner_stream: ONE round (five launches): the critic phase of learn t with the actor phase of learn t-1 (if
+ *                   learn t-1 had the same agent: its actor phase, then this critic phase)
+ * The round's wait for the snapshot is, by default, the device-side gate: the snapshot (one workgroup) stores the
+ * staging rows and the agent index write-through (`sc1`), waits for its stores and publishes a sequence number; the
+ * critic phase's row blocks poll it (bounded: 0.2 s; a waiter that gives up sets an error word and computes nothing,
+ * flock_sc_pipeline_check returns -6) and read the staging rows `sc1` (MI355X_MICROARCH.md hand-off table, row 1).
+ * flock_sc_pipeline_set_gate(p, 0) (and always: data-parallel rounds, rocprofv3 counter collection, which serialises
+ * dispatches) makes it a cross-queue event wait instead; it returns the hand-off in use (1 gate, 0 events). Both are
+ * deadlock-free whatever hardware queues the streams map to: every snapshot is enqueued before the round that waits
+ * for it, and nothing on env_stream waits for that round. The actor phase of the last learn() stays pending until the
+ * next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise those of the serial
+ * learn() sequence. Returns NULL (create) or a negative code; flock_learn_last_error() has the message. */
 typedef struct FlockScPipeline FlockScPipeline;
 FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slots, const FlockScRows* ring,
                                           const FlockScRows* staging);
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent);
-/* Direct learns (no snapshot), for a loop whose every env step rewrites the WHOLE replay ring (E N >= capacity, so the
- * ring's content after step t is a function of step t alone) and that keeps one physical copy of the ring per slot:
- *   flock_sc_pipeline_acquire(p, env_stream) -> slot s: enqueues, on env_stream, the wait until slot s's previous
- *     learn() has finished with its rows; the caller then steps the env into ring copy s (the fused insert);
- *   flock_sc_pipeline_learn_direct(..., &copy_s): event on env_stream -> the learner stream waits for it -> the same
- *     rounds as flock_sc_pipeline_learn, whose critic phase draws its minibatch rows itself (the same Philox rows the
- *     snapshot copies) straight from copy s and takes `agent` by value.
- * Bitwise the snapshot learns (the rows, the agent and every round are the same); what it removes is the snapshot
- * kernel between the env steps on env_stream. Not with data-parallel rounds or graph replays (-5). The copy a loop
- * wrote last holds the logical ring (ScTrainLoop: the caller copies it back into the ring). */
-int flock_sc_pipeline_acquire(FlockScPipeline* p, void* env_stream);
-/* Copy learns: the same ring copies (any number, 2..8, used in turn; copy c's env step waits until the snapshot that
- * last read copy c has run: flock_sc_pipeline_copy_acquire), but the minibatch snapshot runs on a stream of the
- * pipeline's own, behind an event wait for the env step that wrote the copy, and publishes a sequence number through
- * the device gate (`sc1` rows, csrc/flock_mem.h); the learner stream polls it with one wave and runs the rounds. So
- * neither the env stream (no snapshot between its steps) nor the learner stream (no cross-queue wait) carries the
- * snapshot's latency. Bitwise the snapshot learns. Needs the gate (flock_sc_pipeline_copy_ok: not data-parallel, not
- * graph replays, not under rocprofv3 counter collection, which serialises dispatches). */
-int flock_sc_pipeline_copy_ok(const FlockScPipeline* p);
-int flock_sc_pipeline_copy_acquire(FlockScPipeline* p, void* env_stream, int copy);
-int flock_sc_pipeline_learn_copy(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
-                                 uint64_t seed, uint64_t counter, int64_t agent, int copy, const FlockScRows* ring);
-int flock_sc_pipeline_learn_direct(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
-                                   uint64_t seed, uint64_t counter, int64_t agent, const FlockScRows* ring);
+int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on);
+int flock_sc_pipeline_gated(const FlockScPipeline* p);
+int flock_sc_pipeline_check(FlockScPipeline* p);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);
 /* Data-parallel rounds (one replica per GPU, the same learn() sequence on every rank): after this call every round
@@ -255,24 +239,19 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p);
  * flock_sc_round_adam with grad_scale (device scalar, 1 / world: the mean). Bitwise one process learning on the
  * union of the ranks' minibatches when the sums are exact in any order (SharedCriticLearner.dp_learn). Call before
  * the first flock_sc_pipeline_learn. */
-/* The device-side snapshot gate (single GPU, opt-in: FLOCK_SC_GATE=1 / 2; the default 0, and always under rocprofv3
- * counter collection, which serialises dispatches, is the cross-queue event wait, measured faster in round 4): the
- * snapshot kernel writes the staging rows `sc1` and publishes a sequence number after all its stores completed, and
- * the learner stream waits for it on the device instead of for an event: FLOCK_SC_GATE=2 one wave launched before
- * the round polls it (bounded, 0.2 s),
- * FLOCK_SC_GATE=1 the round's critic row blocks poll it. A waiter that gives up sets an error word and computes
- * nothing; flock_sc_pipeline_check (synchronous: call after synchronising the learner stream) returns -6 then.
- * flock_sc_pipeline_gated: the gate mode in use (0 = event waits). */
-int flock_sc_pipeline_check(FlockScPipeline* p);
-/* The fused rounds (the reference widths; FLOCK_SC_FUSE=1: three launches, 2: two; default 0, five launches: the
- * fused launches measured slower beside the env kernels, whose slots their waiting blocks hold) hand rows between the
- * workgroups of one launch through counters in the update's workspace; a wait that gives up (bounded, 0.2 s) sets an
- * error word there. Synchronous check of it (flock_sc_pipeline_check checks every slot's workspace too): -6. */
-int flock_sc_workspace_check(const FlockScUpdate* u);
-int flock_sc_pipeline_gated(const FlockScPipeline* p);
 typedef int (*FlockAllreduceFn)(void* ctx, float* data, int64_t n, void* learner_stream);
 int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_off,
                              int64_t bucket_floats, const float* grad_scale, FlockAllreduceFn allreduce, void* ctx);
+/* The actor half of each data-parallel round off the learner chain (after flock_sc_pipeline_set_dp, before the first
+ * learn): slot i's actor gradient goes to actor_grads[i] (one actor's floats, 16-B aligned, one buffer per slot), and
+ * its all-reduce (`allreduce(ctx, actor_grads[i], actor_floats, actor_stream)`, e.g. over a second process group) and
+ * Adam step run on a stream of the pipeline's own, behind an event for the round's gradient launches; only the critic
+ * all-reduce and the critic Adam stay on learner_stream, whose next critic phase needs them. Every later reader of
+ * that agent's actor on learner_stream (its next learn: 256 learns later at config 3) waits for the actor step's
+ * event unless the host already sees it complete; flush joins the actor stream into learner_stream. Bitwise the
+ * unsplit rounds (agent_simple_shared_critic.py:137-150; the reference steps the actor right after the critic). */
+int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads, int n_agents,
+                                   FlockAllreduceFn allreduce, void* ctx);
 
 #ifdef __cplusplus
 }

@@ -155,17 +155,12 @@ SIGNATURES.update({
                                  ctypes.POINTER(FlockScRows)],
     "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],
     "flock_sc_pipeline_flush": [_c_void_p, _c_void_p],
-    "flock_sc_pipeline_acquire": [_c_void_p, _c_void_p],
-    "flock_sc_pipeline_copy_ok": [_c_void_p],
-    "flock_sc_pipeline_copy_acquire": [_c_void_p, _c_void_p, ctypes.c_int],
-    "flock_sc_pipeline_learn_copy": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64, ctypes.c_int,
-                                                       _c_void_p],
-    "flock_sc_pipeline_learn_direct": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64, _c_void_p],
+    "flock_sc_pipeline_set_gate": [_c_void_p, _c_int],
     "flock_sc_pipeline_check": [_c_void_p],
-    "flock_sc_workspace_check": [ctypes.POINTER(FlockScUpdate)],
     "flock_sc_pipeline_gated": [_c_void_p],
     "flock_sc_pipeline_set_dp": [_c_void_p, _c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_void_p,
                                  _c_void_p, _c_void_p],
+    "flock_sc_pipeline_set_dp_actor": [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p],
     "flock_sc_pipeline_destroy": [_c_void_p],
 })
 RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,

@@ -36,8 +36,8 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// env rows per block: TM = 64 (two 32-row bands, 4 waves) or 128 (four bands, 8 waves: every fc2.weight chunk staged in
-// LDS is read by twice the rows, so the L2 -> LDS traffic per FLOP halves); FLOCK_ACT_TM picks it (default 64: the 128-row blocks measured 8% slower, 2.755 vs 2.553 ms)
+// env rows per block: TM = 64 (two 32-row bands, 4 waves); 128-row blocks (four bands, every staged fc2.weight chunk read
+// by twice the rows) measured 8 % slower in round 4 (2.755 vs 2.553 ms) and are not instantiated
 // k depth of an LDS-staged fc2.weight chunk (STG; a multiple of 8) and the waves per SIMD the register allocation must
 // allow (launch bounds). Round 4: 16-deep chunks (a 25.6-KB chunk buffer, 8 float4 of prefetch per thread) fit the block
 // in 168 VGPRs and ~41 KB of LDS, so THREE blocks share a CU (was 40-deep chunks, 245 VGPRs, two blocks): 2.49-2.51
@@ -690,7 +690,7 @@ int launch_act_tm(hipStream_t st, ActArgs a, int inp, bool stage, int tm) {
     a.tiles = (int)((a.rows + tm - 1) / tm);
     const size_t lds = sizeof(float) * ((size_t)a.H1 * inp + 4 * (size_t)a.H1 + (size_t)tm * inp + 8 * (size_t)tm);
     if (lds > 64 * 1024) return fail(-5, "flock_sc_act: fc1 too wide for the LDS staging");
-    return tm == 128 ? launch_act<NT, INC, 128>(st, a, lds, stage) : launch_act<NT, INC, 64>(st, a, lds, stage);
+    return launch_act<NT, INC, 64>(st, a, lds, stage);
 }
 
 }  // namespace
@@ -707,10 +707,7 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
     const int64_t per = (int64_t)fc1 * (in_dim + 3) + (int64_t)fc2 * (fc1 + 5) + 2;
     if (actor_stride < per) return fail(-5, "flock_sc_act: actor_stride smaller than one actor");
     if (rows == 0) return 0;
-    static const int tm = [] {  // FLOCK_ACT_TM=64 / 128: env rows per block (A/B)
-        const char* e = getenv("FLOCK_ACT_TM");
-        return e && atoi(e) == 128 ? 128 : 64;
-    }();
+    constexpr int tm = 64;  // env rows per block (128-row blocks measured 8 % slower, round 4)
     if ((rows + 63) / 64 * n_agents > 0x7fffffff) return fail(-5, "flock_sc_act: too many rows x agents");
     ActArgs a;
     a.obs = obs;
@@ -731,15 +728,8 @@ extern "C" int flock_sc_act(void* stream, int64_t rows, int n_agents, int in_dim
     const int inp = (in_dim + 3) & ~3;
     hipStream_t st = (hipStream_t)stream;
     const int nt = (fc2 + 63) / 64;
-    static const bool stage = [] {  // FLOCK_ACT_STAGE=0/1: fc2.weight straight from global memory / through LDS (A/B)
-        const char* e = getenv("FLOCK_ACT_STAGE");
-        return e ? e[0] == '1' : true;
-    }();
-    static const int mfma = [] {  // FLOCK_ACT_MFMA=16 / 32: the 16 x 16 kernel (default) or the 32 x 32 one (A/B)
-        const char* e = getenv("FLOCK_ACT_MFMA");
-        return e && atoi(e) == 32 ? 32 : 16;
-    }();
-    if (in_dim == 4 && mfma == 16 && stage && tm == 64) {
+    constexpr bool stage = true;  // fc2.weight through LDS (launch_act falls back to global reads past 64 KB of LDS)
+    if (in_dim == 4) {  // the 16 x 16 kernel at the widths it is instantiated for
         switch ((fc2 + 15) / 16) {  // the widths with an instantiation; others take the 32 x 32 kernel
             case 7: return launch_act16<7>(st, a);
             case 19: return launch_act16<19>(st, a);

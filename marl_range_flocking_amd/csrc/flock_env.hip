@@ -243,21 +243,13 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
-using flock_mem::st_sc1;  // write-through stores (csrc/flock_mem.h): A/B builds below
-
 // replay-ring stores of the fused insert: non-temporal (the rows are read back only by the learner's minibatch
 // gathers, long after the XCD's L2 has turned over). Same-box A/B at config 3 (`profiles/r03/ntring/`): env kernel
-// alone 42.5-43.8 -> 39.2-42.1 us; non-temporal stores for the other output streams too were slower (44.9-45.2 us).
-// -DFLOCK_PLAIN_RING: plain stores, -DFLOCK_SC1_RING: write-through stores (A/B builds)
+// alone 42.5-43.8 -> 39.2-42.1 us against plain stores; write-through stores and non-temporal stores for the other
+// output streams too were slower (44.9-45.2 us)
 template <typename T>
 __device__ __forceinline__ void st_ring(T* p, T v) {
-#if defined(FLOCK_PLAIN_RING)
-    *p = v;
-#elif defined(FLOCK_SC1_RING)
-    st_sc1(p, v);
-#else
     __builtin_nontemporal_store(v, p);
-#endif
 }
 
 // pair_d2 of two candidates at once: the squares and sums as packed f32 ops (v_pk_mul / v_pk_add, one candidate
@@ -266,48 +258,22 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-// Accessors of the step kernel's per-agent streams (state in, state / observation / replay record out). Plain
-// accesses by default; -DFLOCK_NT makes them non-temporal (measured: the env kernel 51.4 -> 52.2 us and the
-// overlapped config-3 step 159.5 -> 162.5 us, so keeping the streams out of L2 does not help the co-running update).
-#ifdef FLOCK_NT
+// Accessors of the step kernel's per-agent streams (state in, state / observation / replay record out): plain
+// accesses. Measured and dropped (round 1-3 A/B builds): non-temporal loads and stores of every stream (env kernel
+// 51.4 -> 52.2 us, the co-running update slower), non-temporal input loads only (43.9-45.2 against 38.2-39.5 us),
+// non-temporal or write-through output stores (44.9-45.2 us): these streams are the next step's inputs.
 template <typename T>
 __device__ __forceinline__ T ldnt(const T* p) {
-    return __builtin_nontemporal_load(p);
-}
-template <typename T>
-__device__ __forceinline__ void stnt(T* p, T v) {
-    __builtin_nontemporal_store(v, p);
-}
-#else
-template <typename T>
-__device__ __forceinline__ T ldnt(const T* p) {
-#ifdef FLOCK_NT_LOADS  // A/B builds: the per-agent input streams non-temporal
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 template <typename T>
 __device__ __forceinline__ void stnt(T* p, T v) {
-#if defined(FLOCK_NT_STORES)  // A/B builds: the per-agent output streams non-temporal, the loads plain
-    __builtin_nontemporal_store(v, p);
-#elif defined(FLOCK_SC1_OUT)  // A/B builds: the per-agent output streams write-through
-    st_sc1(p, v);
-#else
     *p = v;
-#endif
 }
-#endif
-
-// inputs read once and never written back by the step (the action, the previous observation row of the fused
-// insert); -DFLOCK_NT_ONCE (A/B builds): non-temporal
+// inputs read once and never written back by the step (the action, the previous observation row of the fused insert)
 template <typename T>
 __device__ __forceinline__ T ld_once(const T* p) {
-#ifdef FLOCK_NT_ONCE
-    return __builtin_nontemporal_load(p);
-#else
-    return ldnt(p);
-#endif
+    return *p;
 }
 
 template <bool PERIODIC>
@@ -882,12 +848,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     const int env = p.env0 + blockIdx.x * p.G + g;
     const bool active = in_group && env < p.E;
     const size_t a = (size_t)env * p.N + i;
-#ifdef FLOCK_STAGGER  // diagnostics: offset the phases of the first-round blocks sharing a CU (b, b + 256, ...)
-    if (blockIdx.x < 2048) {
-        const int m = (blockIdx.x >> 8) & 7;
-        for (int q = 0; q < m * FLOCK_STAGGER; ++q) __builtin_amdgcn_s_sleep(1);
-    }
-#endif
     if (in_group && i == 0) flags[g] = 0;
     if (t == 0) flags[p.G] = 0;  // arrival counter of the G = 1 any_done (published by the phase-2 barrier)
     if (CELL && in_group)  // published by the phase-2 barrier
@@ -895,12 +855,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
     // ---- phase 1: kinematics + boundary ------------------------------------------------------------------
     float x = 0.0f, y = 0.0f, h = 0.0f;
-#ifdef FLOCK_LATE_KIN_STORES  // A/B: v2's position / heading / velocity stores with the other outputs (phase 5)
-    constexpr bool kLateKinStores = VAR == FLOCK_VARIANT_V2;
-#else
-    constexpr bool kLateKinStores = false;
-#endif
-    float kin_vx = 0.0f, kin_vy = 0.0f;
     float2 act_in = make_float2(0.0f, 0.0f);  // fused replay insert: the raw action (v2) or the f32 action id
     float prev_obs[L - 2];  // fused replay insert: the previous observation row, loaded early (latency hidden)
 #pragma unroll
@@ -950,12 +904,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             }
         }
     };
-#ifndef FLOCK_LOAD_LATE_FIRST
-    constexpr bool kLateAfter = true;
-#else
-    constexpr bool kLateAfter = false;
-#endif
-    if (!kLateAfter) load_late();
+    constexpr bool kLateAfter = true;  // the seeds / previous-obs loads after the kinematics loads (round 1)
     // small-N Euclidean kernels (uw / flock observation memory): the three frames the roll keeps, loaded now so
     // their latency hides behind the step (only in the !CELL, !PERIODIC instantiation: no register cost elsewhere)
     constexpr bool kMemEarly = !CELL && !PERIODIC;
@@ -1015,13 +964,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             vy = __fmul_rn(nan_to_num(vy), p.dt);
             x = __fadd_rn(x, vx);                                            // :350
             y = __fadd_rn(y, vy);
-            if (!kLateKinStores) {
-                stnt(p.heading + a, h);
-                stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
-            } else {
-                kin_vx = vx;
-                kin_vy = vy;
-            }
+            stnt(p.heading + a, h);
+            stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
         } else if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:269-302 (heading=False)
             const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
             const float n = sqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
@@ -1085,7 +1029,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (variant != kSense) {
             x = boundary(x, p.box, p.rigid);  // check_boundary :271-304
             y = boundary(y, p.box, p.rigid);
-            if (!(kLateKinStores && variant == FLOCK_VARIANT_V2)) stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
+            stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
         }
         lpos[g * p.S + i] = make_float2(x, y);
     }
@@ -1403,11 +1347,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
     int coll = 0;
-    if (kLateKinStores && active) {
-        stnt(p.heading + a, h);
-        stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{kin_vx, kin_vy});
-        stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
-    }
     if (active) {
         float dv[L - 1];
 #pragma unroll
@@ -1738,24 +1677,17 @@ int check_common(int E, int N, int k) {
     return FLOCK_OK;
 }
 
-// diagnostics knobs, read once (first launch): FLOCK_ENV_LAUNCHES=n splits a step into n launches over consecutive
-// env ranges; FLOCK_NO_SPEC=1 takes the generic instantiations; FLOCK_NO_SPLIT=1 the one-lane-per-agent scan of the
-// split (SPL > 1) instantiations; FLOCK_NO_CELLS=1 the full scan instead of the cell list (A/B tests)
+// diagnostics knobs (flock_set_diag; A/B tests and tools): env_launches = n splits a step into n launches over
+// consecutive env ranges; no_spec takes the generic instantiations; no_split the one-lane-per-agent scan of the split
+// (SPL > 1) instantiations; no_cells the full scan instead of the cell list; pf = 0 turns off the env blocks' L2
+// pull-ahead (step_kernel's PFM, compiled only into the shapes that use it; -1: on)
 struct Knobs {
-    int env_launches;
-    bool no_spec, no_split, no_cells;
-    int pf;  // FLOCK_ENV_PF: the env blocks' L2 pull-ahead (step_kernel's PFM) where launch_spec has one: -1 (default)
-             // on, 0 off (A/B; the pull is compiled only into the shapes that use it)
-    int lds_pad;  // FLOCK_ENV_LDS_PAD: extra dynamic LDS bytes per step block (caps the blocks per CU; A/B only)
+    int env_launches = 1;
+    bool no_spec = false, no_split = false, no_cells = false;
+    int pf = -1;
 };
 Knobs& knobs_mut() {
-    static Knobs k = [] {
-        const char* e = getenv("FLOCK_ENV_LAUNCHES");
-        const char* lp = getenv("FLOCK_ENV_LDS_PAD");
-        return Knobs{e ? atoi(e) : 1, getenv("FLOCK_NO_SPEC") != nullptr, getenv("FLOCK_NO_SPLIT") != nullptr,
-                     getenv("FLOCK_NO_CELLS") != nullptr,
-                     getenv("FLOCK_ENV_PF") ? atoi(getenv("FLOCK_ENV_PF")) : -1, lp ? atoi(lp) : 0};
-    }();
+    static Knobs k;
     return k;
 }
 const Knobs& knobs() { return knobs_mut(); }
@@ -1783,7 +1715,6 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
     if (knobs().no_spec) return false;  // A/B diagnostics: the generic instantiation
     Cfg c = c0;
-    c.lds += (size_t)knobs().lds_pad;
     if (SPL > 1) {  // one env per block of SPL * NC lanes; LDS: the G = 1 layout + the merge lists in place of ext
         if (knobs().no_split) return false;
         c = make_cfg(p.E, NC, false, 0, 0, 0, 1);
@@ -1799,11 +1730,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
             pf_lds = (int)c.lds;
         }
         Params q = p;
-        static const int gen = [] {  // FLOCK_ENV_PF_GEN (A/B): pull that many block generations ahead (default 1)
-            const char* e = getenv("FLOCK_ENV_PF_GEN");
-            return e && atoi(e) > 0 ? atoi(e) : 1;
-        }();
-        q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? gen * pf_res : 0;
+        // one block generation ahead (two measured flat at config 5, round 4)
+        q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? pf_res : 0;
         hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(c.T), c.lds, s, q);
         return true;
     }
@@ -1916,8 +1844,6 @@ Params base(int E, int N, int k, float box) {
 // C ABI
 
 void flock_sc_diag_no_spec(bool v);  // flock_sc.hip
-void flock_sc_diag_no_fuse(bool v);  // flock_sc.hip
-void flock_sc_diag_fuse_k1(int v);   // flock_sc.hip
 
 extern "C" {
 
@@ -1938,10 +1864,6 @@ int flock_set_diag(const char* name, int value) {
         k.pf = value;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
-    else if (!strcmp(name, "sc_no_fuse"))
-        flock_sc_diag_no_fuse(value != 0);
-    else if (!strcmp(name, "sc_fuse_k1"))  // 0 / 1; -1: back to FLOCK_SC_FUSE
-        flock_sc_diag_fuse_k1(value);
     else
         return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
     return FLOCK_OK;

@@ -37,13 +37,9 @@ namespace {
 using flock_learn_internal::fail;
 using flock_learn_internal::launched;
 
-// replay rows per row-kernel block: 4 waves x kRW rows each (-DFLOCK_SC_RW=2 / 4: fewer, longer row blocks beside the
-// env kernel; A/B builds)
-#ifndef FLOCK_SC_RW
-#define FLOCK_SC_RW 1
-#endif
-constexpr int kRW = FLOCK_SC_RW;
-constexpr int kRowsPerBlock = 4 * kRW;
+// replay rows per row-kernel block: one row per wave (round 4 measured 2 and 4 rows per wave 10-20 us per step slower
+// beside the env kernel: DESIGN.md §3.3)
+constexpr int kRowsPerBlock = 4;
 constexpr int kMaxAct = 4;
 constexpr int kMaxIn = 64;
 constexpr int kMaxFeat = 1024;
@@ -108,13 +104,7 @@ struct Ws {
     float* Z2b;                            // [2][B][H2] actor fc2, critic fc2
     float *AXH2, *ARS2, *AH2, *DM, *ADY2, *ADZ2, *ALOSS;
     float *ADY1, *ADXH1, *APS1;
-    // fused rounds (launch_round_fused): [0, 16) arrivals of the forward GEMM tiles per 32-row tile, [16] arrivals of
-    // the bwd blocks, [17] the launch's finished blocks (the last one resets the counters it used), [18] error word.
-    // Zero between launches (workspaces are allocated zeroed).
-    unsigned* SYNC;
 };
-// [20 + 16 path + tile): arrivals of the k1 row blocks per path and 32-row tile (the k1-fused forward launch)
-constexpr int kSyncTiles = 16, kSyncBwd = 16, kSyncDone = 17, kSyncErr = 18, kSyncK1 = 20, kSyncWords = 128;
 
 int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
     int64_t off = 0;
@@ -137,8 +127,6 @@ int64_t ws_layout(int B, int in, int na, int H1, int H2, float* base, Ws* w) {
     x.AXH2 = take(H2); x.ARS2 = take(1); x.AH2 = take(H2); x.DM = take(na); x.ADY2 = take(H2); x.ADZ2 = take(H2);
     x.ALOSS = take(1);
     x.ADY1 = take(H1); x.ADXH1 = take(H1); x.APS1 = take(ps);
-    x.SYNC = base ? reinterpret_cast<unsigned*>(base + off) : nullptr;
-    off += kSyncWords;
     if (w) *w = x;
     return off;
 }
@@ -158,12 +146,6 @@ struct RowArgs {
     // (published by the snapshot kernel) instead of a cross-queue event wait; NULL: no wait
     unsigned long long* gate;
     unsigned long long gate_seq;
-    // direct rounds (flock_sc_pipeline_learn_direct): rows > 0 makes the critic phase's k1 draw its minibatch rows
-    // itself (sample_row(seed, counter, rows, r); idx unused) from the ring copy the env step just wrote, and take the
-    // agent index by value (agent_val >= 0; its path-0 blocks also store it to *agent for the round's later launches)
-    uint64_t seed, counter;
-    int64_t rows;
-    int64_t agent_val;
 };
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -270,41 +252,21 @@ __device__ __forceinline__ void ln_stats(const float (&z)[C], int F, int lane, f
     rstd = rsqrt_rn(wave_sum(q) / (float)F + kLnEps);
 }
 
-// F (fused rounds, launch_round_fused): the row was written by another workgroup of the SAME launch and handed off
-// through an arrival counter, so it is read `sc1` (csrc/flock_mem.h); otherwise by an earlier launch: plain loads
-template <int C, bool F = false>
+// a register row from a [B][Fw] array (lane j holds features j, j + 64, ...; zero past Fw)
+template <int C>
 __device__ __forceinline__ void load_row(float (&v)[C], const float* p, int Fw, int lane) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int j = lane + 64 * c;
-        v[c] = j < Fw ? (F ? flock_mem::ld_sc1(p + j) : p[j]) : 0.0f;
+        v[c] = j < Fw ? p[j] : 0.0f;
     }
 }
-// reads of data another workgroup of the same launch produced (fused rounds): `sc1`
-template <bool F>
-__device__ __forceinline__ float ld_in(const float* p) {
-    return F ? flock_mem::ld_sc1(p) : *p;
-}
-// stores of the kernels' per-row outputs (read by the next launch of the round); -DFLOCK_SC_NT (diagnostics A/B)
-// makes them non-temporal. F: read by a later workgroup of the same launch (fused rounds): write-through `sc1`
-template <bool F = false>
-__device__ __forceinline__ void st_out(float* p, float v) {
-    if constexpr (F) {
-        flock_mem::st_sc1(p, v);
-    } else {
-#ifdef FLOCK_SC_NT
-        __builtin_nontemporal_store(v, p);
-#else
-        *p = v;
-#endif
-    }
-}
-template <int C, bool FU = false>
+template <int C>
 __device__ __forceinline__ void store_row(float* p, const float (&v)[C], int F, int lane) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const int j = lane + 64 * c;
-        if (j < F) st_out<FU>(p + j, v[c]);
+        if (j < F) p[j] = v[c];
     }
 }
 
@@ -374,117 +336,83 @@ __device__ __forceinline__ void ln_backward(const float (&dy)[C], const float (&
 
 // ---------------------------------------------------------------------------------------------------------------
 // c1 (grid.y = path): 0 target actor on s', 1 critic on s', 2 critic on s (+ the gathered minibatch rows)
-// F (the k1-fused forward launch): every output row is read by later workgroups of the same launch (the GEMM tiles,
-// the k3 rows): stored write-through `sc1`
-template <int C, int HC, bool F = false>
+template <int C, int HC>
 __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, int path) {
     const int H1 = HC ? HC : a.H1;
     extern __shared__ float4 smem4[];
     float* xs = reinterpret_cast<float*>(smem4);  // [4 rows][kMaxIn] inputs, then the fc1 image
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // the replay rows and the agent index are read `sc1`: with the device-side gate (sc_k1) they are a snapshot
-    // another queue's kernel has just written through (csrc/flock_mem.h)
+    const int r = bx * kRowsPerBlock + wv;
+    // the staged replay rows and the agent index are read `sc1`: with the device-side gate (sc_k1) they are a
+    // snapshot another queue's kernel has just written through (csrc/flock_mem.h); the index rows are constant
     using flock_mem::ld_sc1;
-    const float* net = path == 0 ? a.actors_target + (a.agent_val >= 0 ? a.agent_val : ld_sc1(a.agent)) * a.stride
-                                 : a.critic;  // fc1 block at offset 0
-    // direct rounds: this learn's agent index for the round's later readers (F: the fused forward launch's GEMM tiles
-    // and k3 rows read it `sc1` after this block's arrival, which follows every wave's vmcnt(0) wait)
-    if (path == 0 && a.agent_val >= 0 && threadIdx.x == 0) {
-        int64_t* ag = const_cast<int64_t*>(a.agent);
-        if constexpr (F)
-            flock_mem::st_sc1(ag, a.agent_val);
-        else
-            *ag = a.agent_val;
-    }
-    // wave wv takes rows bx kRowsPerBlock + 4 q + wv, q < kRW
-#pragma unroll
-    for (int q = 0; q < kRW; ++q) {
-        const int r = bx * kRowsPerBlock + 4 * q + wv;
-        if (r >= a.B) continue;
-        const int64_t ir = a.rows > 0 ? sample_row(a.seed, a.counter, a.rows, r) : a.idx[r];
+    const float* net = path == 0 ? a.actors_target + ld_sc1(a.agent) * a.stride : a.critic;  // fc1 block at offset 0
+    const bool live = r < a.B;
+    if (live) {
+        const int64_t ir = a.idx[r];
         const float* x = (path == 2 ? a.rs : a.rs2) + ir * a.in;
         const float xv = lane < a.in ? ld_sc1(x + lane) : 0.0f;
-        if (lane < a.in) xs[(4 * q + wv) * kMaxIn + lane] = xv;
+        if (lane < a.in) xs[wv * kMaxIn + lane] = xv;
         if (path == 2) {
             if (lane < a.in) {
-                st_out<F>(w.S + (int64_t)r * a.in + lane, xv);
-                st_out<F>(w.S2 + (int64_t)r * a.in + lane, ld_sc1(a.rs2 + ir * a.in + lane));
+                w.S[(int64_t)r * a.in + lane] = xv;
+                w.S2[(int64_t)r * a.in + lane] = ld_sc1(a.rs2 + ir * a.in + lane);
             }
-            if (lane < a.na) st_out<F>(w.A + (int64_t)r * a.na + lane, ld_sc1(a.ra + ir * a.na + lane));
+            if (lane < a.na) w.A[(int64_t)r * a.na + lane] = ld_sc1(a.ra + ir * a.na + lane);
             if (lane == 0) {
-                st_out<F>(w.R + r, ld_sc1(a.rr + ir));
-                st_out<F>(w.T + r, ld_sc1(a.rt + ir));
+                w.R[r] = ld_sc1(a.rr + ir);
+                w.T[r] = ld_sc1(a.rt + ir);
             }
         }
     }
     stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kRW; ++q) {
-        const int r = bx * kRowsPerBlock + 4 * q + wv;
-        if (r >= a.B) continue;
-        float xh[C], h[C], rs;
-        fc1_ln_relu<C>(xs + (4 * q + wv) * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
-        const int64_t ro = (int64_t)r * H1;
-        if (path == 0) {
-            store_row<C, F>(w.TH1 + ro, h, H1, lane);
-        } else if (path == 1) {
-            store_row<C, F>(w.NH1 + ro, h, H1, lane);
-        } else {
-            store_row<C, F>(w.XH1 + ro, xh, H1, lane);
-            store_row<C, F>(w.H1 + ro, h, H1, lane);
-            if (lane == 0) st_out<F>(w.RS1 + r, rs);
-        }
+    if (!live) return;
+    float xh[C], h[C], rs;
+    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
+    const int64_t ro = (int64_t)r * H1;
+    if (path == 0) {
+        store_row<C>(w.TH1 + ro, h, H1, lane);
+    } else if (path == 1) {
+        store_row<C>(w.NH1 + ro, h, H1, lane);
+    } else {
+        store_row<C>(w.XH1 + ro, xh, H1, lane);
+        store_row<C>(w.H1 + ro, h, H1, lane);
+        if (lane == 0) w.RS1[r] = rs;
     }
 }
 
 // c3: heads, TD target, MSE and the critic backward down to the fc2 pre-activation
-template <int C, int HC, int NAC, bool F = false>
+template <int C, int HC, int NAC>
 __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);  // critic tail
     const int H2 = HC ? HC : a.H2, na = NAC ? NAC : a.na;
     float* at = ct + round4(crit_tail_len(na, H2));  // target actor tail
     const int lane = threadIdx.x & 63;
+    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
+    const bool live = r < a.B;
     const CriticOff co = critic_off(a.in, na, a.H1, H2);
     const ActorOff ao = actor_off(a.in, na, a.H1, H2);
-    // every row of this wave (bx kRowsPerBlock + 4 q + wave, q < kRW) loaded before the tails' staging barrier
-    float ztq[kRW][C], znq[kRW][C], zsq[kRW][C];
-    float rwdq[kRW], termq[kRW], actq[kRW][kMaxAct];
+    float zt[C], zn[C], zs[C];
+    float rwd = 0.0f, term = 0.0f, act[kMaxAct];
+    if (live) {
+        load_row<C>(zt, w.Z2 + (int64_t)r * H2, H2, lane);
+        load_row<C>(zn, w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
+        load_row<C>(zs, w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
+        rwd = w.R[r];
+        term = w.T[r];
 #pragma unroll
-    for (int rq = 0; rq < kRW; ++rq) {
-        const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
-        rwdq[rq] = 0.0f;
-        termq[rq] = 0.0f;
-#pragma unroll
-        for (int o = 0; o < kMaxAct; ++o) actq[rq][o] = 0.0f;
-        if (r < a.B) {
-            load_row<C, F>(ztq[rq], w.Z2 + (int64_t)r * H2, H2, lane);
-            load_row<C, F>(znq[rq], w.Z2 + ((int64_t)a.B + r) * H2, H2, lane);
-            load_row<C, F>(zsq[rq], w.Z2 + (2 * (int64_t)a.B + r) * H2, H2, lane);
-            rwdq[rq] = ld_in<F>(w.R + r);
-            termq[rq] = ld_in<F>(w.T + r);
-#pragma unroll
-            for (int o = 0; o < kMaxAct; ++o) actq[rq][o] = o < na ? ld_in<F>(w.A + (int64_t)r * na + o) : 0.0f;
-        }
+        for (int o = 0; o < kMaxAct; ++o) act[o] = o < na ? w.A[(int64_t)r * na + o] : 0.0f;
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
-    // F: the agent index as the snapshot wrote it (the k1-fused launch may have started before the snapshot ran)
-    stage(at, a.actors_target + flock_mem::ld_sc1(a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    stage(at, a.actors_target + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
+    if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
     const float cbq = cWq[H2];
     const float *tg2 = at, *tbe2 = at + H2, *tWmu = at + 2 * H2, *tbmu = tWmu + na * H2;
-#pragma unroll
-    for (int rq = 0; rq < kRW; ++rq) {
-    const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
-    if (r >= a.B) continue;
-    const float(&zt)[C] = ztq[rq];
-    const float(&zn)[C] = znq[rq];
-    const float(&zs)[C] = zsq[rq];
-    const float rwd = rwdq[rq], term = termq[rq];
-    const float(&act)[kMaxAct] = actq[rq];
     float xh[C], y[C], rs;
 
     // target actor on s': mu' = tanh(Wmu ReLU(LN2(z)) + bmu)                    (:126, ddpg_network.py:134-140)
@@ -566,77 +494,62 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
     store_row<C>(w.XH2 + ro, xh, H2, lane);
     store_row<C>(w.DZ2 + ro, dz2, H2, lane);
     if (lane == 0) w.RS2[r] = rs;
-    }
 }
 
 // c5 / a5: ReLU + LN1 backward: dy = dh * [h > 0]; dz = LN backward(dy)
 // a1 (grid.y = path): 0 the agent's actor fc1/LN/ReLU on s (saved for backward), 1 the updated critic's on s
-template <int C, int HC, bool F = false>
+template <int C, int HC>
 __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, int path) {
     const int H1 = HC ? HC : a.H1;
     extern __shared__ float4 smem4[];
     float* xs = reinterpret_cast<float*>(smem4);
     float* sp = xs + kRowsPerBlock * kMaxIn;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const float* net = path == 0 ? a.actors + flock_mem::ld_sc1(a.agent) * a.stride : a.critic;
-#pragma unroll
-    for (int q = 0; q < kRW; ++q) {
-        const int r = bx * kRowsPerBlock + 4 * q + wv;
-        if (r < a.B && lane < a.in) xs[(4 * q + wv) * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
-    }
+    const int r = bx * kRowsPerBlock + wv;
+    const bool live = r < a.B;
+    const float* net = path == 0 ? a.actors + (*a.agent) * a.stride : a.critic;
+    if (live && lane < a.in) xs[wv * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
     stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < kRW; ++q) {
-        const int r = bx * kRowsPerBlock + 4 * q + wv;
-        if (r >= a.B) continue;
-        float xh[C], h[C], rs;
-        fc1_ln_relu<C>(xs + (4 * q + wv) * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
-        const int64_t ro = (int64_t)r * H1;
-        if (path == 0) {
-            store_row<C, F>(w.AXH1 + ro, xh, H1, lane);
-            store_row<C, F>(w.AH1 + ro, h, H1, lane);
-            if (lane == 0) st_out<F>(w.ARS1 + r, rs);
-        } else {
-            store_row<C, F>(w.CH1 + ro, h, H1, lane);
-        }
+    if (!live) return;
+    float xh[C], h[C], rs;
+    fc1_ln_relu<C>(xs + wv * kMaxIn, a.in, sp, H1, lane, xh, h, rs);
+    const int64_t ro = (int64_t)r * H1;
+    if (path == 0) {
+        store_row<C>(w.AXH1 + ro, xh, H1, lane);
+        store_row<C>(w.AH1 + ro, h, H1, lane);
+        if (lane == 0) w.ARS1[r] = rs;
+    } else {
+        store_row<C>(w.CH1 + ro, h, H1, lane);
     }
 }
 
 // a3: actor LN2/ReLU/mu/tanh, Q(s, mu) with the updated critic, actor loss -mean Q, and the backward through the
 // critic's action branch (dQ/dmu) and the actor head down to the actor's fc2 pre-activation
-template <int C, int HC, int NAC, bool F = false>
+template <int C, int HC, int NAC>
 __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     extern __shared__ float4 smem4[];
     float* ct = reinterpret_cast<float*>(smem4);
     const int H2 = HC ? HC : a.H2, na = NAC ? NAC : a.na;
     float* at = ct + round4(crit_tail_len(na, H2));
     const int lane = threadIdx.x & 63;
+    const int r = bx * kRowsPerBlock + (threadIdx.x >> 6);
+    const bool live = r < a.B;
     const CriticOff co = critic_off(a.in, na, a.H1, H2);
     const ActorOff ao = actor_off(a.in, na, a.H1, H2);
-    // every row of this wave (bx kRowsPerBlock + 4 q + wave, q < kRW) loaded before the tails' staging barrier
-    float za2q[kRW][C], zc2q[kRW][C];
-#pragma unroll
-    for (int rq = 0; rq < kRW; ++rq) {
-        const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
-        if (r < a.B) {
-            load_row<C, F>(za2q[rq], w.Z2b + (int64_t)r * H2, H2, lane);
-            load_row<C, F>(zc2q[rq], w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
-        }
+    const int64_t ro = (int64_t)r * H2;
+    float za2[C], zc2[C];
+    if (live) {
+        load_row<C>(za2, w.Z2b + ro, H2, lane);
+        load_row<C>(zc2, w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
-    stage(at, a.actors + flock_mem::ld_sc1(a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    stage(at, a.actors + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
+    if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
     const float cbq = cWq[H2];
     const float *ag2 = at, *abe2 = at + H2, *aWmu = at + 2 * H2, *abmu = aWmu + na * H2;
-#pragma unroll
-    for (int rq = 0; rq < kRW; ++rq) {
-    const int r = bx * kRowsPerBlock + 4 * rq + (threadIdx.x >> 6);
-    if (r >= a.B) continue;
-    const int64_t ro = (int64_t)r * H2;
-    const float(&za2)[C] = za2q[rq];
-    const float(&zc2)[C] = zc2q[rq];
 
     float xh[C], y[C], h2[C], rs;
     ln_affine<C>(za2, ag2, abe2, H2, lane, xh, y, rs);
@@ -718,7 +631,6 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
     store_row<C>(w.ADY2 + ro, dy2, H2, lane);
     store_row<C>(w.ADZ2 + ro, dz2, H2, lane);
     if (lane == 0) w.ARS2[r] = rs;
-    }
 }
 
 // -DFLOCK_SC_PROF (diagnostics build, tools/sc_block_prof.py): per-block start / end times (s_memrealtime, 100 MHz)
@@ -747,14 +659,6 @@ __device__ unsigned long long g_scmark[4096][8];
 #define SC_PROF(k)
 #define SC_MARK(MK, i)
 #endif
-// -DFLOCK_SC_PRIO=n (A/B builds): the round kernels' waves raise their issue priority (s_setprio n) over the env
-// kernel's waves they share SIMDs with
-#ifdef FLOCK_SC_PRIO
-#define SC_PRIO() __builtin_amdgcn_s_setprio(FLOCK_SC_PRIO)
-#else
-#define SC_PRIO()
-#endif
-
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
 // blocks past them).
@@ -785,31 +689,9 @@ __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned lon
     return ok != 0;
 }
 
-// a fused launch's wait for n arrivals on a counter (same hand-off form as gate_wait)
-__device__ __forceinline__ bool wait_count(const unsigned* ctr, unsigned need, unsigned* err) {
-    __shared__ int ok;
-    if (threadIdx.x == 0) {
-        int good = 1;
-        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
-                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    good = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        ok = good;
-    }
-    __syncthreads();
-    return ok != 0;
-}
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     SC_PROF(0);
-    SC_PRIO();
     if (ac.gate && (int)blockIdx.y < npc && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
     if ((int)blockIdx.y < npc)
         c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
@@ -819,7 +701,6 @@ __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, 
 template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
     SC_PROF(2);
-    SC_PRIO();
     if ((int)blockIdx.x < nbc)
         c3_body<C, HC, NAC>(wc, ac, blockIdx.x);
     else
@@ -834,8 +715,8 @@ __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, 
 // 2 = any strides (scalar).
 constexpr int kT = 32;
 constexpr int kKC = 512;
-constexpr int kFwdKC = 200;   // forward / input-gradient GEMM K chunk (FLOCK_GEMM_KC overrides): 0.098 ms per config-3
-                              // step vs 0.117 with whole 400-deep panels (lighter blocks co-run with the env kernel)
+constexpr int kFwdKC = 200;   // forward / input-gradient GEMM K chunk: 0.098 ms per config-3 step vs 0.117 with whole
+                              // 400-deep panels (lighter blocks co-run with the env kernel; tools/gpu_kc_sweep.sh)
 constexpr int kGradKC = 128;  // the gradient kernels share one launch with ~400 LDS-free reduction blocks: a 34-KB
                               // panel keeps 4 blocks per CU resident so the whole grid runs in one round
 constexpr int kPitch = 33;
@@ -849,8 +730,6 @@ struct GemmP {
     const int64_t* agent;
     int tiles_n, tiles;
     int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
-    unsigned* sig;  // fused rounds: one arrival per finished tile at sig[tile row] (the k3 rows' hand-off); NULL: none
-    const unsigned* wait;  // k1-fused forward launch: the k1 row blocks' arrivals per tile row of A
 };
 constexpr int kMaxBatch = 5;  // a round's forward GEMMs: 3 (critic phase) + 2 (actor phase)
 struct GemmBatch {
@@ -943,27 +822,18 @@ __device__ __forceinline__ void load_panel(float* __restrict__ P, const float* _
 // panel_fetch issues the global loads into registers, panel_store writes them to LDS. gemm_tile fetches the A and
 // B panels of a chunk together (one memory round trip instead of two) and the next chunk's panels before the
 // current chunk's MFMAs.
-// SC (V = 0 only; the k1-fused forward launch): the panel was written by other workgroups of the same launch and is
-// read with `sc1` 16-B buffer loads (X uniform: one buffer resource; csrc/flock_mem.h)
-template <int V, int NF, bool SC = false>
+template <int V, int NF>
 __device__ __forceinline__ void panel_fetch(float4 (&v)[NF], const float* __restrict__ X, int R, int Kd, int sr,
                                             int sk, int r0, int k0, int kc) {
     const int tid = threadIdx.x;
     if (V == 0) {
         const int q = kc >> 2, items = 32 * q;
-        __amdgpu_buffer_rsrc_t rsrc;
-        if constexpr (SC) rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
             const int t = tid + 256 * i;
             const int rr = t / q, k = k0 + 4 * (t - rr * q), rw = r0 + rr;
-            const bool in = t < items && rw < R && k < Kd;
-            if constexpr (SC) {
-                const auto u = __builtin_amdgcn_raw_buffer_load_b128(rsrc, in ? (rw * sr + k) * 4 : 0, 0, 16);
-                v[i] = in ? __builtin_bit_cast(float4, u) : make_float4(0.f, 0.f, 0.f, 0.f);
-            } else {
-                v[i] = in ? *reinterpret_cast<const float4*>(X + (int64_t)rw * sr + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            v[i] = (t < items && rw < R && k < Kd) ? *reinterpret_cast<const float4*>(X + (int64_t)rw * sr + k)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     } else {
         const int items = 8 * kc;
@@ -1029,8 +899,7 @@ __device__ __forceinline__ f32x16 mfma_panel(f32x16 acc, const float* a, const f
 }
 
 // the 4 outputs of thread (wave w, lane l): rows 8w + 4(l >> 5) + q (q < 4), column l & 31
-// ASC: the A panels are read `sc1` (panel_fetch SC; the k1-fused forward launch)
-template <int AV, int BV, int NF, int MK = 0, bool ASC = false>
+template <int AV, int BV, int NF, int MK = 0>
 __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int tm, int tn, float* smem,
                                           float (&out)[4]) {
     SC_MARK(MK, 0)
@@ -1045,7 +914,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
     if constexpr (AV != 2 && BV != 2) {
         float4 va[NF], vb[NF];
         int kc = gemm_kc(g.K, g.kchunk);
-        panel_fetch<AV, NF, ASC>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
+        panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, 0, kc);
         panel_fetch<BV, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, 0, kc);
         for (int k0 = 0; k0 < g.K; k0 += g.kchunk) {
             panel_store<AV, NF>(As, va, kc);
@@ -1055,7 +924,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
             SC_MARK(MK, (k0 ? 5 : 2))
             const int k1 = k0 + g.kchunk, kc1 = k1 < g.K ? gemm_kc(g.K - k1, g.kchunk) : 0;
             if (k1 < g.K) {  // the next chunk's loads fly during this chunk's MFMAs
-                panel_fetch<AV, NF, ASC>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
+                panel_fetch<AV, NF>(va, g.A, g.M, g.K, g.sam, g.sak, tm * kT, k1, kc1);
                 panel_fetch<BV, NF>(vb, Bp, g.N, g.K, g.sbn, g.sbk, tn * kT, k1, kc1);
             }
             const int kq = kc >> 2;  // multiple of 2
@@ -1099,38 +968,25 @@ __device__ __forceinline__ int xcd_tile(int x, int tiles) {
     return (tiles & 7) == 0 && (int)gridDim.x == tiles ? (x & 7) * (tiles >> 3) + (x >> 3) : x;
 }
 
-// one forward GEMM tile: block x of problem y computes tile xcd_tile(x). F (fused rounds): the tile is stored
-// write-through and its arrival counted at g.sig[tile row] once every wave's stores have completed (csrc/flock_mem.h)
-// K1 (the k1-fused forward launch): the tile first waits for the k1 row blocks of its 32 rows (g.wait[tm]) and reads
-// its A panels `sc1`
-template <int AV, int BV, int NF, bool F, bool K1 = false>
-__device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x, unsigned* err = nullptr) {
+// one forward GEMM tile: block x of problem y computes tile xcd_tile(x)
+template <int AV, int BV, int NF>
+__device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const GemmP& g = gb.p[y];
     if (x >= g.tiles) return;
     const int t = xcd_tile(x, g.tiles);
     const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    if (K1) {  // first the k1 rows of this tile: they follow the snapshot (gate), which also wrote *g.agent
-        const int rows = min(g.M - tm * kT, kT);
-        if (!wait_count(g.wait + tm, (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock), err)) return;
-    }
-    // K1: this launch may have started before the snapshot wrote the agent index: read it `sc1` after the wait
-    const int64_t rel = g.relB ? g.relB * flock_mem::ld_sc1(g.agent) : 0;
+    const int64_t rel = g.relB ? g.relB * (*g.agent) : 0;
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int n = tn * kT + (l & 31);
     const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
     float out[4];
-    gemm_tile<AV, BV, NF, 1, K1>(g, g.B + rel, tm, tn, smem, out);
+    gemm_tile<AV, BV, NF, 1>(g, g.B + rel, tm, tn, smem, out);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-        if (m < g.M && n < g.N) st_out<F>(g.C + (int64_t)m * g.ldc + n, g.bias ? out[q] + bias : out[q]);
-    }
-    if (F) {
-        flock_mem::wait_vmem();
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(g.sig + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (m < g.M && n < g.N) g.C[(int64_t)m * g.ldc + n] = g.bias ? out[q] + bias : out[q];
     }
 }
 
@@ -1138,8 +994,7 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x, un
 template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     SC_PROF(1);
-    SC_PRIO();
-    gemm_block<AV, BV, NF, false>(gb, blockIdx.y, blockIdx.x);
+    gemm_block<AV, BV, NF>(gb, blockIdx.y, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1165,11 +1020,8 @@ struct RedP {
 };
 constexpr int kMaxRed = 12;
 // output elements per reduction block; the block's 256 threads are kRedElems elements x kRedGroups row groups (group q
-// takes rows q, q + kRedGroups, ...). -DFLOCK_RED_ELEMS=8 / 4: more row groups, fewer rows per thread (A/B builds)
-#ifndef FLOCK_RED_ELEMS
-#define FLOCK_RED_ELEMS 16
-#endif
-constexpr int kRedElems = FLOCK_RED_ELEMS;
+// takes rows q, q + kRedGroups, ...; 8 and 4 elements per block measured slower in round 4: DESIGN.md §3.3)
+constexpr int kRedElems = 16;
 constexpr int kRedGroups = 256 / kRedElems;
 constexpr int kMaxRedBlocks = 4096;
 
@@ -1182,8 +1034,6 @@ struct DzArgs {
 // One block's reduction: the kRedElems-element slice of rp for block b (thread el = tid % kRedElems, row group
 // q = tid / kRedElems);
 // returns the sum in threads q == 0 (0 elsewhere). part: 256 floats of LDS; mst: [B][2] LDS (modes 4 / 5)
-// F (fused rounds): D and the row sums PS were written by the bwd blocks of the same launch: `sc1` loads
-template <bool F = false>
 __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const DzArgs& dz, float* part, float* mst,
                                            int& e_out, bool& live_out) {
     const int tid = threadIdx.x;
@@ -1195,17 +1045,15 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
     const int o = per_in ? e / rp.in : e;
     const int i = per_in ? e - o * rp.in : e;
     const bool prod = rp.mode == 1 || rp.mode == 2 || rp.mode == 4;
-#ifndef FLOCK_RED_RB
-#define FLOCK_RED_RB 8
-#endif
-    constexpr int kRB = FLOCK_RED_RB;  // rows per batch of loads (row group q takes rows q, q + kRedGroups, ...)
+    constexpr int kRB = 8;  // rows per batch of loads (row group q takes rows q, q + kRedGroups, ...; 4 and 16 flat or
+                            // slower in round 3)
     float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
     auto load = [&](int r0) {
 #pragma unroll
         for (int k = 0; k < kRB; ++k) {
             const int r = r0 + kRedGroups * k;
             const bool in = live && r < B;
-            dv[k] = in ? ld_in<F>(rp.D + (int64_t)r * rp.ldd + o) : 0.0f;
+            dv[k] = in ? rp.D[(int64_t)r * rp.ldd + o] : 0.0f;
             xv[k] = (in && prod) ? rp.X[(int64_t)r * rp.ldx + i] : 0.0f;
             xh[k] = (in && dzm) ? dz.XH[(int64_t)r * dz.F + o] : 0.0f;
             rs[k] = (in && dzm) ? dz.RS[r] : 0.0f;
@@ -1223,7 +1071,7 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
                 float2 v[kPB];
 #pragma unroll
                 for (int u = 0; u < kPB; ++u)
-                    v[u] = t0 + u < dz.ntn ? (F ? flock_mem::ld_sc1_f2(ps + t0 + u) : ps[t0 + u]) : make_float2(0.0f, 0.0f);
+                    v[u] = t0 + u < dz.ntn ? ps[t0 + u] : make_float2(0.0f, 0.0f);
 #pragma unroll
                 for (int u = 0; u < kPB; ++u)
                     if (t0 + u < dz.ntn) {
@@ -1279,18 +1127,17 @@ struct BwdJob {
 __host__ __device__ inline int bwd_blocks(const BwdJob& j) { return j.dh.tiles + j.dw.tiles + j.nblk; }
 
 // the 4 rows of thread (wave w, lane l) in a 32 x 32 tile: 8w + 4(l >> 5) + q; its column: l & 31
-// F (fused rounds): every output is read by the grad blocks of the same launch: write-through `sc1` stores
-template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW, bool F = false>
+template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
 __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-    const int64_t base = j.rel ? j.rel * flock_mem::ld_sc1(j.agent) : 0;
-    const int64_t gbase = j.grad_rel ? j.grad_rel * flock_mem::ld_sc1(j.agent) : 0;
+    const int64_t base = j.rel ? j.rel * (*j.agent) : 0;
+    const int64_t gbase = j.grad_rel ? j.grad_rel * (*j.agent) : 0;
     if (bx < j.dh.tiles) {
         const GemmP& g = j.dh;
         const int tm = bx / g.tiles_n, tn = bx - tm * g.tiles_n;
-        const int64_t relB = g.relB ? g.relB * flock_mem::ld_sc1(g.agent) : 0;
+        const int64_t relB = g.relB ? g.relB * (*g.agent) : 0;
         const int n = tn * kT + (l & 31);
         const bool nok = n < g.N;
         // the epilogue's inputs, loaded before the GEMM
@@ -1313,8 +1160,8 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
             const float dy = hv[q] > 0.0f ? out[q] : 0.0f;  // through the ReLU
             const float dxh = dy * gam;
             if (ok) {
-                st_out<F>(j.DY1 + (int64_t)m * j.F + n, dy);
-                st_out<F>(j.DXH1 + (int64_t)m * j.F + n, dxh);
+                j.DY1[(int64_t)m * j.F + n] = dy;
+                j.DXH1[(int64_t)m * j.F + n] = dxh;
             }
             s1[q] = ok ? dxh : 0.0f;
             s2[q] = ok ? dxh * xv[q] : 0.0f;
@@ -1332,8 +1179,8 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
             for (int q = 0; q < 4; ++q) {
                 const int m = tm * kT + 8 * wv + 4 * (l >> 5) + q;
                 if (m < g.M) {
-                    st_out<F>(j.PS1 + ((int64_t)m * j.ntn + tn) * 2, s1[q]);
-                    st_out<F>(j.PS1 + ((int64_t)m * j.ntn + tn) * 2 + 1, s2[q]);
+                    j.PS1[((int64_t)m * j.ntn + tn) * 2] = s1[q];
+                    j.PS1[((int64_t)m * j.ntn + tn) * 2 + 1] = s2[q];
                 }
             }
         }
@@ -1347,7 +1194,7 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int mm = tm * kT + 8 * wv + 4 * (l >> 5) + q;
-            if (mm < g.M && nn < g.N) st_out<F>(j.grad + gbase + j.w2_off + (int64_t)mm * g.ldc + nn, out[q]);
+            if (mm < g.M && nn < g.N) j.grad[gbase + j.w2_off + (int64_t)mm * g.ldc + nn] = out[q];
         }
     } else {
         const int b = bx - j.dh.tiles - j.dw.tiles;
@@ -1361,9 +1208,9 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
         const float gsum = red_block(rp, b, j.B, none, smem, nullptr, e, wr);
         if (wr) {
             if (rp.mode == 3)
-                st_out<F>(j.loss, gsum * (1.0f / (float)j.B));
+                *j.loss = gsum * (1.0f / (float)j.B);
             else
-                st_out<F>(j.grad + gbase + rp.off + e, gsum);
+                j.grad[gbase + rp.off + e] = gsum;
         }
     }
 }
@@ -1375,7 +1222,6 @@ struct Bwd2 {
 template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
 __global__ __launch_bounds__(256) void sc_bwd(Bwd2 bb) {
     SC_PROF(3);
-    SC_PRIO();
     if ((int)blockIdx.x < bb.nb0)
         bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
     else
@@ -1439,19 +1285,17 @@ __device__ __forceinline__ void adam_store(const GradAdam& ga, int64_t i, AdamSt
 
 // one job's blocks of the late launch: [0, nblk) reductions, [nblk, + adam_blocks) Adam of the bwd launch's
 // gradients, then soft_blocks self soft update blocks
-// F (fused rounds): the gradients and LN1 row sums the bwd blocks of the same launch wrote are read `sc1`
-template <bool F = false>
 __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int nb) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     __shared__ float sh[2];
     __shared__ int sh_soft;
     const int tid = threadIdx.x;
-    const int64_t agent = ga.rel ? flock_mem::ld_sc1(ga.agent) : 0;
+    const int64_t agent = ga.rel ? *ga.agent : 0;
     const int64_t base = ga.rel * agent, gbase = ga.grad_rel * agent;
     if (tid == 0) {
         const int64_t step0 = ga.do_adam ? ga.step[agent] : 0;
-        const int64_t count = ga.soft_count ? ga.soft_count[flock_mem::ld_sc1(ga.agent)] : step0;
+        const int64_t count = ga.soft_count ? ga.soft_count[*ga.agent] : step0;
         sh_soft = ga.do_adam && ga.soft_rate > 0 && (count % ga.soft_rate) == 0;  // this learn's count
         if (ga.do_adam) {
             const double st = (double)(step0 + 1);
@@ -1483,7 +1327,7 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
         for (int q = 0; q < 4; ++q) {
             const int64_t e = e0 + q * 256 + tid;
             st[q] = e < end ? adam_load(ga, base + e) : AdamState{0.f, 0.f, 0.f, 0.f};
-            gi[q] = e < end ? ld_in<F>(ga.grad + gbase + e) : 0.0f;
+            gi[q] = e < end ? ga.grad[gbase + e] : 0.0f;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1501,7 +1345,7 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
         const AdamState st = ad ? adam_load(ga, base + rp.off + e1) : AdamState{0.f, 0.f, 0.f, 0.f};
         int e;
         bool wr;
-        const float gsum = red_block<F>(rp, b, ga.B, ga.dz, smem, smem + 256, e, wr);
+        const float gsum = red_block(rp, b, ga.B, ga.dz, smem, smem + 256, e, wr);
         if (wr) {
             ga.grad[gbase + rp.off + e] = gsum;
             if (ga.do_adam) adam_store(ga, base + rp.off + e, st, gsum, sh[0], sh[1], sh_soft != 0);
@@ -1526,7 +1370,6 @@ struct GradAdam2 {
 };
 __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
     SC_PROF(4);
-    SC_PRIO();
     if ((int)blockIdx.x < gg.nb0)
         grad_adam_body(gg.j0, blockIdx.x, gg.nb0);
     else
@@ -1534,133 +1377,7 @@ __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Fused rounds: three launches instead of five. [k1] rows, then ONE launch of the forward GEMM tiles and the k3 rows
-// (each k3 block waits for the tiles of its 32-row tile), then ONE launch of the bwd blocks and the gradient / Adam
-// blocks (each waits for every bwd block of its job). Hand-offs inside a launch follow MI355X_MICROARCH.md's row 1
-// (csrc/flock_mem.h): the producer's outputs are stored `sc1`, every wave waits for its stores, a workgroup barrier,
-// one lane's agent-scope counter add; the consumer's lane 0 polls the counter with `sc1` loads, a workgroup barrier,
-// then `sc1` loads of the handed-off rows. Consumers have higher block indices than every producer they wait for, so
-// they are dispatched after them and the wait always ends; a wait beyond kGateTimeoutTicks sets the workspace's error
-// word and the block computes nothing (flock_sc_pipeline_check / flock_sc_workspace_check report it). The counters
-// are zero between launches: the launch's last finishing block resets the ones it used. The math of every block is
-// the unfused kernels' (results bitwise equal: tests/test_gpu_overlap.py).
-// every block of a fused launch ends here: the last one to finish resets the counters the launch used
-struct SyncReset {
-    unsigned* done;
-    unsigned total;  // blocks of the launch
-    unsigned* r[4];  // counter ranges to zero
-    int n[4];
-};
-__device__ __forceinline__ void launch_done(const SyncReset& sr) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(sr.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev == sr.total - 1u) {
-            for (int k = 0; k < 4; ++k)
-                for (int i = 0; i < sr.n[k]; ++i) __hip_atomic_store(sr.r[k] + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(sr.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-struct K3Side {
-    Ws w;
-    RowArgs a;
-    int nb;         // k3 blocks of this job (0: absent)
-    unsigned need;  // tile arrivals per 32-row tile (paths x column tiles)
-};
-// forward launch: grid (max tiles, [k1 rows +] problems + k3 rows): with K1 the first ny1 rows of the grid are the k1
-// row blocks (critic job: 3 paths x rb, actor job: 2 paths x rb; linear index), each signalling its path's 32-row
-// tile; then y - ny1 < gb.n GEMM tiles (waiting for their A rows with K1, signalling), then the k3 blocks of the
-// critic job (kc) and of the actor job (ka), linear index over the trailing rows
-template <int AV, int BV, int NF, int C, int HC, int NAC, bool K1>
-__global__ __launch_bounds__(256) void sc_fwd(GemmBatch gb, K3Side kc, K3Side ka, SyncReset sr, int ny1) {
-    SC_PRIO();
-    const int y = (int)blockIdx.y - (K1 ? ny1 : 0);
-    if (K1 && y < 0) {
-        const int kb = (int)blockIdx.y * (int)gridDim.x + (int)blockIdx.x;
-        const int rb = (kc.nb > 0 ? kc : ka).nb;  // row blocks per path (the jobs share B)
-        const int nc = kc.nb > 0 ? 3 * rb : 0, na = ka.nb > 0 ? 2 * rb : 0;
-        if (kb < nc + na) {
-            const bool crit = kb < nc;
-            const K3Side& j = crit ? kc : ka;
-            const int path = (crit ? kb : kb - nc) / rb, bx = (crit ? kb : kb - nc) - path * rb;
-            if (crit) {
-                if (j.a.gate && !gate_wait(j.a.gate, j.a.gate_seq)) {  // this learn's snapshot
-                    launch_done(sr);
-                    return;
-                }
-                c1_body<7, 400, true>(j.w, j.a, bx, path);
-            } else {
-                a1_body<7, 400, true>(j.w, j.a, bx, path);
-            }
-            flock_mem::wait_vmem();
-            __syncthreads();
-            if (threadIdx.x == 0)
-                __hip_atomic_fetch_add(j.w.SYNC + kSyncK1 + 16 * path + (bx * kRowsPerBlock) / kT, 1u,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else if (y < gb.n) {
-        gemm_block<AV, BV, NF, true, K1>(gb, y, blockIdx.x, kc.w.SYNC + kSyncErr);
-    } else {
-        const int kb = (y - gb.n) * (int)gridDim.x + (int)blockIdx.x;
-        if (kb < kc.nb) {
-            if (wait_count(kc.w.SYNC + (kb * kRowsPerBlock) / kT, kc.need, kc.w.SYNC + kSyncErr))
-                c3_body<C, HC, NAC, true>(kc.w, kc.a, kb);
-        } else if (kb < kc.nb + ka.nb) {
-            const int b = kb - kc.nb;
-            if (wait_count(ka.w.SYNC + (b * kRowsPerBlock) / kT, ka.need, ka.w.SYNC + kSyncErr))
-                a3_body<C, HC, NAC, true>(ka.w, ka.a, b);
-        }
-    }
-    launch_done(sr);
-}
-// backward launch: [bwd blocks of j0 | of j1 | gradient / Adam blocks of j0 | of j1]
-struct BwdSync {
-    unsigned* arr[2];  // bwd arrivals of each job
-    unsigned* err[2];
-    int nbw[2];        // bwd blocks of each job (0: absent)
-};
-template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
-__global__ __launch_bounds__(256) void sc_bwdg(Bwd2 bb, GradAdam2 gg, BwdSync bs, SyncReset sr) {
-    SC_PRIO();
-    const int bx = blockIdx.x;
-    const int nbw = bs.nbw[0] + bs.nbw[1];
-    if (bx < nbw) {
-        const int j = bx < bs.nbw[0] ? 0 : 1;
-        bwd_body<AVH, BVH, AVW, BVW, NFH, NFW, true>(j == 0 ? bb.j0 : bb.j1, j == 0 ? bx : bx - bs.nbw[0]);
-        flock_mem::wait_vmem();
-        __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(bs.arr[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        const int g = bx - nbw;
-        const int j = g < gg.nb0 ? 0 : 1;
-        if (wait_count(bs.arr[j], (unsigned)bs.nbw[j], bs.err[j])) {
-            if (j == 0)
-                grad_adam_body<true>(gg.j0, g, gg.nb0);
-            else
-                grad_adam_body<true>(gg.j1, g - gg.nb0, (int)gridDim.x - nbw - gg.nb0);
-        }
-    }
-    launch_done(sr);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
 // host side
-// K-panel depth of the forward / input-gradient GEMMs: whole panels (kKC) by default; FLOCK_GEMM_KC (a multiple
-// of 8 in [8, 512]) stages them in chunks (smaller LDS footprint per block; A/B diagnostics)
-int kc_knob(const char* name, int dflt) {
-    const char* e = getenv(name);
-    const int v = e ? atoi(e) : 0;
-    return (v >= 8 && v <= kKC && (v & 7) == 0) ? v : dflt;
-}
-int fwd_kc() {
-    static const int kc = kc_knob("FLOCK_GEMM_KC", kFwdKC);
-    return kc;
-}
-int grad_kc() {
-    static const int kc = kc_knob("FLOCK_GRAD_KC", kGradKC);
-    return kc;
-}
 // K chunk for a K-deep GEMM with at most kcmax per chunk: the chunks balanced, a multiple of 8
 int balanced_kc(int K, int kcmax) {
     const int n = (K + kcmax - 1) / kcmax;
@@ -1678,9 +1395,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.agent = agent;
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
-    g.kchunk = balanced_kc(K, fwd_kc());
-    g.sig = nullptr;
-    g.wait = nullptr;
+    g.kchunk = balanced_kc(K, kFwdKC);
     return g;
 }
 
@@ -1805,10 +1520,6 @@ RowArgs row_args(const FlockScUpdate* u) {
     a.invB = 1.0f / (float)u->B;
     a.gate = nullptr;  // only flock_sc_pipeline_learn gates a critic phase on its snapshot
     a.gate_seq = 0;
-    a.seed = 0;
-    a.counter = 0;
-    a.rows = 0;  // the rows come through idx (only flock_sc_pipeline_learn_direct samples in k1)
-    a.agent_val = -1;
     return a;
 }
 
@@ -1851,7 +1562,7 @@ void bwd_common(Job& j, const float* W2, int64_t rel_w2, const int64_t* agent, c
     BwdJob& bw = j.bw;
     bw.dh = gemm_p(DZ2, W2, nullptr, nullptr, B, H1n, H2, H2, 1, H1n, 1, H1n, rel_w2, agent);
     bw.dw = gemm_p(DZ2, H1, nullptr, nullptr, H2, H1n, B, 1, H2, H1n, 1, H1n, 0);
-    bw.dw.kchunk = balanced_kc(B, grad_kc());
+    bw.dw.kchunk = balanced_kc(B, kGradKC);
     bw.H1 = H1; bw.XH1 = XH1; bw.g1 = g1; bw.DY1 = DY1; bw.DXH1 = DXH1; bw.PS1 = PS1;
     bw.F = H1n; bw.ntn = bw.dh.tiles_n;
     bw.w2_off = w2_off;
@@ -2018,14 +1729,12 @@ bool spec_shape(const Job& j) { return !g_sc_no_spec && j.H1 == 400 && j.H2 == 3
 // One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in five launches; either may be
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
 // computes exactly what the actor phase followed by the critic phase would.
-int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja);
 
 int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
     const Job& A = jc ? *jc : *ja;  // the first job (placeholder arguments for an absent one)
     const Job& Z = ja ? *ja : *jc;
     if (jc && ja && (jc->B != ja->B || jc->in != ja->in || jc->na != ja->na || jc->H1 != ja->H1 || jc->H2 != ja->H2))
         return fail(-5, "flock_sc_round: the two updates must have the same shapes");
-    if (const int fr = launch_round_fused(st, jc, ja); fr != 1) return fr;  // the three-launch round (or its error)
     const int C = A.C, rb = A.rb;
     int rc = 0;
     {  // 1: fc1 rows
@@ -2105,118 +1814,6 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
     return launched();
 }
 
-// FLOCK_SC_FUSE=0 (read once) or flock_set_diag("sc_no_fuse", 1): the five-launch rounds everywhere (A/B and the
-// bitwise tests of the fused rounds)
-bool g_sc_no_fuse = false;
-int g_sc_fuse_k1 = -1;  // flock_set_diag("sc_fuse_k1", 0 / 1); -1: FLOCK_SC_FUSE
-int fuse_env() {
-    static const int v = [] {
-        const char* e = getenv("FLOCK_SC_FUSE");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-bool fuse_rounds() { return fuse_env() != 0 && !g_sc_no_fuse; }
-// FLOCK_SC_FUSE=2: the k1 row blocks join the forward launch too (two launches per round)
-bool fuse_k1() { return g_sc_fuse_k1 >= 0 ? g_sc_fuse_k1 != 0 : fuse_env() == 2; }
-
-// The fused three-launch round (see sc_fwd / sc_bwdg) where its instantiation covers the shapes: the reference's
-// widths (fc1 400, fc2 300, 2 actions: the specialised row kernels), the forward GEMMs on the (k-contiguous,
-// k-contiguous) panel loaders at 7 float4 per operand (balanced K chunks of 200), the bwd launch's fast variant and
-// B <= 512 (16 row tiles). Returns 1 when the shapes are not covered (the caller runs the five launches).
-int launch_round_fused(hipStream_t st, const Job* jc, const Job* ja) {
-    const Job& A = jc ? *jc : *ja;
-    const Job& Z = ja ? *ja : *jc;
-    const bool both = jc && ja;
-    if (!fuse_rounds() || !spec_shape(A) || A.B > kSyncTiles * kT || A.rb > 65535) return 1;
-    GemmBatch gb;
-    gb.n = 0;
-    if (jc)
-        for (int i = 0; i < jc->nfwd; ++i) {
-            gb.p[gb.n] = jc->fwd[i];
-            gb.p[gb.n++].sig = jc->w.SYNC;
-        }
-    if (ja)
-        for (int i = 0; i < ja->nfwd; ++i) {
-            gb.p[gb.n] = ja->fwd[i];
-            gb.p[gb.n++].sig = ja->w.SYNC;
-        }
-    int kc = 8, tiles = 0;
-    for (int i = 0; i < gb.n; ++i) {
-        if (gemm_variant(gb.p[i]) != 0) return 1;
-        const int c = gemm_kc(gb.p[i].K, gb.p[i].kchunk);
-        kc = c > kc ? c : kc;
-        tiles = gb.p[i].tiles > tiles ? gb.p[i].tiles : tiles;
-    }
-    if (nf_of(kc) != 7) return 1;
-    int kh = 8, kw = 8;
-    for (const BwdJob* b : {&A.bw, &Z.bw}) {
-        if (gemm_variant(b->dh) != 1 || gemm_variant(b->dw) != 2) return 1;
-        const int ch = gemm_kc(b->dh.K, b->dh.kchunk), cw = gemm_kc(b->dw.K, b->dw.kchunk);
-        kh = ch > kh ? ch : kh;
-        kw = cw > kw ? cw : kw;
-    }
-    if (nf_of(kh) != 7 || nf_of(kw) != 4) return 1;
-    if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks || A.bw.nblk > kMaxRedBlocks) return 1;
-    int rc = 0;
-    const int rb = A.rb, tile_rows = (A.B + kT - 1) / kT;
-    const bool k1f = fuse_k1();
-    if (!k1f) {  // 1: fc1 rows (the unfused row launch)
-        const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
-        const size_t lds = zmax(A.lds1, Z.lds1);
-        const dim3 grid(rb, npc + npa);
-        if ((rc = allow_lds(sc_k1<7, 400>, lds))) return rc;
-        hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a);
-        if ((rc = launched())) return rc;
-    }
-    {  // 2: [fc1 rows +] forward GEMM tiles + the k3 rows
-        K3Side kcs{jc ? jc->w : A.w, jc ? jc->a : A.a, jc ? rb : 0, (unsigned)(3 * gb.p[0].tiles_n)};
-        K3Side kas{ja ? ja->w : A.w, ja ? ja->a : A.a, ja ? rb : 0, (unsigned)(2 * gb.p[0].tiles_n)};
-        if (k1f)  // each problem's A rows come from one k1 path of its job: critic 0, 1, 2 then actor 0, 1
-            for (int i = 0; i < gb.n; ++i) {
-                const bool crit = jc && i < jc->nfwd;
-                const int path = crit ? i : i - (jc ? jc->nfwd : 0);
-                gb.p[i].wait = (crit ? jc->w.SYNC : ja->w.SYNC) + kSyncK1 + 16 * path;
-            }
-        const int nk3 = kcs.nb + kas.nb, nk1 = k1f ? (jc ? 3 * rb : 0) + (ja ? 2 * rb : 0) : 0;
-        const int ny1 = (nk1 + tiles - 1) / tiles;
-        const dim3 grid(tiles, ny1 + gb.n + (nk3 + tiles - 1) / tiles);
-        size_t lds = zmax(gemm_lds_bytes(kc, kc), zmax(A.lds3, Z.lds3));
-        if (k1f) lds = zmax(lds, zmax(A.lds1, Z.lds1));
-        SyncReset sr{A.w.SYNC + kSyncDone, grid.x * grid.y,
-                     {jc ? jc->w.SYNC : nullptr, ja ? ja->w.SYNC : nullptr,
-                      jc ? jc->w.SYNC + kSyncK1 : nullptr, ja ? ja->w.SYNC + kSyncK1 : nullptr},
-                     {jc ? tile_rows : 0, ja ? tile_rows : 0, jc && k1f ? 16 * 3 : 0, ja && k1f ? 16 * 2 : 0}};
-        if (k1f) {
-            if ((rc = allow_lds(sc_fwd<0, 0, 7, 5, 300, 2, true>, lds))) return rc;
-            hipLaunchKernelGGL((sc_fwd<0, 0, 7, 5, 300, 2, true>), grid, dim3(256), lds, st, gb, kcs, kas, sr, ny1);
-        } else {
-            if ((rc = allow_lds(sc_fwd<0, 0, 7, 5, 300, 2, false>, lds))) return rc;
-            hipLaunchKernelGGL((sc_fwd<0, 0, 7, 5, 300, 2, false>), grid, dim3(256), lds, st, gb, kcs, kas, sr, 0);
-        }
-        if ((rc = launched())) return rc;
-    }
-    // 3: bwd blocks + gradient / Adam blocks
-    Bwd2 bb;
-    bb.j0 = A.bw;
-    bb.j1 = Z.bw;
-    bb.nb0 = bwd_blocks(A.bw);
-    GradAdam2 gg;
-    gg.j0 = A.ga;
-    gg.j1 = Z.ga;
-    gg.nb0 = late_blocks(A.ga);
-    BwdSync bs{{A.w.SYNC + kSyncBwd, Z.w.SYNC + kSyncBwd}, {A.w.SYNC + kSyncErr, Z.w.SYNC + kSyncErr},
-               {bb.nb0, both ? bwd_blocks(Z.bw) : 0}};
-    const int nb = bs.nbw[0] + bs.nbw[1] + gg.nb0 + (both ? late_blocks(Z.ga) : 0);
-    const size_t lds = zmax(zmax(bwd_lds(A.bw), bwd_lds(Z.bw)), red_lds(A.B));
-    SyncReset sr{A.w.SYNC + kSyncDone, (unsigned)nb, {A.w.SYNC + kSyncBwd, Z.w.SYNC + kSyncBwd, nullptr, nullptr},
-                 {1, both ? 1 : 0, 0, 0}};
-    if ((rc = allow_lds(sc_bwdg<0, 1, 1, 1, 7, 4>, lds))) return rc;
-    hipLaunchKernelGGL((sc_bwdg<0, 1, 1, 1, 7, 4>), dim3(nb), dim3(256), lds, st, bb, gg, bs, sr);
-    return launched();
-}
-
-
 __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx,
                                                int64_t* agent_out, int64_t agent) {
     const int r = blockIdx.x * 256 + threadIdx.x;
@@ -2287,20 +1884,10 @@ __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows
     if (threadIdx.x == 0) __hip_atomic_store(gate, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// gate mode 2: ONE wave on the learner stream waits for gate[0] >= seq (gate_wait's bounded poll); the round's launches
-// follow it on the same stream, so no round block ever spins and only this wave holds a slot while the env runs. The
-// round reads the staged rows and the agent index `sc1` (c1_body, ld_sc1 of every *agent), so the hand-off holds
-// whatever the kernel boundary does to the other XCDs' L2.
-__global__ __launch_bounds__(64) void sc_gate_kernel(unsigned long long* gate, unsigned long long seq) {
-    (void)gate_wait(gate, seq);
-}
-
 }  // namespace
 
 // the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
 void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
-void flock_sc_diag_no_fuse(bool v) { g_sc_no_fuse = v; }
-void flock_sc_diag_fuse_k1(int v) { g_sc_fuse_k1 = v; }
 
 extern "C" {
 
@@ -2403,38 +1990,28 @@ int flock_sc_round(void* stream, const FlockScUpdate* critic_u, const FlockScUpd
 
 // ---------------------------------------------------------------------------------------------------------------
 // learn() pipeline: the config-3 loop's per-step learner work in one call (see include/flock_learn.h). Rounds are
-// replayed from HIP graphs captured once: merged[s] = critic phase of slot s + actor phase of slot s - 1 (mod n),
-// conly[s] / aonly[s] = one phase alone.
+// launched directly from arguments built once per slot (round = critic phase of slot s + actor phase of the previous
+// learn's slot: five hipLaunchKernel; replaying the same rounds from HIP graphs measured 0.125 against 0.117 ms per
+// config-3 step in round 2, so there is no graph path).
 constexpr int kMaxSlots = 8;
 struct FlockScPipeline {
     int n;
     FlockScUpdate u[kMaxSlots];
     FlockScRows ring, staging[kMaxSlots];
-    hipGraphExec_t merged[kMaxSlots], conly[kMaxSlots], aonly[kMaxSlots];
-    Job jc[kMaxSlots], ja[kMaxSlots];  // direct launches (graphs == false): the rounds' arguments, built once
-    bool graphs;
-    int diag;  // -DFLOCK_SC_PIPELINE_DIAG=<bits> builds only (timing diagnostics; results are wrong): 1 no learner wait on the
-               // snapshot, 2 no env wait on the slot, 3 neither
+    Job jc[kMaxSlots], ja[kMaxSlots];  // the rounds' launch arguments, built once
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
-    // device-side snapshot gate (direct launches, single GPU): gate[0] the published sequence number, gate[1] the
-    // error word of a waiter that gave up; seq counts this pipeline's snapshots. NULL: cross-queue event waits.
-    // gate_mode 1: the critic phase's k1 row blocks poll; 2: one wave on the learner stream (sc_gate_kernel) polls
+    // device-side snapshot gate: gate[0] the published sequence number, gate[1] the error word of a waiter that gave
+    // up; seq counts this pipeline's snapshots. gate_on: the critic phase's row blocks poll gate[0] (single GPU, not
+    // under counter collection); otherwise the learner stream waits for each snapshot on a cross-queue event.
     unsigned long long* gate;
     unsigned long long seq;
-    int gate_mode;
+    bool gate_on;
     bool used[kMaxSlots];
     int slot;
-    int acquired;  // flock_sc_pipeline_acquire's slot (its ring copy may be written), -1 otherwise
-    // copy learns (flock_sc_pipeline_learn_copy): the snapshots run on a stream of their own (created at the first
-    // copy learn); copy_written[c]: env step into ring copy c done (env stream), copy_read[c]: the snapshot that read
-    // copy c done (snapshot stream)
-    hipStream_t snap_stream;
-    hipEvent_t copy_written[kMaxSlots], copy_read[kMaxSlots];
-    bool copy_used[kMaxSlots];
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
     int64_t pending_agent;
-    // data-parallel rounds (flock_sc_pipeline_set_dp): gradients into the [critic | actor] bucket, the caller's
-    // all-reduce of the part a round wrote, then the Adam launch with grad_scale
+    // data-parallel rounds (flock_sc_pipeline_set_dp): gradients into the bucket, the caller's all-reduce of the part a
+    // round wrote, then the Adam launch with grad_scale
     bool dp;
     FlockScUpdate ug[kMaxSlots], uadam[kMaxSlots];
     float* bucket;
@@ -2442,43 +2019,79 @@ struct FlockScPipeline {
     const float* grad_scale;
     FlockAllreduceFn allreduce;
     void* allreduce_ctx;
+    // the actor half off the learner chain (flock_sc_pipeline_set_dp_actor): each slot's actor gradient in a buffer of
+    // its own, all-reduced and stepped on actor_stream through the second callback
+    bool split;
+    hipStream_t actor_stream;
+    hipEvent_t grads_done[kMaxSlots], actor_done[kMaxSlots], actor_joined;
+    bool actor_used[kMaxSlots];
+    int64_t actor_floats;
+    FlockAllreduceFn actor_allreduce;
+    void* actor_ctx;
+    int n_agents;
+    int* last_actor_slot;  // [n_agents]: the slot of the agent's last actor step on actor_stream, -1: none
 };
 
 namespace {
-int capture_round(const FlockScUpdate* uc, const FlockScUpdate* ua, hipGraphExec_t* out) {
-    hipStream_t cs;
-    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return fail(-4, "flock_sc_pipeline: stream");
-    hipGraph_t g = nullptr;
-    int rc = 0;
-    if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-        rc = fail(-4, "flock_sc_pipeline: begin capture");
-    } else {
-        rc = flock_sc_round(cs, uc, ua);
-        const hipError_t e = hipStreamEndCapture(cs, &g);
-        if (!rc && e != hipSuccess) rc = fail(-4, hipGetErrorString(e));
-        if (!rc && hipGraphInstantiate(out, g, nullptr, nullptr, 0) != hipSuccess)
-            rc = fail(-4, "flock_sc_pipeline: graph instantiate");
-    }
-    if (g) (void)hipGraphDestroy(g);
-    (void)hipStreamDestroy(cs);
-    return rc;
+bool counter_collection() {  // rocprofv3 counter collection serialises dispatches: no spinning consumers under it
+    const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
+    return pmc && pmc[0] && pmc[0] != '0';
 }
-// one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none)
-int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a) {
-    if (p->dp) {
+
+// the learner stream waits for an event unless the host already sees it complete (a completed event's writes are
+// visible to every later launch: the producer kernel's end released them)
+int wait_unless_done(hipStream_t st, hipEvent_t ev) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return fail(-4, "flock_sc_pipeline: event query");
+    return hipStreamWaitEvent(st, ev, 0) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: stream wait");
+}
+
+// the actor step of `agent` that is still in flight on actor_stream (split data-parallel rounds): every reader of
+// that agent's actor, target actor, moments or step count on the learner stream waits for it
+int wait_actor(FlockScPipeline* p, hipStream_t ls, int64_t agent) {
+    if (!p->split || agent < 0 || agent >= p->n_agents) return 0;
+    const int s = p->last_actor_slot[agent];
+    return s >= 0 ? wait_unless_done(ls, p->actor_done[s]) : 0;
+}
+
+// one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none);
+// agents: the learns' agent indices (split data-parallel rounds)
+int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a, int64_t agent_c, int64_t agent_a) {
+    if (!p->dp) return launch_round(ls, c >= 0 ? &p->jc[c] : nullptr, a >= 0 ? &p->ja[a] : nullptr);
+    int rc = 0;
+    if (!p->split) {
         // gradients only (do_adam = 0) into the bucket, ONE all-reduce (sum) of the part they wrote, then the Adam
         // launch (gradients scaled by *grad_scale): SharedCriticLearner._dp_round
-        int rc = flock_sc_round(ls, c >= 0 ? &p->ug[c] : nullptr, a >= 0 ? &p->ug[a] : nullptr);
-        if (rc) return rc;
+        if ((rc = flock_sc_round(ls, c >= 0 ? &p->ug[c] : nullptr, a >= 0 ? &p->ug[a] : nullptr))) return rc;
         const int64_t lo = c >= 0 ? 0 : p->actor_off, hi = a >= 0 ? p->bucket_floats : p->critic_floats;
         if ((rc = p->allreduce(p->allreduce_ctx, p->bucket + lo, hi - lo, ls)))
             return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
         return flock_sc_round_adam(ls, c >= 0 ? &p->uadam[c] : nullptr, a >= 0 ? &p->uadam[a] : nullptr,
                                    p->grad_scale);
     }
-    if (!p->graphs) return launch_round(ls, c >= 0 ? &p->jc[c] : nullptr, a >= 0 ? &p->ja[a] : nullptr);
-    hipGraphExec_t g = c >= 0 && a >= 0 ? p->merged[c] : (c >= 0 ? p->conly[c] : p->aonly[a]);
-    return hipGraphLaunch(g, ls) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: graph launch failed");
+    // split: the critic half stays on the learner chain (the next critic phase needs this critic step); the actor
+    // half is all-reduced and stepped on actor_stream (that actor is read again only by its agent's next learn)
+    if ((rc = wait_actor(p, ls, agent_c))) return rc;
+    if (a >= 0 && p->actor_used[a] && (rc = wait_unless_done(ls, p->actor_done[a]))) return rc;  // slot a's buffer
+    if ((rc = flock_sc_round(ls, c >= 0 ? &p->ug[c] : nullptr, a >= 0 ? &p->ug[a] : nullptr))) return rc;
+    if (a >= 0) {
+        hipStream_t as = p->actor_stream;
+        if (hipEventRecord(p->grads_done[a], ls) != hipSuccess || hipStreamWaitEvent(as, p->grads_done[a], 0) != hipSuccess)
+            return fail(-4, "flock_sc_pipeline: stream operation failed");
+        if ((rc = p->actor_allreduce(p->actor_ctx, p->ug[a].actor_grad_out, p->actor_floats, as)))
+            return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the actor all-reduce callback failed");
+        if ((rc = flock_sc_round_adam(as, nullptr, &p->uadam[a], p->grad_scale))) return rc;
+        if (hipEventRecord(p->actor_done[a], as) != hipSuccess) return fail(-4, "flock_sc_pipeline: event record");
+        p->actor_used[a] = true;
+        p->last_actor_slot[agent_a] = a;
+    }
+    if (c >= 0) {
+        if ((rc = p->allreduce(p->allreduce_ctx, p->bucket, p->critic_floats, ls)))
+            return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
+        if ((rc = flock_sc_round_adam(ls, &p->uadam[c], nullptr, p->grad_scale))) return rc;
+    }
+    return 0;
 }
 }  // namespace
 
@@ -2509,65 +2122,36 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     FlockScPipeline* p = new FlockScPipeline();
     p->n = n_slots;
     p->ring = *ring;
-    for (int i = 0; i < n_slots; ++i) {
-        p->u[i] = slots[i];
-        p->staging[i] = staging[i];
-    }
-    // rounds launched directly from arguments built here (6 hipLaunchKernel per round), or replayed as HIP graphs
-    // (FLOCK_SC_PIPELINE_GRAPHS=1, read here once): config-3 step 0.117 ms direct vs 0.125 ms with graphs
-    const char* ge = getenv("FLOCK_SC_PIPELINE_GRAPHS");
-    p->graphs = ge && ge[0] == '1';
-#ifdef FLOCK_SC_PIPELINE_DIAG
-    p->diag = FLOCK_SC_PIPELINE_DIAG;  // a diagnostics build (tools/build_variant.sh): drops stream dependencies
-#else
-    p->diag = 0;  // the shipped library never skips a dependency
-#endif
     int rc = 0;
     for (int i = 0; i < n_slots && !rc; ++i) {
+        p->u[i] = slots[i];
+        p->staging[i] = staging[i];
         critic_job(&p->u[i], p->jc[i]);
         actor_job(&p->u[i], p->ja[i]);
-        if (p->graphs) {
-            rc = capture_round(&p->u[i], nullptr, &p->conly[i]);
-            if (!rc) rc = capture_round(nullptr, &p->u[i], &p->aonly[i]);
-            if (!rc) rc = capture_round(&p->u[i], &p->u[(i + n_slots - 1) % n_slots], &p->merged[i]);
-        }
-        hipEvent_t* evs[2] = {&p->snap_done[i], &p->slot_free[i]};
+        hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};
         for (hipEvent_t* e : evs)
             if (!rc && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
                 rc = fail(-4, "flock_sc_pipeline_create: event");
         p->used[i] = false;
+        p->actor_used[i] = false;
     }
     p->slot = 0;
-    p->acquired = -1;
-    p->snap_stream = nullptr;
-    for (int i = 0; i < kMaxSlots; ++i) {
-        p->copy_written[i] = p->copy_read[i] = nullptr;
-        p->copy_used[i] = false;
-    }
     p->pending = -1;
     p->pending_agent = -1;
     p->dp = false;
+    p->split = false;
+    p->actor_stream = nullptr;
+    p->actor_joined = nullptr;
+    p->last_actor_slot = nullptr;
+    p->n_agents = 0;
     p->gate = nullptr;
     p->seq = 0;
-    // the learner stream's wait for each snapshot: a cross-queue event wait (0, the default), or on the device
-    // (FLOCK_SC_GATE=1: the critic phase's row blocks poll gate[0]; 2: one wave launched before the round polls it).
-    // Round 4, same-box interleaved A/B at config 3 (profiles/r04/eval1): event 0.0819-0.0825 ms per step, gate 2
-    // 0.0826-0.0839. The spin needs the two queues' kernels to run concurrently: under rocprofv3 counter collection
-    // (ROCPROF_COUNTER_COLLECTION, which serialises dispatches) a round dispatched ahead of its snapshot would wait out
-    // its bound, so the event waits are forced there. Graph replays and data-parallel rounds keep the events.
-    const char* gte = getenv("FLOCK_SC_GATE");
-    const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
-    const bool pmc_on = pmc && pmc[0] && pmc[0] != '0';
-    p->gate_mode = pmc_on ? 0 : gte ? atoi(gte) : 0;
-    if (p->gate_mode < 0 || p->gate_mode > 2) p->gate_mode = 0;
-    // the gate words exist whenever a device-side wait may be used: the snapshot learns' gate modes and the copy
-    // learns (flock_sc_pipeline_learn_copy), not under counter collection
-    if (!rc && !p->graphs && p->diag == 0 && !pmc_on) {
-        if (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
-            hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess)
-            rc = fail(-4, "flock_sc_pipeline_create: gate");
-    }
+    p->gate_on = false;
+    if (!rc && (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
+                hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
+                hipDeviceSynchronize() != hipSuccess))
+        rc = fail(-4, "flock_sc_pipeline_create: gate");
+    if (!rc) (void)flock_sc_pipeline_set_gate(p, 1);  // the default hand-off
     if (rc) {
         flock_sc_pipeline_destroy(p);
         return nullptr;
@@ -2575,37 +2159,32 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     return p;
 }
 
-namespace {
-// gate mode 2: the learner stream's wait for this learn's snapshot (the seq just published by pipeline_learn)
-int gate_kernel(FlockScPipeline* p, hipStream_t ls, bool always = false) {
-    if (!p->gate || p->dp || (!always && p->gate_mode != 2)) return 0;
-    hipLaunchKernelGGL(sc_gate_kernel, dim3(1), dim3(64), 0, ls, p->gate, p->seq);
-    return launched();
+int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on) {
+    if (!p) return fail(-3, "flock_sc_pipeline_set_gate: NULL pipeline");
+    p->gate_on = on != 0 && p->gate && !p->dp && !counter_collection();
+    return p->gate_on ? 1 : 0;
 }
-}  // namespace
 
 namespace {
-// the rounds of a learn() whose critic phase (slot s) reads inputs the learner stream already waits for: the critic
-// phase of s beside the actor phase of the previous learn, or one after the other (same agent). gated: gate mode 2's
-// polling wave goes in front of the critic phase (snapshot learns only)
-int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent, bool gated, bool poll = false) {
+// the rounds of a learn() whose critic phase (slot s) reads inputs the learner stream can use (after its event wait
+// or its row blocks' gate): the critic phase of s beside the actor phase of the previous learn, or one after the other
+// (same agent)
+int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent) {
     const int n = p->n;
     int rc = 0;
     bool ok = true;
     const int q = p->pending;
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
         // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
-        if (gated && (rc = gate_kernel(p, ls, poll))) return rc;
-        if ((rc = pipeline_round(p, ls, s, q))) return rc;
+        if ((rc = pipeline_round(p, ls, s, q, agent, p->pending_agent))) return rc;
         ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
     } else {
         // same agent (this critic phase reads the target actor that actor phase soft-updates): one after the other
         if (q >= 0) {
-            if ((rc = pipeline_round(p, ls, -1, q))) return rc;
+            if ((rc = pipeline_round(p, ls, -1, q, -1, p->pending_agent))) return rc;
             ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
         }
-        if (ok && gated && (rc = gate_kernel(p, ls, poll))) return rc;
-        if (ok && (rc = pipeline_round(p, ls, s, -1))) return rc;
+        if (ok && (rc = pipeline_round(p, ls, s, -1, agent, -1))) return rc;
     }
     if (!ok) return fail(-4, "flock_sc_pipeline: stream operation failed");
     p->pending = s;
@@ -2619,30 +2198,18 @@ int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent, boo
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent) {
     if (!p) return fail(-3, "flock_sc_pipeline_learn: NULL pipeline");
+    if (rows < 1 || agent < 0) return fail(-5, "flock_sc_pipeline_learn: need rows >= 1 and an agent");
+    if (p->split && agent >= p->n_agents) return fail(-5, "flock_sc_pipeline_learn: agent out of range");
     hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
     const int s = p->slot;
     const FlockScUpdate& u = p->u[s];
-    p->acquired = -1;
-    if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
+    if (p->used[s] && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
-    {  // the critic phase reads the slot's staging rows through the identity index (a direct learn may have run)
-        RowArgs& a = p->jc[s].a;
-        a.idx = u.idx;
-        a.rs = u.ring_state;
-        a.rs2 = u.ring_new_state;
-        a.ra = u.ring_action;
-        a.rr = u.ring_reward;
-        a.rt = u.ring_terminal;
-        a.rows = 0;
-        a.agent_val = -1;
-        a.gate = nullptr;
-    }
     int rc = 0;
-    bool ok = true;
-    const bool gated = p->gate && p->gate_mode && !p->dp;
-    if (gated) {
-        // the snapshot publishes gate[0] = seq; this learn's critic row blocks wait for it on the device
-        if (u.B < 1 || rows < 1) return fail(-5, "flock_sc_pipeline_learn: need B, rows >= 1");
+    if (p->gate_on) {
+        // the snapshot publishes gate[0] = seq after its write-through stores; this learn's critic row blocks wait
+        // for it on the device. No deadlock whatever the streams' hardware queues: the snapshot is enqueued before
+        // the round that waits for it, and nothing on the env stream waits for that round
         const FlockScRows& src = p->ring;
         const FlockScRows& dst = p->staging[s];
         int vec = u.in_dim == 4 && u.n_actions == 2;
@@ -2652,122 +2219,17 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
                            const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq);
         if ((rc = launched())) return rc;
-        p->jc[s].a.gate = p->gate_mode == 1 ? p->gate : nullptr;
+        p->jc[s].a.gate = p->gate;
         p->jc[s].a.gate_seq = seq;
     } else {
-#ifndef FLOCK_SC_DIAG_NOSNAP  // timing-only builds (results wrong): no snapshot kernel on the env stream
-        rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
-                                    u.in_dim, u.n_actions, &p->ring, &p->staging[s]);
-#endif
-        if (rc) return rc;
-        ok = hipEventRecord(p->snap_done[s], es) == hipSuccess &&
-             ((p->diag & 1) || hipStreamWaitEvent(ls, p->snap_done[s], 0) == hipSuccess);
+        if ((rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
+                                         u.in_dim, u.n_actions, &p->ring, &p->staging[s])))
+            return rc;
+        p->jc[s].a.gate = nullptr;
+        if (hipEventRecord(p->snap_done[s], es) != hipSuccess || hipStreamWaitEvent(ls, p->snap_done[s], 0) != hipSuccess)
+            return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     }
-    if (!ok) return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
-    return enqueue_rounds(p, ls, s, agent, gated);
-}
-
-int flock_sc_pipeline_acquire(FlockScPipeline* p, void* env_stream) {
-    if (!p) return fail(-3, "flock_sc_pipeline_acquire: NULL pipeline");
-    const int s = p->slot;
-    if (p->used[s] && !(p->diag & 2) && hipStreamWaitEvent((hipStream_t)env_stream, p->slot_free[s], 0) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_acquire: wait");
-    p->acquired = s;
-    return s;
-}
-
-int flock_sc_pipeline_learn_direct(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
-                                   uint64_t seed, uint64_t counter, int64_t agent, const FlockScRows* ring) {
-    if (!p || !ring) return fail(-3, "flock_sc_pipeline_learn_direct: NULL argument");
-    if (p->dp || p->graphs)
-        return fail(-5, "flock_sc_pipeline_learn_direct: not with data-parallel rounds or graph replays");
-    if (!ring->state || !ring->new_state || !ring->action || !ring->reward || !ring->terminal)
-        return fail(-3, "flock_sc_pipeline_learn_direct: NULL field pointer");
-    if (rows < 1 || agent < 0) return fail(-5, "flock_sc_pipeline_learn_direct: need rows >= 1 and an agent");
-    const int s = p->slot;
-    if (p->acquired != s)
-        return fail(-5, "flock_sc_pipeline_learn_direct: flock_sc_pipeline_acquire must precede the env step that "
-                        "writes the ring copy");
-    p->acquired = -1;
-    hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
-    RowArgs& a = p->jc[s].a;
-    a.idx = nullptr;
-    a.rs = ring->state;
-    a.rs2 = ring->new_state;
-    a.ra = ring->action;
-    a.rr = ring->reward;
-    a.rt = ring->terminal;
-    a.seed = seed;
-    a.counter = counter;
-    a.rows = rows;
-    a.agent_val = agent;
-    a.gate = nullptr;
-    if (hipEventRecord(p->snap_done[s], es) != hipSuccess ||
-        (!(p->diag & 1) && hipStreamWaitEvent(ls, p->snap_done[s], 0) != hipSuccess))
-        return fail(-4, "flock_sc_pipeline_learn_direct: stream operation failed");
-    return enqueue_rounds(p, ls, s, agent, false);
-}
-
-int flock_sc_pipeline_copy_acquire(FlockScPipeline* p, void* env_stream, int copy) {
-    if (!p) return fail(-3, "flock_sc_pipeline_copy_acquire: NULL pipeline");
-    if (copy < 0 || copy >= kMaxSlots) return fail(-5, "flock_sc_pipeline_copy_acquire: copy out of range");
-    if (p->copy_used[copy] && hipStreamWaitEvent((hipStream_t)env_stream, p->copy_read[copy], 0) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_copy_acquire: wait");
-    return 0;
-}
-
-int flock_sc_pipeline_learn_copy(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows,
-                                 uint64_t seed, uint64_t counter, int64_t agent, int copy, const FlockScRows* ring) {
-    if (!p || !ring) return fail(-3, "flock_sc_pipeline_learn_copy: NULL argument");
-    if (!flock_sc_pipeline_copy_ok(p))
-        return fail(-5, "flock_sc_pipeline_learn_copy: needs the device gate (not with data-parallel rounds, graph "
-                        "replays or under counter collection)");
-    if (copy < 0 || copy >= kMaxSlots) return fail(-5, "flock_sc_pipeline_learn_copy: copy out of range");
-    if (!ring->state || !ring->new_state || !ring->action || !ring->reward || !ring->terminal)
-        return fail(-3, "flock_sc_pipeline_learn_copy: NULL field pointer");
-    const int s = p->slot;
-    const FlockScUpdate& u = p->u[s];
-    if (u.B < 1 || rows < 1) return fail(-5, "flock_sc_pipeline_learn_copy: need B, rows >= 1");
-    hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
-    p->acquired = -1;
-    if (!p->snap_stream && hipStreamCreateWithFlags(&p->snap_stream, hipStreamNonBlocking) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_learn_copy: stream");
-    for (hipEvent_t* e : {&p->copy_written[copy], &p->copy_read[copy]})
-        if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
-            return fail(-4, "flock_sc_pipeline_learn_copy: event");
-    hipStream_t ss = p->snap_stream;
-    // snapshot stream: after the env step that wrote the copy, and once the slot's previous learn() is done with its
-    // staging rows, the minibatch snapshot (copy -> staging, published through the gate); the copy is free again
-    // after it
-    if (hipEventRecord(p->copy_written[copy], es) != hipSuccess || hipStreamWaitEvent(ss, p->copy_written[copy], 0) ||
-        (p->used[s] && hipStreamWaitEvent(ss, p->slot_free[s], 0) != hipSuccess))
-        return fail(-4, "flock_sc_pipeline_learn_copy: stream operation failed");
-    {  // the critic phase reads the slot's staging rows (identity index), the agent index from *u.agent
-        RowArgs& a = p->jc[s].a;
-        a.idx = u.idx;
-        a.rs = u.ring_state;
-        a.rs2 = u.ring_new_state;
-        a.ra = u.ring_action;
-        a.rr = u.ring_reward;
-        a.rt = u.ring_terminal;
-        a.rows = 0;
-        a.agent_val = -1;
-        a.gate = nullptr;
-    }
-    const FlockScRows& dst = p->staging[s];
-    int vec = u.in_dim == 4 && u.n_actions == 2;
-    for (const FlockScRows* x : {ring, &dst})
-        vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
-    const unsigned long long seq = ++p->seq;
-    hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, ss, u.B, rows, seed, counter,
-                       const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, *ring, dst, vec, p->gate, seq);
-    int rc = launched();
-    if (rc) return rc;
-    if (hipEventRecord(p->copy_read[copy], ss) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_learn_copy: stream operation failed");
-    p->copy_used[copy] = true;
-    // learner stream: one polling wave for this snapshot's sequence number, then the rounds
-    return enqueue_rounds(p, ls, s, agent, true, true);
+    return enqueue_rounds(p, ls, s, agent);
 }
 
 int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_offset,
@@ -2782,6 +2244,7 @@ int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_f
     if (((uintptr_t)(bucket + actor_offset) & 15) != 0)
         return fail(-5, "flock_sc_pipeline_set_dp: the actor part of the bucket must be 16-B aligned");
     p->dp = true;
+    p->gate_on = false;  // data-parallel rounds wait for their snapshots on events
     p->bucket = bucket;
     p->critic_floats = critic_floats;
     p->actor_off = actor_offset;
@@ -2801,15 +2264,52 @@ int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_f
     return 0;
 }
 
+int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads, int n_agents,
+                                   FlockAllreduceFn allreduce, void* ctx) {
+    if (!p || !actor_grads || !allreduce) return fail(-3, "flock_sc_pipeline_set_dp_actor: NULL argument");
+    if (!p->dp) return fail(-5, "flock_sc_pipeline_set_dp_actor: call flock_sc_pipeline_set_dp first");
+    if (p->used[0] || p->pending >= 0) return fail(-5, "flock_sc_pipeline_set_dp_actor: the pipeline has already learned");
+    if (n_agents < 1) return fail(-5, "flock_sc_pipeline_set_dp_actor: n_agents >= 1");
+    const FlockScUpdate& u0 = p->u[0];
+    for (int i = 0; i < p->n; ++i) {
+        if (!actor_grads[i] || ((uintptr_t)actor_grads[i] & 15) != 0)
+            return fail(-5, "flock_sc_pipeline_set_dp_actor: one 16-B aligned actor gradient buffer per slot");
+        for (int j = 0; j < i; ++j)
+            if (actor_grads[i] == actor_grads[j])
+                return fail(-5, "flock_sc_pipeline_set_dp_actor: the slots' buffers must differ");
+    }
+    if (!p->actor_stream && (hipStreamCreateWithFlags(&p->actor_stream, hipStreamNonBlocking) != hipSuccess ||
+                             hipEventCreateWithFlags(&p->actor_joined, hipEventDisableTiming) != hipSuccess))
+        return fail(-4, "flock_sc_pipeline_set_dp_actor: stream");
+    delete[] p->last_actor_slot;
+    p->last_actor_slot = new int[n_agents];
+    for (int i = 0; i < n_agents; ++i) p->last_actor_slot[i] = -1;
+    p->n_agents = n_agents;
+    p->actor_floats = actor_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).total;
+    for (int i = 0; i < p->n; ++i) {
+        p->ug[i].actor_grad_out = actor_grads[i];
+        p->uadam[i].actor_grad_out = actor_grads[i];
+    }
+    p->actor_allreduce = allreduce;
+    p->actor_ctx = ctx;
+    p->split = true;
+    return 0;
+}
+
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream) {
     if (!p) return fail(-3, "flock_sc_pipeline_flush: NULL pipeline");
-    const int q = p->pending;
-    if (q < 0) return 0;
     hipStream_t ls = (hipStream_t)learner_stream;
-    if (int rc = pipeline_round(p, ls, -1, q)) return rc;
-    if (hipEventRecord(p->slot_free[q], ls) != hipSuccess)
+    const int q = p->pending;
+    if (q >= 0) {
+        if (int rc = pipeline_round(p, ls, -1, q, -1, p->pending_agent)) return rc;
+        if (hipEventRecord(p->slot_free[q], ls) != hipSuccess)
+            return fail(-4, "flock_sc_pipeline_flush: stream operation failed");
+        p->pending = -1;
+    }
+    // split rounds: the learner stream joins the actor stream, so synchronising the learner stream covers every step
+    if (p->split && (hipEventRecord(p->actor_joined, p->actor_stream) != hipSuccess ||
+                     hipStreamWaitEvent(ls, p->actor_joined, 0) != hipSuccess))
         return fail(-4, "flock_sc_pipeline_flush: stream operation failed");
-    p->pending = -1;
     return 0;
 }
 
@@ -2825,8 +2325,6 @@ int flock_sc_mark_read(unsigned long long* host) {
 
 int flock_sc_pipeline_check(FlockScPipeline* p) {
     if (!p) return fail(-3, "flock_sc_pipeline_check: NULL pipeline");
-    for (int i = 0; i < p->n; ++i)
-        if (int rc = flock_sc_workspace_check(&p->u[i])) return rc;
     if (!p->gate) return 0;
     unsigned long long flag = 0;
     if (hipMemcpy(&flag, p->gate + 1, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
@@ -2836,35 +2334,16 @@ int flock_sc_pipeline_check(FlockScPipeline* p) {
                 : 0;
 }
 
-int flock_sc_workspace_check(const FlockScUpdate* u) {
-    if (!u || !u->workspace) return fail(-3, "flock_sc_workspace_check: NULL argument");
-    Ws w;
-    ws_layout(u->B, u->in_dim, u->n_actions, u->fc1, u->fc2, u->workspace, &w);
-    unsigned flag = 0;
-    if (hipMemcpy(&flag, w.SYNC + kSyncErr, sizeof(flag), hipMemcpyDeviceToHost) != hipSuccess)
-        return fail(-4, "flock_sc_workspace_check: copy failed");
-    return flag ? fail(-6, "flock_sc: a fused round's block gave up waiting for its inputs (hand-off timeout); the "
-                           "update's results are invalid")
-                : 0;
-}
-
-int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate && !p->dp ? p->gate_mode : 0; }
-
-int flock_sc_pipeline_copy_ok(const FlockScPipeline* p) { return p && p->gate && !p->dp && !p->graphs ? 1 : 0; }
+int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate_on ? 1 : 0; }
 
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;
     if (p->gate) (void)hipFree(p->gate);
-    if (p->snap_stream) (void)hipStreamDestroy(p->snap_stream);
-    for (int i = 0; i < kMaxSlots; ++i) {
-        if (p->copy_written[i]) (void)hipEventDestroy(p->copy_written[i]);
-        if (p->copy_read[i]) (void)hipEventDestroy(p->copy_read[i]);
-    }
+    if (p->actor_stream) (void)hipStreamDestroy(p->actor_stream);
+    if (p->actor_joined) (void)hipEventDestroy(p->actor_joined);
+    delete[] p->last_actor_slot;
     for (int i = 0; i < p->n; ++i) {
-        hipGraphExec_t* gs[3] = {&p->merged[i], &p->conly[i], &p->aonly[i]};
-        for (hipGraphExec_t* g : gs)
-            if (*g) (void)hipGraphExecDestroy(*g);
-        hipEvent_t* evs[2] = {&p->snap_done[i], &p->slot_free[i]};
+        hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};
         for (hipEvent_t* e : evs)
             if (*e) (void)hipEventDestroy(*e);
     }

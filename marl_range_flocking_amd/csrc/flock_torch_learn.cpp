@@ -731,20 +731,6 @@ void sc_prep_meta(const Tensor& agent_out, const optional<Tensor>& idx, int64_t 
     sc_prep_checks(agent_out, idx, rows);
 }
 
-// the fused rounds' hand-off error word of a job workspace (flock_sc_workspace_check): raises if a block gave up
-void sc_check_hip(const Tensor& workspace, at::IntArrayRef dims) {
-    hip_only(workspace, "sc_check");
-    TORCH_CHECK(dims.size() == 7, "sc_check: dims [7]");
-    dense(workspace, "workspace", at::kFloat, workspace);
-    numel_is(workspace, "workspace",
-             flock_sc_workspace_floats((int)dims[0], (int)dims[1], (int)dims[2], (int)dims[3], (int)dims[4]));
-    const at::OptionalDeviceGuard g(workspace.device());
-    FlockScUpdate u{};
-    u.B = (int)dims[0], u.in_dim = (int)dims[1], u.n_actions = (int)dims[2], u.fc1 = (int)dims[3], u.fc2 = (int)dims[4];
-    u.workspace = ptr<float>(workspace);
-    rc_check(flock_sc_workspace_check(&u), "flock_sc_workspace_check");
-}
-
 // ------------------------------------------------------------------------------------------------------- sc_act
 // obs [rows, A, in] f32 contiguous; actors: the agent-major actor buffer [A * stride] (stride = numel / A);
 // actions [rows, A, 2]; ou_state / noise [rows, A, 2] (both or neither)
@@ -826,7 +812,6 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         "sc_round_adam(Tensor(a!)[] learner, Tensor(b!)[] critic_job, Tensor(c!)[] actor_job, int[] dims, "
         "float[] hyper, Tensor? grad_scale) -> ()");
     m.def("sc_prep(Tensor(a!) agent_out, Tensor(b!)? idx, int rows, int seed, int counter, int agent) -> ()");
-    m.def("sc_check(Tensor workspace, int[] dims) -> ()");
     // the workspace floats one shared-critic job needs (flock_sc_workspace_floats; no tensors: a CatchAll kernel)
     m.def("sc_workspace_floats(int B, int in_dim, int n_actions, int fc1, int fc2) -> int",
           [](int64_t B, int64_t in_dim, int64_t na, int64_t fc1, int64_t fc2) -> int64_t {
@@ -858,7 +843,6 @@ TORCH_LIBRARY_IMPL(flock, CUDA, m) {
     m.impl("sc_round_adam", &sc_round_adam_hip);
     m.impl("sc_prep", &sc_prep_hip);
     m.impl("sc_act", &sc_act_hip);
-    m.impl("sc_check", &sc_check_hip);
 }
 
 TORCH_LIBRARY_IMPL(flock, Meta, m) {

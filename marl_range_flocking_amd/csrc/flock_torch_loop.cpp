@@ -58,8 +58,9 @@ struct ScPipeline : torch::CustomClassHolder {
     at::Device device = at::Device(at::kCPU);
     int64_t batch = 0, in_dim = 0, n_actions = 0, n_agents = 0, n_slots = 0;
     // data-parallel rounds
-    c10::intrusive_ptr<c10d::ProcessGroup> pg;
+    c10::intrusive_ptr<c10d::ProcessGroup> pg, pg_actor;
     Tensor bucket, grad_scale;
+    std::vector<Tensor> actor_grads;
     std::string cb_error;
 
     // learner: the 13 state tensors; slots: n_slots jobs of 9 tensors (SharedCriticLearner._slots[i]["job"]: the
@@ -167,40 +168,6 @@ struct ScPipeline : torch::CustomClassHolder {
         check(flock_sc_pipeline_flush(pipe, reinterpret_cast<void*>(learner_stream)), "flock_sc_pipeline_flush");
     }
 
-    // direct learns (ScTrainLoop with ring copies): the slot whose ring copy the next env step may write (its wait
-    // enqueued on env_stream), then the learn() reading that copy (flock_sc_pipeline_learn_direct)
-    int64_t acquire(int64_t env_stream) {
-        const at::OptionalDeviceGuard g(device);
-        const int s = flock_sc_pipeline_acquire(pipe, reinterpret_cast<void*>(env_stream));
-        check(s < 0 ? s : 0, "flock_sc_pipeline_acquire");
-        return s;
-    }
-    // copy learns (flock_sc_pipeline_learn_copy): the snapshot of ring copy `copy` on the pipeline's own stream
-    bool copy_ok() const { return flock_sc_pipeline_copy_ok(pipe) != 0; }
-    void copy_acquire(int64_t env_stream, int64_t copy) {
-        const at::OptionalDeviceGuard g(device);
-        check(flock_sc_pipeline_copy_acquire(pipe, reinterpret_cast<void*>(env_stream), (int)copy),
-              "flock_sc_pipeline_copy_acquire");
-    }
-    void learn_copy(int64_t rows, int64_t seed, int64_t counter, int64_t agent, int64_t env_stream,
-                    int64_t learner_stream, int64_t copy, const FlockScRows& ring_copy) {
-        TORCH_CHECK(agent >= 0 && agent < n_agents, "ScPipeline.learn: agent out of range");
-        const at::OptionalDeviceGuard g(device);
-        check(flock_sc_pipeline_learn_copy(pipe, reinterpret_cast<void*>(env_stream),
-                                           reinterpret_cast<void*>(learner_stream), rows, (uint64_t)seed,
-                                           (uint64_t)counter, agent, (int)copy, &ring_copy),
-              "flock_sc_pipeline_learn_copy");
-    }
-    void learn_direct(int64_t rows, int64_t seed, int64_t counter, int64_t agent, int64_t env_stream,
-                      int64_t learner_stream, const FlockScRows& copy) {
-        TORCH_CHECK(agent >= 0 && agent < n_agents, "ScPipeline.learn: agent out of range");
-        const at::OptionalDeviceGuard g(device);
-        check(flock_sc_pipeline_learn_direct(pipe, reinterpret_cast<void*>(env_stream),
-                                             reinterpret_cast<void*>(learner_stream), rows, (uint64_t)seed,
-                                             (uint64_t)counter, agent, &copy),
-              "flock_sc_pipeline_learn_direct");
-    }
-
     // raises if a round gave up waiting for its snapshot (device-side gate timeout; its results are invalid).
     // Synchronous: call once the learner stream has been synchronised
     void verify() {
@@ -209,6 +176,48 @@ struct ScPipeline : torch::CustomClassHolder {
     }
 
     int64_t gated() const { return flock_sc_pipeline_gated(pipe); }
+
+    // the snapshot hand-off: 1 the device-side gate (the default on one GPU), 0 cross-queue event waits; returns the
+    // hand-off in use (data-parallel rounds and rocprofv3 counter collection always take the events)
+    int64_t set_gate(bool on) {
+        const at::OptionalDeviceGuard g(device);
+        return flock_sc_pipeline_set_gate(pipe, on ? 1 : 0);
+    }
+
+    // the actor half of each data-parallel round off the learner chain (flock_sc_pipeline_set_dp_actor): one actor
+    // gradient buffer per slot, all-reduced (SUM) over `group` on the pipeline's actor stream
+    static int actor_allreduce_cb(void* ctx, float* data, int64_t n, void* stream) {
+        auto* self = static_cast<ScPipeline*>(ctx);
+        try {
+            const c10::hip::HIPStream hs =
+                c10::hip::getStreamFromExternal(static_cast<hipStream_t>(stream), self->device.index());
+            const c10::hip::HIPStreamGuard guard(hs);
+            std::vector<Tensor> ts{at::from_blob(data, {n}, at::TensorOptions().dtype(at::kFloat).device(self->device))};
+            c10d::AllreduceOptions opts;
+            opts.reduceOp = c10d::ReduceOp::SUM;
+            self->pg_actor->allreduce(ts, opts)->wait();
+            return 0;
+        } catch (const std::exception& e) {
+            self->cb_error = e.what();
+            return -4;
+        }
+    }
+    void set_dp_actor(c10::intrusive_ptr<c10d::ProcessGroup> group, std::vector<Tensor> grads) {
+        TORCH_CHECK(group, "ScPipeline.set_dp_actor: a process group");
+        TORCH_CHECK((int64_t)grads.size() == n_slots, "ScPipeline.set_dp_actor: one actor gradient buffer per slot");
+        std::vector<float*> ptrs;
+        for (const Tensor& t : grads) {
+            TORCH_CHECK(t.device() == device && t.scalar_type() == at::kFloat && t.is_contiguous(),
+                        "ScPipeline.set_dp_actor: contiguous f32 buffers on ", device);
+            ptrs.push_back(static_cast<float*>(t.data_ptr()));
+        }
+        pg_actor = std::move(group);
+        actor_grads = grads;
+        const at::OptionalDeviceGuard g(device);
+        const int rc = flock_sc_pipeline_set_dp_actor(pipe, ptrs.data(), (int)n_agents, &ScPipeline::actor_allreduce_cb,
+                                                      this);
+        TORCH_CHECK(rc == 0, "flock_sc_pipeline_set_dp_actor: ", flock_learn_last_error());
+    }
 };
 
 struct ScTrainLoop : torch::CustomClassHolder {
@@ -224,15 +233,6 @@ struct ScTrainLoop : torch::CustomClassHolder {
     // learner
     c10::intrusive_ptr<ScPipeline> pipe;
     int64_t seed, learn_calls;
-    // ring copies (set_copies), [copy][state, action, reward, new_state, terminal]: every env step writes one copy
-    // of the WHOLE ring. mode 1 (direct learns): one copy per pipeline slot, the env step before learn t writes the
-    // copy of learn t's slot and the round's critic phase samples its rows there (no snapshot); mode 2 (copy learns):
-    // copies in turn, each learn's snapshot on the pipeline's own stream, the learner polling the device gate.
-    // last_copy: the copy the last step wrote (it holds the logical ring), -1: none
-    std::vector<Tensor> copies;
-    int64_t mode = 0, n_copies = 0, next_copy = 0;
-    int64_t last_copy = -1;
-
     ScTrainLoop(std::vector<Tensor> env_, std::vector<double> env_f, std::vector<int64_t> env_i,
                 std::vector<Tensor> ring_, int64_t counter_, c10::intrusive_ptr<ScPipeline> pipe_, int64_t seed_,
                 int64_t learn_calls_)
@@ -280,38 +280,6 @@ struct ScTrainLoop : torch::CustomClassHolder {
         for (int i = 0; i < 5; ++i) f32(ring[i], rn[i], capacity * w[i], pos);
     }
 
-    // ring copies for direct learns (empty: snapshot learns). Every env step must rewrite the whole ring (E N >=
-    // capacity: the ring's content after a step depends on that step alone), and the pipeline must not be
-    // data-parallel (flock_sc_pipeline_learn_direct refuses it)
-    void set_copies(std::vector<Tensor> copies_, int64_t mode_) {
-        if (copies_.empty() || mode_ == 0) {
-            copies.clear();
-            mode = 0;
-            return;
-        }
-        TORCH_CHECK(mode_ == 1 || mode_ == 2, "ScTrainLoop.set_copies: mode 1 (direct learns) or 2 (copy learns)");
-        TORCH_CHECK(copies_.size() % 5 == 0, "ScTrainLoop.set_copies: 5 fields per ring copy");
-        const int64_t nc = (int64_t)copies_.size() / 5;
-        TORCH_CHECK(mode_ == 2 || nc == pipe->n_slots, "ScTrainLoop.set_copies: direct learns need one copy per "
-                    "pipeline slot");
-        TORCH_CHECK(mode_ == 1 || (nc >= 2 && nc <= 8), "ScTrainLoop.set_copies: copy learns need 2..8 copies");
-        TORCH_CHECK(mode_ == 1 || pipe->copy_ok(), "ScTrainLoop.set_copies: copy learns need the pipeline's device gate "
-                    "(not data-parallel, not graph replays, not under counter collection)");
-        TORCH_CHECK(E * N >= capacity, "ScTrainLoop.set_copies: every env step must rewrite the whole ring (E N >= "
-                    "capacity)");
-        const int64_t w[5] = {k, 2, 1, k, 1};
-        for (size_t i = 0; i < copies_.size(); ++i) {
-            f32(copies_[i], "ring copy", capacity * w[i % 5], env[0]);
-            TORCH_CHECK(copies_[i].data_ptr() != ring[i % 5].data_ptr(), "ScTrainLoop.set_copies: the copies are "
-                        "buffers of their own");
-        }
-        copies = std::move(copies_);
-        mode = mode_;
-        n_copies = nc;
-        next_copy = 0;
-        last_copy = -1;
-    }
-
     // the Python objects' current values (VecFlockEnv._cur, ReplayRing.counter, SharedCriticLearner._learn_calls):
     // per-step Python steps may have advanced them since the last call
     void set_state(int64_t parity_, int64_t counter_, int64_t learn_calls_) {
@@ -333,16 +301,10 @@ struct ScTrainLoop : torch::CustomClassHolder {
         void* es = reinterpret_cast<void*>(env_stream);
         const int64_t n = E * N;
         size_t ev = 0;
-        const bool direct = mode == 1, copying = mode == 2;
-        last_copy = -1;
         for (int64_t s = 0; s < K; ++s) {
             const int64_t step = first + s;
             const int64_t skip = n > capacity ? n - capacity : 0;
-            // direct learns: the slot of the next learn() (its wait for that slot's previous learn on the env stream)
-            // names the ring copy this step writes
-            const int64_t copy = direct ? pipe->acquire(env_stream) : copying ? next_copy : -1;
-            if (copying) pipe->copy_acquire(env_stream, copy);  // the copy's previous snapshot has read it
-            const Tensor* rf = copy >= 0 ? &copies[5 * copy] : ring.data();
+            const Tensor* rf = ring.data();
             FlockRing r{};
             r.state = static_cast<float*>(rf[0].data_ptr());
             r.action = static_cast<float*>(rf[1].data_ptr());
@@ -374,27 +336,18 @@ struct ScTrainLoop : torch::CustomClassHolder {
             }
             parity = nxt;
             counter += n;
-            if (copy >= 0) last_copy = copy;
-            if (copying) next_copy = (next_copy + 1) % n_copies;
             if (counter >= pipe->batch) {  // SharedCriticLearner.pipeline_learn: learn() once the ring holds a batch
                 ++learn_calls;
                 const int64_t rows = counter < capacity ? counter : capacity;
-                const FlockScRows rc{r.state, r.new_state, r.action, r.reward, r.terminal};
-                if (direct)
-                    pipe->learn_direct(rows, seed, learn_calls, step % pipe->n_agents, env_stream, learner_stream, rc);
-                else if (copying)
-                    pipe->learn_copy(rows, seed, learn_calls, step % pipe->n_agents, env_stream, learner_stream, copy,
-                                     rc);
-                else
-                    pipe->learn(rows, seed, learn_calls, step % pipe->n_agents, env_stream, learner_stream);
+                pipe->learn(rows, seed, learn_calls, step % pipe->n_agents, env_stream, learner_stream);
             }
         }
     }
 
     void flush(int64_t learner_stream) { pipe->flush(learner_stream); }
 
-    // [env parity, ring counter, learn() calls, the ring copy the last step wrote (-1: the ring itself)]
-    std::vector<int64_t> state() const { return {parity, counter, learn_calls, mode == 0 ? -1 : last_copy}; }
+    // [env parity, ring counter, learn() calls]
+    std::vector<int64_t> state() const { return {parity, counter, learn_calls}; }
 };
 
 }  // namespace
@@ -408,12 +361,12 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         .def("flush", &ScPipeline::flush)
         .def("verify", &ScPipeline::verify)
         .def("gated", &ScPipeline::gated)
-        .def("copy_ok", &ScPipeline::copy_ok);
+        .def("set_gate", &ScPipeline::set_gate)
+        .def("set_dp_actor", &ScPipeline::set_dp_actor);
     m.class_<ScTrainLoop>("ScTrainLoop")
         .def(torch::init<std::vector<Tensor>, std::vector<double>, std::vector<int64_t>, std::vector<Tensor>, int64_t,
                          c10::intrusive_ptr<ScPipeline>, int64_t, int64_t>())
         .def("set_state", &ScTrainLoop::set_state)
-        .def("set_copies", &ScTrainLoop::set_copies)
         .def("run", &ScTrainLoop::run)
         .def("flush", &ScTrainLoop::flush)
         .def("state", &ScTrainLoop::state);

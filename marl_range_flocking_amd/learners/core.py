@@ -548,23 +548,11 @@ class ReplayRing:
         self._bufs = OrderedDict((k, torch.zeros((self.capacity, *v), dtype=torch.float32, device=self.device))
                                  for k, v in self.fields.items())
         self.counter = 0
-        self._pending = None  # {name: tensor}: a physical copy that holds the ring's current content (see bufs)
 
     @property
     def bufs(self):
-        """name -> [capacity, *row] tensor. After a loop with direct learns (ScTrainLoop.set_copies: every env step
-        rewrote the whole ring into one of the learner pipeline's ring copies) the newest rows live in that copy; the
-        first access copies them back here, on the current stream (ordered after the loop's env steps)."""
-        if self._pending is not None:
-            src, self._pending = self._pending, None
-            for k, t in src.items():
-                self._bufs[k].copy_(t)
+        """name -> [capacity, *row] tensor."""
         return self._bufs
-
-    def set_pending_copy(self, src):
-        """src: {name: tensor} of a ring copy whose content replaces this ring's at the next access of bufs."""
-        assert set(src) == set(self._bufs), (sorted(src), sorted(self._bufs))
-        self._pending = dict(src)
 
     def __len__(self):
         return min(self.counter, self.capacity)

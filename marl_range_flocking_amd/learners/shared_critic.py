@@ -85,7 +85,7 @@ class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
                  ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
-                 snapshot=False, replay=None, n_slots=2):
+                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=True):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -133,6 +133,18 @@ class SharedCriticLearner:
         # update runs (snapshot_into / update_slot: the copy on the env stream, the update on another one)
         self.snapshot = bool(snapshot and fused)
         self.n_slots = max(2, int(n_slots))
+        # the native pipeline's snapshot hand-off (pipeline()): "gate" the device-side gate polled by the critic row
+        # blocks (single GPU), "event" a cross-queue event wait
+        if handoff not in ("gate", "event"):
+            raise ValueError("handoff is 'gate' or 'event'")
+        self.handoff = handoff
+        # data-parallel pipelines: the actor half of each round all-reduced and stepped off the learner chain, over a
+        # second process group of the same ranks (flock_sc_pipeline_set_dp_actor); created here, collectively
+        self.dp_split = bool(dp_split and self.distributed and self.snapshot)
+        self.actor_group = None
+        if self.dp_split:
+            ranks = torch.distributed.get_process_group_ranks(dist_group) if dist_group is not None else None
+            self.actor_group = torch.distributed.new_group(ranks=ranks)
         if fused:
             self._init_fused()
 
@@ -493,9 +505,12 @@ class SharedCriticLearner:
         over the n_slots staging slots: per learn() the minibatch snapshot on the env stream and ONE round (this
         learn's critic phase with the previous learn's actor phase, flock_sc_round) on the learner stream, enqueued by
         one call. ONE object per learner: the per-step path (pipeline_learn) and the C++ training loop
-        (ScTrainLoop) share its slots and its pending actor phase. Data-parallel learners (dist_group) run every
-        round as gradients, one RCCL all-reduce of the [critic | actor] bucket over the group and the Adam launch
-        (set_dp; dp_learn's rounds, enqueued from C++)."""
+        (ScTrainLoop) share its slots and its pending actor phase. The round waits for its snapshot on the device-side
+        gate (handoff="gate", single GPU) or on a cross-queue event. Data-parallel learners (dist_group) run every
+        round as gradients, one RCCL all-reduce of the critic gradient over the group and the critic Adam launch on
+        the learner stream; with dp_split (default) the round's actor gradient is all-reduced over a second group and
+        stepped on the pipeline's actor stream, off the learner chain (set_dp_actor); without, one all-reduce of the
+        [critic | actor] bucket (set_dp; dp_learn's rounds, enqueued from C++)."""
         if self._pipe is None:
             if not (self.snapshot and self.fused):
                 raise RuntimeError("the native pipeline needs a fused learner with snapshot=True")
@@ -509,6 +524,12 @@ class SharedCriticLearner:
                 group = self.group if self.group is not None else torch.distributed.group.WORLD
                 # the c10d ProcessGroup as the TorchScript object the C++ class takes (ProcessGroup.boxed())
                 p.set_dp(group.boxed(), self.dp_bucket, self.critic.numel, self.dp_actor_off, self.inv_world)
+                if self.dp_split:  # one actor gradient buffer per slot, all-reduced over actor_group off the chain
+                    self.dp_actor_grads = [torch.zeros(self.actors.per_agent, device=self.device)
+                                           for _ in range(self.n_slots)]
+                    p.set_dp_actor(self.actor_group.boxed(), self.dp_actor_grads)
+            else:
+                p.set_gate(self.handoff == "gate")
             self._pipe = p
         return self._pipe
 
@@ -516,9 +537,6 @@ class SharedCriticLearner:
         """Enqueue learn(agent) through the native pipeline (raw stream handles): the snapshot on env_stream, the
         round on learner_stream. The actor phase stays pending until the next call or pipeline_flush. Returns False
         (nothing enqueued) before the buffer holds a batch, like snapshot_into."""
-        if self.replay._pending is not None:  # (see learn) the copy-back runs on env_stream, before the snapshot
-            with torch.cuda.stream(torch.cuda.ExternalStream(int(env_stream), device=self.device)):
-                self.replay.bufs  # noqa: B018
         if self.replay.counter < self.batch_size:
             return False
         self._learn_calls += 1
@@ -533,14 +551,10 @@ class SharedCriticLearner:
             self._pipe.flush(int(learner_stream))
 
     def pipeline_check(self):
-        """Raise if a round gave up waiting for its inputs: the device-side snapshot gate or a fused round's in-launch
-        hand-off (bounded waits; flock_sc_pipeline_check / flock_sc_workspace_check): its update is invalid.
-        Synchronous; call after synchronising."""
+        """Raise if a round gave up waiting for its minibatch snapshot (the device-side gate's bounded wait,
+        flock_sc_pipeline_check): its update is invalid. Synchronous; call after synchronising."""
         if self._pipe is not None:
             self._pipe.verify()
-        if self.fused:
-            for ws in self.sc_workspaces:
-                _ops().sc_check(ws, self._sc_dims)
 
     # ------------------------------------------------------------------ data-parallel rounds (bench, N > 1)
     def _dp_round(self, c, a):
@@ -615,7 +629,8 @@ class SharedCriticBench:
     """bench.py hook for BASELINE config 3: after each vectorized env step, insert every agent's transition into the
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
-    def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=None, buffer_size=1_000_000):
+    def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=None, buffer_size=1_000_000,
+                 handoff="gate", dp_split=True):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
@@ -623,11 +638,11 @@ class SharedCriticBench:
         # exploration), so step s+1 does not depend on learn(s) and every kernel still sees the same data
         # (with data-parallel replicas the update's two all-reduces run on the learner stream too)
         self.overlap = bool(overlap and fused)
-        if n_slots is None:  # staging slots (and ring copies of direct learns); FLOCK_SC_SLOTS: A/B
+        if n_slots is None:  # staging slots; FLOCK_SC_SLOTS: A/B
             n_slots = int(os.environ.get("FLOCK_SC_SLOTS", "3"))
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
                                            buffer_size=buffer_size, dist_group=group, fused=fused,
-                                           snapshot=self.overlap, n_slots=n_slots)
+                                           snapshot=self.overlap, n_slots=n_slots, handoff=handoff, dp_split=dp_split)
         if self.overlap:
             # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
             # with graphs, the native pipeline (one merged six-launch round per step on self.stream,
@@ -682,32 +697,7 @@ class SharedCriticBench:
             ring = [rb["state"], rb["action"], rb["reward"], rb["new_state"], rb["terminal"]]
             self._loop = torch.classes.flock.ScTrainLoop(e, ef, ei, ring, L.replay.counter, L.pipeline(), L.seed,
                                                          L._learn_calls)
-            self._copies = None
-            mode = self.ring_copy_mode()
-            if mode:
-                # physical copies of the ring, one written per env step (every step rewrites the whole ring):
-                # mode 2 (copy learns): 3 copies in turn, each learn's snapshot on the pipeline's own stream and the
-                # learner polling the device gate (flock_sc_pipeline_learn_copy); mode 1 (direct learns): one copy
-                # per pipeline slot, the critic phase samples its rows there (flock_sc_pipeline_learn_direct).
-                # Both bitwise the snapshot learns
-                n = L.n_slots if mode == 1 else 3
-                self._copies = [[torch.zeros_like(t) for t in ring] for _ in range(n)]
-                self._loop.set_copies([t for c in self._copies for t in c], mode)
         return self._loop
-
-    def ring_copy_mode(self):
-        """How the loop's learns get their minibatch: 0 the snapshot on the env stream (flock_sc_pipeline_learn),
-        1 direct learns, 2 copy learns (see loop()). 1 and 2 need every env step to rewrite the whole ring (E N >=
-        capacity, as at config 3: 1,048,576 transitions into a 1e6-row ring) and a single-GPU pipeline launching its
-        rounds directly; 2 also the device gate (not under counter collection). FLOCK_SC_RING_COPIES=0/1/2 (A/B)."""
-        L = self.learner
-        want = int(os.environ.get("FLOCK_SC_RING_COPIES", "0"))
-        if (want == 0 or L.distributed or os.environ.get("FLOCK_SC_PIPELINE_GRAPHS", "0") == "1"
-                or self.env.E * self.env.N < L.replay.capacity):
-            return 0
-        if want == 2 and not L.pipeline().copy_ok():
-            return 0
-        return want
 
     def can_loop(self):
         return (self.overlap and self.pipelined and self.learner.use_graph and self.env.cfg.variant == "v2")
@@ -727,11 +717,7 @@ class SharedCriticBench:
         lp.set_state(env._cur, L.replay.counter, L._learn_calls)
         lp.run(int(first), int(K), list(actions), torch.cuda.current_stream(env.device).cuda_stream,
                self.stream.cuda_stream, handles, int(ev_every))
-        parity, counter, calls, last_copy = lp.state()
-        if last_copy >= 0:  # direct learns: the newest rows are in that ring copy (ReplayRing.bufs copies them back)
-            c = self._copies[last_copy]
-            L.replay.set_pending_copy({"state": c[0], "action": c[1], "reward": c[2], "new_state": c[3],
-                                       "terminal": c[4]})
+        parity, counter, calls = lp.state()
         learns = calls - L._learn_calls
         for s in range(first + K - learns, first + K):
             L.count[s % L.n_agents] += 1

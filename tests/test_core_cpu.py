@@ -22,25 +22,3 @@ def test_linear_t_is_differentiable_without_gradient_views():
     with torch.no_grad():
         torch.testing.assert_close(linear_t(x, W, b), ref)
         torch.testing.assert_close(linear_t(x, W), ref - b[..., None])
-
-
-def test_replay_ring_pending_copy_is_copied_back_on_first_access():
-    """ReplayRing.set_pending_copy (a loop's ring copies, SharedCriticBench.run_steps): the copy's rows replace the
-    ring's at the next access of bufs, once; later writes to the copy are not seen."""
-    from marl_range_flocking_amd.learners.core import ReplayRing
-
-    ring = ReplayRing(6, {"state": (4,), "reward": ()}, "cpu")
-    src = {"state": torch.arange(24, dtype=torch.float32).reshape(6, 4), "reward": torch.full((6,), 2.0)}
-    ring.set_pending_copy(src)
-    assert ring._pending is not None
-    b = ring.bufs
-    assert ring._pending is None
-    assert torch.equal(b["state"], src["state"]) and torch.equal(b["reward"], src["reward"])
-    src["reward"].fill_(7.0)  # the copy is a buffer of its own: the ring does not alias it
-    assert torch.equal(ring.bufs["reward"], torch.full((6,), 2.0))
-    try:
-        ring.set_pending_copy({"state": src["state"]})
-    except AssertionError:
-        pass
-    else:
-        raise AssertionError("a pending copy must name every field")

@@ -1,0 +1,70 @@
+"""BASELINE config 5's exact env launch against the oracle (verdict r4 item 3): gym_flock_v2 periodic, N = 1024 agents,
+k = 4, main.py density (box 506), the specialised cell-list instantiation with the PFM = 3 L2 pull (E = 4096 envs:
+eight generations of the 512 one-env blocks the device holds at once, so every block but the last generation pulls
+its successor's inputs), compact kNN seeds from the previous steps, and the RNN-MADDPG record insert fused into the
+step (one ring row per env, ReplayBufferMaddpg.add_record, memory_rnn.py:53-67; a 3000-row ring, so the step's
+first E - 3000 records are skipped as the reference's slice assignment would overwrite them).
+
+Checked on sampled envs at every block-generation edge (multiples of 512, both sides) plus a stride: the step
+against oracle.step_v2 from the same pre-step state (environments/gym_flock_v2.py:71-83; state within rtol 1e-5),
+the kNN bit-exact on the GPU's own post-step positions, reward / done of every row, and the ring rows the step wrote
+(obs, next obs, actor obs, actor next obs, raw action, reward, done) for the sampled envs."""
+import numpy as np
+import pytest
+import torch
+
+from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def test_config5_exact_launch_shape_against_oracle(cuda):
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+    from oracle import oracle as O
+    from parity import _knn_exact
+
+    E, N, k = 4096, 1024, 4
+    box = float(round(np.sqrt(250 * N)))  # 506
+    env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                  range_start=(0, box), sensor_range=14.0, seed=1234, step_launches=1), device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(1234)
+    env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
+    env.headings.copy_((1.0 - torch.rand(E, N, device=cuda, generator=g)) * 1.5 * np.pi)
+    pool = [torch.stack([torch.rand(E, N, device=cuda, generator=g),
+                         torch.rand(E, N, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
+    # small networks: only the learner's replay ring (45k rows at config 5; 3000 here) takes part in the step
+    L = MADDPGLearner(N, k, recurrent=True, hidden1=8, hidden2=8, batch_size=8, chunk_size=4, buffer_capacity=3000,
+                      min_size_buffer=8, device=cuda, use_graph=False)
+    for s in range(2):  # the seeded scan needs the previous steps' neighbour lists
+        env.step(pool[s], ring=L.replay_slots(E))
+    torch.cuda.synchronize()
+    assert env.seeds is not None
+    edges = torch.tensor([e for b in range(0, E + 1, 512) for e in (b - 1, b) if 0 <= e < E], device=cuda)
+    sample = torch.unique(torch.cat([torch.arange(37, E, 331, device=cuda), edges]))
+    pre_pos, pre_head = env.positions[sample].cpu().numpy(), env.headings[sample].cpu().numpy()
+    prev_obs = env.dnn.clone()
+    counter, cap = L.replay.counter, L.replay.capacity
+    act = pool[2]
+    env.step(act, ring=L.replay_slots(E))  # the step under test
+    torch.cuda.synchronize()
+    ref = O.step_v2(pre_pos, pre_head, act[sample].cpu().numpy(), k=k, box=box, sensor_range=14.0, cd=2.5)
+    pos = env.positions[sample].cpu().numpy()
+    np.testing.assert_allclose(pos, ref["pos"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(env.headings[sample].cpu().numpy(), ref["heading"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(env.velocities[sample].cpu().numpy(), ref["vel"], rtol=1e-5, atol=1e-6)
+    _knn_exact(pos, k, box, 14.0, True, True, env.dnn[sample].cpu().numpy(), env.nn_idx[sample].cpu().numpy())
+    d = env.dnn
+    assert torch.equal(env.done, (d < 2.5).any(-1)) and torch.equal(env.any_done, env.done.any(-1))
+    assert torch.equal(env.reward, torch.where(env.done, torch.tensor(-5.0, device=cuda),
+                                               torch.tensor(0.01, device=cuda)))
+    # ring rows: one record per env; only the last `cap` of the step's E records survive: env e >= skip at row
+    # (start + e - skip) mod cap
+    skip = E - cap
+    start = (counter + skip) % cap
+    e = sample[sample >= skip]
+    rows = (start + e - skip) % cap
+    rb = L.replay.bufs
+    for name, want in (("state", prev_obs[e]), ("actor_state", prev_obs[e]), ("next_state", d[e]),
+                       ("actor_next_state", d[e]), ("action", act[e]), ("reward", env.reward[e]),
+                       ("done", env.done[e].float())):
+        assert torch.equal(rb[name][rows], want), name

@@ -180,7 +180,9 @@ def test_two_ranks_overlapped_bench_loop_equals_serial(cuda):
 def _loop_worker(rank, port, q):
     """The data-parallel config-3 loop through the C++ ScTrainLoop (each round: gradients, the all-reduce over the
     c10d ProcessGroup enqueued from C++, the Adam launch) against the per-step Python data-parallel rounds
-    (FLOCK_LEARN_PIPELINE=0: SharedCriticLearner.dp_learn) on 2 ranks (gloo, cuda:0): bitwise equal."""
+    (FLOCK_LEARN_PIPELINE=0: SharedCriticLearner.dp_learn) on 2 ranks (gloo, cuda:0), with the actor half of every
+    round split off the learner chain (dp_split: the actor all-reduce over a second group and the actor Adam on the
+    pipeline's actor stream) and without (one [critic | actor] all-reduce): all three bitwise equal."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", RANK=str(rank))
     try:
         torch.distributed.init_process_group("gloo")
@@ -194,7 +196,7 @@ def _loop_worker(rank, port, q):
                              torch.rand(E, Na, device=dev, generator=ga) * 3 - 1.5], -1).contiguous()
                 for _ in range(3)]
         states = []
-        for mode in ("python", "loop"):
+        for mode in ("python", "loop_split", "loop"):
             if mode == "python":
                 os.environ["FLOCK_LEARN_PIPELINE"] = "0"
             else:
@@ -204,8 +206,8 @@ def _loop_worker(rank, port, q):
             g = torch.Generator(device=dev).manual_seed(3 + rank)
             env.positions.copy_(torch.rand(E, Na, 2, device=dev, generator=g) * 63.0)
             env.headings.copy_(torch.rand(E, Na, device=dev, generator=g) * 4.7)
-            hook = SharedCriticBench(env, device=dev, seed=11)
-            assert hook.learner.distributed
+            hook = SharedCriticBench(env, device=dev, seed=11, dp_split=mode == "loop_split")
+            assert hook.learner.distributed and hook.learner.dp_split == (mode == "loop_split")
             if mode == "python":
                 assert not hook.can_loop()
                 for s in range(S):
@@ -246,9 +248,10 @@ def test_two_ranks_dp_train_loop_equals_python_dp_rounds(cuda):
         p.join(timeout=60)
     for o in out:
         assert not isinstance(o[1], str), o
-    for rank, (py, loop) in out:
-        for i, (x, y) in enumerate(zip(py, loop)):
-            np.testing.assert_array_equal(x, y, err_msg=f"rank {rank} field {i}")
+    for rank, (py, split, loop) in out:
+        for other, name in ((split, "split loop"), (loop, "loop")):
+            for i, (x, y) in enumerate(zip(py, other)):
+                np.testing.assert_array_equal(x, y, err_msg=f"rank {rank} {name} field {i}")
     for i in range(9):  # the learner replicas stay identical (env state differs per rank)
         np.testing.assert_array_equal(out[0][1][1][i], out[1][1][1][i])
 

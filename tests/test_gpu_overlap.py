@@ -1,7 +1,6 @@
 """Overlapped env step / learner (bench.py config 3 hook): learn(s) on its own stream after its minibatch snapshot,
 env step s+1 concurrently on the main stream. Every kernel must still see the same data, so after several steps
 every parameter, Adam moment, replay field and loss equals the serial loop's bit for bit."""
-import os
 
 import pytest
 import torch
@@ -118,16 +117,18 @@ def test_pipelined_phases_same_agent_equal_serial(cuda):
 @pytest.mark.parametrize("agents,n_slots", [((0, 0, 0, 1, 1, 0, 2, 1, 1, 2), 2), ((0, 1, 2, 0, 0, 1, 2, 2, 1, 0), 3),
                                             ((3, 1, 4, 1, 5, 9, 2, 6, 5, 3), 4)],
                          ids=["same-agent-runs-2slots", "mixed-3slots", "distinct-4slots"])
-def test_native_pipeline_rounds_equal_serial(agents, n_slots, cuda):
+@pytest.mark.parametrize("handoff", ["gate", "event"])
+def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
     """The native pipeline (flock_sc_pipeline_learn): one six-launch round per learn() = its critic phase merged
     with the previous learn's actor phase (flock_sc_round), or the two phases one after the other when both learns
     have the same agent; the last actor phase is enqueued by flock_sc_pipeline_flush. After a sequence with runs of
-    the same agent, every parameter, moment, target, step counter and loss is bitwise the serial learn() sequence."""
+    the same agent, every parameter, moment, target, step counter and loss is bitwise the serial learn() sequence,
+    with either snapshot hand-off (the device-side gate polled by the critic row blocks, or the event wait)."""
     from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
 
     ser = SharedCriticLearner(10, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=False)
     pip = SharedCriticLearner(10, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=True,
-                              n_slots=n_slots)
+                              n_slots=n_slots, handoff=handoff)
     g = torch.Generator(device=cuda).manual_seed(4)
     n = 300
     rows = (torch.rand(n, 4, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g),
@@ -147,7 +148,7 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, cuda):
     main.wait_stream(ls)
     torch.cuda.synchronize()
     pip.pipeline_check()  # no round gave up waiting for its snapshot (device-side gate)
-    assert pip.pipeline().gated() == int(os.environ.get("FLOCK_SC_GATE", "0"))
+    assert pip.pipeline().gated() == int(handoff == "gate")
     for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg, pip.critic.exp_avg),
                  (ser.critic.exp_avg_sq, pip.critic.exp_avg_sq), (ser.actors.data, pip.actors.data),
                  (ser.actors.exp_avg, pip.actors.exp_avg), (ser.actors.target, pip.actors.target),
@@ -193,89 +194,40 @@ def test_specialised_row_kernels_equal_generic(cuda):
 
 
 @pytest.mark.parametrize("n_slots", [2, 3])
-def test_device_gate_and_fused_rounds_are_bitwise_the_plain_pipeline(n_slots, cuda):
-    """The device-side snapshot gate (the critic row blocks poll a sequence number the `sc1` snapshot publishes;
-    FLOCK_SC_GATE=0: the cross-queue event wait) and the fused three-launch rounds (forward GEMM tiles + k3 rows in one
-    launch, bwd + gradient / Adam blocks in one launch, hand-offs through workspace counters; flock_set_diag
-    "sc_no_fuse": five launches; "sc_fuse_k1": the fc1 rows in the forward launch too, two launches), in all six
-    combinations: the overlapped config-3 loop at the reference widths with
-    env kernels co-running on the env stream (uneven load, L1-warm consumers) ends with every learner tensor bitwise
-    equal, and no wait gave up."""
-    from marl_range_flocking_amd import FlockConfig, VecFlockEnv, _native
+def test_device_gate_is_bitwise_the_event_wait(n_slots, cuda):
+    """The device-side snapshot gate (the critic row blocks poll a sequence number the `sc1` snapshot publishes, then
+    read the staged rows `sc1`) against the cross-queue event wait, in the overlapped config-3 loop at the reference
+    widths with env kernels co-running on the env stream (uneven load, L1-warm consumers): every learner tensor ends
+    bitwise equal (the event loop runs twice: a determinism baseline), and no wait gave up."""
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
     from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
-    lib = _native.lib()
     E, Na, steps = 512, 256, 24
     g = torch.Generator(device=cuda).manual_seed(2)
     pool = [torch.stack([torch.rand(E, Na, device=cuda, generator=g),
                          torch.rand(E, Na, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
     out = []
-    modes = (("0", 0), ("0", 0), ("1", 0), ("2", 0), ("0", 1), ("1", 1), ("2", 1), ("1", 2), ("2", 2))  # plain twice
-    for gate, fuse in modes:
-        os.environ["FLOCK_SC_GATE"] = gate
-        assert lib.flock_set_diag(b"sc_no_fuse", int(fuse == 0)) == 0
-        assert lib.flock_set_diag(b"sc_fuse_k1", int(fuse == 2)) == 0
-        try:
-            env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
-                                          range_start=(0, 253.0), sensor_range=14.0, step_launches=3), device=cuda)
-            gp = torch.Generator(device=cuda).manual_seed(5)
-            env.positions.copy_(torch.rand(E, Na, 2, device=cuda, generator=gp) * 253.0)
-            env.headings.copy_(torch.rand(E, Na, device=cuda, generator=gp) * 4.7)
-            hook = SharedCriticBench(env, device=cuda, seed=7, n_slots=n_slots)
-            hook.run_steps(0, steps, pool)
-            hook.finish()
-            torch.cuda.synchronize()
-            L = hook.learner
-            L.pipeline_check()
-            assert L.pipeline().gated() == int(gate)
-            C, A = L.critic, L.actors
-            out.append([C.data.clone(), C.exp_avg.clone(), C.exp_avg_sq.clone(), A.data.clone(), A.target.clone(),
-                        A.exp_avg.clone(), A.exp_avg_sq.clone(), L.actor_steps.clone(), L.losses.clone(),
-                        C.step_dev.clone()])
-        finally:
-            os.environ.pop("FLOCK_SC_GATE", None)
-            lib.flock_set_diag(b"sc_no_fuse", 0)
-            lib.flock_set_diag(b"sc_fuse_k1", -1)
+    modes = ("event", "event", "gate", "gate")
+    for handoff in modes:
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
+                                      range_start=(0, 253.0), sensor_range=14.0, step_launches=3), device=cuda)
+        gp = torch.Generator(device=cuda).manual_seed(5)
+        env.positions.copy_(torch.rand(E, Na, 2, device=cuda, generator=gp) * 253.0)
+        env.headings.copy_(torch.rand(E, Na, device=cuda, generator=gp) * 4.7)
+        hook = SharedCriticBench(env, device=cuda, seed=7, n_slots=n_slots, handoff=handoff)
+        hook.run_steps(0, steps, pool)
+        hook.finish()
+        torch.cuda.synchronize()
+        L = hook.learner
+        L.pipeline_check()
+        assert L.pipeline().gated() == int(handoff == "gate")
+        C, A = L.critic, L.actors
+        out.append([C.data.clone(), C.exp_avg.clone(), C.exp_avg_sq.clone(), A.data.clone(), A.target.clone(),
+                    A.exp_avg.clone(), A.exp_avg_sq.clone(), L.actor_steps.clone(), L.losses.clone(),
+                    C.step_dev.clone()])
     bad = {}
     for m, mode in enumerate(out[1:], 1):
         diff = [i for i, (x, y) in enumerate(zip(out[0], mode)) if not torch.equal(x, y)]
         if diff:
-            bad[modes[m]] = (diff, float((out[0][0] - mode[0]).abs().max()))
-    assert not bad, bad  # (gate, fuse) -> (differing tensors, max |critic diff|)
-
-
-def test_fused_rounds_bitwise_serial_learns(cuda):
-    """The fused rounds (three launches; two with the fc1 rows fused too) through the plain learn() path (one
-    critic-only and one actor-only round per learn, the reference widths, B = 256) against the five-launch rounds: bitwise equal after a sequence with a repeated agent;
-    the workspace error word stays clear."""
-    from marl_range_flocking_amd import _native
-    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
-
-    lib = _native.lib()
-    g = torch.Generator(device=cuda).manual_seed(9)
-    n, d = 2000, 4
-    rows = (torch.rand(n, d, device=cuda, generator=g) * 14, torch.rand(n, 2, device=cuda, generator=g) * 2 - 1,
-            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, d, device=cuda, generator=g) * 14,
-            torch.rand(n, device=cuda, generator=g) > 0.9)
-    out = []
-    for fuse in (0, 1, 2):
-        assert lib.flock_set_diag(b"sc_no_fuse", int(fuse == 0)) == 0
-        assert lib.flock_set_diag(b"sc_fuse_k1", int(fuse == 2)) == 0
-        try:
-            L = SharedCriticLearner(5, d, device=cuda, seed=3, batch_size=256, buffer_size=3000, use_graph=False)
-            L.store_transitions(*rows)
-            for a in (0, 3, 3, 1, 4, 2, 0):
-                L.learn(a)
-            torch.cuda.synchronize()
-            L.pipeline_check()
-        finally:
-            lib.flock_set_diag(b"sc_no_fuse", 0)
-            lib.flock_set_diag(b"sc_fuse_k1", -1)
-        out.append(L)
-    a = out[0]
-    for b in out[1:]:
-        for x, y in ((a.critic.data, b.critic.data), (a.critic.exp_avg_sq, b.critic.exp_avg_sq),
-                     (a.actors.data, b.actors.data), (a.actors.target, b.actors.target), (a.losses, b.losses),
-                     (a.actor_steps, b.actor_steps)):
-            assert torch.equal(x, y)
-    assert torch.isfinite(a.critic.data).all() and a.losses.abs().sum() > 0
+            bad[(m, modes[m])] = (diff, float((out[0][0] - mode[0]).abs().max()))
+    assert not bad, bad  # (run, hand-off) -> (differing tensors, max |critic diff|)

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 E, N, K = 16, 128, 4
 
 
-def _bench(cuda, buffer_size=1_000_000):
+def _bench(cuda, buffer_size=1_000_000, handoff="gate"):
     from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
     box = float(round((250 * N) ** 0.5))
@@ -21,7 +21,7 @@ def _bench(cuda, buffer_size=1_000_000):
     g = torch.Generator(device=cuda).manual_seed(0)
     env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
     env.headings.copy_((1.0 - torch.rand(E, N, device=cuda, generator=g)) * 4.712389)
-    return env, SharedCriticBench(env, device=cuda, seed=3, buffer_size=buffer_size)
+    return env, SharedCriticBench(env, device=cuda, seed=3, buffer_size=buffer_size, handoff=handoff)
 
 
 def _pool(cuda):
@@ -42,21 +42,19 @@ def _state(env, hook):
     return out
 
 
-# buffer 1500 < E N = 2048: every env step rewrites the whole ring, so the loop may keep physical ring copies: direct
-# learns (mode 1: one copy per pipeline slot, the critic phase samples its rows there) or copy learns (mode 2: the
-# snapshot on the pipeline's own stream, the learner polling the device gate), against the per-step path's snapshots
-@pytest.mark.parametrize("buffer_size,mode", [(1_000_000, "0"), (1500, "0"), (1500, "1"), (1500, "2")])
-def test_train_loop_is_bitwise_the_per_step_path(buffer_size, mode, cuda, monkeypatch):
-    monkeypatch.setenv("FLOCK_SC_RING_COPIES", mode)
+# buffer 1500 < E N = 2048: every env step rewrites the whole ring (the per-step snapshots are then all that keeps a
+# learn's rows); both snapshot hand-offs (the device gate, the event wait)
+@pytest.mark.parametrize("buffer_size,handoff", [(1_000_000, "gate"), (1500, "gate"), (1500, "event")])
+def test_train_loop_is_bitwise_the_per_step_path(buffer_size, handoff, cuda):
     pool = _pool(cuda)
-    env_a, hook_a = _bench(cuda, buffer_size)
+    env_a, hook_a = _bench(cuda, buffer_size, handoff)
     for s in range(12):
         hook_a.step(s, pool[s % len(pool)])
     hook_a.finish()
-    env_b, hook_b = _bench(cuda, buffer_size)
+    env_b, hook_b = _bench(cuda, buffer_size, handoff)
     assert hook_b.can_loop()
     hook_b.loop()
-    assert hook_b.ring_copy_mode() == int(mode) and (hook_b._copies is not None) == (mode != "0")
+    assert hook_b.learner.pipeline().gated() == int(handoff == "gate")
     hook_b.run_steps(0, 5, pool)
     hook_b.run_steps(5, 7, pool)
     hook_b.finish()
@@ -74,7 +72,7 @@ def test_train_loop_is_bitwise_the_per_step_path(buffer_size, mode, cuda, monkey
     assert torch.equal(env_a.positions, env_b.positions) and torch.equal(env_a.dnn, env_b.dnn)
     for n in La.replay.bufs:
         assert torch.equal(La.replay.bufs[n], Lb.replay.bufs[n]), n
-    # per-step learns, then the loop again (its copies hold older rows than the ring now): both paths still equal
+    # per-step learns, then the loop again: both paths still equal
     hook_b.after(12, pool[0])  # (hook_a.step(12) ran its learn)
     for s in range(13, 17):
         hook_a.step(s, pool[s % len(pool)])
@@ -86,39 +84,6 @@ def test_train_loop_is_bitwise_the_per_step_path(buffer_size, mode, cuda, monkey
     sa, sb = _state(env_a, hook_a), _state(env_b, hook_b)
     for name in sa:
         assert torch.equal(sa[name], sb[name]), name
-
-
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_ring_copy_learns_equal_snapshot_learns_in_the_overlapped_loop(mode, cuda, monkeypatch):
-    """The loop's direct learns (FLOCK_SC_RING_COPIES=1) and copy learns (2) against its snapshot learns (0) at
-    512 x 256 with a 100k-row ring (every step rewrites it), 30 steps in two calls: env kernels co-run with the
-    rounds; every learner tensor, the env state and the ring (copied back from the last copy) bitwise equal, and no
-    device-gate wait gave up (pipeline_check)."""
-    from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
-
-    Ee, Na = 512, 256
-    g = torch.Generator(device=cuda).manual_seed(4)
-    pool = [torch.stack([torch.rand(Ee, Na, device=cuda, generator=g),
-                         torch.rand(Ee, Na, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
-    out = []
-    for direct in (mode, "0"):
-        monkeypatch.setenv("FLOCK_SC_RING_COPIES", direct)
-        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=Ee, num_agents=Na, k=4, collision_distance=2.5,
-                                      range_start=(0, 253.0), sensor_range=14.0, step_launches=3), device=cuda)
-        gp = torch.Generator(device=cuda).manual_seed(5)
-        env.positions.copy_(torch.rand(Ee, Na, 2, device=cuda, generator=gp) * 253.0)
-        env.headings.copy_(torch.rand(Ee, Na, device=cuda, generator=gp) * 4.7)
-        hook = SharedCriticBench(env, device=cuda, seed=7, buffer_size=100_000)
-        hook.loop()
-        assert (hook._copies is not None) == (direct != "0")
-        hook.run_steps(0, 13, pool)
-        hook.run_steps(13, 17, pool)
-        hook.finish()
-        torch.cuda.synchronize()
-        hook.learner.pipeline_check()
-        out.append(_state(env, hook))
-    for name in out[0]:
-        assert torch.equal(out[0][name], out[1][name]), name
 
 
 def test_train_loop_records_timing_events(cuda):

@@ -3,10 +3,11 @@
 # built in place on the CPU) and this tree. Usage: tools/gpu_ab_trees.sh REPS "<bench args>" [more bench-arg sets...]
 # Results: gpurun_out/abt/<set>_<tree>_<rep>.json, summary in gpurun_out/abt/summary.txt
 set -o pipefail
-O=$PWD/gpurun_out/abt
+O=$PWD/gpurun_out/${ABT_OUT:-abt}
 mkdir -p $O
+rm -f $O/s*_*.json
 REPS=$1; shift
-TREES="$(ls _ab) cur"
+TREES="${TREES:-$(ls _ab) cur}"  # TREES="<sha> ... cur": a subset
 s=0
 for args in "$@"; do
   s=$((s + 1))
@@ -21,7 +22,8 @@ done
 python - "$@" <<'PY' | tee $O/summary.txt
 import json, glob, sys, collections
 rows = collections.defaultdict(list)
-for f in sorted(glob.glob("gpurun_out/abt/s*_*.json")):
+import os
+for f in sorted(glob.glob("gpurun_out/%s/s*_*.json" % os.environ.get("ABT_OUT", "abt"))):
     name = f.split("/")[-1][:-5]
     s, t, r = name.split("_")
     d = json.loads(open(f).read().strip().splitlines()[-1])
