@@ -52,9 +52,9 @@ VALU_PEAK_FULL_RATE = 64 * SIMDS * CLOCK_HZ / 2  # 78.6e12 lane-op/s: every wave
 BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  # SURVEY §8(d) (flock: +vel rw)
 # fused replay insert (flock_step_v2_store / the uw_discrete ring), per agent-step: + previous obs read (k=4 floats)
 # + the ring fields written. shared critic: state 16 + action 8 + reward 4 + new_state 16 + terminal 4; RNN-MADDPG
-# record: state, next_state, actor_state, actor_next_state 16 each + action 8 + reward 4 + done 4; VDN team
-# transition: s 16 + a (f32 id) 4 + r 4 + s' 16 (+ one done flag per env: 4 / N)
-RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 80, "vdn": 16 + 40}
+# record: state, next_state 16 each (actor_state / actor_next_state alias them: MADDPGLearner(shared_obs=True)) +
+# action 8 + reward 4 + done 4; VDN team transition: s 16 + a (f32 id) 4 + r 4 + s' 16 (+ one done flag per env: 4 / N)
+RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 48, "vdn": 16 + 40}
 EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 4))  # steps between HIP-event-timed env launches (timed region)
 
 
@@ -365,8 +365,11 @@ class MADDPGBench:
         group = torch.distributed.group.WORLD if torch.distributed.is_initialized() else None
         # under torchrun: agent-sharded critics (each rank owns N / world critics; the minibatches and the actor
         # heads' actions are all-gathered instead of all-reducing the 3.6-GB critic gradient)
+        # shared_obs: gym_flock_v2's critic and actor observations are the same dnn rows (gym_flock_v2.py:110-125),
+        # so the record's actor copies alias state / next_state in the ring (written once by the env kernel)
         self.learner = MADDPGLearner(env.N, env.k, recurrent=True, device=dev, seed=seed, dist_group=group,
-                                     agent_shard=group is not None and env.N % torch.distributed.get_world_size() == 0)
+                                     agent_shard=group is not None and env.N % torch.distributed.get_world_size() == 0,
+                                     shared_obs=True)
         self.prev = None
 
     def describe(self):

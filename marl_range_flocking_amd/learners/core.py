@@ -539,14 +539,24 @@ class StepRing:
 
 
 class ReplayRing:
-    """Device-resident ring buffer of named row tensors (``fields``: name -> row shape)."""
+    """Device-resident ring buffer of named row tensors (``fields``: name -> row shape). ``aliases`` {name: target}:
+    fields whose every row is, by the caller's construction, the target field's row (gym_flock_v2's critic and actor
+    observations are the same dnn rows): one buffer serves both names, written once."""
 
-    def __init__(self, capacity, fields, device):
+    def __init__(self, capacity, fields, device, aliases=None):
         self.capacity = int(capacity)
         self.device = torch.device(device)
         self.fields = OrderedDict((k, tuple(v)) for k, v in fields.items())
-        self._bufs = OrderedDict((k, torch.zeros((self.capacity, *v), dtype=torch.float32, device=self.device))
-                                 for k, v in self.fields.items())
+        self.aliases = dict(aliases or {})
+        for a, t in self.aliases.items():
+            assert a in self.fields and t in self.fields and t not in self.aliases and self.fields[a] == self.fields[t]
+        self._bufs = OrderedDict()
+        for k, v in self.fields.items():
+            if k not in self.aliases:
+                self._bufs[k] = torch.zeros((self.capacity, *v), dtype=torch.float32, device=self.device)
+        for a, t in self.aliases.items():
+            self._bufs[a] = self._bufs[t]
+        self._bufs = OrderedDict((k, self._bufs[k]) for k in self.fields)
         self.counter = 0
 
     @property
@@ -574,6 +584,8 @@ class ReplayRing:
             return
         srcs, dsts, kinds = [], [], []
         for name, val in rows.items():
+            if name in self.aliases:  # written through its target field
+                continue
             w = self._width(name)
             val = torch.as_tensor(val, device=self.device)
             kind = 0

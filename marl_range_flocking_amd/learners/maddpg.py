@@ -231,8 +231,14 @@ class MADDPGLearner:
     def __init__(self, n_agents, k, recurrent=True, n_actions=2, hidden1=400, hidden2=300, actor_lr=3e-3,
                  critic_lr=3e-3, gamma=0.99, tau=0.001, batch_size=128, chunk_size=10, buffer_capacity=45_000,
                  min_size_buffer=8_000, ou_theta=0.15, ou_mu=0.0, ou_sigma=0.2, ou_sigma_min=0.001, device="cuda",
-                 seed=0, use_graph=True, reference_action_layout=True, dist_group=None, agent_shard=False):
+                 seed=0, use_graph=True, reference_action_layout=True, dist_group=None, agent_shard=False,
+                 shared_obs=False):
         self.device = torch.device(device)
+        # shared_obs: every record's actor observations ARE its critic observations (gym_flock_v2's "actors" and
+        # "critic" are the same dnn rows, gym_flock_v2.py:110-125, and main.py:34-41 stores both): the replay ring keeps
+        # one buffer for each pair (ReplayRing aliases), which the env kernel's fused insert writes once (bitwise the
+        # same records and minibatches; 32 B per agent-step less to write at config 5)
+        self.shared_obs = bool(shared_obs)
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.N, self.k, self.recurrent, self.h1 = n_agents, k, recurrent, hidden1
         self.actor_lr, self.critic_lr, self.gamma, self.tau = actor_lr, critic_lr, gamma, tau
@@ -270,7 +276,8 @@ class MADDPGLearner:
         self.replay = ReplayRing(buffer_capacity, {
             "state": (n_agents, k), "next_state": (n_agents, k), "actor_state": (n_agents, k),
             "actor_next_state": (n_agents, k), "action": (n_agents, n_actions), "reward": (n_agents,),
-            "done": (n_agents,)}, self.device)
+            "done": (n_agents,)}, self.device,
+            aliases={"actor_state": "state", "actor_next_state": "next_state"} if self.shared_obs else None)
         self.n_games = 0
         self.random_process = SharedOU(n_actions, ou_theta, ou_mu, ou_sigma, ou_sigma_min if recurrent else None,
                                        1e-2, self.device, self.gen, anneal_per_sample=not recurrent)
@@ -324,6 +331,9 @@ class MADDPGLearner:
         n = 1 if st.dim() == 2 else st.shape[0]
         f = lambda t, *shape: torch.as_tensor(t, device=self.device, dtype=torch.float32).reshape(n, *shape)  # noqa
         N, k = self.N, self.k
+        if self.shared_obs and not (torch.equal(f(actor_states, N, k), f(state, N, k)) and
+                                    torch.equal(f(actor_next_states, N, k), f(next_state, N, k))):
+            raise ValueError("shared_obs: a record's actor observations must equal its critic observations")
         self.replay.store({"state": f(state, N, k), "next_state": f(next_state, N, k),
                            "actor_state": f(actor_states, N, k), "actor_next_state": f(actor_next_states, N, k),
                            "action": f(actions, N, 2), "reward": f(reward, N), "done": f(done, N)})
@@ -332,6 +342,9 @@ class MADDPGLearner:
         """Reserve the next n_envs records for an env step that writes them itself (VecFlockEnv.step(ring=...)):
         the record add_record(obs, next_obs, actions, obs, next_obs, reward, done) of every env, one ring row per
         env (critic and actor observations are the same dnn rows here, as main.py:34-41 passes for v2)."""
+        if self.shared_obs:  # the actor fields alias state / next_state: the kernel writes them once
+            return self.replay.step_slots(n_envs, "state", "action", "reward", "next_state", "done", group=self.N,
+                                          store_done=True)
         return self.replay.step_slots(n_envs, "state", "action", "reward", "next_state", "done",
                                       actor_state="actor_state", actor_new_state="actor_next_state", group=self.N,
                                       store_done=True)

@@ -2,8 +2,9 @@
 k = 4, main.py density (box 506), the specialised cell-list instantiation with the PFM = 3 L2 pull (E = 4096 envs:
 eight generations of the 512 one-env blocks the device holds at once, so every block but the last generation pulls
 its successor's inputs), compact kNN seeds from the previous steps, and the RNN-MADDPG record insert fused into the
-step (one ring row per env, ReplayBufferMaddpg.add_record, memory_rnn.py:53-67; a 3000-row ring, so the step's
-first E - 3000 records are skipped as the reference's slice assignment would overwrite them).
+step (one ring row per env, ReplayBufferMaddpg.add_record, memory_rnn.py:53-67, with the actor observation fields
+aliasing the critic ones as bench.py's config 5 runs it: MADDPGLearner(shared_obs=True); a 3000-row ring, so the
+step's first E - 3000 records are skipped as the reference's slice assignment would overwrite them).
 
 Checked on sampled envs at every block-generation edge (multiples of 512, both sides) plus a stride: the step
 against oracle.step_v2 from the same pre-step state (environments/gym_flock_v2.py:71-83; state within rtol 1e-5),
@@ -34,7 +35,7 @@ def test_config5_exact_launch_shape_against_oracle(cuda):
                          torch.rand(E, N, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
     # small networks: only the learner's replay ring (45k rows at config 5; 3000 here) takes part in the step
     L = MADDPGLearner(N, k, recurrent=True, hidden1=8, hidden2=8, batch_size=8, chunk_size=4, buffer_capacity=3000,
-                      min_size_buffer=8, device=cuda, use_graph=False)
+                      min_size_buffer=8, device=cuda, use_graph=False, shared_obs=True)
     for s in range(2):  # the seeded scan needs the previous steps' neighbour lists
         env.step(pool[s], ring=L.replay_slots(E))
     torch.cuda.synchronize()
@@ -68,3 +69,42 @@ def test_config5_exact_launch_shape_against_oracle(cuda):
                        ("actor_next_state", d[e]), ("action", act[e]), ("reward", env.reward[e]),
                        ("done", env.done[e].float())):
         assert torch.equal(rb[name][rows], want), name
+
+
+def test_shared_obs_ring_is_bitwise_the_separate_fields(cuda):
+    """MADDPGLearner(shared_obs=True) (the actor observation fields alias the critic ones; the env kernel's fused insert
+    writes them once) against separate fields: after rollouts with the fused insert and two train() calls on the
+    same sampled chunks, every ring field, critic, target and loss is bitwise equal; add_record refuses records
+    whose actor and critic observations differ."""
+    from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
+
+    E, N, k = 48, 32, 4
+    box = float(round(np.sqrt(250 * N)))
+    out = []
+    for shared in (False, True):
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=k, collision_distance=2.5,
+                                      range_start=(0, box), sensor_range=14.0, seed=5), device=cuda)
+        g = torch.Generator(device=cuda).manual_seed(5)
+        env.positions.copy_(torch.rand(E, N, 2, device=cuda, generator=g) * box)
+        env.headings.copy_(torch.rand(E, N, device=cuda, generator=g) * 4.7)
+        L = MADDPGLearner(N, k, recurrent=True, hidden1=32, hidden2=24, batch_size=16, chunk_size=4,
+                          buffer_capacity=600, min_size_buffer=16, device=cuda, seed=3, shared_obs=shared)
+        for s in range(12):
+            act = torch.stack([torch.rand(E, N, device=cuda, generator=g),
+                               torch.rand(E, N, device=cuda, generator=g) * 3 - 1.5], -1).contiguous()
+            env.step(act, ring=L.replay_slots(E))
+            if s in (7, 11):
+                L.train(starts=np.random.default_rng(s).choice(E * (s - 1) - 8, 16, replace=False))
+        torch.cuda.synchronize()
+        out.append(L)
+    a, b = out
+    for name in a.replay.bufs:
+        assert torch.equal(a.replay.bufs[name], b.replay.bufs[name]), name
+    assert b.replay.bufs["actor_state"].data_ptr() == b.replay.bufs["state"].data_ptr()
+    for x, y in ((a.critics.data, b.critics.data), (a.critics.target, b.critics.target),
+                 (a.critics.exp_avg_sq, b.critics.exp_avg_sq), (a.actors.target, b.actors.target)):
+        assert torch.equal(x, y)
+    obs = torch.rand(N, k, device=cuda)
+    with pytest.raises(ValueError):
+        b.add_record(obs, obs, torch.zeros(N, 2, device=cuda), obs + 1, obs, torch.zeros(N, device=cuda),
+                     torch.zeros(N, device=cuda))
