@@ -544,7 +544,7 @@ def main():
             handoff = {0: "cross-queue event wait", 1: "device gate polled by the critic row blocks"}[
                 hook.learner.pipeline().gated()]
             if getattr(hook.learner, "dp_split", False):
-                handoff += "; data-parallel actor all-reduce + Adam on a second group and stream
+                handoff += "; data-parallel actor all-reduce + Adam on a second group and stream"
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
