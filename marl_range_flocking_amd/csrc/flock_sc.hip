@@ -689,22 +689,69 @@ __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned lon
     return ok != 0;
 }
 
+// XCD-aligned work order (speed only; every map here is a bijection of the block index, whatever the placement).
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md: b and b + 8 share one), and lines an XCD's L2
+// holds survive the kernel boundary (tools/ubench_l2_persist.hip: a same-XCD re-read in the next launch runs at the
+// L2-hit time, 0.49 us, against 1.5 us from another XCD; profiles/r05/xcd/). With n a multiple of 8, block x takes
+// work item (x mod 8) (n / 8) + x / 8: the items of group g = x mod 8 (row strip g of the minibatch: rows
+// [g B / 8, (g + 1) B / 8)) run on one XCD in every launch of a round, so the fc1 rows k1 writes are L2 hits for the
+// forward GEMM tiles of that strip (xcd_tile), its fc2 outputs for the k3 rows, and k1 / k3 rows for the bwd launch's
+// dH1 tiles.
+__device__ __forceinline__ int xcd_perm(int x, int n) { return (n & 7) == 0 ? (x & 7) * (n >> 3) + (x >> 3) : x; }
+
+// L2 pull of the forward GEMM's B operands (the fc2.weight panels of the round's nets) by the k1 blocks of each XCD,
+// one dword per 128-B line, consumed by nothing (the lines are what the GEMM tiles of that XCD read next launch)
+struct Pull {
+    const float* p[2];
+    const int64_t* agent[2];  // p[i] + rel[i] * (*agent[i]) when agent[i] != NULL
+    int64_t rel[2];
+    int64_t n[2];  // floats
+};
+__device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bool sc1_agent) {
+    float sink = 0.0f;
+    int64_t lines[2], total = 0;
+    const float* base[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        lines[i] = (pl.n[i] + 31) >> 5;
+        total += lines[i];
+        const int64_t ag = pl.agent[i] ? (sc1_agent ? flock_mem::ld_sc1(pl.agent[i]) : *pl.agent[i]) : 0;
+        base[i] = pl.p[i] ? pl.p[i] + pl.rel[i] * ag : nullptr;
+    }
+    const int64_t lo = total * rank / ranks, hi = total * (rank + 1) / ranks;
+    for (int64_t l = lo + threadIdx.x; l < hi; l += 256) {
+        const int i = l < lines[0] ? 0 : 1;
+        const int64_t li = i ? l - lines[0] : l;
+        if (base[i]) sink += base[i][li << 5];
+    }
+    return sink;
+}
+
 template <int C, int HC>
-__global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
+__global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa, Pull pc, Pull pa) {
     SC_PROF(0);
-    if (ac.gate && (int)blockIdx.y < npc && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
-    if ((int)blockIdx.y < npc)
-        c1_body<C, HC>(wc, ac, blockIdx.x, blockIdx.y);
+    const bool crit = (int)blockIdx.y < npc;
+    if (ac.gate && crit && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
+    // the pull: this block's share of its job's panels among the job's blocks of its XCD group (x mod 8)
+    const int rb8 = (int)gridDim.x >> 3, yj = crit ? (int)blockIdx.y : (int)blockIdx.y - npc;
+    const int nj = crit ? npc : (int)gridDim.y - npc;
+    float sink = 0.0f;
+    if ((gridDim.x & 7) == 0) sink = pull_l2(crit ? pc : pa, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, crit);
+    const int bx = xcd_perm(blockIdx.x, gridDim.x);
+    if (crit)
+        c1_body<C, HC>(wc, ac, bx, blockIdx.y);
     else
-        a1_body<C, HC>(wa, aa, blockIdx.x, blockIdx.y - npc);
+        a1_body<C, HC>(wa, aa, bx, blockIdx.y - npc);
+    asm volatile("" ::"v"(sink));
 }
 template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
     SC_PROF(2);
+    const int nba = (int)gridDim.x - nbc;
     if ((int)blockIdx.x < nbc)
-        c3_body<C, HC, NAC>(wc, ac, blockIdx.x);
+        c3_body<C, HC, NAC>(wc, ac, (nbc & 7) == 0 ? xcd_perm(blockIdx.x, nbc) : (int)blockIdx.x);
     else
-        a3_body<C, HC, NAC>(wa, aa, blockIdx.x - nbc);
+        a3_body<C, HC, NAC>(wa, aa, (nbc & 7) == 0 ? xcd_perm(blockIdx.x - nbc, nba) : (int)blockIdx.x - nbc);
 }
 // ---------------------------------------------------------------------------------------------------------------
 // f32 GEMM tile on MFMA: C[m, n] = sum_k A(m, k) B(k, n) for one 32x32 output tile; A(m, k) = A[m*sam + k*sak],
@@ -1136,7 +1183,8 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
     const int64_t gbase = j.grad_rel ? j.grad_rel * (*j.agent) : 0;
     if (bx < j.dh.tiles) {
         const GemmP& g = j.dh;
-        const int tm = bx / g.tiles_n, tn = bx - tm * g.tiles_n;
+        const int t = xcd_perm(bx, g.tiles);  // row strips on the XCDs of the k1 / k3 rows they read (xcd_perm)
+        const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
         const int64_t relB = g.relB ? g.relB * (*g.agent) : 0;
         const int n = tn * kT + (l & 31);
         const bool nok = n < g.N;
@@ -1217,15 +1265,17 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
 
 struct Bwd2 {
     BwdJob j0, j1;
-    int nb0;
+    int nb0;  // blocks of job j0, padded to a multiple of 8 (j1's dH1 tiles then start on XCD group 0 too)
+    int n0;   // blocks job j0 uses
 };
 template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
 __global__ __launch_bounds__(256) void sc_bwd(Bwd2 bb) {
     SC_PROF(3);
-    if ((int)blockIdx.x < bb.nb0)
-        bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
-    else
+    if ((int)blockIdx.x < bb.nb0) {
+        if ((int)blockIdx.x < bb.n0) bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
+    } else {
         bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j1, blockIdx.x - bb.nb0);
+    }
 }
 
 struct GradAdam {
@@ -1726,6 +1776,20 @@ size_t zmax(size_t a, size_t b) { return a > b ? a : b; }
 bool g_sc_no_spec = false;  // set by flock_sc_diag_no_spec (flock_set_diag)
 bool spec_shape(const Job& j) { return !g_sc_no_spec && j.H1 == 400 && j.H2 == 300 && j.na == 2; }
 
+// the fc2.weight panels a job's forward GEMMs read: the first problem's (the target actor / actor of the agent) and
+// the second's (the critic, or the critic view the actor phase reads; the critic phase's third problem shares it)
+Pull gemm_pull(const Job& j) {
+    Pull p{};
+    for (int i = 0; i < 2 && i < j.nfwd; ++i) {
+        const GemmP& g = j.fwd[i];
+        p.p[i] = g.B;
+        p.agent[i] = g.relB ? g.agent : nullptr;
+        p.rel[i] = g.relB;
+        p.n[i] = (int64_t)g.K * g.N;  // fc2.weight [H2][H1]: K = H1 rows of B, N = H2 columns
+    }
+    return p;
+}
+
 // One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in five launches; either may be
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
 // computes exactly what the actor phase followed by the critic phase would.
@@ -1737,16 +1801,18 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
         return fail(-5, "flock_sc_round: the two updates must have the same shapes");
     const int C = A.C, rb = A.rb;
     int rc = 0;
-    {  // 1: fc1 rows
+    {  // 1: fc1 rows (+ the L2 pull of the forward GEMMs' fc2.weight panels)
         const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
         const size_t lds = zmax(A.lds1, Z.lds1);
         const dim3 grid(rb, npc + npa);
+        const Pull pc = jc ? gemm_pull(*jc) : Pull{}, pa = ja ? gemm_pull(*ja) : Pull{};
         if (spec_shape(A)) {
             if ((rc = allow_lds(sc_k1<7, 400>, lds))) return rc;
-            hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a);
+            hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a, pc, pa);
         } else {
             SC_C_SWITCH(C, if ((rc = allow_lds(sc_k1<CC, 0>, lds))) return rc;
-                        hipLaunchKernelGGL((sc_k1<CC, 0>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a))
+                        hipLaunchKernelGGL((sc_k1<CC, 0>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a, pc,
+                                           pa))
         }
         if ((rc = launched())) return rc;
     }
@@ -1776,7 +1842,8 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
         Bwd2 bb;
         bb.j0 = A.bw;
         bb.j1 = Z.bw;
-        bb.nb0 = bwd_blocks(A.bw);
+        bb.n0 = bwd_blocks(A.bw);
+        bb.nb0 = (jc && ja) ? (bb.n0 + 7) & ~7 : bb.n0;
         const int nb = bb.nb0 + ((jc && ja) ? bwd_blocks(Z.bw) : 0);
         const size_t lds = zmax(bwd_lds(A.bw), bwd_lds(Z.bw));
         bool fast = true;
