@@ -4,7 +4,8 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# FLOCK_TREE: run against another source tree (an _ab/<sha> export, tools/gpu_ab_trees.sh)
+sys.path.insert(0, os.environ.get("FLOCK_TREE") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
