@@ -215,8 +215,8 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
  * staging rows and the agent index write-through (`sc1`), waits for its stores and publishes a sequence number; the
  * critic phase's row blocks poll it (bounded: 0.2 s; a waiter that gives up sets an error word and computes nothing,
  * flock_sc_pipeline_check returns -6) and read the staging rows `sc1` (MI355X_MICROARCH.md hand-off table, row 1).
- * flock_sc_pipeline_set_gate(p, 0) (and always: data-parallel rounds, rocprofv3 counter collection, which serialises
- * dispatches) makes it a cross-queue event wait instead; it returns the hand-off in use (1 gate, 0 events). Both are
+ * flock_sc_pipeline_set_gate(p, 0) (and always under rocprofv3 counter collection, which serialises dispatches)
+ * makes it a cross-queue event wait instead; it returns the hand-off in use (1 gate, 0 events). Both are
  * deadlock-free whatever hardware queues the streams map to: every snapshot is enqueued before the round that waits
  * for it, and nothing on env_stream waits for that round. The actor phase of the last learn() stays pending until the
  * next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise those of the serial
@@ -246,7 +246,10 @@ int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_f
  * learn): slot i's actor gradient goes to actor_grads[i] (one actor's floats, 16-B aligned, one buffer per slot), and
  * its all-reduce (`allreduce(ctx, actor_grads[i], actor_floats, actor_stream)`, e.g. over a second process group) and
  * Adam step run on a stream of the pipeline's own, behind an event for the round's gradient launches; only the critic
- * all-reduce and the critic Adam stay on learner_stream, whose next critic phase needs them. Every later reader of
+ * all-reduce and the critic Adam stay on learner_stream, whose next critic phase needs them, and of the critic all-reduce
+ * only the fc1 / LayerNorm-1 part [0, fc2.weight offset) follows the gradient launch: the rest, complete after the bwd
+ * launch, is all-reduced (first `allreduce` call of the round, on a third stream of the pipeline's own) while the
+ * gradient launch runs. Every later reader of
  * that agent's actor on learner_stream (its next learn: 256 learns later at config 3) waits for the actor step's
  * event unless the host already sees it complete; flush joins the actor stream into learner_stream. Bitwise the
  * unsplit rounds (agent_simple_shared_critic.py:137-150; the reference steps the actor right after the critic). */

@@ -1794,7 +1794,13 @@ Pull gemm_pull(const Job& j) {
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
 // computes exactly what the actor phase followed by the critic phase would.
 
-int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
+// a callback between the bwd launch and the gradient / Adam launch (data-parallel pipelines: the all-reduce of the
+// critic gradient the bwd launch completed starts there, beside the gradient launch)
+struct MidHook {
+    int (*fn)(void*);
+    void* ctx;
+};
+int launch_round(hipStream_t st, const Job* jc, const Job* ja, const MidHook* mid = nullptr) {
     const Job& A = jc ? *jc : *ja;  // the first job (placeholder arguments for an absent one)
     const Job& Z = ja ? *ja : *jc;
     if (jc && ja && (jc->B != ja->B || jc->in != ja->in || jc->na != ja->na || jc->H1 != ja->H1 || jc->H2 != ja->H2))
@@ -1867,6 +1873,7 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja) {
                           : launch_bwd_v<0, 1, 1, 1, 16, 16>(st, bb, grid, lds);
         if (rc) return rc;
     }
+    if (mid && (rc = mid->fn(mid->ctx))) return rc;
     // 5: fc1 / LN1 gradients + every Adam step
     if (A.ga.nblk > kMaxRedBlocks || Z.ga.nblk > kMaxRedBlocks || A.bw.nblk > kMaxRedBlocks)
         return fail(-2, "flock_sc: too many reduction blocks (fc1 * in_dim too large)");
@@ -2081,6 +2088,7 @@ struct FlockScPipeline {
     // round wrote, then the Adam launch with grad_scale
     bool dp;
     FlockScUpdate ug[kMaxSlots], uadam[kMaxSlots];
+    Job jgc[kMaxSlots], jga[kMaxSlots];  // the gradient rounds' launch arguments (ug), built once
     float* bucket;
     int64_t actor_off, bucket_floats, critic_floats;
     const float* grad_scale;
@@ -2091,6 +2099,11 @@ struct FlockScPipeline {
     bool split;
     hipStream_t actor_stream;
     hipEvent_t grads_done[kMaxSlots], actor_done[kMaxSlots], actor_joined;
+    // split rounds: the critic gradient's [fc2.weight .. q.bias] part (complete after the bwd launch) is all-reduced on
+    // comm_stream beside the gradient launch; only the fc1 / LN1 part ([0, critic_w2)) follows the gradient launch
+    hipStream_t comm_stream;
+    hipEvent_t bwd_done, ar_done;
+    int64_t critic_w2;
     bool actor_used[kMaxSlots];
     int64_t actor_floats;
     FlockAllreduceFn actor_allreduce;
@@ -2117,9 +2130,27 @@ int wait_unless_done(hipStream_t st, hipEvent_t ev) {
 // the actor step of `agent` that is still in flight on actor_stream (split data-parallel rounds): every reader of
 // that agent's actor, target actor, moments or step count on the learner stream waits for it
 int wait_actor(FlockScPipeline* p, hipStream_t ls, int64_t agent) {
-    if (!p->split || agent < 0 || agent >= p->n_agents) return 0;
+    if (!p->last_actor_slot || agent < 0 || agent >= p->n_agents) return 0;
     const int s = p->last_actor_slot[agent];
     return s >= 0 ? wait_unless_done(ls, p->actor_done[s]) : 0;
+}
+
+// one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none);
+// agents: the learns' agent indices (split data-parallel rounds)
+// the early part of a split round's critic all-reduce (MidHook): the bwd launch has completed the critic gradient's
+// [fc2.weight, total) part; it is all-reduced on comm_stream while the gradient launch runs on the learner stream
+struct EarlyAr {
+    FlockScPipeline* p;
+    hipStream_t ls;
+};
+int early_critic_allreduce(void* ctx) {
+    const EarlyAr& e = *static_cast<EarlyAr*>(ctx);
+    FlockScPipeline* p = e.p;
+    if (hipEventRecord(p->bwd_done, e.ls) != hipSuccess || hipStreamWaitEvent(p->comm_stream, p->bwd_done, 0) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline: stream operation failed");
+    if (int rc = p->allreduce(p->allreduce_ctx, p->bucket + p->critic_w2, p->critic_floats - p->critic_w2, p->comm_stream))
+        return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
+    return hipEventRecord(p->ar_done, p->comm_stream) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: event record");
 }
 
 // one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none);
@@ -2127,21 +2158,26 @@ int wait_actor(FlockScPipeline* p, hipStream_t ls, int64_t agent) {
 int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a, int64_t agent_c, int64_t agent_a) {
     if (!p->dp) return launch_round(ls, c >= 0 ? &p->jc[c] : nullptr, a >= 0 ? &p->ja[a] : nullptr);
     int rc = 0;
+    const Job* gc = c >= 0 ? &p->jgc[c] : nullptr;
+    const Job* ga = a >= 0 ? &p->jga[a] : nullptr;
     if (!p->split) {
         // gradients only (do_adam = 0) into the bucket, ONE all-reduce (sum) of the part they wrote, then the Adam
         // launch (gradients scaled by *grad_scale): SharedCriticLearner._dp_round
-        if ((rc = flock_sc_round(ls, c >= 0 ? &p->ug[c] : nullptr, a >= 0 ? &p->ug[a] : nullptr))) return rc;
+        if ((rc = launch_round(ls, gc, ga))) return rc;
         const int64_t lo = c >= 0 ? 0 : p->actor_off, hi = a >= 0 ? p->bucket_floats : p->critic_floats;
         if ((rc = p->allreduce(p->allreduce_ctx, p->bucket + lo, hi - lo, ls)))
             return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
         return flock_sc_round_adam(ls, c >= 0 ? &p->uadam[c] : nullptr, a >= 0 ? &p->uadam[a] : nullptr,
                                    p->grad_scale);
     }
-    // split: the critic half stays on the learner chain (the next critic phase needs this critic step); the actor
-    // half is all-reduced and stepped on actor_stream (that actor is read again only by its agent's next learn)
+    // split: the critic half stays on the learner chain (the next critic phase needs this critic step), its larger
+    // part all-reduced beside the gradient launch; the actor half is all-reduced and stepped on actor_stream (that
+    // actor is read again only by its agent's next learn)
     if ((rc = wait_actor(p, ls, agent_c))) return rc;
     if (a >= 0 && p->actor_used[a] && (rc = wait_unless_done(ls, p->actor_done[a]))) return rc;  // slot a's buffer
-    if ((rc = flock_sc_round(ls, c >= 0 ? &p->ug[c] : nullptr, a >= 0 ? &p->ug[a] : nullptr))) return rc;
+    EarlyAr ear{p, ls};
+    const MidHook mid{&early_critic_allreduce, &ear};
+    if ((rc = launch_round(ls, gc, ga, c >= 0 ? &mid : nullptr))) return rc;
     if (a >= 0) {
         hipStream_t as = p->actor_stream;
         if (hipEventRecord(p->grads_done[a], ls) != hipSuccess || hipStreamWaitEvent(as, p->grads_done[a], 0) != hipSuccess)
@@ -2154,8 +2190,9 @@ int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a, int64_t age
         p->last_actor_slot[agent_a] = a;
     }
     if (c >= 0) {
-        if ((rc = p->allreduce(p->allreduce_ctx, p->bucket, p->critic_floats, ls)))
+        if ((rc = p->allreduce(p->allreduce_ctx, p->bucket, p->critic_w2, ls)))
             return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
+        if (hipStreamWaitEvent(ls, p->ar_done, 0) != hipSuccess) return fail(-4, "flock_sc_pipeline: stream wait");
         if ((rc = flock_sc_round_adam(ls, &p->uadam[c], nullptr, p->grad_scale))) return rc;
     }
     return 0;
@@ -2209,6 +2246,9 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->split = false;
     p->actor_stream = nullptr;
     p->actor_joined = nullptr;
+    p->comm_stream = nullptr;
+    p->bwd_done = p->ar_done = nullptr;
+    p->critic_w2 = 0;
     p->last_actor_slot = nullptr;
     p->n_agents = 0;
     p->gate = nullptr;
@@ -2228,7 +2268,7 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
 
 int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on) {
     if (!p) return fail(-3, "flock_sc_pipeline_set_gate: NULL pipeline");
-    p->gate_on = on != 0 && p->gate && !p->dp && !counter_collection();
+    p->gate_on = on != 0 && p->gate && !counter_collection();
     return p->gate_on ? 1 : 0;
 }
 
@@ -2266,7 +2306,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
                             uint64_t counter, int64_t agent) {
     if (!p) return fail(-3, "flock_sc_pipeline_learn: NULL pipeline");
     if (rows < 1 || agent < 0) return fail(-5, "flock_sc_pipeline_learn: need rows >= 1 and an agent");
-    if (p->split && agent >= p->n_agents) return fail(-5, "flock_sc_pipeline_learn: agent out of range");
+    if (p->last_actor_slot && agent >= p->n_agents) return fail(-5, "flock_sc_pipeline_learn: agent out of range");
     hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
     const int s = p->slot;
     const FlockScUpdate& u = p->u[s];
@@ -2286,13 +2326,13 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
                            const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq);
         if ((rc = launched())) return rc;
-        p->jc[s].a.gate = p->gate;
-        p->jc[s].a.gate_seq = seq;
+        p->jc[s].a.gate = p->jgc[s].a.gate = p->gate;
+        p->jc[s].a.gate_seq = p->jgc[s].a.gate_seq = seq;
     } else {
         if ((rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                          u.in_dim, u.n_actions, &p->ring, &p->staging[s])))
             return rc;
-        p->jc[s].a.gate = nullptr;
+        p->jc[s].a.gate = p->jgc[s].a.gate = nullptr;
         if (hipEventRecord(p->snap_done[s], es) != hipSuccess || hipStreamWaitEvent(ls, p->snap_done[s], 0) != hipSuccess)
             return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     }
@@ -2311,7 +2351,6 @@ int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_f
     if (((uintptr_t)(bucket + actor_offset) & 15) != 0)
         return fail(-5, "flock_sc_pipeline_set_dp: the actor part of the bucket must be 16-B aligned");
     p->dp = true;
-    p->gate_on = false;  // data-parallel rounds wait for their snapshots on events
     p->bucket = bucket;
     p->critic_floats = critic_floats;
     p->actor_off = actor_offset;
@@ -2327,6 +2366,8 @@ int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_f
         a.do_adam = 0;
         a.update_rate = 0;
         p->ug[i] = a;  // the gradient round
+        critic_job(&p->ug[i], p->jgc[i]);
+        actor_job(&p->ug[i], p->jga[i]);
     }
     return 0;
 }
@@ -2353,9 +2394,15 @@ int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads
     for (int i = 0; i < n_agents; ++i) p->last_actor_slot[i] = -1;
     p->n_agents = n_agents;
     p->actor_floats = actor_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).total;
+    if (!p->comm_stream && (hipStreamCreateWithFlags(&p->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+                            hipEventCreateWithFlags(&p->bwd_done, hipEventDisableTiming) != hipSuccess ||
+                            hipEventCreateWithFlags(&p->ar_done, hipEventDisableTiming) != hipSuccess))
+        return fail(-4, "flock_sc_pipeline_set_dp_actor: stream");
+    p->critic_w2 = critic_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).W2;
     for (int i = 0; i < p->n; ++i) {
         p->ug[i].actor_grad_out = actor_grads[i];
         p->uadam[i].actor_grad_out = actor_grads[i];
+        actor_job(&p->ug[i], p->jga[i]);
     }
     p->actor_allreduce = allreduce;
     p->actor_ctx = ctx;
@@ -2408,6 +2455,9 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (p->gate) (void)hipFree(p->gate);
     if (p->actor_stream) (void)hipStreamDestroy(p->actor_stream);
     if (p->actor_joined) (void)hipEventDestroy(p->actor_joined);
+    if (p->comm_stream) (void)hipStreamDestroy(p->comm_stream);
+    if (p->bwd_done) (void)hipEventDestroy(p->bwd_done);
+    if (p->ar_done) (void)hipEventDestroy(p->ar_done);
     delete[] p->last_actor_slot;
     for (int i = 0; i < p->n; ++i) {
         hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};

@@ -134,7 +134,7 @@ class SharedCriticLearner:
         self.snapshot = bool(snapshot and fused)
         self.n_slots = max(2, int(n_slots))
         # the native pipeline's snapshot hand-off (pipeline()): "gate" the device-side gate polled by the critic row
-        # blocks (single GPU), "event" a cross-queue event wait
+        # blocks, "event" a cross-queue event wait
         if handoff not in ("gate", "event"):
             raise ValueError("handoff is 'gate' or 'event'")
         self.handoff = handoff
@@ -528,8 +528,7 @@ class SharedCriticLearner:
                     self.dp_actor_grads = [torch.zeros(self.actors.per_agent, device=self.device)
                                            for _ in range(self.n_slots)]
                     p.set_dp_actor(self.actor_group.boxed(), self.dp_actor_grads)
-            else:
-                p.set_gate(self.handoff == "gate")
+            p.set_gate(self.handoff == "gate")
             self._pipe = p
         return self._pipe
 
