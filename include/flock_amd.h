@@ -124,9 +124,6 @@ typedef struct FlockStepExt {
      * the raw positions. Ignored by the periodic v2 step (gym_flock_v2.py:135-151 never normalises). Such steps take
      * the full-scan kernels (no cell list). */
     int normalize_distance;
-    /* non-NULL (v2 with a one-row-per-agent ring insert, the shared-critic loop): the previous learn()'s minibatch
-     * snapshot rides in block 0 of the step's first launch (include/flock_learn.h, FlockStepSnapshot) */
-    const struct FlockStepSnapshot* snapshot;
 } FlockStepExt;
 int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,
                       float dt, float v_min, float v_max, int periodic, int rigid_boundary,

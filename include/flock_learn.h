@@ -176,22 +176,6 @@ typedef struct FlockScRows {
 int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
                            int64_t* agent_out, int64_t agent, int in_dim, int n_actions, const FlockScRows* ring,
                            const FlockScRows* staging);
-/* The same snapshot carried by the NEXT env step (flock_sc_pipeline_learn_deferred fills it, FlockStepExt.snapshot
- * passes it to flock_step_v2_ext): block 0 of that step's first launch copies the B sampled rows of `src` (the ring) to
- * `dst` (the slot's staging rows) with write-through (`sc1`) stores, waits for them and publishes gate[0] = seq; every
- * env block of the launch waits for gate[0] >= seq before its replay-ring stores (the rows the snapshot reads are
- * rewritten by this very step), and the learn()'s critic row blocks wait for it as for a standalone snapshot. vec:
- * the 16-B / 8-B row copies (in_dim 4, n_actions 2, aligned fields). */
-typedef struct FlockStepSnapshot {
-    int B, in_dim, n_actions, vec;
-    int64_t rows;
-    uint64_t seed, counter;
-    int64_t agent;
-    int64_t* agent_out;
-    FlockScRows src, dst;
-    unsigned long long* gate;
-    unsigned long long seq;
-} FlockStepSnapshot;
 /* Agent.choose_action of every agent on every env row in one launch (learners/maddpg_shared_critic/
  * agent_simple_shared_critic.py:92-107; actor ddpg_network.py:132-141; OUActionNoiseGPU utils.py:15-18 with one
  * process per (row, agent)). obs [rows][n_agents][in_dim] f32; actors: the agent-major actor buffer of
@@ -246,17 +230,6 @@ int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on);
 int flock_sc_pipeline_gated(const FlockScPipeline* p);
 int flock_sc_pipeline_check(FlockScPipeline* p);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
-/* Deferred learns (the C++ loop, torch.classes.flock.ScTrainLoop; gate hand-off): flock_sc_pipeline_defer registers
- * learn() t exactly as flock_sc_pipeline_learn would (slot, the slot wait on env_stream, Philox rows, agent) but, instead
- * of launching the snapshot, writes its descriptor to *snap for the caller's NEXT env step (FlockStepExt.snapshot: it
- * rides in block 0 of that step's first launch) and returns 1; flock_sc_pipeline_commit(p, 1) then enqueues the learn's
- * rounds, after that env step, so every round is enqueued behind the snapshot it waits for. commit(p, 0): no env step
- * carried it, the standalone snapshot is launched on env_stream first (e.g. after the loop's last step). With the event
- * hand-off defer runs the learn at once and returns 0. A deferred learn must be committed before the next defer, learn
- * or flush (-5). Results are bitwise those of flock_sc_pipeline_learn. */
-int flock_sc_pipeline_defer(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
-                            uint64_t counter, int64_t agent, FlockStepSnapshot* snap);
-int flock_sc_pipeline_commit(FlockScPipeline* p, int carried);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);
 /* Data-parallel rounds (one replica per GPU, the same learn() sequence on every rank): after this call every round
  * of the pipeline runs as gradients only (do_adam = 0, critic_grad = bucket, actor_grad_out = bucket + actor_off),

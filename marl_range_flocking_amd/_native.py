@@ -130,7 +130,7 @@ class FlockStepExt(ctypes.Structure):
     """Mirror of ``FlockStepExt`` (include/flock_amd.h): optional extras of the *_ext step entry points."""
 
     _fields_ = [("ring", ctypes.POINTER(FlockRing)), ("seeds", _c_void_p), ("launches", _c_int),
-                ("normalize_distance", _c_int), ("snapshot", _c_void_p)]
+                ("normalize_distance", _c_int)]
 
 
 for _name in ("flock_step_v2_ext", "flock_step_uw_ext", "flock_step_uw_discrete_ext", "flock_step_flock_ext"):
@@ -156,8 +156,6 @@ SIGNATURES.update({
     "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],
     "flock_sc_pipeline_flush": [_c_void_p, _c_void_p],
     "flock_sc_pipeline_set_gate": [_c_void_p, _c_int],
-    "flock_sc_pipeline_defer": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64, _c_void_p],
-    "flock_sc_pipeline_commit": [_c_void_p, _c_int],
     "flock_sc_pipeline_check": [_c_void_p],
     "flock_sc_pipeline_gated": [_c_void_p],
     "flock_sc_pipeline_set_dp": [_c_void_p, _c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_void_p,

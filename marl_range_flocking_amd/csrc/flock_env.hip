@@ -48,7 +48,6 @@
 
 #include "flock_amd.h"
 #include "flock_mem.h"
-#include "flock_snap.h"
 
 #pragma clang fp contract(off)
 
@@ -107,10 +106,6 @@ struct Params {
     const uint8_t* env_mask;
     uint8_t* valid;
     int normalize;  // normalize_distance: Euclidean kNN of positions / max_e |p| (full-scan path only, see dispatch)
-    // a learn()'s minibatch snapshot carried by this launch (FlockStepExt.snapshot; the step's first launch only):
-    // block 0 runs it, the env blocks are blockIdx.x - 1 and wait for its gate before their replay-ring stores
-    int snap_on;
-    FlockStepSnapshot snap;
 };
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -846,16 +841,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     const unsigned long long st0_ = t_prev, rt0_ = __builtin_amdgcn_s_memrealtime();  // in-kernel clock
 #endif
     const int t = threadIdx.x;
-    if (p.snap_on && blockIdx.x == 0) {  // the previous learn()'s minibatch snapshot (csrc/flock_snap.h)
-        flock_snap::snapshot_block(p.snap);
-        return;
-    }
-    const int bx = (int)blockIdx.x - p.snap_on;  // this env block
     const int g = t / p.N;
     const int i = t - g * p.N;
     const bool in_group = g < p.G;
     PHASE_COUNT(20, 1);
-    const int env = p.env0 + bx * p.G + g;
+    const int env = p.env0 + blockIdx.x * p.G + g;
     const bool active = in_group && env < p.E;
     const size_t a = (size_t)env * p.N + i;
     if (in_group && i == 0) flags[g] = 0;
@@ -926,7 +916,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     if (active && variant == FLOCK_VARIANT_UW) prev_h = p.prev_heading[a];
     if constexpr (SPL > 1 && kMemEarly) {  // split instantiation: lane groups 1..3 roll memory frames 0..2 (k = 4)
         const int q = t / NC, ia = t - q * NC;
-        const int envb = p.env0 + bx;
+        const int envb = p.env0 + (int)blockIdx.x;
         if (q >= 1 && q < kMem && envb < p.E && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
             const size_t ab = (size_t)envb * NC + ia;
             reinterpret_cast<float4*>(p.mem_out + ab * kMem * 4)[q] =
@@ -1059,7 +1049,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     int pf_sink = 0;
     const bool pf_on = PFM != 0 && p.pf_ahead > 0;  // PFM: 1 the kinematics inputs, 3 also the late inputs
     if (pf_on) {
-        const int eb = p.env0 + (bx + p.pf_ahead) * p.G;
+        const int eb = p.env0 + (int)(blockIdx.x + p.pf_ahead) * p.G;
         const int ne = min(p.G, p.E - eb);
         if (ne > 0) {
             const int nb = ne * p.N;             // agents of that block
@@ -1305,7 +1295,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     if constexpr (SPL > 1) {  // split scan: every lane group takes 1 / SPL of the candidates, then the merge
         constexpr int Q = NC / SPL;
         const int q = t / NC, ia = t - q * NC;
-        const bool live = p.env0 + bx < p.E;
+        const bool live = p.env0 + (int)blockIdx.x < p.E;
         uint32_t part[L];
         if (live) {
             const float2 me = lpos[ia];  // published by the phase-2 barrier
@@ -1430,16 +1420,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
                 r = coll ? -5.0f : 0.01f;  // gym_flock_v2.py:217-220, gym_flock.py:142-145
             }
             stnt(p.reward + a, r);
-            if (p.snap_on) {  // the snapshot block reads ring rows this launch rewrites: wait until it has published
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while ((long long)(flock_mem::ld_sc1(p.snap.gate) - p.snap.seq) < 0) {
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s: the error word, no hang
-                        __hip_atomic_store(p.snap.gate + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
             if (p.r_state && r_unit >= p.r_skip) {  // fused replay insert: row (start + unit - skip) mod cap
                 int64_t row = p.r_start + r_unit - p.r_skip;
                 if (row >= p.r_cap) row -= p.r_cap;
@@ -1752,23 +1732,21 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         Params q = p;
         // one block generation ahead (two measured flat at config 5, round 4)
         q.pf_ahead = (pf_res > 0 && c.blocks > pf_res) ? pf_res : 0;
-        hipLaunchKernelGGL(kern, dim3(c.blocks + p.snap_on), dim3(c.T), c.lds, s, q);
+        hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(c.T), c.lds, s, q);
         return true;
     }
     if (parts <= 1) {
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks + p.snap_on),
-                           dim3(c.T), c.lds, s, p);
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks), dim3(c.T), c.lds, s,
+                           p);
         return true;
     }
-    // the step as `parts` back-to-back launches over consecutive env ranges (same results: envs are independent); a
-    // carried snapshot rides in the first
+    // the step as `parts` back-to-back launches over consecutive env ranges (same results: envs are independent)
     const int per = (c.blocks + parts - 1) / parts;
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
-        q.snap_on = b0 == 0 ? p.snap_on : 0;
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>),
-                           dim3(min(per, c.blocks - b0) + q.snap_on), dim3(c.T), c.lds, s, q);
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
+                           dim3(c.T), c.lds, s, q);
     }
     return true;
 }
@@ -1781,17 +1759,16 @@ void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
         if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
     }
-    const dim3 grid(c.blocks + p.snap_on);
     if (p.cells) {
         if (p.periodic)
-            hipLaunchKernelGGL((step_kernel<L, true, true>), grid, dim3(c.T), c.lds, s, p);
+            hipLaunchKernelGGL((step_kernel<L, true, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
         else
-            hipLaunchKernelGGL((step_kernel<L, false, true>), grid, dim3(c.T), c.lds, s, p);
+            hipLaunchKernelGGL((step_kernel<L, false, true>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
     } else {
         if (p.periodic)
-            hipLaunchKernelGGL((step_kernel<L, true, false>), grid, dim3(c.T), c.lds, s, p);
+            hipLaunchKernelGGL((step_kernel<L, true, false>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
         else
-            hipLaunchKernelGGL((step_kernel<L, false, false>), grid, dim3(c.T), c.lds, s, p);
+            hipLaunchKernelGGL((step_kernel<L, false, false>), dim3(c.blocks), dim3(c.T), c.lds, s, p);
     }
 }
 
@@ -1962,26 +1939,13 @@ int set_ring(Params& p, const FlockRing* ring, int E, int N, const char* who) {
 int step_v2_impl(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance, float dt,
                  float v_min, float v_max, int periodic, int rigid_boundary, float* pos, float* heading,
                  const float* action, float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done,
-                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds, int launches = 0, int normalize = 0,
-                 const FlockStepSnapshot* snap = nullptr) {
+                 uint8_t* any_done, const FlockRing* ring, uint16_t* seeds, int launches = 0, int normalize = 0) {
     int rc = check_common(E, N, k);
     if (rc) return rc;
     if (E && (!pos || !heading || !action || !vel || !dnn || !reward || !done || !any_done))
         return fail(FLOCK_E_NULL, "flock_step_v2: NULL pointer");
     Params p = base(E, N, k, box);
     if ((rc = set_ring(p, ring, E, N, "flock_step_v2_store"))) return rc;
-    if (snap) {  // a learn()'s minibatch snapshot rides in block 0 of the first launch (FlockStepExt.snapshot)
-        if (!ring || ring->group != 1 || ring->env_done)
-            return fail(FLOCK_E_ARG, "flock_step_v2_ext: a carried snapshot needs the one-row-per-agent ring insert");
-        if (!snap->gate || !snap->agent_out || snap->B < 1 || snap->rows < 1 || snap->in_dim < 1 || snap->n_actions < 1 ||
-            !snap->src.state || !snap->src.new_state || !snap->src.action || !snap->src.reward || !snap->src.terminal ||
-            !snap->dst.state || !snap->dst.new_state || !snap->dst.action || !snap->dst.reward || !snap->dst.terminal)
-            return fail(FLOCK_E_ARG, "flock_step_v2_ext: incomplete snapshot");
-        if (E) {
-            p.snap_on = 1;
-            p.snap = *snap;
-        }
-    }
     p.variant = FLOCK_VARIANT_V2;
     p.periodic = periodic != 0;
     p.rigid = rigid_boundary != 0;
@@ -2035,7 +1999,7 @@ int flock_step_v2_ext(void* stream, int E, int N, int k, float box, float sensor
     return step_v2_impl(stream, E, N, k, box, sensor_range, collision_distance, dt, v_min, v_max, periodic,
                         rigid_boundary, pos, heading, action, vel, dnn, nn_idx, reward, done, any_done,
                         ext ? ext->ring : nullptr, ext ? ext->seeds : nullptr, ext ? ext->launches : 0,
-                        ext ? ext->normalize_distance : 0, ext ? ext->snapshot : nullptr);
+                        ext ? ext->normalize_distance : 0);
 }
 
 int flock_step_uw_ext(void* stream, int E, int N, int k, float box, float sensor_range, float collision_distance,

@@ -30,7 +30,6 @@
 
 #include "flock_learn.h"
 #include "flock_mem.h"
-#include "flock_snap.h"
 #include "learn_internal.h"
 
 namespace {
@@ -171,7 +170,31 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 __device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
 
-using flock_snap::sample_row;
+// learn() prologue: the agent index and the minibatch rows (Philox4x32-10, counter = (learn counter, row))
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return make_uint4(c0, c1, c2, c3);
+}
+// the replay row that minibatch row r of learn `counter` samples: Philox4x32-10(seed, (r, 0x5C5C5C5C, counter)) mod rows
+// (uniform with replacement, ReplayBuffer.sample_buffer utils.py:65-76; sc_prep, the snapshot and the direct rounds'
+// k1 rows all draw it this way)
+__device__ __forceinline__ int64_t sample_row(uint64_t seed, uint64_t counter, int64_t rows, int r) {
+    const uint4 q = philox4(seed, (uint32_t)r, 0x5C5C5C5Cu, (uint32_t)counter, (uint32_t)(counter >> 32));
+    const uint64_t u = ((uint64_t)q.x << 32) | q.y;
+    return (int64_t)(u % (uint64_t)rows);
+}
 __device__ __forceinline__ float rsqrt_rn(float x) { return 1.0f / __builtin_sqrtf(x); }
 
 // copy n floats global -> LDS (dst 16-B aligned) with every load of a round issued before any LDS store
@@ -1872,17 +1895,68 @@ __global__ __launch_bounds__(256) void sc_prep(int B, int64_t rows, uint64_t see
     if (idx && r < B) idx[r] = sample_row(seed, counter, rows, r);
 }
 
+// learn() prologue with a minibatch snapshot: the sampled rows of every replay field are copied to staging rows
+// 0..B-1, so the update can read the staging copy (with the identity index) while the next env step rewrites the ring.
+// SC1: every staging store write-through (the device-side gate's producer, csrc/flock_mem.h)
+template <bool SC1>
+__device__ __forceinline__ void snapshot_row(int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
+                                             int in_dim, int n_actions, const FlockScRows& src,
+                                             const FlockScRows& dst, int vec, int r) {
+    const int64_t row = sample_row(seed, counter, rows, r);  // the row sc_prep samples for r
+    if (idx_out) idx_out[r] = row;
+    auto st = [](auto* p, auto v) {
+        if constexpr (SC1)
+            flock_mem::st_sc1(p, v);
+        else
+            *p = v;
+    };
+    // every load of the row first, then the stores (src and dst may alias as far as the compiler knows: interleaved,
+    // each store would wait for its load, one memory round trip per field)
+    if (vec) {  // the v2 shapes (in_dim 4, n_actions 2) with aligned fields: 16-B / 8-B rows
+        const float4 s0 = *reinterpret_cast<const float4*>(src.state + row * 4);
+        const float4 ns = *reinterpret_cast<const float4*>(src.new_state + row * 4);
+        const float2 ac = *reinterpret_cast<const float2*>(src.action + row * 2);
+        const float rw = src.reward[row], te = src.terminal[row];
+        st(reinterpret_cast<float4*>(dst.state + (int64_t)r * 4), s0);
+        st(reinterpret_cast<float4*>(dst.new_state + (int64_t)r * 4), ns);
+        st(reinterpret_cast<float2*>(dst.action + (int64_t)r * 2), ac);
+        st(dst.reward + r, rw);
+        st(dst.terminal + r, te);
+        return;
+    }
+    for (int c = 0; c < in_dim; ++c) {
+        const float a = src.state[row * in_dim + c], b = src.new_state[row * in_dim + c];
+        st(dst.state + (int64_t)r * in_dim + c, a);
+        st(dst.new_state + (int64_t)r * in_dim + c, b);
+    }
+    for (int c = 0; c < n_actions; ++c) st(dst.action + (int64_t)r * n_actions + c, src.action[row * n_actions + c]);
+    const float rw = src.reward[row], te = src.terminal[row];
+    st(dst.reward + r, rw);
+    st(dst.terminal + r, te);
+}
+
 __global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint64_t seed, uint64_t counter,
                                                         int64_t* idx_out, int64_t* agent_out, int64_t agent,
                                                         int in_dim, int n_actions, FlockScRows src,
                                                         FlockScRows dst, int vec) {
     const int r = blockIdx.x * 64 + threadIdx.x;
     if (r == 0) *agent_out = agent;
-    if (r < B) flock_snap::snapshot_row<false>(rows, seed, counter, idx_out, in_dim, n_actions, src, dst, vec, r);
+    if (r < B) snapshot_row<false>(rows, seed, counter, idx_out, in_dim, n_actions, src, dst, vec, r);
 }
 
-// the same snapshot as ONE block that publishes it through the device-side gate (csrc/flock_snap.h)
-__global__ __launch_bounds__(256) void sc_prep_snapshot_gate(FlockStepSnapshot sn) { flock_snap::snapshot_block(sn); }
+// the same snapshot as ONE block that publishes it through the device-side gate: rows and agent stored `sc1`, every
+// wave's stores waited for, a workgroup barrier, then one lane's `sc1` store of gate[0] = seq (csrc/flock_mem.h)
+__global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows, uint64_t seed, uint64_t counter,
+                                                             int64_t* agent_out, int64_t agent, int in_dim,
+                                                             int n_actions, FlockScRows src, FlockScRows dst, int vec,
+                                                             unsigned long long* gate, unsigned long long seq) {
+    if (threadIdx.x == 0) flock_mem::st_sc1(agent_out, agent);
+    for (int r = threadIdx.x; r < B; r += 256)
+        snapshot_row<true>(rows, seed, counter, nullptr, in_dim, n_actions, src, dst, vec, r);
+    flock_mem::wait_vmem();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(gate, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 }  // namespace
 
@@ -2036,12 +2110,6 @@ struct FlockScPipeline {
     void* actor_ctx;
     int n_agents;
     int* last_actor_slot;  // [n_agents]: the slot of the agent's last actor step on actor_stream, -1: none
-    // a deferred learn (flock_sc_pipeline_defer): its slot, agent, snapshot and streams until flock_sc_pipeline_commit
-    bool deferred;
-    int def_slot;
-    int64_t def_agent;
-    FlockStepSnapshot def_snap;
-    hipStream_t def_es, def_ls;
 };
 
 namespace {
@@ -2172,7 +2240,6 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
         p->actor_used[i] = false;
     }
     p->slot = 0;
-    p->deferred = false;
     p->pending = -1;
     p->pending_agent = -1;
     p->dp = false;
@@ -2238,7 +2305,6 @@ int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent) {
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent) {
     if (!p) return fail(-3, "flock_sc_pipeline_learn: NULL pipeline");
-    if (p->deferred) return fail(-5, "flock_sc_pipeline_learn: a deferred learn is not committed");
     if (rows < 1 || agent < 0) return fail(-5, "flock_sc_pipeline_learn: need rows >= 1 and an agent");
     if (p->last_actor_slot && agent >= p->n_agents) return fail(-5, "flock_sc_pipeline_learn: agent out of range");
     hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
@@ -2257,9 +2323,8 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         for (const FlockScRows* x : {&src, &dst})
             vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
         const unsigned long long seq = ++p->seq;
-        const FlockStepSnapshot sn{u.B, u.in_dim, u.n_actions, vec, rows, seed, counter, agent,
-                                   const_cast<int64_t*>(u.agent), src, dst, p->gate, seq};
-        hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, sn);
+        hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
+                           const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq);
         if ((rc = launched())) return rc;
         p->jc[s].a.gate = p->jgc[s].a.gate = p->gate;
         p->jc[s].a.gate_seq = p->jgc[s].a.gate_seq = seq;
@@ -2272,51 +2337,6 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
             return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     }
     return enqueue_rounds(p, ls, s, agent);
-}
-
-int flock_sc_pipeline_defer(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
-                            uint64_t counter, int64_t agent, FlockStepSnapshot* snap) {
-    if (!p || !snap) return fail(-3, "flock_sc_pipeline_defer: NULL argument");
-    if (p->deferred) return fail(-5, "flock_sc_pipeline_defer: commit the previous deferred learn first");
-    if (!p->gate_on) {  // the event hand-off: nothing to carry, the learn runs now
-        const int rc = flock_sc_pipeline_learn(p, env_stream, learner_stream, rows, seed, counter, agent);
-        return rc ? rc : 0;
-    }
-    if (rows < 1 || agent < 0) return fail(-5, "flock_sc_pipeline_defer: need rows >= 1 and an agent");
-    if (p->last_actor_slot && agent >= p->n_agents) return fail(-5, "flock_sc_pipeline_defer: agent out of range");
-    hipStream_t es = (hipStream_t)env_stream;
-    const int s = p->slot;
-    const FlockScUpdate& u = p->u[s];
-    if (p->used[s] && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_defer: wait");
-    const FlockScRows& src = p->ring;
-    const FlockScRows& dst = p->staging[s];
-    int vec = u.in_dim == 4 && u.n_actions == 2;
-    for (const FlockScRows* x : {&src, &dst})
-        vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
-    const unsigned long long seq = ++p->seq;
-    *snap = FlockStepSnapshot{u.B, u.in_dim, u.n_actions, vec, rows, seed, counter, agent,
-                              const_cast<int64_t*>(u.agent), src, dst, p->gate, seq};
-    p->jc[s].a.gate = p->jgc[s].a.gate = p->gate;
-    p->jc[s].a.gate_seq = p->jgc[s].a.gate_seq = seq;
-    p->deferred = true;
-    p->def_slot = s;
-    p->def_agent = agent;
-    p->def_snap = *snap;
-    p->def_es = es;
-    p->def_ls = (hipStream_t)learner_stream;
-    return 1;
-}
-
-int flock_sc_pipeline_commit(FlockScPipeline* p, int carried) {
-    if (!p) return fail(-3, "flock_sc_pipeline_commit: NULL pipeline");
-    if (!p->deferred) return 0;
-    if (!carried) {  // no env step carried the snapshot: it runs on its own, right behind the env stream's work
-        hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, p->def_es, p->def_snap);
-        if (int rc = launched()) return rc;
-    }
-    p->deferred = false;
-    return enqueue_rounds(p, p->def_ls, p->def_slot, p->def_agent);
 }
 
 int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_floats, int64_t actor_offset,
@@ -2392,7 +2412,6 @@ int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads
 
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream) {
     if (!p) return fail(-3, "flock_sc_pipeline_flush: NULL pipeline");
-    if (p->deferred) return fail(-5, "flock_sc_pipeline_flush: a deferred learn is not committed");
     hipStream_t ls = (hipStream_t)learner_stream;
     const int q = p->pending;
     if (q >= 0) {

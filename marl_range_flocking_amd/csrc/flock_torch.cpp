@@ -95,7 +95,7 @@ void step_v2_hip(const Tensor& pos, const Tensor& heading, const Tensor& action,
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0, nullptr};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_v2_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, (float)v_min,
                                (float)v_max, periodic, rigid_boundary, ptr<float>(pos), ptr<float>(heading),
@@ -143,7 +143,7 @@ void step_uw_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_he
     const at::OptionalDeviceGuard guard(pos.device());
     step_uw_checks(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
                    seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0, nullptr};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_uw_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, rigid_boundary,
                                ptr<float>(pos), ptr<const float>(heading), ptr<float>(prev_heading),
@@ -196,7 +196,7 @@ void step_uwd_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_h
     const at::OptionalDeviceGuard guard(pos.device());
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0, nullptr};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_uw_discrete_ext(
                  stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
                  (float)collision_distance, (float)dt, (float)v_max, rigid_boundary, ptr<float>(pos),
@@ -245,7 +245,7 @@ void step_flock_hip(const Tensor& pos, const Tensor& vel, const Tensor& action, 
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_flock_checks(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0, nullptr};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_flock_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                   (float)collision_distance, (float)dt, rigid_boundary, ptr<float>(pos),
                                   ptr<float>(vel), ptr<const float>(action), ptr<const float>(mem_in),
@@ -333,7 +333,7 @@ void step_v2_store_hip(const Tensor& pos, const Tensor& heading, const Tensor& a
     TORCH_CHECK(ring_meta.size() == 6 && ring_meta[4] == 0 && ring_meta[5] == 0,
                 "step_v2_store: action ids / env done flags are the uw_discrete ring's");
     const FlockRing r = ring_of(pos, ring, actor_state, actor_new_state, prev_obs, ring_meta, k);
-    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0, nullptr};
+    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_v2_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, (float)v_min,
                                (float)v_max, periodic, rigid_boundary, ptr<float>(pos), ptr<float>(heading),
@@ -365,7 +365,7 @@ void step_uwd_store_hip(const Tensor& pos, const Tensor& heading, const Tensor& 
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
     const FlockRing r = ring_of(pos, ring, c10::nullopt, c10::nullopt, prev_obs, ring_meta, k);
-    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0, nullptr};
+    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0};
     rc_check(flock_step_uw_discrete_ext(
                  stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
                  (float)collision_distance, (float)dt, (float)v_max, rigid_boundary, ptr<float>(pos),

@@ -168,23 +168,6 @@ struct ScPipeline : torch::CustomClassHolder {
         check(flock_sc_pipeline_flush(pipe, reinterpret_cast<void*>(learner_stream)), "flock_sc_pipeline_flush");
     }
 
-    // deferred learns (ScTrainLoop): learn() whose snapshot the caller's next env step carries; returns whether it was
-    // deferred (the gate hand-off), then commit once that env step is enqueued (carried) or without one
-    bool defer(int64_t rows, int64_t seed, int64_t counter, int64_t agent, int64_t env_stream, int64_t learner_stream,
-               FlockStepSnapshot* snap) {
-        TORCH_CHECK(agent >= 0 && agent < n_agents, "ScPipeline.learn: agent out of range");
-        const at::OptionalDeviceGuard g(device);
-        const int rc = flock_sc_pipeline_defer(pipe, reinterpret_cast<void*>(env_stream),
-                                               reinterpret_cast<void*>(learner_stream), rows, (uint64_t)seed,
-                                               (uint64_t)counter, agent, snap);
-        check(rc < 0 ? rc : 0, "flock_sc_pipeline_defer");
-        return rc == 1;
-    }
-    void commit(bool carried) {
-        const at::OptionalDeviceGuard g(device);
-        check(flock_sc_pipeline_commit(pipe, carried ? 1 : 0), "flock_sc_pipeline_commit");
-    }
-
     // raises if a round gave up waiting for its snapshot (device-side gate timeout; its results are invalid).
     // Synchronous: call once the learner stream has been synchronised
     void verify() {
@@ -318,10 +301,6 @@ struct ScTrainLoop : torch::CustomClassHolder {
         void* es = reinterpret_cast<void*>(env_stream);
         const int64_t n = E * N;
         size_t ev = 0;
-        // the previous learn()'s minibatch snapshot rides in this step's first launch (the gate hand-off): its rounds
-        // are enqueued right after the step, so each round follows the snapshot it waits for in host order too
-        FlockStepSnapshot carry{};
-        bool carrying = false;
         for (int64_t s = 0; s < K; ++s) {
             const int64_t step = first + s;
             const int64_t skip = n > capacity ? n - capacity : 0;
@@ -338,7 +317,7 @@ struct ScTrainLoop : torch::CustomClassHolder {
             r.skip = skip;
             r.group = 1;
             const int nxt = (int)(parity ^ 1);
-            FlockStepExt ext{&r, ptr_or_null<uint16_t>(env[10]), (int)launches, 0, carrying ? &carry : nullptr};
+            FlockStepExt ext{&r, ptr_or_null<uint16_t>(env[10]), (int)launches, 0};
             const bool timed = s % ev_every == 0 && ev + 1 < events.size();
             if (timed) TORCH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[ev]),
                                                   static_cast<hipStream_t>(es)) == hipSuccess, "hipEventRecord");
@@ -357,16 +336,12 @@ struct ScTrainLoop : torch::CustomClassHolder {
             }
             parity = nxt;
             counter += n;
-            if (carrying) pipe->commit(true);
-            carrying = false;
             if (counter >= pipe->batch) {  // SharedCriticLearner.pipeline_learn: learn() once the ring holds a batch
                 ++learn_calls;
                 const int64_t rows = counter < capacity ? counter : capacity;
-                carrying = pipe->defer(rows, seed, learn_calls, step % pipe->n_agents, env_stream, learner_stream,
-                                       &carry);
+                pipe->learn(rows, seed, learn_calls, step % pipe->n_agents, env_stream, learner_stream);
             }
         }
-        if (carrying) pipe->commit(false);  // the last learn's snapshot on its own, right behind the last env step
     }
 
     void flush(int64_t learner_stream) { pipe->flush(learner_stream); }

@@ -105,23 +105,18 @@ def test_shared_critic_round_and_pipeline_argument_checks(lib):
     assert lib.flock_sc_pipeline_flush(None, None) == -3
     assert lib.flock_sc_pipeline_learn(None, None, None, 1, 0, 0, 0) == -3
     assert lib.flock_sc_pipeline_set_dp(None, None, 0, 0, 0, None, None, None) == -3
-    assert lib.flock_sc_pipeline_defer(None, None, None, 1, 0, 0, 0, None) == -3
-    assert lib.flock_sc_pipeline_commit(None, 1) == -3
-    assert lib.flock_sc_pipeline_set_gate(None, 1) == -3
 
 
 def test_step_ext_layout_and_launches_option():
-    """FlockStepExt mirrors the header ({ring*, seeds*, int launches, int normalize_distance, snapshot*}: 32 bytes on
-    x86-64); step_launches < 1 is rejected by FlockConfig and by the ext builder before any launch."""
+    """FlockStepExt mirrors the header ({ring*, seeds*, int launches, int normalize_distance}: 24 bytes on x86-64);
+    step_launches < 1 is rejected by FlockConfig and by the ext builder before any launch."""
     from marl_range_flocking_amd import FlockConfig, _native, ops
 
-    assert ctypes.sizeof(_native.FlockStepExt) == 32
-    assert [f[0] for f in _native.FlockStepExt._fields_] == ["ring", "seeds", "launches", "normalize_distance",
-                                                             "snapshot"]
+    assert ctypes.sizeof(_native.FlockStepExt) == 24
+    assert [f[0] for f in _native.FlockStepExt._fields_] == ["ring", "seeds", "launches", "normalize_distance"]
     header = open(os.path.join(INCLUDE, "flock_amd.h")).read()
     body = header[header.index("typedef struct FlockStepExt"):header.index("} FlockStepExt;")]
     assert "int launches;" in body and body.index("int launches;") < body.index("int normalize_distance;")
-    assert body.index("int normalize_distance;") < body.index("FlockStepSnapshot* snapshot;")
     with pytest.raises(ValueError):
         FlockConfig(step_launches=0).resolved()
     with pytest.raises(ValueError):
