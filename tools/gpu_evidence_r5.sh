@@ -6,7 +6,9 @@
 # PHASES="tests bench pmc" selects parts. Every GPU step has its own time limit; the script stops at a failure.
 set -u
 OUT=gpurun_out/ev5; mkdir -p $OUT; export TMPDIR=/tmp
-PHASES=${PHASES:-"tests bench pmc"}
+PHASES=${PHASES:-"tests pmc bench driver ab"}
+PASS_A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE"
+PASS_B="SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 step() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > $OUT/$name 2>&1; local rc=$?; echo "rc($name)=$rc";
   if [ $rc -ne 0 ]; then tail -20 $OUT/$name; exit $rc; fi; }
 tag_of() { case $1 in 3) echo v2_ring_N256_E4096;; 2) echo uw_N64_E1024;; 4) echo uw_discrete_ring_N512_E8192;;
@@ -27,6 +29,9 @@ if [[ $PHASES == *pmc* ]]; then
     python tools/pmc_traffic.py $OUT/pmc_${t}_FETCH_SIZE $OUT/pmc_${t}_WRITE_SIZE --kernel step_kernel --algorithmic-bytes $(alg_of $c) --out $OUT/pmc_$t.json
     step pmc_sq_$t.log 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM -d $OUT/pmc_sq_$t -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3 --step-launches 1
     python tools/pmc_sq_json.py $OUT/pmc_sq_$t --kernel step_kernel --out $OUT/pmc_sq_$t.json
+    step pmc_valuA_$t.log 240 rocprofv3 --pmc $PASS_A -d $OUT/pmc_valuA_$t -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3 --step-launches 1
+    step pmc_valuB_$t.log 240 rocprofv3 --pmc $PASS_B -d $OUT/pmc_valuB_$t -o run --output-format csv -- python3 bench.py --config $c --no-cpu-baseline --steps 30 --warmup 3 --step-launches 1
+    python tools/pmc_sq_json.py $OUT/pmc_valuA_$t $OUT/pmc_valuB_$t --kernel step_kernel --out $OUT/pmc_valu_$t.json
   done
   cp $OUT/pmc_*.json profiles/  # the bench lines below read them (copy them into the repo afterwards)
 fi
@@ -43,5 +48,11 @@ if [[ $PHASES == *driver* ]]; then
   step driver_1.json 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
   step driver_2.json 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
   step prof_driver.log 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_driver -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+fi
+# same-box A/B of the round-3 head, the round-4 head and this tree (verdict r4 item 1), both commands
+if [[ $PHASES == *ab* ]]; then
+  ABT_OUT=ev5/ab TREES="89c4346 c2589f5 cur" tools/gpu_ab_trees.sh 3 \
+    "--gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --policy-steps 0" \
+    "--steps 200 --warmup 20 --no-cpu-baseline --policy-steps 0" || exit 1
 fi
 echo ALLDONE2
