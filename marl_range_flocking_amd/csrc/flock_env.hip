@@ -275,6 +275,23 @@ template <typename T>
 __device__ __forceinline__ T ld_once(const T* p) {
     return *p;
 }
+#ifndef FLOCK_EXP_NTOUT
+#define FLOCK_EXP_NTOUT 0
+#endif
+#ifndef FLOCK_EXP_NTIN
+#define FLOCK_EXP_NTIN 0
+#endif
+#ifndef FLOCK_EXP_PULL_AT
+#define FLOCK_EXP_PULL_AT 0
+#endif
+template <bool NT, typename T>
+__device__ __forceinline__ void st_o(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_i(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p); else return *p;
+}
 
 template <bool PERIODIC>
 __device__ __forceinline__ f32x2 pair_d2x2(float xi, float yi, float x0, float y0, float x1, float y1, float box) {
@@ -806,6 +823,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     static_assert(SPL == 1 || (NC > 0 && !CELL && (NC % (2 * SPL)) == 0), "split scans: specialised N, no cells");
     Params p = pin;
     if (VAR >= 0) p.variant = VAR;
+    constexpr bool kNtOut = PFM == 3 && FLOCK_EXP_NTOUT;
+    constexpr bool kNtIn = PFM == 3 && FLOCK_EXP_NTIN;
+    constexpr int kPullAt = PFM == 3 ? FLOCK_EXP_PULL_AT : 0;
     if (NC > 0) {  // make_cfg / dispatch values for N = NC
         p.N = NC;
         p.k = L - 2;
@@ -876,7 +896,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     // kinematics waits on are not queued behind them
     auto load_late = [&]() {
         if (seed_packed) {
-            const u32x2 sv = ldnt(reinterpret_cast<const u32x2*>(p.seeds + a * p.k));
+            const u32x2 sv = ld_i<kNtIn>(reinterpret_cast<const u32x2*>(p.seeds + a * p.k));
             seed_raw = make_uint2(sv.x, sv.y);
         } else if (has_hint && p.seeds) {
             const uint16_t* hp = p.seeds + a * p.k;
@@ -892,7 +912,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (active && p.r_state && r_unit >= p.r_skip) {
             const float* po = p.r_prev + a * p.k;
             if (L - 2 == 4 && p.k == 4) {  // one 16-B load (rows of 4 floats are 16-B aligned)
-                const f32x4 v = ld_once(reinterpret_cast<const f32x4*>(po));
+                const f32x4 v = ld_i<kNtIn>(reinterpret_cast<const f32x4*>(po));
                 prev_obs[0] = v.x;
                 prev_obs[1 % (L - 2)] = v.y;
                 prev_obs[2 % (L - 2)] = v.z;
@@ -943,14 +963,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
     }
     if (active) {
-        const f32x2 pp = ldnt(reinterpret_cast<const f32x2*>(p.pos) + a);
+        const f32x2 pp = ld_i<kNtIn>(reinterpret_cast<const f32x2*>(p.pos) + a);
         x = pp.x;
         y = pp.y;
         if (variant == FLOCK_VARIANT_V2) {  // gym_flock_v2.py:317-350 (heading=True)
-            const f32x2 ac = ld_once(reinterpret_cast<const f32x2*>(p.action) + a);
+            const f32x2 ac = ld_i<kNtIn>(reinterpret_cast<const f32x2*>(p.action) + a);
             act_in = make_float2(ac.x, ac.y);
             const float ang = clamp_t(ac.y, -kHalfPi, kHalfPi);             // :327
-            h = __fadd_rn(ldnt(p.heading + a), __fmul_rn(ang, p.dt));        // :329
+            h = __fadd_rn(ld_i<kNtIn>(p.heading + a), __fmul_rn(ang, p.dt));        // :329
 #ifdef FLOCK_PHASE_PROF  // diagnostics: the kinematics inputs' arrival (phase 9) apart from the rest of phase 0
             asm volatile("s_waitcnt vmcnt(0)" ::"v"(h), "v"(x) : "memory");
             PHASE(9);
@@ -964,8 +984,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             vy = __fmul_rn(nan_to_num(vy), p.dt);
             x = __fadd_rn(x, vx);                                            // :350
             y = __fadd_rn(y, vy);
-            stnt(p.heading + a, h);
-            stnt(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
+            st_o<kNtOut>(p.heading + a, h);
+            st_o<kNtOut>(reinterpret_cast<f32x2*>(p.vel) + a, f32x2{vx, vy});
         } else if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:269-302 (heading=False)
             const float2 ac = reinterpret_cast<const float2*>(p.action)[a];
             const float n = sqrt_rn(__fadd_rn(__fmul_rn(ac.x, ac.x), __fmul_rn(ac.y, ac.y)));  // :294
@@ -1029,7 +1049,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (variant != kSense) {
             x = boundary(x, p.box, p.rigid);  // check_boundary :271-304
             y = boundary(y, p.box, p.rigid);
-            stnt(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
+            st_o<kNtOut>(reinterpret_cast<f32x2*>(p.pos) + a, f32x2{x, y});
         }
         lpos[g * p.S + i] = make_float2(x, y);
     }
@@ -1048,7 +1068,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     // (the late inputs there: 38.7-39.7 µs, not pulled) (profiles/r04/pf/)
     int pf_sink = 0;
     const bool pf_on = PFM != 0 && p.pf_ahead > 0;  // PFM: 1 the kinematics inputs, 3 also the late inputs
-    if (pf_on) {
+    auto do_pull = [&]() {
         const int eb = p.env0 + (int)(blockIdx.x + p.pf_ahead) * p.G;
         const int ne = min(p.G, p.E - eb);
         if (ne > 0) {
@@ -1073,7 +1093,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             }
             if (base) pf_sink = *reinterpret_cast<const int*>(base + (size_t)q * 128);
         }
-    }
+    };
+    if (pf_on && kPullAt == 0) do_pull();
 
     PHASE(0);
     // ---- phase 2: per-env sums in a fixed tree order (same order as oracle tree_sum) -------------------------
@@ -1131,6 +1152,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
 
     PHASE(1);
+    if (pf_on && kPullAt == 3) do_pull();
     // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
     int cx = 0, cy = 0;
 #ifdef FLOCK_DIAG_BINREP  // diagnostics: the binning phase run FLOCK_DIAG_BINREP times (its marginal cost; same results)
@@ -1208,6 +1230,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
 
     PHASE(2);
+    if (pf_on && kPullAt == 1) do_pull();
     // ---- phase 3/4: kNN -------------------------------------------------------------------------------
     float bd[L - 1];
     int bj[L - 1];
@@ -1289,6 +1312,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
         PHASE(4);
     }
+    if (pf_on && kPullAt == 4) do_pull();
 #ifdef FLOCK_PHASE_PROF
     if (__ballot(active && !ok) != 0) PHASE_COUNT(17, 1);
 #endif
@@ -1344,6 +1368,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #endif
     }
     PHASE(5);
+    if (pf_on && kPullAt == 2) do_pull();
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
     int coll = 0;
@@ -1361,11 +1386,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             }
         }
         if (L - 2 == 4 && p.k == 4)  // one 16-B store
-            stnt(reinterpret_cast<f32x4*>(p.dnn + a * p.k), f32x4{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]});
+            st_o<kNtOut>(reinterpret_cast<f32x4*>(p.dnn + a * p.k), f32x4{dv[0], dv[1 % (L - 1)], dv[2 % (L - 1)], dv[3 % (L - 1)]});
         if (CELL && p.seeds) {  // this step's neighbours: the next step's search seeds
             uint16_t* sp = p.seeds + a * p.k;
             if (L - 2 == 4 && p.k == 4)
-                stnt(reinterpret_cast<u32x2*>(sp), u32x2{(uint32_t)bj[1] | ((uint32_t)bj[2 % (L - 1)] << 16),
+                st_o<kNtOut>(reinterpret_cast<u32x2*>(sp), u32x2{(uint32_t)bj[1] | ((uint32_t)bj[2 % (L - 1)] << 16),
                                                          (uint32_t)bj[3 % (L - 1)] | ((uint32_t)bj[4 % (L - 1)] << 16)});
             else
 #pragma unroll
@@ -1401,7 +1426,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             }
         }
         if (variant != kSense) {
-            stnt(p.done + a, (uint8_t)coll);
+            st_o<kNtOut>(p.done + a, (uint8_t)coll);
             float r;
             if (variant == FLOCK_VARIANT_UW) {  // gym_flock_uw.py:206-221
                 const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
@@ -1419,7 +1444,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             } else {
                 r = coll ? -5.0f : 0.01f;  // gym_flock_v2.py:217-220, gym_flock.py:142-145
             }
-            stnt(p.reward + a, r);
+            st_o<kNtOut>(p.reward + a, r);
             if (p.r_state && r_unit >= p.r_skip) {  // fused replay insert: row (start + unit - skip) mod cap
                 int64_t row = p.r_start + r_unit - p.r_skip;
                 if (row >= p.r_cap) row -= p.r_cap;
