@@ -275,15 +275,10 @@ template <typename T>
 __device__ __forceinline__ T ld_once(const T* p) {
     return *p;
 }
-#ifndef FLOCK_EXP_NTOUT
-#define FLOCK_EXP_NTOUT 0
-#endif
-#ifndef FLOCK_EXP_NTIN
-#define FLOCK_EXP_NTIN 0
-#endif
-#ifndef FLOCK_EXP_PULL_AT
-#define FLOCK_EXP_PULL_AT 0
-#endif
+// The same streams with a compile-time cache policy: non-temporal in the instantiation whose launches have more env
+// blocks than are resident and whose state does not fit the MALL (config 5, PFM 3: 1.5 GB of state per step), so
+// that the lines the L2 pull-ahead brings in for the next block generation are not evicted by this generation's
+// streams (step_kernel's kNtIn / kNtOut)
 template <bool NT, typename T>
 __device__ __forceinline__ void st_o(T* p, T v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p); else *p = v;
@@ -823,9 +818,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     static_assert(SPL == 1 || (NC > 0 && !CELL && (NC % (2 * SPL)) == 0), "split scans: specialised N, no cells");
     Params p = pin;
     if (VAR >= 0) p.variant = VAR;
-    constexpr bool kNtOut = PFM == 3 && FLOCK_EXP_NTOUT;
-    constexpr bool kNtIn = PFM == 3 && FLOCK_EXP_NTIN;
-    constexpr int kPullAt = PFM == 3 ? FLOCK_EXP_PULL_AT : 0;
+    // config 5 (PFM 3): non-temporal state streams and the pull-ahead issued after the binning (kPullAt 1), so that
+    // the pulled lines spend less time in an L2 this generation's streams are turning over. Same-box A/B
+    // (profiles/r05/c5pull/): env launch 0.639 -> 0.590 ms, PMC reads 88.7 -> 58.6 B per agent-step; the pull after
+    // the kinematics (0, kept for PFM 1), before the binning, after the scans or before the outputs, and either policy
+    // alone, measured between the two
+    constexpr bool kNtOut = PFM == 3;
+    constexpr bool kNtIn = PFM == 3;
+    constexpr int kPullAt = PFM == 3 ? 1 : 0;
     if (NC > 0) {  // make_cfg / dispatch values for N = NC
         p.N = NC;
         p.k = L - 2;
@@ -1152,7 +1152,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
 
     PHASE(1);
-    if (pf_on && kPullAt == 3) do_pull();
     // ---- phase 3c: cell binning (counting sort into the extended cell-sorted array) --------------------------
     int cx = 0, cy = 0;
 #ifdef FLOCK_DIAG_BINREP  // diagnostics: the binning phase run FLOCK_DIAG_BINREP times (its marginal cost; same results)
@@ -1312,7 +1311,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
         PHASE(4);
     }
-    if (pf_on && kPullAt == 4) do_pull();
 #ifdef FLOCK_PHASE_PROF
     if (__ballot(active && !ok) != 0) PHASE_COUNT(17, 1);
 #endif
@@ -1368,7 +1366,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #endif
     }
     PHASE(5);
-    if (pf_on && kPullAt == 2) do_pull();
 
     // ---- phase 5: outputs -----------------------------------------------------------------------------
     int coll = 0;

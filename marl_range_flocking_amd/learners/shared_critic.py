@@ -734,8 +734,10 @@ class SharedCriticBench:
                 f"agent = step mod "
                 f"{self.learner.n_agents}; all {self.env.E * self.env.N} transitions inserted into a 1e6-row "
                 f"device replay ring per step by the env kernel itself"
-                + ("; one [critic | actor] gradient all-reduce over RCCL per learn)" if self.learner.distributed
-                   else ")"))
+                + (")" if not self.learner.distributed else
+                   "; critic gradient all-reduce on the learner chain, the actor's on a second group and stream)"
+                   if getattr(self.learner, "dp_split", False) else
+                   "; one [critic | actor] gradient all-reduce over RCCL per learn)"))
 
     # bench.py hook interface: before(s) -> ring for the fused env step; after(s, a) -> learn(); prime()
     def before(self, s):

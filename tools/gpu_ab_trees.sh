@@ -25,9 +25,12 @@ rows = collections.defaultdict(list)
 import os
 for f in sorted(glob.glob("gpurun_out/%s/s*_*.json" % os.environ.get("ABT_OUT", "abt"))):
     name = f.split("/")[-1][:-5]
-    s, t, r = name.split("_")
+    s, rest = name.split("_", 1)
+    t, r = rest.rsplit("_", 1)
     d = json.loads(open(f).read().strip().splitlines()[-1])
-    rows[(s, t)].append(d["ms_per_step"])
+    rows[(s, t)].append((d["ms_per_step"], (d.get("roofline") or {}).get("kernel_ms")))
 for (s, t), v in sorted(rows.items()):
-    print(f"{s} ({sys.argv[int(s[1:])]}) {t:8s} ms/step " + " ".join("%.4f" % x for x in v) + "  min %.4f" % min(v))
+    ks = [k for _, k in v if k]
+    print(f"{s} ({sys.argv[int(s[1:])]}) {t:8s} ms/step " + " ".join("%.4f" % x for x, _ in v) +
+          "  min %.4f" % min(x for x, _ in v) + ("  env launch ms " + " ".join("%.4f" % k for k in ks) if ks else ""))
 PY

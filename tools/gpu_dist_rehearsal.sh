@@ -9,6 +9,10 @@ run() { local name=$1; shift; timeout -k 10 400 python -m torch.distributed.run 
   --master-addr 127.0.0.1 --master-port $((29500 + RANDOM % 1000)) bench.py --gpus 2 --no-cpu-baseline "$@" \
   > $OUT/$name.json 2> $OUT/$name.err; local rc=$?; echo "rc($name)=$rc"; tail -c 700 $OUT/$name.json; echo;
   [ $rc -eq 0 ] || { tail -20 $OUT/$name.err; exit $rc; }; }
-run config3 --config 3 --steps 40 --warmup 5
-run config5 --config 5 --steps 250 --warmup 5
-run config4 --config 4 --steps 150 --warmup 5
+for c in ${CONFIGS:-3 5 4}; do
+  case $c in
+    3) run config3 --config 3 --steps 40 --warmup 5 ;;
+    5) run config5 --config 5 --steps 250 --warmup 5 ;;
+    4) run config4 --config 4 --steps 150 --warmup 5 ;;
+  esac
+done

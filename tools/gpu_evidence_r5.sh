@@ -5,7 +5,7 @@
 #   run the step as one launch (--step-launches 1), so a dispatch's counters are one whole step's.
 # PHASES="tests bench pmc" selects parts. Every GPU step has its own time limit; the script stops at a failure.
 set -u
-OUT=gpurun_out/ev5; mkdir -p $OUT; export TMPDIR=/tmp
+OUT=${EV_OUT:-gpurun_out/ev5}; mkdir -p $OUT; export TMPDIR=/tmp
 PHASES=${PHASES:-"tests pmc bench driver ab"}
 PASS_A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE"
 PASS_B="SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
