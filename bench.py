@@ -109,7 +109,9 @@ def parse():
                          "the warmup steps (clock / power-state probe)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
-                         "results; the env kernel time is unchanged by it); 0: the learner runs after each step")
+                         "results; the env kernel time is unchanged by it); configs 4 / 5: train() on its own stream "
+                         "beside the env steps that follow it (its sampled rows copied out first; same results); "
+                         "0: the learner runs after each step")
     args = ap.parse_args()
     c = CONFIGS[args.config]
     args.global_split = args.envs is None and "global_envs" in c
@@ -324,18 +326,25 @@ class VDNBench:
 
     every = 150
 
-    def __init__(self, env, dev, seed=0):
+    def __init__(self, env, dev, seed=0, overlap=True):
         from marl_range_flocking_amd.learners.vdn import VDNLearner
 
         self.env = env
         group = torch.distributed.group.WORLD if torch.distributed.is_initialized() else None
         self.learner = VDNLearner(env.N, env.k, 10, device=dev, seed=seed, dist_group=group)
+        # train() beside the env steps that follow it (random actions: they do not read the QNet); the sampled rows
+        # are copied out of the ring first (learners/core.py OverlappedTrain); data-parallel: in line
+        self.overlap = overlap and not self.learner.distributed
         self.prev = None
 
+    def _train(self):
+        return self.learner.train_overlapped() if self.overlap else self.learner.train()
+
     def describe(self):
-        return (f"VDN train() every {self.every} vectorized steps (update_iter 10, B 32, chunk 10); all "
-                f"{self.env.E} team transitions per step inserted into a 50k-row device replay ring by the env "
-                f"kernel itself" + ("; gradient all-reduce over RCCL" if self.learner.distributed else ""))
+        return (f"VDN train() every {self.every} vectorized steps (update_iter 10, B 32, chunk 10"
+                + ("; on its own stream beside the following env steps, sampled rows copied out first" if self.overlap
+                   else "") + f"); all {self.env.E} team transitions per step inserted into a 50k-row device replay "
+                f"ring by the env kernel itself" + ("; gradient all-reduce over RCCL" if self.learner.distributed else ""))
 
     def before(self, s):
         # the env kernel writes every env's team transition itself (memory.put, train_flock.py:102: previous obs,
@@ -344,10 +353,14 @@ class VDNBench:
 
     def after(self, s, a):
         if (s + 1) % self.every == 0 and self.learner.size() > self.learner.chunk:
-            self.learner.train()
+            self._train()
 
     def prime(self):
-        self.learner.train()
+        self._train()
+        self.finish()
+
+    def finish(self):  # an overlapped train() still running joins the env stream (inside the timed region)
+        self.learner.sync()
 
 
 class MADDPGBench:
@@ -358,7 +371,7 @@ class MADDPGBench:
 
     every = 250
 
-    def __init__(self, env, dev, seed=0):
+    def __init__(self, env, dev, seed=0, overlap=True):
         from marl_range_flocking_amd.learners.maddpg import MADDPGLearner
 
         self.env = env
@@ -370,13 +383,20 @@ class MADDPGBench:
         self.learner = MADDPGLearner(env.N, env.k, recurrent=True, device=dev, seed=seed, dist_group=group,
                                      agent_shard=group is not None and env.N % torch.distributed.get_world_size() == 0,
                                      shared_obs=True)
+        # train() beside the env steps that follow it (random actions: they do not read the networks); the sampled
+        # chunks are copied out of the ring first (learners/core.py OverlappedTrain); multi-rank: in line
+        self.overlap = overlap and not (self.learner.distributed or self.learner.shard)
         self.prev = None
+
+    def _train(self):
+        return self.learner.train_overlapped() if self.overlap else self.learner.train()
 
     def describe(self):
         L = self.learner
         return (f"RNN-MADDPG train() every {self.every} vectorized steps (B 128, chunk 10, {self.env.N} critics "
-                f"400/300); all {self.env.E} env records per step inserted into a 45k-row device replay ring by the "
-                f"env kernel itself"
+                f"400/300" + ("; on its own stream beside the following env steps, sampled chunks copied out first"
+                             if self.overlap else "") + f"); all {self.env.E} env records per step inserted into a "
+                f"45k-row device replay ring by the env kernel itself"
                 + ("; agent-sharded critics, minibatch + action all-gathers over RCCL" if L.shard else
                    "; critic gradient all-reduce over RCCL" if L.distributed else ""))
 
@@ -387,11 +407,15 @@ class MADDPGBench:
     def after(self, s, a):
         L = self.learner
         if (s + 1) % self.every == 0 and L.check_buffer_size():
-            L.train()
+            self._train()
 
     def prime(self):
         if self.learner.check_buffer_size():
-            self.learner.train()
+            self._train()
+        self.finish()
+
+    def finish(self):  # an overlapped train() still running joins the env stream (inside the timed region)
+        self.learner.sync()
 
 
 def policy_loop(hook, env, first, steps):
@@ -474,9 +498,9 @@ def main():
 
         hook = SharedCriticBench(env, device=dev, seed=1234 + rank, overlap=bool(args.overlap))
     elif args.learner == "vdn":
-        hook = VDNBench(env, dev, seed=1234 + rank)
+        hook = VDNBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap))
     elif args.learner == "maddpg_rnn":
-        hook = MADDPGBench(env, dev, seed=1234 + rank)
+        hook = MADDPGBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap))
 
     def one_step(s, ev=None):
         a = pool[s % len(pool)]

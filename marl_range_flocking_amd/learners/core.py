@@ -650,6 +650,50 @@ class ReplayRing:
         return out
 
 
+class OverlappedTrain:
+    """A learner's train() beside the env steps that follow it (the random-action exploration regime, where the next
+    steps do not read the networks): the rows the update samples are copied out of the replay ring on the caller's
+    (env) stream — one row gather per field, ordered before the env kernels that overwrite ring rows — and the update
+    itself, the learner's own graph-captured code re-captured over this snapshot, runs on a stream of its own. Results
+    are bitwise those of train() on the same draws (the same kernels on the same rows). ``sync()`` makes the caller's
+    stream wait for the update (before anything reads the networks; bench.py's finish())."""
+
+    def __init__(self, ring, n_rows):
+        self.ring = ring
+        self.snap = ReplayRing(n_rows, ring.fields, ring.device, aliases=ring.aliases)
+        self.snap.counter = n_rows
+        self.stream = torch.cuda.Stream(ring.device)
+        self.done = torch.cuda.Event()
+        self.pending = False
+        self.graph = None
+
+    def snapshot(self, idx):
+        """Rows idx (int64, n_rows in all, any shape) of every field into snapshot rows 0..n_rows-1 in idx's order, on
+        the current stream, after the previous update has finished reading the snapshot."""
+        cur = torch.cuda.current_stream(self.ring.device)
+        if self.pending:
+            cur.wait_event(self.done)
+        flat = idx.reshape(-1)
+        assert flat.numel() == self.snap.capacity
+        for name in self.ring.fields:
+            if name not in self.ring.aliases:
+                self.ring.gather(name, flat, out=self.snap.bufs[name])
+
+    def launch(self, fn):
+        """Run fn (enqueues the update) on the update stream, after the current stream's work so far."""
+        cur = torch.cuda.current_stream(self.ring.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            fn()
+            self.done.record(self.stream)
+        self.pending = True
+
+    def sync(self):
+        if self.pending:
+            torch.cuda.current_stream(self.ring.device).wait_event(self.done)
+            self.pending = False
+
+
 def capture_graph(fn, device, state, warmup=2):
     """Capture ``fn`` (a learner update on static tensors) into a HIP graph. ``state``: tensors the warm-up runs
     mutate (parameters, moments, step counters) — snapshotted and restored so capture has no side effect."""

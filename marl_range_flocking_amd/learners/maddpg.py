@@ -33,7 +33,8 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import FlatParams, ReplayRing, _ops, blinear, capture_graph, gru_cell, gru_seq, linear_t, shared_linear
+from .core import (FlatParams, OverlappedTrain, ReplayRing, _ops, blinear, capture_graph, gru_cell, gru_seq, linear_t,
+                   shared_linear)
 
 HR = 32  # hidden_rnn (net.py:15,100)
 
@@ -527,6 +528,41 @@ class MADDPGLearner:
             dist.allreduce_mean_(self.critics.grad, self.group)
             self._step()
         return self.losses
+
+    def train_overlapped(self, starts=None):
+        """train() beside the env steps that follow (core.OverlappedTrain): the B x C sampled rows are copied out of
+        the ring on the current stream, the update runs on a stream of its own; bitwise train() on the same draws.
+        Single-process graph path only (the data-parallel and agent-sharded updates call collectives: train())."""
+        if self.distributed or self.shard or not self.use_graph:
+            return self.train(starts)
+        if not self.check_buffer_size():
+            return None
+        ov = self.__dict__.get("_ov")
+        if ov is None:
+            ov = self._ov = OverlappedTrain(self.replay, self.B * self.C)
+            ov.idx = torch.arange(self.B * self.C, device=self.device).view(self.B, self.C)
+        rng = min(self.replay.counter, self.replay.capacity)
+        hi = rng - self.C if self.recurrent else rng
+        if starts is None:  # the same draws as train()
+            starts = torch.randperm(hi, device=self.device, generator=self.gen)[:self.B]
+        starts = torch.as_tensor(starts, device=self.device)
+        ov.snapshot(starts[:, None] + torch.arange(self.C, device=self.device)[None])
+        if ov.graph is None:  # _update over the snapshot rows: the same code, its own graph
+            saved = self.replay, self.static_idx
+            self.replay, self.static_idx = ov.snap, ov.idx
+            try:
+                ov.graph = capture_graph(self._update, self.device, self.critics.state_tensors()
+                                         + self.actors.state_tensors() + [self.losses])
+            finally:
+                self.replay, self.static_idx = saved
+        ov.launch(ov.graph.replay)
+        return self.losses
+
+    def sync(self):
+        """The current stream waits for an overlapped train() (before anything reads the networks)."""
+        ov = self.__dict__.get("_ov")
+        if ov is not None:
+            ov.sync()
 
     # ---------------------------------------------------------------- state dicts (reference names)
     def load_reference_state(self, sds):

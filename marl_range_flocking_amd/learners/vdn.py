@@ -19,7 +19,8 @@ import torch
 import torch.nn.functional as F
 
 from .. import dist
-from .core import gru_seq_q, FlatParams, GradNorm, ReplayRing, blinear, capture_graph, gru_cell, gru_seq, vdn_feat
+from .core import (gru_seq_q, FlatParams, GradNorm, OverlappedTrain, ReplayRing, blinear, capture_graph, gru_cell,
+                   gru_seq, vdn_feat)
 
 HX = 32
 
@@ -267,6 +268,46 @@ class VDNLearner:
     def sample_starts(self):
         n = len(self.replay)
         return torch.randint(0, n - self.chunk, (self.B,), device=self.device, generator=self.gen)
+
+    def train_overlapped(self, starts=None):
+        """train() beside the env steps that follow (core.OverlappedTrain): the update_iter x B x C sampled rows of
+        all iterations are copied out of the ring on the current stream, the iterations run on a stream of their own;
+        bitwise train() on the same draws. Single-process graph path only (data-parallel: train())."""
+        if self.distributed or not self.use_graph:
+            return self.train(starts)
+        U, B, C = self.update_iter, self.B, self.chunk
+        ov = self.__dict__.get("_ov")
+        if ov is None:
+            ov = self._ov = OverlappedTrain(self.replay, U * B * C)
+            ov.idx_all = torch.arange(U * B * C, device=self.device).view(U, B, C)
+            ov.static_idx = torch.zeros((B, C), dtype=torch.int64, device=self.device)
+        n = len(self.replay)
+        base = self.replay.counter - n
+        ar = torch.arange(C, device=self.device)
+        st = torch.stack([self.sample_starts() if starts is None else torch.as_tensor(starts[it], device=self.device)
+                          for it in range(U)])  # the same draws, in the same order, as train()
+        ov.snapshot((base + st[:, :, None] + ar[None, None, :]) % self.replay.capacity)
+        if ov.graph is None:  # _iteration over the snapshot rows: the same code, its own graph
+            saved = self.replay, self.static_idx
+            self.replay, self.static_idx = ov.snap, ov.static_idx
+            try:
+                ov.graph = capture_graph(self._iteration, self.device,
+                                         self.q.P.state_tensors() + [self.loss, self.norm.out])
+            finally:
+                self.replay, self.static_idx = saved
+
+        def run():
+            for it in range(U):
+                ov.static_idx.copy_(ov.idx_all[it])
+                ov.graph.replay()
+        ov.launch(run)
+        return self.loss
+
+    def sync(self):
+        """The current stream waits for an overlapped train() (before anything reads the networks)."""
+        ov = self.__dict__.get("_ov")
+        if ov is not None:
+            ov.sync()
 
     def train(self, starts=None):
         """train(q, q_target, memory, optimizer, gamma, batch_size, update_iter, chunk_size) for every agent at
