@@ -1778,6 +1778,8 @@ void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
     if constexpr (L == 6) {
         if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6, 1, 1>(c, p, s)) return;  // config 3 (+ L2 pull)
         if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12, 1, 3>(c, p, s)) return;  // config 5 (+ L2 pull, late)
+        // config 4: no pull (the config-5 pull + non-temporal streams measured 0.1954-0.1959 against 0.1929-0.1937 ms
+        // per step, the kinematics pull 0.1952; profiles/r05/c4pf/)
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
         if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
     }

@@ -85,7 +85,7 @@ class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
                  ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
-                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=True):
+                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=True, dp=None):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -117,7 +117,10 @@ class SharedCriticLearner:
         self.critic_leaves = self.critic.new_leaves(squeeze=True)
         self.scratch_leaves = self.scratch.new_leaves(squeeze=True)
         self.group = dist_group
-        self.distributed = dist.active(dist_group)
+        # dp: None = data-parallel when the group has more than one rank; True = the data-parallel path even on one
+        # rank (its collectives then run over a one-rank communicator: the RCCL path tested on a one-GPU box)
+        self.distributed = dist.active(dist_group) if dp is None else bool(
+            dp and torch.distributed.is_available() and torch.distributed.is_initialized())
         # fused data-parallel path: gradients are all-reduced as sums and the Adam kernels scale them by 1 / world
         # (bitwise the mean for power-of-two worlds)
         self.inv_world = (torch.full((1,), 1.0 / torch.distributed.get_world_size(dist_group), device=device)
@@ -629,7 +632,7 @@ class SharedCriticBench:
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
     def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=None, buffer_size=1_000_000,
-                 handoff="gate", dp_split=True):
+                 handoff="gate", dp_split=True, dp=None):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
@@ -641,7 +644,8 @@ class SharedCriticBench:
             n_slots = int(os.environ.get("FLOCK_SC_SLOTS", "3"))
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
                                            buffer_size=buffer_size, dist_group=group, fused=fused,
-                                           snapshot=self.overlap, n_slots=n_slots, handoff=handoff, dp_split=dp_split)
+                                           snapshot=self.overlap, n_slots=n_slots, handoff=handoff, dp_split=dp_split,
+                                           dp=dp)
         if self.overlap:
             # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
             # with graphs, the native pipeline (one merged six-launch round per step on self.stream,

@@ -256,6 +256,79 @@ def test_two_ranks_dp_train_loop_equals_python_dp_rounds(cuda):
         np.testing.assert_array_equal(out[0][1][1][i], out[1][1][1][i])
 
 
+def _rccl_worker(port, q):
+    """The data-parallel C++ loops over RCCL itself: one rank, backend "nccl" on cuda:0, the learner forced onto its
+    data-parallel path (SharedCriticLearner(dp=True)), so every round's critic all-reduces (the early fc2-onward
+    part on the comm stream, the fc1 part on the learner stream) and the split actor all-reduce (second process group,
+    the pipeline's actor stream) are ProcessGroupNCCL collectives enqueued from C++ on those streams. Against the
+    per-step Python data-parallel rounds: bitwise equal (a one-rank sum is the identity; the grad scale is 1)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0")
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        torch.distributed.init_process_group("nccl", device_id=dev)
+        from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+        from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
+
+        E, Na, S = 24, 16, 7
+        ga = torch.Generator(device=dev).manual_seed(7)
+        pool = [torch.stack([torch.rand(E, Na, device=dev, generator=ga),
+                             torch.rand(E, Na, device=dev, generator=ga) * 3 - 1.5], -1).contiguous()
+                for _ in range(3)]
+        states = []
+        for mode in ("python", "loop_split", "loop"):
+            if mode == "python":
+                os.environ["FLOCK_LEARN_PIPELINE"] = "0"
+            else:
+                os.environ.pop("FLOCK_LEARN_PIPELINE", None)
+            env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
+                                          range_start=(0, 63.0), sensor_range=14.0, step_launches=3), device=dev)
+            g = torch.Generator(device=dev).manual_seed(3)
+            env.positions.copy_(torch.rand(E, Na, 2, device=dev, generator=g) * 63.0)
+            env.headings.copy_(torch.rand(E, Na, device=dev, generator=g) * 4.7)
+            hook = SharedCriticBench(env, device=dev, seed=11, dp_split=mode == "loop_split", dp=True)
+            assert hook.learner.distributed and hook.learner.dp_split == (mode == "loop_split")
+            if mode == "python":
+                for s in range(S):
+                    hook.step(s, pool[s % len(pool)])
+            else:
+                assert hook.can_loop()
+                hook.run_steps(0, 4, pool)
+                hook.run_steps(4, S - 4, pool)
+            hook.finish()
+            torch.cuda.synchronize()
+            L = hook.learner
+            C, A = L.critic, L.actors
+            states.append([t.cpu().numpy() for t in (C.data, C.exp_avg, C.exp_avg_sq, C.step_dev, A.data, A.target,
+                                                     A.exp_avg, A.exp_avg_sq, L.actor_steps, L.losses,
+                                                     env.positions, env.dnn)]
+                          + [L.replay.counter, L._learn_calls])
+        os.environ.pop("FLOCK_LEARN_PIPELINE", None)
+        q.put(states)
+        torch.distributed.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        q.put(traceback.format_exc() + repr(e))
+
+
+def test_one_rank_rccl_dp_train_loop_equals_python_dp_rounds(cuda):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    out = q.get(timeout=300)
+    p.join(timeout=60)
+    assert not isinstance(out, str), out
+    py, split, loop = out
+    for other, name in ((split, "split loop"), (loop, "loop")):
+        for i, (x, y) in enumerate(zip(py, other)):
+            np.testing.assert_array_equal(x, y, err_msg=f"{name} field {i}")
+
+
 NS = 4  # agents of the sharded test (divisible by the world size)
 
 
