@@ -411,6 +411,13 @@ __device__ __forceinline__ void scan_range(uint32_t (&key)[L], const float2* __r
 // copy, else 0.
 constexpr int kRg = 8;    // ghost columns per side of a row
 constexpr int kRows = 3;  // rows of a seeded scan (its radius is at most one row height)
+// EVR (step_kernel's even-row layout, per instantiation): every virtual row of ext ends with a one-entry sentinel
+// cell (+inf position), so that the seeded scan may read one entry past any row range without reaching the next row,
+// and pads every row range to an even length: a slot pair then never straddles two rows (scan_seeded)
+// virtual cells per row of the prefix: front ghosts, the gx columns, back ghosts (and the row sentinel)
+__host__ __device__ constexpr int row_stride(int gx, bool evr) { return gx + 2 * kRg + (evr ? 1 : 0); }
+// ext capacity per env: N entries, at most N ghost copies, two trailing sentinels (and the row sentinels)
+__host__ __device__ constexpr int ext_cap(int n, int gy, bool evr) { return 2 * n + 2 + (evr ? gy : 0); }
 
 // d2 of two candidates, bit-identical to the reference's periodic / Euclidean d2 in op order (gym_flock_v2.py:140-144,
 // :160-165). x: with Gx >= 2 kRg + 4 and every scanned cell at most kRg(+1) columns from the lane's cell, a regular
@@ -441,13 +448,13 @@ __device__ __forceinline__ int wrap_row(int yy, int G) { return yy < 0 ? yy + G 
 // as ONE sequence: candidate t of the lane is ext[t + b_q] for the row q with P_q <= t < P_{q+1} (P = running row
 // totals). The wave runs max-over-lanes(total) slots, two per iteration, with the slot index t wave-uniform.
 // Call with every lane of the wave active; lanes with use = false scan nothing.
-template <int L, bool PERIODIC>
+template <int L, bool PERIODIC, bool EVR>
 __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __restrict__ ext,
                                             const int* __restrict__ pre, int gx, int gy, int cy, bool use, float r,
                                             int ib, float xi, float yi, float box, float cwy, float inv_cwx,
                                             float inv_cwy, int cmax) {
     const uint32_t hi_mask = ~((1u << ib) - 1u);
-    const int W2 = gx + 2 * kRg;
+    const int W2 = row_stride(gx, EVR);
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
     int b[kRows], P[kRows];  // P[u]: candidates before row slot u; b[u]: ext index of candidate t in slot u minus t
@@ -480,11 +487,12 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
                 const int* pr = pre + (PERIODIC ? wrap_row(yy, gy) : yy) * W2;
                 const int s0 = pr[xa + kRg], e0 = pr[xb + kRg + 1];
                 b[u] = s0 - tot;
-                tot += e0 - s0;
+                tot += EVR ? (e0 - s0 + 1) & ~1 : e0 - s0;  // EVR: the padded slot reads the entry after the range
             }
         }
     }
     const int slots = wave_max(tot);
+    const int b0 = b[0], b1 = b[1], b2 = b[2], P1 = P[1], P2 = P[2];  // (EVR)
 #ifdef FLOCK_PHASE_PROF
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(&g_phase[(blockIdx.x & 63) * 32 + 21], (unsigned long long)((slots + 1) / 2));
@@ -509,8 +517,18 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
 #pragma unroll 1
     for (int t = 0; t < slots; t += 2) {
         int c0, c1;
-        cand_index(t, c0, c1);
-        const float4 q0 = ext[c0], q1 = ext[c1];
+        float4 q0, q1;
+        if constexpr (EVR) {
+            static_assert(kRows == 3, "the even-row slot map is written for three rows");
+            c0 = min(t + (t >= P2 ? b2 : (t >= P1 ? b1 : b0)), cmax);
+            c1 = c0 + 1;  // same row (even row totals), or the second sentinel at cmax + 1
+            q0 = ext[c0];
+            q1 = ext[c0 + 1];
+        } else {
+            cand_index(t, c0, c1);
+            q0 = ext[c0];
+            q1 = ext[c1];
+        }
         const f32x2 d = cand_d2x2<PERIODIC>(xi, yi, box, q0, q1);
         key_insert<L>(key, (__float_as_uint(d.x) & hi_mask) | (uint32_t)__float_as_int(q0.z));
         key_insert<L>(key, (__float_as_uint(d.y) & hi_mask) | (uint32_t)__float_as_int(q1.z));
@@ -522,13 +540,13 @@ __device__ __forceinline__ void scan_seeded(uint32_t (&key)[L], const float4* __
 // those of the full scan: every agent outside the block lies at least m = the distance to the block's edge away, so
 // if the truncated-d2 bucket of m^2 (shrunk by a 1e-5 safety factor) exceeds the L-th key, no unscanned key can enter
 // the top L. Call with every lane of the wave active (lanes with live = false scan nothing and return true).
-template <int L, bool PERIODIC>
+template <int L, bool PERIODIC, bool EVR>
 __device__ __forceinline__ bool scan_square(uint32_t (&key)[L], const float4* __restrict__ ext,
                                             const int* __restrict__ pre, int gx, int gy, int cx, int cy, int Ry,
                                             int ib, float xi, float yi, float box, float cwx, float cwy, float eps,
                                             int cmax, bool live) {
     const uint32_t hi_mask = ~((1u << ib) - 1u);
-    const int W2 = gx + 2 * kRg;
+    const int W2 = row_stride(gx, EVR);
 #pragma unroll
     for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #pragma unroll 1
@@ -585,13 +603,13 @@ __device__ __forceinline__ void insert_exact(float (&bd)[W], int (&bj)[W], float
 // exact rescan of an ambiguous bucket over the scanned neighbourhood only (rows cy-Ry..cy+Ry, columns cx-kRg..cx+kRg,
 // which contains a seeded lane's disk and a square lane's proved block): every unscanned d2 exceeds every d2 of the
 // ambiguous bucket, so the exact top k+1 by (d2, j) lies in the scanned ranges (per-lane loops: no wave-wide ops)
-template <int L, bool PERIODIC>
+template <int L, bool PERIODIC, bool EVR>
 __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)[L - 1],
                                                    const float4* __restrict__ ext, const int* __restrict__ pre,
                                                    int gx, int gy, int cx, int cy, int Ry, float xi, float yi,
                                                    float box) {
     constexpr int W = L - 1;
-    const int W2 = gx + 2 * kRg;
+    const int W2 = row_stride(gx, EVR);
 #pragma unroll
     for (int s = 0; s < W; ++s) {
         bd[s] = __builtin_inff();
@@ -619,14 +637,14 @@ __device__ __forceinline__ void exact_rescan_cells(float (&bd)[L - 1], int (&bj)
 // j among the lanes holding that d2): the same (d2, j) set, hence the same result, as exact_rescan_cells.
 // R = 0 lanes (no cell list, or a cell lane that fell back to the full scan) rescan all N agents of their env from
 // lpos the same way (knn_finalize's serial full rescan: the config-2 kernel's straggler blocks).
-template <int L, bool PERIODIC, bool CELL>
+template <int L, bool PERIODIC, bool CELL, bool EVR>
 __device__ __forceinline__ void exact_rescan_wave(float (&bd)[L - 1], int (&bj)[L - 1], bool amb, int R,
                                                   const float2* __restrict__ lpos, int S, int N,
                                                   const float4* __restrict__ ext_all, const int* __restrict__ pre_all,
                                                   int ecap, int npre, int g, int gx, int gy, int cx, int cy, float xi,
                                                   float yi, float box) {
     constexpr int W = L - 1;
-    const int W2 = gx + 2 * kRg;
+    const int W2 = row_stride(gx, EVR);
     const int lane = __lane_id();
     uint64_t todo = __ballot(amb);
     while (todo) {
@@ -813,7 +831,8 @@ constexpr int clog2c(int n) {
 // candidates [q N / SPL, (q + 1) N / SPL) for agent (t mod N), and the agents' lanes merge the SPL partial top-L
 // key lists through LDS (the same key set, hence the same result, as the one-lane scan). At N = 64 this gives 4x the
 // waves of one lane per agent, where one wave per SIMD left every latency exposed.
-template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1, int PFM = 0>
+template <int L, bool PERIODIC, bool CELL, int VAR = -1, int NC = 0, int GXC = 0, int GYC = 0, int SPL = 1, int PFM = 0,
+          bool EVR = false>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) void step_kernel(const Params pin) {
     static_assert(SPL == 1 || (NC > 0 && !CELL && (NC % (2 * SPL)) == 0), "split scans: specialised N, no cells");
     Params p = pin;
@@ -836,7 +855,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         if (CELL) {
             p.gx = GXC;
             p.gy = GYC;
-            p.ecap = 2 * NC + 2;
+            p.ecap = ext_cap(NC, GYC, EVR);
         }
     }
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -845,7 +864,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     int* flags = reinterpret_cast<int*>(red + 2 * p.G * p.P);     // [G] collision flags, [G] arrivals (G = 1)
     // cell list (CELL): ext [G][ecap] float4 (16-B aligned), cnt [G][gx*gy], pre [G][npre]: exclusive prefix over
     // the "virtual cells" of every row [ghosts of columns gx-kRg..gx-1, columns 0..gx-1, ghosts of columns 0..kRg-1]
-    const int gx = p.gx, gy = p.gy, ncell = gx * gy, W2 = gx + 2 * kRg, npre = gy * W2 + 1;
+    const int gx = p.gx, gy = p.gy, ncell = gx * gy, W2 = row_stride(gx, EVR), npre = gy * W2 + 1;
     float4* ext_all =
         reinterpret_cast<float4*>(smem + ((((size_t)(flags + 2 * p.G) - (size_t)smem) + 15) & ~(size_t)15));
     int* cnt_all = reinterpret_cast<int*>(ext_all + (CELL ? p.G * p.ecap : 0));
@@ -1182,6 +1201,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             const int f0 = in_group ? i * per : npre;
             const int y0 = f0 / W2, e0 = f0 - y0 * W2;
             auto vcount = [&](int yy, int e) {
+                if (EVR && e == W2 - 1) return 1;                                        // the row sentinel
                 if (e < kRg) return PERIODIC ? cnt[yy * gx + gx - kRg + e] : 0;          // ghosts of the last columns
                 if (e >= gx + kRg) return PERIODIC ? cnt[yy * gx + e - gx - kRg] : 0;    // ghosts of the first columns
                 return cnt[yy * gx + e - kRg];
@@ -1223,8 +1243,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         }
         // a sentinel behind the last entry (the seeded scan's clamp target): +inf position, d2 = +inf, a key above
         // every real one
-        if (in_group && i == 0)
+        if (in_group && i == 0) {
             ext[pre[npre - 1]] = make_float4(__builtin_inff(), __builtin_inff(), __int_as_float(0), 0.0f);
+            if (EVR)  // and a second one (ext_cap): the scan's slot pairs read c and c + 1
+                ext[pre[npre - 1] + 1] = make_float4(__builtin_inff(), __builtin_inff(), __int_as_float(0), 0.0f);
+        }
+        if (EVR && in_group && i < gy)  // each row's sentinel cell
+            ext[pre[i * W2 + W2 - 1]] = make_float4(__builtin_inff(), __builtin_inff(), __int_as_float(0), 0.0f);
         __syncthreads();
     }
 
@@ -1287,7 +1312,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #pragma unroll
         for (int s = 0; s < L; ++s) key[s] = kEmpty;
 #else
-        scan_seeded<L, PERIODIC>(key, ext, pre, gx, gy, cy, use, r, p.ib, x, y, p.box, p.cwy, p.inv_cwx, p.inv_cwy,
+        scan_seeded<L, PERIODIC, EVR>(key, ext, pre, gx, gy, cy, use, r, p.ib, x, y, p.box, p.cwy, p.inv_cwx, p.inv_cwy,
                                  pre[npre - 1]);
 #endif
         ok = use;
@@ -1301,7 +1326,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #endif
             PHASE_COUNT(16, 1);
             uint32_t key2[L];
-            const bool ok2 = scan_square<L, PERIODIC>(key2, ext, pre, gx, gy, cx, cy, 1, p.ib, x, y, p.box, p.cwx,
+            const bool ok2 = scan_square<L, PERIODIC, EVR>(key2, ext, pre, gx, gy, cx, cy, 1, p.ib, x, y, p.box, p.cwx,
                                                       p.cwy, p.cell_eps, cmax, active && !use);
             if (!use) {
 #pragma unroll
@@ -1358,10 +1383,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 #ifdef FLOCK_SERIAL_RESCAN  // A/B builds: the one-lane rescans
         if (amb && R == 0) knn_finalize<L, PERIODIC>(key, lpos + g * p.S, p.N, p.k, p.ib, kx, ky, p.box, bd, bj, true);
         if (CELL && amb && R == 1)
-            exact_rescan_cells<L, PERIODIC>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, gx, gy, cx, cy, R, x, y,
+            exact_rescan_cells<L, PERIODIC, EVR>(bd, bj, ext_all + g * p.ecap, pre_all + g * npre, gx, gy, cx, cy, R, x, y,
                                             p.box);
 #else
-        exact_rescan_wave<L, PERIODIC, CELL>(bd, bj, amb, R, lpos, p.S, p.N, ext_all, pre_all, p.ecap, npre, g, gx, gy,
+        exact_rescan_wave<L, PERIODIC, CELL, EVR>(bd, bj, amb, R, lpos, p.S, p.N, ext_all, pre_all, p.ecap, npre, g, gx, gy,
                                              cx, cy, kx, ky, p.box);
 #endif
     }
@@ -1673,7 +1698,7 @@ bool cell_grid(int N, int variant, int* gx, int* gy) {
     return true;
 }
 
-Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy, int G = 0) {
+Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy, int G = 0, bool evr = false) {
     Cfg c;
     c.S = (N + 1) & ~1;
     c.P = 1 << ceil_log2(N);
@@ -1686,7 +1711,8 @@ Cfg make_cfg(int E, int N, bool reset, int cells, int gx, int gy, int G = 0) {
         c.lds = (size_t)c.G * c.S * sizeof(float2) + (size_t)2 * c.G * c.P * sizeof(float) + 2 * c.G * sizeof(int);
     if (!reset && cells) {  // ext (2N + 2 float4, 16-B aligned) + cnt + pre per env
         c.lds = (c.lds + 15) & ~(size_t)15;
-        c.lds += (size_t)c.G * ((2 * N + 2) * sizeof(float4) + (size_t)(gx * gy + gy * (gx + 2 * kRg) + 1 + 16) * 4);
+        c.lds += (size_t)c.G * ((size_t)ext_cap(N, gy, evr) * sizeof(float4) +
+                                (size_t)(gx * gy + gy * row_stride(gx, evr) + 1 + 16) * 4);
     }
     return c;
 }
@@ -1729,14 +1755,20 @@ int resident_blocks(const void* kernel, int T, size_t lds) {
     return per_cu * cus;
 }
 
-template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1, int PF = 0>
-bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
-    if (p.variant != VAR || p.N != NC || p.k != 4 || (p.periodic != 0) != PERIODIC || (p.cells != 0) != CELL ||
-        p.normalize)
+template <int VAR, int NC, bool PERIODIC, bool CELL, int GXC, int GYC, int SPL = 1, int PF = 0, bool EVR = false>
+bool launch_spec(const Cfg& c0, const Params& p0, hipStream_t s) {
+    if (p0.variant != VAR || p0.N != NC || p0.k != 4 || (p0.periodic != 0) != PERIODIC || (p0.cells != 0) != CELL ||
+        p0.normalize)
         return false;
-    if (CELL && (p.gx != GXC || p.gy != GYC || p.ecap != 2 * NC + 2)) return false;
+    if (CELL && (p0.gx != GXC || p0.gy != GYC || p0.ecap != ext_cap(NC, GYC, false))) return false;
     if (knobs().no_spec) return false;  // A/B diagnostics: the generic instantiation
     Cfg c = c0;
+    Params p = p0;
+    if (EVR) {  // the even-row layout: row sentinels in ext (its capacity and the LDS size)
+        static_assert(!EVR || CELL, "the even-row layout is a cell-list layout");
+        c = make_cfg(p.E, NC, false, p.cells, GXC, GYC, 0, true);
+        p.ecap = ext_cap(NC, GYC, true);
+    }
     if (SPL > 1) {  // one env per block of SPL * NC lanes; LDS: the G = 1 layout + the merge lists in place of ext
         if (knobs().no_split) return false;
         c = make_cfg(p.E, NC, false, 0, 0, 0, 1);
@@ -1745,7 +1777,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     }
     const int parts = env_launches(c.blocks, p.launches);
     if (PF != 0 && parts <= 1 && knobs().pf != 0) {  // each block pulls a later block's inputs into L2
-        auto* kern = step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, PF>;
+        auto* kern = step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, PF, EVR>;
         static int pf_lds = -1, pf_res = 0;  // per instantiation (the LDS size is fixed by NC, GXC, GYC)
         if (pf_lds != (int)c.lds) {
             pf_res = resident_blocks(reinterpret_cast<const void*>(kern), c.T, c.lds);
@@ -1758,8 +1790,8 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
         return true;
     }
     if (parts <= 1) {
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(c.blocks), dim3(c.T), c.lds, s,
-                           p);
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, 0, EVR>), dim3(c.blocks), dim3(c.T),
+                           c.lds, s, p);
         return true;
     }
     // the step as `parts` back-to-back launches over consecutive env ranges (same results: envs are independent)
@@ -1767,7 +1799,7 @@ bool launch_spec(const Cfg& c0, const Params& p, hipStream_t s) {
     Params q = p;
     for (int b0 = 0; b0 < c.blocks; b0 += per) {
         q.env0 = b0 * c.G;
-        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL>), dim3(min(per, c.blocks - b0)),
+        hipLaunchKernelGGL((step_kernel<6, PERIODIC, CELL, VAR, NC, GXC, GYC, SPL, 0, EVR>), dim3(min(per, c.blocks - b0)),
                            dim3(c.T), c.lds, s, q);
     }
     return true;
@@ -1777,10 +1809,12 @@ template <int L>
 void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
     if constexpr (L == 6) {
         if (launch_spec<FLOCK_VARIANT_V2, 256, true, true, 42, 6, 1, 1>(c, p, s)) return;  // config 3 (+ L2 pull)
-        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12, 1, 3>(c, p, s)) return;  // config 5 (+ L2 pull, late)
+        if (launch_spec<FLOCK_VARIANT_V2, 1024, true, true, 85, 12, 1, 3, true>(c, p, s)) return;  // config 5 (+ L2 pull, late)
         // config 4: no pull (the config-5 pull + non-temporal streams measured 0.1954-0.1959 against 0.1929-0.1937 ms
-        // per step, the kinematics pull 0.1952; profiles/r05/c4pf/)
-        if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8>(c, p, s)) return;  // config 4
+        // per step, the kinematics pull 0.1952; profiles/r05/c4pf/). The even-row layout (EVR) in configs 4 and 5
+        // only: 0.1929-0.1936 -> 0.1890-0.1907 and 0.7535-0.7570 -> 0.7393-0.7417 ms per step, config 3 0.0809-0.0815
+        // -> 0.0820-0.0823 (profiles/r05/evenrows/)
+        if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8, 1, 0, true>(c, p, s)) return;  // config 4
         if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
     }
     if (p.cells) {
@@ -1807,7 +1841,7 @@ int dispatch(Params& p, hipStream_t s, bool reset) {
     // normalize_distance runs on the generic full-scan instantiations (a runtime flag there; launch_spec declines)
     p.cells = (reset || knobs().no_cells || p.normalize) ? 0 : cell_grid(p.N, p.variant, &p.gx, &p.gy);
     if (p.cells) {
-        p.ecap = 2 * p.N + 2;
+        p.ecap = ext_cap(p.N, p.gy, false);  // the generic instantiations: no row sentinels
         p.cwx = p.box / (float)p.gx;
         p.cwy = p.box / (float)p.gy;
         p.inv_cwx = (float)p.gx / p.box;
