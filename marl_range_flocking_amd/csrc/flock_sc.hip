@@ -707,7 +707,9 @@ struct Pull {
     int64_t rel[2];
     int64_t n[2];  // floats
 };
-__device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bool sc1_agent) {
+// part: 0 every panel, 1 only the panels at fixed addresses, 2 only the agent-relative ones (the agent index of a
+// critic-phase job is part of its snapshot: read after the gate)
+__device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bool sc1_agent, int part = 0) {
     float sink = 0.0f;
     int64_t lines[2], total = 0;
     const float* base[2];
@@ -715,8 +717,9 @@ __device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bo
     for (int i = 0; i < 2; ++i) {
         lines[i] = (pl.n[i] + 31) >> 5;
         total += lines[i];
-        const int64_t ag = pl.agent[i] ? (sc1_agent ? flock_mem::ld_sc1(pl.agent[i]) : *pl.agent[i]) : 0;
-        base[i] = pl.p[i] ? pl.p[i] + pl.rel[i] * ag : nullptr;
+        const bool skip = (part == 1 && pl.agent[i]) || (part == 2 && !pl.agent[i]);
+        const int64_t ag = (pl.agent[i] && !skip) ? (sc1_agent ? flock_mem::ld_sc1(pl.agent[i]) : *pl.agent[i]) : 0;
+        base[i] = (pl.p[i] && !skip) ? pl.p[i] + pl.rel[i] * ag : nullptr;
     }
     const int64_t lo = total * rank / ranks, hi = total * (rank + 1) / ranks;
     for (int64_t l = lo + threadIdx.x; l < hi; l += 256) {
@@ -731,12 +734,21 @@ template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa, Pull pc, Pull pa) {
     SC_PROF(0);
     const bool crit = (int)blockIdx.y < npc;
-    if (ac.gate && crit && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
     // the pull: this block's share of its job's panels among the job's blocks of its XCD group (x mod 8)
     const int rb8 = (int)gridDim.x >> 3, yj = crit ? (int)blockIdx.y : (int)blockIdx.y - npc;
     const int nj = crit ? npc : (int)gridDim.y - npc;
     float sink = 0.0f;
-    if ((gridDim.x & 7) == 0) sink = pull_l2(crit ? pc : pa, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, crit);
+    // gated critic blocks: the fixed panels while the block waits for its snapshot, the agent-relative ones after it
+    // (same-box A/B against the whole pull after the gate: 200 steps 0.0798-0.0804 vs 0.0803-0.0811 ms per step,
+    // profiles/r05/pullearly/)
+    if (ac.gate && crit) {
+        if ((gridDim.x & 7) == 0) sink = pull_l2(pc, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, true, 1);
+        if (!gate_wait(ac.gate, ac.gate_seq)) return;
+        if ((gridDim.x & 7) == 0) sink += pull_l2(pc, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, true, 2);
+    } else {
+        if (ac.gate && crit && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
+        if ((gridDim.x & 7) == 0) sink = pull_l2(crit ? pc : pa, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, crit);
+    }
     const int bx = xcd_perm(blockIdx.x, gridDim.x);
     if (crit)
         c1_body<C, HC>(wc, ac, bx, blockIdx.y);
