@@ -136,6 +136,7 @@ struct RowArgs {
     int B, in, na, H1, H2;
     const int64_t* idx;
     const int64_t* agent;
+    int64_t agent_v;  // >= 0: the agent index itself (the host's pipeline knows it), read instead of *agent
     const float *rs, *rs2, *ra, *rr, *rt;  // ring
     const float* critic;
     const float* actors;
@@ -147,6 +148,9 @@ struct RowArgs {
     unsigned long long* gate;
     unsigned long long gate_seq;
 };
+// the agent index of a job: the host's value when it has one (flock_sc_pipeline: no dependent load before the agent's
+// parameter addresses), else the device word (graph-captured learns)
+__device__ __forceinline__ int64_t agent_at(const int64_t* p, int64_t v) { return v >= 0 ? v : *p; }
 
 // ---------------------------------------------------------------------------------------------------------------
 // helpers
@@ -347,7 +351,7 @@ __device__ __forceinline__ void c1_body(const Ws& w, const RowArgs& a, int bx, i
     // the staged replay rows and the agent index are read `sc1`: with the device-side gate (sc_k1) they are a
     // snapshot another queue's kernel has just written through (csrc/flock_mem.h); the index rows are constant
     using flock_mem::ld_sc1;
-    const float* net = path == 0 ? a.actors_target + ld_sc1(a.agent) * a.stride : a.critic;  // fc1 block at offset 0
+    const float* net = path == 0 ? a.actors_target + (a.agent_v >= 0 ? a.agent_v : ld_sc1(a.agent)) * a.stride : a.critic;  // fc1 block at offset 0
     const bool live = r < a.B;
     if (live) {
         const int64_t ir = a.idx[r];
@@ -407,7 +411,7 @@ __device__ __forceinline__ void c3_body(const Ws& w, const RowArgs& a, int bx) {
         for (int o = 0; o < kMaxAct; ++o) act[o] = o < na ? w.A[(int64_t)r * na + o] : 0.0f;
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
-    stage(at, a.actors_target + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    stage(at, a.actors_target + agent_at(a.agent, a.agent_v) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
     if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
@@ -507,7 +511,7 @@ __device__ __forceinline__ void a1_body(const Ws& w, const RowArgs& a, int bx, i
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = bx * kRowsPerBlock + wv;
     const bool live = r < a.B;
-    const float* net = path == 0 ? a.actors + (*a.agent) * a.stride : a.critic;
+    const float* net = path == 0 ? a.actors + agent_at(a.agent, a.agent_v) * a.stride : a.critic;
     if (live && lane < a.in) xs[wv * kMaxIn + lane] = w.S[(int64_t)r * a.in + lane];
     stage(sp, net, H1 * (a.in + 3));
     __syncthreads();
@@ -544,7 +548,7 @@ __device__ __forceinline__ void a3_body(const Ws& w, const RowArgs& a, int bx) {
         load_row<C>(zc2, w.Z2b + ((int64_t)a.B + r) * H2, H2, lane);
     }
     stage(ct, a.critic + co.g2, crit_tail_len(na, H2));
-    stage(at, a.actors + (*a.agent) * a.stride + ao.g2, act_tail_len(na, H2));
+    stage(at, a.actors + agent_at(a.agent, a.agent_v) * a.stride + ao.g2, act_tail_len(na, H2));
     __syncthreads();
     if (!live) return;
     const float *cg2 = ct, *cbe2 = ct + H2, *cWa = ct + 2 * H2, *cba = cWa + H2 * na, *cWq = cba + H2;
@@ -704,6 +708,7 @@ __device__ __forceinline__ int xcd_perm(int x, int n) { return (n & 7) == 0 ? (x
 struct Pull {
     const float* p[2];
     const int64_t* agent[2];  // p[i] + rel[i] * (*agent[i]) when agent[i] != NULL
+    int64_t agent_v[2];       // >= 0: the agent index itself
     int64_t rel[2];
     int64_t n[2];  // floats
 };
@@ -718,7 +723,10 @@ __device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bo
         lines[i] = (pl.n[i] + 31) >> 5;
         total += lines[i];
         const bool skip = (part == 1 && pl.agent[i]) || (part == 2 && !pl.agent[i]);
-        const int64_t ag = (pl.agent[i] && !skip) ? (sc1_agent ? flock_mem::ld_sc1(pl.agent[i]) : *pl.agent[i]) : 0;
+        const int64_t ag = (pl.agent[i] && !skip)
+                               ? (pl.agent_v[i] >= 0 ? pl.agent_v[i]
+                                                     : (sc1_agent ? flock_mem::ld_sc1(pl.agent[i]) : *pl.agent[i]))
+                               : 0;
         base[i] = (pl.p[i] && !skip) ? pl.p[i] + pl.rel[i] * ag : nullptr;
     }
     const int64_t lo = total * rank / ranks, hi = total * (rank + 1) / ranks;
@@ -787,6 +795,7 @@ struct GemmP {
     int M, N, K, sam, sak, sbk, sbn, ldc;
     int64_t relB;  // B and bias are agent-relative: + relB * (*agent)
     const int64_t* agent;
+    int64_t agent_v;  // >= 0: the agent index itself (RowArgs::agent_v)
     int tiles_n, tiles;
     int kchunk;  // K panel depth staged per round (<= kKC, multiple of 8)
 };
@@ -1036,7 +1045,7 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
     if (x >= g.tiles) return;
     const int t = xcd_tile(x, g.tiles);
     const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-    const int64_t rel = g.relB ? g.relB * (*g.agent) : 0;
+    const int64_t rel = g.relB ? g.relB * agent_at(g.agent, g.agent_v) : 0;
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int n = tn * kT + (l & 31);
     const float bias = (g.bias && n < g.N) ? g.bias[rel + n] : 0.0f;
@@ -1181,6 +1190,7 @@ struct BwdJob {
     int64_t rel;       // g1 is agent-relative: + rel * (*agent)
     int64_t grad_rel;  // grad is agent-relative: + grad_rel * (*agent) (0: FlockScUpdate.actor_grad_out)
     const int64_t* agent;
+    int64_t agent_v;  // >= 0: the agent index itself
     float* loss;
 };
 __host__ __device__ inline int bwd_blocks(const BwdJob& j) { return j.dh.tiles + j.dw.tiles + j.nblk; }
@@ -1191,13 +1201,13 @@ __device__ __forceinline__ void bwd_body(const BwdJob& j, int bx) {
     extern __shared__ float4 smem4[];
     float* smem = reinterpret_cast<float*>(smem4);
     const int tid = threadIdx.x, wv = tid >> 6, l = tid & 63;
-    const int64_t base = j.rel ? j.rel * (*j.agent) : 0;
-    const int64_t gbase = j.grad_rel ? j.grad_rel * (*j.agent) : 0;
+    const int64_t base = j.rel ? j.rel * agent_at(j.agent, j.agent_v) : 0;
+    const int64_t gbase = j.grad_rel ? j.grad_rel * agent_at(j.agent, j.agent_v) : 0;
     if (bx < j.dh.tiles) {
         const GemmP& g = j.dh;
         const int t = xcd_perm(bx, g.tiles);  // row strips on the XCDs of the k1 / k3 rows they read (xcd_perm)
         const int tm = t / g.tiles_n, tn = t - tm * g.tiles_n;
-        const int64_t relB = g.relB ? g.relB * (*g.agent) : 0;
+        const int64_t relB = g.relB ? g.relB * agent_at(g.agent, g.agent_v) : 0;
         const int n = tn * kT + (l & 31);
         const bool nok = n < g.N;
         // the epilogue's inputs, loaded before the GEMM
@@ -1301,6 +1311,7 @@ struct GradAdam {
     int64_t grad_rel;  // grad likewise: + grad_rel * (*agent) (0 with FlockScUpdate.actor_grad_out)
     const float* grad_scale;  // Adam-only blocks: gradient *= *grad_scale first (data-parallel 1 / world), or NULL
     const int64_t* agent;
+    int64_t agent_v;  // >= 0: the agent index itself
     int64_t* step;  // step[0], or step[*agent] when rel != 0
     unsigned* counter;
     float lr, b1, b2, eps;
@@ -1353,11 +1364,11 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
     __shared__ float sh[2];
     __shared__ int sh_soft;
     const int tid = threadIdx.x;
-    const int64_t agent = ga.rel ? *ga.agent : 0;
+    const int64_t agent = ga.rel ? agent_at(ga.agent, ga.agent_v) : 0;
     const int64_t base = ga.rel * agent, gbase = ga.grad_rel * agent;
     if (tid == 0) {
         const int64_t step0 = ga.do_adam ? ga.step[agent] : 0;
-        const int64_t count = ga.soft_count ? ga.soft_count[*ga.agent] : step0;
+        const int64_t count = ga.soft_count ? ga.soft_count[agent_at(ga.agent, ga.agent_v)] : step0;
         sh_soft = ga.do_adam && ga.soft_rate > 0 && (count % ga.soft_rate) == 0;  // this learn's count
         if (ga.do_adam) {
             const double st = (double)(step0 + 1);
@@ -1455,6 +1466,7 @@ GemmP gemm_p(const float* A, const float* B, float* C, const float* bias, int M,
     g.A = A; g.B = B; g.C = C; g.bias = bias;
     g.M = M; g.N = N; g.K = K; g.sam = sam; g.sak = sak; g.sbk = sbk; g.sbn = sbn; g.ldc = ldc; g.relB = relB;
     g.agent = agent;
+    g.agent_v = -1;
     g.tiles_n = (N + kT - 1) / kT;
     g.tiles = ((M + kT - 1) / kT) * g.tiles_n;
     g.kchunk = balanced_kc(K, kFwdKC);
@@ -1574,7 +1586,7 @@ int chunks(const FlockScUpdate* u) {
 RowArgs row_args(const FlockScUpdate* u) {
     RowArgs a;
     a.B = u->B; a.in = u->in_dim; a.na = u->n_actions; a.H1 = u->fc1; a.H2 = u->fc2;
-    a.idx = u->idx; a.agent = u->agent;
+    a.idx = u->idx; a.agent = u->agent; a.agent_v = -1;
     a.rs = u->ring_state; a.rs2 = u->ring_new_state; a.ra = u->ring_action; a.rr = u->ring_reward;
     a.rt = u->ring_terminal;
     a.critic = u->critic; a.actors = u->actors; a.actors_target = u->actors_target; a.stride = u->actor_stride;
@@ -1629,7 +1641,7 @@ void bwd_common(Job& j, const float* W2, int64_t rel_w2, const int64_t* agent, c
     bw.F = H1n; bw.ntn = bw.dh.tiles_n;
     bw.w2_off = w2_off;
     bw.nred = 0; bw.nblk = 0; bw.B = B;
-    bw.grad = grad; bw.rel = rel; bw.grad_rel = rel; bw.agent = agent; bw.loss = loss;
+    bw.grad = grad; bw.rel = rel; bw.grad_rel = rel; bw.agent = agent; bw.agent_v = -1; bw.loss = loss;
 }
 
 // the late launch's job: fc1 / LN1 reductions (+ Adam), Adam of [W2, total)
@@ -1689,6 +1701,7 @@ void critic_job(const FlockScUpdate* u, Job& j) {
     ga.rel = 0;
     ga.grad_rel = 0;
     ga.agent = u->agent;
+    ga.agent_v = -1;
     ga.step = u->critic_step;
     ga.counter = u->counters;
     ga.lr = u->beta;
@@ -1741,6 +1754,7 @@ void actor_job(const FlockScUpdate* u, Job& j) {
         ga.grad_rel = 0;
     }
     ga.agent = u->agent;
+    ga.agent_v = -1;
     ga.step = u->actor_steps;
     ga.counter = u->counters + 1;
     ga.lr = u->alpha;
@@ -1792,10 +1806,12 @@ bool spec_shape(const Job& j) { return !g_sc_no_spec && j.H1 == 400 && j.H2 == 3
 // the second's (the critic, or the critic view the actor phase reads; the critic phase's third problem shares it)
 Pull gemm_pull(const Job& j) {
     Pull p{};
+    p.agent_v[0] = p.agent_v[1] = -1;
     for (int i = 0; i < 2 && i < j.nfwd; ++i) {
         const GemmP& g = j.fwd[i];
         p.p[i] = g.B;
         p.agent[i] = g.relB ? g.agent : nullptr;
+        p.agent_v[i] = g.agent_v;
         p.rel[i] = g.relB;
         p.n[i] = (int64_t)g.K * g.N;  // fc2.weight [H2][H1]: K = H1 rows of B, N = H2 columns
     }
@@ -2165,13 +2181,36 @@ int early_critic_allreduce(void* ctx) {
     return hipEventRecord(p->ar_done, p->comm_stream) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: event record");
 }
 
+// a job with its agent index as a value (the pipeline's learns know theirs: every kernel of the round computes the
+// agent's parameter addresses without first loading the index). Same-box A/B against the device-word reads
+// (profiles/r05/agentv/): driver command 0.0897-0.0904 vs 0.0908-0.0920, 200 steps 0.0809-0.0819 vs 0.0803-0.0815 ms
+// per step: within the noise either way
+Job with_agent(const Job& j0, int64_t agent) {
+    Job j = j0;
+    j.a.agent_v = agent;
+    for (int i = 0; i < j.nfwd; ++i) j.fwd[i].agent_v = agent;
+    j.bw.dh.agent_v = agent;
+    j.bw.dw.agent_v = agent;
+    j.bw.agent_v = agent;
+    j.ga.agent_v = agent;
+    return j;
+}
+
 // one round of the pipeline on stream ls: critic phase of slot c and / or actor phase of slot a (-1: none);
 // agents: the learns' agent indices (split data-parallel rounds)
 int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a, int64_t agent_c, int64_t agent_a) {
-    if (!p->dp) return launch_round(ls, c >= 0 ? &p->jc[c] : nullptr, a >= 0 ? &p->ja[a] : nullptr);
+    if (!p->dp) {
+        Job jc, ja;
+        if (c >= 0) jc = with_agent(p->jc[c], agent_c);
+        if (a >= 0) ja = with_agent(p->ja[a], agent_a);
+        return launch_round(ls, c >= 0 ? &jc : nullptr, a >= 0 ? &ja : nullptr);
+    }
     int rc = 0;
-    const Job* gc = c >= 0 ? &p->jgc[c] : nullptr;
-    const Job* ga = a >= 0 ? &p->jga[a] : nullptr;
+    Job jgc, jga;
+    if (c >= 0) jgc = with_agent(p->jgc[c], agent_c);
+    if (a >= 0) jga = with_agent(p->jga[a], agent_a);
+    const Job* gc = c >= 0 ? &jgc : nullptr;
+    const Job* ga = a >= 0 ? &jga : nullptr;
     if (!p->split) {
         // gradients only (do_adam = 0) into the bucket, ONE all-reduce (sum) of the part they wrote, then the Adam
         // launch (gradients scaled by *grad_scale): SharedCriticLearner._dp_round

@@ -106,5 +106,32 @@ int main() {
         printf("rep %d: Y reads its own lines %.3f us; after X rewrote them: Y reads %.3f us (stale words %u), X reads "
                "%.3f us (stale words %u)\n", rep, t0, t2, hbad, t3, hbad2 - hbad);
     }
+    // 3. lines WRITTEN by XCD X in the previous launch, read by X in the next (the learner round's producer ->
+    //    consumer hand-off): k0 X writes (plain stores), k1 X reads; against k1' X re-reading lines it only read
+    for (int rep = 0; rep < 3; ++rep) {
+        const int X = 4;
+        const float v0 = 100.0f + rep;
+        wr<<<kBlocks, 256>>>(buf, X, v0);
+        hipMemset(bad, 0, 4);
+        hipMemset(t, 0, kBlocks * 8);
+        rd<<<kBlocks, 256>>>(buf, X, v0, bad, t);  // X reads the lines it wrote one launch earlier
+        if (hipDeviceSynchronize()) return 6;
+        hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
+        const double tw = mean_us(ht);
+        hipMemset(t, 0, kBlocks * 8);
+        rd<<<kBlocks, 256>>>(buf, X, v0, bad, t);  // and again (lines it read one launch earlier)
+        if (hipDeviceSynchronize()) return 7;
+        hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
+        const double tr = mean_us(ht);
+        hipMemset(t, 0, kBlocks * 8);
+        rd<<<kBlocks, 256>>>(buf, (X + 3) & 7, v0, bad, t);  // another XCD reads them
+        if (hipDeviceSynchronize()) return 8;
+        hipMemcpy(ht, t, sizeof(ht), hipMemcpyDeviceToHost);
+        const double to = mean_us(ht);
+        unsigned hb = 0;
+        hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
+        printf("rep %d: X reads the lines it wrote last launch %.3f us; lines it read last launch %.3f us; another XCD "
+               "%.3f us (stale words %u)\n", rep, tw, tr, to, hb);
+    }
     return 0;
 }
