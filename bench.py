@@ -107,10 +107,13 @@ def parse():
     ap.add_argument("--diag-prewarm-ms", type=float, default=0.0,
                     help="diagnostics only (never a bench line): keep the GPU busy with matmuls for this long before "
                          "the warmup steps (clock / power-state probe)")
+    ap.add_argument("--train-overlap", default="auto", choices=["auto", "0", "1"],
+                    help="configs 4 / 5: train() on its own stream beside the following env steps (auto: on for VDN, "
+                         "where it measured -3.5 %% per step; off for RNN-MADDPG, where it measured flat and its "
+                         "update's HBM traffic slows the env launches it overlaps, profiles/r05/trainov/)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
-                         "results; the env kernel time is unchanged by it); configs 4 / 5: train() on its own stream "
-                         "beside the env steps that follow it (its sampled rows copied out first; same results); "
+                         "results; the env kernel time is unchanged by it); configs 4 / 5: see --train-overlap; "
                          "0: the learner runs after each step")
     args = ap.parse_args()
     c = CONFIGS[args.config]
@@ -498,9 +501,10 @@ def main():
 
         hook = SharedCriticBench(env, device=dev, seed=1234 + rank, overlap=bool(args.overlap))
     elif args.learner == "vdn":
-        hook = VDNBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap))
+        hook = VDNBench(env, dev, seed=1234 + rank,
+                        overlap=bool(args.overlap) and args.train_overlap in ("auto", "1"))
     elif args.learner == "maddpg_rnn":
-        hook = MADDPGBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap))
+        hook = MADDPGBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap) and args.train_overlap == "1")
 
     def one_step(s, ev=None):
         a = pool[s % len(pool)]
