@@ -571,8 +571,11 @@ def main():
         if hook.learner.__dict__.get("_pipe") is not None:
             handoff = {0: "cross-queue event wait", 1: "device gate polled by the critic row blocks"}[
                 hook.learner.pipeline().gated()]
-            if getattr(hook.learner, "dp_split", False):
-                handoff += "; data-parallel actor all-reduce + Adam on a second group and stream"
+            if getattr(hook.learner, "distributed", False):
+                handoff += ("; data-parallel actor all-reduce + Adam on a second group and stream"
+                            if getattr(hook.learner, "dp_split", False) else "; data-parallel rounds, one all-reduce")
+                handoff += (", direct RCCL calls" if getattr(hook.learner, "dp_rccl", False)
+                            and torch.distributed.get_backend() == "nccl" else ", c10d ProcessGroup calls")
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

@@ -7,7 +7,10 @@
 //   C++ loop below drive the same object, so the pending actor phase and the slot rotation carry over between them.
 //   set_dp() turns every round into the data-parallel form (gradients into the [critic | actor] bucket, a SUM
 //   all-reduce over the c10d ProcessGroup enqueued on the learner stream, the Adam launch with grad_scale = 1 / world;
-//   SharedCriticLearner.dp_learn).
+//   SharedCriticLearner.dp_learn). set_rccl() makes the same collectives direct RCCL calls (ncclAllReduce on the
+//   pipeline's streams over communicators of its own, one for the critic and one for the actor part) instead of
+//   c10d ProcessGroup calls: the host cost of a collective drops from tens of microseconds (work objects, events,
+//   stream guards) to the RCCL enqueue, which at N > 1 is what sets the step (tools/rccl_host_cost.py).
 // torch.classes.flock.ScTrainLoop: the config-3 training loop (BASELINE config 3, the reference's
 //   learners/maddpg_shared_critic/train_flock.py:112-123 cadence: env.step, store_transitions, one learn() per step)
 //   enqueued K steps per call from C++, so the host cost of a vectorized step is a few launch calls instead of a
@@ -30,6 +33,9 @@
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
+#include <dlfcn.h>
+
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -40,6 +46,41 @@
 namespace {
 
 using at::Tensor;
+
+// The RCCL entry points the direct path needs, resolved from the librccl torch itself loaded (librccl.so.1: one RCCL
+// in the process, the one ProcessGroupNCCL uses), with the ABI types spelled out (rccl.h: ncclUniqueId is 128 bytes,
+// ncclFloat32 = 7, ncclSum = 0, ncclSuccess = 0).
+struct RcclUid {
+    char internal[128];
+};
+typedef struct RcclComm* RcclCommT;
+struct RcclApi {
+    int (*get_unique_id)(RcclUid*) = nullptr;
+    int (*comm_init_rank)(RcclCommT*, int, RcclUid, int) = nullptr;
+    int (*all_reduce)(const void*, void*, size_t, int, int, RcclCommT, hipStream_t) = nullptr;
+    int (*comm_destroy)(RcclCommT) = nullptr;
+    const char* (*error_string)(int) = nullptr;
+    bool ok = false;
+};
+const RcclApi& rccl() {
+    static RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) return a;
+        a.get_unique_id = reinterpret_cast<int (*)(RcclUid*)>(dlsym(h, "ncclGetUniqueId"));
+        a.comm_init_rank = reinterpret_cast<int (*)(RcclCommT*, int, RcclUid, int)>(dlsym(h, "ncclCommInitRank"));
+        a.all_reduce = reinterpret_cast<int (*)(const void*, void*, size_t, int, int, RcclCommT, hipStream_t)>(
+            dlsym(h, "ncclAllReduce"));
+        a.comm_destroy = reinterpret_cast<int (*)(RcclCommT)>(dlsym(h, "ncclCommDestroy"));
+        a.error_string = reinterpret_cast<const char* (*)(int)>(dlsym(h, "ncclGetErrorString"));
+        a.ok = a.get_unique_id && a.comm_init_rank && a.all_reduce && a.comm_destroy;
+        return a;
+    }();
+    return api;
+}
+constexpr int kRcclFloat32 = 7, kRcclSum = 0;
 
 template <typename T>
 T* ptr_or_null(const Tensor& t) {
@@ -59,6 +100,13 @@ struct ScPipeline : torch::CustomClassHolder {
     int64_t batch = 0, in_dim = 0, n_actions = 0, n_agents = 0, n_slots = 0;
     // data-parallel rounds
     c10::intrusive_ptr<c10d::ProcessGroup> pg, pg_actor;
+    // set_rccl: direct RCCL collectives instead of pg / pg_actor. A communicator is used from ONE stream only (two
+    // collectives of one communicator on different streams could run concurrently): the critic part's two streams
+    // (the learner stream; the comm stream of the split rounds' early part) each get their own, bound to a stream at
+    // its first use (the same order on every rank), the actor part one for the actor stream
+    RcclCommT comm_c[2] = {nullptr, nullptr};
+    void* comm_c_stream[2] = {nullptr, nullptr};
+    RcclCommT comm_actor = nullptr;
     Tensor bucket, grad_scale;
     std::vector<Tensor> actor_grads;
     std::string cb_error;
@@ -106,6 +154,62 @@ struct ScPipeline : torch::CustomClassHolder {
 
     ~ScPipeline() override {
         if (pipe) flock_sc_pipeline_destroy(pipe);
+        for (RcclCommT c : comm_c)
+            if (c) rccl().comm_destroy(c);
+        if (comm_actor) rccl().comm_destroy(comm_actor);
+    }
+
+    // one RCCL unique id (128 bytes) per call, made on ONE rank and sent to the others (SharedCriticLearner.pipeline)
+    static Tensor rccl_unique_id() {
+        TORCH_CHECK(rccl().ok, "ScPipeline.rccl_unique_id: RCCL (librccl.so.1) is not loaded");
+        RcclUid id;
+        const int rc = rccl().get_unique_id(&id);
+        TORCH_CHECK(rc == 0, "ncclGetUniqueId failed: ", rccl().error_string ? rccl().error_string(rc) : "");
+        Tensor t = at::empty({128}, at::TensorOptions().dtype(at::kByte));
+        std::memcpy(t.data_ptr(), id.internal, 128);
+        return t;
+    }
+    static RcclCommT rccl_comm(const Tensor& uid, int64_t rank, int64_t world) {
+        TORCH_CHECK(uid.device().is_cpu() && uid.scalar_type() == at::kByte && uid.numel() == 128 && uid.is_contiguous(),
+                    "ScPipeline.set_rccl: the unique ids are 128-byte CPU uint8 tensors");
+        RcclUid id;
+        std::memcpy(id.internal, uid.data_ptr(), 128);
+        RcclCommT c = nullptr;
+        const int rc = rccl().comm_init_rank(&c, (int)world, id, (int)rank);
+        TORCH_CHECK(rc == 0 && c, "ncclCommInitRank failed: ", rccl().error_string ? rccl().error_string(rc) : "");
+        return c;
+    }
+    // the data-parallel collectives as direct RCCL calls (after set_dp / set_dp_actor): a communicator for the critic
+    // part (learner and comm streams) and one for the actor part (actor stream), every rank calling with the same ids
+    // uids: [critic (first stream), critic (second stream), actor], each [128] uint8 on the CPU
+    void set_rccl(std::vector<Tensor> uids, int64_t rank, int64_t world) {
+        TORCH_CHECK(rccl().ok, "ScPipeline.set_rccl: RCCL (librccl.so.1) is not loaded");
+        TORCH_CHECK(pg, "ScPipeline.set_rccl: call set_dp first");
+        TORCH_CHECK(uids.size() == 3, "ScPipeline.set_rccl: three unique ids");
+        TORCH_CHECK(!comm_c[0], "ScPipeline.set_rccl: already set");
+        const at::OptionalDeviceGuard g(device);
+        comm_c[0] = rccl_comm(uids[0], rank, world);
+        comm_c[1] = rccl_comm(uids[1], rank, world);
+        if (pg_actor) comm_actor = rccl_comm(uids[2], rank, world);
+    }
+    RcclCommT critic_comm(void* stream) {
+        for (int i = 0; i < 2; ++i) {
+            if (comm_c_stream[i] == stream) return comm_c[i];
+            if (!comm_c_stream[i]) {
+                comm_c_stream[i] = stream;
+                return comm_c[i];
+            }
+        }
+        return nullptr;  // a third stream: no communicator for it
+    }
+    static int rccl_sum(RcclCommT c, float* data, int64_t n, void* stream, std::string& err) {
+        const int rc = rccl().all_reduce(data, data, (size_t)n, kRcclFloat32, kRcclSum, c,
+                                         static_cast<hipStream_t>(stream));
+        if (rc != 0) {
+            err = std::string("ncclAllReduce failed: ") + (rccl().error_string ? rccl().error_string(rc) : "");
+            return -4;
+        }
+        return 0;
     }
 
     // the all-reduce between a data-parallel round's gradient and Adam launches: a SUM over the process group,
@@ -113,6 +217,14 @@ struct ScPipeline : torch::CustomClassHolder {
     // stream for the collective; no host wait)
     static int allreduce_cb(void* ctx, float* data, int64_t n, void* stream) {
         auto* self = static_cast<ScPipeline*>(ctx);
+        if (self->comm_c[0]) {
+            RcclCommT c = self->critic_comm(stream);
+            if (!c) {
+                self->cb_error = "ScPipeline: the critic all-reduce was called from a third stream";
+                return -4;
+            }
+            return rccl_sum(c, data, n, stream, self->cb_error);
+        }
         try {
             const c10::hip::HIPStream hs =
                 c10::hip::getStreamFromExternal(static_cast<hipStream_t>(stream), self->device.index());
@@ -188,6 +300,7 @@ struct ScPipeline : torch::CustomClassHolder {
     // gradient buffer per slot, all-reduced (SUM) over `group` on the pipeline's actor stream
     static int actor_allreduce_cb(void* ctx, float* data, int64_t n, void* stream) {
         auto* self = static_cast<ScPipeline*>(ctx);
+        if (self->comm_actor) return rccl_sum(self->comm_actor, data, n, stream, self->cb_error);
         try {
             const c10::hip::HIPStream hs =
                 c10::hip::getStreamFromExternal(static_cast<hipStream_t>(stream), self->device.index());
@@ -362,7 +475,9 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         .def("verify", &ScPipeline::verify)
         .def("gated", &ScPipeline::gated)
         .def("set_gate", &ScPipeline::set_gate)
-        .def("set_dp_actor", &ScPipeline::set_dp_actor);
+        .def("set_dp_actor", &ScPipeline::set_dp_actor)
+        .def("set_rccl", &ScPipeline::set_rccl)
+        .def_static("rccl_unique_id", &ScPipeline::rccl_unique_id);
     m.class_<ScTrainLoop>("ScTrainLoop")
         .def(torch::init<std::vector<Tensor>, std::vector<double>, std::vector<int64_t>, std::vector<Tensor>, int64_t,
                          c10::intrusive_ptr<ScPipeline>, int64_t, int64_t>())

@@ -85,7 +85,7 @@ class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
                  ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
-                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=True, dp=None):
+                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=False, dp=None, dp_rccl=True):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -144,6 +144,13 @@ class SharedCriticLearner:
         # data-parallel pipelines: the actor half of each round all-reduced and stepped off the learner chain, over a
         # second process group of the same ranks (flock_sc_pipeline_set_dp_actor); created here, collectively
         self.dp_split = bool(dp_split and self.distributed and self.snapshot)
+        # the native pipeline's collectives as direct RCCL calls when the group's backend is RCCL ("nccl"): c10d
+        # ProcessGroup calls from the C++ loop cost tens of microseconds of host time each. One rank over RCCL on one
+        # GPU (tools/rccl_host_cost.py, profiles/r05/rccl_host/): single GPU 0.084 ms per step; unsplit rounds 0.112
+        # (c10d) / 0.091 (direct RCCL); split rounds (dp_split) 0.205 / 0.150: the split's extra chain work (a
+        # second critic all-reduce, a cross-stream wait, the separate Adam launches) costs more than the actor
+        # all-reduce it takes off the chain, so the unsplit round is the default
+        self.dp_rccl = bool(dp_rccl)
         self.actor_group = None
         if self.dp_split:
             ranks = torch.distributed.get_process_group_ranks(dist_group) if dist_group is not None else None
@@ -511,7 +518,7 @@ class SharedCriticLearner:
         (ScTrainLoop) share its slots and its pending actor phase. The round waits for its snapshot on the device-side
         gate (handoff="gate", single GPU) or on a cross-queue event. Data-parallel learners (dist_group) run every
         round as gradients, one RCCL all-reduce of the critic gradient over the group and the critic Adam launch on
-        the learner stream; with dp_split (default) the round's actor gradient is all-reduced over a second group and
+        the learner stream; with dp_split (opt-in) the round's actor gradient is all-reduced over a second group and
         stepped on the pipeline's actor stream, off the learner chain (set_dp_actor); without, one all-reduce of the
         [critic | actor] bucket (set_dp; dp_learn's rounds, enqueued from C++)."""
         if self._pipe is None:
@@ -531,6 +538,18 @@ class SharedCriticLearner:
                     self.dp_actor_grads = [torch.zeros(self.actors.per_agent, device=self.device)
                                            for _ in range(self.n_slots)]
                     p.set_dp_actor(self.actor_group.boxed(), self.dp_actor_grads)
+                if self.dp_rccl and torch.distributed.get_backend(group) == "nccl":
+                    # the collectives as direct RCCL calls on the pipeline's streams (ScPipeline.set_rccl): unique ids
+                    # made on the group's first rank, sent to the others over the group itself
+                    ids = torch.zeros(3, 128, dtype=torch.uint8, device=self.device)
+                    ranks = torch.distributed.get_process_group_ranks(group)
+                    if torch.distributed.get_rank() == ranks[0]:
+                        for i in range(3):
+                            ids[i].copy_(torch.classes.flock.ScPipeline.rccl_unique_id())
+                    torch.distributed.broadcast(ids, src=ranks[0], group=group)
+                    ids = ids.cpu()
+                    p.set_rccl([ids[i].contiguous() for i in range(3)], ranks.index(torch.distributed.get_rank()),
+                               len(ranks))
             p.set_gate(self.handoff == "gate")
             self._pipe = p
         return self._pipe
@@ -632,7 +651,7 @@ class SharedCriticBench:
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
     def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=None, buffer_size=1_000_000,
-                 handoff="gate", dp_split=True, dp=None):
+                 handoff="gate", dp_split=False, dp=None, dp_rccl=True):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
@@ -645,7 +664,7 @@ class SharedCriticBench:
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
                                            buffer_size=buffer_size, dist_group=group, fused=fused,
                                            snapshot=self.overlap, n_slots=n_slots, handoff=handoff, dp_split=dp_split,
-                                           dp=dp)
+                                           dp=dp, dp_rccl=dp_rccl)
         if self.overlap:
             # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
             # with graphs, the native pipeline (one merged six-launch round per step on self.stream,
