@@ -953,13 +953,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     for (int s = 0; s < kMemKeep; ++s) mrow[s] = 0.0f;
     float prev_h = 0.0f;  // uw reward: the previous heading (:202-204), loaded early
     if (active && variant == FLOCK_VARIANT_UW) prev_h = p.prev_heading[a];
-    if constexpr (SPL > 1 && kMemEarly) {  // split instantiation: lane groups 1..3 roll memory frames 0..2 (k = 4)
+    if constexpr (SPL > 1 && kMemEarly) {  // split instantiation: lane groups 1..SPL-1 roll memory frames 0..2 (k = 4)
         const int q = t / NC, ia = t - q * NC;
         const int envb = p.env0 + (int)blockIdx.x;
-        if (q >= 1 && q < kMem && envb < p.E && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
+        if (q >= 1 && envb < p.E && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
             const size_t ab = (size_t)envb * NC + ia;
-            reinterpret_cast<float4*>(p.mem_out + ab * kMem * 4)[q] =
-                reinterpret_cast<const float4*>(p.mem_in + ab * kMem * 4)[q - 1];
+#pragma unroll
+            for (int f = q - 1; f < kMem - 1; f += SPL - 1)
+                reinterpret_cast<float4*>(p.mem_out + ab * kMem * 4)[f + 1] =
+                    reinterpret_cast<const float4*>(p.mem_in + ab * kMem * 4)[f];
         }
     }
     if (kMemEarly && SPL == 1 && active && (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_FLOCK)) {
@@ -1815,7 +1817,9 @@ void launch_step_L(const Cfg& c, const Params& p, hipStream_t s) {
         // only: 0.1929-0.1936 -> 0.1890-0.1907 and 0.7535-0.7570 -> 0.7393-0.7417 ms per step, config 3 0.0809-0.0815
         // -> 0.0820-0.0823 (profiles/r05/evenrows/)
         if (launch_spec<FLOCK_VARIANT_UW_DISCRETE, 512, false, true, 64, 8, 1, 0, true>(c, p, s)) return;  // config 4
-        if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;       // config 2
+        // config 2: the candidate scan split over 4 lanes per agent (2 lanes with the memory roll on one lane group:
+        // 0.0096 against 0.0094-0.0096 ms per step; 8 lanes 0.0100; profiles/r05/c2spl/)
+        if (launch_spec<FLOCK_VARIANT_UW, 64, false, false, 0, 0, 4>(c, p, s)) return;  // config 2
     }
     if (p.cells) {
         if (p.periodic)
