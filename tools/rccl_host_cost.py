@@ -31,12 +31,17 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1)
     pool = [torch.stack([torch.rand(E, N, device=dev, generator=g),
                          torch.rand(E, N, device=dev, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(8)]
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None  # a variant name prefix
+    if "--side-stream" in sys.argv:  # the env work on a non-blocking stream instead of the legacy default stream
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     for name, kw in (("single GPU", dict(dp=False)),
                      ("DP unsplit, c10d", dict(dp=True, dp_split=False, dp_rccl=False)),
                      ("DP unsplit, RCCL", dict(dp=True, dp_split=False, dp_rccl=True)),
                      ("DP split, c10d", dict(dp=True, dp_split=True, dp_rccl=False)),
                      ("DP split, RCCL", dict(dp=True, dp_split=True, dp_rccl=True)),
                      ("single GPU", dict(dp=False))):
+        if only and not name.startswith(only):
+            continue
         env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=N, k=4, collision_distance=2.5,
                                       range_start=(0, 253.0), sensor_range=14.0, step_launches=3), device=dev)
         env.positions.copy_(torch.rand(E, N, 2, device=dev, generator=g) * 253.0)
