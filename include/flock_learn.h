@@ -213,7 +213,7 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
  *                   learn t-1 had the same agent: its actor phase, then this critic phase)
  * The round's wait for the snapshot is, by default, the device-side gate: the snapshot (one workgroup) stores the
  * staging rows and the agent index write-through (`sc1`), waits for its stores and publishes a sequence number; the
- * critic phase's row blocks poll it (bounded: 0.2 s; a waiter that gives up sets an error word and computes nothing,
+ * critic phase's row blocks poll it (bounded: 2 s; a waiter that gives up sets an error word and computes nothing,
  * flock_sc_pipeline_check returns -6) and read the staging rows `sc1` (MI355X_MICROARCH.md hand-off table, row 1).
  * flock_sc_pipeline_set_gate(p, 0) (and always under rocprofv3 counter collection, which serialises dispatches)
  * makes it a cross-queue event wait instead; it returns the hand-off in use (1 gate, 0 events). Both are

@@ -671,7 +671,9 @@ __device__ unsigned long long g_scmark[4096][8];
 // reaches seq; the block's waves then read the snapshot rows with `sc1` loads after the barrier (the producer wrote
 // them `sc1`, waited for every store, and set the flag after a workgroup barrier: csrc/flock_mem.h). A wait longer
 // than kGateTimeoutTicks sets the error word and the block computes nothing (the host raises; no silent result).
-constexpr unsigned long long kGateTimeoutTicks = 20000000ull;  // 0.2 s of s_memrealtime (100 MHz)
+// 2 s of s_memrealtime (100 MHz): the env stream may be held up by work enqueued on it before the learn() (an
+// evaluation rollout, a long copy); 0.2 s failed a learn behind a 0.2-s kernel (tools/rccl_host_cost.py, round 5)
+constexpr unsigned long long kGateTimeoutTicks = 200000000ull;
 __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned long long seq) {
     __shared__ int ok;
     if (threadIdx.x == 0) {

@@ -157,6 +157,39 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
         assert torch.equal(x, y)
 
 
+def test_gate_waits_behind_a_busy_env_stream(cuda):
+    """The device-side gate when the env stream is held up: a 0.5-s kernel enqueued on the env stream before the
+    learns, so every round's critic blocks start polling long before their snapshot runs (their wait is bounded at
+    2 s). No wait gives up, and the results are bitwise the serial learn() sequence."""
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    ser = SharedCriticLearner(10, 4, device=cuda, seed=7, batch_size=64, buffer_size=500, snapshot=False)
+    pip = SharedCriticLearner(10, 4, device=cuda, seed=7, batch_size=64, buffer_size=500, snapshot=True, n_slots=3,
+                              handoff="gate")
+    g = torch.Generator(device=cuda).manual_seed(9)
+    n = 300
+    rows = (torch.rand(n, 4, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g),
+            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, 4, device=cuda, generator=g),
+            torch.rand(n, device=cuda, generator=g) > 0.5)
+    for L in (ser, pip):
+        L.store_transitions(*rows)
+    ls = torch.cuda.Stream(device=cuda)
+    main = torch.cuda.current_stream(cuda)
+    torch.cuda.synchronize()
+    torch.cuda._sleep(int(2.4e9 * 0.5))  # ~0.5 s on the env stream, ahead of every snapshot
+    for a in (1, 2, 3):
+        ser.learn(a)
+        assert pip.pipeline_learn(a, main.cuda_stream, ls.cuda_stream)
+    pip.pipeline_flush(ls.cuda_stream)
+    main.wait_stream(ls)
+    torch.cuda.synchronize()
+    assert pip.pipeline().gated() == 1
+    pip.pipeline_check()
+    for x, y in ((ser.critic.data, pip.critic.data), (ser.actors.data, pip.actors.data),
+                 (ser.actors.target, pip.actors.target), (ser.losses, pip.losses)):
+        assert torch.equal(x, y)
+
+
 def test_specialised_row_kernels_equal_generic(cuda):
     """At the reference widths (fc1 400, fc2 300, 2 actions) the rounds run row kernels with compile-time widths;
     flock_set_diag("sc_no_spec", 1) forces the generic ones. Merged rounds of both are bitwise equal."""
