@@ -750,7 +750,8 @@ __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, 
     float sink = 0.0f;
     // gated critic blocks: the fixed panels while the block waits for its snapshot, the agent-relative ones after it
     // (same-box A/B against the whole pull after the gate: 200 steps 0.0798-0.0804 vs 0.0803-0.0811 ms per step,
-    // profiles/r05/pullearly/)
+    // profiles/r05/pullearly/). The whole pull before the gate when the host passed the agent indices by value: 200 steps
+    // 0.0806-0.0823 vs 0.0811-0.0835, driver command 0.0895-0.0929 vs 0.0882-0.0904 (profiles/r05/pullknown/): not kept
     if (ac.gate && crit) {
         if ((gridDim.x & 7) == 0) sink = pull_l2(pc, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, true, 1);
         if (!gate_wait(ac.gate, ac.gate_seq)) return;
