@@ -1119,6 +1119,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
     PHASE(0);
     // ---- phase 2: per-env sums in a fixed tree order (same order as oracle tree_sum) -------------------------
+    // (the rounds s < 64 as wave shuffles, 5 block barriers instead of 10 at N = 512: bitwise the same, config 4
+    // 0.1899-0.1910 vs 0.1893-0.1906 ms per step, config 2 flat; profiles/r05/wavetail/: not kept)
     float s0 = 0.0f, s1 = 0.0f;
     if (variant == FLOCK_VARIANT_UW || variant == FLOCK_VARIANT_UW_DISCRETE) {
         float* r0 = red + (size_t)g * 2 * p.P;

@@ -58,7 +58,7 @@ def run(E, N, k, steps, variant="v2", seeds=False, windows=0):
         [ctypes.c_void_p] * 9
     stream = torch.cuda.current_stream(dev).cuda_stream
     ext = None
-    if seeds:  # the compact seed buffer (v2 only), as VecFlockEnv passes it
+    if seeds:  # the compact seed buffer, as VecFlockEnv passes it (v2, uwd)
         from marl_range_flocking_amd._native import FlockStepExt
 
         sb = torch.zeros(E, N, k, dtype=torch.int16, device=dev)
@@ -69,6 +69,8 @@ def run(E, N, k, steps, variant="v2", seeds=False, windows=0):
     gd.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 5 + [ctypes.c_int] + \
         [ctypes.c_void_p] * 5 + [ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int] + \
         [ctypes.c_void_p] * 7
+    gde = lib.flock_step_uw_discrete_ext
+    gde.argtypes = gd.argtypes + [ctypes.c_void_p]
     gu = lib.flock_step_uw
     gu.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_float] * 4 + [ctypes.c_int] + \
         [ctypes.c_void_p] * 12
@@ -90,6 +92,10 @@ def run(E, N, k, steps, variant="v2", seeds=False, windows=0):
             rc = gu(stream, E, N, k, box, 14.0, 2.5, 0.1, 0, pos.data_ptr(), head.data_ptr(), prev.data_ptr(),
                     act.data_ptr(), mem.data_ptr(), mem.data_ptr(), vel.data_ptr(), dnn.data_ptr(), idx.data_ptr(),
                     rew.data_ptr(), done.data_ptr(), anyd.data_ptr())
+        elif ext is not None:
+            rc = gde(stream, E, N, k, box, 14.0, 2.5, 0.1, 2.5, 0, pos.data_ptr(), head.data_ptr(), prev.data_ptr(),
+                     aid.data_ptr(), None, 0.1, 7, 0, table.data_ptr(), 10, vel.data_ptr(), dnn.data_ptr(),
+                     idx.data_ptr(), rew.data_ptr(), done.data_ptr(), anyd.data_ptr(), None, ctypes.addressof(ext))
         else:
             rc = gd(stream, E, N, k, box, 14.0, 2.5, 0.1, 2.5, 0, pos.data_ptr(), head.data_ptr(), prev.data_ptr(),
                     aid.data_ptr(), None, 0.1, 7, 0, table.data_ptr(), 10, vel.data_ptr(), dnn.data_ptr(),
@@ -173,7 +179,7 @@ if __name__ == "__main__":
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--variant", default="v2", choices=["v2", "uw", "uwd"])
-    ap.add_argument("--seeds", action="store_true", help="v2 through flock_step_v2_ext with a seed buffer")
+    ap.add_argument("--seeds", action="store_true", help="v2 / uwd through the _ext entry with a seed buffer")
     ap.add_argument("--windows", type=int, default=0, help="first time this many windows of --steps steps (drift)")
     a = ap.parse_args()
     if a.build:
