@@ -69,7 +69,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     if (t) *t = a.target_mode == 0 ? *t * a.one_minus_tau + p * a.tau : a.tau * p + a.one_minus_tau * *t;
 }
 
-// VEC: every pointer 16-B aligned -> one float4 of each stream per thread and iteration (the update is HBM-bound:
+// VEC: every pointer 16-B aligned -> float4 loads and stores of each stream (the update is HBM-bound:
 // 16 or 20 B read + 12 or 16 B written per parameter), the n % 4 tail by block 0. Same per-element arithmetic as
 // the scalar path, so both give identical bits.
 template <bool VEC>
@@ -93,21 +93,40 @@ __global__ __launch_bounds__(kBlock) void adam_kernel(AdamArgs a) {
     int64_t i0 = blockIdx.x * (int64_t)kBlock + threadIdx.x;
     if (VEC) {
         const int64_t nq = a.n >> 2;
-        for (int64_t q = i0; q < nq; q += stride) {
-            float4 p = reinterpret_cast<const float4*>(a.p)[q];
-            const float4 g = reinterpret_cast<const float4*>(a.g)[q];
-            float4 m = reinterpret_cast<const float4*>(a.m)[q];
-            float4 v = reinterpret_cast<const float4*>(a.v)[q];
-            float4 t = a.target ? reinterpret_cast<const float4*>(a.target)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            float* tp = a.target ? &t.x : nullptr;
-            adam_elem(p.x, g.x, m.x, v.x, tp, a, gs, neg_step, bc2s);
-            adam_elem(p.y, g.y, m.y, v.y, tp ? tp + 1 : nullptr, a, gs, neg_step, bc2s);
-            adam_elem(p.z, g.z, m.z, v.z, tp ? tp + 2 : nullptr, a, gs, neg_step, bc2s);
-            adam_elem(p.w, g.w, m.w, v.w, tp ? tp + 3 : nullptr, a, gs, neg_step, bc2s);
-            reinterpret_cast<float4*>(a.p)[q] = p;
-            reinterpret_cast<float4*>(a.m)[q] = m;
-            reinterpret_cast<float4*>(a.v)[q] = v;
-            if (a.target) reinterpret_cast<float4*>(a.target)[q] = t;
+        // two float4 of every stream per thread and iteration, all loads issued before the arithmetic: 906M
+        // parameters with the target (config 5's critics), 6.68 -> 5.80-5.86 ms per call (4.9 -> 5.6 TB/s; another box
+        // 7.21 -> 6.81-6.83); four: as two; non-temporal loads and stores: flat (tools/adam_bw.py, profiles/r05/adam/)
+        constexpr int U = 2;
+        auto ld4 = [](const float* b, int64_t q) { return reinterpret_cast<const float4*>(b)[q]; };
+        auto st4 = [](float* b, int64_t q, float4 x) { reinterpret_cast<float4*>(b)[q] = x; };
+        for (int64_t q0 = i0; q0 < nq; q0 += U * stride) {
+            float4 p[U], g[U], m[U], v[U], t[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t q = q0 + u * stride;
+                if (q < nq) {
+                    p[u] = ld4(a.p, q);
+                    g[u] = ld4(a.g, q);
+                    m[u] = ld4(a.m, q);
+                    v[u] = ld4(a.v, q);
+                    t[u] = a.target ? ld4(a.target, q) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t q = q0 + u * stride;
+                if (q < nq) {
+                    float* tp = a.target ? &t[u].x : nullptr;
+                    adam_elem(p[u].x, g[u].x, m[u].x, v[u].x, tp, a, gs, neg_step, bc2s);
+                    adam_elem(p[u].y, g[u].y, m[u].y, v[u].y, tp ? tp + 1 : nullptr, a, gs, neg_step, bc2s);
+                    adam_elem(p[u].z, g[u].z, m[u].z, v[u].z, tp ? tp + 2 : nullptr, a, gs, neg_step, bc2s);
+                    adam_elem(p[u].w, g[u].w, m[u].w, v[u].w, tp ? tp + 3 : nullptr, a, gs, neg_step, bc2s);
+                    st4(a.p, q, p[u]);
+                    st4(a.m, q, m[u]);
+                    st4(a.v, q, v[u]);
+                    if (a.target) st4(a.target, q, t[u]);
+                }
+            }
         }
         if (blockIdx.x != 0) return;
         i0 = (nq << 2) + threadIdx.x;  // tail

@@ -50,6 +50,31 @@ def test_fused_adam_soft_update_and_per_agent(cuda):
     torch.testing.assert_close(fp.data, 0.001 * c + 0.999 * c, rtol=0, atol=0)
 
 
+def test_fused_adam_vector_path_is_bitwise_the_scalar_path_at_grid_stride_sizes(cuda):
+    """The float4 path (two per thread and iteration over the grid stride, csrc/flock_learn.hip adam_kernel) against
+    the scalar one (unaligned views) at sizes past one and two grid strides of 2048 x 256 float4, with a tail; the
+    target soft update on."""
+    from marl_range_flocking_amd.learners.core import _ops
+
+    for n in (4 * 2048 * 256 * 2 + 4 * 77 + 3, 4 * 2048 * 256 * 3 - 4 * 5 + 1):
+        g0 = torch.Generator(device=cuda).manual_seed(n)
+        base = [torch.rand(n + 1, device=cuda, generator=g0) for _ in range(5)]
+        base[3] *= 1e-3  # v >= 0
+        vec = [b[:n].clone() for b in base]      # 16-B aligned: adam_kernel<true>
+        sca = [torch.empty(n + 1, device=cuda) for _ in range(5)]
+        for s_, b in zip(sca, base):
+            s_[1:].copy_(b[:n])
+        sca = [s_[1:] for s_ in sca]            # 4-B aligned only: adam_kernel<false>
+        for bufs in (vec, sca):
+            step = torch.zeros(1, dtype=torch.int64, device=cuda)
+            p, g, m, v, t = bufs
+            for _ in range(2):
+                step.add_(1)
+                _ops().adam_step(p, g, m, v, step, None, t, 3e-3, 0.9, 0.999, 1e-8, 0.01, 0)
+        for a, b in zip(vec, sca):
+            assert torch.equal(a, b)
+
+
 def test_grad_norm_and_clip_scale(cuda):
     g = torch.randn(1_000_003, device=cuda) * 0.01
     out = GradNorm(cuda)(g, 5.0)
