@@ -57,8 +57,9 @@ const char* flock_last_error(void);
  * ranges per step), "no_spec" (generic step instantiations), "no_split" (one lane per agent in the split-scan
  * instantiations), "no_cells" (full scans instead of the cell list), "pf" (-1 default / 0 off: the env blocks' L2
  * pull-ahead of a later block's inputs in the shapes compiled with it), "sc_no_spec" (generic shared-critic row
- * kernels at fc 400/300). The env knobs are initialised once from FLOCK_ENV_LAUNCHES, FLOCK_NO_SPEC, FLOCK_NO_SPLIT,
- * FLOCK_NO_CELLS, FLOCK_ENV_PF; not thread-safe against concurrent launches. */
+ * kernels at fc 400/300). The library reads no environment variable for them: flock_set_diag is the only way to
+ * set them (process-wide; not thread-safe against concurrent launches). Returns FLOCK_OK, or FLOCK_E_ARG for an
+ * unknown name. */
 int flock_set_diag(const char* name, int value);
 
 /* gym_flock_v2 step: pos (rw), heading (rw), action [lin, ang] → vel, dnn, nn_idx, reward, done, any_done. */

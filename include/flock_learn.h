@@ -213,10 +213,18 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
  *                   learn t-1 had the same agent: its actor phase, then this critic phase)
  * The round's wait for the snapshot is, by default, the device-side gate: the snapshot (one workgroup) stores the
  * staging rows and the agent index write-through (`sc1`), waits for its stores and publishes a sequence number; the
- * critic phase's row blocks poll it (bounded: 2 s; a waiter that gives up sets an error word and computes nothing,
- * flock_sc_pipeline_check returns -6) and read the staging rows `sc1` (MI355X_MICROARCH.md hand-off table, row 1).
- * flock_sc_pipeline_set_gate(p, 0) (and always under rocprofv3 counter collection, which serialises dispatches)
- * makes it a cross-queue event wait instead; it returns the hand-off in use (1 gate, 0 events). Both are
+ * critic phase's row blocks poll it and read the staging rows `sc1` (MI355X_MICROARCH.md hand-off table, row 1). A
+ * learn() is gated only when the caller called flock_sc_pipeline_mark since the previous learn():
+ * mark(p, env_stream, 1) records an event behind everything env_stream holds at that point, and the round first waits
+ * for it on the learner stream (a cross-queue wait that occupies no CU and is usually complete already), so the row
+ * blocks spin only over the env work enqueued after the mark (the caller's own env step); mark(p, env_stream, 0)
+ * declares that nothing but the caller's own env step was enqueued on env_stream since the previous learn's
+ * snapshot (the C++ training loop, after its first step). Without a mark the learn() takes the cross-queue event
+ * hand-off, so a learn never fails because env_stream is busy with other work. The spin stays bounded (2 s, far
+ * above any env step; a waiter that gives up sets an error word and computes nothing, flock_sc_pipeline_check
+ * returns -6). flock_sc_pipeline_set_gate(p, 0) (and always under rocprofv3 counter collection, which serialises
+ * dispatches) makes every learn() take the event wait; it returns the hand-off in use (1 gate, 0 events). The gate
+ * serves single-GPU and data-parallel pipelines alike. Both are
  * deadlock-free whatever hardware queues the streams map to: every snapshot is enqueued before the round that waits
  * for it, and nothing on env_stream waits for that round. The actor phase of the last learn() stays pending until the
  * next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise those of the serial
@@ -227,6 +235,7 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
 int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_stream, int64_t rows, uint64_t seed,
                             uint64_t counter, int64_t agent);
 int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on);
+int flock_sc_pipeline_mark(FlockScPipeline* p, void* env_stream, int wait);
 int flock_sc_pipeline_gated(const FlockScPipeline* p);
 int flock_sc_pipeline_check(FlockScPipeline* p);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
@@ -255,6 +264,9 @@ int flock_sc_pipeline_set_dp(FlockScPipeline* p, float* bucket, int64_t critic_f
  * unsplit rounds (agent_simple_shared_critic.py:137-150; the reference steps the actor right after the critic). */
 int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads, int n_agents,
                                    FlockAllreduceFn allreduce, void* ctx);
+/* The pipeline's own comm stream (split data-parallel rounds: the early critic all-reduce), NULL before
+ * flock_sc_pipeline_set_dp_actor: lets a caller bind one collective communicator to each stream that calls it. */
+void* flock_sc_pipeline_comm_stream(const FlockScPipeline* p);
 
 #ifdef __cplusplus
 }

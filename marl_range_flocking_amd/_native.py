@@ -156,6 +156,8 @@ SIGNATURES.update({
     "flock_sc_pipeline_learn": [_c_void_p] * 3 + [ctypes.c_int64, _c_u64, _c_u64, ctypes.c_int64],
     "flock_sc_pipeline_flush": [_c_void_p, _c_void_p],
     "flock_sc_pipeline_set_gate": [_c_void_p, _c_int],
+    "flock_sc_pipeline_mark": [_c_void_p, _c_void_p, _c_int],
+    "flock_sc_pipeline_comm_stream": [_c_void_p],
     "flock_sc_pipeline_check": [_c_void_p],
     "flock_sc_pipeline_gated": [_c_void_p],
     "flock_sc_pipeline_set_dp": [_c_void_p, _c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_void_p,
@@ -165,7 +167,8 @@ SIGNATURES.update({
 })
 RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,
             "flock_sc_workspace_floats": ctypes.c_int64, "flock_sc_update_size": ctypes.c_int64,
-            "flock_sc_pipeline_create": _c_void_p, "flock_sc_pipeline_destroy": None}
+            "flock_sc_pipeline_create": _c_void_p, "flock_sc_pipeline_destroy": None,
+            "flock_sc_pipeline_comm_stream": _c_void_p}
 
 _lib = None
 

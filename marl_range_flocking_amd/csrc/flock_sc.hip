@@ -2108,11 +2108,18 @@ struct FlockScPipeline {
     Job jc[kMaxSlots], ja[kMaxSlots];  // the rounds' launch arguments, built once
     hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
     // device-side snapshot gate: gate[0] the published sequence number, gate[1] the error word of a waiter that gave
-    // up; seq counts this pipeline's snapshots. gate_on: the critic phase's row blocks poll gate[0] (single GPU, not
-    // under counter collection); otherwise the learner stream waits for each snapshot on a cross-queue event.
+    // up; seq counts this pipeline's snapshots. gate_on: the critic phase's row blocks poll gate[0] (single GPU and
+    // data-parallel rounds alike; never under counter collection); otherwise the learner stream waits for each snapshot
+    // on a cross-queue event.
     unsigned long long* gate;
     unsigned long long seq;
     bool gate_on;
+    // the gate's guard (flock_sc_pipeline_mark): a learn() is gated only when the caller marked the env stream since
+    // the previous learn(): mark 2 = the round first waits (cross-queue, usually already complete) for mark_ev, recorded
+    // behind everything the env stream held then; 1 = the caller declared that only its own env step was enqueued since
+    // the previous snapshot; 0 = no mark: the event hand-off, so that no round ever spins on work of unknown length
+    hipEvent_t mark_ev;
+    int mark;
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
@@ -2310,6 +2317,10 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->gate = nullptr;
     p->seq = 0;
     p->gate_on = false;
+    p->mark = 0;
+    p->mark_ev = nullptr;
+    if (!rc && hipEventCreateWithFlags(&p->mark_ev, hipEventDisableTiming) != hipSuccess)
+        rc = fail(-4, "flock_sc_pipeline_create: event");
     if (!rc && (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
                 hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
                 hipDeviceSynchronize() != hipSuccess))
@@ -2326,6 +2337,18 @@ int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on) {
     if (!p) return fail(-3, "flock_sc_pipeline_set_gate: NULL pipeline");
     p->gate_on = on != 0 && p->gate && !counter_collection();
     return p->gate_on ? 1 : 0;
+}
+
+int flock_sc_pipeline_mark(FlockScPipeline* p, void* env_stream, int wait) {
+    if (!p) return fail(-3, "flock_sc_pipeline_mark: NULL pipeline");
+    if (wait) {
+        if (hipEventRecord(p->mark_ev, (hipStream_t)env_stream) != hipSuccess)
+            return fail(-4, "flock_sc_pipeline_mark: event record");
+        p->mark = 2;
+    } else if (p->mark == 0) {
+        p->mark = 1;
+    }
+    return 0;
 }
 
 namespace {
@@ -2369,10 +2392,16 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     if (p->used[s] && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
         return fail(-4, "flock_sc_pipeline_learn: wait");
     int rc = 0;
-    if (p->gate_on) {
+    const int mark = p->mark;
+    p->mark = 0;
+    if (p->gate_on && mark) {
         // the snapshot publishes gate[0] = seq after its write-through stores; this learn's critic row blocks wait
         // for it on the device. No deadlock whatever the streams' hardware queues: the snapshot is enqueued before
-        // the round that waits for it, and nothing on the env stream waits for that round
+        // the round that waits for it, and nothing on the env stream waits for that round. The guard: the learner
+        // stream first waits (cross-queue, without occupying a CU) for the caller's mark, so the row blocks spin only
+        // over the env work enqueued since the mark (the caller's own env step), never behind a backlog of unknown
+        // length; with mark 1 the caller declared that nothing else was enqueued since the previous snapshot
+        if (mark == 2 && (rc = wait_unless_done(ls, p->mark_ev))) return rc;
         const FlockScRows& src = p->ring;
         const FlockScRows& dst = p->staging[s];
         int vec = u.in_dim == 4 && u.n_actions == 2;
@@ -2506,6 +2535,8 @@ int flock_sc_pipeline_check(FlockScPipeline* p) {
 
 int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate_on ? 1 : 0; }
 
+void* flock_sc_pipeline_comm_stream(const FlockScPipeline* p) { return p ? (void*)p->comm_stream : nullptr; }
+
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;
     if (p->gate) (void)hipFree(p->gate);
@@ -2514,6 +2545,7 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (p->comm_stream) (void)hipStreamDestroy(p->comm_stream);
     if (p->bwd_done) (void)hipEventDestroy(p->bwd_done);
     if (p->ar_done) (void)hipEventDestroy(p->ar_done);
+    if (p->mark_ev) (void)hipEventDestroy(p->mark_ev);
     delete[] p->last_actor_slot;
     for (int i = 0; i < p->n; ++i) {
         hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};

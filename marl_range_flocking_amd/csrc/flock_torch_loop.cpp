@@ -36,7 +36,10 @@
 #include <dlfcn.h>
 
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "flock_amd.h"
@@ -101,12 +104,13 @@ struct ScPipeline : torch::CustomClassHolder {
     // data-parallel rounds
     c10::intrusive_ptr<c10d::ProcessGroup> pg, pg_actor;
     // set_rccl: direct RCCL collectives instead of pg / pg_actor. A communicator is used from ONE stream only (two
-    // collectives of one communicator on different streams could run concurrently): the critic part's two streams
-    // (the learner stream; the comm stream of the split rounds' early part) each get their own, bound to a stream at
-    // its first use (the same order on every rank), the actor part one for the actor stream
+    // collectives of one communicator on different streams could run concurrently), bound when it is made: the
+    // critic part's first communicator to the learner stream set_rccl names, the second to the pipeline's comm stream
+    // (split rounds' early part), the actor part's to the pipeline's actor stream. Any other stream is an error.
     RcclCommT comm_c[2] = {nullptr, nullptr};
     void* comm_c_stream[2] = {nullptr, nullptr};
     RcclCommT comm_actor = nullptr;
+    void* rccl_learner_stream = nullptr;
     Tensor bucket, grad_scale;
     std::vector<Tensor> actor_grads;
     std::string cb_error;
@@ -180,27 +184,31 @@ struct ScPipeline : torch::CustomClassHolder {
         return c;
     }
     // the data-parallel collectives as direct RCCL calls (after set_dp / set_dp_actor): a communicator for the critic
-    // part (learner and comm streams) and one for the actor part (actor stream), every rank calling with the same ids
-    // uids: [critic (first stream), critic (second stream), actor], each [128] uint8 on the CPU
-    void set_rccl(std::vector<Tensor> uids, int64_t rank, int64_t world) {
+    // part on learner_stream (every learn / flush / loop call of this pipeline must then use that stream), one for the
+    // critic part on the pipeline's comm stream (split rounds) and one for the actor part (actor stream), every rank
+    // calling with the same ids. uids: [critic (learner stream), critic (comm stream), actor], each [128] uint8 (CPU)
+    void set_rccl(std::vector<Tensor> uids, int64_t rank, int64_t world, int64_t learner_stream) {
         TORCH_CHECK(rccl().ok, "ScPipeline.set_rccl: RCCL (librccl.so.1) is not loaded");
         TORCH_CHECK(pg, "ScPipeline.set_rccl: call set_dp first");
         TORCH_CHECK(uids.size() == 3, "ScPipeline.set_rccl: three unique ids");
         TORCH_CHECK(!comm_c[0], "ScPipeline.set_rccl: already set");
+        TORCH_CHECK(learner_stream != 0, "ScPipeline.set_rccl: name the learner stream the rounds run on");
         const at::OptionalDeviceGuard g(device);
+        rccl_learner_stream = reinterpret_cast<void*>(learner_stream);
         comm_c[0] = rccl_comm(uids[0], rank, world);
+        comm_c_stream[0] = rccl_learner_stream;
         comm_c[1] = rccl_comm(uids[1], rank, world);
+        comm_c_stream[1] = flock_sc_pipeline_comm_stream(pipe);  // NULL unless split: then never called
         if (pg_actor) comm_actor = rccl_comm(uids[2], rank, world);
     }
-    RcclCommT critic_comm(void* stream) {
-        for (int i = 0; i < 2; ++i) {
-            if (comm_c_stream[i] == stream) return comm_c[i];
-            if (!comm_c_stream[i]) {
-                comm_c_stream[i] = stream;
-                return comm_c[i];
-            }
-        }
-        return nullptr;  // a third stream: no communicator for it
+    RcclCommT critic_comm(void* stream) const {
+        for (int i = 0; i < 2; ++i)
+            if (comm_c_stream[i] && comm_c_stream[i] == stream) return comm_c[i];
+        return nullptr;  // not a stream a communicator was bound to
+    }
+    void check_learner_stream(int64_t learner_stream, const char* fn) const {
+        TORCH_CHECK(!rccl_learner_stream || reinterpret_cast<void*>(learner_stream) == rccl_learner_stream, fn,
+                    ": the RCCL communicators are bound to the learner stream set_rccl named; enqueue the rounds there");
     }
     static int rccl_sum(RcclCommT c, float* data, int64_t n, void* stream, std::string& err) {
         const int rc = rccl().all_reduce(data, data, (size_t)n, kRcclFloat32, kRcclSum, c,
@@ -220,7 +228,7 @@ struct ScPipeline : torch::CustomClassHolder {
         if (self->comm_c[0]) {
             RcclCommT c = self->critic_comm(stream);
             if (!c) {
-                self->cb_error = "ScPipeline: the critic all-reduce was called from a third stream";
+                self->cb_error = "ScPipeline: the critic all-reduce was called from a stream no communicator is bound to";
                 return -4;
             }
             return rccl_sum(c, data, n, stream, self->cb_error);
@@ -269,6 +277,7 @@ struct ScPipeline : torch::CustomClassHolder {
     // learn() of `agent` on `rows` ring rows (min(counter, capacity)), the learn counter `counter` (Philox)
     void learn(int64_t rows, int64_t seed, int64_t counter, int64_t agent, int64_t env_stream, int64_t learner_stream) {
         TORCH_CHECK(agent >= 0 && agent < n_agents, "ScPipeline.learn: agent out of range");
+        check_learner_stream(learner_stream, "ScPipeline.learn");
         const at::OptionalDeviceGuard g(device);
         check(flock_sc_pipeline_learn(pipe, reinterpret_cast<void*>(env_stream), reinterpret_cast<void*>(learner_stream),
                                       rows, (uint64_t)seed, (uint64_t)counter, agent),
@@ -276,6 +285,7 @@ struct ScPipeline : torch::CustomClassHolder {
     }
 
     void flush(int64_t learner_stream) {
+        check_learner_stream(learner_stream, "ScPipeline.flush");
         const at::OptionalDeviceGuard g(device);
         check(flock_sc_pipeline_flush(pipe, reinterpret_cast<void*>(learner_stream)), "flock_sc_pipeline_flush");
     }
@@ -288,6 +298,38 @@ struct ScPipeline : torch::CustomClassHolder {
     }
 
     int64_t gated() const { return flock_sc_pipeline_gated(pipe); }
+
+    // the device gate's guard (flock_sc_pipeline_mark): wait = true records an event behind everything env_stream holds
+    // now, which the next learn's round waits for on the learner stream; wait = false declares that only the caller's
+    // own env step will be enqueued on env_stream before the next learn (the C++ loop after its first step). A learn
+    // with no mark since the previous one takes the event hand-off (never spins behind work of unknown length)
+    void mark(int64_t env_stream, bool wait) {
+        const at::OptionalDeviceGuard g(device);
+        check(flock_sc_pipeline_mark(pipe, reinterpret_cast<void*>(env_stream), wait ? 1 : 0), "flock_sc_pipeline_mark");
+    }
+
+    // The learner stream of a device's pipelines, created once per (device, priority) and never destroyed, so that
+    // every learner of a process runs on the same stream whatever torch's stream pool holds (a pool stream can share
+    // its hardware queue with the env stream once a process has more streams than GPU_MAX_HW_QUEUES: the same loop
+    // then serialises, profiles/r05/rccl_host/host_cost_q4.txt). Non-blocking; high = the device's greatest priority,
+    // whose streams HIP places on hardware queues apart from the normal-priority ones (the env stream's)
+    static int64_t stream(int64_t device_index, bool high) {
+        static std::mutex m;
+        static std::map<std::pair<int64_t, bool>, hipStream_t> streams;
+        const std::lock_guard<std::mutex> lock(m);
+        const auto key = std::make_pair(device_index, high);
+        auto it = streams.find(key);
+        if (it != streams.end()) return reinterpret_cast<int64_t>(it->second);
+        const c10::hip::HIPGuard g((c10::DeviceIndex)device_index);
+        int least = 0, greatest = 0;
+        TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess,
+                    "ScPipeline.stream: hipDeviceGetStreamPriorityRange");
+        hipStream_t s = nullptr;
+        TORCH_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least) == hipSuccess && s,
+                    "ScPipeline.stream: hipStreamCreateWithPriority");
+        streams[key] = s;
+        return reinterpret_cast<int64_t>(s);
+    }
 
     // the snapshot hand-off: 1 the device-side gate (the default on one GPU), 0 cross-queue event waits; returns the
     // hand-off in use (data-parallel rounds and rocprofv3 counter collection always take the events)
@@ -414,6 +456,7 @@ struct ScTrainLoop : torch::CustomClassHolder {
         void* es = reinterpret_cast<void*>(env_stream);
         const int64_t n = E * N;
         size_t ev = 0;
+        bool marked = false;
         for (int64_t s = 0; s < K; ++s) {
             const int64_t step = first + s;
             const int64_t skip = n > capacity ? n - capacity : 0;
@@ -431,6 +474,12 @@ struct ScTrainLoop : torch::CustomClassHolder {
             r.group = 1;
             const int nxt = (int)(parity ^ 1);
             FlockStepExt ext{&r, ptr_or_null<uint16_t>(env[10]), (int)launches, 0};
+            // the device gate's guard, for the steps that learn: the first such step's mark waits for whatever the env
+            // stream held before it; later steps declare that only this loop's own env step precedes their snapshot
+            if (counter + n >= pipe->batch) {
+                pipe->mark(env_stream, !marked);
+                marked = true;
+            }
             const bool timed = s % ev_every == 0 && ev + 1 < events.size();
             if (timed) TORCH_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[ev]),
                                                   static_cast<hipStream_t>(es)) == hipSuccess, "hipEventRecord");
@@ -475,6 +524,8 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         .def("verify", &ScPipeline::verify)
         .def("gated", &ScPipeline::gated)
         .def("set_gate", &ScPipeline::set_gate)
+        .def("mark", &ScPipeline::mark)
+        .def_static("stream", &ScPipeline::stream)
         .def("set_dp_actor", &ScPipeline::set_dp_actor)
         .def("set_rccl", &ScPipeline::set_rccl)
         .def_static("rccl_unique_id", &ScPipeline::rccl_unique_id);

@@ -71,6 +71,14 @@ class FlatParams:
             p.grad = self.view(self.grad, name)
             self.params[name] = p
         self._agent_params = {}
+        self.writers = []  # OverlappedTrain updates that write this buffer on a stream of their own
+
+    def sync_writers(self):
+        """The current stream waits for every pending overlapped update of these parameters (OverlappedTrain): called
+        by the host-side readers and writers (export / load / hard_update_target, the learners' acting and
+        state-dict methods), so mixing train_overlapped() with them never races."""
+        for w in self.writers:
+            w.sync()
 
     def view(self, buf, name, agent=None):
         """Stacked [agents, *shape] view of ``buf`` (data / grad / target / moments) for ``name``."""
@@ -189,10 +197,12 @@ class FlatParams:
         _ops().soft_update(dst[lo:hi], self.data[lo:hi], float(tau), int(mode))
 
     def hard_update_target(self):
+        self.sync_writers()
         self.target.copy_(self.data)
 
     def load(self, name, value, agent=None, target=False):
         """Copy a per-agent (agent=i) or stacked value into params (or the target copy)."""
+        self.sync_writers()
         dst = self.view(self.target if target else self.data, name)
         v = torch.as_tensor(value, dtype=torch.float32).to(self.device)
         with torch.no_grad():
@@ -202,6 +212,7 @@ class FlatParams:
                 dst[agent].copy_(v.reshape(dst[agent].shape))
 
     def export(self, name, agent=None, target=False):
+        self.sync_writers()
         v = self.view(self.target if target else self.data, name)
         return v.detach().clone() if agent is None else v[agent].detach().clone()
 
@@ -656,9 +667,10 @@ class OverlappedTrain:
     (env) stream — one row gather per field, ordered before the env kernels that overwrite ring rows — and the update
     itself, the learner's own graph-captured code re-captured over this snapshot, runs on a stream of its own. Results
     are bitwise those of train() on the same draws (the same kernels on the same rows). ``sync()`` makes the caller's
-    stream wait for the update (before anything reads the networks; bench.py's finish())."""
+    stream wait for the update (before anything reads the networks; bench.py's finish()); ``writes``: the FlatParams
+    the update writes, which then sync on it before their host-side reads and writes (FlatParams.sync_writers)."""
 
-    def __init__(self, ring, n_rows):
+    def __init__(self, ring, n_rows, writes=()):
         self.ring = ring
         self.snap = ReplayRing(n_rows, ring.fields, ring.device, aliases=ring.aliases)
         self.snap.counter = n_rows
@@ -666,6 +678,8 @@ class OverlappedTrain:
         self.done = torch.cuda.Event()
         self.pending = False
         self.graph = None
+        for fp in writes:
+            fp.writers.append(self)
 
     def snapshot(self, idx):
         """Rows idx (int64, n_rows in all, any shape) of every field into snapshot rows 0..n_rows-1 in idx's order, on

@@ -240,6 +240,7 @@ class MADDPGLearner:
         # one buffer for each pair (ReplayRing aliases), which the env kernel's fused insert writes once (bitwise the
         # same records and minibatches; 32 B per agent-step less to write at config 5)
         self.shared_obs = bool(shared_obs)
+        self._shared_obs_bad = None  # device flag: a shared_obs record whose actor / critic observations differed
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.N, self.k, self.recurrent, self.h1 = n_agents, k, recurrent, hidden1
         self.actor_lr, self.critic_lr, self.gamma, self.tau = actor_lr, critic_lr, gamma, tau
@@ -301,6 +302,7 @@ class MADDPGLearner:
         """actor_states [N, k] (one env) or [E, N, k]; hidden [N, E, 32] -> (actions like actor_states[..., :2],
         hidden'). Noise: the shared OU process, sampled agent after agent (agent.py:53-64)."""
         single = actor_states.dim() == 2
+        self.sync()  # an overlapped train() still writing the networks
         x = actor_states.reshape(-1, self.N, self.k).transpose(0, 1)  # [N, E, k]
         E = x.shape[1]
         if hidden is None:
@@ -332,12 +334,22 @@ class MADDPGLearner:
         n = 1 if st.dim() == 2 else st.shape[0]
         f = lambda t, *shape: torch.as_tensor(t, device=self.device, dtype=torch.float32).reshape(n, *shape)  # noqa
         N, k = self.N, self.k
-        if self.shared_obs and not (torch.equal(f(actor_states, N, k), f(state, N, k)) and
-                                    torch.equal(f(actor_next_states, N, k), f(next_state, N, k))):
-            raise ValueError("shared_obs: a record's actor observations must equal its critic observations")
+        if self.shared_obs:
+            # one device-side check per record, OR-ed into a flag read at the next train() (check_shared_obs): no host
+            # sync on the per-step store path
+            bad = ((f(actor_states, N, k) != f(state, N, k)).any()
+                   | (f(actor_next_states, N, k) != f(next_state, N, k)).any())
+            self._shared_obs_bad = bad if self._shared_obs_bad is None else self._shared_obs_bad | bad
         self.replay.store({"state": f(state, N, k), "next_state": f(next_state, N, k),
                            "actor_state": f(actor_states, N, k), "actor_next_state": f(actor_next_states, N, k),
                            "action": f(actions, N, 2), "reward": f(reward, N), "done": f(done, N)})
+
+    def check_shared_obs(self):
+        """Raise if a record stored since the last check had actor observations that differ from its critic
+        observations (shared_obs=True keeps one copy of them). One host read; train() calls it."""
+        bad, self._shared_obs_bad = self._shared_obs_bad, None
+        if bad is not None and bool(bad):
+            raise ValueError("shared_obs: a record's actor observations must equal its critic observations")
 
     def replay_slots(self, n_envs):
         """Reserve the next n_envs records for an env step that writes them itself (VecFlockEnv.step(ring=...)):
@@ -505,6 +517,8 @@ class MADDPGLearner:
 
     def train(self, starts=None):
         """SuperAgent.train(): one update of every agent. starts: optional [B] physical chunk starts (parity)."""
+        self.sync()  # after a train_overlapped(): its update must land first (same stream order as serial trains)
+        self.check_shared_obs()
         if not self.check_buffer_size():
             return None
         rng = min(self.replay.counter, self.replay.capacity)
@@ -535,11 +549,12 @@ class MADDPGLearner:
         Single-process graph path only (the data-parallel and agent-sharded updates call collectives: train())."""
         if self.distributed or self.shard or not self.use_graph:
             return self.train(starts)
+        self.check_shared_obs()
         if not self.check_buffer_size():
             return None
         ov = self.__dict__.get("_ov")
         if ov is None:
-            ov = self._ov = OverlappedTrain(self.replay, self.B * self.C)
+            ov = self._ov = OverlappedTrain(self.replay, self.B * self.C, writes=(self.critics, self.actors))
             ov.idx = torch.arange(self.B * self.C, device=self.device).view(self.B, self.C)
         rng = min(self.replay.counter, self.replay.capacity)
         hi = rng - self.C if self.recurrent else rng

@@ -21,7 +21,6 @@ learn() has two implementations with the same semantics:
   * autograd (fused=False): the same update written with torch ops and the batched helpers of core.py.
 """
 import math
-import os
 
 import torch
 import torch.nn.functional as F
@@ -85,7 +84,8 @@ class SharedCriticLearner:
     def __init__(self, n_agents, input_dim, n_actions=2, fc1=400, fc2=300, alpha=3e-4, beta=3e-4, gamma=0.99,
                  tau=0.001, batch_size=256, update_rate=3, buffer_size=1_000_000, device="cuda", seed=0,
                  ou_sigma=0.15, ou_theta=0.2, ou_dt=1e-2, use_graph=True, dist_group=None, fused=True,
-                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=False, dp=None, dp_rccl=True):
+                 snapshot=False, replay=None, n_slots=2, handoff="gate", dp_split=False, dp=None, dp_rccl=True,
+                 learner_priority="high"):
         self.device = torch.device(device)
         self.n_agents, self.input_dim, self.n_actions = n_agents, input_dim, n_actions
         self.alpha, self.beta, self.gamma, self.tau = alpha, beta, gamma, tau
@@ -141,6 +141,15 @@ class SharedCriticLearner:
         if handoff not in ("gate", "event"):
             raise ValueError("handoff is 'gate' or 'event'")
         self.handoff = handoff
+        # the native pipeline's learner stream: one per (device, priority) for the whole process, created in C++
+        # (ScPipeline.stream), not taken from torch's stream pool, whose streams share hardware queues with the env
+        # stream once a process holds more streams than GPU_MAX_HW_QUEUES (the same loop then serialises: 0.084 vs
+        # 0.125 ms per step, profiles/r05/rccl_host/host_cost_q4.txt). "high": the device's greatest priority, whose
+        # streams HIP keeps on hardware queues of their own, apart from every normal-priority stream
+        if learner_priority not in ("high", "normal"):
+            raise ValueError("learner_priority is 'high' or 'normal'")
+        self.learner_priority = learner_priority
+        self._learner_stream = None
         # data-parallel pipelines: the actor half of each round all-reduced and stepped off the learner chain, over a
         # second process group of the same ranks (flock_sc_pipeline_set_dp_actor); created here, collectively
         self.dp_split = bool(dp_split and self.distributed and self.snapshot)
@@ -510,6 +519,17 @@ class SharedCriticLearner:
                 after_actor.record(actor_stream)
         return self._finish_learn(agent, soft_in_kernel=True)
 
+    @property
+    def learner_stream(self):
+        """The stream the native pipeline's rounds run on (torch.cuda.ExternalStream over ScPipeline.stream)."""
+        if self._learner_stream is None:
+            from .. import torch_ops
+
+            torch_ops.load()
+            h = torch.classes.flock.ScPipeline.stream(self.device.index or 0, self.learner_priority == "high")
+            self._learner_stream = torch.cuda.ExternalStream(h, device=self.device)
+        return self._learner_stream
+
     def pipeline(self):
         """The native learn() pipeline (torch.classes.flock.ScPipeline over flock_sc_pipeline_*, include/flock_learn.h)
         over the n_slots staging slots: per learn() the minibatch snapshot on the env stream and ONE round (this
@@ -549,15 +569,26 @@ class SharedCriticLearner:
                     torch.distributed.broadcast(ids, src=ranks[0], group=group)
                     ids = ids.cpu()
                     p.set_rccl([ids[i].contiguous() for i in range(3)], ranks.index(torch.distributed.get_rank()),
-                               len(ranks))
+                               len(ranks), self.learner_stream.cuda_stream)
             p.set_gate(self.handoff == "gate")
             self._pipe = p
         return self._pipe
 
+    def pipeline_mark(self, env_stream, wait=True):
+        """The device gate's guard (ScPipeline.mark) for the NEXT pipeline_learn: call it before enqueueing that
+        learn's env step on env_stream (raw handle). wait=True: the learn's round first waits on the learner stream
+        for an event behind everything env_stream holds now, so the gate spins only over the env step that follows;
+        wait=False: the caller guarantees that nothing but its own env step is enqueued on env_stream between the
+        previous learn and the next one. A pipeline_learn without a mark takes the cross-queue event hand-off (it never
+        spins behind work of unknown length). No-op before the ring holds a batch (that learn enqueues nothing)."""
+        if self.replay.counter >= self.batch_size:
+            self.pipeline().mark(int(env_stream), bool(wait))
+
     def pipeline_learn(self, agent, env_stream, learner_stream):
         """Enqueue learn(agent) through the native pipeline (raw stream handles): the snapshot on env_stream, the
         round on learner_stream. The actor phase stays pending until the next call or pipeline_flush. Returns False
-        (nothing enqueued) before the buffer holds a batch, like snapshot_into."""
+        (nothing enqueued) before the buffer holds a batch, like snapshot_into. The snapshot hand-off is the device
+        gate when pipeline_mark was called since the previous learn (and handoff="gate"), else an event wait."""
         if self.replay.counter < self.batch_size:
             return False
         self._learn_calls += 1
@@ -651,7 +682,8 @@ class SharedCriticBench:
     replay ring and run ONE learn() (agent round-robin, B=256)."""
 
     def __init__(self, env, device, seed=0, fused=True, overlap=True, n_slots=None, buffer_size=1_000_000,
-                 handoff="gate", dp_split=False, dp=None, dp_rccl=True):
+                 handoff="gate", dp_split=False, dp=None, dp_rccl=True, pipelined=True, high_priority=None,
+                 learner_priority="high"):
         self.env = env
         group = torch.distributed.group.WORLD if dist.active() else None  # replicas synced over RCCL
         # overlap: learn(s) runs on its own stream once its minibatch snapshot is taken, concurrently with env step
@@ -659,27 +691,32 @@ class SharedCriticBench:
         # exploration), so step s+1 does not depend on learn(s) and every kernel still sees the same data
         # (with data-parallel replicas the update's two all-reduces run on the learner stream too)
         self.overlap = bool(overlap and fused)
-        if n_slots is None:  # staging slots; FLOCK_SC_SLOTS: A/B
-            n_slots = int(os.environ.get("FLOCK_SC_SLOTS", "3"))
+        if n_slots is None:  # staging slots (3: the env stream runs at most two learns ahead of the learner)
+            n_slots = 3
         self.learner = SharedCriticLearner(env.N, env.k, device=device, seed=seed, batch_size=256,
                                            buffer_size=buffer_size, dist_group=group, fused=fused,
                                            snapshot=self.overlap, n_slots=n_slots, handoff=handoff, dp_split=dp_split,
-                                           dp=dp, dp_rccl=dp_rccl)
+                                           dp=dp, dp_rccl=dp_rccl, learner_priority=learner_priority)
         if self.overlap:
             # single GPU: learn() runs as two phases, the actor phase of learn s beside the critic phase of learn s+1:
             # with graphs, the native pipeline (one merged six-launch round per step on self.stream,
             # SharedCriticLearner.pipeline_learn); without, two streams (update_slot_pipelined).
-            # FLOCK_LEARN_PIPELINE=0 keeps one serial learn() per step on self.stream (data-parallel: the Python
-            # dp_learn rounds). Data-parallel learners run the same native pipeline, every round as gradients + one
-            # RCCL all-reduce + the Adam launch (SharedCriticLearner.pipeline, set_dp).
-            self.pipelined = os.environ.get("FLOCK_LEARN_PIPELINE") != "0"
-            # stream priority (FLOCK_LEARNER_PRIORITY=1): the one-stream learner ran at high priority; with the two
-            # pipelined streams high priority made steps 2-3x slower in fresh processes; with the native pipeline's
-            # one learner stream it changes nothing (tools/cu_mask_probe.py)
-            hi = os.environ.get("FLOCK_LEARNER_PRIORITY", "0" if self.pipelined else "1") == "1"
-            prio = torch.cuda.Stream.priority_range()[1] if hi else 0
-            self.stream = torch.cuda.Stream(device=device, priority=prio)
-            self.actor_stream = torch.cuda.Stream(device=device, priority=prio) if self.pipelined else None
+            # pipelined=False keeps one serial learn() per step on self.stream (data-parallel: the Python dp_learn
+            # rounds). Data-parallel learners run the same native pipeline, every round as gradients + one RCCL
+            # all-reduce + the Adam launch (SharedCriticLearner.pipeline, set_dp).
+            self.pipelined = bool(pipelined)
+            if self.pipelined and self.learner.use_graph:
+                # the native pipeline: its rounds on the learner's own stream (SharedCriticLearner.learner_stream)
+                self.stream = self.learner.learner_stream
+                self.actor_stream = None
+            else:
+                # stream priority (high_priority; default: high only for the non-pipelined one-stream learner): with
+                # the two pipelined streams high priority made steps 2-3x slower in fresh processes
+                # (tools/cu_mask_probe.py)
+                hi = (not self.pipelined) if high_priority is None else bool(high_priority)
+                prio = torch.cuda.Stream.priority_range()[1] if hi else 0
+                self.stream = torch.cuda.Stream(device=device, priority=prio)
+                self.actor_stream = torch.cuda.Stream(device=device, priority=prio) if self.pipelined else None
             self.critic_done = [torch.cuda.Event(), torch.cuda.Event()]
             self._handles = None
             ns = self.learner.n_slots
@@ -764,7 +801,12 @@ class SharedCriticBench:
 
     # bench.py hook interface: before(s) -> ring for the fused env step; after(s, a) -> learn(); prime()
     def before(self, s):
-        return self.learner.replay_slots(self.env.E * self.env.N)
+        slots = self.learner.replay_slots(self.env.E * self.env.N)
+        if self.overlap and self.pipelined and self.learner.use_graph:
+            # the device gate's guard of this step's learn (after the slots: it marks only a step that will learn),
+            # before the env step is enqueued on the current (env) stream
+            self.learner.pipeline_mark(torch.cuda.current_stream(self.learner.device).cuda_stream)
+        return slots
 
     def after(self, s, action):
         L = self.learner

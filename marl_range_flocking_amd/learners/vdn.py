@@ -116,6 +116,7 @@ class BatchedQNet:
 
     def __call__(self, obs, hidden):
         """Reference layout: obs [B,A,n_obs], hidden [B,A,H] -> (q [B,A,n_actions], hidden [B,A,H])."""
+        self.P.sync_writers()  # an overlapped train() still writing these parameters
         q, h = self.forward_am(obs.transpose(0, 1), hidden.transpose(0, 1))
         return q.transpose(0, 1), h.transpose(0, 1)
 
@@ -140,6 +141,7 @@ class BatchedQNet:
     def state_dict(self):
         """Reference key names (so learners/vdn/test_flock.py-style loaders can read it)."""
         out = {}
+        self.P.sync_writers()
         for name in self.P.shapes:
             v = self.P.view(self.P.data, name).detach().cpu()
             for i in range(self.n_agents):
@@ -278,7 +280,7 @@ class VDNLearner:
         U, B, C = self.update_iter, self.B, self.chunk
         ov = self.__dict__.get("_ov")
         if ov is None:
-            ov = self._ov = OverlappedTrain(self.replay, U * B * C)
+            ov = self._ov = OverlappedTrain(self.replay, U * B * C, writes=(self.q.P,))
             ov.idx_all = torch.arange(U * B * C, device=self.device).view(U, B, C)
             ov.static_idx = torch.zeros((B, C), dtype=torch.int64, device=self.device)
         n = len(self.replay)
@@ -312,6 +314,7 @@ class VDNLearner:
     def train(self, starts=None):
         """train(q, q_target, memory, optimizer, gamma, batch_size, update_iter, chunk_size) for every agent at
         once. starts: optional [update_iter, B] logical chunk starts (parity tests); returns the last loss."""
+        self.sync()  # after a train_overlapped(): its update must land first (same stream order as serial trains)
         n = len(self.replay)
         base = self.replay.counter - n  # logical index 0 = oldest row still in the ring
         ar = torch.arange(self.chunk, device=self.device)

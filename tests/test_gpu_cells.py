@@ -1,4 +1,5 @@
-"""The step kernel's cell-list kNN (N >= 128) against its own full scan (FLOCK_NO_CELLS=1) and the C oracle.
+"""The step kernel's cell-list kNN (N >= 128) against its own full scan (flock_set_diag("no_cells", 1)) and the C
+oracle.
 
 The cell path must be indistinguishable from the all-pairs scan: every output of a step (positions, velocities,
 headings, neighbour distances and indices, reward, done) is compared BITWISE between the two paths from the same
@@ -294,7 +295,7 @@ def test_untracked_indices_change_nothing_else(variant, periodic, N, kind, cuda)
 
 
 def test_env_range_launches_are_bitwise_one_launch(cuda):
-    """FLOCK_ENV_LAUNCHES=n splits a step into n launches over consecutive env ranges (Params.env0): a four-step
+    """flock_set_diag("env_launches", n) splits a step into n launches over consecutive env ranges (Params.env0): a four-step
     config-3-shape rollout (v2, N = 256, seeds, every output) is bit for bit the one-launch rollout."""
     k, E, N = 4, 37, 256  # E not a multiple of the split: the last range is short
     box = float(round(np.sqrt(250 * N)))

@@ -105,6 +105,12 @@ def test_shared_obs_ring_is_bitwise_the_separate_fields(cuda):
                  (a.critics.exp_avg_sq, b.critics.exp_avg_sq), (a.actors.target, b.actors.target)):
         assert torch.equal(x, y)
     obs = torch.rand(N, k, device=cuda)
+    b.add_record(obs, obs, torch.zeros(N, 2, device=cuda), obs, obs, torch.zeros(N, device=cuda),
+                 torch.zeros(N, device=cuda))
+    b.check_shared_obs()  # equal observations: accepted
+    # differing observations: the device-side flag (no host sync in add_record) raises at the next check / train()
+    b.add_record(obs, obs, torch.zeros(N, 2, device=cuda), obs + 1, obs, torch.zeros(N, device=cuda),
+                 torch.zeros(N, device=cuda))
     with pytest.raises(ValueError):
-        b.add_record(obs, obs, torch.zeros(N, 2, device=cuda), obs + 1, obs, torch.zeros(N, device=cuda),
-                     torch.zeros(N, device=cuda))
+        b.train()
+    b.check_shared_obs()  # the flag is consumed by the raise

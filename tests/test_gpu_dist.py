@@ -180,8 +180,8 @@ def test_two_ranks_overlapped_bench_loop_equals_serial(cuda):
 def _loop_worker(rank, port, q):
     """The data-parallel config-3 loop through the C++ ScTrainLoop (each round: gradients, the all-reduce over the
     c10d ProcessGroup enqueued from C++, the Adam launch) against the per-step Python data-parallel rounds
-    (FLOCK_LEARN_PIPELINE=0: SharedCriticLearner.dp_learn) on 2 ranks (gloo, cuda:0), with the actor half of every
-    round split off the learner chain (dp_split: the actor all-reduce over a second group and the actor Adam on the
+    (SharedCriticBench(pipelined=False): SharedCriticLearner.dp_learn) on 2 ranks (gloo, cuda:0), with the actor half
+    of every round split off the learner chain (dp_split: the actor all-reduce over a second group and the actor Adam on the
     pipeline's actor stream) and without (one [critic | actor] all-reduce): all three bitwise equal."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", RANK=str(rank))
     try:
@@ -197,16 +197,13 @@ def _loop_worker(rank, port, q):
                 for _ in range(3)]
         states = []
         for mode in ("python", "loop_split", "loop"):
-            if mode == "python":
-                os.environ["FLOCK_LEARN_PIPELINE"] = "0"
-            else:
-                os.environ.pop("FLOCK_LEARN_PIPELINE", None)
             env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
                                           range_start=(0, 63.0), sensor_range=14.0, step_launches=3), device=dev)
             g = torch.Generator(device=dev).manual_seed(3 + rank)
             env.positions.copy_(torch.rand(E, Na, 2, device=dev, generator=g) * 63.0)
             env.headings.copy_(torch.rand(E, Na, device=dev, generator=g) * 4.7)
-            hook = SharedCriticBench(env, device=dev, seed=11, dp_split=mode == "loop_split")
+            hook = SharedCriticBench(env, device=dev, seed=11, dp_split=mode == "loop_split",
+                                     pipelined=mode != "python")
             assert hook.learner.distributed and hook.learner.dp_split == (mode == "loop_split")
             if mode == "python":
                 assert not hook.can_loop()
@@ -224,7 +221,6 @@ def _loop_worker(rank, port, q):
                                                      A.exp_avg, A.exp_avg_sq, L.actor_steps, L.losses,
                                                      env.positions, env.dnn)]
                           + [L.replay.counter, L._learn_calls])
-        os.environ.pop("FLOCK_LEARN_PIPELINE", None)
         q.put((rank, states))
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
@@ -277,16 +273,13 @@ def _rccl_worker(port, q):
                 for _ in range(3)]
         states = []
         for mode in ("python", "loop_split", "loop"):
-            if mode == "python":
-                os.environ["FLOCK_LEARN_PIPELINE"] = "0"
-            else:
-                os.environ.pop("FLOCK_LEARN_PIPELINE", None)
             env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
                                           range_start=(0, 63.0), sensor_range=14.0, step_launches=3), device=dev)
             g = torch.Generator(device=dev).manual_seed(3)
             env.positions.copy_(torch.rand(E, Na, 2, device=dev, generator=g) * 63.0)
             env.headings.copy_(torch.rand(E, Na, device=dev, generator=g) * 4.7)
-            hook = SharedCriticBench(env, device=dev, seed=11, dp_split=mode == "loop_split", dp=True)
+            hook = SharedCriticBench(env, device=dev, seed=11, dp_split=mode == "loop_split", dp=True,
+                                     pipelined=mode != "python")
             assert hook.learner.distributed and hook.learner.dp_split == (mode == "loop_split")
             if mode == "python":
                 for s in range(S):
@@ -303,7 +296,6 @@ def _rccl_worker(port, q):
                                                      A.exp_avg, A.exp_avg_sq, L.actor_steps, L.losses,
                                                      env.positions, env.dnn)]
                           + [L.replay.counter, L._learn_calls])
-        os.environ.pop("FLOCK_LEARN_PIPELINE", None)
         q.put(states)
         torch.distributed.destroy_process_group()
     except Exception as e:  # noqa: BLE001

@@ -84,3 +84,85 @@ def test_vdn_overlapped_train_is_bitwise_train(cuda):
     P, Q = a.q.P, b.q.P
     for x, y in ((P.data, Q.data), (P.target, Q.target), (P.exp_avg, Q.exp_avg), (P.exp_avg_sq, Q.exp_avg_sq)):
         assert torch.equal(x, y)
+
+
+def _delay_current_stream(cuda):
+    """Queue ~10 ms of work on the current stream so that a missing cross-stream wait would show as a race."""
+    x = torch.rand(2048, 2048, device=cuda)
+    for _ in range(8):
+        x = x @ x / 2048.0
+    return x
+
+
+def test_maddpg_mixed_paths_are_bitwise_serial(cuda):
+    """train() and get_actions() / state_dict() right after train_overlapped() wait for the overlapped update
+    (FlatParams.sync_writers): the results equal serial train() calls on the same draws."""
+    out = []
+    for mixed in (False, True):
+        L = _maddpg(cuda)
+        g = torch.Generator(device=cuda).manual_seed(23)
+        for _ in range(6):
+            _maddpg_records(L, g, 50, cuda)
+        acts = []
+        for rep in range(3):
+            if mixed and rep % 2 == 0:
+                if "_ov" in L.__dict__:  # the overlapped update then starts ~10 ms late on its stream
+                    with torch.cuda.stream(L._ov.stream):
+                        _delay_current_stream(cuda)
+                L.train_overlapped()
+            else:
+                L.train()
+            x = torch.rand(4, L.N, L.k, device=cuda, generator=g)
+            acts.append(L.get_actions(x, test=True)[0].clone())
+            sd = L.state_dict("critic", 0)
+            _maddpg_records(L, g, 50, cuda)
+        loss = L.train().clone()
+        torch.cuda.synchronize()
+        out.append((L, loss, acts, sd))
+    (a, la, aa, sa), (b, lb, ab, sb) = out
+    assert torch.equal(la, lb)
+    for x, y in zip(aa, ab):
+        assert torch.equal(x, y)
+    for n in sa:
+        assert torch.equal(sa[n], sb[n]), n
+    for x, y in ((a.critics.data, b.critics.data), (a.critics.exp_avg_sq, b.critics.exp_avg_sq),
+                 (a.actors.target, b.actors.target)):
+        assert torch.equal(x, y)
+
+
+def test_vdn_mixed_paths_are_bitwise_serial(cuda):
+    """VDN: train(), sync_target(), the q network's forward and state_dict() right after train_overlapped() wait for
+    the overlapped update; bitwise serial train() calls on the same draws."""
+    out = []
+    for mixed in (False, True):
+        L = _vdn(cuda)
+        g = torch.Generator(device=cuda).manual_seed(29)
+        for _ in range(5):
+            _vdn_put(L, g, 60, cuda)
+        qs = []
+        for rep in range(3):
+            if mixed and rep % 2 == 0:
+                if "_ov" in L.__dict__:  # the overlapped update then starts ~10 ms late on its stream
+                    with torch.cuda.stream(L._ov.stream):
+                        _delay_current_stream(cuda)
+                L.train_overlapped()
+            else:
+                L.train()
+            obs = torch.rand(4, L.A, L.n_obs, device=cuda, generator=g)
+            qs.append(L.q(obs, L.q.init_hidden(4))[0].clone())
+            if rep == 1:
+                L.sync_target()
+            sd = L.q.state_dict()
+            _vdn_put(L, g, 60, cuda)
+        loss = L.train().clone()
+        torch.cuda.synchronize()
+        out.append((L, loss, qs, sd))
+    (a, la, qa, sa), (b, lb, qb, sb) = out
+    assert torch.equal(la, lb)
+    for x, y in zip(qa, qb):
+        assert torch.equal(x, y)
+    for n in sa:
+        assert torch.equal(sa[n], sb[n]), n
+    P, Q = a.q.P, b.q.P
+    for x, y in ((P.data, Q.data), (P.target, Q.target), (P.exp_avg_sq, Q.exp_avg_sq)):
+        assert torch.equal(x, y)

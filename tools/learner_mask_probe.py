@@ -66,6 +66,13 @@ if __name__ == "__main__":
         for keep in (192, 128, 64):
             arr.append((f"learner on the lowest {keep} CU bits", list(range(keep)), None))
             arr.append((f"learner on {keep} CU bits spread", spread(keep), None))
+    elif os.environ.get("MODE") == "split":
+        arr.append(("both on all CU bits (masked streams)", list(range(NCU)), list(range(NCU))))
+        for keep in [int(x) for x in os.environ.get("KEEP", "32,64,96,128").split(",")]:
+            lb = list(range(keep))
+            arr.append((f"learner lowest {keep} bits, env the rest", lb, [i for i in range(NCU) if i not in set(lb)]))
+            lb = spread(keep)
+            arr.append((f"learner {keep} spread bits, env the rest", lb, [i for i in range(NCU) if i not in set(lb)]))
     else:
         arr.append(("env on all CU bits (masked stream)", None, list(range(NCU))))
         for off in (8, 16, 32, 64):
