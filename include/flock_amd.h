@@ -140,6 +140,20 @@ int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_ran
                   const float* mem_in, float* mem_out,
                   float* vel, float* dnn, int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done);
 
+/* K gym_flock_uw steps in one call (the random-action rollout regime: the K actions are known up front; BASELINE
+ * config 2 runs it): actions [K][E][N][2]; step t writes obs_out[t] ([E][N][4][k], the observation memory after the
+ * step), reward_out[t] ([E][N]), done_out[t] ([E][N]) and any_done_out[t] ([E]). On return pos, vel, prev_heading,
+ * mem_out, dnn, nn_idx (may be NULL), reward, done and any_done hold the state after step K - 1, exactly as K
+ * flock_step_uw calls leave it (mem_in is read before anything is written: it may alias mem_out). At N = 64, k = 4
+ * (config 2) one launch runs all K steps with the env state kept on chip; other shapes (and normalize_distance) run K
+ * step launches. ext: seeds / launches / normalize_distance as for flock_step_uw_ext (no ring). Replaces K calls of
+ * environments/gym_flock_uw.py:69-81. */
+int flock_rollout_uw(void* stream, int K, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                     float dt, int rigid_boundary, float* pos, const float* heading, float* prev_heading,
+                     const float* actions, const float* mem_in, float* mem_out, float* vel, float* dnn,
+                     int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done, float* obs_out,
+                     float* reward_out, uint8_t* done_out, uint8_t* any_done_out, const FlockStepExt* ext);
+
 /* gym_flock_uw_discrete step: action_id indexes table [n_actions][2] (action_dictionary means). noise [E][N][2]
  * holds the N(0, noise_std) draws torch.normal adds to the means; if noise is NULL they are drawn in-kernel from
  * Philox4x32-10(seed, counter = (agent, rng_offset)). status (may be NULL): device int, bit 0 set if any action id

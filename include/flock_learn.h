@@ -237,6 +237,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
 int flock_sc_pipeline_set_gate(FlockScPipeline* p, int on);
 int flock_sc_pipeline_mark(FlockScPipeline* p, void* env_stream, int wait);
 int flock_sc_pipeline_gated(const FlockScPipeline* p);
+int64_t flock_sc_pipeline_gated_learns(const FlockScPipeline* p); /* learns so far that took the gate */
 int flock_sc_pipeline_check(FlockScPipeline* p);
 int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream);
 void flock_sc_pipeline_destroy(FlockScPipeline* p);

@@ -32,6 +32,8 @@ SIGNATURES = {
     "flock_step_uw_discrete_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float,
                                    _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                    _c_float, _c_u64, _c_u64, _c_void_p, _c_int] + [_c_void_p] * 8,
+    "flock_rollout_uw": [_c_void_p, _c_int, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_float, _c_int]
+                        + [_c_void_p] * 17,
     "flock_step_flock_ext": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_float, _c_int]
                             + [_c_void_p] * 11,
     "flock_knn": [_c_void_p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int] + [_c_void_p] * 3,
@@ -158,6 +160,7 @@ SIGNATURES.update({
     "flock_sc_pipeline_set_gate": [_c_void_p, _c_int],
     "flock_sc_pipeline_mark": [_c_void_p, _c_void_p, _c_int],
     "flock_sc_pipeline_comm_stream": [_c_void_p],
+    "flock_sc_pipeline_gated_learns": [_c_void_p],
     "flock_sc_pipeline_check": [_c_void_p],
     "flock_sc_pipeline_gated": [_c_void_p],
     "flock_sc_pipeline_set_dp": [_c_void_p, _c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_void_p,
@@ -168,7 +171,7 @@ SIGNATURES.update({
 RESTYPES = {"flock_last_error": ctypes.c_char_p, "flock_learn_last_error": ctypes.c_char_p,
             "flock_sc_workspace_floats": ctypes.c_int64, "flock_sc_update_size": ctypes.c_int64,
             "flock_sc_pipeline_create": _c_void_p, "flock_sc_pipeline_destroy": None,
-            "flock_sc_pipeline_comm_stream": _c_void_p}
+            "flock_sc_pipeline_comm_stream": _c_void_p, "flock_sc_pipeline_gated_learns": ctypes.c_int64}
 
 _lib = None
 

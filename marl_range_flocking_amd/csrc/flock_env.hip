@@ -1533,6 +1533,141 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 }
 
 // ---------------------------------------------------------------------------------------------------------------
+// K steps of gym_flock_uw in ONE launch (flock_rollout_uw; BASELINE config 2: 64 agents per env, k = 4, Euclidean kNN,
+// 4-frame observation memory), for the random-action rollout regime where the K actions are known up front. One
+// workgroup of 4 x 64 lanes owns one env for all K steps and keeps its state on chip: positions, previous headings and
+// the memory frames in registers, each step's positions in LDS. A step's HBM traffic is then its action read and its
+// observation / reward / done writes (77 B per agent-step; a single step also reads and rewrites the state and the
+// memory: the 149 B of SURVEY §8(d)'s accounting), and the launch pays its dispatch and its first loads once per K steps.
+// Lane (w, l) of the 4 waves: agent ia = 16 w + (l & 15), candidate quarter r = l >> 4. The 4 lanes of an agent run
+// its kinematics redundantly, scan candidates [16 r, 16 r + 16) each, and merge their partial top-L key lists by two
+// xor shuffles: the same key set, hence the same result, as the split step kernel's LDS merge. Lane r holds memory
+// frame r, so the memory roll is one shuffle. The centre of mass is the step kernel's fixed power-of-two tree
+// (r[i] += r[i + s], s = 32 .. 1) as wave shuffles: the same pairs in the same order, bitwise equal. One workgroup
+// barrier per step (the positions are double-buffered in LDS, so a wave one step ahead never overwrites the positions
+// another wave still scans). The results are bitwise those of K flock_step_uw calls (tests/test_gpu_rollout.py).
+constexpr int kRollN = 64;
+__global__ __launch_bounds__(4 * kRollN) void rollout_uw_kernel(const Params p, int K, const float* __restrict__ actions,
+                                                                float* __restrict__ obs, float* __restrict__ rew_out,
+                                                                uint8_t* __restrict__ done_out,
+                                                                uint8_t* __restrict__ any_out) {
+    constexpr int N = kRollN, L = 6, KN = L - 2, Q = N / 4, IB = 6;  // k = 4; IB = ceil_log2(N)
+    __shared__ float2 lpos[2][N];
+    __shared__ int flag[2];  // any_done of a step, by step parity
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int ia = 16 * w + (l & 15), r = l >> 4;
+    const int env = blockIdx.x;
+    const size_t a = (size_t)env * N + ia;
+    const size_t EN = (size_t)p.E * N;
+    if (t < 2) flag[t] = 0;
+    const f32x2 p0 = reinterpret_cast<const f32x2*>(p.pos)[a];
+    float x = p0.x, y = p0.y;
+    const float h = p.heading[a];
+    float prev_h = p.prev_heading[a];
+    float4 fr = reinterpret_cast<const float4*>(p.mem_in)[a * kMem + r];  // memory frame r
+    f32x2 act = ld_i<true>(reinterpret_cast<const f32x2*>(actions) + a);
+    float vx = 0.0f, vy = 0.0f, rw = 0.0f;
+    float dv[KN];
+    int bj[L - 1];
+#pragma unroll
+    for (int q = 0; q < KN; ++q) dv[q] = 0.0f;
+#pragma unroll
+    for (int q = 0; q < L - 1; ++q) bj[q] = 0;
+    int coll = 0;
+    for (int s = 0; s < K; ++s) {
+        f32x2 nxt = act;  // the next step's action, in flight during this step
+        if (s + 1 < K) nxt = ld_i<true>(reinterpret_cast<const f32x2*>(actions) + (size_t)(s + 1) * EN + a);
+        // kinematics + check_boundary (gym_flock_uw.py:269-302; the step kernel's FLOCK_VARIANT_UW branch)
+        const float n = sqrt_rn(__fadd_rn(__fmul_rn(act.x, act.x), __fmul_rn(act.y, act.y)));
+        vx = __fmul_rn(nan_to_num(__fdiv_rn(act.x, n)), p.dt);
+        vy = __fmul_rn(nan_to_num(__fdiv_rn(act.y, n)), p.dt);
+        x = boundary(__fadd_rn(x, vx), p.box, p.rigid);
+        y = boundary(__fadd_rn(y, vy), p.box, p.rigid);
+        float2* lp = lpos[s & 1];
+        if (r == 0) lp[ia] = make_float2(x, y);
+        __syncthreads();
+        if (t == 0 && s > 0) {  // the previous step's any_done: every wave ORed into it before this barrier
+            any_out[(size_t)(s - 1) * p.E + env] = (uint8_t)flag[(s - 1) & 1];
+            flag[(s - 1) & 1] = 0;  // reused by step s + 1, whose ORs come after the next barrier
+        }
+        // centre of mass (gym_flock_uw.py:206-210): every wave, lane = agent
+        const float2 c = lp[l];
+        float sx = c.x, sy = c.y;
+#pragma unroll
+        for (int o = N / 2; o >= 1; o >>= 1) {
+            sx = __fadd_rn(sx, __shfl_down(sx, o));
+            sy = __fadd_rn(sy, __shfl_down(sy, o));
+        }
+        const float s0 = __fdiv_rn(__shfl(sx, 0), (float)N), s1 = __fdiv_rn(__shfl(sy, 0), (float)N);
+        // kNN (_computeDistances :155-175 + topk): a quarter of the candidates per lane, the lists merged
+        uint32_t key[L];
+        scan_range<L, false>(key, lp, Q * r, Q * r + Q, IB, x, y, p.box);
+#pragma unroll
+        for (int m = 16; m <= 32; m <<= 1) {
+            uint32_t o[L];
+#pragma unroll
+            for (int q = 0; q < L; ++q) o[q] = (uint32_t)__shfl_xor((int)key[q], m);
+#pragma unroll
+            for (int q = 0; q < L; ++q) key_insert<L>(key, o[q]);
+        }
+        float bd[L - 1];
+        const bool amb = knn_finalize<L, false>(key, lp, N, KN, IB, x, y, p.box, bd, bj, false) && r == 0;
+        if (__ballot(amb) != 0)
+            exact_rescan_wave<L, false, false, false>(bd, bj, amb, 0, lp, N, N, nullptr, nullptr, 0, 0, 0, 0, 0, 0,
+                                                      0, x, y, p.box);
+        // outputs of step s: distances of the agent's r == 0 lane (clamp, collisions: gym_flock_uw.py:120-123, 215)
+        float d4[KN];
+#pragma unroll
+        for (int q = 0; q < KN; ++q) d4[q] = clamp_t(sqrt_rn(bd[q + 1]), 0.0f, p.sensor_range);
+        coll = 0;
+#pragma unroll
+        for (int q = 0; q < KN; ++q) {
+            dv[q] = __shfl(d4[q], l & 15);
+            coll |= (dv[q] < p.cd);
+        }
+        // torch.roll + insert of the observation memory: frame r <- frame r - 1 (lane l - 16), frame 0 <- dv
+        float4 nf;
+        nf.x = __shfl(fr.x, (l - 16) & 63);
+        nf.y = __shfl(fr.y, (l - 16) & 63);
+        nf.z = __shfl(fr.z, (l - 16) & 63);
+        nf.w = __shfl(fr.w, (l - 16) & 63);
+        fr = r == 0 ? make_float4(dv[0], dv[1], dv[2], dv[3]) : nf;
+        st_o<true>(reinterpret_cast<f32x4*>(obs) + ((size_t)s * EN + a) * kMem + r, f32x4{fr.x, fr.y, fr.z, fr.w});
+        if (r == 0) {  // reward (gym_flock_uw.py:206-221)
+            const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
+            const float dist = sqrt_rn(__fadd_rn(__fmul_rn(com_x, com_x), __fmul_rn(com_y, com_y)));
+            const float com = (dist < p.com_r) ? 0.01f : 0.0f;
+            const float angp = (fabsf(__fsub_rn(prev_h, h)) > 0.27f) ? -0.01f : 0.001f;
+            rw = __fadd_rn(__fadd_rn(coll ? -5.0f : 0.01f, com), angp);
+            st_o<true>(rew_out + (size_t)s * EN + a, rw);
+            st_o<true>(done_out + (size_t)s * EN + a, (uint8_t)coll);
+        }
+        prev_h = h;
+        if (__ballot(r == 0 && coll) != 0 && l == 0) atomicOr(&flag[s & 1], 1);
+        act = nxt;
+    }
+    __syncthreads();
+    if (t == 0) {
+        const uint8_t f = (uint8_t)flag[(K - 1) & 1];
+        any_out[(size_t)(K - 1) * p.E + env] = f;
+        p.any_done[env] = f;
+    }
+    // the state after the last step, as K flock_step_uw calls leave it
+    reinterpret_cast<float4*>(p.mem_out)[a * kMem + r] = fr;
+    if (r == 0) {
+        reinterpret_cast<f32x2*>(p.pos)[a] = f32x2{x, y};
+        reinterpret_cast<f32x2*>(p.vel)[a] = f32x2{vx, vy};
+        p.prev_heading[a] = prev_h;
+        reinterpret_cast<f32x4*>(p.dnn)[a] = f32x4{dv[0], dv[1], dv[2], dv[3]};
+        p.reward[a] = rw;
+        p.done[a] = (uint8_t)coll;
+        if (p.idx)
+#pragma unroll
+            for (int q = 0; q < KN; ++q) p.idx[a * KN + q] = (int64_t)bj[q + 1];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
 // reset: bounded in-kernel rejection sampling (replaces the reference's unbounded recursion)
 
 template <int L>
@@ -2108,6 +2243,66 @@ int flock_step_uw(void* stream, int E, int N, int k, float box, float sensor_ran
     return flock_step_uw_ext(stream, E, N, k, box, sensor_range, collision_distance, dt, rigid_boundary, pos, heading,
                              prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
                              nullptr);
+}
+
+int flock_rollout_uw(void* stream, int K, int E, int N, int k, float box, float sensor_range, float collision_distance,
+                     float dt, int rigid_boundary, float* pos, const float* heading, float* prev_heading,
+                     const float* actions, const float* mem_in, float* mem_out, float* vel, float* dnn,
+                     int64_t* nn_idx, float* reward, uint8_t* done, uint8_t* any_done, float* obs_out,
+                     float* reward_out, uint8_t* done_out, uint8_t* any_done_out, const FlockStepExt* ext) {
+    if (ext && ext->ring) return fail(FLOCK_E_ARG, "flock_rollout_uw: the fused replay insert is v2 / uw_discrete only");
+    int rc = check_common(E, N, k);
+    if (rc) return rc;
+    if (K < 0) return fail(FLOCK_E_ARG, "flock_rollout_uw: K must be >= 0");
+    if (K == 0 || E == 0) return FLOCK_OK;
+    if (!pos || !heading || !prev_heading || !actions || !mem_in || !mem_out || !vel || !dnn || !reward || !done ||
+        !any_done || !obs_out || !reward_out || !done_out || !any_done_out)
+        return fail(FLOCK_E_NULL, "flock_rollout_uw: NULL pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const bool normalize = ext && ext->normalize_distance;
+    const size_t EN = (size_t)E * N;
+    if (N == kRollN && k == 4 && !normalize && !knobs().no_spec) {  // the one-launch kernel (config 2's shape)
+        Params p = base(E, N, k, box);
+        p.variant = FLOCK_VARIANT_UW;
+        p.rigid = rigid_boundary != 0;
+        p.sensor_range = sensor_range;
+        p.cd = collision_distance;
+        p.com_r = (float)((double)collision_distance * 4.0);  // collision_distance*4 (gym_flock_uw.py:197)
+        p.dt = dt;
+        p.pos = pos;
+        p.heading = const_cast<float*>(heading);
+        p.prev_heading = prev_heading;
+        p.mem_in = mem_in;
+        p.mem_out = mem_out;
+        p.vel = vel;
+        p.dnn = dnn;
+        p.idx = nn_idx;
+        p.reward = reward;
+        p.done = done;
+        p.any_done = any_done;
+        hipLaunchKernelGGL(rollout_uw_kernel, dim3(E), dim3(4 * kRollN), 0, st, p, K, actions, obs_out, reward_out,
+                           done_out, any_done_out);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? FLOCK_OK : fail(FLOCK_E_LAUNCH, hipGetErrorString(e));
+    }
+    // other shapes: K step launches writing the stacked outputs directly (step t's memory input is step t - 1's
+    // observation), then the last step's memory / reward / done into the env buffers
+    for (int s = 0; s < K; ++s) {
+        const float* mi = s == 0 ? mem_in : obs_out + (size_t)(s - 1) * EN * kMem * k;
+        if ((rc = flock_step_uw_ext(stream, E, N, k, box, sensor_range, collision_distance, dt, rigid_boundary, pos,
+                                    heading, prev_heading, actions + (size_t)s * EN * 2, mi,
+                                    obs_out + (size_t)s * EN * kMem * k, vel, dnn, nn_idx, reward_out + (size_t)s * EN,
+                                    done_out + (size_t)s * EN, any_done_out + (size_t)s * E, ext)))
+            return rc;
+    }
+    const size_t last = (size_t)(K - 1);
+    if (hipMemcpyAsync(mem_out, obs_out + last * EN * kMem * k, EN * kMem * k * sizeof(float),
+                       hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(reward, reward_out + last * EN, EN * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(done, done_out + last * EN, EN, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(any_done, any_done_out + last * E, E, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return fail(FLOCK_E_LAUNCH, "flock_rollout_uw: copy of the last step's outputs");
+    return FLOCK_OK;
 }
 
 int flock_step_uw_discrete_ext(void* stream, int E, int N, int k, float box, float sensor_range,

@@ -2120,6 +2120,7 @@ struct FlockScPipeline {
     // the previous snapshot; 0 = no mark: the event hand-off, so that no round ever spins on work of unknown length
     hipEvent_t mark_ev;
     int mark;
+    int64_t gated_learns;  // learns that took the gate (the rest: the event hand-off)
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
@@ -2318,6 +2319,7 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->seq = 0;
     p->gate_on = false;
     p->mark = 0;
+    p->gated_learns = 0;
     p->mark_ev = nullptr;
     if (!rc && hipEventCreateWithFlags(&p->mark_ev, hipEventDisableTiming) != hipSuccess)
         rc = fail(-4, "flock_sc_pipeline_create: event");
@@ -2402,6 +2404,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         // over the env work enqueued since the mark (the caller's own env step), never behind a backlog of unknown
         // length; with mark 1 the caller declared that nothing else was enqueued since the previous snapshot
         if (mark == 2 && (rc = wait_unless_done(ls, p->mark_ev))) return rc;
+        ++p->gated_learns;
         const FlockScRows& src = p->ring;
         const FlockScRows& dst = p->staging[s];
         int vec = u.in_dim == 4 && u.n_actions == 2;
@@ -2536,6 +2539,8 @@ int flock_sc_pipeline_check(FlockScPipeline* p) {
 int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate_on ? 1 : 0; }
 
 void* flock_sc_pipeline_comm_stream(const FlockScPipeline* p) { return p ? (void*)p->comm_stream : nullptr; }
+
+int64_t flock_sc_pipeline_gated_learns(const FlockScPipeline* p) { return p ? p->gated_learns : 0; }
 
 void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (!p) return;

@@ -8,6 +8,7 @@
 //
 //   flock::step_v2           gym_flock_v2.py:71-83
 //   flock::step_uw           gym_flock_uw.py:69-81
+//   flock::rollout_uw        K step_uw calls in one (the random-action rollout regime; config 2: one launch)
 //   flock::step_uw_discrete  gym_flock_uw_discrete.py:110-122
 //   flock::step_flock        gym_flock.py:48-60
 //   flock::step_v2_store     step_v2 + the training loop's replay insert in the same launch (store_transitions,
@@ -91,11 +92,11 @@ void step_v2_hip(const Tensor& pos, const Tensor& heading, const Tensor& action,
                  const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
                  const Tensor& any_done, const optional<Tensor>& seeds, int64_t k, double box, double sensor_range,
                  double collision_distance, double dt, double v_min, double v_max, bool periodic,
-                 bool rigid_boundary, int64_t launches) {
+                 bool rigid_boundary, int64_t launches, bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), normalize_distance ? 1 : 0};
     rc_check(flock_step_v2_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, (float)v_min,
                                (float)v_max, periodic, rigid_boundary, ptr<float>(pos), ptr<float>(heading),
@@ -107,7 +108,7 @@ void step_v2_hip(const Tensor& pos, const Tensor& heading, const Tensor& action,
 void step_v2_meta(const Tensor& pos, const Tensor& heading, const Tensor& action, const Tensor& vel,
                   const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done,
                   const Tensor& any_done, const optional<Tensor>& seeds, int64_t k, double, double, double, double,
-                  double, double, bool, bool, int64_t launches) {
+                  double, double, bool, bool, int64_t launches, bool) {
     launch_count(launches);
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
 }
@@ -138,12 +139,13 @@ void step_uw_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_he
                  const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
                  const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
                  const optional<Tensor>& seeds, int64_t k, double box, double sensor_range,
-                 double collision_distance, double dt, bool rigid_boundary, int64_t launches) {
+                 double collision_distance, double dt, bool rigid_boundary, int64_t launches,
+                 bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_uw_checks(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
                    seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), normalize_distance ? 1 : 0};
     rc_check(flock_step_uw_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, rigid_boundary,
                                ptr<float>(pos), ptr<const float>(heading), ptr<float>(prev_heading),
@@ -156,10 +158,63 @@ void step_uw_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_he
 void step_uw_meta(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading, const Tensor& action,
                   const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
                   const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
-                  const optional<Tensor>& seeds, int64_t k, double, double, double, double, bool, int64_t launches) {
+                  const optional<Tensor>& seeds, int64_t k, double, double, double, double, bool, int64_t launches,
+                  bool) {
     launch_count(launches);
     step_uw_checks(pos, heading, prev_heading, action, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
                    seeds, k);
+}
+
+// -------------------------------------------------------------------------------------------------- rollout_uw
+// K steps of step_uw in one call (flock_rollout_uw): actions [K, E, N, 2]; per-step outputs obs_out [K, E, N, 4, k],
+// reward_out [K, E, N], done_out [K, E, N], any_done_out [K, E]; the env buffers end as after K step_uw calls
+void rollout_uw_checks(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading, const Tensor& actions,
+                       const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
+                       const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
+                       const Tensor& obs_out, const Tensor& reward_out, const Tensor& done_out,
+                       const Tensor& any_done_out, const optional<Tensor>& seeds, int64_t k) {
+    TORCH_CHECK(actions.dim() == 4, "actions must be [K, E, N, 2], got ", actions.sizes());
+    const int64_t K = actions.size(0);
+    auto [E, N] = dims(pos);
+    step_uw_checks(pos, heading, prev_heading, actions[0], mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
+                   seeds, k);
+    need(actions, "actions", at::kFloat, {K, E, N, 2}, pos);
+    need(obs_out, "obs_out", at::kFloat, {K, E, N, 4, k}, pos);
+    need(reward_out, "reward_out", at::kFloat, {K, E, N}, pos);
+    need(done_out, "done_out", at::kBool, {K, E, N}, pos);
+    need(any_done_out, "any_done_out", at::kBool, {K, E}, pos);
+}
+
+void rollout_uw_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading, const Tensor& actions,
+                    const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
+                    const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
+                    const Tensor& obs_out, const Tensor& reward_out, const Tensor& done_out,
+                    const Tensor& any_done_out, const optional<Tensor>& seeds, int64_t k, double box,
+                    double sensor_range, double collision_distance, double dt, bool rigid_boundary,
+                    bool normalize_distance) {
+    TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
+    const at::OptionalDeviceGuard guard(pos.device());
+    rollout_uw_checks(pos, heading, prev_heading, actions, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
+                      obs_out, reward_out, done_out, any_done_out, seeds, k);
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), 1, normalize_distance ? 1 : 0};
+    rc_check(flock_rollout_uw(stream_of(pos), (int)actions.size(0), (int)pos.size(0), (int)pos.size(1), (int)k,
+                              (float)box, (float)sensor_range, (float)collision_distance, (float)dt, rigid_boundary,
+                              ptr<float>(pos), ptr<const float>(heading), ptr<float>(prev_heading),
+                              ptr<const float>(actions), ptr<const float>(mem_in), ptr<float>(mem_out), ptr<float>(vel),
+                              ptr<float>(dnn), ptr<int64_t>(nn_idx), ptr<float>(reward), ptr<uint8_t>(done),
+                              ptr<uint8_t>(any_done), ptr<float>(obs_out), ptr<float>(reward_out),
+                              ptr<uint8_t>(done_out), ptr<uint8_t>(any_done_out), &ext),
+             "flock_rollout_uw");
+}
+
+void rollout_uw_meta(const Tensor& pos, const Tensor& heading, const Tensor& prev_heading, const Tensor& actions,
+                     const Tensor& mem_in, const Tensor& mem_out, const Tensor& vel, const Tensor& dnn,
+                     const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
+                     const Tensor& obs_out, const Tensor& reward_out, const Tensor& done_out,
+                     const Tensor& any_done_out, const optional<Tensor>& seeds, int64_t k, double, double, double,
+                     double, bool, bool) {
+    rollout_uw_checks(pos, heading, prev_heading, actions, mem_in, mem_out, vel, dnn, nn_idx, reward, done, any_done,
+                      obs_out, reward_out, done_out, any_done_out, seeds, k);
 }
 
 // -------------------------------------------------------------------------------------------- step_uw_discrete
@@ -191,12 +246,12 @@ void step_uwd_hip(const Tensor& pos, const Tensor& heading, const Tensor& prev_h
                   const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
                   const Tensor& status, const optional<Tensor>& seeds, int64_t k, double box, double sensor_range,
                   double collision_distance, double dt, double v_max, bool rigid_boundary, double noise_std,
-                  int64_t seed, int64_t rng_offset, int64_t launches) {
+                  int64_t seed, int64_t rng_offset, int64_t launches, bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), normalize_distance ? 1 : 0};
     rc_check(flock_step_uw_discrete_ext(
                  stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
                  (float)collision_distance, (float)dt, (float)v_max, rigid_boundary, ptr<float>(pos),
@@ -212,7 +267,7 @@ void step_uwd_meta(const Tensor& pos, const Tensor& heading, const Tensor& prev_
                    const optional<Tensor>& noise, const Tensor& table, const Tensor& vel, const Tensor& dnn,
                    const optional<Tensor>& nn_idx, const Tensor& reward, const Tensor& done, const Tensor& any_done,
                    const Tensor& status, const optional<Tensor>& seeds, int64_t k, double, double, double, double,
-                   double, bool, double, int64_t, int64_t, int64_t launches) {
+                   double, bool, double, int64_t, int64_t, int64_t launches, bool) {
     launch_count(launches);
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
@@ -241,11 +296,12 @@ void step_flock_checks(const Tensor& pos, const Tensor& vel, const Tensor& actio
 void step_flock_hip(const Tensor& pos, const Tensor& vel, const Tensor& action, const Tensor& mem_in,
                     const Tensor& mem_out, const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward,
                     const Tensor& done, const Tensor& any_done, const optional<Tensor>& seeds, int64_t k,
-                    double box, double collision_distance, double dt, bool rigid_boundary, int64_t launches) {
+                    double box, double collision_distance, double dt, bool rigid_boundary, int64_t launches,
+                    bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_flock_checks(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, seeds, k);
-    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    FlockStepExt ext{nullptr, ptr<uint16_t>(seeds), launch_count(launches), normalize_distance ? 1 : 0};
     rc_check(flock_step_flock_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                   (float)collision_distance, (float)dt, rigid_boundary, ptr<float>(pos),
                                   ptr<float>(vel), ptr<const float>(action), ptr<const float>(mem_in),
@@ -257,7 +313,7 @@ void step_flock_hip(const Tensor& pos, const Tensor& vel, const Tensor& action, 
 void step_flock_meta(const Tensor& pos, const Tensor& vel, const Tensor& action, const Tensor& mem_in,
                      const Tensor& mem_out, const Tensor& dnn, const optional<Tensor>& nn_idx, const Tensor& reward,
                      const Tensor& done, const Tensor& any_done, const optional<Tensor>& seeds, int64_t k, double,
-                     double, double, bool, int64_t launches) {
+                     double, double, bool, int64_t launches, bool) {
     launch_count(launches);
     step_flock_checks(pos, vel, action, mem_in, mem_out, dnn, nn_idx, reward, done, any_done, seeds, k);
 }
@@ -326,14 +382,14 @@ void step_v2_store_hip(const Tensor& pos, const Tensor& heading, const Tensor& a
                        const optional<Tensor>& actor_state, const optional<Tensor>& actor_new_state,
                        const Tensor& prev_obs, at::IntArrayRef ring_meta, int64_t k, double box, double sensor_range,
                        double collision_distance, double dt, double v_min, double v_max, bool periodic,
-                       bool rigid_boundary, int64_t launches) {
+                       bool rigid_boundary, int64_t launches, bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
     TORCH_CHECK(ring_meta.size() == 6 && ring_meta[4] == 0 && ring_meta[5] == 0,
                 "step_v2_store: action ids / env done flags are the uw_discrete ring's");
     const FlockRing r = ring_of(pos, ring, actor_state, actor_new_state, prev_obs, ring_meta, k);
-    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), normalize_distance ? 1 : 0};
     rc_check(flock_step_v2_ext(stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box,
                                (float)sensor_range, (float)collision_distance, (float)dt, (float)v_min,
                                (float)v_max, periodic, rigid_boundary, ptr<float>(pos), ptr<float>(heading),
@@ -347,7 +403,7 @@ void step_v2_store_meta(const Tensor& pos, const Tensor& heading, const Tensor& 
                         const Tensor& any_done, const optional<Tensor>& seeds, at::TensorList ring,
                         const optional<Tensor>& actor_state, const optional<Tensor>& actor_new_state,
                         const Tensor& prev_obs, at::IntArrayRef ring_meta, int64_t k, double, double, double, double,
-                        double, double, bool, bool, int64_t launches) {
+                        double, double, bool, bool, int64_t launches, bool) {
     launch_count(launches);
     step_v2_checks(pos, heading, action, vel, dnn, nn_idx, reward, done, any_done, seeds, k);
     ring_of(pos, ring, actor_state, actor_new_state, prev_obs, ring_meta, k);
@@ -359,13 +415,14 @@ void step_uwd_store_hip(const Tensor& pos, const Tensor& heading, const Tensor& 
                         const Tensor& any_done, const Tensor& status, const optional<Tensor>& seeds,
                         at::TensorList ring, const Tensor& prev_obs, at::IntArrayRef ring_meta, int64_t k, double box,
                         double sensor_range, double collision_distance, double dt, double v_max, bool rigid_boundary,
-                        double noise_std, int64_t seed, int64_t rng_offset, int64_t launches) {
+                        double noise_std, int64_t seed, int64_t rng_offset, int64_t launches,
+                        bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
     const FlockRing r = ring_of(pos, ring, c10::nullopt, c10::nullopt, prev_obs, ring_meta, k);
-    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), 0};
+    FlockStepExt ext{&r, ptr<uint16_t>(seeds), launch_count(launches), normalize_distance ? 1 : 0};
     rc_check(flock_step_uw_discrete_ext(
                  stream_of(pos), (int)pos.size(0), (int)pos.size(1), (int)k, (float)box, (float)sensor_range,
                  (float)collision_distance, (float)dt, (float)v_max, rigid_boundary, ptr<float>(pos),
@@ -383,7 +440,7 @@ void step_uwd_store_meta(const Tensor& pos, const Tensor& heading, const Tensor&
                          const Tensor& done, const Tensor& any_done, const Tensor& status,
                          const optional<Tensor>& seeds, at::TensorList ring, const Tensor& prev_obs,
                          at::IntArrayRef ring_meta, int64_t k, double, double, double, double, double, bool, double,
-                         int64_t, int64_t, int64_t launches) {
+                         int64_t, int64_t, int64_t launches, bool) {
     launch_count(launches);
     step_uwd_checks(pos, heading, prev_heading, action_id, noise, table, vel, dnn, nn_idx, reward, done, any_done,
                     status, seeds, k);
@@ -439,16 +496,16 @@ void reset_hip(const Tensor& pos, const Tensor& dnn, const optional<Tensor>& hea
                const optional<Tensor>& mem, const optional<Tensor>& valid, const optional<Tensor>& env_mask,
                int64_t variant, int64_t k, double range_lo, double range_hi, double box, double sensor_range,
                double check_distance, bool rigid_boundary, int64_t max_attempts, int64_t seed, int64_t rng_offset,
-               int64_t repair_rounds) {
+               int64_t repair_rounds, bool normalize_distance) {
     TORCH_CHECK(on_hip(pos), "flock ops run on a HIP device only (no CPU fallback); got ", pos.device());
     const at::OptionalDeviceGuard guard(pos.device());
     reset_checks(pos, dnn, heading, prev_heading, vel, nn_idx, mem, valid, env_mask, variant, k);
-    rc_check(flock_reset_ext(stream_of(pos), (int)variant, (int)pos.size(0), (int)pos.size(1), (int)k,
-                             (float)range_lo, (float)range_hi, (float)box, (float)sensor_range, (float)check_distance,
-                             rigid_boundary, (int)max_attempts, (uint64_t)seed, (uint64_t)rng_offset,
-                             ptr<const uint8_t>(env_mask), ptr<float>(pos), ptr<float>(heading),
-                             ptr<float>(prev_heading), ptr<float>(vel), ptr<float>(dnn), ptr<int64_t>(nn_idx),
-                             ptr<float>(mem), ptr<uint8_t>(valid), (int)repair_rounds),
+    rc_check(flock_reset_ext2(stream_of(pos), (int)variant, (int)pos.size(0), (int)pos.size(1), (int)k,
+                              (float)range_lo, (float)range_hi, (float)box, (float)sensor_range, (float)check_distance,
+                              rigid_boundary, (int)max_attempts, (uint64_t)seed, (uint64_t)rng_offset,
+                              ptr<const uint8_t>(env_mask), ptr<float>(pos), ptr<float>(heading),
+                              ptr<float>(prev_heading), ptr<float>(vel), ptr<float>(dnn), ptr<int64_t>(nn_idx),
+                              ptr<float>(mem), ptr<uint8_t>(valid), (int)repair_rounds, normalize_distance ? 1 : 0),
              "flock_reset");
 }
 
@@ -456,7 +513,7 @@ void reset_meta(const Tensor& pos, const Tensor& dnn, const optional<Tensor>& he
                 const optional<Tensor>& prev_heading, const optional<Tensor>& vel, const optional<Tensor>& nn_idx,
                 const optional<Tensor>& mem, const optional<Tensor>& valid, const optional<Tensor>& env_mask,
                 int64_t variant, int64_t k, double, double, double, double, double, bool, int64_t, int64_t, int64_t,
-                int64_t) {
+                int64_t, bool) {
     reset_checks(pos, dnn, heading, prev_heading, vel, nn_idx, mem, valid, env_mask, variant, k);
 }
 
@@ -467,36 +524,46 @@ TORCH_LIBRARY(flock, m) {
         "step_v2(Tensor(a!) pos, Tensor(b!) heading, Tensor action, Tensor(c!) vel, Tensor(d!) dnn, "
         "Tensor(e!)? nn_idx, Tensor(f!) reward, Tensor(g!) done, Tensor(h!) any_done, Tensor(i!)? seeds, int k, "
         "float box, float sensor_range, float collision_distance, float dt=0.1, float v_min=0.005, "
-        "float v_max=2.5, bool periodic=True, bool rigid_boundary=False, int launches=1) -> ()");
+        "float v_max=2.5, bool periodic=True, bool rigid_boundary=False, int launches=1, "
+        "bool normalize_distance=False) -> ()");
     m.def(
         "step_uw(Tensor(a!) pos, Tensor heading, Tensor(b!) prev_heading, Tensor action, Tensor mem_in, "
         "Tensor(c!) mem_out, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
         "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!)? seeds, int k, float box, float sensor_range, "
-        "float collision_distance, float dt=0.1, bool rigid_boundary=False, int launches=1) -> ()");
+        "float collision_distance, float dt=0.1, bool rigid_boundary=False, int launches=1, "
+        "bool normalize_distance=False) -> ()");
+    m.def(
+        "rollout_uw(Tensor(a!) pos, Tensor heading, Tensor(b!) prev_heading, Tensor actions, Tensor mem_in, "
+        "Tensor(c!) mem_out, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
+        "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!) obs_out, Tensor(k!) reward_out, Tensor(l!) done_out, "
+        "Tensor(m!) any_done_out, Tensor(n!)? seeds, int k, float box, float sensor_range, float collision_distance, "
+        "float dt=0.1, bool rigid_boundary=False, bool normalize_distance=False) -> ()");
     m.def(
         "step_uw_discrete(Tensor(a!) pos, Tensor(b!) heading, Tensor(c!) prev_heading, Tensor action_id, "
         "Tensor? noise, Tensor table, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
         "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!) status, Tensor(l!)? seeds, int k, float box, "
         "float sensor_range, float collision_distance, float dt=0.1, float v_max=2.5, bool rigid_boundary=False, "
-        "float noise_std=0.1, int seed=0, int rng_offset=0, int launches=1) -> ()");
+        "float noise_std=0.1, int seed=0, int rng_offset=0, int launches=1, bool normalize_distance=False) "
+        "-> ()");
     m.def(
         "step_flock(Tensor(a!) pos, Tensor(b!) vel, Tensor action, Tensor mem_in, Tensor(c!) mem_out, "
         "Tensor(d!) dnn, Tensor(e!)? nn_idx, Tensor(f!) reward, Tensor(g!) done, Tensor(h!) any_done, "
         "Tensor(i!)? seeds, int k, float box, float collision_distance, float dt=0.1, "
-        "bool rigid_boundary=False, int launches=1) -> ()");
+        "bool rigid_boundary=False, int launches=1, bool normalize_distance=False) -> ()");
     m.def(
         "step_v2_store(Tensor(a!) pos, Tensor(b!) heading, Tensor action, Tensor(c!) vel, Tensor(d!) dnn, "
         "Tensor(e!)? nn_idx, Tensor(f!) reward, Tensor(g!) done, Tensor(h!) any_done, Tensor(i!)? seeds, "
         "Tensor(j!)[] ring, Tensor(k!)? ring_actor_state, Tensor(l!)? ring_actor_new_state, Tensor prev_obs, "
         "int[] ring_meta, int k, float box, float sensor_range, float collision_distance, float dt=0.1, "
-        "float v_min=0.005, float v_max=2.5, bool periodic=True, bool rigid_boundary=False, int launches=1) -> ()");
+        "float v_min=0.005, float v_max=2.5, bool periodic=True, bool rigid_boundary=False, int launches=1, "
+        "bool normalize_distance=False) -> ()");
     m.def(
         "step_uw_discrete_store(Tensor(a!) pos, Tensor(b!) heading, Tensor(c!) prev_heading, Tensor action_id, "
         "Tensor? noise, Tensor table, Tensor(d!) vel, Tensor(e!) dnn, Tensor(f!)? nn_idx, Tensor(g!) reward, "
         "Tensor(h!) done, Tensor(i!) any_done, Tensor(j!) status, Tensor(l!)? seeds, Tensor(m!)[] ring, "
         "Tensor prev_obs, int[] ring_meta, int k, float box, float sensor_range, float collision_distance, "
         "float dt=0.1, float v_max=2.5, bool rigid_boundary=False, float noise_std=0.1, int seed=0, "
-        "int rng_offset=0, int launches=1) -> ()");
+        "int rng_offset=0, int launches=1, bool normalize_distance=False) -> ()");
     m.def(
         "knn(Tensor pos, int k, float box, float sensor_range=14.0, bool periodic=True, bool clamp=True) "
         "-> (Tensor dnn, Tensor nn_idx)");
@@ -504,12 +571,14 @@ TORCH_LIBRARY(flock, m) {
         "reset(Tensor(a!) pos, Tensor(b!) dnn, Tensor(c!)? heading, Tensor(d!)? prev_heading, Tensor(e!)? vel, "
         "Tensor(f!)? nn_idx, Tensor(g!)? mem, Tensor(h!)? valid, Tensor? env_mask, int variant, int k, "
         "float range_lo, float range_hi, float box, float sensor_range, float check_distance, "
-        "bool rigid_boundary=False, int max_attempts=64, int seed=0, int rng_offset=0, int repair_rounds=0) -> ()");
+        "bool rigid_boundary=False, int max_attempts=64, int seed=0, int rng_offset=0, int repair_rounds=0, "
+        "bool normalize_distance=False) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(flock, CUDA, m) {  // ROCm builds of PyTorch dispatch HIP tensors under the CUDA key
     m.impl("step_v2", &step_v2_hip);
     m.impl("step_uw", &step_uw_hip);
+    m.impl("rollout_uw", &rollout_uw_hip);
     m.impl("step_uw_discrete", &step_uwd_hip);
     m.impl("step_flock", &step_flock_hip);
     m.impl("step_v2_store", &step_v2_store_hip);
@@ -521,6 +590,7 @@ TORCH_LIBRARY_IMPL(flock, CUDA, m) {  // ROCm builds of PyTorch dispatch HIP ten
 TORCH_LIBRARY_IMPL(flock, Meta, m) {
     m.impl("step_v2", &step_v2_meta);
     m.impl("step_uw", &step_uw_meta);
+    m.impl("rollout_uw", &rollout_uw_meta);
     m.impl("step_uw_discrete", &step_uwd_meta);
     m.impl("step_flock", &step_flock_meta);
     m.impl("step_v2_store", &step_v2_store_meta);

@@ -298,6 +298,7 @@ struct ScPipeline : torch::CustomClassHolder {
     }
 
     int64_t gated() const { return flock_sc_pipeline_gated(pipe); }
+    int64_t gated_learns() const { return flock_sc_pipeline_gated_learns(pipe); }
 
     // the device gate's guard (flock_sc_pipeline_mark): wait = true records an event behind everything env_stream holds
     // now, which the next learn's round waits for on the learner stream; wait = false declares that only the caller's
@@ -523,6 +524,7 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         .def("flush", &ScPipeline::flush)
         .def("verify", &ScPipeline::verify)
         .def("gated", &ScPipeline::gated)
+        .def("gated_learns", &ScPipeline::gated_learns)
         .def("set_gate", &ScPipeline::set_gate)
         .def("mark", &ScPipeline::mark)
         .def_static("stream", &ScPipeline::stream)

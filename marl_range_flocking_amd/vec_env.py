@@ -182,12 +182,13 @@ class VecFlockEnv:
         if env_mask is not None:
             env_mask = env_mask.to(device=self.device, dtype=torch.bool).contiguous()
         heading = self.headings if c.variant != "flock" else None
-        if self._torch_ops is not None and not c.normalize_distance:
+        if self._torch_ops is not None:
             self._torch_ops.reset(self.positions, b["dnn"], heading, self.prev_headings, self.velocities, b["idx"],
                                   b["mem"], self.valid, env_mask, ops.VARIANT_IDS[c.variant], self.k,
                                   float(c.range_start[0]), float(c.range_start[1]), self.box, c.sensor_range,
                                   c.reset_check_distance, c.rigid_boundary, c.max_reset_attempts,
-                                  _seed64(c.seed), _seed64(self._rng_offset), c.reset_repair_rounds)
+                                  _seed64(c.seed), _seed64(self._rng_offset), c.reset_repair_rounds,
+                                  bool(c.normalize_distance))
         else:
             ops.reset(c.variant, self.positions, b["dnn"], k=self.k, range_start=c.range_start, box=self.box,
                       sensor_range=c.sensor_range, check_distance=c.reset_check_distance, heading=heading,
@@ -225,21 +226,22 @@ class VecFlockEnv:
         c = self.cfg
         common = (self.k, self.box)
         L = c.step_launches
+        nd = bool(c.normalize_distance)
         if c.variant == "v2":
             if ring is None:
                 T.step_v2(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"], self.reward,
                           self.done, self.any_done, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
-                          c.v_min, c.max_linear_velocity, c.periodic, c.rigid_boundary, L)
+                          c.v_min, c.max_linear_velocity, c.periodic, c.rigid_boundary, L, nd)
             else:
                 T.step_v2_store(self.positions, self.headings, a, self.velocities, dst["dnn"], dst["idx"],
                                 self.reward, self.done, self.any_done, self.seeds, ring.fields, ring.actor_state,
                                 ring.actor_new_state, src["dnn"], ring.meta, *common, c.sensor_range,
                                 c.collision_distance, dt, c.v_min, c.max_linear_velocity, c.periodic,
-                                c.rigid_boundary, L)
+                                c.rigid_boundary, L, nd)
         elif c.variant == "uw":
             T.step_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"], self.velocities,
                       dst["dnn"], dst["idx"], self.reward, self.done, self.any_done, self.seeds, *common,
-                      c.sensor_range, c.collision_distance, dt, c.rigid_boundary, L)
+                      c.sensor_range, c.collision_distance, dt, c.rigid_boundary, L, nd)
         elif c.variant == "uw_discrete":
             if noise is not None:
                 noise = torch.as_tensor(noise, device=self.device, dtype=torch.float32).reshape(
@@ -249,18 +251,18 @@ class VecFlockEnv:
                                    self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
                                    self.status, self.seeds, *common, c.sensor_range, c.collision_distance, dt,
                                    c.max_linear_velocity, c.rigid_boundary, 0.1, _seed64(c.seed),
-                                   _seed64(self._rng_offset), L)
+                                   _seed64(self._rng_offset), L, nd)
             else:
                 T.step_uw_discrete_store(self.positions, self.headings, self.prev_headings, a, noise, self.table,
                                          self.velocities, dst["dnn"], dst["idx"], self.reward, self.done,
                                          self.any_done, self.status, self.seeds, ring.fields, src["dnn"], ring.meta,
                                          *common, c.sensor_range, c.collision_distance, dt, c.max_linear_velocity,
-                                         c.rigid_boundary, 0.1, _seed64(c.seed), _seed64(self._rng_offset), L)
+                                         c.rigid_boundary, 0.1, _seed64(c.seed), _seed64(self._rng_offset), L, nd)
             self._rng_offset += 1
         else:
             T.step_flock(self.positions, self.velocities, a, src["mem"], dst["mem"], dst["dnn"], dst["idx"],
                          self.reward, self.done, self.any_done, self.seeds, *common, c.collision_distance, dt,
-                         c.rigid_boundary, L)
+                         c.rigid_boundary, L, nd)
 
     def _step_plan(self, a, noise, dt, src, dst, nxt, ring):
         """The step through the C ABI (ops.*): a launch plan per buffer parity (fixed buffers, so later steps skip
@@ -298,6 +300,40 @@ class VecFlockEnv:
                            self.reward, self.done, self.any_done, seeds=self.seeds, launches=c.step_launches,
                            **common)
 
+    def rollout(self, actions, dt=None, out=None):
+        """K vectorized steps in one call, for the random-action rollout regime where the K actions are known up front
+        (gym_flock_uw: torch.ops.flock.rollout_uw, flock_rollout_uw; BASELINE config 2 runs all K steps in ONE launch
+        with the env state kept on chip). actions [K, E, N, 2] f32. Returns (obs [K, E, N, 4, k], reward [K, E, N],
+        done [K, E, N], any_done [K, E]): step t's observation memory, reward and dones, exactly what K step(actions[t])
+        calls return (tests/test_gpu_rollout.py); the env then holds the state after the last step. out: a tuple of
+        those four tensors to write into (reused across calls), or None."""
+        c = self.cfg
+        if c.variant != "uw":
+            raise NotImplementedError("rollout is built for gym_flock_uw (config 2); step() the other variants")
+        if self._torch_ops is None:
+            raise RuntimeError('rollout runs through torch.ops.flock (VecFlockEnv(launch="torch"))')
+        dt = c.dt if dt is None else float(dt)
+        E, N, k = self.E, self.N, self.k
+        a = torch.as_tensor(actions, device=self.device, dtype=torch.float32)
+        K = a.shape[0]
+        a = a.reshape(K, E, N, 2).contiguous()
+        if out is None:
+            out = (torch.empty(K, E, N, 4, k, device=self.device), torch.empty(K, E, N, device=self.device),
+                   torch.empty(K, E, N, dtype=torch.bool, device=self.device),
+                   torch.empty(K, E, dtype=torch.bool, device=self.device))
+        if K == 0:
+            return out
+        nxt = self._cur ^ 1
+        src, dst = self._bufs[self._cur], self._bufs[nxt]
+        self._torch_ops.rollout_uw(self.positions, self.headings, self.prev_headings, a, src["mem"], dst["mem"],
+                                   self.velocities, dst["dnn"], dst["idx"], self.reward, self.done, self.any_done,
+                                   *out, self.seeds, k, self.box, c.sensor_range, c.collision_distance, dt,
+                                   c.rigid_boundary, bool(c.normalize_distance))
+        self._cur = nxt
+        self.steps += K
+        _DEVICE_WRITES[0] += K
+        return out
+
     def step(self, action, noise=None, dt=None, copy=False, ring=None, auto_reset=False):
         """One vectorized step. action: [E,N,2] f32 (v2: [lin, ang]; uw/flock: velocity/acceleration) or
         [E,N] integer ids (uw_discrete). Returns (obs, reward [E,N], (done [E,N], any_done [E]), info).
@@ -322,9 +358,9 @@ class VecFlockEnv:
             a = torch.as_tensor(action, device=self.device, dtype=torch.float32).reshape(E, N, 2).contiguous()
         if ring is not None and c.variant not in ("v2", "uw_discrete"):
             raise NotImplementedError("the fused replay insert is built for the v2 and uw_discrete steps")
-        # the custom ops (default); launch="plan" and normalize_distance steps take the validated C-ABI launch plans
-        # (ops.StepPlan; FlockStepExt carries the normalize_distance flag)
-        T = self._torch_ops if not c.normalize_distance else None
+        # the custom ops (default, normalize_distance included: the ops' flag); launch="plan" takes the validated
+        # C-ABI launch plans (ops.StepPlan)
+        T = self._torch_ops
         if T is not None:
             self._step_torch(T, a, noise, dt, src, dst, ring)
         else:

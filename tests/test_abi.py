@@ -103,6 +103,9 @@ def test_shared_critic_round_and_pipeline_argument_checks(lib):
     assert not lib.flock_sc_pipeline_create(1, ctypes.byref(u), ctypes.byref(rows), ctypes.byref(rows))
     assert "n_slots" in lib.flock_learn_last_error().decode()
     assert lib.flock_sc_pipeline_flush(None, None) == -3
+    assert lib.flock_sc_pipeline_mark(None, None, 1) == -3
+    assert lib.flock_sc_pipeline_gated_learns(None) == 0
+    assert lib.flock_sc_pipeline_comm_stream(None) is None
     assert lib.flock_sc_pipeline_learn(None, None, None, 1, 0, 0, 0) == -3
     assert lib.flock_sc_pipeline_set_dp(None, None, 0, 0, 0, None, None, None) == -3
 

@@ -139,9 +139,10 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
     ls = torch.cuda.Stream(device=cuda)
     main = torch.cuda.current_stream(cuda)
     losses = []
-    for a in agents:
+    for i, a in enumerate(agents):
         ser.learn(a)
         losses.append(ser.losses.clone())
+        pip.pipeline_mark(main.cuda_stream, wait=i % 3 != 2)  # the gate's guard: an event, or declared bounded
         assert pip.pipeline_learn(a, main.cuda_stream, ls.cuda_stream)
     pip.pipeline_flush(ls.cuda_stream)
     pip.pipeline_flush(ls.cuda_stream)  # nothing pending: a no-op
@@ -149,6 +150,7 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
     torch.cuda.synchronize()
     pip.pipeline_check()  # no round gave up waiting for its snapshot (device-side gate)
     assert pip.pipeline().gated() == int(handoff == "gate")
+    assert pip.pipeline().gated_learns() == (len(agents) if handoff == "gate" else 0)
     for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg, pip.critic.exp_avg),
                  (ser.critic.exp_avg_sq, pip.critic.exp_avg_sq), (ser.actors.data, pip.actors.data),
                  (ser.actors.exp_avg, pip.actors.exp_avg), (ser.actors.target, pip.actors.target),
@@ -157,37 +159,64 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
         assert torch.equal(x, y)
 
 
-def test_gate_waits_behind_a_busy_env_stream(cuda):
-    """The device-side gate when the env stream is held up: a 0.5-s kernel enqueued on the env stream before the
-    learns, so every round's critic blocks start polling long before their snapshot runs (their wait is bounded at
-    2 s). No wait gives up, and the results are bitwise the serial learn() sequence."""
-    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+def _sleep_s(seconds):
+    """A kernel that holds the current stream for about `seconds` (s_memtime cycles at >= 2.1 GHz)."""
+    torch.cuda._sleep(int(2.5e9 * seconds))
 
-    ser = SharedCriticLearner(10, 4, device=cuda, seed=7, batch_size=64, buffer_size=500, snapshot=False)
-    pip = SharedCriticLearner(10, 4, device=cuda, seed=7, batch_size=64, buffer_size=500, snapshot=True, n_slots=3,
-                              handoff="gate")
-    g = torch.Generator(device=cuda).manual_seed(9)
-    n = 300
-    rows = (torch.rand(n, 4, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g),
-            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, 4, device=cuda, generator=g),
-            torch.rand(n, device=cuda, generator=g) > 0.5)
-    for L in (ser, pip):
-        L.store_transitions(*rows)
-    ls = torch.cuda.Stream(device=cuda)
-    main = torch.cuda.current_stream(cuda)
-    torch.cuda.synchronize()
-    torch.cuda._sleep(int(2.4e9 * 0.5))  # ~0.5 s on the env stream, ahead of every snapshot
-    for a in (1, 2, 3):
-        ser.learn(a)
-        assert pip.pipeline_learn(a, main.cuda_stream, ls.cuda_stream)
-    pip.pipeline_flush(ls.cuda_stream)
-    main.wait_stream(ls)
-    torch.cuda.synchronize()
-    assert pip.pipeline().gated() == 1
-    pip.pipeline_check()
-    for x, y in ((ser.critic.data, pip.critic.data), (ser.actors.data, pip.actors.data),
-                 (ser.actors.target, pip.actors.target), (ser.losses, pip.losses)):
-        assert torch.equal(x, y)
+
+@pytest.mark.parametrize("path", ["no-mark", "mark", "loop"])
+def test_learn_never_fails_behind_a_busy_env_stream(path, cuda):
+    """A learn() must never fail because the env stream is busy (agent_simple_shared_critic.py:115-117: learn() is
+    synchronous and never fails): a ~3-s kernel on the env stream ahead of the learns, longer than the gate's 2-s
+    bound. Without a mark the learns take the event hand-off; with a mark (wait) behind the sleep, the round first
+    waits for the mark on the learner stream (no CU held) and the gate spins only over the env step; the C++ loop
+    marks its first learning step the same way. Every case: no error word, bitwise the serial learn() sequence."""
+    from marl_range_flocking_amd import FlockConfig, VecFlockEnv
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
+
+    E, Na, steps = 64, 16, 5
+    g = torch.Generator(device=cuda).manual_seed(2)
+    pool = [torch.stack([torch.rand(E, Na, device=cuda, generator=g),
+                         torch.rand(E, Na, device=cuda, generator=g) * 3 - 1.5], -1).contiguous() for _ in range(3)]
+    out = []
+    for mode in ("serial", path):
+        env = VecFlockEnv(FlockConfig(variant="v2", num_envs=E, num_agents=Na, k=4, collision_distance=2.5,
+                                      range_start=(0, 63.0), sensor_range=14.0), device=cuda)
+        gp = torch.Generator(device=cuda).manual_seed(5)
+        env.positions.copy_(torch.rand(E, Na, 2, device=cuda, generator=gp) * 63.0)
+        env.headings.copy_(torch.rand(E, Na, device=cuda, generator=gp) * 4.7)
+        hook = SharedCriticBench(env, device=cuda, seed=7, overlap=mode != "serial", buffer_size=2000)
+        L = hook.learner
+        main = torch.cuda.current_stream(cuda)
+        # the ring holds a batch before the timed steps (one env step of 64 x 16 transitions)
+        env.step(pool[0], ring=L.replay_slots(E * Na))
+        torch.cuda.synchronize()
+        if mode == "loop":
+            _sleep_s(3.0)
+            hook.run_steps(1, steps, pool)
+        else:
+            for s in range(1, 1 + steps):
+                if mode == "serial":
+                    hook.step(s, pool[s % 3])
+                    continue
+                ring = L.replay_slots(E * Na)
+                if s == 2:
+                    _sleep_s(3.0)  # foreign work on the env stream between two learns
+                if mode == "mark":
+                    L.pipeline_mark(main.cuda_stream)  # behind the sleep
+                env.step(pool[s % 3], ring=ring)
+                hook.after(s, pool[s % 3])
+        hook.finish()
+        torch.cuda.synchronize()
+        if mode != "serial":
+            L.pipeline_check()  # no error word
+            gl = L.pipeline().gated_learns()
+            assert gl == (0 if mode == "no-mark" else steps), gl
+        C, A = L.critic, L.actors
+        out.append([C.data.clone(), C.exp_avg_sq.clone(), A.data.clone(), A.target.clone(), L.actor_steps.clone(),
+                    L.losses.clone(), env.positions.clone()])
+    for i, (x, y) in enumerate(zip(*out)):
+        assert torch.equal(x, y), i
 
 
 def test_specialised_row_kernels_equal_generic(cuda):

@@ -46,6 +46,19 @@ def test_opcheck_step_uw(flock, cuda):
     torch.library.opcheck(flock.step_uw.default, args, test_utils=TESTS)
 
 
+@pytest.mark.parametrize("N", [64, 32], ids=["one-launch", "step-launches"])
+def test_opcheck_rollout_uw(flock, cuda, N):
+    st = _state(cuda, N=N)
+    E, k, K = 4, 4, 3
+    mem_in, mem_out = torch.rand(E, N, 4, k, device=cuda), torch.zeros(E, N, 4, k, device=cuda)
+    prev = torch.zeros(E, N, device=cuda)
+    outs = (torch.zeros(K, E, N, 4, k, device=cuda), torch.zeros(K, E, N, device=cuda),
+            torch.zeros(K, E, N, dtype=torch.bool, device=cuda), torch.zeros(K, E, dtype=torch.bool, device=cuda))
+    args = (st["pos"], st["heading"], prev, torch.rand(K, E, N, 2, device=cuda), mem_in, mem_out, st["vel"],
+            st["dnn"], None, st["reward"], st["done"], st["any_done"], *outs, None, k, 60.0, 14.0, 2.5)
+    torch.library.opcheck(flock.rollout_uw.default, args, test_utils=TESTS)
+
+
 def test_opcheck_step_uw_discrete(flock, cuda):
     st = _state(cuda)
     E, N, k = 4, 32, 4
@@ -88,12 +101,16 @@ def test_ops_errors(flock, cuda):
         flock.step_v2(*dict(st, action=st["action"].double()).values(), None, 4, 60.0, 14.0, 2.5)
 
 
-@pytest.mark.parametrize("variant,N", [("v2", 64), ("v2", 256), ("uw", 64), ("uw_discrete", 128), ("flock", 16)])
-def test_torch_ops_path_is_bitwise_the_plan_path(variant, N, cuda):
+@pytest.mark.parametrize("variant,N,norm", [("v2", 64, False), ("v2", 256, False), ("uw", 64, False),
+                                            ("uw_discrete", 128, False), ("flock", 16, False), ("uw", 64, True),
+                                            ("uw_discrete", 128, True), ("flock", 16, True)])
+def test_torch_ops_path_is_bitwise_the_plan_path(variant, N, norm, cuda):
+    """norm: normalize_distance=True steps and resets through the ops' normalize_distance flag (the full-scan
+    kernels, FlockStepExt.normalize_distance / flock_reset_ext2) against the plan path."""
     E, k = 16, 4
     box = float(round((250 * N) ** 0.5))
-    cfg = FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5, range_start=(0, box),
-                      sensor_range=14.0, seed=7, max_reset_attempts=8)
+    cfg = FlockConfig(variant=variant, num_envs=E, num_agents=N, k=k, collision_distance=2.5 if not norm else 0.05,
+                      range_start=(0, box), sensor_range=14.0, seed=7, max_reset_attempts=8, normalize_distance=norm)
     envs = [VecFlockEnv(cfg, device=cuda, launch=o) for o in ("plan", "torch")]
     for e in envs:
         e.reset()
