@@ -55,7 +55,38 @@ BYTES_PER_AGENT_STEP = {"v2": 93, "uw": 149, "uw_discrete": 69, "flock": 129}  #
 # record: state, next_state 16 each (actor_state / actor_next_state alias them: MADDPGLearner(shared_obs=True)) +
 # action 8 + reward 4 + done 4; VDN team transition: s 16 + a (f32 id) 4 + r 4 + s' 16 (+ one done flag per env: 4 / N)
 RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 48, "vdn": 16 + 40}
+# the uw rollout kernel's HBM bytes per agent-step (state on chip): action 8 r + observation memory 64 w + reward 4 w +
+# done 1 w (+ any_done per env, and the state once per launch)
+ROLLOUT_MOVED_BYTES = 8 + 64 + 4 + 1
 EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 4))  # steps between HIP-event-timed env launches (timed region)
+
+
+class DevEvent:
+    """A timing event whose record is a DEVICE-scope release (hipEventReleaseToDevice). torch.cuda.Event records a
+    system-scope fence (an L2 writeback + invalidation on this GPU) each time: inside the timed region that would
+    perturb the very kernels it times. Same interface as torch.cuda.Event for what bench.py uses (record, elapsed_time,
+    cuda_event)."""
+    _hip = None
+
+    def __init__(self):
+        import ctypes
+
+        if DevEvent._hip is None:
+            DevEvent._hip = ctypes.CDLL("libamdhip64.so")
+        self._ct = ctypes
+        h = ctypes.c_void_p()
+        assert DevEvent._hip.hipEventCreateWithFlags(ctypes.byref(h), ctypes.c_uint(0x40000000)) == 0
+        self.cuda_event = h.value
+
+    def record(self, stream=None):
+        s = (stream or torch.cuda.current_stream()).cuda_stream
+        assert DevEvent._hip.hipEventRecord(self._ct.c_void_p(self.cuda_event), self._ct.c_void_p(s)) == 0
+
+    def elapsed_time(self, end):
+        ms = self._ct.c_float()
+        assert DevEvent._hip.hipEventElapsedTime(self._ct.byref(ms), self._ct.c_void_p(self.cuda_event),
+                                                 self._ct.c_void_p(end.cuda_event)) == 0
+        return ms.value
 
 
 def binding(valu, hbm_frac, alone_ms, alg_bytes):
@@ -107,10 +138,18 @@ def parse():
     ap.add_argument("--diag-prewarm-ms", type=float, default=0.0,
                     help="diagnostics only (never a bench line): keep the GPU busy with matmuls for this long before "
                          "the warmup steps (clock / power-state probe)")
+    ap.add_argument("--diag-knob", action="append", default=[],
+                    help="diagnostics only (A/B): name=value for flock_set_diag before anything is built, e.g. "
+                         "sc_event_system_scope=1 (the learner pipeline's events as system-scope fences)")
     ap.add_argument("--train-overlap", default="auto", choices=["auto", "0", "1"],
                     help="configs 4 / 5: train() on its own stream beside the following env steps (auto: on for VDN, "
                          "where it measured -3.5 %% per step; off for RNN-MADDPG, where it measured flat and its "
                          "update's HBM traffic slows the env launches it overlaps, profiles/r05/trainov/)")
+    ap.add_argument("--rollout", type=int, default=None,
+                    help="uw with no learner (config 2): the timed steps as VecFlockEnv.rollout calls of this many "
+                         "steps each (flock_rollout_uw: all of them in ONE launch at N = 64, k = 4, the env state on "
+                         "chip; the random-action regime, actions known up front). Default 20 for config 2, 0 "
+                         "(one launch per step) otherwise")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
                          "results; the env kernel time is unchanged by it); configs 4 / 5: see --train-overlap; "
@@ -471,6 +510,13 @@ def main():
     world, rank, dev = setup_dist(args)
     from marl_range_flocking_amd import FlockConfig, VecFlockEnv
 
+    if args.diag_knob:
+        from marl_range_flocking_amd import _native
+
+        for kv in args.diag_knob:
+            name, val = kv.split("=")
+            assert _native.lib().flock_set_diag(name.encode(), int(val)) == 0, kv
+
     E, N, k = args.envs, args.agents, args.k
     launches = args.step_launches or (3 if args.learner == "shared_critic" and args.overlap else 1)
     box = float(round(np.sqrt(250.0 * N)))  # main.py density: 10 agents in 50x50
@@ -506,6 +552,23 @@ def main():
     elif args.learner == "maddpg_rnn":
         hook = MADDPGBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap) and args.train_overlap == "1")
 
+    R = args.rollout if args.rollout is not None else (20 if args.config == 2 else 0)
+    use_rollout = R > 0 and hook is None and args.variant == "uw"
+    if use_rollout:  # the action stack of a rollout call: the pool's actions, resident before timing
+        acts = torch.stack([pool[i % len(pool)] for i in range(R)]).contiguous()
+        r_out = env.rollout(acts[:1])
+        r_out = tuple(torch.empty((R,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev) for o in r_out)
+
+    def rollout_steps(s0, n, evs_r=None):
+        for s in range(s0, s0 + n, R):
+            r = min(R, s0 + n - s)
+            e = evs_r.get(s - s0) if evs_r is not None else None
+            if e is not None:
+                e[0].record(stream)
+            env.rollout(acts[:r], out=tuple(o[:r] for o in r_out))
+            if e is not None:
+                e[1].record(stream)
+
     def one_step(s, ev=None):
         a = pool[s % len(pool)]
         ring = hook.before(s) if hook is not None else None
@@ -530,6 +593,8 @@ def main():
     use_loop = bool(args.loop) and hook is not None and getattr(hook, "can_loop", lambda: False)()
     if use_loop:
         hook.run_steps(0, args.warmup, pool)
+    elif use_rollout:
+        rollout_steps(0, args.warmup)
     else:
         for s in range(args.warmup):
             one_step(s)
@@ -538,13 +603,12 @@ def main():
     torch.cuda.synchronize(dev)
     # the env kernel's HIP-event timing: every EV_EVERY-th step of the timed region (two timing markers per step
     # would add host and queue work of their own to a ~13-us launch-bound step)
-    ev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for s in range(0, args.steps, EV_EVERY)}
+    ev = {s: (DevEvent(), DevEvent()) for s in range(0, args.steps, R if use_rollout else EV_EVERY)}
     evs = [e for s in sorted(ev) for e in ev[s]]
     for e in evs:  # create the HIP events outside the timed region
         e.record(stream)
 
-    span = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    span = (DevEvent(), DevEvent())
     for e in span:
         e.record(stream)
     barrier(world)
@@ -555,6 +619,8 @@ def main():
         torch.cuda._sleep(int(args.diag_presleep_us * 1e-6 * 2.1e9))  # ~2.1 GHz shader clock under load
     if use_loop:
         hook.run_steps(args.warmup, args.steps, pool, evs, EV_EVERY)
+    elif use_rollout:
+        rollout_steps(args.warmup, args.steps, ev)
     else:
         for s in range(args.steps):
             one_step(args.warmup + s, ev.get(s))
@@ -580,13 +646,16 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
+    if use_rollout:  # per step: each timed rollout call over the steps it ran
+        kern_ms = float(np.mean([a.elapsed_time(b) / min(R, args.steps - s) for s, (a, b) in ev.items()]))
+    else:
+        kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev.values()]))
     # the env step alone (after the timed region, no learner beside it, as ONE launch): what the kernel does when it
     # has the GPU to itself
     alone_ms = None
     if hook is not None:
         env.set_param("step_launches", 1)
-        ev_alone = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        ev_alone = [(DevEvent(), DevEvent()) for _ in range(10)]
         for i, (a0, a1) in enumerate(ev_alone):
             a = pool[i % len(pool)]
             ring = hook.before(args.warmup + args.steps + i)
@@ -617,7 +686,7 @@ def main():
     ins = RING_BYTES_PER_AGENT_STEP.get(args.learner, 0)
     kern_s = kern_ms * 1e-3
     achieved = bpa * E * N / kern_s / 1e9
-    tag = f"{args.variant}{'_ring' if fused_ring else ''}_N{N}_E{E}"
+    tag = f"{args.variant}{'_ring' if fused_ring else ''}{'_rollout' if use_rollout else ''}_N{N}_E{E}"
     prof = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
 
     def pmc(name):
@@ -659,8 +728,10 @@ def main():
         "gpu_span_ms_per_step": span[0].elapsed_time(span[1]) / args.steps,
         **({"diag_presleep_us": args.diag_presleep_us} if args.diag_presleep_us > 0 else {}),
         **({"diag_prewarm_ms": args.diag_prewarm_ms} if args.diag_prewarm_ms > 0 else {}),
+        **({"diag_knobs": args.diag_knob} if args.diag_knob else {}),
         "host_enqueue_us_per_step": host_us,
         "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
+                      f"VecFlockEnv.rollout: {R} steps per call (torch.ops.flock.rollout_uw)" if use_rollout else
                       "one Python step per vectorized step (torch.ops.flock)"),
         "snapshot_handoff": handoff,
         "higher_is_better": True,
@@ -676,9 +747,13 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": hbm_frac, "traffic": traffic,
-                     "kernel": f"step_kernel<{k + 2},{'periodic' if periodic else 'euclidean'}"
-                               f"{',cells' if N >= 128 else ''}>" + (" + fused replay insert" if fused_ring else ""),
+                     "kernel": (f"rollout_uw_kernel ({R} steps per launch, env state on chip)" if use_rollout
+                                and N == 64 and k == 4 else
+                                f"step_kernel<{k + 2},{'periodic' if periodic else 'euclidean'}"
+                                f"{',cells' if N >= 128 else ''}>" + (" + fused replay insert" if fused_ring else "")),
                      "kernel_ms": kern_ms, "bytes_per_agent_step": bpa,
+                     **({"rollout_steps_per_launch": R,
+                         "moved_bytes_per_agent_step": ROLLOUT_MOVED_BYTES} if use_rollout else {}),
                      "insert_bytes_per_agent_step": ins,
                      "achieved_incl_insert": (bpa + ins) * E * N / kern_s / 1e9,
                      "valu": valu,
@@ -688,9 +763,13 @@ def main():
                      "kernel_alone_ms": alone_ms,
                      "frac_alone": (bpa * E * N / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if alone_ms else None,
                      "valu_frac_alone": valu["frac_alone"] if valu else None,
-                     "note": "kernel_ms / frac / valu: HIP events around every 4th env step of the timed region (the "
-                             "step's launches, with the learner's kernels beside them); *_alone: the same step as one "
-                             "launch with no learner, after the timed region"},
+                     "note": ("kernel_ms / frac: HIP events around every rollout launch of the timed region, per "
+                              "step; frac on SURVEY 8(d)'s 149-B accounting (a single step reads and rewrites the "
+                              "state and the memory); the rollout moves the action read and the observation / "
+                              "reward / done writes (moved_bytes_per_agent_step)" if use_rollout else
+                              "kernel_ms / frac / valu: HIP events around every 4th env step of the timed region (the "
+                              "step's launches, with the learner's kernels beside them); *_alone: the same step as one "
+                              "launch with no learner, after the timed region")},
     }
     if (hook is not None and args.learner == "shared_critic" and world == 1 and args.policy_steps > 0
             and args.variant == "v2"):

@@ -2042,7 +2042,8 @@ Params base(int E, int N, int k, float box) {
 // ---------------------------------------------------------------------------------------------------------------
 // C ABI
 
-void flock_sc_diag_no_spec(bool v);  // flock_sc.hip
+void flock_sc_diag_no_spec(bool v);       // flock_sc.hip
+void flock_sc_diag_event_system(bool v);  // flock_sc.hip
 
 extern "C" {
 
@@ -2063,6 +2064,8 @@ int flock_set_diag(const char* name, int value) {
         k.pf = value;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
+    else if (!strcmp(name, "sc_event_system_scope"))
+        flock_sc_diag_event_system(value != 0);
     else
         return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
     return FLOCK_OK;

@@ -1396,7 +1396,6 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
             }
         }
     } else if (bx >= adam0) {  // Adam of gradients the bwd launch wrote: every load first, then the updates
-        __syncthreads();
         const int64_t e0 = ga.adam_lo + (int64_t)(bx - adam0) * 1024, end = ga.adam_lo + ga.adam_n;
         AdamState st[4];
         float gi[4];
@@ -1407,6 +1406,9 @@ __device__ __forceinline__ void grad_adam_body(const GradAdam& ga, int bx, int n
             st[q] = e < end ? adam_load(ga, base + e) : AdamState{0.f, 0.f, 0.f, 0.f};
             gi[q] = e < end ? ga.grad[gbase + e] : 0.0f;
         }
+        // the bias corrections of thread 0 (its step load and pow) after the loads are issued: one memory round trip
+        // for the whole block instead of the step load's followed by the element loads'
+        __syncthreads();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int64_t e = e0 + q * 256 + tid;
@@ -1995,6 +1997,7 @@ __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows
 
 // the "sc_no_spec" diagnostics knob of flock_set_diag (flock_env.hip)
 void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
+void flock_sc_diag_event_system(bool v);  // below (the pipeline's event flags)
 
 extern "C" {
 
@@ -2154,6 +2157,15 @@ struct FlockScPipeline {
 };
 
 namespace {
+// The pipeline's events order work between its streams on ONE device (slot reuse, snapshot hand-offs, the guard
+// mark, the split rounds' actor stream): a device-scope release is all they need. HIP's default event is a system-scope
+// sequentially consistent fence when it is recorded (a cache writeback and invalidation behind the round the event
+// follows: the next round's kernels then start from a cold L2). flock_set_diag("sc_event_system_scope", 1) restores the
+// default for A/B (read when a pipeline is created).
+bool g_sc_event_system = false;
+unsigned pipeline_event_flags() {
+    return hipEventDisableTiming | (g_sc_event_system ? 0u : (unsigned)hipEventReleaseToDevice);
+}
 bool counter_collection() {  // rocprofv3 counter collection serialises dispatches: no spinning consumers under it
     const char* pmc = getenv("ROCPROF_COUNTER_COLLECTION");
     return pmc && pmc[0] && pmc[0] != '0';
@@ -2298,7 +2310,7 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
         actor_job(&p->u[i], p->ja[i]);
         hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};
         for (hipEvent_t* e : evs)
-            if (!rc && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess)
+            if (!rc && hipEventCreateWithFlags(e, pipeline_event_flags()) != hipSuccess)
                 rc = fail(-4, "flock_sc_pipeline_create: event");
         p->used[i] = false;
         p->actor_used[i] = false;
@@ -2321,7 +2333,7 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->mark = 0;
     p->gated_learns = 0;
     p->mark_ev = nullptr;
-    if (!rc && hipEventCreateWithFlags(&p->mark_ev, hipEventDisableTiming) != hipSuccess)
+    if (!rc && hipEventCreateWithFlags(&p->mark_ev, pipeline_event_flags()) != hipSuccess)
         rc = fail(-4, "flock_sc_pipeline_create: event");
     if (!rc && (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
                 hipMemset(p->gate, 0, 4 * sizeof(unsigned long long)) != hipSuccess ||
@@ -2475,7 +2487,7 @@ int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads
                 return fail(-5, "flock_sc_pipeline_set_dp_actor: the slots' buffers must differ");
     }
     if (!p->actor_stream && (hipStreamCreateWithFlags(&p->actor_stream, hipStreamNonBlocking) != hipSuccess ||
-                             hipEventCreateWithFlags(&p->actor_joined, hipEventDisableTiming) != hipSuccess))
+                             hipEventCreateWithFlags(&p->actor_joined, pipeline_event_flags()) != hipSuccess))
         return fail(-4, "flock_sc_pipeline_set_dp_actor: stream");
     delete[] p->last_actor_slot;
     p->last_actor_slot = new int[n_agents];
@@ -2483,8 +2495,8 @@ int flock_sc_pipeline_set_dp_actor(FlockScPipeline* p, float* const* actor_grads
     p->n_agents = n_agents;
     p->actor_floats = actor_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).total;
     if (!p->comm_stream && (hipStreamCreateWithFlags(&p->comm_stream, hipStreamNonBlocking) != hipSuccess ||
-                            hipEventCreateWithFlags(&p->bwd_done, hipEventDisableTiming) != hipSuccess ||
-                            hipEventCreateWithFlags(&p->ar_done, hipEventDisableTiming) != hipSuccess))
+                            hipEventCreateWithFlags(&p->bwd_done, pipeline_event_flags()) != hipSuccess ||
+                            hipEventCreateWithFlags(&p->ar_done, pipeline_event_flags()) != hipSuccess))
         return fail(-4, "flock_sc_pipeline_set_dp_actor: stream");
     p->critic_w2 = critic_off(u0.in_dim, u0.n_actions, u0.fc1, u0.fc2).W2;
     for (int i = 0; i < p->n; ++i) {
@@ -2537,6 +2549,10 @@ int flock_sc_pipeline_check(FlockScPipeline* p) {
 }
 
 int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate_on ? 1 : 0; }
+
+}  // extern "C"
+void flock_sc_diag_event_system(bool v) { g_sc_event_system = v; }
+extern "C" {
 
 void* flock_sc_pipeline_comm_stream(const FlockScPipeline* p) { return p ? (void*)p->comm_stream : nullptr; }
 

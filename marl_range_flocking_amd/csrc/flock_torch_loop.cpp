@@ -333,7 +333,8 @@ struct ScPipeline : torch::CustomClassHolder {
     }
 
     // the snapshot hand-off: 1 the device-side gate (the default on one GPU), 0 cross-queue event waits; returns the
-    // hand-off in use (data-parallel rounds and rocprofv3 counter collection always take the events)
+    // hand-off in use (single-GPU and data-parallel pipelines alike; rocprofv3 counter collection always takes the
+    // events). A learn takes the gate only after a mark (see mark below)
     int64_t set_gate(bool on) {
         const at::OptionalDeviceGuard g(device);
         return flock_sc_pipeline_set_gate(pipe, on ? 1 : 0);

@@ -536,7 +536,8 @@ class SharedCriticLearner:
         learn's critic phase with the previous learn's actor phase, flock_sc_round) on the learner stream, enqueued by
         one call. ONE object per learner: the per-step path (pipeline_learn) and the C++ training loop
         (ScTrainLoop) share its slots and its pending actor phase. The round waits for its snapshot on the device-side
-        gate (handoff="gate", single GPU) or on a cross-queue event. Data-parallel learners (dist_group) run every
+        gate (handoff="gate", single-GPU and data-parallel pipelines alike, for a learn whose env step was marked:
+        pipeline_mark) or on a cross-queue event. Data-parallel learners (dist_group) run every
         round as gradients, one RCCL all-reduce of the critic gradient over the group and the critic Adam launch on
         the learner stream; with dp_split (opt-in) the round's actor gradient is all-reduced over a second group and
         stepped on the pipeline's actor stream, off the learner chain (set_dp_actor); without, one all-reduce of the

@@ -1,4 +1,6 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the env-shard and data-parallel learner plumbing."""
+"""Multi-process (world_size 2, 4 and 8, gloo, CPU) tests of the env-shard and data-parallel learner plumbing: the
+global env split of configs 4 / 5 (8192 / 16384 envs over W ranks), the gradient all-reduce, the replica sync and the
+max-over-ranks timing of bench.py."""
 import os
 import socket
 
@@ -25,7 +27,7 @@ def _worker(rank, world, port, q):
         first, count = dist.env_shard(4099, world, rank)
         spans = [None] * world
         torch.distributed.all_gather_object(spans, (first, count))
-        # gradient all-reduce: mean of per-rank buffers
+        # gradient all-reduce: mean of per-rank buffers (exact: small integers, a power-of-two world)
         g = torch.full((1000,), float(rank + 1))
         dist.allreduce_mean_(g)
         # parameter sync from rank 0 (FlatParams on CPU: only the HIP update kernels need a GPU)
@@ -43,8 +45,9 @@ def _worker(rank, world, port, q):
         q.put((rank, "error", repr(e)))
 
 
-def test_two_rank_gloo_shard_allreduce_sync():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_shard_allreduce_sync(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -55,12 +58,14 @@ def test_two_rank_gloo_shard_allreduce_sync():
         p.join(timeout=60)
     for o in out:
         assert o[1] != "error", o
+    mean = (world + 1) / 2.0
     for rank, spans, g0, gsum, data_u, targ_u, m in out:
         assert sum(c for _, c in spans) == 4099
-        assert spans[0][0] == 0 and spans[1][0] == spans[0][1]
-        assert g0 == pytest.approx(1.5) and gsum == pytest.approx(1500.0)
+        assert spans[0][0] == 0 and all(spans[i + 1][0] == spans[i][0] + spans[i][1] for i in range(world - 1))
+        assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+        assert g0 == mean and gsum == 1000 * mean
         assert data_u == [0.5] and targ_u == [-0.5]
-        assert m == 10.0
+        assert m == 10.0 * (world - 1)
 
 
 def test_env_shard_single_process():

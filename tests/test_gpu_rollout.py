@@ -56,7 +56,7 @@ def _check(envs, actions, out):
         assert torch.equal(getattr(ref, name), getattr(roll, name)), name
     if ref.nn_idx is not None:
         assert torch.equal(ref.nn_idx, roll.nn_idx)
-    assert ref._cur == roll._cur and ref.steps == roll.steps
+    assert ref.steps == roll.steps  # (the buffer parity may differ: a rollout flips the double buffers once)
 
 
 @pytest.mark.parametrize("layout", ["uniform", "dense", "lattice", "edges"])
