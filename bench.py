@@ -759,7 +759,8 @@ def main():
                      "valu": valu,
                      "binding": binding(valu, hbm_frac, alone_ms, bpa * E * N),
                      "step_launches": launches,
-                     "kernel_ms_per_launch": kern_ms / launches,  # compare with rocprofv3's per-dispatch average
+                     # compare with rocprofv3's per-dispatch average
+                     "kernel_ms_per_launch": kern_ms * R if use_rollout else kern_ms / launches,
                      "kernel_alone_ms": alone_ms,
                      "frac_alone": (bpa * E * N / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if alone_ms else None,
                      "valu_frac_alone": valu["frac_alone"] if valu else None,

@@ -1539,23 +1539,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 // the memory frames in registers, each step's positions in LDS. A step's HBM traffic is then its action read and its
 // observation / reward / done writes (77 B per agent-step; a single step also reads and rewrites the state and the
 // memory: the 149 B of SURVEY §8(d)'s accounting), and the launch pays its dispatch and its first loads once per K steps.
-// Lane (w, l) of the 4 waves: agent ia = 16 w + (l & 15), candidate quarter r = l >> 4. The 4 lanes of an agent run
-// its kinematics redundantly, scan candidates [16 r, 16 r + 16) each, and merge their partial top-L key lists by two
-// xor shuffles: the same key set, hence the same result, as the split step kernel's LDS merge. Lane r holds memory
-// frame r, so the memory roll is one shuffle. The centre of mass is the step kernel's fixed power-of-two tree
+// SPL lanes per agent (SPL waves per env; 2 by default): lane r of agent ia runs its kinematics redundantly, scans
+// candidates [r N / SPL, (r + 1) N / SPL), and the SPL partial top-L key lists are merged by xor shuffles: the same key
+// set, hence the same result, as the split step kernel's LDS merge. Lane r holds memory frames [r 4 / SPL, (r + 1) 4 /
+// SPL), so the memory roll is one shuffle. The centre of mass is the step kernel's fixed power-of-two tree
 // (r[i] += r[i + s], s = 32 .. 1) as wave shuffles: the same pairs in the same order, bitwise equal. One workgroup
 // barrier per step (the positions are double-buffered in LDS, so a wave one step ahead never overwrites the positions
 // another wave still scans). The results are bitwise those of K flock_step_uw calls (tests/test_gpu_rollout.py).
 constexpr int kRollN = 64;
-__global__ __launch_bounds__(4 * kRollN) void rollout_uw_kernel(const Params p, int K, const float* __restrict__ actions,
-                                                                float* __restrict__ obs, float* __restrict__ rew_out,
-                                                                uint8_t* __restrict__ done_out,
-                                                                uint8_t* __restrict__ any_out) {
-    constexpr int N = kRollN, L = 6, KN = L - 2, Q = N / 4, IB = 6;  // k = 4; IB = ceil_log2(N)
+// SPL lanes per agent (2 or 4): SPL waves per env, each wave 64 / SPL agents; lane r of an agent scans candidates
+// [r N / SPL, (r + 1) N / SPL) and holds memory frames [r 4 / SPL, (r + 1) 4 / SPL)
+template <int SPL>
+__global__ __launch_bounds__(SPL * kRollN) void rollout_uw_kernel(const Params p, int K,
+                                                                  const float* __restrict__ actions,
+                                                                  float* __restrict__ obs, float* __restrict__ rew_out,
+                                                                  uint8_t* __restrict__ done_out,
+                                                                  uint8_t* __restrict__ any_out) {
+    constexpr int N = kRollN, L = 6, KN = L - 2, IB = 6;  // k = 4; IB = ceil_log2(N)
+    constexpr int APW = 64 / SPL, Q = N / SPL, FPL = kMem / SPL;  // agents per wave, candidates / frames per lane
+    static_assert(SPL == 2 || SPL == 4, "2 or 4 lanes per agent");
     __shared__ float2 lpos[2][N];
     __shared__ int flag[2];  // any_done of a step, by step parity
     const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int ia = 16 * w + (l & 15), r = l >> 4;
+    const int ia = APW * w + (l & (APW - 1)), r = l / APW;
     const int env = blockIdx.x;
     const size_t a = (size_t)env * N + ia;
     const size_t EN = (size_t)p.E * N;
@@ -1564,7 +1570,9 @@ __global__ __launch_bounds__(4 * kRollN) void rollout_uw_kernel(const Params p, 
     float x = p0.x, y = p0.y;
     const float h = p.heading[a];
     float prev_h = p.prev_heading[a];
-    float4 fr = reinterpret_cast<const float4*>(p.mem_in)[a * kMem + r];  // memory frame r
+    float4 fr[FPL];  // memory frames r FPL .. r FPL + FPL - 1
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) fr[f] = reinterpret_cast<const float4*>(p.mem_in)[a * kMem + r * FPL + f];
     f32x2 act = ld_i<true>(reinterpret_cast<const f32x2*>(actions) + a);
     float vx = 0.0f, vy = 0.0f, rw = 0.0f;
     float dv[KN];
@@ -1599,11 +1607,11 @@ __global__ __launch_bounds__(4 * kRollN) void rollout_uw_kernel(const Params p, 
             sy = __fadd_rn(sy, __shfl_down(sy, o));
         }
         const float s0 = __fdiv_rn(__shfl(sx, 0), (float)N), s1 = __fdiv_rn(__shfl(sy, 0), (float)N);
-        // kNN (_computeDistances :155-175 + topk): a quarter of the candidates per lane, the lists merged
+        // kNN (_computeDistances :155-175 + topk): 1 / SPL of the candidates per lane, the lists merged
         uint32_t key[L];
         scan_range<L, false>(key, lp, Q * r, Q * r + Q, IB, x, y, p.box);
 #pragma unroll
-        for (int m = 16; m <= 32; m <<= 1) {
+        for (int m = APW; m < 64; m <<= 1) {
             uint32_t o[L];
 #pragma unroll
             for (int q = 0; q < L; ++q) o[q] = (uint32_t)__shfl_xor((int)key[q], m);
@@ -1622,17 +1630,23 @@ __global__ __launch_bounds__(4 * kRollN) void rollout_uw_kernel(const Params p, 
         coll = 0;
 #pragma unroll
         for (int q = 0; q < KN; ++q) {
-            dv[q] = __shfl(d4[q], l & 15);
+            dv[q] = __shfl(d4[q], l & (APW - 1));
             coll |= (dv[q] < p.cd);
         }
-        // torch.roll + insert of the observation memory: frame r <- frame r - 1 (lane l - 16), frame 0 <- dv
-        float4 nf;
-        nf.x = __shfl(fr.x, (l - 16) & 63);
-        nf.y = __shfl(fr.y, (l - 16) & 63);
-        nf.z = __shfl(fr.z, (l - 16) & 63);
-        nf.w = __shfl(fr.w, (l - 16) & 63);
-        fr = r == 0 ? make_float4(dv[0], dv[1], dv[2], dv[3]) : nf;
-        st_o<true>(reinterpret_cast<f32x4*>(obs) + ((size_t)s * EN + a) * kMem + r, f32x4{fr.x, fr.y, fr.z, fr.w});
+        // torch.roll + insert of the observation memory: frame j <- frame j - 1, frame 0 <- dv. The lane's first frame
+        // comes from the previous lane of its agent (l - APW), its others from itself
+        float4 in;
+        in.x = __shfl(fr[FPL - 1].x, (l - APW) & 63);
+        in.y = __shfl(fr[FPL - 1].y, (l - APW) & 63);
+        in.z = __shfl(fr[FPL - 1].z, (l - APW) & 63);
+        in.w = __shfl(fr[FPL - 1].w, (l - APW) & 63);
+#pragma unroll
+        for (int f = FPL - 1; f >= 1; --f) fr[f] = fr[f - 1];
+        fr[0] = r == 0 ? make_float4(dv[0], dv[1], dv[2], dv[3]) : in;
+#pragma unroll
+        for (int f = 0; f < FPL; ++f)
+            st_o<true>(reinterpret_cast<f32x4*>(obs) + ((size_t)s * EN + a) * kMem + r * FPL + f,
+                       f32x4{fr[f].x, fr[f].y, fr[f].z, fr[f].w});
         if (r == 0) {  // reward (gym_flock_uw.py:206-221)
             const float com_x = __fsub_rn(x, s0), com_y = __fsub_rn(y, s1);
             const float dist = sqrt_rn(__fadd_rn(__fmul_rn(com_x, com_x), __fmul_rn(com_y, com_y)));
@@ -1653,7 +1667,8 @@ __global__ __launch_bounds__(4 * kRollN) void rollout_uw_kernel(const Params p, 
         p.any_done[env] = f;
     }
     // the state after the last step, as K flock_step_uw calls leave it
-    reinterpret_cast<float4*>(p.mem_out)[a * kMem + r] = fr;
+#pragma unroll
+    for (int f = 0; f < FPL; ++f) reinterpret_cast<float4*>(p.mem_out)[a * kMem + r * FPL + f] = fr[f];
     if (r == 0) {
         reinterpret_cast<f32x2*>(p.pos)[a] = f32x2{x, y};
         reinterpret_cast<f32x2*>(p.vel)[a] = f32x2{vx, vy};
@@ -1872,6 +1887,7 @@ struct Knobs {
     int env_launches = 1;
     bool no_spec = false, no_split = false, no_cells = false;
     int pf = -1;
+    int rollout_spl = 2;  // lanes per agent of the uw rollout kernel (2 or 4)
 };
 Knobs& knobs_mut() {
     static Knobs k;
@@ -2062,6 +2078,8 @@ int flock_set_diag(const char* name, int value) {
         k.no_cells = value != 0;
     else if (!strcmp(name, "pf"))
         k.pf = value;
+    else if (!strcmp(name, "rollout_spl") && (value == 2 || value == 4))
+        k.rollout_spl = value;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
     else if (!strcmp(name, "sc_event_system_scope"))
@@ -2283,8 +2301,12 @@ int flock_rollout_uw(void* stream, int K, int E, int N, int k, float box, float 
         p.reward = reward;
         p.done = done;
         p.any_done = any_done;
-        hipLaunchKernelGGL(rollout_uw_kernel, dim3(E), dim3(4 * kRollN), 0, st, p, K, actions, obs_out, reward_out,
-                           done_out, any_done_out);
+        if (knobs().rollout_spl == 4)
+            hipLaunchKernelGGL(rollout_uw_kernel<4>, dim3(E), dim3(4 * kRollN), 0, st, p, K, actions, obs_out,
+                               reward_out, done_out, any_done_out);
+        else
+            hipLaunchKernelGGL(rollout_uw_kernel<2>, dim3(E), dim3(2 * kRollN), 0, st, p, K, actions, obs_out,
+                               reward_out, done_out, any_done_out);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? FLOCK_OK : fail(FLOCK_E_LAUNCH, hipGetErrorString(e));
     }

@@ -248,12 +248,17 @@ def _loop_worker(rank, port, q, world=2):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_ranks_dp_train_loop_equals_python_dp_rounds(world, cuda):
     """bench.py --gpus W's data-parallel config-3 loop (ScTrainLoop + the pipeline's all-reduces) at 2, 4 and 8 ranks:
-    bitwise the per-step Python data-parallel rounds, and every learner replica identical."""
+    bitwise the per-step Python data-parallel rounds (the same all-reduce calls), and every learner replica identical.
+    The split rounds all-reduce the critic gradient in two calls of other sizes: a ring all-reduce's summation order
+    per element follows its chunking, so beyond 2 ranks (where a + b == b + a) they agree to rounding."""
     out = _spawn(_loop_worker, world, world)
     for rank, (py, split, loop) in out:
         for other, name in ((split, "split loop"), (loop, "loop")):
             for i, (x, y) in enumerate(zip(py, other)):
-                np.testing.assert_array_equal(x, y, err_msg=f"rank {rank} {name} field {i}")
+                if name == "split loop" and world > 2 and np.asarray(x).dtype == np.float32:
+                    np.testing.assert_allclose(y, x, rtol=1e-4, atol=1e-6, err_msg=f"rank {rank} {name} field {i}")
+                else:
+                    np.testing.assert_array_equal(x, y, err_msg=f"rank {rank} {name} field {i}")
     for o in out[1:]:
         for i in range(9):  # the learner replicas stay identical (env state differs per rank)
             np.testing.assert_array_equal(out[0][1][1][i], o[1][1][i])

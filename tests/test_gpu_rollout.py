@@ -59,9 +59,22 @@ def _check(envs, actions, out):
     assert ref.steps == roll.steps  # (the buffer parity may differ: a rollout flips the double buffers once)
 
 
+@pytest.fixture(params=[2, 4], ids=["spl2", "spl4"])
+def spl(request):
+    """The one-launch kernel's lanes per agent (flock_set_diag("rollout_spl"); 2 is the default)."""
+    from marl_range_flocking_amd import _native
+
+    lib = _native.lib()
+    assert lib.flock_set_diag(b"rollout_spl", request.param) == 0
+    yield request.param
+    lib.flock_set_diag(b"rollout_spl", 2)
+
+
 @pytest.mark.parametrize("layout", ["uniform", "dense", "lattice", "edges"])
 @pytest.mark.parametrize("N,k", [(64, 4), (32, 4), (64, 3)], ids=["config2-one-launch", "N32-steps", "k3-steps"])
-def test_rollout_is_bitwise_k_steps(N, k, layout, cuda):
+def test_rollout_is_bitwise_k_steps(N, k, layout, spl, cuda):
+    if spl == 4 and N != 64:
+        pytest.skip("the lanes-per-agent knob only changes the one-launch kernel")
     E, K = 48, 7
     envs, g = _pair(cuda, E, N, k, layout=layout, rigid=layout == "edges")
     actions = (torch.rand(K, E, N, 2, device=cuda, generator=g) * 2 - 1)
@@ -73,7 +86,7 @@ def test_rollout_is_bitwise_k_steps(N, k, layout, cuda):
     _check(envs, actions2, envs[1].rollout(actions2, out=tuple(o[:3] for o in out)))
 
 
-def test_rollout_config2_full_size(cuda):
+def test_rollout_config2_full_size(spl, cuda):
     """BASELINE config 2 (uw, 1024 envs x 64 agents) over K = 12 steps in one launch: bitwise 12 single steps."""
     E, N, K = 1024, 64, 12
     envs, g = _pair(cuda, E, N)
