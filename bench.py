@@ -148,8 +148,11 @@ def parse():
     ap.add_argument("--rollout", type=int, default=None,
                     help="uw with no learner (config 2): the timed steps as VecFlockEnv.rollout calls of this many "
                          "steps each (flock_rollout_uw: all of them in ONE launch at N = 64, k = 4, the env state on "
-                         "chip; the random-action regime, actions known up front). Default 20 for config 2, 0 "
+                         "chip; the random-action regime, actions known up front). Default 50 for config 2, 0 "
                          "(one launch per step) otherwise")
+    ap.add_argument("--sc-slots", type=int, default=None,
+                    help="config 3: staging slots of the learn() pipeline (default 3; 5 or more also record the "
+                         "slot-free events on every ((slots - 1) / 2)-th round only)")
     ap.add_argument("--overlap", type=int, default=1, choices=[0, 1],
                     help="config 3: run learn(s) on its own stream beside env step s+1 (minibatch snapshot; same "
                          "results; the env kernel time is unchanged by it); configs 4 / 5: see --train-overlap; "
@@ -545,14 +548,14 @@ def main():
     if args.learner == "shared_critic":
         from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
-        hook = SharedCriticBench(env, device=dev, seed=1234 + rank, overlap=bool(args.overlap))
+        hook = SharedCriticBench(env, device=dev, seed=1234 + rank, overlap=bool(args.overlap), n_slots=args.sc_slots)
     elif args.learner == "vdn":
         hook = VDNBench(env, dev, seed=1234 + rank,
                         overlap=bool(args.overlap) and args.train_overlap in ("auto", "1"))
     elif args.learner == "maddpg_rnn":
         hook = MADDPGBench(env, dev, seed=1234 + rank, overlap=bool(args.overlap) and args.train_overlap == "1")
 
-    R = args.rollout if args.rollout is not None else (20 if args.config == 2 else 0)
+    R = args.rollout if args.rollout is not None else (50 if args.config == 2 else 0)
     use_rollout = R > 0 and hook is None and args.variant == "uw"
     if use_rollout:  # the action stack of a rollout call: the pool's actions, resident before timing
         acts = torch.stack([pool[i % len(pool)] for i in range(R)]).contiguous()

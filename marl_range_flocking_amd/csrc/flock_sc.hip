@@ -2109,7 +2109,7 @@ struct FlockScPipeline {
     FlockScUpdate u[kMaxSlots];
     FlockScRows ring, staging[kMaxSlots];
     Job jc[kMaxSlots], ja[kMaxSlots];  // the rounds' launch arguments, built once
-    hipEvent_t snap_done[kMaxSlots], slot_free[kMaxSlots];
+    hipEvent_t snap_done[kMaxSlots];
     // device-side snapshot gate: gate[0] the published sequence number, gate[1] the error word of a waiter that gave
     // up; seq counts this pipeline's snapshots. gate_on: the critic phase's row blocks poll gate[0] (single GPU and
     // data-parallel rounds alike; never under counter collection); otherwise the learner stream waits for each snapshot
@@ -2124,6 +2124,18 @@ struct FlockScPipeline {
     hipEvent_t mark_ev;
     int mark;
     int64_t gated_learns;  // learns that took the gate (the rest: the event hand-off)
+    // slot reuse: the "free point" of a slot is where its last learn's actor phase has been enqueued on the learner
+    // stream (one point per learn, in order); the env stream waits for it before the slot's next snapshot. An event is
+    // recorded only at every free_every-th point (each record is a barrier packet between two rounds on the learner
+    // stream, and each wait one on the env stream): a reuse waits for the first recorded point at or after its own,
+    // which n_slots >= free_every + 1 guarantees is already enqueued (else a fresh event on the learner stream)
+    int free_every;
+    int64_t points;               // free points emitted so far
+    int64_t slot_point[kMaxSlots];
+    static constexpr int kRec = 16;
+    hipEvent_t rec_ev[kRec];
+    int64_t rec_pt[kRec];
+    hipEvent_t fresh_ev;
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
@@ -2308,7 +2320,7 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
         p->staging[i] = staging[i];
         critic_job(&p->u[i], p->jc[i]);
         actor_job(&p->u[i], p->ja[i]);
-        hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};
+        hipEvent_t* evs[3] = {&p->snap_done[i], &p->grads_done[i], &p->actor_done[i]};
         for (hipEvent_t* e : evs)
             if (!rc && hipEventCreateWithFlags(e, pipeline_event_flags()) != hipSuccess)
                 rc = fail(-4, "flock_sc_pipeline_create: event");
@@ -2333,6 +2345,18 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->mark = 0;
     p->gated_learns = 0;
     p->mark_ev = nullptr;
+    p->free_every = n_slots >= 5 ? (n_slots - 1) / 2 : 1;
+    p->points = 0;
+    p->fresh_ev = nullptr;
+    for (int i = 0; i < kMaxSlots; ++i) p->slot_point[i] = -1;
+    for (int i = 0; i < FlockScPipeline::kRec; ++i) {
+        p->rec_ev[i] = nullptr;
+        p->rec_pt[i] = -1;
+        if (!rc && hipEventCreateWithFlags(&p->rec_ev[i], pipeline_event_flags()) != hipSuccess)
+            rc = fail(-4, "flock_sc_pipeline_create: event");
+    }
+    if (!rc && hipEventCreateWithFlags(&p->fresh_ev, pipeline_event_flags()) != hipSuccess)
+        rc = fail(-4, "flock_sc_pipeline_create: event");
     if (!rc && hipEventCreateWithFlags(&p->mark_ev, pipeline_event_flags()) != hipSuccess)
         rc = fail(-4, "flock_sc_pipeline_create: event");
     if (!rc && (hipMalloc(&p->gate, 4 * sizeof(unsigned long long)) != hipSuccess ||
@@ -2366,27 +2390,50 @@ int flock_sc_pipeline_mark(FlockScPipeline* p, void* env_stream, int wait) {
 }
 
 namespace {
+// slot q is free once everything enqueued on ls so far has run (its last learn's actor phase is enqueued): one free
+// point; an event on every free_every-th point only
+int emit_free_point(FlockScPipeline* p, hipStream_t ls, int q) {
+    const int64_t j = p->points++;
+    p->slot_point[q] = j;
+    if (j % p->free_every != p->free_every - 1) return 0;
+    const int k = (int)((j / p->free_every) % FlockScPipeline::kRec);
+    p->rec_pt[k] = j;
+    return hipEventRecord(p->rec_ev[k], ls) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline: event record");
+}
+// the env stream waits until slot s is free: for the first recorded free point at or after the slot's, or (none
+// recorded yet) for everything the learner stream holds now
+int wait_slot_free(FlockScPipeline* p, hipStream_t es, hipStream_t ls, int s) {
+    const int64_t P = p->slot_point[s];
+    if (P < 0) return 0;
+    const int64_t j = P + (p->free_every - 1 - P % p->free_every);  // the first recorded point >= P
+    const int k = (int)((j / p->free_every) % FlockScPipeline::kRec);
+    hipEvent_t ev = p->fresh_ev;
+    if (j < p->points && p->rec_pt[k] == j)
+        ev = p->rec_ev[k];
+    else if (hipEventRecord(p->fresh_ev, ls) != hipSuccess)
+        return fail(-4, "flock_sc_pipeline: event record");
+    return hipStreamWaitEvent(es, ev, 0) == hipSuccess ? 0 : fail(-4, "flock_sc_pipeline_learn: wait");
+}
+
 // the rounds of a learn() whose critic phase (slot s) reads inputs the learner stream can use (after its event wait
 // or its row blocks' gate): the critic phase of s beside the actor phase of the previous learn, or one after the other
 // (same agent)
 int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent) {
     const int n = p->n;
     int rc = 0;
-    bool ok = true;
     const int q = p->pending;
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
         // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
         if ((rc = pipeline_round(p, ls, s, q, agent, p->pending_agent))) return rc;
-        ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
+        if ((rc = emit_free_point(p, ls, q))) return rc;
     } else {
         // same agent (this critic phase reads the target actor that actor phase soft-updates): one after the other
         if (q >= 0) {
             if ((rc = pipeline_round(p, ls, -1, q, -1, p->pending_agent))) return rc;
-            ok = hipEventRecord(p->slot_free[q], ls) == hipSuccess;
+            if ((rc = emit_free_point(p, ls, q))) return rc;
         }
-        if (ok && (rc = pipeline_round(p, ls, s, -1, agent, -1))) return rc;
+        if ((rc = pipeline_round(p, ls, s, -1, agent, -1))) return rc;
     }
-    if (!ok) return fail(-4, "flock_sc_pipeline: stream operation failed");
     p->pending = s;
     p->pending_agent = agent;
     p->used[s] = true;
@@ -2403,9 +2450,8 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     hipStream_t es = (hipStream_t)env_stream, ls = (hipStream_t)learner_stream;
     const int s = p->slot;
     const FlockScUpdate& u = p->u[s];
-    if (p->used[s] && hipStreamWaitEvent(es, p->slot_free[s], 0) != hipSuccess)
-        return fail(-4, "flock_sc_pipeline_learn: wait");
     int rc = 0;
+    if (p->used[s] && (rc = wait_slot_free(p, es, ls, s))) return rc;
     const int mark = p->mark;
     p->mark = 0;
     if (p->gate_on && mark) {
@@ -2516,8 +2562,7 @@ int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream) {
     const int q = p->pending;
     if (q >= 0) {
         if (int rc = pipeline_round(p, ls, -1, q, -1, p->pending_agent)) return rc;
-        if (hipEventRecord(p->slot_free[q], ls) != hipSuccess)
-            return fail(-4, "flock_sc_pipeline_flush: stream operation failed");
+        if (int rc = emit_free_point(p, ls, q)) return rc;
         p->pending = -1;
     }
     // split rounds: the learner stream joins the actor stream, so synchronising the learner stream covers every step
@@ -2567,9 +2612,12 @@ void flock_sc_pipeline_destroy(FlockScPipeline* p) {
     if (p->bwd_done) (void)hipEventDestroy(p->bwd_done);
     if (p->ar_done) (void)hipEventDestroy(p->ar_done);
     if (p->mark_ev) (void)hipEventDestroy(p->mark_ev);
+    if (p->fresh_ev) (void)hipEventDestroy(p->fresh_ev);
+    for (hipEvent_t e : p->rec_ev)
+        if (e) (void)hipEventDestroy(e);
     delete[] p->last_actor_slot;
     for (int i = 0; i < p->n; ++i) {
-        hipEvent_t* evs[4] = {&p->snap_done[i], &p->slot_free[i], &p->grads_done[i], &p->actor_done[i]};
+        hipEvent_t* evs[3] = {&p->snap_done[i], &p->grads_done[i], &p->actor_done[i]};
         for (hipEvent_t* e : evs)
             if (*e) (void)hipEventDestroy(*e);
     }

@@ -115,8 +115,10 @@ def test_pipelined_phases_same_agent_equal_serial(cuda):
 
 
 @pytest.mark.parametrize("agents,n_slots", [((0, 0, 0, 1, 1, 0, 2, 1, 1, 2), 2), ((0, 1, 2, 0, 0, 1, 2, 2, 1, 0), 3),
-                                            ((3, 1, 4, 1, 5, 9, 2, 6, 5, 3), 4)],
-                         ids=["same-agent-runs-2slots", "mixed-3slots", "distinct-4slots"])
+                                            ((3, 1, 4, 1, 5, 9, 2, 6, 5, 3), 4),
+                                            ((3, 1, 4, 1, 5, 9, 2, 6, 5, 3, 5, 8, 9, 7, 9, 3, 2, 3, 8, 4, 6, 6), 8)],
+                         ids=["same-agent-runs-2slots", "mixed-3slots", "distinct-4slots",
+                              "8slots-sparse-free-events"])
 @pytest.mark.parametrize("handoff", ["gate", "event"])
 def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
     """The native pipeline (flock_sc_pipeline_learn): one six-launch round per learn() = its critic phase merged
@@ -255,7 +257,7 @@ def test_specialised_row_kernels_equal_generic(cuda):
     assert torch.isfinite(a.critic.data).all() and a.losses.abs().sum() > 0
 
 
-@pytest.mark.parametrize("n_slots", [2, 3])
+@pytest.mark.parametrize("n_slots", [2, 3, 8])
 def test_device_gate_is_bitwise_the_event_wait(n_slots, cuda):
     """The device-side snapshot gate (the critic row blocks poll a sequence number the `sc1` snapshot publishes, then
     read the staged rows `sc1`) against the cross-queue event wait, in the overlapped config-3 loop at the reference
