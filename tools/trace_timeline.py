@@ -5,14 +5,21 @@ sc_fwd, .. its last: sc_grad_adam or sc_bwdg) prints the start / end
 relative to the first step, and summarises: the step period, the env launches' span, the round's span, the gap
 between the snapshot and the round's first kernel, the gaps between the round's kernels, and which stream set the
 period (did the env stream start its next step right after its previous one, or later).
-Usage: python tools/trace_timeline.py TRACE.csv [first_step=...]"""
+Usage: python tools/trace_timeline.py TRACE.csv|RESULTS.db (rocprofv3's csv kernel trace or its sqlite database)"""
 import csv
+import sqlite3
 import statistics as st
 import sys
 
 
 def load(path):
     rows = []
+    if path.endswith(".db"):
+        q = ("select s.kernel_name, d.start, d.end from rocpd_kernel_dispatch d "
+             "join rocpd_info_kernel_symbol s on d.kernel_id = s.id")
+        rows = [(a, b, n) for n, a, b in sqlite3.connect(path).execute(q)]
+        rows.sort()
+        return rows
     with open(path) as f:
         for r in csv.DictReader(f):
             name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
@@ -54,7 +61,8 @@ def main():
     n = min(len(env_steps), len(rounds))
     skip = max(0, n - 60)  # the last 60 steps (the timed region sits at the end of a short bench)
     t0 = env_steps[skip][0][0][0]
-    per, env_span, rnd_span, snap_gap, env_idle = [], [], [], [], []
+    per, env_span, rnd_span, snap_gap, env_idle, between = [], [], [], [], [], []
+    prev_end = None
     kgaps = {k: [] for k in order[1:]}
     kdur = {k: [] for k in order}
     for i in range(skip, n - 1):
@@ -70,6 +78,9 @@ def main():
         if any(k not in r for k in order):
             continue
         snap_gap.append((r["_first"][1] - snap[1]) / 1e3)
+        pr = rounds[rounds.index(r) - 1] if rounds.index(r) > 0 else None
+        if pr is not None:
+            between.append((r["_first"][0] - pr[order[-1]][1]) / 1e3)
         rnd_span.append((r[order[-1]][1] - r["_first"][0]) / 1e3)
         for a, b in zip(order, order[1:]):
             kgaps[b].append((r[b][0] - r[a][1]) / 1e3)
@@ -91,6 +102,8 @@ def main():
     print("round order               ", " ".join(order))
     print("snapshot end -> 1st k end ", m(snap_gap))
     print("round span us             ", m(rnd_span))
+    if between:
+        print("previous round end -> 1st k start", m(between))
     for k, v in kdur.items():
         print("  %-13s dur %s" % (k, m(v)))
     for k, v in kgaps.items():
