@@ -207,8 +207,8 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
  * per call; replaces agent_simple_shared_critic.py:115-185 called in that cadence): n_slots (2..8) staging slots, each
  * with its own FlockScUpdate (do_adam, own critic_view, own workspace; ring fields = that slot's staging rows, idx =
  * 0..B-1). flock_sc_pipeline_learn enqueues learn() t of `agent` with no host synchronisation:
- *   env_stream:     [wait until the slot's previous learn() has finished] minibatch snapshot (rows sampled with
- *                   Philox(seed, counter), as flock_sc_prep_snapshot)
+ *   env_stream:     [wait until the slot's previous learn() has consumed its staging rows] minibatch snapshot
+ *                   (rows sampled with Philox(seed, counter), as flock_sc_prep_snapshot)
  *   learner_stream: ONE round (five launches): the critic phase of learn t with the actor phase of learn t-1 (if
  *                   learn t-1 had the same agent: its actor phase, then this critic phase)
  * The round's wait for the snapshot is, by default, the device-side gate: the snapshot (one workgroup) stores the
@@ -224,9 +224,13 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
  * above any env step; a waiter that gives up sets an error word and computes nothing, flock_sc_pipeline_check
  * returns -6). flock_sc_pipeline_set_gate(p, 0) (and always under rocprofv3 counter collection, which serialises
  * dispatches) makes every learn() take the event wait; it returns the hand-off in use (1 gate, 0 events). The gate
- * serves single-GPU and data-parallel pipelines alike. Both are
- * deadlock-free whatever hardware queues the streams map to: every snapshot is enqueued before the round that waits
- * for it, and nothing on env_stream waits for that round. The actor phase of the last learn() stays pending until the
+ * serves single-GPU and data-parallel pipelines alike. Slot reuse: when a single-GPU learn() and the slot's previous
+ * learn() are both gated, the previous round's fc2 GEMM launch (after its row launch, the staging rows' only reader)
+ * stores that learn's sequence number write-through and the new snapshot polls it (bounded like the gate) before
+ * writing; otherwise (event hand-off, data-parallel rounds, flock_set_diag "sc_free_events") the env stream waits for
+ * a learner-stream event recorded after the round that freed the slot. Both hand-offs are deadlock-free whatever
+ * hardware queues the streams map to: every snapshot is enqueued before the round that waits for it, and a snapshot
+ * waits only for a round enqueued before it whose own snapshot precedes it on env_stream. The actor phase of the last learn() stays pending until the
  * next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise those of the serial
  * learn() sequence. Returns NULL (create) or a negative code; flock_learn_last_error() has the message. */
 typedef struct FlockScPipeline FlockScPipeline;

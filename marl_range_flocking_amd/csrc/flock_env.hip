@@ -2066,6 +2066,7 @@ Params base(int E, int N, int k, float box) {
 
 void flock_sc_diag_no_spec(bool v);       // flock_sc.hip
 void flock_sc_diag_event_system(bool v);  // flock_sc.hip
+void flock_sc_diag_free_events(bool v);   // flock_sc.hip
 
 extern "C" {
 
@@ -2092,6 +2093,8 @@ int flock_set_diag(const char* name, int value) {
         flock_sc_diag_no_spec(value != 0);
     else if (!strcmp(name, "sc_event_system_scope"))
         flock_sc_diag_event_system(value != 0);
+    else if (!strcmp(name, "sc_free_events"))
+        flock_sc_diag_free_events(value != 0);
     else
         return fail(FLOCK_E_ARG, "flock_set_diag: unknown knob");
     return FLOCK_OK;

@@ -674,7 +674,8 @@ __device__ unsigned long long g_scmark[4096][8];
 // 2 s of s_memrealtime (100 MHz): the env stream may be held up by work enqueued on it before the learn() (an
 // evaluation rollout, a long copy); 0.2 s failed a learn behind a 0.2-s kernel (tools/rccl_host_cost.py, round 5)
 constexpr unsigned long long kGateTimeoutTicks = 200000000ull;
-__device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned long long seq) {
+__device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned long long seq,
+                                          unsigned long long* err = nullptr) {
     __shared__ int ok;
     if (threadIdx.x == 0) {
         int good = 1;
@@ -682,7 +683,7 @@ __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned lon
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             while ((long long)(flock_mem::ld_sc1(gate) - seq) < 0) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
-                    __hip_atomic_store(gate + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(err ? err : gate + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     good = 0;
                     break;
                 }
@@ -808,6 +809,10 @@ constexpr int kMaxBatch = 5;  // a round's forward GEMMs: 3 (critic phase) + 2 (
 struct GemmBatch {
     GemmP p[kMaxBatch];
     int n;
+    // the critic phase's snapshot consumed (its k1 launch, the only reader of the staging rows, has completed): block
+    // (0, 0) stores done_seq to *done write-through for a snapshot kernel waiting to reuse the slot; NULL: none
+    unsigned long long* done;
+    unsigned long long done_seq;
 };
 
 __host__ __device__ inline int gemm_kc(int K, int chunk = kKC) {
@@ -1067,6 +1072,7 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
 template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     SC_PROF(1);
+    if (gb.done && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) flock_mem::st_sc1(gb.done, gb.done_seq);
     gemm_block<AV, BV, NF>(gb, blockIdx.y, blockIdx.x);
 }
 
@@ -1623,6 +1629,7 @@ struct Job {
     int nfwd;
     BwdJob bw;
     GradAdam ga;
+    bool free_dev;  // gated critic phase whose slot is freed on the device (gate[2], sc_gemm): FlockScPipeline.gseq
 };
 
 void job_common(const FlockScUpdate* u, Job& j) {
@@ -1633,6 +1640,7 @@ void job_common(const FlockScUpdate* u, Job& j) {
     j.rb = (j.B + kRowsPerBlock - 1) / kRowsPerBlock;
     j.lds1 = fc1_lds(j.in, j.H1);
     j.lds3 = tails_lds(j.na, j.H2);
+    j.free_dev = false;
 }
 
 // the bwd launch's job: dH1 = dZ2 W2 (+ LN1 epilogue), dW2 = dZ2^T H1, then the caller's early reductions
@@ -1860,6 +1868,8 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja, const MidHook* mi
     {  // 2: forward fc2 GEMMs
         GemmBatch gb;
         gb.n = 0;
+        gb.done = (jc && jc->a.gate && jc->free_dev) ? jc->a.gate + 2 : nullptr;
+        gb.done_seq = jc ? jc->a.gate_seq : 0;
         if (jc)
             for (int i = 0; i < jc->nfwd; ++i) gb.p[gb.n++] = jc->fwd[i];
         if (ja)
@@ -1980,11 +1990,16 @@ __global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint
 }
 
 // the same snapshot as ONE block that publishes it through the device-side gate: rows and agent stored `sc1`, every
-// wave's stores waited for, a workgroup barrier, then one lane's `sc1` store of gate[0] = seq (csrc/flock_mem.h)
+// wave's stores waited for, a workgroup barrier, then one lane's `sc1` store of gate[0] = seq (csrc/flock_mem.h).
+// reuse > 0: the slot's previous snapshot (that sequence number) must have been consumed first: one lane polls gate[2]
+// (stored by that round's sc_gemm after its k1 launch, the staging rows' only reader) with `sc1` loads, bounded like
+// gate_wait; a snapshot that gives up sets the error word and writes nothing
 __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows, uint64_t seed, uint64_t counter,
                                                              int64_t* agent_out, int64_t agent, int in_dim,
                                                              int n_actions, FlockScRows src, FlockScRows dst, int vec,
-                                                             unsigned long long* gate, unsigned long long seq) {
+                                                             unsigned long long* gate, unsigned long long seq,
+                                                             unsigned long long reuse) {
+    if (reuse && !gate_wait(gate + 2, reuse, gate + 1)) return;
     if (threadIdx.x == 0) flock_mem::st_sc1(agent_out, agent);
     for (int r = threadIdx.x; r < B; r += 256)
         snapshot_row<true>(rows, seed, counter, nullptr, in_dim, n_actions, src, dst, vec, r);
@@ -2136,6 +2151,12 @@ struct FlockScPipeline {
     hipEvent_t rec_ev[kRec];
     int64_t rec_pt[kRec];
     hipEvent_t fresh_ev;
+    // slots freed on the device (single-GPU gated learns, g_sc_free_events off): gseq[s] = the snapshot sequence
+    // number of slot s's last learn when that learn was gated (0: it took the event hand-off). Its round's sc_gemm
+    // stores that number to gate[2] once its k1 launch, the only reader of the staging rows, has completed, and the
+    // slot's next gated snapshot polls gate[2] before writing (sc_prep_snapshot_gate): no free-point event between
+    // the rounds on the learner stream and no cross-queue wait on the env stream
+    unsigned long long gseq[kMaxSlots];
     bool used[kMaxSlots];
     int slot;
     int pending;  // slot of the learn() whose actor phase is not enqueued yet, or -1
@@ -2175,6 +2196,8 @@ namespace {
 // follows: the next round's kernels then start from a cold L2). flock_set_diag("sc_event_system_scope", 1) restores the
 // default for A/B (read when a pipeline is created).
 bool g_sc_event_system = false;
+// flock_set_diag("sc_free_events", 1): every slot freed by a learner-stream event (the round-5 scheme; A/B)
+bool g_sc_free_events = false;
 unsigned pipeline_event_flags() {
     return hipEventDisableTiming | (g_sc_event_system ? 0u : (unsigned)hipEventReleaseToDevice);
 }
@@ -2348,7 +2371,10 @@ FlockScPipeline* flock_sc_pipeline_create(int n_slots, const FlockScUpdate* slot
     p->free_every = n_slots >= 5 ? (n_slots - 1) / 2 : 1;
     p->points = 0;
     p->fresh_ev = nullptr;
-    for (int i = 0; i < kMaxSlots; ++i) p->slot_point[i] = -1;
+    for (int i = 0; i < kMaxSlots; ++i) {
+        p->slot_point[i] = -1;
+        p->gseq[i] = 0;
+    }
     for (int i = 0; i < FlockScPipeline::kRec; ++i) {
         p->rec_ev[i] = nullptr;
         p->rec_pt[i] = -1;
@@ -2425,12 +2451,12 @@ int enqueue_rounds(FlockScPipeline* p, hipStream_t ls, int s, int64_t agent) {
     if (q >= 0 && q == (s + n - 1) % n && p->pending_agent != agent) {
         // the actor phase of the previous learn() beside this critic phase (different agents: no shared state)
         if ((rc = pipeline_round(p, ls, s, q, agent, p->pending_agent))) return rc;
-        if ((rc = emit_free_point(p, ls, q))) return rc;
+        if (!p->gseq[q] && (rc = emit_free_point(p, ls, q))) return rc;
     } else {
         // same agent (this critic phase reads the target actor that actor phase soft-updates): one after the other
         if (q >= 0) {
             if ((rc = pipeline_round(p, ls, -1, q, -1, p->pending_agent))) return rc;
-            if ((rc = emit_free_point(p, ls, q))) return rc;
+            if (!p->gseq[q] && (rc = emit_free_point(p, ls, q))) return rc;
         }
         if ((rc = pipeline_round(p, ls, s, -1, agent, -1))) return rc;
     }
@@ -2451,10 +2477,24 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const int s = p->slot;
     const FlockScUpdate& u = p->u[s];
     int rc = 0;
-    if (p->used[s] && (rc = wait_slot_free(p, es, ls, s))) return rc;
     const int mark = p->mark;
     p->mark = 0;
-    if (p->gate_on && mark) {
+    const bool gated = p->gate_on && mark;
+    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated and
+    // the rounds are single-GPU (a data-parallel round's collective may wait on other ranks for longer than the
+    // snapshot's bounded poll), else an event
+    const bool dev_free = gated && !p->dp && !g_sc_free_events;
+    const unsigned long long reuse = (p->used[s] && dev_free) ? p->gseq[s] : 0;
+    if (p->used[s] && !reuse) {
+        if (p->gseq[s]) {  // a gated learn freed on the device, reused now by the event path: everything enqueued so far
+            if (hipEventRecord(p->fresh_ev, ls) != hipSuccess || hipStreamWaitEvent(es, p->fresh_ev, 0) != hipSuccess)
+                return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
+        } else if ((rc = wait_slot_free(p, es, ls, s))) {
+            return rc;
+        }
+    }
+    p->gseq[s] = 0;
+    if (gated) {
         // the snapshot publishes gate[0] = seq after its write-through stores; this learn's critic row blocks wait
         // for it on the device. No deadlock whatever the streams' hardware queues: the snapshot is enqueued before
         // the round that waits for it, and nothing on the env stream waits for that round. The guard: the learner
@@ -2470,15 +2510,19 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
             vec = vec && al16(x->state) && al16(x->new_state) && (((uintptr_t)x->action & 7) == 0);
         const unsigned long long seq = ++p->seq;
         hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
-                           const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq);
+                           const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq,
+                           reuse);
         if ((rc = launched())) return rc;
         p->jc[s].a.gate = p->jgc[s].a.gate = p->gate;
         p->jc[s].a.gate_seq = p->jgc[s].a.gate_seq = seq;
+        p->jc[s].free_dev = p->jgc[s].free_dev = dev_free;
+        if (dev_free) p->gseq[s] = seq;
     } else {
         if ((rc = flock_sc_prep_snapshot(es, u.B, rows, seed, counter, nullptr, const_cast<int64_t*>(u.agent), agent,
                                          u.in_dim, u.n_actions, &p->ring, &p->staging[s])))
             return rc;
         p->jc[s].a.gate = p->jgc[s].a.gate = nullptr;
+        p->jc[s].free_dev = p->jgc[s].free_dev = false;
         if (hipEventRecord(p->snap_done[s], es) != hipSuccess || hipStreamWaitEvent(ls, p->snap_done[s], 0) != hipSuccess)
             return fail(-4, "flock_sc_pipeline_learn: stream operation failed");
     }
@@ -2562,7 +2606,7 @@ int flock_sc_pipeline_flush(FlockScPipeline* p, void* learner_stream) {
     const int q = p->pending;
     if (q >= 0) {
         if (int rc = pipeline_round(p, ls, -1, q, -1, p->pending_agent)) return rc;
-        if (int rc = emit_free_point(p, ls, q)) return rc;
+        if (int rc = p->gseq[q] ? 0 : emit_free_point(p, ls, q)) return rc;
         p->pending = -1;
     }
     // split rounds: the learner stream joins the actor stream, so synchronising the learner stream covers every step
@@ -2597,6 +2641,7 @@ int flock_sc_pipeline_gated(const FlockScPipeline* p) { return p && p->gate_on ?
 
 }  // extern "C"
 void flock_sc_diag_event_system(bool v) { g_sc_event_system = v; }
+void flock_sc_diag_free_events(bool v) { g_sc_free_events = v; }
 extern "C" {
 
 void* flock_sc_pipeline_comm_stream(const FlockScPipeline* p) { return p ? (void*)p->comm_stream : nullptr; }

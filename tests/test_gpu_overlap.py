@@ -161,6 +161,51 @@ def test_native_pipeline_rounds_equal_serial(agents, n_slots, handoff, cuda):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("n_slots", [2, 3])
+@pytest.mark.parametrize("free_events", [0, 1], ids=["slots-freed-on-device", "slot-free-events"])
+def test_pipeline_mixed_gated_and_event_learns_equal_serial(n_slots, free_events, cuda):
+    """Learns with and without a mark in one pipeline: the gated ones take the device gate, the rest the event
+    hand-off, so a slot passes between the two ways of being freed (on the device: the round's sc_gemm stores the
+    consumed snapshot's number and the slot's next gated snapshot polls it; by event: a free point on the learner
+    stream; and, under flock_set_diag("sc_free_events", 1), every slot by event). Bitwise the serial learns."""
+    from marl_range_flocking_amd import _native
+    from marl_range_flocking_amd.learners.shared_critic import SharedCriticLearner
+
+    lib = _native.lib()
+    agents = (0, 1, 2, 0, 0, 1, 2, 2, 1, 0, 3, 4, 3)
+    marks = (1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1, 1, 1)
+    g = torch.Generator(device=cuda).manual_seed(6)
+    n = 300
+    rows = (torch.rand(n, 4, device=cuda, generator=g), torch.rand(n, 2, device=cuda, generator=g),
+            torch.rand(n, 1, device=cuda, generator=g), torch.rand(n, 4, device=cuda, generator=g),
+            torch.rand(n, device=cuda, generator=g) > 0.5)
+    ls = torch.cuda.Stream(device=cuda)
+    main = torch.cuda.current_stream(cuda)
+    assert lib.flock_set_diag(b"sc_free_events", free_events) == 0
+    try:
+        ser = SharedCriticLearner(5, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=False)
+        pip = SharedCriticLearner(5, 4, device=cuda, seed=5, batch_size=64, buffer_size=500, snapshot=True,
+                                  n_slots=n_slots)
+        for L in (ser, pip):
+            L.store_transitions(*rows)
+        for a, mk in zip(agents, marks):
+            ser.learn(a)
+            if mk:
+                pip.pipeline_mark(main.cuda_stream)
+            assert pip.pipeline_learn(a, main.cuda_stream, ls.cuda_stream)
+        pip.pipeline_flush(ls.cuda_stream)
+        main.wait_stream(ls)
+        torch.cuda.synchronize()
+    finally:
+        lib.flock_set_diag(b"sc_free_events", 0)
+    pip.pipeline_check()
+    assert pip.pipeline().gated_learns() == sum(marks)
+    for x, y in ((ser.critic.data, pip.critic.data), (ser.critic.exp_avg_sq, pip.critic.exp_avg_sq),
+                 (ser.actors.data, pip.actors.data), (ser.actors.target, pip.actors.target),
+                 (ser.actor_steps, pip.actor_steps), (ser.losses, pip.losses)):
+        assert torch.equal(x, y)
+
+
 def _sleep_s(seconds):
     """A kernel that holds the current stream for about `seconds` (s_memtime cycles at >= 2.1 GHz)."""
     torch.cuda._sleep(int(2.5e9 * seconds))
