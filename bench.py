@@ -58,7 +58,9 @@ RING_BYTES_PER_AGENT_STEP = {"shared_critic": 16 + 48, "maddpg_rnn": 16 + 48, "v
 # the uw rollout kernel's HBM bytes per agent-step (state on chip): action 8 r + observation memory 64 w + reward 4 w +
 # done 1 w (+ any_done per env, and the state once per launch)
 ROLLOUT_MOVED_BYTES = 8 + 64 + 4 + 1
-EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 4))  # steps between HIP-event-timed env launches (timed region)
+# steps between HIP-event-timed env launches in the timed region: each timed step adds two marker packets to the env
+# stream (every 4th step: driver command 0.0855-0.0860 ms per step, every 16th 0.0838-0.0848; profiles/r06/ev/)
+EV_EVERY = int(os.environ.get("FLOCK_BENCH_EV_EVERY", 16))
 
 
 class DevEvent:

@@ -663,6 +663,13 @@ __device__ unsigned long long g_scmark[4096][8];
 #define SC_PROF(k)
 #define SC_MARK(MK, i)
 #endif
+// -DFLOCK_SC_PRIO=n (A/B builds only, tools/build_variant_sc.sh): the round kernels' waves raise their issue priority
+// to n (s_setprio) over co-resident env waves
+#ifdef FLOCK_SC_PRIO
+#define SC_WAVE_PRIO() __builtin_amdgcn_s_setprio(FLOCK_SC_PRIO)
+#else
+#define SC_WAVE_PRIO()
+#endif
 // Merged row kernels of a learn() round (launch_round): the critic-phase job of one learn() and the actor-phase job of
 // the previous one in ONE launch, picked by a block-uniform branch (either job may be absent: npc / nbc = 0, or no
 // blocks past them).
@@ -744,6 +751,7 @@ __device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bo
 template <int C, int HC>
 __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa, Pull pc, Pull pa) {
     SC_PROF(0);
+    SC_WAVE_PRIO();
     const bool crit = (int)blockIdx.y < npc;
     // the pull: this block's share of its job's panels among the job's blocks of its XCD group (x mod 8)
     const int rb8 = (int)gridDim.x >> 3, yj = crit ? (int)blockIdx.y : (int)blockIdx.y - npc;
@@ -771,6 +779,7 @@ __global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, 
 template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
     SC_PROF(2);
+    SC_WAVE_PRIO();
     const int nba = (int)gridDim.x - nbc;
     if ((int)blockIdx.x < nbc)
         c3_body<C, HC, NAC>(wc, ac, (nbc & 7) == 0 ? xcd_perm(blockIdx.x, nbc) : (int)blockIdx.x);
@@ -1072,6 +1081,7 @@ __device__ __forceinline__ void gemm_block(const GemmBatch& gb, int y, int x) {
 template <int AV, int BV, int NF>
 __global__ __launch_bounds__(256) void sc_gemm(GemmBatch gb) {
     SC_PROF(1);
+    SC_WAVE_PRIO();
     if (gb.done && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) flock_mem::st_sc1(gb.done, gb.done_seq);
     gemm_block<AV, BV, NF>(gb, blockIdx.y, blockIdx.x);
 }
@@ -1304,6 +1314,7 @@ struct Bwd2 {
 template <int AVH, int BVH, int AVW, int BVW, int NFH, int NFW>
 __global__ __launch_bounds__(256) void sc_bwd(Bwd2 bb) {
     SC_PROF(3);
+    SC_WAVE_PRIO();
     if ((int)blockIdx.x < bb.nb0) {
         if ((int)blockIdx.x < bb.n0) bwd_body<AVH, BVH, AVW, BVW, NFH, NFW>(bb.j0, blockIdx.x);
     } else {
@@ -1456,6 +1467,7 @@ struct GradAdam2 {
 };
 __global__ __launch_bounds__(256) void sc_grad_adam(GradAdam2 gg) {
     SC_PROF(4);
+    SC_WAVE_PRIO();
     if ((int)blockIdx.x < gg.nb0)
         grad_adam_body(gg.j0, blockIdx.x, gg.nb0);
     else
