@@ -682,14 +682,15 @@ __device__ unsigned long long g_scmark[4096][8];
 // evaluation rollout, a long copy); 0.2 s failed a learn behind a 0.2-s kernel (tools/rccl_host_cost.py, round 5)
 constexpr unsigned long long kGateTimeoutTicks = 200000000ull;
 __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned long long seq,
-                                          unsigned long long* err = nullptr) {
+                                          unsigned long long* err = nullptr,
+                                          unsigned long long ticks = kGateTimeoutTicks) {
     __shared__ int ok;
     if (threadIdx.x == 0) {
         int good = 1;
         if ((long long)(flock_mem::ld_sc1(gate) - seq) < 0) {
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             while ((long long)(flock_mem::ld_sc1(gate) - seq) < 0) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                     __hip_atomic_store(err ? err : gate + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     good = 0;
                     break;
@@ -2004,14 +2005,14 @@ __global__ __launch_bounds__(64) void sc_prep_snapshot(int B, int64_t rows, uint
 // the same snapshot as ONE block that publishes it through the device-side gate: rows and agent stored `sc1`, every
 // wave's stores waited for, a workgroup barrier, then one lane's `sc1` store of gate[0] = seq (csrc/flock_mem.h).
 // reuse > 0: the slot's previous snapshot (that sequence number) must have been consumed first: one lane polls gate[2]
-// (stored by that round's sc_gemm after its k1 launch, the staging rows' only reader) with `sc1` loads, bounded like
-// gate_wait; a snapshot that gives up sets the error word and writes nothing
+// (stored by that round's sc_gemm after its k1 launch, the staging rows' only reader) with `sc1` loads for at most
+// ticks (s_memrealtime); a snapshot that gives up sets the error word and writes nothing
 __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows, uint64_t seed, uint64_t counter,
                                                              int64_t* agent_out, int64_t agent, int in_dim,
                                                              int n_actions, FlockScRows src, FlockScRows dst, int vec,
                                                              unsigned long long* gate, unsigned long long seq,
-                                                             unsigned long long reuse) {
-    if (reuse && !gate_wait(gate + 2, reuse, gate + 1)) return;
+                                                             unsigned long long reuse, unsigned long long ticks) {
+    if (reuse && !gate_wait(gate + 2, reuse, gate + 1, ticks)) return;
     if (threadIdx.x == 0) flock_mem::st_sc1(agent_out, agent);
     for (int r = threadIdx.x; r < B; r += 256)
         snapshot_row<true>(rows, seed, counter, nullptr, in_dim, n_actions, src, dst, vec, r);
@@ -2492,10 +2493,12 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const int mark = p->mark;
     p->mark = 0;
     const bool gated = p->gate_on && mark;
-    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated and
-    // the rounds are single-GPU (a data-parallel round's collective may wait on other ranks for longer than the
-    // snapshot's bounded poll), else an event
-    const bool dev_free = gated && !p->dp && !g_sc_free_events;
+    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated, else
+    // an event (and always an event for split data-parallel rounds, whose actor halves run on a stream of their own).
+    // Data-parallel rounds: the round that consumed the slot may sit behind an all-reduce that waits for the other
+    // ranks, so the poll's bound is 60 s there (a collective that never completes hangs the ranks anyway)
+    const bool dev_free = gated && !g_sc_free_events && !(p->dp && p->split);
+    const unsigned long long ticks = p->dp ? 30 * kGateTimeoutTicks : kGateTimeoutTicks;
     const unsigned long long reuse = (p->used[s] && dev_free) ? p->gseq[s] : 0;
     if (p->used[s] && !reuse) {
         if (p->gseq[s]) {  // a gated learn freed on the device, reused now by the event path: everything enqueued so far
@@ -2523,7 +2526,7 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
         const unsigned long long seq = ++p->seq;
         hipLaunchKernelGGL(sc_prep_snapshot_gate, dim3(1), dim3(256), 0, es, u.B, rows, seed, counter,
                            const_cast<int64_t*>(u.agent), agent, u.in_dim, u.n_actions, src, dst, vec, p->gate, seq,
-                           reuse);
+                           reuse, ticks);
         if ((rc = launched())) return rc;
         p->jc[s].a.gate = p->jgc[s].a.gate = p->gate;
         p->jc[s].a.gate_seq = p->jgc[s].a.gate_seq = seq;
