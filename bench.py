@@ -37,6 +37,7 @@ Configs 4 and 5 are 8-GPU configs: their GLOBAL env count (8192 / 16384) is spli
 config 3 (the headline) keeps 4096 envs per GPU (weak scaling).
 """
 import argparse
+import ctypes
 import json
 import os
 import time
@@ -140,6 +141,9 @@ def parse():
     ap.add_argument("--diag-prewarm-ms", type=float, default=0.0,
                     help="diagnostics only (never a bench line): keep the GPU busy with matmuls for this long before "
                          "the warmup steps (clock / power-state probe)")
+    ap.add_argument("--diag-cu-split", type=int, default=0,
+                    help="diagnostics only (A/B): the learner stream on this many CUs (spread CU-mask bits) and the env "
+                         "stream on the rest (hipExtStreamCreateWithCUMask, two masked streams made once)")
     ap.add_argument("--diag-knob", action="append", default=[],
                     help="diagnostics only (A/B): name=value for flock_set_diag before anything is built, e.g. "
                          "sc_event_system_scope=1 (the learner pipeline's events as system-scope fences)")
@@ -510,6 +514,24 @@ def policy_loop(hook, env, first, steps):
                     "learn(agent s mod 256), serial: the next step's actions need this learn()'s actor update"}
 
 
+def cu_split_streams(dev, keep):
+    """Two CU-masked streams (diagnostics): the learner's on `keep` CUs spread over the mask bits, the env's on the
+    rest."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    lb = [i for i in range(ncu) if (i * keep) // ncu != ((i + 1) * keep) // ncu]
+
+    def masked(bits):
+        words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
+        for i in bits:
+            words[i // 32] |= 1 << (i % 32)
+        h = ctypes.c_void_p()
+        assert hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), words) == 0
+        return torch.cuda.ExternalStream(h.value, device=dev)
+
+    return masked(lb), masked([i for i in range(ncu) if i not in set(lb)])
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
@@ -551,6 +573,11 @@ def main():
         from marl_range_flocking_amd.learners.shared_critic import SharedCriticBench
 
         hook = SharedCriticBench(env, device=dev, seed=1234 + rank, overlap=bool(args.overlap), n_slots=args.sc_slots)
+        if args.diag_cu_split > 0:  # A/B diagnostics: the GPU partitioned between the learner and the env stream
+            ls_m, es_m = cu_split_streams(dev, args.diag_cu_split)
+            torch.cuda.synchronize(dev)
+            torch.cuda.set_stream(es_m)
+            hook.stream = ls_m
     elif args.learner == "vdn":
         hook = VDNBench(env, dev, seed=1234 + rank,
                         overlap=bool(args.overlap) and args.train_overlap in ("auto", "1"))
@@ -734,6 +761,7 @@ def main():
         **({"diag_presleep_us": args.diag_presleep_us} if args.diag_presleep_us > 0 else {}),
         **({"diag_prewarm_ms": args.diag_prewarm_ms} if args.diag_prewarm_ms > 0 else {}),
         **({"diag_knobs": args.diag_knob} if args.diag_knob else {}),
+        **({"diag_cu_split": args.diag_cu_split} if args.diag_cu_split else {}),
         "host_enqueue_us_per_step": host_us,
         "host_path": ("torch.classes.flock.ScTrainLoop: all timed steps in one C++ call" if use_loop else
                       f"VecFlockEnv.rollout: {R} steps per call (torch.ops.flock.rollout_uw)" if use_rollout else

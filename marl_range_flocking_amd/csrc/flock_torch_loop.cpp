@@ -314,11 +314,16 @@ struct ScPipeline : torch::CustomClassHolder {
     // its hardware queue with the env stream once a process has more streams than GPU_MAX_HW_QUEUES: the same loop
     // then serialises, profiles/r05/rccl_host/host_cost_q4.txt). Non-blocking; high = the device's greatest priority,
     // whose streams HIP places on hardware queues apart from the normal-priority ones (the env stream's)
-    static int64_t stream(int64_t device_index, bool high) {
+    static int64_t stream(int64_t device_index, bool high) { return owned_stream(device_index, high ? 1 : 0); }
+    // the overlapped-train update stream of the config-4 / 5 learners (learners/core.py OverlappedTrain): normal
+    // priority, distinct from the learn() pipelines' streams
+    static int64_t side_stream(int64_t device_index) { return owned_stream(device_index, 2); }
+    // kind 0: normal priority, 1: high priority, 2: the side stream; created once per device and kept for the process
+    static int64_t owned_stream(int64_t device_index, int kind) {
         static std::mutex m;
-        static std::map<std::pair<int64_t, bool>, hipStream_t> streams;
+        static std::map<std::pair<int64_t, int>, hipStream_t> streams;
         const std::lock_guard<std::mutex> lock(m);
-        const auto key = std::make_pair(device_index, high);
+        const auto key = std::make_pair(device_index, kind);
         auto it = streams.find(key);
         if (it != streams.end()) return reinterpret_cast<int64_t>(it->second);
         const c10::hip::HIPGuard g((c10::DeviceIndex)device_index);
@@ -326,7 +331,8 @@ struct ScPipeline : torch::CustomClassHolder {
         TORCH_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess,
                     "ScPipeline.stream: hipDeviceGetStreamPriorityRange");
         hipStream_t s = nullptr;
-        TORCH_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, high ? greatest : least) == hipSuccess && s,
+        TORCH_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, kind == 1 ? greatest : least) == hipSuccess &&
+                        s,
                     "ScPipeline.stream: hipStreamCreateWithPriority");
         streams[key] = s;
         return reinterpret_cast<int64_t>(s);
@@ -529,6 +535,7 @@ TORCH_LIBRARY_FRAGMENT(flock, m) {
         .def("set_gate", &ScPipeline::set_gate)
         .def("mark", &ScPipeline::mark)
         .def_static("stream", &ScPipeline::stream)
+        .def_static("side_stream", &ScPipeline::side_stream)
         .def("set_dp_actor", &ScPipeline::set_dp_actor)
         .def("set_rccl", &ScPipeline::set_rccl)
         .def_static("rccl_unique_id", &ScPipeline::rccl_unique_id);

@@ -674,7 +674,13 @@ class OverlappedTrain:
         self.ring = ring
         self.snap = ReplayRing(n_rows, ring.fields, ring.device, aliases=ring.aliases)
         self.snap.counter = n_rows
-        self.stream = torch.cuda.Stream(ring.device)
+        # a stream created once per device in C++ (not torch's pool: a pool stream may share the env stream's hardware
+        # queue, and the update would then run behind the env steps instead of beside them)
+        from .. import torch_ops
+
+        torch_ops.load()
+        h = torch.classes.flock.ScPipeline.side_stream(ring.device.index or 0)
+        self.stream = torch.cuda.ExternalStream(h, device=ring.device)
         self.done = torch.cuda.Event()
         self.pending = False
         self.graph = None
