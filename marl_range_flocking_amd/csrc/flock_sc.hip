@@ -2493,12 +2493,11 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const int mark = p->mark;
     p->mark = 0;
     const bool gated = p->gate_on && mark;
-    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated, else
-    // an event (and always an event for split data-parallel rounds, whose actor halves run on a stream of their own).
-    // Data-parallel rounds: the round that consumed the slot may sit behind an all-reduce that waits for the other
-    // ranks, so the poll's bound is 60 s there (a collective that never completes hangs the ranks anyway)
-    const bool dev_free = gated && !g_sc_free_events && !(p->dp && p->split);
-    const unsigned long long ticks = p->dp ? 30 * kGateTimeoutTicks : kGateTimeoutTicks;
+    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated and
+    // the rounds single-GPU, else an event. Data-parallel rounds keep the event: their Adam launch
+    // (flock_sc_round_adam) reads the slot's agent word, which the snapshot rewrites, after the round's k1 launch
+    const bool dev_free = gated && !p->dp && !g_sc_free_events;
+    const unsigned long long ticks = kGateTimeoutTicks;
     const unsigned long long reuse = (p->used[s] && dev_free) ? p->gseq[s] : 0;
     if (p->used[s] && !reuse) {
         if (p->gseq[s]) {  // a gated learn freed on the device, reused now by the event path: everything enqueued so far
