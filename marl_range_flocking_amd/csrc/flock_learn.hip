@@ -616,8 +616,20 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
                                                              const float* __restrict__ W, const float* __restrict__ bias,
                                                              const uint8_t* __restrict__ keep, int64_t kt, int64_t ka,
                                                              int64_t kb, float* __restrict__ hs,
-                                                             float* __restrict__ ws, QHead qh = QHead{}) {
+                                                             float* __restrict__ ws, QHead qh = QHead{}, int Bg = 0) {
+    // row chunks (the rows' recurrences are independent): block (a, y) runs rows [y B, y B + B) of the Bg rows
+    // (Bg = 0: one chunk of B rows); global rows are indexed in Bg, the LDS state in the chunk
+    // (the fused q head's instantiation runs one chunk: QH compiles the chunk arithmetic out)
     extern __shared__ float4 seq_smem[];
+    const int64_t rb0 = (!QH && Bg) ? (int64_t)blockIdx.y * B : 0;
+    const int64_t BG = (!QH && Bg) ? Bg : B;
+    if constexpr (!QH) {
+        if (Bg) B = (int)min((int64_t)B, BG - rb0);
+        gi += rb0 * 3 * H;
+        keep += rb0 * kb;
+        if (hs) hs += rb0 * H;
+        if (ws) ws += rb0 * 4 * H;
+    }
     float* hcur = reinterpret_cast<float*>(seq_smem);
     float* hnxt = hcur + B * H;
     float* hq = hnxt + B * H;      // QH: [2][B][H] step outputs (ping-pong)
@@ -651,7 +663,7 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
             for (int u = 0; u < RB; ++u) {
                 const int b = b0 + u * bstep;
                 if (b < B) {
-                    const float* g = gi + ((a * C + t) * B + b) * 3 * H;
+                    const float* g = gi + ((a * C + t) * BG + b) * 3 * H;
                     gr[u] = g[j];
                     gz[u] = g[H + j];
                     gn[u] = g[2 * H + j];
@@ -672,7 +684,7 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
                     sr = fmaf(wr[4 * i4 + 2], v.z, sr); sz = fmaf(wz[4 * i4 + 2], v.z, sz); sn = fmaf(wn[4 * i4 + 2], v.z, sn);
                     sr = fmaf(wr[4 * i4 + 3], v.w, sr); sz = fmaf(wz[4 * i4 + 3], v.w, sz); sn = fmaf(wn[4 * i4 + 3], v.w, sn);
                 }
-                const int64_t row = (a * C + t) * B + b;
+                const int64_t row = (a * C + t) * BG + b;
                 const float r = sigmoidf_((sr + br) + gr[u]);
                 const float z = sigmoidf_((sz + bz) + gz[u]);
                 const float ghn = sn + bn;
@@ -707,7 +719,7 @@ __global__ __launch_bounds__(kBlock) void gru_seq_fwd_kernel(int C, int B, const
                     acc = fmaf(w.z, h.z, acc);
                     acc = fmaf(w.w, h.w, acc);
                 }
-                qh.q[((a * C + t) * B + b) * qh.NA + o] = acc;
+                qh.q[((a * C + t) * BG + rb0 + b) * qh.NA + o] = acc;
             }
         }
         float* tmp = hcur;
@@ -740,8 +752,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
                                                              const uint8_t* __restrict__ keep, int64_t kt, int64_t ka,
                                                              int64_t kb, float* __restrict__ dgi,
                                                              float* __restrict__ dW, float* __restrict__ db,
-                                                             QHeadBwd qh = QHeadBwd{}) {
+                                                             QHeadBwd qh = QHeadBwd{}, int Bg = 0, int64_t rb0 = 0,
+                                                             int acc = 0) {
+    // row chunk (non-QH): rows [rb0, rb0 + B) of Bg (Bg = 0: all B rows); acc: dW / db += this chunk's sums (chunks
+    // launched in order on one stream, so the sums run over the chunks in row order)
     constexpr bool QH = NQ > 0;
+    const int64_t BG = (!QH && Bg) ? Bg : B;
+    if constexpr (!QH) {
+        dhs += rb0 * H;
+        hs += rb0 * H;
+        ws += rb0 * 4 * H;
+        keep += rb0 * kb;
+        dgi += rb0 * 3 * H;
+    } else {
+        acc = 0;
+    }
     constexpr int NQA = QH ? NQ : 1;
     constexpr int G = 3 * H, NW = G * H / kBlock;  // dW entries per thread
     extern __shared__ float4 seq_smem[];
@@ -776,14 +801,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
         for (int e = tid; e < B * H; e += kBlock) {
             const int b = e / H;
             float v = 0.0f;
-            if (t > 0 && keep[(t - 1) * kt + a * ka + b * kb]) v = hs[((a * C + t - 1) * B + b) * H + (e - b * H)];
+            if (t > 0 && keep[(t - 1) * kt + a * ka + b * kb]) v = hs[((a * C + t - 1) * BG + b) * H + (e - b * H)];
             hprev[e] = v;
         }
         if (QH)  // this step's dq rows (contiguous [B][NA]) into LDS: one coalesced round trip, broadcast reads below
             for (int e = tid; e < B * qh.NA; e += kBlock) dqs[e] = dhs[(a * C + t) * B * qh.NA + e];
         __syncthreads();  // carry (previous iteration), hprev and dq visible
         for (int b = tid / H; b < B; b += bstep) {
-            const int64_t row = (a * C + t) * B + b;
+            const int64_t row = (a * C + t) * BG + b;
             const float* w = ws + row * 4 * H;
             const float r = w[i], z = w[H + i], nn = w[2 * H + i], ghn = w[3 * H + i];
             float dho;
@@ -872,9 +897,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2))) voi
 #pragma unroll
     for (int q = 0; q < NW; ++q) {  // entry (g, ii) of thread tid: g = 4 (m0 + (kBlock / H) (q / 4)) + q % 4
         const int g = 4 * (tid / H + (kBlock / H) * (q >> 2)) + (q & 3);
-        dW[a * G * H + g * H + tid % H] = accw[q];
+        float* d = dW + a * G * H + g * H + tid % H;
+        *d = acc ? *d + accw[q] : accw[q];
     }
-    if (tid < G) db[a * G + tid] = accb;
+    if (tid < G) db[a * G + tid] = acc ? db[a * G + tid] + accb : accb;
     if (QH) {  // the q head's gradients: the bstep row groups' partials summed in group order
         float* redb = dgh;  // [bstep][NA] db_q partials (the loop is done with dgh: its last barrier)
         const int grp = tid / H;
@@ -1061,18 +1087,24 @@ int flock_gru_bwd(void* stream, int64_t rows, int H, const float* dhout, const f
     return launched();
 }
 
+// rows per block of the whole-chunk GRU recurrences: LDS [2][rows][32] floats forward (<= 160 KB: 640 rows), [5][rows]
+// [32] backward (256 rows)
+constexpr int kSeqRows = 640, kSeqBwdRows = 256;
+
 int flock_gru_seq_fwd(void* stream, int A, int C, int B, int H, const float* gi, const float* w_hh, const float* b_hh,
                       const uint8_t* keep, int64_t keep_st, int64_t keep_sa, int64_t keep_sb, float* hs, float* ws) {
     if (A <= 0 || C <= 0 || B <= 0) return 0;
     if (!gi || !w_hh || !b_hh || !keep || !hs) return fail(-3, "flock_gru_seq_fwd: NULL pointer");
     if (H != 32) return fail(-2, "flock_gru_seq_fwd: hidden size must be 32");
-    const size_t lds = (size_t)2 * B * H * sizeof(float);
-    if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_fwd: B too large for LDS");
+    // more rows than one block's LDS holds (e.g. the union batch of agent-sharded critics at 8 ranks): row chunks of
+    // kSeqRows in grid y (the rows' recurrences are independent)
+    const int Bc = B <= kSeqRows ? B : kSeqRows, nch = (B + Bc - 1) / Bc;
+    const size_t lds = (size_t)2 * Bc * H * sizeof(float);
     if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(gru_seq_fwd_kernel<32>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(-4, "flock_gru_seq_fwd: cannot raise the LDS limit");
-    hipLaunchKernelGGL(gru_seq_fwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, gi, w_hh, b_hh,
-                       keep, keep_st, keep_sa, keep_sb, hs, ws);
+    hipLaunchKernelGGL(gru_seq_fwd_kernel<32>, dim3(A, nch), dim3(kBlock), lds, (hipStream_t)stream, C, Bc, gi, w_hh,
+                       b_hh, keep, keep_st, keep_sa, keep_sb, hs, ws, QHead{}, nch > 1 ? B : 0);
     return launched();
 }
 
@@ -1090,7 +1122,7 @@ int flock_gru_seq_q_fwd(void* stream, int A, int C, int B, int H, int NA, const 
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(-4, "flock_gru_seq_q_fwd: cannot raise the LDS limit");
     hipLaunchKernelGGL((gru_seq_fwd_kernel<32, true>), dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, gi, w_hh,
-                       b_hh, keep, keep_st, keep_sa, keep_sb, hs, ws, QHead{w_q, b_q, q, NA});
+                       b_hh, keep, keep_st, keep_sa, keep_sb, hs, ws, QHead{w_q, b_q, q, NA}, 0);
     return launched();
 }
 
@@ -1115,7 +1147,7 @@ int flock_gru_seq_q_bwd(void* stream, int A, int C, int B, int H, int NA, const 
                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return fail(-4, "flock_gru_seq_q_bwd: cannot raise the LDS limit");
         hipLaunchKernelGGL(kern, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dq, hs, ws, w_hh, keep,
-                           keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh, qh);
+                           keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh, qh, 0, (int64_t)0, 0);
         return launched();
     };
     // registers sized for the head: the smallest instantiation that holds NA
@@ -1133,14 +1165,20 @@ int flock_gru_seq_bwd(void* stream, int A, int C, int B, int H, const float* dhs
     if (!dhs || !hs || !ws || !w_hh || !keep || !dgi || !dw_hh || !db_hh)
         return fail(-3, "flock_gru_seq_bwd: NULL pointer");
     if (H != 32) return fail(-2, "flock_gru_seq_bwd: hidden size must be 32");
-    const size_t lds = (size_t)B * (3 * H + 2 * H) * sizeof(float);
-    if (lds > 160 * 1024) return fail(-2, "flock_gru_seq_bwd: B too large for LDS");
+    // more rows than one block's LDS holds: row chunks of kSeqBwdRows launched in order, each adding its dW / db sums
+    const int Bc = B <= kSeqBwdRows ? B : kSeqBwdRows;
+    const size_t lds = (size_t)Bc * (3 * H + 2 * H) * sizeof(float);
     if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(gru_seq_bwd_kernel<32>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return fail(-4, "flock_gru_seq_bwd: cannot raise the LDS limit");
-    hipLaunchKernelGGL(gru_seq_bwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, B, dhs, hs, ws,
-                       w_hh, keep, keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh);
-    return launched();
+    for (int b0 = 0; b0 < B; b0 += Bc) {
+        const int n = B - b0 < Bc ? B - b0 : Bc;
+        hipLaunchKernelGGL(gru_seq_bwd_kernel<32>, dim3(A), dim3(kBlock), lds, (hipStream_t)stream, C, n, dhs, hs, ws,
+                           w_hh, keep, keep_st, keep_sa, keep_sb, dgi, dw_hh, db_hh, QHeadBwd{}, Bc < B ? B : 0,
+                           (int64_t)b0, b0 > 0 ? 1 : 0);
+        if (int rc = launched()) return rc;
+    }
+    return 0;
 }
 
 int flock_vdn_feat_fwd(void* stream, int A, int R, int B, int n_in, const float* x, int64_t x_sa, int64_t x_sc,

@@ -148,10 +148,13 @@ def test_ring_store_fused_matches_row_copies(cap, n, steps, cuda):
 
 
 @pytest.mark.parametrize("A,C,B,per_agent", [(3, 10, 32, False), (5, 10, 128, True), (2, 1, 7, True), (4, 4, 200, False),
-                                             (2, 3, 16, True), (3, 5, 8, False), (512, 10, 32, False)])
+                                             (2, 3, 16, True), (3, 5, 8, False), (512, 10, 32, False),
+                                             (2, 3, 1000, True), (3, 4, 700, False)])
 def test_gru_seq_matches_per_step_grucell(A, C, B, per_agent, cuda):
     """flock_gru_seq_fwd/_bwd (one launch per chunk) against the per-step loop the learners used before: gru_cell
-    per step (hidden GEMM + gate kernel) with the done reset between steps, fp32 autograd, same inputs."""
+    per step (hidden GEMM + gate kernel) with the done reset between steps, fp32 autograd, same inputs. B = 700 and
+    1000: more rows than one block's LDS holds (the union batch of agent-sharded critics at 8 ranks): row chunks of
+    640 in the forward launch, 256-row backward launches adding their dW / db sums in order."""
     g = torch.Generator(device=cuda).manual_seed(A * 100 + B)
     H = 32
     gi = torch.randn(A, C, B, 3 * H, device=cuda, generator=g, requires_grad=True)

@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 6: the multi-rank GPU tests (gloo ranks on one GPU, world 2 / 4 / 8), the pipeline and overlapped-train tests
-# (slots freed on the device, the C++-owned side stream), configs 4 / 5 once, then the bench's N > 1 path rehearsed
-# with 8 and 4 gloo ranks on the one GPU (not a scaling number)
+# Round 6: the GRU-recurrence row chunks, the multi-rank GPU tests (gloo ranks on one GPU, world 2 / 4 / 8), the
+# pipeline and overlapped-train tests, configs 4 / 5 once, then the bench's N > 1 path rehearsed with 8 and 4 gloo
+# ranks on the one GPU (not a scaling number), then the acting-kernel variants
 set -o pipefail
 O=gpurun_out/r6dist; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_overlap.py tests/test_gpu_train_loop.py tests/test_gpu_overlap_train.py -x -v --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_learn_kernels.py tests/test_gpu_dist.py tests/test_gpu_overlap.py tests/test_gpu_train_loop.py tests/test_gpu_overlap_train.py -x -v --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
 tail -3 $O/pytest.txt
 for c in 4 5; do
   timeout -k 10 300 python bench.py --config $c --no-cpu-baseline > $O/bench_c$c.json 2> $O/err.txt || { tail $O/err.txt; exit 1; }
@@ -12,3 +12,4 @@ for c in 4 5; do
 done
 NPROC=8 CONFIGS="3 5 4" bash tools/gpu_dist_rehearsal.sh || exit 1
 NPROC=4 CONFIGS="3" bash tools/gpu_dist_rehearsal.sh || exit 1
+bash tools/gpu_r6_act.sh bpf2 w3bpf4
