@@ -730,6 +730,8 @@ def main():
 
     pt = pmc(os.path.basename(args.pmc)) if args.pmc else pmc(f"pmc_{tag}.json")
     traffic = pt.get("hbm_bytes_per_launch") if pt else None
+    if traffic is not None and use_rollout:  # per step, like achieved: the PMC pass's launches ran R steps each
+        traffic = traffic / pt.get("steps_per_launch", R)
     vp = pmc(f"pmc_valu_{tag}.json")
     valu = None
     if vp and "SQ_ACTIVE_INST_VALU2" in vp:

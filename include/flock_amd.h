@@ -59,9 +59,8 @@ const char* flock_last_error(void);
  * pull-ahead of a later block's inputs in the shapes compiled with it), "sc_no_spec" (generic shared-critic row
  * kernels at fc 400/300), "sc_event_system_scope" (the learn() pipeline's events as HIP's default system-scope fences
  * instead of device-scope releases; read when a pipeline is created), "sc_free_events" (every learn() slot freed by
- * a learner-stream event, as in round 5, instead of on the device for gated single-GPU learns), "env_cu_blocks" (at
- * most this many env blocks per CU, 0 = no cap: the specialised step launches' LDS size padded), "rollout_spl" (2 or
- * 4 lanes per agent in the uw rollout kernel). The library reads no environment variable for them: flock_set_diag is the only way to
+ * a learner-stream event, as in round 5, instead of on the device for gated single-GPU learns), "rollout_spl" (2 or 4
+ * lanes per agent in the uw rollout kernel). The library reads no environment variable for them: flock_set_diag is the only way to
  * set them (process-wide; not thread-safe against concurrent launches). Returns FLOCK_OK, or FLOCK_E_ARG for an
  * unknown name. */
 int flock_set_diag(const char* name, int value);

@@ -1888,8 +1888,6 @@ struct Knobs {
     bool no_spec = false, no_split = false, no_cells = false;
     int pf = -1;
     int rollout_spl = 2;  // lanes per agent of the uw rollout kernel (2 or 4)
-    int cu_blocks = 0;    // > 0: at most this many env blocks per CU (the launch's LDS size padded), so that wave
-                          // slots stay free for a learner kernel dispatched while an env launch fills the machine
 };
 Knobs& knobs_mut() {
     static Knobs k;
@@ -1931,10 +1929,6 @@ bool launch_spec(const Cfg& c0, const Params& p0, hipStream_t s) {
         c = make_cfg(p.E, NC, false, 0, 0, 0, 1);
         c.T = SPL * NC;
         c.lds = ((c.lds + 15) & ~(size_t)15) + (size_t)(SPL - 1) * 6 * NC * sizeof(uint32_t);
-    }
-    if (knobs().cu_blocks > 0) {  // 160 KB of LDS per CU: cu_blocks blocks fit, one more does not
-        const size_t cap = (size_t)160 * 1024 / (knobs().cu_blocks + 1) + 1024;
-        c.lds = c.lds > cap ? c.lds : cap;
     }
     const int parts = env_launches(c.blocks, p.launches);
     if (PF != 0 && parts <= 1 && knobs().pf != 0) {  // each block pulls a later block's inputs into L2
@@ -2087,8 +2081,6 @@ int flock_set_diag(const char* name, int value) {
         k.pf = value;
     else if (!strcmp(name, "rollout_spl") && (value == 2 || value == 4))
         k.rollout_spl = value;
-    else if (!strcmp(name, "env_cu_blocks") && value >= 0 && value <= 16)
-        k.cu_blocks = value;
     else if (!strcmp(name, "sc_no_spec"))
         flock_sc_diag_no_spec(value != 0);
     else if (!strcmp(name, "sc_event_system_scope"))

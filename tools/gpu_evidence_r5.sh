@@ -16,7 +16,7 @@ tag_of() { case $1 in 3) echo v2_ring_N256_E4096;; 2) echo uw_N64_E1024;; 4) ech
 alg_of() { case $1 in 3) echo $(( (93 + 64) * 256 * 4096 ));; 2) echo $(( 149 * 64 * 1024 ));;
   4) echo $(( (69 + 56) * 512 * 8192 ));; 5) echo $(( (93 + 64) * 1024 * 16384 ));; esac; }
 if [[ $PHASES == *tests* ]]; then
-  step pytest_gpu.txt 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
+  step pytest_gpu.txt 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   tail -2 $OUT/pytest_gpu.txt
   step smoke.txt 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
