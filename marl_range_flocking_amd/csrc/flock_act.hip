@@ -63,9 +63,6 @@ constexpr int kKC16 = FLOCK_ACT16_KC;
 #define FLOCK_ACT16_PITCH (FLOCK_ACT16_KC + 2)
 #endif
 constexpr int kBP16 = FLOCK_ACT16_PITCH;
-#ifndef FLOCK_ACT16_BPF
-#define FLOCK_ACT16_BPF 0
-#endif
 #ifndef FLOCK_ACT16_WAVES
 #define FLOCK_ACT16_WAVES 4
 #endif
@@ -581,36 +578,12 @@ __global__ __launch_bounds__(256, FLOCK_ACT16_WAVES) void sc_act16_kernel(ActArg
             const int kn = k0 + ks + 8;
             a_vals(kn < H1 ? kn : 0, an);
             const float* bcol = sB + rl * kBP16 + ks + 2 * g;
-#if FLOCK_ACT16_BPF
-            // the next tile group's B pairs are read before this group's MFMAs (one LDS latency per step instead of
-            // one per group of MFMAs)
-            constexpr int GT = FLOCK_ACT16_BPF;  // tiles per group
-            float2 cur[GT], nxt[GT];
-#pragma unroll
-            for (int u = 0; u < GT; ++u)
-                cur[u] = u < NT ? *reinterpret_cast<const float2*>(bcol + 16 * u * kBP16) : make_float2(0.f, 0.f);
-#pragma unroll
-            for (int t = 0; t < NT; t += GT) {
-#pragma unroll
-                for (int u = 0; u < GT; ++u)
-                    if (t + GT + u < NT) nxt[u] = *reinterpret_cast<const float2*>(bcol + 16 * (t + GT + u) * kBP16);
-#pragma unroll
-                for (int u = 0; u < GT; ++u)
-                    if (t + u < NT) acc[t + u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cur[u].x, acc[t + u], 0, 0, 0);
-#pragma unroll
-                for (int u = 0; u < GT; ++u)
-                    if (t + u < NT) acc[t + u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cur[u].y, acc[t + u], 0, 0, 0);
-#pragma unroll
-                for (int u = 0; u < GT; ++u) cur[u] = nxt[u];
-            }
-#else
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const float2 bb = *reinterpret_cast<const float2*>(bcol + 16 * t * kBP16);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb.x, acc[t], 0, 0, 0);
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb.y, acc[t], 0, 0, 0);
             }
-#endif
             a[0] = an[0];
             a[1] = an[1];
         }

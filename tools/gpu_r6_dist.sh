@@ -7,7 +7,7 @@ set -o pipefail
 O=gpurun_out/r6dist; mkdir -p $O; export TMPDIR=/tmp
 (while true; do date >> $O/heartbeat.txt; sleep 30; done) & HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -k 10 1000 python -u -m pytest ${TESTS:-tests/test_gpu_dist.py tests/test_gpu_learn_kernels.py tests/test_gpu_overlap.py tests/test_gpu_train_loop.py tests/test_gpu_overlap_train.py} -x -v --durations=15 --timeout 600 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
+timeout -k 10 1000 python -u -m pytest ${TESTS:-tests/test_gpu_dist.py tests/test_gpu_learn_kernels.py tests/test_gpu_overlap.py tests/test_gpu_train_loop.py tests/test_gpu_overlap_train.py} -x -v --durations=15 --timeout ${PT_TIMEOUT:-600} --timeout-method thread > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
 tail -20 $O/pytest.txt
 [ -n "${ONLY_TESTS:-}" ] && exit 0
 for c in 4 5; do
@@ -16,4 +16,4 @@ for c in 4 5; do
 done
 NPROC=8 CONFIGS="3 5 4" bash tools/gpu_dist_rehearsal.sh || exit 1
 NPROC=4 CONFIGS="3" bash tools/gpu_dist_rehearsal.sh || exit 1
-bash tools/gpu_r6_act.sh bpf2 w3bpf4
+bash tools/gpu_r6_act.sh bpf2 w3bpf4 av
