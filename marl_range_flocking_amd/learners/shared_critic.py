@@ -537,7 +537,7 @@ class SharedCriticLearner:
         one call. ONE object per learner: the per-step path (pipeline_learn) and the C++ training loop
         (ScTrainLoop) share its slots and its pending actor phase. The round waits for its snapshot on the device-side
         gate (handoff="gate", single-GPU and data-parallel pipelines alike, for a learn whose env step was marked:
-        pipeline_mark) or on a cross-queue event. Data-parallel learners (dist_group) run every
+        pipeline_mark; not when ranks share a GPU) or on a cross-queue event. Data-parallel learners (dist_group) run every
         round as gradients, one RCCL all-reduce of the critic gradient over the group and the critic Adam launch on
         the learner stream; with dp_split (opt-in) the round's actor gradient is all-reduced over a second group and
         stepped on the pipeline's actor stream, off the learner chain (set_dp_actor); without, one all-reduce of the
@@ -571,7 +571,12 @@ class SharedCriticLearner:
                     ids = ids.cpu()
                     p.set_rccl([ids[i].contiguous() for i in range(3)], ranks.index(torch.distributed.get_rank()),
                                len(ranks), self.learner_stream.cuda_stream)
-            p.set_gate(self.handoff == "gate")
+            # ranks sharing one GPU (gloo rehearsals and tests: more ranks than devices) take the event hand-off: a
+            # device-side wait needs its producer's queue to be scheduled, and with many processes' queues on one GPU
+            # the hardware scheduler time-slices them, so a round could spin (high priority) while its snapshot's
+            # queue waits for a slice
+            shared = self.distributed and torch.distributed.get_world_size(self.group) > torch.cuda.device_count()
+            p.set_gate(self.handoff == "gate" and not shared)
             self._pipe = p
         return self._pipe
 
