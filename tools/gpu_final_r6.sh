@@ -5,6 +5,8 @@
 # Two gpurun calls: PHASES=tests (GPU suite + smoke), then PHASES="pmc bench driver" (the default)
 set -u
 OUT=gpurun_out/ev6; mkdir -p $OUT; export TMPDIR=/tmp
+(while true; do date >> $OUT/heartbeat.txt; sleep 30; done) & HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 P=${PHASES:-pmc bench driver}
 if [[ $P == *tests* ]]; then EV_OUT=$OUT PHASES=tests bash tools/gpu_evidence_r5.sh || exit 1; fi
 if [[ $P == *pmc* ]]; then
