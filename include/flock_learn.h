@@ -224,12 +224,12 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
  * above any env step; a waiter that gives up sets an error word and computes nothing, flock_sc_pipeline_check
  * returns -6). flock_sc_pipeline_set_gate(p, 0) (and always under rocprofv3 counter collection, which serialises
  * dispatches) makes every learn() take the event wait; it returns the hand-off in use (1 gate, 0 events). The gate
- * serves single-GPU and data-parallel pipelines alike. Slot reuse: when a single-GPU learn() and the slot's previous
- * learn() are both gated, the previous round's fc2 GEMM launch (after its row launch, the staging rows' and agent
- * word's only reader there) stores that learn's sequence number write-through and the new snapshot polls it (bounded
- * like the gate) before writing; otherwise (event hand-off, data-parallel rounds, whose Adam launch reads the slot's
- * agent word later in the round, flock_set_diag "sc_free_events") the env stream waits for a learner-stream event
- * recorded after the round that freed the slot. Both hand-offs are deadlock-free whatever
+ * serves single-GPU and data-parallel pipelines alike. Slot reuse: when a learn() and the slot's previous learn() are
+ * both gated, the previous round's fc2 GEMM launch (after its row launch, the staging rows' only reader; the later
+ * launches carry the agent index by value) stores that learn's sequence number write-through and the new snapshot
+ * polls it before writing (bounded like the gate; 60 s for data-parallel rounds, whose GEMM may sit behind an
+ * all-reduce waiting for other ranks); otherwise (event hand-off, split data-parallel rounds, flock_set_diag
+ * "sc_free_events") the env stream waits for a learner-stream event recorded after the round that freed the slot. Both hand-offs are deadlock-free whatever
  * hardware queues the streams map to: every snapshot is enqueued before the round that waits for it, and a snapshot
  * waits only for a round enqueued before it whose own snapshot precedes it on env_stream. The actor phase of the last learn() stays pending until the
  * next call or flock_sc_pipeline_flush (which enqueues it on learner_stream). Results are bitwise those of the serial

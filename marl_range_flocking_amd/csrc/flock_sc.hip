@@ -2027,6 +2027,8 @@ __global__ __launch_bounds__(256) void sc_prep_snapshot_gate(int B, int64_t rows
 void flock_sc_diag_no_spec(bool v) { g_sc_no_spec = v; }
 void flock_sc_diag_event_system(bool v);  // below (the pipeline's event flags)
 
+int round_adam(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u, const float* grad_scale,
+               int64_t agent_c, int64_t agent_a);
 extern "C" {
 
 int flock_sc_prep_snapshot(void* stream, int B, int64_t rows, uint64_t seed, uint64_t counter, int64_t* idx_out,
@@ -2069,6 +2071,14 @@ int flock_sc_actor_update(void* stream, const FlockScUpdate* u) { return flock_s
 
 int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u,
                         const float* grad_scale) {
+    return round_adam(stream, critic_u, actor_u, grad_scale, -1, -1);
+}
+}  // extern "C"
+
+// flock_sc_round_adam with the learns' agent indices by value when >= 0 (the pipeline's data-parallel rounds: the
+// slot's agent word may already hold a later learn's agent, written by a snapshot released at this round's GEMM)
+int round_adam(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u, const float* grad_scale,
+               int64_t agent_c, int64_t agent_a) {
     if (!critic_u && !actor_u) return fail(-3, "flock_sc_round_adam: NULL argument");
     int rc = 0;
     if (critic_u && (rc = check(critic_u))) return rc;
@@ -2103,6 +2113,8 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
         ja.ga.adam_n = ao.total;
         ja.ga.adam_blocks = (int)((ao.total + 1023) / 1024);
     }
+    if (critic_u) jc.ga.agent_v = agent_c;
+    if (actor_u) ja.ga.agent_v = agent_a;
     GradAdam2 gg;
     gg.j0 = *js[0];
     gg.j1 = *js[n - 1];
@@ -2111,6 +2123,7 @@ int flock_sc_round_adam(void* stream, const FlockScUpdate* critic_u, const Flock
     hipLaunchKernelGGL(sc_grad_adam, dim3(nb), dim3(256), 0, (hipStream_t)stream, gg);
     return launched();
 }
+extern "C" {
 
 int flock_sc_round(void* stream, const FlockScUpdate* critic_u, const FlockScUpdate* actor_u) {
     if (!critic_u && !actor_u) return fail(-3, "flock_sc_round: NULL argument");
@@ -2291,8 +2304,8 @@ int pipeline_round(FlockScPipeline* p, hipStream_t ls, int c, int a, int64_t age
         const int64_t lo = c >= 0 ? 0 : p->actor_off, hi = a >= 0 ? p->bucket_floats : p->critic_floats;
         if ((rc = p->allreduce(p->allreduce_ctx, p->bucket + lo, hi - lo, ls)))
             return fail(rc < 0 ? rc : -4, "flock_sc_pipeline: the all-reduce callback failed");
-        return flock_sc_round_adam(ls, c >= 0 ? &p->uadam[c] : nullptr, a >= 0 ? &p->uadam[a] : nullptr,
-                                   p->grad_scale);
+        return round_adam(ls, c >= 0 ? &p->uadam[c] : nullptr, a >= 0 ? &p->uadam[a] : nullptr, p->grad_scale,
+                          agent_c, agent_a);
     }
     // split: the critic half stays on the learner chain (the next critic phase needs this critic step), its larger
     // part all-reduced beside the gradient launch; the actor half is all-reduced and stepped on actor_stream (that
@@ -2493,11 +2506,14 @@ int flock_sc_pipeline_learn(FlockScPipeline* p, void* env_stream, void* learner_
     const int mark = p->mark;
     p->mark = 0;
     const bool gated = p->gate_on && mark;
-    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated and
-    // the rounds single-GPU, else an event. Data-parallel rounds keep the event: their Adam launch
-    // (flock_sc_round_adam) reads the slot's agent word, which the snapshot rewrites, after the round's k1 launch
-    const bool dev_free = gated && !p->dp && !g_sc_free_events;
-    const unsigned long long ticks = kGateTimeoutTicks;
+    // slot reuse (the previous learn's snapshot in this slot consumed): on the device when both learns are gated,
+    // else an event (and always an event for split data-parallel rounds, whose actor halves run on a stream of their
+    // own). Every launch of a round after its k1 launch gets the learns' agent indices by value (with_agent, and
+    // round_adam for the data-parallel Adam launch), since the snapshot released at the GEMM rewrites the slot's agent
+    // word. Data-parallel rounds: the consuming round's GEMM may sit behind an all-reduce that waits for the other
+    // ranks, so the poll's bound is 60 s there (a collective that never completes hangs the ranks anyway)
+    const bool dev_free = gated && !g_sc_free_events && !(p->dp && p->split);
+    const unsigned long long ticks = p->dp ? 30 * kGateTimeoutTicks : kGateTimeoutTicks;
     const unsigned long long reuse = (p->used[s] && dev_free) ? p->gseq[s] : 0;
     if (p->used[s] && !reuse) {
         if (p->gseq[s]) {  // a gated learn freed on the device, reused now by the event path: everything enqueued so far
