@@ -803,7 +803,8 @@ def main():
                               "step; frac on SURVEY 8(d)'s 149-B accounting (a single step reads and rewrites the "
                               "state and the memory); the rollout moves the action read and the observation / "
                               "reward / done writes (moved_bytes_per_agent_step)" if use_rollout else
-                              "kernel_ms / frac / valu: HIP events around every 4th env step of the timed region (the "
+                              f"kernel_ms / frac / valu: HIP events around every {EV_EVERY}th env step of the timed "
+                              "region (the "
                               "step's launches, with the learner's kernels beside them); *_alone: the same step as one "
                               "launch with no learner, after the timed region")},
     }
