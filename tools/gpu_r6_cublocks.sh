@@ -1,4 +1,5 @@
 #!/bin/bash
+# HISTORICAL (round 6): the knob this A/B sets was removed after it measured flat / slower; flock_set_diag now rejects it, so the script fails fast against the current tree.
 # Round 6: env blocks per CU capped through the launch's LDS size (flock_set_diag env_cu_blocks 0 = off / 7 / 6), so a
 # learner kernel dispatched while an env launch fills the machine finds free wave slots: interleaved config-3 A/B
 # (driver command + 200 steps)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6: the GRU-recurrence row chunks, the multi-rank GPU tests (gloo ranks on one GPU, world 2 / 4 / 8), the
 # pipeline and overlapped-train tests, configs 4 / 5 once, then the bench's N > 1 path rehearsed with 8 and 4 gloo
-# ranks on the one GPU (not a scaling number), then the acting-kernel variants. A heartbeat file keeps the silence
+# ranks on the one GPU (not a scaling number). A heartbeat file keeps the silence
 # watchdog informed while the 8-rank tests run (their ranks print nothing for minutes).
 set -o pipefail
 O=gpurun_out/r6dist; mkdir -p $O; export TMPDIR=/tmp
@@ -16,4 +16,3 @@ for c in 4 5; do
 done
 NPROC=8 CONFIGS="3 5 4" bash tools/gpu_dist_rehearsal.sh || exit 1
 NPROC=4 CONFIGS="3" bash tools/gpu_dist_rehearsal.sh || exit 1
-bash tools/gpu_r6_act.sh bpf2 w3bpf4 av

@@ -1,4 +1,5 @@
 #!/bin/bash
+# HISTORICAL (round 6): the knob this A/B sets was removed after it measured flat / slower; flock_set_diag now rejects it, so the script fails fast against the current tree.
 # Round 6: forward GEMM K slices (flock_set_diag sc_fwd_split 1 / 2 / 4): the pipeline tests, an interleaved config-3
 # A/B (driver command + 200 steps) and a kernel trace of each
 set -o pipefail
