@@ -2,7 +2,7 @@
 # Longer runs as a stability check (the device gate's error word is checked after the timed region by bench.py):
 # config 3 with 3000 timed steps, config 4 with 1500, config 5 with 1000 (gpurun_out/long/).
 set -u
-O=gpurun_out/long; mkdir -p $O
+O=${LONG_OUT:-gpurun_out/long}; mkdir -p $O
 for a in "3 3000" "4 1500" "5 1000"; do
   set -- $a
   timeout -k 10 300 python bench.py --config $1 --steps $2 --warmup 20 --no-cpu-baseline --policy-steps 0 > $O/config$1.json 2> $O/config$1.err || { tail -20 $O/config$1.err; exit 1; }
