@@ -1,4 +1,5 @@
 #!/bin/bash
+# HISTORICAL (round 6): the knob this A/B sets was removed after it measured slower; flock_set_diag now rejects it, so the script fails fast against the current tree.
 # Round 6: forward GEMMs as 32 x 64 tiles (flock_set_diag sc_fwd_wide 1) against 32 x 32: the pipeline tests, the
 # per-kernel durations of a short traced loop each, and an interleaved config-3 A/B (200 steps + the driver command)
 set -o pipefail
