@@ -8,7 +8,7 @@ import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 BUILD_DIR = os.path.join(PKG, "_build")
-LIB_PATH = os.environ.get("FLOCK_LIB") or os.path.join(BUILD_DIR, "libflock_amd.so")  # FLOCK_LIB: A/B of builds
+LIB_PATH = os.path.join(BUILD_DIR, "libflock_amd.so")  # A/B of builds: copy a variant over it (tools/gpu_ab_swap.sh)
 
 _c_void_p, _c_int, _c_float, _c_u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
 

@@ -1,4 +1,5 @@
 # A/B of library builds through bench.py (config 3 default): alternate runs, kernel_ms of each
+# HISTORICAL (rounds 1-2): selected builds through FLOCK_LIB, which the library no longer reads; tools/gpu_ab_swap.sh copies a variant over _build/libflock_amd.so instead.
 set -e
 for r in 1 2; do
   for lib in "$@"; do

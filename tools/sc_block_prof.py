@@ -34,9 +34,9 @@ def build():
 
 def run(corun, learns):
     # the learner launches through libflock_torch.so, which links _build/libflock_amd.so: run with the profiling
-    # build copied over it (SWAPPED=1; tools/gpu_scprof.sh), else through FLOCK_LIB (the ctypes paths only)
+    # build copied over it (SWAPPED=1; tools/gpu_scprof.sh)
     if os.environ.get("SWAPPED") != "1":
-        os.environ["FLOCK_LIB"] = SO
+        raise SystemExit("run through tools/gpu_scprof.sh (the -DFLOCK_SC_PROF build copied over _build/libflock_amd.so)")
     sys.path.insert(0, ROOT)
     import numpy as np
     import torch
