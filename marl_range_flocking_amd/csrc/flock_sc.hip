@@ -714,68 +714,22 @@ __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned lon
 // dH1 tiles.
 __device__ __forceinline__ int xcd_perm(int x, int n) { return (n & 7) == 0 ? (x & 7) * (n >> 3) + (x >> 3) : x; }
 
-// L2 pull of the forward GEMM's B operands (the fc2.weight panels of the round's nets) by the k1 blocks of each XCD,
-// one dword per 128-B line, consumed by nothing (the lines are what the GEMM tiles of that XCD read next launch)
-struct Pull {
-    const float* p[2];
-    const int64_t* agent[2];  // p[i] + rel[i] * (*agent[i]) when agent[i] != NULL
-    int64_t agent_v[2];       // >= 0: the agent index itself
-    int64_t rel[2];
-    int64_t n[2];  // floats
-};
-// part: 0 every panel, 1 only the panels at fixed addresses, 2 only the agent-relative ones (the agent index of a
-// critic-phase job is part of its snapshot: read after the gate)
-__device__ __forceinline__ float pull_l2(const Pull& pl, int rank, int ranks, bool sc1_agent, int part = 0) {
-    float sink = 0.0f;
-    int64_t lines[2], total = 0;
-    const float* base[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        lines[i] = (pl.n[i] + 31) >> 5;
-        total += lines[i];
-        const bool skip = (part == 1 && pl.agent[i]) || (part == 2 && !pl.agent[i]);
-        const int64_t ag = (pl.agent[i] && !skip)
-                               ? (pl.agent_v[i] >= 0 ? pl.agent_v[i]
-                                                     : (sc1_agent ? flock_mem::ld_sc1(pl.agent[i]) : *pl.agent[i]))
-                               : 0;
-        base[i] = (pl.p[i] && !skip) ? pl.p[i] + pl.rel[i] * ag : nullptr;
-    }
-    const int64_t lo = total * rank / ranks, hi = total * (rank + 1) / ranks;
-    for (int64_t l = lo + threadIdx.x; l < hi; l += 256) {
-        const int i = l < lines[0] ? 0 : 1;
-        const int64_t li = i ? l - lines[0] : l;
-        if (base[i]) sink += base[i][li << 5];
-    }
-    return sink;
-}
-
+// Round 5 also had each XCD's k1 blocks pull the forward GEMM's fc2.weight panels into that XCD's L2 (one dword per
+// 128-B line): it took the GEMM 18.1 -> 14.5 us in the loop while the rounds waited on a slot-free event between them;
+// with the rounds back to back (round 6) the pull on k1's path cost more than it saved (same-box A/B, 200 steps
+// 0.0743-0.0750 without against 0.0775-0.0790 ms per step, driver command 0.0825-0.0849 against 0.0838-0.0863;
+// profiles/r06/nopull/) and was removed
 template <int C, int HC>
-__global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa, Pull pc, Pull pa) {
+__global__ __launch_bounds__(256) void sc_k1(Ws wc, RowArgs ac, int npc, Ws wa, RowArgs aa) {
     SC_PROF(0);
     SC_WAVE_PRIO();
     const bool crit = (int)blockIdx.y < npc;
-    // the pull: this block's share of its job's panels among the job's blocks of its XCD group (x mod 8)
-    const int rb8 = (int)gridDim.x >> 3, yj = crit ? (int)blockIdx.y : (int)blockIdx.y - npc;
-    const int nj = crit ? npc : (int)gridDim.y - npc;
-    float sink = 0.0f;
-    // gated critic blocks: the fixed panels while the block waits for its snapshot, the agent-relative ones after it
-    // (same-box A/B against the whole pull after the gate: 200 steps 0.0798-0.0804 vs 0.0803-0.0811 ms per step,
-    // profiles/r05/pullearly/). The whole pull before the gate when the host passed the agent indices by value: 200 steps
-    // 0.0806-0.0823 vs 0.0811-0.0835, driver command 0.0895-0.0929 vs 0.0882-0.0904 (profiles/r05/pullknown/): not kept
-    if (ac.gate && crit) {
-        if ((gridDim.x & 7) == 0) sink = pull_l2(pc, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, true, 1);
-        if (!gate_wait(ac.gate, ac.gate_seq)) return;
-        if ((gridDim.x & 7) == 0) sink += pull_l2(pc, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, true, 2);
-    } else {
-        if (ac.gate && crit && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
-        if ((gridDim.x & 7) == 0) sink = pull_l2(crit ? pc : pa, (int)(blockIdx.x >> 3) + rb8 * yj, rb8 * nj, crit);
-    }
+    if (ac.gate && crit && !gate_wait(ac.gate, ac.gate_seq)) return;  // this learn's snapshot
     const int bx = xcd_perm(blockIdx.x, gridDim.x);
     if (crit)
         c1_body<C, HC>(wc, ac, bx, blockIdx.y);
     else
         a1_body<C, HC>(wa, aa, bx, blockIdx.y - npc);
-    asm volatile("" ::"v"(sink));
 }
 template <int C, int HC, int NAC>
 __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, RowArgs aa) {
@@ -1832,19 +1786,6 @@ bool spec_shape(const Job& j) { return !g_sc_no_spec && j.H1 == 400 && j.H2 == 3
 
 // the fc2.weight panels a job's forward GEMMs read: the first problem's (the target actor / actor of the agent) and
 // the second's (the critic, or the critic view the actor phase reads; the critic phase's third problem shares it)
-Pull gemm_pull(const Job& j) {
-    Pull p{};
-    p.agent_v[0] = p.agent_v[1] = -1;
-    for (int i = 0; i < 2 && i < j.nfwd; ++i) {
-        const GemmP& g = j.fwd[i];
-        p.p[i] = g.B;
-        p.agent[i] = g.relB ? g.agent : nullptr;
-        p.agent_v[i] = g.agent_v;
-        p.rel[i] = g.relB;
-        p.n[i] = (int64_t)g.K * g.N;  // fc2.weight [H2][H1]: K = H1 rows of B, N = H2 columns
-    }
-    return p;
-}
 
 // One round: the critic phase of one learn() (jc) and the actor phase of another (ja) in five launches; either may be
 // NULL. The two jobs share no written state when they are of different agents (the caller's guarantee), so the round
@@ -1863,18 +1804,16 @@ int launch_round(hipStream_t st, const Job* jc, const Job* ja, const MidHook* mi
         return fail(-5, "flock_sc_round: the two updates must have the same shapes");
     const int C = A.C, rb = A.rb;
     int rc = 0;
-    {  // 1: fc1 rows (+ the L2 pull of the forward GEMMs' fc2.weight panels)
+    {  // 1: fc1 rows
         const int npc = jc ? 3 : 0, npa = ja ? 2 : 0;
         const size_t lds = zmax(A.lds1, Z.lds1);
         const dim3 grid(rb, npc + npa);
-        const Pull pc = jc ? gemm_pull(*jc) : Pull{}, pa = ja ? gemm_pull(*ja) : Pull{};
         if (spec_shape(A)) {
             if ((rc = allow_lds(sc_k1<7, 400>, lds))) return rc;
-            hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a, pc, pa);
+            hipLaunchKernelGGL((sc_k1<7, 400>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a);
         } else {
             SC_C_SWITCH(C, if ((rc = allow_lds(sc_k1<CC, 0>, lds))) return rc;
-                        hipLaunchKernelGGL((sc_k1<CC, 0>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a, pc,
-                                           pa))
+                        hipLaunchKernelGGL((sc_k1<CC, 0>), grid, dim3(256), lds, st, A.w, A.a, npc, Z.w, Z.a))
         }
         if ((rc = launched())) return rc;
     }
