@@ -1,4 +1,5 @@
 #!/bin/bash
+# HISTORICAL (round 6): FLOCK_SC_NO_PULL became the product (the pull was removed), so this A/B no longer builds a variant.
 # Round 6: the k1 launch's L2 pull of the forward GEMM's fc2.weight panels, now that the rounds run back to back:
 # same-box A/B of the product build against -DFLOCK_SC_NO_PULL, 200 steps and the driver command, three rounds
 set -o pipefail
