@@ -712,11 +712,7 @@ __device__ __forceinline__ bool gate_wait(unsigned long long* gate, unsigned lon
 // [g B / 8, (g + 1) B / 8)) run on one XCD in every launch of a round, so the fc1 rows k1 writes are L2 hits for the
 // forward GEMM tiles of that strip (xcd_tile), its fc2 outputs for the k3 rows, and k1 / k3 rows for the bwd launch's
 // dH1 tiles.
-#ifndef FLOCK_SC_NO_XCD  // (-DFLOCK_SC_NO_XCD: A/B builds only, tools/build_variant_sc.sh)
 __device__ __forceinline__ int xcd_perm(int x, int n) { return (n & 7) == 0 ? (x & 7) * (n >> 3) + (x >> 3) : x; }
-#else
-__device__ __forceinline__ int xcd_perm(int x, int) { return x; }
-#endif
 
 // Round 5 also had each XCD's k1 blocks pull the forward GEMM's fc2.weight panels into that XCD's L2 (one dword per
 // 128-B line): it took the GEMM 18.1 -> 14.5 us in the loop while the rounds waited on a slot-free event between them;
@@ -1011,12 +1007,7 @@ __device__ __forceinline__ void gemm_tile(const GemmP& g, const float* Bp, int t
 // tile (x % 8) * (tiles / 8) + x / 8, so each XCD computes a contiguous run of tiles (at 8 row strips: one strip of
 // A and all of B) and its L2 fetches ~1/8 of A from the Infinity Cache instead of nearly all of it
 __device__ __forceinline__ int xcd_tile(int x, int tiles) {
-#ifndef FLOCK_SC_NO_XCD
     return (tiles & 7) == 0 && (int)gridDim.x == tiles ? (x & 7) * (tiles >> 3) + (x >> 3) : x;
-#else
-    (void)tiles;
-    return x;
-#endif
 }
 
 // one forward GEMM tile: block x of problem y computes tile xcd_tile(x)

@@ -1,4 +1,5 @@
 #!/bin/bash
+# HISTORICAL (round 6): the FLOCK_SC_NO_XCD macro was removed after this A/B measured flat (profiles/r06/noxcd/).
 # Round 6: the XCD-aligned block maps of the learner round (xcd_perm, xcd_tile), now that the rounds run back to back:
 # same-box A/B of the product build against -DFLOCK_SC_NO_XCD, 200 steps and the driver command, three rounds
 set -o pipefail
