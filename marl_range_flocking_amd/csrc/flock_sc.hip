@@ -750,11 +750,17 @@ __global__ __launch_bounds__(256) void sc_k3(Ws wc, RowArgs ac, int nbc, Ws wa, 
 // 2 = any strides (scalar).
 constexpr int kT = 32;
 constexpr int kKC = 512;
-constexpr int kFwdKC = 200;   // (round 5 with the XCD-aligned round: 0.0814-0.0822 ms per step against 0.0836-0.0843
+#ifndef FLOCK_FWD_KC  // (A/B builds only, tools/build_variant_sc.sh)
+#define FLOCK_FWD_KC 200
+#endif
+#ifndef FLOCK_GRAD_KC
+#define FLOCK_GRAD_KC 128
+#endif
+constexpr int kFwdKC = FLOCK_FWD_KC;   // (round 5 with the XCD-aligned round: 0.0814-0.0822 ms per step against 0.0836-0.0843
                               // for 136-deep chunks and 0.098 for whole panels, profiles/r05/fwdkc/)
                               // forward / input-gradient GEMM K chunk: 0.098 ms per config-3 step vs 0.117 with whole
                               // 400-deep panels (lighter blocks co-run with the env kernel; tools/gpu_kc_sweep.sh)
-constexpr int kGradKC = 128;  // the gradient kernels share one launch with ~400 LDS-free reduction blocks: a 34-KB
+constexpr int kGradKC = FLOCK_GRAD_KC;  // the gradient kernels share one launch with ~400 LDS-free reduction blocks: a 34-KB
                               // panel keeps 4 blocks per CU resident so the whole grid runs in one round
 constexpr int kPitch = 33;
 struct GemmP {
