@@ -1069,6 +1069,9 @@ struct RedP {
     int64_t off;
 };
 constexpr int kMaxRed = 12;
+#ifndef FLOCK_RED_RB  // (A/B builds only, tools/build_variant_sc.sh)
+#define FLOCK_RED_RB 8
+#endif
 // output elements per reduction block; the block's 256 threads are kRedElems elements x kRedGroups row groups (group q
 // takes rows q, q + kRedGroups, ...; 8 and 4 elements per block measured slower in round 4: DESIGN.md §3.3)
 constexpr int kRedElems = 16;
@@ -1095,7 +1098,7 @@ __device__ __forceinline__ float red_block(const RedP& rp, int b, int B, const D
     const int o = per_in ? e / rp.in : e;
     const int i = per_in ? e - o * rp.in : e;
     const bool prod = rp.mode == 1 || rp.mode == 2 || rp.mode == 4;
-    constexpr int kRB = 8;  // rows per batch of loads (row group q takes rows q, q + kRedGroups, ...; 4 and 16 flat or
+    constexpr int kRB = FLOCK_RED_RB;  // rows per batch of loads (row group q takes rows q, q + kRedGroups, ...; 4 and 16 flat or
                             // slower in round 3)
     float dv[kRB], xv[kRB], xh[kRB], rs[kRB];
     auto load = [&](int r0) {
